@@ -1,0 +1,120 @@
+// pybind11 bindings of the host-side native runtime (_twtml_host).
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <stdexcept>
+#include <vector>
+
+#include "featurize_cpu.h"
+#include "synth.h"
+#include "unicode_lower.h"
+
+namespace py = pybind11;
+using namespace twtml;
+
+template <typename T>
+using Arr = py::array_t<T, py::array::c_style | py::array::forcecast>;
+
+template <typename T>
+static T* mut_ptr(py::array& a, size_t need, const char* what) {
+  if (!(a.flags() & py::array::c_style)) throw std::invalid_argument(std::string(what) + " not contiguous");
+  if (a.itemsize() != sizeof(T)) throw std::invalid_argument(std::string(what) + ": wrong dtype");
+  if (size_t(a.size()) < need) throw std::invalid_argument(std::string(what) + ": too small");
+  if (!a.writeable()) throw std::invalid_argument(std::string(what) + ": read-only");
+  return static_cast<T*>(a.mutable_data());
+}
+
+static SynthParams params_from(const py::dict& d) {
+  SynthParams p;
+#define GET(name, type) if (d.contains(#name)) p.name = d[#name].cast<type>();
+  GET(seed, uint64_t) GET(retweet_fraction, double) GET(rt_lo, int64_t) GET(rt_hi, int64_t)
+  GET(rt_base, double) GET(rt_slope, double) GET(rt_noise, double) GET(rt_tail, double)
+  GET(min_len, int32_t) GET(max_len, int32_t) GET(unicode_fraction, double)
+  GET(special_fraction, double) GET(now_ms, int64_t) GET(max_age_ms, int64_t)
+#undef GET
+  return p;
+}
+
+template <typename T>
+static py::array_t<T> to_numpy(std::vector<T>&& v) {
+  auto* heap = new std::vector<T>(std::move(v));
+  py::capsule owner(heap, [](void* p) { delete static_cast<std::vector<T>*>(p); });
+  return py::array_t<T>({heap->size()}, {sizeof(T)}, heap->data(), owner);
+}
+
+PYBIND11_MODULE(_twtml_host, m) {
+  m.doc() = "twtml host runtime: synthetic tweet source, unicode lowering, CPU featurizer";
+
+  m.def("synth_max_units", [](const py::dict& d, size_t n) { return synth_max_units(params_from(d), n); });
+
+  m.def("synth_generate_into",
+        [](const py::dict& d, uint64_t start, size_t n, py::array text, py::array offsets,
+           py::array is_rt, py::array scalars, int nthreads) {
+          SynthParams p = params_from(d);
+          uint16_t* t = mut_ptr<uint16_t>(text, 0, "text");
+          int64_t* o = mut_ptr<int64_t>(offsets, n + 1, "offsets");
+          uint8_t* r = mut_ptr<uint8_t>(is_rt, n, "is_rt");
+          int64_t* s = mut_ptr<int64_t>(scalars, 5 * n, "scalars");
+          int64_t res;
+          {
+            py::gil_scoped_release nogil;
+            res = synth_generate(p, start, n, t, size_t(text.size()), o, r, s, nthreads);
+          }
+          return res;
+        },
+        py::arg("params"), py::arg("start"), py::arg("n"), py::arg("text"), py::arg("offsets"),
+        py::arg("is_rt"), py::arg("scalars"), py::arg("nthreads") = 0,
+        "Generate rows [start, start+n) into caller buffers; returns units written or -needed.");
+
+  m.def("count_special_rows", [](Arr<uint16_t> text, Arr<int64_t> offsets) {
+    const size_t n = size_t(offsets.size()) - 1;
+    return count_special_rows(text.data(), offsets.data(), n);
+  });
+
+  m.def("prelower_special_rows", [](Arr<uint16_t> text, Arr<int64_t> offsets) {
+    const size_t n = size_t(offsets.size()) - 1;
+    std::vector<uint16_t> ot;
+    std::vector<int64_t> oo;
+    size_t changed;
+    {
+      py::gil_scoped_release nogil;
+      changed = prelower_special_rows(text.data(), offsets.data(), n, ot, oo);
+    }
+    return py::make_tuple(to_numpy(std::move(ot)), to_numpy(std::move(oo)), changed);
+  });
+
+  m.def("lower_row", [](Arr<uint16_t> units) {
+    std::vector<uint16_t> out;
+    lower_full(units.data(), size_t(units.size()), out);
+    return to_numpy(std::move(out));
+  });
+
+  m.def("row_needs_special", [](Arr<uint16_t> units) {
+    return row_needs_special(units.data(), size_t(units.size()));
+  });
+
+  m.def("featurize_rows",
+        [](Arr<uint16_t> text, Arr<int64_t> offsets, Arr<int64_t> rows, int64_t F,
+           const std::string& hash, int nthreads) {
+          const int kind = hash == "java" ? 0 : hash == "murmur3" ? 1 : -1;
+          if (kind < 0) throw std::invalid_argument("hash must be 'java' or 'murmur3'");
+          if (F <= 0) throw std::invalid_argument("F must be positive");
+          const int64_t nr = offsets.size() - 1;
+          for (py::ssize_t i = 0; i < rows.size(); ++i)
+            if (rows.data()[i] < 0 || rows.data()[i] >= nr) throw std::out_of_range("row id");
+          std::vector<int64_t> indptr, indices;
+          {
+            py::gil_scoped_release nogil;
+            featurize_rows_cpu(text.data(), offsets.data(), rows.data(), size_t(rows.size()), F,
+                               kind, indptr, indices, nthreads);
+          }
+          return py::make_tuple(to_numpy(std::move(indptr)), to_numpy(std::move(indices)));
+        },
+        py::arg("text"), py::arg("offsets"), py::arg("rows"), py::arg("F"),
+        py::arg("hash") = "java", py::arg("nthreads") = 0);
+
+  m.def("term_index", [](Arr<uint16_t> units, int64_t F, const std::string& hash) {
+    return term_index(units.data(), int(units.size()), F, hash == "java" ? 0 : 1);
+  });
+}

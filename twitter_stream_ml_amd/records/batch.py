@@ -1,0 +1,172 @@
+"""Columnar micro-batch of raw tweets (host side).
+
+A :class:`RawBatch` is what a receiver seals every interval: struct-of-arrays
+scalars plus the *original* tweet texts as one ragged UTF-16 buffer with CSR
+offsets.  It is the unit that crosses PCIe to the GPU (SURVEY §7.1
+``records/``; U14/U15).  Text is stored as UTF-16 **code units** because Java
+strings are UTF-16 and the reference's bigrams are ``String.sliding(2)`` over
+code units.
+
+Scalar rows (``scalars[k]``), all of the *retweeted* (original) status, as the
+reference reads them through ``getRetweetedStatus`` (``MllibHelper.scala:43,59,
+81,85``):
+
+====  ======================  ==========================================
+row   name                    source
+====  ======================  ==========================================
+0     retweet_count           ``getRetweetCount`` (label, filter)
+1     followers               ``getUser.getFollowersCount``
+2     favourites              ``getUser.getFavouritesCount``
+3     friends                 ``getUser.getFriendsCount``
+4     created_at_ms           ``getCreatedAt.getTime``
+====  ======================  ==========================================
+
+``is_retweet`` is separate (uint8).  For non-retweets the scalar/text columns
+hold the tweet's own fields; every consumer filters on ``is_retweet`` first.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Iterable, List, Optional, Sequence
+
+import numpy as np
+
+from .schema import Status, User
+
+__all__ = ["RawBatch", "SCALAR_FIELDS", "RETWEET_COUNT", "FOLLOWERS", "FAVOURITES",
+           "FRIENDS", "CREATED_AT", "utf16_units", "units_to_str"]
+
+RETWEET_COUNT, FOLLOWERS, FAVOURITES, FRIENDS, CREATED_AT = range(5)
+SCALAR_FIELDS = ("retweet_count", "followers", "favourites", "friends", "created_at_ms")
+
+
+def utf16_units(s: str) -> np.ndarray:
+    """Java ``String`` code units of ``s`` (surrogate pairs for astral chars)."""
+    return np.frombuffer(s.encode("utf-16-le", "surrogatepass"), dtype="<u2")
+
+
+def units_to_str(units: np.ndarray) -> str:
+    return np.asarray(units, dtype="<u2").tobytes().decode("utf-16-le", "surrogatepass")
+
+
+@dataclass
+class RawBatch:
+    text: np.ndarray          # uint16 [total_units]
+    offsets: np.ndarray       # int64  [n+1]
+    is_retweet: np.ndarray    # uint8  [n]
+    scalars: np.ndarray       # int64  [5, n]
+    batch_time_ms: int = 0    # seal time ("now" for featurizeNumbers)
+
+    def __post_init__(self) -> None:
+        self.text = np.ascontiguousarray(self.text, dtype=np.uint16)
+        self.offsets = np.ascontiguousarray(self.offsets, dtype=np.int64)
+        self.is_retweet = np.ascontiguousarray(self.is_retweet, dtype=np.uint8)
+        self.scalars = np.ascontiguousarray(self.scalars, dtype=np.int64)
+        n = self.n
+        if self.offsets.shape != (n + 1,) or self.scalars.shape != (5, n):
+            raise ValueError(f"inconsistent RawBatch shapes: n={n} offsets={self.offsets.shape} "
+                             f"scalars={self.scalars.shape}")
+        if n and (self.offsets[0] != 0 or self.offsets[-1] != self.text.shape[0]):
+            raise ValueError("offsets must start at 0 and end at len(text)")
+
+    # ------------------------------------------------------------------
+    @property
+    def n(self) -> int:
+        return int(self.is_retweet.shape[0])
+
+    def __len__(self) -> int:
+        return self.n
+
+    @property
+    def total_units(self) -> int:
+        return int(self.text.shape[0])
+
+    @property
+    def nbytes(self) -> int:
+        return (self.text.nbytes + self.offsets.nbytes + self.is_retweet.nbytes
+                + self.scalars.nbytes)
+
+    def column(self, k: int) -> np.ndarray:
+        return self.scalars[k]
+
+    def text_of(self, i: int) -> str:
+        return units_to_str(self.text[self.offsets[i]:self.offsets[i + 1]])
+
+    # ------------------------------------------------------------------
+    @classmethod
+    def empty(cls, batch_time_ms: int = 0) -> "RawBatch":
+        return cls(np.zeros(0, np.uint16), np.zeros(1, np.int64), np.zeros(0, np.uint8),
+                   np.zeros((5, 0), np.int64), batch_time_ms)
+
+    @classmethod
+    def from_statuses(cls, statuses: Sequence[Status], batch_time_ms: int = 0) -> "RawBatch":
+        n = len(statuses)
+        chunks: List[np.ndarray] = []
+        offsets = np.zeros(n + 1, np.int64)
+        is_rt = np.zeros(n, np.uint8)
+        sc = np.zeros((5, n), np.int64)
+        for i, st in enumerate(statuses):
+            src = st.retweetedStatus if st.retweetedStatus is not None else st
+            is_rt[i] = 1 if st.retweetedStatus is not None else 0
+            u = utf16_units(src.text)
+            chunks.append(u)
+            offsets[i + 1] = offsets[i] + u.shape[0]
+            sc[RETWEET_COUNT, i] = src.retweetCount
+            sc[FOLLOWERS, i] = src.user.followersCount
+            sc[FAVOURITES, i] = src.user.favouritesCount
+            sc[FRIENDS, i] = src.user.friendsCount
+            sc[CREATED_AT, i] = src.createdAt
+        text = np.concatenate(chunks) if chunks else np.zeros(0, np.uint16)
+        return cls(text, offsets, is_rt, sc, batch_time_ms)
+
+    def to_statuses(self) -> List[Status]:
+        out: List[Status] = []
+        for i in range(self.n):
+            orig = Status(
+                text=self.text_of(i),
+                retweetCount=int(self.scalars[RETWEET_COUNT, i]),
+                createdAt=int(self.scalars[CREATED_AT, i]),
+                user=User(int(self.scalars[FOLLOWERS, i]), int(self.scalars[FAVOURITES, i]),
+                          int(self.scalars[FRIENDS, i])),
+            )
+            if self.is_retweet[i]:
+                out.append(Status(text="RT " + orig.text, retweetCount=orig.retweetCount,
+                                  createdAt=orig.createdAt, retweetedStatus=orig))
+            else:
+                out.append(orig)
+        return out
+
+    def take(self, rows: Iterable[int]) -> "RawBatch":
+        rows = np.asarray(list(rows), dtype=np.int64)
+        lens = self.offsets[rows + 1] - self.offsets[rows]
+        offsets = np.zeros(rows.shape[0] + 1, np.int64)
+        np.cumsum(lens, out=offsets[1:])
+        text = (np.concatenate([self.text[self.offsets[r]:self.offsets[r + 1]] for r in rows])
+                if rows.shape[0] else np.zeros(0, np.uint16))
+        return RawBatch(text, offsets, self.is_retweet[rows], self.scalars[:, rows],
+                        self.batch_time_ms)
+
+    def slice(self, start: int, stop: int) -> "RawBatch":
+        start = max(0, start)
+        stop = min(self.n, stop)
+        t0, t1 = int(self.offsets[start]), int(self.offsets[stop])
+        return RawBatch(self.text[t0:t1], self.offsets[start:stop + 1] - t0,
+                        self.is_retweet[start:stop], self.scalars[:, start:stop],
+                        self.batch_time_ms)
+
+    def shard(self, rank: int, world: int) -> "RawBatch":
+        """Contiguous shard ``rank`` of ``world`` (DP split of one micro-batch)."""
+        per = (self.n + world - 1) // world
+        return self.slice(rank * per, (rank + 1) * per)
+
+    @staticmethod
+    def concat(batches: Sequence["RawBatch"], batch_time_ms: Optional[int] = None) -> "RawBatch":
+        if not batches:
+            return RawBatch.empty(batch_time_ms or 0)
+        text = np.concatenate([b.text for b in batches])
+        lens = np.concatenate([np.diff(b.offsets) for b in batches])
+        offsets = np.zeros(lens.shape[0] + 1, np.int64)
+        np.cumsum(lens, out=offsets[1:])
+        return RawBatch(text, offsets, np.concatenate([b.is_retweet for b in batches]),
+                        np.concatenate([b.scalars for b in batches], axis=1),
+                        batches[0].batch_time_ms if batch_time_ms is None else batch_time_ms)
