@@ -1,0 +1,167 @@
+#!/usr/bin/env python3
+"""Headline benchmark: tweets/sec trained (whole node) + p50 micro-batch latency.
+
+Config (BASELINE.json config 2/3): online linear regression
+(StreamingLinearRegressionWithSGD, stepSize 0.005, numIterations 50,
+miniBatchFraction 1.0, convergence tol 1e-3) on 1M-dim hashed character-bigram
+features (+4 numeric), synthetic tweet-shaped data, random/zero-init weights
+as in the reference (``Vectors.zeros``), data-parallel over N GPUs with the
+gradient all-reduced over RCCL every GD iteration.
+
+One *step* = one micro-batch end to end: H2D of the raw tweets (overlapped
+with the previous batch), filter, lower-case + bigram hashing, prequential
+predict + stats, and up to 50 GD iterations (early exit on convergence, as
+MLlib).  Each rank trains ``--batch`` raw tweets per step (weak scaling).
+Tweets are replayed from a pool of pre-generated pinned batches (the
+generator runs at ~1M tweets/s/core, slower than the GPU consumes them).
+
+Usage:  python bench.py [--gpus N --steps K --warmup W]
+        (N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+BASELINE_TWEETS_PER_SEC = None  # the reference publishes no number
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawTextHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=1_000_000, help="raw tweets per GPU per step")
+    ap.add_argument("--features", type=int, default=1_000_000, help="numTextFeatures")
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--step-size", type=float, default=0.005)
+    ap.add_argument("--pool", type=int, default=4, help="pre-generated batches per rank")
+    ap.add_argument("--hash", default="java")
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--sgd-grid", type=int, default=0)
+    ap.add_argument("--json-out", default="")
+    ap.add_argument("--verbose", action="store_true")
+    return ap.parse_args(argv)
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    import torch  # noqa: F401  (binds the HIP runtime before the engine loads)
+    from twitter_stream_ml_amd.parallel import dist as D
+    from twitter_stream_ml_amd.ops.lr_engine import (DeviceLinearRegression, HostBatchView,
+                                                     LRDeviceConfig, prelower)
+    from twitter_stream_ml_amd.sources.synthetic import SynthConfig, generate_batch
+
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != args.gpus:
+        if args.gpus > 1 and world_env == 1:
+            print(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes",
+                  file=sys.stderr)
+            return 2
+    info = D.init_distributed()
+    device = info.local_rank
+    torch.cuda.set_device(device)
+    comm = D.make_rccl_comm(device)
+
+    B = args.batch
+    synth = SynthConfig.profile("bench", seed=args.seed + 7919 * info.rank)
+    now_ms = synth.now_ms
+    # ---- pool of pinned raw batches (generated + host special-row pass)
+    t_gen = time.time()
+    pool_raw = [prelower(generate_batch(synth, i * B, B, batch_time_ms=now_ms))
+                for i in range(args.pool)]
+    max_units = max(r.total_units for r in pool_raw) + 1024
+    cfg = LRDeviceConfig(num_text_features=args.features, hash=args.hash, step_size=args.step_size,
+                         num_iterations=args.iters, fraction=1.0, begin=100, end=1000,
+                         max_rows=B, max_units=max_units, sgd_grid=args.sgd_grid)
+    eng = DeviceLinearRegression(cfg, device=device, comm=comm)
+    pool = [HostBatchView(B, max_units).load(r) for r in pool_raw]
+    del pool_raw
+    t_gen = time.time() - t_gen
+
+    total = args.warmup + args.steps
+    lat = []
+    kept = []
+    iters = []
+    stage = []
+
+    def run(n_steps, record):
+        slot = 0
+        eng.submit(pool[0], slot)
+        sealed = time.perf_counter()
+        for s in range(n_steps):
+            nxt = pool[(s + 1) % len(pool)]
+            if s + 1 < n_steps:
+                eng.submit(nxt, slot ^ 1)
+            sealed_next = time.perf_counter()
+            res = eng.process(slot, now_ms)
+            done = time.perf_counter()
+            if record:
+                lat.append((done - sealed) * 1e3)
+                kept.append(res["n_kept"])
+                iters.append(res["iterations"])
+                stage.append((res["prep_ms"], res["train_ms"]))
+            sealed = sealed_next
+            slot ^= 1
+
+    run(args.warmup, False)
+    eng.synchronize()
+    D.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(args.steps, True)
+    eng.synchronize()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    D.barrier()
+    elapsed = D.allreduce_max_scalar(t1 - t0)
+    tweets = D.allreduce_sum_scalar(float(sum(kept)))
+    p50 = D.allreduce_max_scalar(float(np.median(lat)))
+    value = tweets / elapsed
+    ms = elapsed / args.steps * 1e3
+    if info.is_main:
+        out = {
+            "metric": "tweets/sec trained (whole node)",
+            "value": round(value, 1),
+            "unit": "tweets/s",
+            "n_gpus": info.world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (value / BASELINE_TWEETS_PER_SEC) if BASELINE_TWEETS_PER_SEC else None,
+            "dtype": "fp32",
+            "data": "synthetic tweet-shaped records (seeded C++ generator), zero-init weights",
+            "config": {
+                "model": f"StreamingLinearRegressionWithSGD, {args.features}-dim hashed bigrams + 4 numeric",
+                "global_batch": B * info.world,
+                "seq_len": 280,
+                "parallelism": f"dp{info.world}",
+                "numIterations": args.iters,
+                "stepSize": args.step_size,
+                "miniBatchFraction": 1.0,
+            },
+            "p50_microbatch_latency_ms": round(p50, 3),
+            "trained_tweets_per_step": round(tweets / args.steps, 1),
+            "gd_iterations_mean": float(np.mean(iters)) if iters else 0.0,
+            "prep_ms_mean": float(np.mean([s[0] for s in stage])) if stage else 0.0,
+            "train_ms_mean": float(np.mean([s[1] for s in stage])) if stage else 0.0,
+            "pool_gen_s": round(t_gen, 2),
+        }
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as fh:
+                fh.write(line + "\n")
+    D.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,165 @@
+// pybind11 bindings of the MI355X engine (_twtml_hip).
+#include <hip/hip_runtime.h>
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <memory>
+
+#include "comm.h"
+#include "common.h"
+#include "engine.h"
+#include "kmeans_engine.h"
+
+namespace py = pybind11;
+using namespace twtml;
+
+template <typename T>
+static py::array_t<T> view(T* ptr, std::vector<py::ssize_t> shape, py::handle owner) {
+  std::vector<py::ssize_t> strides(shape.size());
+  py::ssize_t st = sizeof(T);
+  for (int i = int(shape.size()) - 1; i >= 0; --i) {
+    strides[size_t(i)] = st;
+    st *= shape[size_t(i)];
+  }
+  return py::array_t<T>(shape, strides, ptr, owner);
+}
+
+static LRConfig lr_config(const py::dict& d) {
+  LRConfig c;
+#define GET(name, type) if (d.contains(#name)) c.name = d[#name].cast<type>();
+  GET(num_text_features, int64_t) GET(hash_kind, int32_t) GET(step_size, double)
+  GET(num_iterations, int32_t) GET(fraction, double) GET(tol, double) GET(begin, int64_t)
+  GET(end, int64_t) GET(require_retweet, int32_t) GET(range_filter, int32_t)
+  GET(max_rows, int64_t) GET(max_units, int64_t) GET(sgd_grid, int32_t)
+  GET(early_exit_depth, int32_t)
+#undef GET
+  return c;
+}
+
+static py::dict result_dict(BatchResult& r) {
+  py::dict d;
+  d["n_raw"] = r.n_raw;
+  d["n_kept"] = r.n_kept;
+  d["n_kept_global"] = r.n_kept_global;
+  d["n_unique"] = r.n_unique;
+  d["entries"] = r.entries;
+  d["iterations"] = r.iterations;
+  d["converged"] = r.converged;
+  d["stats"] = std::vector<double>(r.stats, r.stats + 6);
+  d["loss_history"] = r.loss_history;
+  d["prep_ms"] = r.prep_ms;
+  d["train_ms"] = r.train_ms;
+  if (!r.pred.empty()) {
+    auto* v = new std::vector<float>(std::move(r.pred));
+    py::capsule own(v, [](void* p) { delete static_cast<std::vector<float>*>(p); });
+    d["pred"] = py::array_t<float>({py::ssize_t(v->size())}, {py::ssize_t(sizeof(float))}, v->data(), own);
+  } else {
+    d["pred"] = py::none();
+  }
+  return d;
+}
+
+PYBIND11_MODULE(_twtml_hip, m) {
+  m.doc() = "twtml MI355X engine: HIP/CDNA4 kernels, micro-batch engines, RCCL";
+
+  m.def("device_count", []() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+  });
+  m.def("device_name", [](int dev) {
+    hipDeviceProp_t p;
+    TWTML_HIP_CHECK(hipGetDeviceProperties(&p, dev));
+    return std::string(p.name) + " (" + p.gcnArchName + ", " + std::to_string(p.multiProcessorCount) + " CUs)";
+  });
+  m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
+  m.def("rccl_version", &rccl_version);
+
+  py::class_<Comm, std::shared_ptr<Comm>>(m, "Comm")
+      .def(py::init([](py::bytes uid, int rank, int world, int device) {
+             std::string s = uid;
+             py::gil_scoped_release nogil;
+             return std::make_shared<Comm>(s, rank, world, device);
+           }),
+           py::arg("unique_id"), py::arg("rank"), py::arg("world"), py::arg("device"))
+      .def_property_readonly("rank", &Comm::rank)
+      .def_property_readonly("world", &Comm::world)
+      .def("abort", &Comm::abort)
+      .def("check", &Comm::check_async);
+
+  py::class_<HostBatch, std::shared_ptr<HostBatch>>(m, "HostBatch")
+      .def(py::init<int64_t, int64_t>(), py::arg("max_rows"), py::arg("max_units"))
+      .def_readonly("max_rows", &HostBatch::max_rows)
+      .def_readonly("max_units", &HostBatch::max_units)
+      .def_property_readonly("text", [](py::object self) {
+        auto& h = self.cast<HostBatch&>();
+        return view<uint16_t>(h.text, {py::ssize_t(h.max_units)}, self);
+      })
+      .def_property_readonly("offsets", [](py::object self) {
+        auto& h = self.cast<HostBatch&>();
+        return view<int64_t>(h.offsets, {py::ssize_t(h.max_rows + 1)}, self);
+      })
+      .def_property_readonly("is_rt", [](py::object self) {
+        auto& h = self.cast<HostBatch&>();
+        return view<uint8_t>(h.is_rt, {py::ssize_t(h.max_rows)}, self);
+      })
+      .def_property_readonly("scalars_flat", [](py::object self) {
+        auto& h = self.cast<HostBatch&>();
+        return view<int64_t>(h.scalars, {py::ssize_t(5 * h.max_rows)}, self);
+      });
+
+  py::class_<LREngine, std::shared_ptr<LREngine>>(m, "LREngine")
+      .def(py::init([](int device, const py::dict& cfg, std::shared_ptr<Comm> comm) {
+             LRConfig c = lr_config(cfg);
+             py::gil_scoped_release nogil;
+             return std::make_shared<LREngine>(device, c, comm);
+           }),
+           py::arg("device"), py::arg("config"), py::arg("comm") = nullptr)
+      .def("submit",
+           [](LREngine& e, const HostBatch& hb, int64_t n, int64_t units, int slot) {
+             py::gil_scoped_release nogil;
+             e.submit(hb, n, units, slot);
+           },
+           py::arg("host_batch"), py::arg("n"), py::arg("units"), py::arg("slot"))
+      .def("process",
+           [](LREngine& e, int slot, int64_t now_ms, bool want_pred) {
+             BatchResult r;
+             {
+               py::gil_scoped_release nogil;
+               r = e.process(slot, now_ms, want_pred);
+             }
+             return result_dict(r);
+           },
+           py::arg("slot"), py::arg("now_ms"), py::arg("want_pred") = false)
+      .def("get_weights", [](const LREngine& e) {
+        py::array_t<double> out(e.num_weights());
+        e.get_weights(out.mutable_data(), e.num_weights());
+        return out;
+      })
+      .def("set_weights", [](LREngine& e, py::array_t<double, py::array::c_style | py::array::forcecast> w) {
+        e.set_weights(w.data(), w.size());
+      })
+      .def("debug_prepared", [](LREngine& e) {
+        std::vector<int64_t> counters, cbase;
+        std::vector<int32_t> clen8, idx, perm, uniq;
+        std::vector<float> y, num;
+        e.debug_prepared(counters, clen8, cbase, idx, perm, y, num, uniq);
+        py::dict d;
+        d["counters"] = py::array_t<int64_t>(py::ssize_t(counters.size()), counters.data());
+        d["clen8"] = py::array_t<int32_t>(py::ssize_t(clen8.size()), clen8.data());
+        d["cbase"] = py::array_t<int64_t>(py::ssize_t(cbase.size()), cbase.data());
+        d["idx"] = py::array_t<int32_t>(py::ssize_t(idx.size()), idx.data());
+        d["perm"] = py::array_t<int32_t>(py::ssize_t(perm.size()), perm.data());
+        d["y"] = py::array_t<float>(py::ssize_t(y.size()), y.data());
+        d["num"] = py::array_t<float>(py::ssize_t(num.size()), num.data());
+        d["uniq"] = py::array_t<int32_t>(py::ssize_t(uniq.size()), uniq.data());
+        return d;
+      })
+      .def("set_step", &LREngine::set_step)
+      .def("synchronize", &LREngine::synchronize)
+      .def_property_readonly("num_weights", &LREngine::num_weights)
+      .def_property_readonly("device", &LREngine::device);
+
+  bind_kmeans(m);
+}

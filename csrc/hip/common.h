@@ -1,0 +1,87 @@
+// Shared device/host helpers for the MI355X (gfx950, CDNA4) engine.
+//
+// Wave64 everywhere: reductions use 64-lane DPP/shuffles, masks are 64-bit.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <stdexcept>
+#include <string>
+
+#define TWTML_HIP_CHECK(expr)                                                              \
+  do {                                                                                     \
+    hipError_t _e = (expr);                                                                \
+    if (_e != hipSuccess)                                                                  \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) + " at " + \
+                               __FILE__ + ":" + std::to_string(__LINE__) + ": " #expr);      \
+  } while (0)
+
+namespace twtml {
+
+constexpr int kWave = 64;
+constexpr int kBlock = 256;          // 4 waves per workgroup
+constexpr int kChunk = 64;           // rows per SELL chunk (one row per lane)
+constexpr int kGroup = 8;            // entries per lane per 16-byte slot load (u16 slots)
+constexpr int kChunkStride = kChunk * kGroup;  // entries per (chunk, group) = 512
+constexpr int kNumNumeric = 4;       // numeric features (MllibHelper.scala:13)
+constexpr int kPadSlots = 64;        // one zero-weight pad slot per lane
+constexpr int kLenBuckets = 4096;    // counting-sort buckets for row length
+
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC__)
+__device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    T o = __shfl_xor(v, off, kWave);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
+// Block-wide sum for kBlock threads; `scratch` needs kBlock/kWave entries.
+template <typename T>
+__device__ __forceinline__ T block_sum(T v, T* scratch) {
+  v = wave_sum(v);
+  const int w = threadIdx.x / kWave;
+  __syncthreads();
+  if (lane_id() == 0) scratch[w] = v;
+  __syncthreads();
+  T r = T(0);
+  const int nw = blockDim.x / kWave;
+  for (int i = 0; i < nw; ++i) r += scratch[i];
+  return r;
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ULL;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+  return x ^ (x >> 31);
+}
+
+// Bit-identical to oracle.mllib.sgd_uniform (Bernoulli row sampling).
+__device__ __forceinline__ double sample_uniform(uint64_t seed, uint64_t row) {
+  const uint64_t key = row ^ (seed * 0xD1B54A32D192ED03ULL);
+  return double(splitmix64(key) >> 11) * (1.0 / 9007199254740992.0);
+}
+
+// Utils.round: BigDecimal HALF_UP = round half away from zero.
+__device__ __forceinline__ double round_half_away(double x) {
+  const double t = trunc(x);
+  return fabs(x - t) >= 0.5 ? t + (x > 0 ? 1.0 : -1.0) : t;
+}
+#endif
+
+inline int ceil_div(long long a, long long b) { return int((a + b - 1) / b); }
+
+}  // namespace twtml

@@ -1,0 +1,364 @@
+// LREngine implementation; see engine.h.
+#include "engine.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <stdexcept>
+
+namespace twtml {
+
+void launch_batch_init(double* state, double m_global, hipStream_t s);
+
+HostBatch::HostBatch(int64_t rows, int64_t units) : max_rows(rows), max_units(units) {
+  auto up = [](size_t x) { return (x + 255) & ~size_t(255); };
+  const size_t t = up(sizeof(uint16_t) * size_t(units));
+  const size_t o = up(sizeof(int64_t) * size_t(rows + 1));
+  const size_t r = up(size_t(rows));
+  const size_t sc = up(sizeof(int64_t) * 5 * size_t(rows));
+  bytes = t + o + r + sc;
+  TWTML_HIP_CHECK(hipHostMalloc(&base, bytes, hipHostMallocDefault));
+  char* p = static_cast<char*>(base);
+  text = reinterpret_cast<uint16_t*>(p);
+  offsets = reinterpret_cast<int64_t*>(p + t);
+  is_rt = reinterpret_cast<uint8_t*>(p + t + o);
+  scalars = reinterpret_cast<int64_t*>(p + t + o + r);
+  offsets[0] = 0;
+}
+
+HostBatch::~HostBatch() {
+  if (base) (void)hipHostFree(base);
+}
+
+template <typename T>
+static T* dmalloc(size_t n) {
+  void* p = nullptr;
+  TWTML_HIP_CHECK(hipMalloc(&p, std::max<size_t>(1, n) * sizeof(T)));
+  return static_cast<T*>(p);
+}
+
+LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
+    : device_(device), cfg_(cfg), comm_(std::move(comm)) {
+  if (cfg_.num_text_features <= 0) throw std::invalid_argument("numTextFeatures must be > 0");
+  if (cfg_.max_rows <= 0 || cfg_.max_units < 0) throw std::invalid_argument("bad capacity");
+  if (cfg_.max_rows >= (int64_t(1) << 31)) throw std::invalid_argument("max_rows must be < 2^31");
+  if (cfg_.fraction <= 0.0 || cfg_.fraction > 1.0 + 1e-12)
+    throw std::invalid_argument("miniBatchFraction must be in (0, 1]");
+  TWTML_HIP_CHECK(hipSetDevice(device_));
+  hipDeviceProp_t prop;
+  TWTML_HIP_CHECK(hipGetDeviceProperties(&prop, device_));
+  num_cu_ = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  TWTML_HIP_CHECK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
+  TWTML_HIP_CHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
+  for (auto& s : slots_) {
+    s.text = dmalloc<uint16_t>(size_t(cfg_.max_units) + 8);
+    s.offsets = dmalloc<int64_t>(size_t(cfg_.max_rows) + 1);
+    s.is_rt = dmalloc<uint8_t>(size_t(cfg_.max_rows));
+    s.scalars = dmalloc<int64_t>(5 * size_t(cfg_.max_rows));
+    TWTML_HIP_CHECK(hipEventCreateWithFlags(&s.h2d_done, hipEventDisableTiming));
+    TWTML_HIP_CHECK(hipEventCreateWithFlags(&s.consumed, hipEventDisableTiming));
+  }
+  for (auto& e : ev_) TWTML_HIP_CHECK(hipEventCreate(&e));
+  upload_lower_tables(compute_, &lower_page_, &lower_blocks_);
+  alloc_prepared();
+  const int64_t nw = num_weights();
+  sgd_.F = cfg_.num_text_features;
+  sgd_.w64 = dmalloc<double>(size_t(nw));
+  TWTML_HIP_CHECK(hipMemset(sgd_.w64, 0, sizeof(double) * size_t(nw)));  // Vectors.zeros
+  sgd_.red64 = dmalloc<double>(4);
+  sgd_.stats = dmalloc<double>(8);
+  sgd_.state = dmalloc<double>(8);
+  sgd_.loss_hist = dmalloc<double>(size_t(std::max(1, cfg_.num_iterations)) + 2);
+  sgd_.pred_out = dmalloc<float>(size_t(cfg_.max_rows));
+  TWTML_HIP_CHECK(hipMemset(sgd_.red64, 0, 4 * sizeof(double)));
+  ensure_compact(4096);
+  const int world = comm_ ? comm_->world() : 1;
+  n_global_ = dmalloc<int64_t>(size_t(world) + 2);
+  TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_counters_), 8 * sizeof(int64_t),
+                                hipHostMallocDefault));
+  TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_out_),
+                                (32 + size_t(std::max(1, cfg_.num_iterations))) * sizeof(double),
+                                hipHostMallocDefault));
+  TWTML_HIP_CHECK(hipDeviceSynchronize());
+}
+
+void LREngine::alloc_prepared() {
+  const int64_t R = cfg_.max_rows;
+  const int64_t C = (R + kChunk - 1) / kChunk;
+  int64_t E = 2 * cfg_.max_units + C * kChunkStride + 65536;
+  E = (E + kChunkStride - 1) / kChunkStride * kChunkStride;
+  prep_.cap_rows = R;
+  prep_.cap_chunks = C;
+  prep_.cap_entries = E;
+  prep_.kept = dmalloc<int64_t>(size_t(R));
+  prep_.nnz = dmalloc<int32_t>(size_t(R));
+  prep_.sorted = dmalloc<int32_t>(size_t(R));
+  prep_.blk = dmalloc<int64_t>(size_t(R / kBlock + 2));
+  prep_.hist = dmalloc<int64_t>(kLenBuckets + 1);
+  prep_.clen8 = dmalloc<int32_t>(size_t(C) + 1);
+  prep_.cbase = dmalloc<int64_t>(size_t(C) + 1);
+  prep_.idx = dmalloc<int32_t>(size_t(E));
+  prep_.slot = dmalloc<uint32_t>(size_t(E));
+  prep_.y = dmalloc<float>(size_t(C) * kChunk);
+  prep_.num = dmalloc<float>(size_t(C) * 4 * kChunk);
+  prep_.perm = dmalloc<int32_t>(size_t(C) * kChunk);
+  // active-feature flags: Java-hash bigrams are < 2^21 whatever F is
+  const int64_t F = cfg_.num_text_features;
+  int64_t fl = cfg_.hash_kind == 0 ? std::min<int64_t>(F, int64_t(1) << 21) : F;
+  fl = (fl + 4095) / 4096 * 4096;
+  prep_.flag_len = fl;
+  prep_.flags = dmalloc<uint8_t>(size_t(fl));
+  TWTML_HIP_CHECK(hipMemset(prep_.flags, 0, size_t(fl)));
+  prep_.uniq = dmalloc<int32_t>(size_t(fl));
+  prep_.slot_of = dmalloc<int32_t>(size_t(fl));
+  prep_.ublk = dmalloc<int64_t>(size_t(fl / 4096) + 2);
+  prep_.counters = dmalloc<int64_t>(8);
+}
+
+void LREngine::ensure_compact(int64_t ns) {
+  if (ns <= ns_cap_) return;
+  int64_t cap = std::max<int64_t>(ns, ns_cap_ * 2);
+  if (sgd_.wc64) {
+    TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
+    (void)hipFree(sgd_.wc64);
+    (void)hipFree(sgd_.wc32);
+    (void)hipFree(sgd_.g32);
+  }
+  sgd_.wc64 = dmalloc<double>(size_t(cap));
+  sgd_.wc32 = dmalloc<float>(size_t(cap));
+  sgd_.g32 = dmalloc<float>(size_t(cap) + 1);
+  TWTML_HIP_CHECK(hipMemset(sgd_.g32, 0, sizeof(float) * (size_t(cap) + 1)));
+  ns_cap_ = cap;
+}
+
+LREngine::~LREngine() {
+  (void)hipSetDevice(device_);
+  (void)hipDeviceSynchronize();
+  for (auto& s : slots_) {
+    (void)hipFree(s.text); (void)hipFree(s.offsets); (void)hipFree(s.is_rt); (void)hipFree(s.scalars);
+    (void)hipEventDestroy(s.h2d_done); (void)hipEventDestroy(s.consumed);
+  }
+  for (auto& e : ev_) (void)hipEventDestroy(e);
+  void* bufs[] = {prep_.kept, prep_.nnz, prep_.sorted, prep_.blk, prep_.hist, prep_.clen8,
+                  prep_.cbase, prep_.idx, prep_.slot, prep_.y, prep_.num, prep_.perm,
+                  prep_.flags, prep_.uniq, prep_.slot_of, prep_.ublk, prep_.counters,
+                  sgd_.w64, sgd_.wc64, sgd_.wc32, sgd_.g32, sgd_.red64, sgd_.stats, sgd_.state,
+                  sgd_.loss_hist, sgd_.pred_out, lower_page_, lower_blocks_, n_global_};
+  for (void* b : bufs) if (b) (void)hipFree(b);
+  if (host_counters_) (void)hipHostFree(host_counters_);
+  if (host_out_) (void)hipHostFree(host_out_);
+  (void)hipStreamDestroy(compute_);
+  (void)hipStreamDestroy(copy_);
+}
+
+void LREngine::submit(const HostBatch& hb, int64_t n, int64_t units, int slot) {
+  if (slot < 0 || slot > 1) throw std::invalid_argument("slot must be 0 or 1");
+  if (n < 0 || n > cfg_.max_rows || n > hb.max_rows) throw std::invalid_argument("rows exceed capacity");
+  if (units < 0 || units > cfg_.max_units || units > hb.max_units)
+    throw std::invalid_argument("text units exceed capacity");
+  if (n > 0 && hb.offsets[n] != units) throw std::invalid_argument("offsets[n] != units");
+  TWTML_HIP_CHECK(hipSetDevice(device_));
+  Slot& s = slots_[slot];
+  // wait until the compute stream has finished reading this slot
+  if (s.used) TWTML_HIP_CHECK(hipStreamWaitEvent(copy_, s.consumed, 0));
+  if (units > 0)
+    TWTML_HIP_CHECK(hipMemcpyAsync(s.text, hb.text, sizeof(uint16_t) * size_t(units),
+                                   hipMemcpyHostToDevice, copy_));
+  TWTML_HIP_CHECK(hipMemcpyAsync(s.offsets, hb.offsets, sizeof(int64_t) * size_t(n + 1),
+                                 hipMemcpyHostToDevice, copy_));
+  if (n > 0) {
+    TWTML_HIP_CHECK(hipMemcpyAsync(s.is_rt, hb.is_rt, size_t(n), hipMemcpyHostToDevice, copy_));
+    // scalars are packed [5][n] at the start of the host buffer
+    TWTML_HIP_CHECK(hipMemcpyAsync(s.scalars, hb.scalars, sizeof(int64_t) * 5 * size_t(n),
+                                   hipMemcpyHostToDevice, copy_));
+  }
+  TWTML_HIP_CHECK(hipEventRecord(s.h2d_done, copy_));
+  s.n = n;
+  s.units = units;
+  s.used = true;
+}
+
+BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
+  if (slot < 0 || slot > 1) throw std::invalid_argument("slot must be 0 or 1");
+  TWTML_HIP_CHECK(hipSetDevice(device_));
+  Slot& sl = slots_[slot];
+  hipStream_t s = compute_;
+  const int world = comm_ ? comm_->world() : 1;
+  const int rank = comm_ ? comm_->rank() : 0;
+  BatchResult res;
+  res.n_raw = sl.n;
+  TWTML_HIP_CHECK(hipStreamWaitEvent(s, sl.h2d_done, 0));
+  TWTML_HIP_CHECK(hipEventRecord(ev_[0], s));
+
+  DevRawBatch b{sl.text, sl.offsets, sl.is_rt, sl.scalars, sl.n, sl.units};
+  FeaturizeParams fp{cfg_.num_text_features, cfg_.hash_kind, cfg_.require_retweet,
+                     cfg_.range_filter, cfg_.begin, cfg_.end, now_ms};
+  TWTML_HIP_CHECK(hipMemsetAsync(prep_.counters, 0, 8 * sizeof(int64_t), s));
+  launch_filter_sort(b, prep_, fp, s);
+  launch_chunk_layout(b, prep_, s);
+  launch_featurize(b, prep_, fp, lower_page_, lower_blocks_, s);
+  TWTML_HIP_CHECK(hipEventRecord(sl.consumed, s));  // raw slot may be overwritten now
+  if (world > 1) comm_->allreduce(prep_.flags, size_t(prep_.flag_len), ncclUint8, ncclMax, s);
+  launch_compact_active(prep_, s);
+  // global kept count (and per-rank counts for sampling offsets)
+  TWTML_HIP_CHECK(hipMemsetAsync(n_global_, 0, sizeof(int64_t) * size_t(world + 2), s));
+  TWTML_HIP_CHECK(hipMemcpyAsync(n_global_ + 1 + rank, prep_.counters, sizeof(int64_t),
+                                 hipMemcpyDeviceToDevice, s));
+  if (world > 1) comm_->allreduce(n_global_ + 1, size_t(world), ncclInt64, ncclSum, s);
+  TWTML_HIP_CHECK(hipMemcpyAsync(host_counters_, prep_.counters, 4 * sizeof(int64_t),
+                                 hipMemcpyDeviceToHost, s));
+  TWTML_HIP_CHECK(hipMemcpyAsync(host_counters_ + 4, n_global_ + 1,
+                                 sizeof(int64_t) * size_t(std::min(world, 4)), hipMemcpyDeviceToHost, s));
+  std::vector<int64_t> per_rank(size_t(world), 0);
+  TWTML_HIP_CHECK(hipStreamSynchronize(s));
+  if (host_counters_[3] != 0) throw std::runtime_error("feature buffer capacity exceeded");
+  res.n_kept = host_counters_[0];
+  res.n_unique = host_counters_[1];
+  res.entries = host_counters_[2] * kChunkStride;
+  int64_t row_offset = 0, n_glob = 0;
+  if (world <= 4) {
+    for (int r = 0; r < world; ++r) per_rank[size_t(r)] = host_counters_[4 + r];
+  } else {
+    TWTML_HIP_CHECK(hipMemcpy(per_rank.data(), n_global_ + 1, sizeof(int64_t) * size_t(world),
+                              hipMemcpyDeviceToHost));
+  }
+  for (int r = 0; r < world; ++r) {
+    if (r < rank) row_offset += per_rank[size_t(r)];
+    n_glob += per_rank[size_t(r)];
+  }
+  res.n_kept_global = n_glob;
+
+  // ---- compact space
+  const int64_t nU = res.n_unique;
+  int64_t ns = kNumNumeric + nU + kPadSlots;
+  ns = (ns + 63) / 64 * 64;
+  ensure_compact(ns);
+  sgd_.ns = ns;
+  sgd_.n_unique = nU;
+  const bool u16 = ns <= 65536;
+  launch_remap(prep_, res.entries, nU, u16, s);
+  TWTML_HIP_CHECK(hipMemsetAsync(sgd_.state, 0, 8 * sizeof(double), s));
+  TWTML_HIP_CHECK(hipMemsetAsync(sgd_.stats, 0, 8 * sizeof(double), s));
+  TWTML_HIP_CHECK(hipMemsetAsync(sgd_.red64, 0, 4 * sizeof(double), s));
+  TWTML_HIP_CHECK(hipMemsetAsync(sgd_.g32 + ns, 0, sizeof(float), s));
+  TWTML_HIP_CHECK(hipMemsetAsync(sgd_.loss_hist, 0, sizeof(double) * size_t(cfg_.num_iterations + 2), s));
+  launch_batch_init(sgd_.state, double(n_glob), s);  // state[5] = m (global kept rows)
+  launch_norm2(sgd_.w64, num_weights(), &sgd_.state[4], s);
+  launch_gather_w(sgd_, prep_, s);
+  TWTML_HIP_CHECK(hipEventRecord(ev_[1], s));
+
+  const int64_t nch = (res.n_kept + kChunk - 1) / kChunk;
+  int grid = cfg_.sgd_grid;
+  if (grid <= 0) {
+    const int64_t lds = 2 * ns * int64_t(sizeof(float));
+    int per_cu = lds > 0 ? int(std::min<int64_t>(4, (160 * 1024) / std::max<int64_t>(lds, 1))) : 4;
+    if (per_cu < 1) per_cu = 1;
+    if (per_cu > 2) per_cu = 2;
+    grid = num_cu_ * per_cu;
+  }
+  grid = int(std::max<int64_t>(1, std::min<int64_t>(grid, (nch + 3) / 4)));
+
+  SgdParams sp{};
+  sp.step_size = cfg_.step_size;
+  sp.fraction = cfg_.fraction;
+  sp.tol = cfg_.tol;
+  sp.num_iterations = cfg_.num_iterations;
+  sp.row_offset = row_offset;
+  sp.want_pred = want_pred ? 1 : 0;
+  sp.sample = cfg_.fraction < 1.0 ? 1 : 0;
+  if (n_glob > 0) {
+    for (int i = 1; i <= cfg_.num_iterations; ++i) {
+      sp.iteration = i;
+      if (res.n_kept > 0) launch_sgd_iter(sgd_, prep_, sp, host_counters_[2], u16, grid, s);
+      else if (i == 1 || sp.sample) {
+        // nothing local to add; still participate in the collectives below
+      }
+      if (world > 1) {
+        comm_->allreduce(sgd_.g32, size_t(ns + 1), ncclFloat32, ncclSum, s);
+        if (sp.sample) comm_->allreduce(sgd_.red64, 2, ncclFloat64, ncclSum, s);
+      }
+      launch_sgd_update(sgd_, sp, s);
+    }
+    launch_scatter_w(sgd_, prep_, s);
+  }
+  TWTML_HIP_CHECK(hipEventRecord(ev_[2], s));
+  if (world > 1) comm_->allreduce(sgd_.stats, 6, ncclFloat64, ncclSum, s);
+  TWTML_HIP_CHECK(hipMemcpyAsync(host_out_, sgd_.stats, 8 * sizeof(double), hipMemcpyDeviceToHost, s));
+  TWTML_HIP_CHECK(hipMemcpyAsync(host_out_ + 8, sgd_.state, 8 * sizeof(double), hipMemcpyDeviceToHost, s));
+  TWTML_HIP_CHECK(hipMemcpyAsync(host_out_ + 16, sgd_.loss_hist,
+                                 sizeof(double) * size_t(cfg_.num_iterations + 1),
+                                 hipMemcpyDeviceToHost, s));
+  if (want_pred && res.n_kept > 0) res.pred.resize(size_t(res.n_kept));
+  if (want_pred && res.n_kept > 0)
+    TWTML_HIP_CHECK(hipMemcpyAsync(res.pred.data(), sgd_.pred_out, sizeof(float) * size_t(res.n_kept),
+                                   hipMemcpyDeviceToHost, s));
+  TWTML_HIP_CHECK(hipStreamSynchronize(s));
+  if (comm_) comm_->check_async();
+  for (int k = 0; k < 6; ++k) res.stats[k] = host_out_[k];
+  const double* st = host_out_ + 8;
+  res.converged = st[1] != 0.0;
+  res.iterations = int32_t(st[3]);
+  for (int i = 1; i <= res.iterations; ++i) res.loss_history.push_back(host_out_[16 + i]);
+  TWTML_HIP_CHECK(hipEventElapsedTime(&res.prep_ms, ev_[0], ev_[1]));
+  TWTML_HIP_CHECK(hipEventElapsedTime(&res.train_ms, ev_[1], ev_[2]));
+  return res;
+}
+
+void LREngine::set_weights(const double* w, int64_t n) {
+  if (n != num_weights()) throw std::invalid_argument("weights size mismatch");
+  TWTML_HIP_CHECK(hipSetDevice(device_));
+  TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
+  TWTML_HIP_CHECK(hipMemcpy(sgd_.w64, w, sizeof(double) * size_t(n), hipMemcpyHostToDevice));
+}
+
+void LREngine::get_weights(double* w, int64_t n) const {
+  if (n != num_weights()) throw std::invalid_argument("weights size mismatch");
+  TWTML_HIP_CHECK(hipSetDevice(device_));
+  TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
+  TWTML_HIP_CHECK(hipMemcpy(w, sgd_.w64, sizeof(double) * size_t(n), hipMemcpyDeviceToHost));
+}
+
+void LREngine::set_step(double step, int iters, double fraction) {
+  if (iters > cfg_.num_iterations) throw std::invalid_argument("cannot raise numIterations after init");
+  cfg_.step_size = step;
+  cfg_.num_iterations = iters;
+  cfg_.fraction = fraction;
+}
+
+void LREngine::synchronize() {
+  TWTML_HIP_CHECK(hipSetDevice(device_));
+  TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
+  TWTML_HIP_CHECK(hipStreamSynchronize(copy_));
+}
+
+void LREngine::debug_prepared(std::vector<int64_t>& counters, std::vector<int32_t>& clen8,
+                              std::vector<int64_t>& cbase, std::vector<int32_t>& idx,
+                              std::vector<int32_t>& perm, std::vector<float>& y,
+                              std::vector<float>& num, std::vector<int32_t>& uniq) {
+  TWTML_HIP_CHECK(hipSetDevice(device_));
+  TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
+  counters.resize(4);
+  TWTML_HIP_CHECK(hipMemcpy(counters.data(), prep_.counters, 4 * sizeof(int64_t), hipMemcpyDeviceToHost));
+  const int64_t nk = counters[0], nu = counters[1], groups = counters[2];
+  const int64_t C = (nk + kChunk - 1) / kChunk;
+  clen8.resize(size_t(C));
+  cbase.resize(size_t(C));
+  idx.resize(size_t(groups * kChunkStride));
+  perm.resize(size_t(C * kChunk));
+  y.resize(size_t(C * kChunk));
+  num.resize(size_t(C * 4 * kChunk));
+  uniq.resize(size_t(nu));
+  if (C) {
+    TWTML_HIP_CHECK(hipMemcpy(clen8.data(), prep_.clen8, sizeof(int32_t) * size_t(C), hipMemcpyDeviceToHost));
+    TWTML_HIP_CHECK(hipMemcpy(cbase.data(), prep_.cbase, sizeof(int64_t) * size_t(C), hipMemcpyDeviceToHost));
+    TWTML_HIP_CHECK(hipMemcpy(perm.data(), prep_.perm, sizeof(int32_t) * size_t(C * kChunk), hipMemcpyDeviceToHost));
+    TWTML_HIP_CHECK(hipMemcpy(y.data(), prep_.y, sizeof(float) * size_t(C * kChunk), hipMemcpyDeviceToHost));
+    TWTML_HIP_CHECK(hipMemcpy(num.data(), prep_.num, sizeof(float) * size_t(C * 4 * kChunk), hipMemcpyDeviceToHost));
+  }
+  if (groups)
+    TWTML_HIP_CHECK(hipMemcpy(idx.data(), prep_.idx, sizeof(int32_t) * idx.size(), hipMemcpyDeviceToHost));
+  if (nu)
+    TWTML_HIP_CHECK(hipMemcpy(uniq.data(), prep_.uniq, sizeof(int32_t) * size_t(nu), hipMemcpyDeviceToHost));
+}
+
+}  // namespace twtml

@@ -1,0 +1,115 @@
+// MI355X micro-batch engine for StreamingLinearRegressionWithSGD.
+//
+// One engine per process/GPU.  A micro-batch flows:
+//   pinned host RawBatch --(copy stream, async H2D)--> device slot (x2)
+//   compute stream: filter -> length sort -> featurize -> [RCCL max of the
+//   active-feature flags] -> compact -> remap -> gather w ->
+//   numIterations x ( fused predict/gradient kernel -> [RCCL all-reduce of
+//   the packed gradient] -> fp64 update + convergence ) -> scatter w
+// Two device slots let batch t+1's H2D overlap batch t's training (SURVEY
+// §2.4 "Ingest || compute pipelining").  Output op #1 (prequential stats)
+// is fused into iteration 1, so it sees the weights before training on the
+// batch (LinearRegression.scala:53-86 ordering).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "comm.h"
+#include "common.h"
+#include "kernels.h"
+
+namespace twtml {
+
+struct LRConfig {
+  int64_t num_text_features = 1000;
+  int32_t hash_kind = 0;
+  double step_size = 0.005;
+  int32_t num_iterations = 50;
+  double fraction = 1.0;
+  double tol = 1e-3;
+  int64_t begin = 100, end = 1000;
+  int32_t require_retweet = 1, range_filter = 1;
+  int64_t max_rows = 1 << 16;
+  int64_t max_units = (1 << 16) * 281;
+  int32_t sgd_grid = 0;       // 0 = auto
+  int32_t early_exit_depth = 3;  // host run-ahead (iterations) for early stop
+};
+
+struct HostBatch {
+  void* base = nullptr;
+  size_t bytes = 0;
+  uint16_t* text = nullptr;
+  int64_t* offsets = nullptr;
+  uint8_t* is_rt = nullptr;
+  int64_t* scalars = nullptr;
+  int64_t max_rows = 0, max_units = 0;
+  HostBatch(int64_t rows, int64_t units);
+  ~HostBatch();
+};
+
+struct BatchResult {
+  int64_t n_raw = 0, n_kept = 0, n_kept_global = 0, n_unique = 0, entries = 0;
+  int32_t iterations = 0;
+  bool converged = false;
+  double stats[6] = {0, 0, 0, 0, 0, 0};  // n, sum y, sum y^2, sum p, sum p^2, sum (y-p)^2
+  std::vector<double> loss_history;
+  std::vector<float> pred;
+  float prep_ms = 0.f, train_ms = 0.f;
+};
+
+class LREngine {
+ public:
+  LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm);
+  ~LREngine();
+
+  // Async H2D of rows [0, n) of a pinned host batch into device slot `slot`.
+  void submit(const HostBatch& hb, int64_t n, int64_t units, int slot);
+  // Train on the batch in `slot` (blocks until done); stats use w before training.
+  BatchResult process(int slot, int64_t now_ms, bool want_pred);
+
+  void set_weights(const double* w, int64_t n);
+  void get_weights(double* w, int64_t n) const;
+  int64_t num_weights() const { return cfg_.num_text_features + kNumNumeric; }
+  const LRConfig& config() const { return cfg_; }
+  void set_step(double step, int iters, double fraction);
+  void synchronize();
+  int device() const { return device_; }
+  // Debug/test access to the last batch's prepared features (host copies).
+  void debug_prepared(std::vector<int64_t>& counters, std::vector<int32_t>& clen8,
+                      std::vector<int64_t>& cbase, std::vector<int32_t>& idx,
+                      std::vector<int32_t>& perm, std::vector<float>& y,
+                      std::vector<float>& num, std::vector<int32_t>& uniq);
+
+ private:
+  void alloc_prepared();
+  void ensure_compact(int64_t ns);
+
+  int device_;
+  LRConfig cfg_;
+  std::shared_ptr<Comm> comm_;
+  hipStream_t compute_ = nullptr, copy_ = nullptr;
+  struct Slot {
+    uint16_t* text = nullptr;
+    int64_t* offsets = nullptr;
+    uint8_t* is_rt = nullptr;
+    int64_t* scalars = nullptr;
+    int64_t n = 0, units = 0;
+    hipEvent_t h2d_done = nullptr, consumed = nullptr;
+    bool used = false;
+  } slots_[2];
+  DevPrepared prep_{};
+  DevSgd sgd_{};
+  int64_t ns_cap_ = 0;
+  uint8_t* lower_page_ = nullptr;
+  uint16_t* lower_blocks_ = nullptr;
+  int64_t* host_counters_ = nullptr;  // pinned [8]
+  double* host_out_ = nullptr;        // pinned [16 + iters]
+  int64_t* n_global_ = nullptr;       // device [world + 1]
+  hipEvent_t ev_[4] = {nullptr, nullptr, nullptr, nullptr};
+  int num_cu_ = 256;
+};
+
+}  // namespace twtml

@@ -1,0 +1,407 @@
+// Ingest-side kernels: filter (K3), length sort, SELL-64 layout, bigram
+// hashing + numeric features (K1+K2), active-set compaction and remap.
+//
+// Reference semantics: MllibHelper.filtrate / featurize
+// (spark/src/main/scala/com/giorgioinf/twtml/spark/MllibHelper.scala:42-95).
+//
+// Layout produced for the SGD kernels ("SELL-64", length-sorted):
+//   kept rows are sorted by descending bigram count, cut into chunks of 64
+//   rows (one row per lane); chunk c owns clen8[c] groups of 8 entries per
+//   lane; entry j of the row in lane l lives at
+//       (cbase[c] + j/8) * 512 + l * 8 + j % 8
+//   so one 16-byte load gives a lane 8 consecutive u16 slots and a wave
+//   reads 1 KiB contiguous per instruction.  Padding entries point at a
+//   per-lane zero-weight pad slot.
+#include <hip/hip_runtime.h>
+
+#include "../common/unicode_tables.h"
+#include "common.h"
+#include "kernels.h"
+
+namespace twtml {
+
+// ---------------------------------------------------------------------------
+// Generic single-workgroup exclusive scan (int64), in-place safe.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_scan_excl(const int64_t* in, int64_t* out, int64_t n,
+                                                    int64_t* total) {
+  __shared__ int64_t wsum[16];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int64_t carry = 0;
+  for (int64_t base = 0; base < n; base += 1024) {
+    const int64_t i = base + tid;
+    const int64_t v = i < n ? in[i] : 0;
+    int64_t x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int64_t y = __shfl_up(x, off, 64);
+      if (lane >= off) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    int64_t woff = 0, tile = 0;
+    for (int k = 0; k < 16; ++k) {
+      if (k < w) woff += wsum[k];
+      tile += wsum[k];
+    }
+    if (i < n) out[i] = carry + woff + x - v;
+    carry += tile;
+    __syncthreads();
+  }
+  if (tid == 0 && total) *total = carry;
+}
+
+static void scan_excl(const int64_t* in, int64_t* out, int64_t n, int64_t* total, hipStream_t s) {
+  hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, s, in, out, n, total);
+}
+
+// ---------------------------------------------------------------------------
+// K3 filter: isRetweet && begin <= retweetCount <= end, order-preserving.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool keep_row(const DevRawBatch& b, int64_t r, const FeaturizeParams& fp) {
+  if (r >= b.n) return false;
+  if (fp.require_retweet && !b.is_rt[r]) return false;
+  if (fp.range_filter) {
+    const int64_t rc = b.scalars[r];
+    if (rc < fp.begin || rc > fp.end) return false;
+  }
+  return true;
+}
+
+__global__ __launch_bounds__(kBlock) void k_filter_count(DevRawBatch b, FeaturizeParams fp,
+                                                         int64_t* blk) {
+  const int64_t r = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  const int c = __syncthreads_count(keep_row(b, r, fp));
+  if (threadIdx.x == 0) blk[blockIdx.x] = c;
+}
+
+__global__ __launch_bounds__(kBlock) void k_filter_write(DevRawBatch b, FeaturizeParams fp,
+                                                         const int64_t* blk_off, int64_t* kept,
+                                                         int32_t* nnz, int64_t* hist) {
+  __shared__ int wtot[kBlock / kWave];
+  const int64_t r = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  const bool pred = keep_row(b, r, fp);
+  const uint64_t mask = __ballot(pred);
+  const int lane = lane_id(), w = threadIdx.x / kWave;
+  const int wpre = __popcll(mask & ((1ull << lane) - 1ull));
+  if (lane == 0) wtot[w] = __popcll(mask);
+  __syncthreads();
+  int woff = 0;
+  for (int k = 0; k < w; ++k) woff += wtot[k];
+  if (pred) {
+    const int64_t k = blk_off[blockIdx.x] + woff + wpre;
+    kept[k] = r;
+    const int64_t len = b.offsets[r + 1] - b.offsets[r];
+    const int64_t nz = len >= 2 ? len - 1 : len;
+    const int32_t n32 = int32_t(nz > 0x7fffffff ? 0x7fffffff : nz);
+    nnz[k] = n32;
+    const int key = kLenBuckets - 1 - (n32 < kLenBuckets - 1 ? n32 : kLenBuckets - 1);
+    atomicAdd(reinterpret_cast<unsigned long long*>(&hist[key]), 1ull);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_sort_scatter(const int32_t* nnz, const int64_t* counters,
+                                                         int64_t* cursor, int32_t* sorted,
+                                                         int64_t cap) {
+  const int64_t n_kept = counters[0];
+  for (int64_t k = int64_t(blockIdx.x) * kBlock + threadIdx.x; k < n_kept && k < cap;
+       k += int64_t(gridDim.x) * kBlock) {
+    const int32_t n32 = nnz[k];
+    const int key = kLenBuckets - 1 - (n32 < kLenBuckets - 1 ? n32 : kLenBuckets - 1);
+    const int64_t pos = int64_t(atomicAdd(reinterpret_cast<unsigned long long*>(&cursor[key]), 1ull));
+    sorted[pos] = int32_t(k);
+  }
+}
+
+void launch_filter_sort(const DevRawBatch& b, const DevPrepared& p, const FeaturizeParams& fp,
+                        hipStream_t s) {
+  const int nb = ceil_div(b.n > 0 ? b.n : 1, kBlock);
+  TWTML_HIP_CHECK(hipMemsetAsync(p.hist, 0, sizeof(int64_t) * (kLenBuckets + 1), s));
+  hipLaunchKernelGGL(k_filter_count, dim3(nb), dim3(kBlock), 0, s, b, fp, p.blk);
+  scan_excl(p.blk, p.blk, nb, &p.counters[0], s);
+  hipLaunchKernelGGL(k_filter_write, dim3(nb), dim3(kBlock), 0, s, b, fp, p.blk, p.kept, p.nnz,
+                     p.hist);
+  scan_excl(p.hist, p.hist, kLenBuckets, nullptr, s);
+  const int g = nb < 2048 ? nb : 2048;
+  hipLaunchKernelGGL(k_sort_scatter, dim3(g), dim3(kBlock), 0, s, p.nnz, p.counters, p.hist,
+                     p.sorted, p.cap_rows);
+}
+
+// ---------------------------------------------------------------------------
+// Chunk layout: groups of 8 entries per lane for every 64-row chunk.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_chunk_len(const int32_t* sorted, const int32_t* nnz,
+                                                      const int64_t* counters, int64_t cmax,
+                                                      int64_t* clen_scratch, int32_t* clen8) {
+  const int64_t n_kept = counters[0];
+  const int lane = lane_id();
+  const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
+  const int64_t nwaves = int64_t(gridDim.x) * kBlock / kWave;
+  for (int64_t c = wave; c < cmax; c += nwaves) {
+    const int64_t p = c * kChunk + lane;
+    const int32_t v = p < n_kept ? nnz[sorted[p]] : 0;
+    const int32_t mx = wave_max(v);
+    const int32_t g = (mx + kGroup - 1) / kGroup;
+    if (lane == 0) {
+      clen8[c] = g;
+      clen_scratch[c] = g;
+    }
+  }
+}
+
+void launch_chunk_layout(const DevRawBatch& b, const DevPrepared& p, hipStream_t s) {
+  const int64_t cmax = (b.n + kChunk - 1) / kChunk;
+  if (cmax == 0) {
+    TWTML_HIP_CHECK(hipMemsetAsync(p.cbase, 0, sizeof(int64_t), s));
+    TWTML_HIP_CHECK(hipMemsetAsync(&p.counters[2], 0, sizeof(int64_t), s));
+    return;
+  }
+  const int grid = ceil_div(cmax, kBlock / kWave) < 4096 ? ceil_div(cmax, kBlock / kWave) : 4096;
+  hipLaunchKernelGGL(k_chunk_len, dim3(grid), dim3(kBlock), 0, s, p.sorted, p.nnz, p.counters,
+                     cmax, p.cbase, p.clen8);
+  scan_excl(p.cbase, p.cbase, cmax, &p.counters[2], s);
+}
+
+// ---------------------------------------------------------------------------
+// K1 + K2: lower-case, bigram hash, numeric features, active-set flags.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lower_dev(uint32_t c, const uint8_t* page, const uint16_t* blocks) {
+  if (c < 128) return (c >= 'A' && c <= 'Z') ? c + 32 : c;
+  return (c + blocks[page[c >> 8] * 256 + (c & 255)]) & 0xFFFFu;
+}
+
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+__device__ __forceinline__ uint32_t mur_k(uint32_t k) { return rotl32(k * 0xCC9E2D51u, 15) * 0x1B873593u; }
+__device__ __forceinline__ uint32_t mur_h(uint32_t h, uint32_t k) { return rotl32(h ^ k, 13) * 5u + 0xE6546B64u; }
+
+// Spark-2 murmur3 (hashUnsafeBytes, seed 42) of the UTF-8 bytes of a
+// 1-2 unit Java string (lone surrogates become '?').
+__device__ int32_t murmur_term(uint32_t u0, uint32_t u1, int n) {
+  uint8_t b[8];
+  int k = 0;
+  auto put = [&](uint32_t cp) {
+    if (cp < 0x80) { b[k++] = uint8_t(cp); }
+    else if (cp < 0x800) { b[k++] = uint8_t(0xC0 | (cp >> 6)); b[k++] = uint8_t(0x80 | (cp & 0x3F)); }
+    else if (cp < 0x10000) {
+      b[k++] = uint8_t(0xE0 | (cp >> 12)); b[k++] = uint8_t(0x80 | ((cp >> 6) & 0x3F));
+      b[k++] = uint8_t(0x80 | (cp & 0x3F));
+    } else {
+      b[k++] = uint8_t(0xF0 | (cp >> 18)); b[k++] = uint8_t(0x80 | ((cp >> 12) & 0x3F));
+      b[k++] = uint8_t(0x80 | ((cp >> 6) & 0x3F)); b[k++] = uint8_t(0x80 | (cp & 0x3F));
+    }
+  };
+  const bool hi0 = u0 >= 0xD800 && u0 <= 0xDBFF, sur0 = u0 >= 0xD800 && u0 <= 0xDFFF;
+  if (n == 2 && hi0 && u1 >= 0xDC00 && u1 <= 0xDFFF) {
+    put(0x10000u + ((u0 - 0xD800u) << 10) + (u1 - 0xDC00u));
+  } else {
+    put(sur0 ? '?' : u0);
+    if (n == 2) put((u1 >= 0xD800 && u1 <= 0xDFFF) ? '?' : u1);
+  }
+  uint32_t h = 42u;
+  const int aligned = k - k % 4;
+  for (int i = 0; i < aligned; i += 4)
+    h = mur_h(h, mur_k(uint32_t(b[i]) | (uint32_t(b[i + 1]) << 8) | (uint32_t(b[i + 2]) << 16) |
+                       (uint32_t(b[i + 3]) << 24)));
+  for (int i = aligned; i < k; ++i) h = mur_h(h, mur_k(uint32_t(int32_t(int8_t(b[i])))));
+  h ^= uint32_t(k);
+  h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+  return int32_t(h);
+}
+
+__device__ __forceinline__ int64_t term_mod(int64_t h, int64_t F) {
+  const int64_t m = h % F;
+  return m < 0 ? m + F : m;
+}
+
+__global__ __launch_bounds__(kBlock) void k_featurize(DevRawBatch b, DevPrepared p, FeaturizeParams fp,
+                                                      const uint8_t* lpage, const uint16_t* lblocks,
+                                                      int64_t cmax) {
+  const int64_t n_kept = p.counters[0];
+  const int lane = lane_id();
+  const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
+  const int64_t nwaves = int64_t(gridDim.x) * kBlock / kWave;
+  const int64_t F = fp.num_text_features;
+  const int64_t cap_groups = p.cap_entries / kChunkStride;
+  for (int64_t c = wave; c < cmax; c += nwaves) {
+    const int64_t pos = c * kChunk + lane;
+    const bool valid = pos < n_kept;
+    const int32_t kidx = valid ? p.sorted[pos] : -1;
+    const int64_t row = valid ? p.kept[kidx] : 0;
+    const int32_t L8 = p.clen8[c];
+    const int64_t g0 = p.cbase[c];
+    if (g0 + L8 > cap_groups) {
+      if (lane == 0) p.counters[3] = 1;  // capacity overflow -> host raises
+      continue;
+    }
+    const int64_t o = valid ? b.offsets[row] : 0;
+    const int64_t len = valid ? b.offsets[row + 1] - o : 0;
+    const int64_t nz = len >= 2 ? len - 1 : len;
+    int32_t* out = p.idx + g0 * kChunkStride + lane * kGroup;
+    uint32_t prev = len > 0 ? lower_dev(b.text[o], lpage, lblocks) : 0;
+    const int32_t total = L8 * kGroup;
+    for (int32_t j = 0; j < total; ++j) {
+      int32_t v = -1;
+      if (j < nz) {
+        int64_t h;
+        if (len >= 2) {
+          const uint32_t nxt = lower_dev(b.text[o + j + 1], lpage, lblocks);
+          h = fp.hash_kind == 0 ? int64_t(31u * prev + nxt) : int64_t(murmur_term(prev, nxt, 2));
+          prev = nxt;
+        } else {
+          h = fp.hash_kind == 0 ? int64_t(prev) : int64_t(murmur_term(prev, 0, 1));
+        }
+        const int64_t idx = term_mod(h, F);
+        v = int32_t(idx);
+        if (idx < p.flag_len) p.flags[idx] = 1;
+      }
+      out[(j >> 3) * kChunkStride + (j & 7)] = v;
+    }
+    const int64_t q = c * kChunk + lane;
+    if (valid) {
+      const int64_t* sc = b.scalars;
+      p.y[q] = float(sc[row]);
+      const double fol = double(sc[1 * b.n + row]), fav = double(sc[2 * b.n + row]);
+      const double fri = double(sc[3 * b.n + row]);
+      const double age = double(fp.now_ms - sc[4 * b.n + row]);
+      p.num[(c * 4 + 0) * kChunk + lane] = float(fol * 1e-12);
+      p.num[(c * 4 + 1) * kChunk + lane] = float(fav * 1e-12);
+      p.num[(c * 4 + 2) * kChunk + lane] = float(fri * 1e-12);
+      p.num[(c * 4 + 3) * kChunk + lane] = float(age * 1e-14);
+    } else {
+      p.y[q] = 0.f;
+      for (int k = 0; k < 4; ++k) p.num[(c * 4 + k) * kChunk + lane] = 0.f;
+    }
+    p.perm[q] = kidx;
+  }
+}
+
+void launch_featurize(const DevRawBatch& b, const DevPrepared& p, const FeaturizeParams& fp,
+                      const uint8_t* lpage, const uint16_t* lblocks, hipStream_t s) {
+  const int64_t cmax = (b.n + kChunk - 1) / kChunk;
+  if (cmax == 0) return;
+  int grid = ceil_div(cmax, kBlock / kWave);
+  if (grid > 8192) grid = 8192;
+  hipLaunchKernelGGL(k_featurize, dim3(grid), dim3(kBlock), 0, s, b, p, fp, lpage, lblocks, cmax);
+}
+
+// ---------------------------------------------------------------------------
+// Active-set compaction: flags[Fh] -> sorted unique ids + slot_of, clears flags
+// ---------------------------------------------------------------------------
+constexpr int kFlagsPerThread = 16;
+constexpr int kFlagsPerBlock = kBlock * kFlagsPerThread;  // 4096
+
+__device__ __forceinline__ int count_bytes(uint4 v) {
+  int c = 0;
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) c += ((w[i] >> (8 * k)) & 0xFF) ? 1 : 0;
+  return c;
+}
+
+__global__ __launch_bounds__(kBlock) void k_compact_count(const uint8_t* flags, int64_t* ublk) {
+  __shared__ int64_t scratch[kBlock / kWave];
+  const int64_t base = int64_t(blockIdx.x) * kFlagsPerBlock + threadIdx.x * kFlagsPerThread;
+  const uint4 v = *reinterpret_cast<const uint4*>(flags + base);
+  const int64_t c = block_sum<int64_t>(count_bytes(v), scratch);
+  if (threadIdx.x == 0) ublk[blockIdx.x] = c;
+}
+
+__global__ __launch_bounds__(kBlock) void k_compact_write(uint8_t* flags, const int64_t* ublk_off,
+                                                          int32_t* uniq, int32_t* slot_of) {
+  __shared__ int wtot[kBlock / kWave];
+  const int lane = lane_id(), w = threadIdx.x / kWave;
+  const int64_t base = int64_t(blockIdx.x) * kFlagsPerBlock + threadIdx.x * kFlagsPerThread;
+  uint4* ptr = reinterpret_cast<uint4*>(flags + base);
+  const uint4 v = *ptr;
+  const int c = count_bytes(v);
+  int x = c;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) wtot[w] = x;
+  __syncthreads();
+  int woff = 0;
+  for (int k = 0; k < w; ++k) woff += wtot[k];
+  int64_t pos = ublk_off[blockIdx.x] + woff + x - c;
+  if (c) {
+    const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
+    for (int i = 0; i < 4; ++i)
+      for (int k = 0; k < 4; ++k)
+        if ((ws[i] >> (8 * k)) & 0xFF) {
+          const int64_t id = base + i * 4 + k;
+          uniq[pos] = int32_t(id);
+          slot_of[id] = int32_t(pos);
+          ++pos;
+        }
+    *ptr = make_uint4(0, 0, 0, 0);
+  }
+}
+
+void launch_compact_active(const DevPrepared& p, hipStream_t s) {
+  const int nb = int(p.flag_len / kFlagsPerBlock);  // flag_len is padded to 4096
+  hipLaunchKernelGGL(k_compact_count, dim3(nb), dim3(kBlock), 0, s, p.flags, p.ublk);
+  scan_excl(p.ublk, p.ublk, nb, &p.counters[1], s);
+  hipLaunchKernelGGL(k_compact_write, dim3(nb), dim3(kBlock), 0, s, p.flags, p.ublk, p.uniq,
+                     p.slot_of);
+}
+
+// ---------------------------------------------------------------------------
+// Remap hashed ids to compact slots: slot = 4 + slot_of[id]; pad -> per-lane pad.
+// ---------------------------------------------------------------------------
+template <typename SlotT>
+__global__ __launch_bounds__(kBlock) void k_remap(const int32_t* idx, const int32_t* slot_of,
+                                                  SlotT* slot, int64_t entries, int64_t pad_base) {
+  for (int64_t e8 = int64_t(blockIdx.x) * kBlock + threadIdx.x; e8 * 8 < entries;
+       e8 += int64_t(gridDim.x) * kBlock) {
+    const int4* src = reinterpret_cast<const int4*>(idx + e8 * 8);
+    const int4 a = src[0], bb = src[1];
+    const int32_t v[8] = {a.x, a.y, a.z, a.w, bb.x, bb.y, bb.z, bb.w};
+    const SlotT pad = SlotT(pad_base + ((e8) & 63));  // (e >> 3) & 63 = lane of the group
+    SlotT out[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) out[k] = v[k] >= 0 ? SlotT(kNumNumeric + slot_of[v[k]]) : pad;
+    if constexpr (sizeof(SlotT) == 2) {
+      uint4 pk;
+      pk.x = uint32_t(out[0]) | (uint32_t(out[1]) << 16);
+      pk.y = uint32_t(out[2]) | (uint32_t(out[3]) << 16);
+      pk.z = uint32_t(out[4]) | (uint32_t(out[5]) << 16);
+      pk.w = uint32_t(out[6]) | (uint32_t(out[7]) << 16);
+      reinterpret_cast<uint4*>(slot)[e8] = pk;
+    } else {
+      uint4* dst = reinterpret_cast<uint4*>(slot + e8 * 8);
+      dst[0] = make_uint4(out[0], out[1], out[2], out[3]);
+      dst[1] = make_uint4(out[4], out[5], out[6], out[7]);
+    }
+  }
+}
+
+void launch_remap(const DevPrepared& p, int64_t entries, int64_t n_unique, bool u16, hipStream_t s) {
+  if (entries == 0) return;
+  const int64_t n8 = entries / 8;
+  int grid = ceil_div(n8, kBlock);
+  if (grid > 16384) grid = 16384;
+  const int64_t pad_base = kNumNumeric + n_unique;
+  if (u16)
+    hipLaunchKernelGGL(k_remap<uint16_t>, dim3(grid), dim3(kBlock), 0, s, p.idx, p.slot_of,
+                       static_cast<uint16_t*>(p.slot), entries, pad_base);
+  else
+    hipLaunchKernelGGL(k_remap<uint32_t>, dim3(grid), dim3(kBlock), 0, s, p.idx, p.slot_of,
+                       static_cast<uint32_t*>(p.slot), entries, pad_base);
+}
+
+// ---------------------------------------------------------------------------
+void upload_lower_tables(hipStream_t s, uint8_t** d_page, uint16_t** d_blocks) {
+  TWTML_HIP_CHECK(hipMalloc(d_page, 256));
+  TWTML_HIP_CHECK(hipMalloc(d_blocks, sizeof(uint16_t) * 256 * uni::kLowerNumBlocks));
+  TWTML_HIP_CHECK(hipMemcpyAsync(*d_page, uni::kLowerPage, 256, hipMemcpyHostToDevice, s));
+  TWTML_HIP_CHECK(hipMemcpyAsync(*d_blocks, uni::kLowerBlocks,
+                                 sizeof(uint16_t) * 256 * uni::kLowerNumBlocks,
+                                 hipMemcpyHostToDevice, s));
+  TWTML_HIP_CHECK(hipStreamSynchronize(s));
+}
+
+}  // namespace twtml

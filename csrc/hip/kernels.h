@@ -1,0 +1,132 @@
+// Host-callable launchers of the engine's HIP kernels.
+//
+// Kernel map:
+//   K3  filter + stream compaction          launch_filter
+//       length counting-sort (SELL-64 prep)  launch_sort_rows / launch_chunk_layout
+//   K1+K2 bigram hash + numeric features     launch_featurize
+//       active-set union / slot compaction   launch_compact_active / launch_remap
+//   K4+K5 predict + LSQ gradient (fused)     launch_sgd_iter
+//   K6  SimpleUpdater + convergence          launch_sgd_update
+//   K7  batch stats (fused into K4 at i=1)
+//   K8-K11 k-means / scaler                  kmeans.hip
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace twtml {
+
+// ---------------------------------------------------------------------------
+// Raw batch on the device (one ingest slot).
+struct DevRawBatch {
+  const uint16_t* text;     // [units]
+  const int64_t* offsets;   // [n+1]
+  const uint8_t* is_rt;     // [n]
+  const int64_t* scalars;   // [5][n]
+  int64_t n;                // rows in this batch (host-known)
+  int64_t units;
+};
+
+// Per-batch prepared (SELL-64, length-sorted) sparse features.
+struct DevPrepared {
+  // filter/sort
+  int64_t* kept;            // [R]   raw row id of kept row k
+  int32_t* nnz;             // [R]   entries of kept row k
+  int32_t* sorted;          // [R]   kept index at sorted position p
+  int64_t* blk;             // [R/256+2] scratch (block counts / offsets)
+  int64_t* hist;            // [kLenBuckets+1]
+  // chunk layout
+  int32_t* clen8;           // [C]   groups of 8 entries per lane in chunk c
+  int64_t* cbase;           // [C+1] first group of chunk c (entries = groups*512)
+  int32_t* idx;             // [E]   hashed feature index per entry (-1 = pad)
+  void* slot;               // [E]   compact slot per entry (u16 or u32)
+  float* y;                 // [C*64] label
+  float* num;               // [C*4*64] numeric features [c][k][lane]
+  int32_t* perm;            // [C*64] kept index of (c, lane), -1 if none
+  // active set
+  uint8_t* flags;           // [Fh]
+  int32_t* uniq;            // [Fh]  sorted touched feature ids
+  int32_t* slot_of;         // [Fh]  feature id -> slot (valid for touched ids)
+  int64_t* ublk;            // [Fh/4096+2]
+  // counters (device): [0]=n_kept [1]=n_unique [2]=groups [3]=error
+  int64_t* counters;
+  int64_t cap_rows, cap_entries, cap_chunks, flag_len;
+};
+
+struct FeaturizeParams {
+  int64_t num_text_features;  // F
+  int32_t hash_kind;          // 0 = Java String.hashCode, 1 = Spark-2 murmur3
+  int32_t require_retweet;    // filter: isRetweet
+  int32_t range_filter;       // filter: begin <= rtCount <= end
+  int64_t begin, end;
+  int64_t now_ms;
+};
+
+void upload_lower_tables(hipStream_t s, uint8_t** d_page, uint16_t** d_blocks);
+
+void launch_filter_sort(const DevRawBatch& b, const DevPrepared& p, const FeaturizeParams& fp,
+                        hipStream_t s);
+void launch_chunk_layout(const DevRawBatch& b, const DevPrepared& p, hipStream_t s);
+void launch_featurize(const DevRawBatch& b, const DevPrepared& p, const FeaturizeParams& fp,
+                      const uint8_t* lower_page, const uint16_t* lower_blocks, hipStream_t s);
+void launch_compact_active(const DevPrepared& p, hipStream_t s);
+void launch_remap(const DevPrepared& p, int64_t entries, int64_t n_unique, bool u16, hipStream_t s);
+
+// ---------------------------------------------------------------------------
+// SGD on the compact active set.
+struct DevSgd {
+  double* w64;          // [F+4] master weights (fp64)
+  double* wc64;         // [NS]  compact master weights
+  float* wc32;          // [NS]  compact fp32 copy read by the gradient kernel
+  float* g32;           // [NS+1] gradient accumulator (+ loss at [NS])
+  double* red64;        // [4] {loss, m, pad, pad} for sampled iterations
+  double* stats;        // [8] n, sum_y, sum_y2, sum_p, sum_p2, sum_e2, -, -
+  double* state;        // [8] 0 done 1 converged 2 n_updates 3 iters 4 wrest2 5 m_global 6 wnorm2_full
+  double* loss_hist;    // [max_iters+1]
+  float* pred_out;      // [R] rounded predictions in kept order (optional)
+  int64_t F;
+  int64_t ns;           // 4 + n_unique + pads (rounded)
+  int64_t n_unique;
+};
+
+struct SgdParams {
+  double step_size;
+  double fraction;
+  double tol;
+  int32_t iteration;    // 1-based
+  int32_t num_iterations;
+  int64_t row_offset;   // global row id of this rank's kept row 0 (sampling)
+  int32_t want_pred;
+  int32_t sample;       // fraction < 1
+};
+
+void launch_gather_w(const DevSgd& d, const DevPrepared& p, hipStream_t s);
+void launch_norm2(const double* v, int64_t n, double* out, hipStream_t s);
+void launch_sgd_iter(const DevSgd& d, const DevPrepared& p, const SgdParams& sp, int64_t groups,
+                     bool u16, int grid, hipStream_t s);
+void launch_sgd_update(const DevSgd& d, const SgdParams& sp, hipStream_t s);
+void launch_scatter_w(const DevSgd& d, const DevPrepared& p, hipStream_t s);
+int sgd_lds_limit_slots();
+
+// ---------------------------------------------------------------------------
+// K-means (kmeans.hip)
+struct DevKMeans {
+  const float* x;       // [n][d] points (row-major, fp32)
+  int64_t n;
+  int32_t d, k;
+  float* centers;       // [k][d] fp32 (copy of fp64 master for the distance GEMM)
+  float* cnorm;         // [k]
+  int32_t* labels;      // [n]
+  double* sums;         // [k][d] + counts [k]  (fp64 accumulators)
+  double* moments;      // [2*d+1] scaler moments
+};
+// (k-means launchers are declared by kmeans.hip)
+void launch_scaler_sum(const float* x, int64_t n, int d, double* out_sum, hipStream_t s);
+void launch_scaler_m2(const float* x, int64_t n, int d, const double* sum_n, double* out_m2,
+                      hipStream_t s);
+void launch_scale(float* x, int64_t n, int d, const double* factor, hipStream_t s);
+void launch_center_norms(const float* c, int k, int d, float* cnorm, hipStream_t s);
+void launch_assign(const DevKMeans& km, bool use_mfma, hipStream_t s);
+void launch_cluster_sums(const DevKMeans& km, hipStream_t s);
+
+}  // namespace twtml

@@ -1,0 +1,30 @@
+"""Shared pytest configuration.
+
+Markers: ``gpu`` -- needs a real MI355X (the driver runs ``-m gpu`` on a GPU
+box and ``-m "not gpu"`` here).  The test "classpath" for application.conf is
+tests/resources (like sbt's src/test/resources).
+"""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+os.environ.setdefault("TWTML_CONFIG_PATH", os.path.join(ROOT, "tests", "resources"))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: requires an AMD Instinct GPU (MI355X)")
+    config.addinivalue_line("markers", "slow: long-running test")
+
+
+@pytest.fixture(scope="session")
+def hip_module():
+    """The HIP engine extension; GPU tests fail loudly if it cannot load."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test selected but no GPU visible")
+    from twitter_stream_ml_amd.ops import _native
+    return _native.hip()

@@ -1,0 +1,129 @@
+"""GPU numerics of the streaming-LR engine against the fp64 oracle.
+
+K1-K3 (filter, lower-case, bigram hash, numeric features) are compared entry
+for entry with ``oracle.featurize_batch``; K4-K7 (prequential predictions and
+stats, GD iterations, convergence) against ``oracle.run_minibatch_sgd`` over
+several warm-started batches.
+"""
+import numpy as np
+import pytest
+
+from twitter_stream_ml_amd.oracle import (featurize_batch, round_half_up_array,
+                                          run_minibatch_sgd)
+from twitter_stream_ml_amd.sources.synthetic import SynthConfig, generate_batch
+
+pytestmark = pytest.mark.gpu
+
+NOW = 1_700_000_000_000
+
+
+def _engine(F, hash="java", **kw):
+    from twitter_stream_ml_amd.ops.lr_engine import DeviceLinearRegression, LRDeviceConfig
+    cfg = LRDeviceConfig(num_text_features=F, hash=hash, max_rows=8192, max_units=8192 * 300, **kw)
+    return DeviceLinearRegression(cfg, device=0)
+
+
+def _rows_from_debug(dbg):
+    """Per kept row (kept order) -> sorted multiset of hashed feature ids."""
+    nk = int(dbg["counters"][0])
+    idx, clen8, cbase, perm = dbg["idx"], dbg["clen8"], dbg["cbase"], dbg["perm"]
+    rows = [None] * nk
+    for c in range(clen8.shape[0]):
+        g0, L8 = int(cbase[c]), int(clen8[c])
+        block = idx[g0 * 512:(g0 + L8) * 512].reshape(L8, 64, 8)
+        for lane in range(64):
+            k = int(perm[c * 64 + lane])
+            if k < 0:
+                continue
+            v = block[:, lane, :].reshape(-1)
+            rows[k] = np.sort(v[v >= 0])
+    return rows
+
+
+@pytest.mark.parametrize("F,hash", [(1000, "java"), (1 << 20, "java"), (1 << 20, "murmur3")])
+def test_featurize_matches_oracle(hip_module, F, hash):
+    cfg = SynthConfig.profile("twitter", seed=11, special_fraction=0.05, unicode_fraction=0.3)
+    raw = generate_batch(cfg, 0, 3000, batch_time_ms=NOW)
+    eng = _engine(F, hash)
+    eng.train_batch(raw, want_pred=True)
+    dbg = eng._eng.debug_prepared()
+    fb = featurize_batch(raw, F, 100, 1000, now_ms=NOW, hash=hash)
+    assert int(dbg["counters"][0]) == fb.n
+    rows = _rows_from_debug(dbg)
+    Xt = fb.X[:, :F].tocsr()
+    for k in range(fb.n):
+        s, e = Xt.indptr[k], Xt.indptr[k + 1]
+        want = np.repeat(Xt.indices[s:e], Xt.data[s:e].astype(np.int64))
+        np.testing.assert_array_equal(rows[k], np.sort(want), err_msg=f"row {k}")
+    # active set = union of touched ids
+    touched = np.unique(Xt.indices)
+    np.testing.assert_array_equal(np.sort(dbg["uniq"]), touched)
+    # labels / numeric features (fp32 of the fp64 oracle values)
+    nk = fb.n
+    y = np.zeros(nk, np.float32)
+    num = np.zeros((nk, 4), np.float32)
+    perm, C = dbg["perm"], dbg["clen8"].shape[0]
+    for c in range(C):
+        for lane in range(64):
+            k = int(perm[c * 64 + lane])
+            if k >= 0:
+                y[k] = dbg["y"][c * 64 + lane]
+                num[k] = dbg["num"][(c * 4 + np.arange(4)) * 64 + lane]
+    np.testing.assert_array_equal(y, fb.y.astype(np.float32))
+    want_num = fb.X[:, F:F + 4].toarray()
+    np.testing.assert_allclose(num, want_num, rtol=2e-7, atol=0)
+
+
+@pytest.mark.parametrize("F", [1000, 1 << 20])
+def test_sgd_matches_oracle_over_batches(hip_module, F):
+    cfg = SynthConfig.profile("twitter", seed=5, unicode_fraction=0.1)
+    eng = _engine(F, step_size=0.005, num_iterations=50)
+    w = np.zeros(F + 4)
+    for t in range(4):
+        raw = generate_batch(cfg, t * 2500, 2500, batch_time_ms=NOW + t * 5000)
+        fb = featurize_batch(raw, F, 100, 1000)
+        pred_o = round_half_up_array(fb.X @ w)
+        res = eng.train_batch(raw, want_pred=True)
+        assert res["n_kept"] == fb.n
+        # prequential predictions (output op #1) with the pre-training weights
+        pred_g = np.asarray(res["pred"], np.float64)
+        mism = np.abs(pred_g - pred_o) > 0
+        assert mism.mean() < 0.01, mism.mean()
+        assert np.all(np.abs(pred_g - pred_o) <= 1.0 + 1e-3 * np.abs(pred_o))
+        n, sy, sy2, sp, sp2, se2 = res["stats"]
+        assert int(n) == fb.n
+        np.testing.assert_allclose(sy, fb.y.sum(), rtol=1e-12)
+        np.testing.assert_allclose(se2 / n, np.mean((fb.y - pred_o) ** 2), rtol=2e-3)
+        # training
+        r = run_minibatch_sgd(fb.X, fb.y, w, 0.005, 50)
+        w = r.weights
+        wg = eng.get_weights()
+        scale = max(np.abs(w).max(), 1e-12)
+        assert abs(res["iterations"] - r.iterations) <= 1, (res["iterations"], r.iterations)
+        if res["iterations"] == r.iterations:
+            np.testing.assert_allclose(wg, w, rtol=2e-3, atol=2e-4 * scale)
+        # continue the oracle from the engine's weights so batches stay comparable
+        w = wg.copy()
+
+
+def test_fraction_sampling_matches_oracle(hip_module):
+    F = 1000
+    cfg = SynthConfig.profile("twitter", seed=9)
+    eng = _engine(F, fraction=0.5, num_iterations=10)
+    raw = generate_batch(cfg, 0, 3000, batch_time_ms=NOW)
+    fb = featurize_batch(raw, F, 100, 1000)
+    res = eng.train_batch(raw)
+    r = run_minibatch_sgd(fb.X, fb.y, np.zeros(F + 4), 0.005, 10, mini_batch_fraction=0.5)
+    assert res["iterations"] == r.iterations
+    wg = eng.get_weights()
+    np.testing.assert_allclose(wg, r.weights, rtol=2e-3, atol=2e-4 * np.abs(r.weights).max())
+
+
+def test_empty_and_filtered_out_batch(hip_module):
+    F = 1000
+    eng = _engine(F)
+    cfg = SynthConfig.profile("twitter", seed=1, retweet_fraction=0.0)
+    raw = generate_batch(cfg, 0, 500, batch_time_ms=NOW)
+    res = eng.train_batch(raw)
+    assert res["n_kept"] == 0 and res["iterations"] == 0
+    assert np.all(eng.get_weights() == 0)

@@ -109,7 +109,7 @@ def hipcc() -> str:
 
 
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
-             "-ffp-contract=fast", "-Wno-unused-result", "-fgpu-flush-denormals-to-zero=false"]
+             "-ffp-contract=fast", "-Wno-unused-result"]
 
 
 def build_hip(force: bool = False, verbose: bool = False) -> str:
@@ -130,7 +130,7 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
     def compile_one(src: str) -> str:
         obj = os.path.join(BUILD_DIR, "hip_" + os.path.basename(src) + ".o")
         if force or _newer(obj, [src] + hdrs):
-            extra = ["-x", "hip"] if src.endswith(".hip") else ["-D__HIP_PLATFORM_AMD__"]
+            extra = ["-x", "hip"] if src.endswith(".hip") else ["-x", "c++", "-D__HIP_PLATFORM_AMD__"]
             if src.endswith(".cpp"):
                 cmd = [cc, "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", *inc, *extra,
                        "-c", src, "-o", obj]
@@ -142,7 +142,7 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
     with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:
         objs = list(ex.map(compile_one, kern + host))
     tl = _torch_lib_dir()
-    link = [cc, "-shared", f"--offload-arch={ARCH}", "-fgpu-rdc=false", "-o", HIP_SO + ".tmp", *objs]
+    link = [cc, "-shared", f"--offload-arch={ARCH}", "-o", HIP_SO + ".tmp", *objs]
     if tl and os.path.exists(os.path.join(tl, "libamdhip64.so")):
         # bind to torch's runtime + RCCL so one process never holds two copies
         link += [os.path.join(tl, "libamdhip64.so"), os.path.join(tl, "librccl.so"),

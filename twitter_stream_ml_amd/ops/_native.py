@@ -33,7 +33,9 @@ def host() -> ModuleType:
     with _lock:
         if _host is None:
             from .. import _build
-            if os.environ.get("TWTML_NO_AUTOBUILD") != "1":
+            # build only when missing (or forced): snapshots copied to another
+            # machine may not preserve mtimes, so staleness is not trusted
+            if os.environ.get("TWTML_REBUILD") == "1" or not os.path.exists(_build.HOST_SO):
                 _build.build_host()
             try:
                 _host = importlib.import_module("twitter_stream_ml_amd._twtml_host")
@@ -50,8 +52,7 @@ def hip() -> ModuleType:
         if _hip is None:
             import torch  # noqa: F401  (binds the HIP runtime/RCCL SONAMEs first)
             from .. import _build
-            if os.environ.get("TWTML_NO_AUTOBUILD") != "1" and _build._newer(
-                    _build.HIP_SO, [os.path.join(_build.CSRC, "hip")]):
+            if os.environ.get("TWTML_REBUILD") == "1" or not os.path.exists(_build.HIP_SO):
                 try:
                     _build.build_hip()
                 except Exception as e:

@@ -1,0 +1,170 @@
+"""Python face of the MI355X streaming-LR engine (``csrc/hip/engine.cpp``).
+
+The engine executes, per micro-batch and entirely on the GPU, what the
+reference runs as ~60 Spark jobs: filter (K3), featurize
+(K1+K2), prequential predict + stats (K4+K7, output op #1 of
+``LinearRegression.scala:53-81``) and ``numIterations`` steps of
+``GradientDescent`` (K5+K6, output op #2 ``model.trainOn`` at ``:86``).
+
+Host-side contract: raw batches live in pinned :class:`HostBatch` buffers
+(``text``/``offsets``/``is_rt``/packed ``[5][n]`` scalars).  Rows whose
+lower-casing is not per-UTF-16-unit (U+0130, U+03A3, astral cased letters)
+are rewritten on the host first (:func:`prelower`); everything else is
+lowered on the device.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from ..records.batch import RETWEET_COUNT, RawBatch
+from ._native import hip, host
+
+__all__ = ["LRDeviceConfig", "DeviceLinearRegression", "prelower", "HostBatchView"]
+
+
+def prelower(raw: RawBatch) -> RawBatch:
+    """Host pre-pass: full-case-map the rare rows the GPU cannot lower per unit."""
+    h = host()
+    if h.count_special_rows(raw.text, raw.offsets) == 0:
+        return raw
+    text, offsets, _ = h.prelower_special_rows(raw.text, raw.offsets)
+    return RawBatch(text, offsets, raw.is_retweet, raw.scalars, raw.batch_time_ms)
+
+
+@dataclass
+class LRDeviceConfig:
+    num_text_features: int = 1000
+    hash: str = "java"
+    step_size: float = 0.005
+    num_iterations: int = 50
+    fraction: float = 1.0
+    tol: float = 1e-3
+    begin: int = 100
+    end: int = 1000
+    require_retweet: bool = True
+    range_filter: bool = True
+    max_rows: int = 1 << 16
+    max_units: int = (1 << 16) * 281
+    sgd_grid: int = 0
+
+    def as_dict(self) -> Dict[str, object]:
+        return {
+            "num_text_features": int(self.num_text_features),
+            "hash_kind": 0 if self.hash == "java" else 1,
+            "step_size": float(self.step_size),
+            "num_iterations": int(self.num_iterations),
+            "fraction": float(self.fraction),
+            "tol": float(self.tol),
+            "begin": int(self.begin),
+            "end": int(self.end),
+            "require_retweet": int(bool(self.require_retweet)),
+            "range_filter": int(bool(self.range_filter)),
+            "max_rows": int(self.max_rows),
+            "max_units": int(self.max_units),
+            "sgd_grid": int(self.sgd_grid),
+        }
+
+
+class HostBatchView:
+    """Pinned host staging buffer with numpy views (zero-copy for H2D)."""
+
+    def __init__(self, max_rows: int, max_units: int):
+        self._hb = hip().HostBatch(int(max_rows), int(max_units))
+        self.text = self._hb.text
+        self.offsets = self._hb.offsets
+        self.is_rt = self._hb.is_rt
+        self.scalars_flat = self._hb.scalars_flat
+        self.n = 0
+        self.units = 0
+        self.batch_time_ms = 0
+
+    @property
+    def max_rows(self) -> int:
+        return self._hb.max_rows
+
+    @property
+    def max_units(self) -> int:
+        return self._hb.max_units
+
+    def scalars(self) -> np.ndarray:
+        return self.scalars_flat[:5 * self.n].reshape(5, self.n)
+
+    def load(self, raw: RawBatch) -> "HostBatchView":
+        raw = prelower(raw)
+        n, u = raw.n, raw.total_units
+        if n > self.max_rows or u > self.max_units:
+            raise ValueError(f"batch ({n} rows, {u} units) exceeds staging capacity "
+                             f"({self.max_rows}, {self.max_units})")
+        self.text[:u] = raw.text
+        self.offsets[:n + 1] = raw.offsets
+        self.is_rt[:n] = raw.is_retweet
+        self.scalars_flat[:5 * n] = raw.scalars.reshape(-1)
+        self.n, self.units, self.batch_time_ms = n, u, raw.batch_time_ms
+        return self
+
+    def as_raw(self) -> RawBatch:
+        return RawBatch(self.text[:self.units].copy(), self.offsets[:self.n + 1].copy(),
+                        self.is_rt[:self.n].copy(), self.scalars().copy(), self.batch_time_ms)
+
+
+class DeviceLinearRegression:
+    """StreamingLinearRegressionWithSGD state + pipeline on one GPU."""
+
+    def __init__(self, cfg: LRDeviceConfig, device: int = 0, comm=None):
+        self.cfg = cfg
+        self.device = int(device)
+        self._eng = hip().LREngine(self.device, cfg.as_dict(), comm)
+        self._staging: List[HostBatchView] = []
+
+    # ---- weights (MLlib setInitialWeights / latestModel.weights) ---------
+    @property
+    def num_weights(self) -> int:
+        return int(self._eng.num_weights)
+
+    def get_weights(self) -> np.ndarray:
+        return np.asarray(self._eng.get_weights())
+
+    def set_weights(self, w: np.ndarray) -> None:
+        w = np.ascontiguousarray(w, dtype=np.float64)
+        if w.shape != (self.num_weights,):
+            raise ValueError(f"expected {self.num_weights} weights, got {w.shape}")
+        self._eng.set_weights(w)
+
+    # ---- staging / pipeline ----------------------------------------------
+    def staging(self, i: int = 0) -> HostBatchView:
+        while len(self._staging) <= i:
+            self._staging.append(HostBatchView(self.cfg.max_rows, self.cfg.max_units))
+        return self._staging[i]
+
+    def submit(self, hb: HostBatchView, slot: int) -> None:
+        self._eng.submit(hb._hb, int(hb.n), int(hb.units), int(slot))
+
+    def process(self, slot: int, now_ms: int, want_pred: bool = False) -> Dict[str, object]:
+        return self._eng.process(int(slot), int(now_ms), bool(want_pred))
+
+    def train_batch(self, raw: RawBatch, want_pred: bool = True, slot: int = 0) -> Dict[str, object]:
+        """Synchronous convenience path: stage, H2D, process."""
+        hb = self.staging(slot).load(raw)
+        self.submit(hb, slot)
+        return self.process(slot, raw.batch_time_ms, want_pred)
+
+    def synchronize(self) -> None:
+        self._eng.synchronize()
+
+
+def batch_report(res: Dict[str, object]) -> Dict[str, float]:
+    """Population stdevs / MSE from the fused stats (``LinearRegression.scala:59-65``)."""
+    n, sy, sy2, sp, sp2, se2 = res["stats"]
+    if n <= 0:
+        return {"count": 0, "mse": float("nan"), "realStdev": float("nan"),
+                "predStdev": float("nan")}
+    my, mp = sy / n, sp / n
+    return {
+        "count": int(round(n)),
+        "mse": se2 / n,
+        "realStdev": float(np.sqrt(max(sy2 / n - my * my, 0.0))),
+        "predStdev": float(np.sqrt(max(sp2 / n - mp * mp, 0.0))),
+    }

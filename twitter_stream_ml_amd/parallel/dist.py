@@ -1,0 +1,140 @@
+"""Process-group bootstrap and collectives (one process per GPU).
+
+Control plane: ``torch.distributed`` (``nccl`` = RCCL on ROCm for GPU jobs,
+``gloo`` for the CPU engine), initialised from the usual ``RANK`` /
+``WORLD_SIZE`` / ``LOCAL_RANK`` / ``MASTER_ADDR`` / ``MASTER_PORT`` variables
+that ``torch.distributed.run`` sets.
+
+Data plane on GPUs: the engine's own RCCL communicator (``csrc/hip/comm.cpp``)
+issues the per-iteration gradient all-reduce on the engine's compute stream
+with no Python in the loop.  Its ``ncclUniqueId`` is created on rank 0 and
+broadcast here.  This replaces Spark's broadcast + treeAggregate per GD
+iteration.
+
+The CPU engine gets :func:`allreduce_fn`, a numpy float64 sum over gloo —
+the same call sites, so DP on CPU and on GPUs run identical algorithms.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Callable, Optional
+
+import numpy as np
+
+__all__ = ["DistInfo", "init_distributed", "dist_info", "make_rccl_comm", "allreduce_fn",
+           "barrier", "allreduce_max_scalar", "allreduce_sum_scalar", "shutdown"]
+
+
+@dataclass(frozen=True)
+class DistInfo:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    backend: str = "none"
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+
+_INFO = DistInfo()
+
+
+def dist_info() -> DistInfo:
+    return _INFO
+
+
+def init_distributed(backend: Optional[str] = None, device: Optional[int] = None,
+                     timeout_s: float = 600.0) -> DistInfo:
+    """Initialise the default process group if ``WORLD_SIZE > 1``."""
+    global _INFO
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if world <= 1:
+        _INFO = DistInfo(0, 1, local, "none")
+        return _INFO
+    import torch
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    kwargs = {}
+    if backend == "nccl":
+        dev = local if device is None else device
+        torch.cuda.set_device(dev)
+        kwargs["device_id"] = torch.device("cuda", dev)
+    if not dist.is_initialized():
+        dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s), **kwargs)
+    _INFO = DistInfo(rank, world, local, backend)
+    return _INFO
+
+
+def make_rccl_comm(device: int):
+    """Engine-owned RCCL communicator for this process (None when world == 1)."""
+    info = dist_info()
+    if info.world <= 1:
+        return None
+    import torch.distributed as dist
+    from ..ops._native import hip
+    h = hip()
+    obj = [h.rccl_unique_id() if info.rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    return h.Comm(obj[0], info.rank, info.world, int(device))
+
+
+def allreduce_fn() -> Optional[Callable[[np.ndarray], np.ndarray]]:
+    """float64 sum across ranks (gloo/nccl via torch), or None for 1 rank."""
+    info = dist_info()
+    if info.world <= 1:
+        return None
+    import torch
+    import torch.distributed as dist
+
+    def _allreduce(v: np.ndarray) -> np.ndarray:
+        t = torch.from_numpy(np.ascontiguousarray(v, dtype=np.float64).copy())
+        if info.backend == "nccl":
+            t = t.cuda()
+        dist.all_reduce(t)
+        return t.cpu().numpy()
+
+    return _allreduce
+
+
+def barrier() -> None:
+    info = dist_info()
+    if info.world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def _reduce_scalar(x: float, op: str) -> float:
+    info = dist_info()
+    if info.world <= 1:
+        return float(x)
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([float(x)], dtype=torch.float64)
+    if info.backend == "nccl":
+        t = t.cuda()
+    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def allreduce_max_scalar(x: float) -> float:
+    return _reduce_scalar(x, "max")
+
+
+def allreduce_sum_scalar(x: float) -> float:
+    return _reduce_scalar(x, "sum")
+
+
+def shutdown() -> None:
+    info = dist_info()
+    if info.world > 1:
+        import torch.distributed as dist
+        if dist.is_initialized():
+            dist.destroy_process_group()
