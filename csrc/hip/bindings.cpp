@@ -32,7 +32,7 @@ static LRConfig lr_config(const py::dict& d) {
   GET(num_iterations, int32_t) GET(fraction, double) GET(tol, double) GET(begin, int64_t)
   GET(end, int64_t) GET(require_retweet, int32_t) GET(range_filter, int32_t)
   GET(max_rows, int64_t) GET(max_units, int64_t) GET(sgd_grid, int32_t)
-  GET(early_exit_depth, int32_t)
+  GET(early_exit_depth, int32_t) GET(ablate, int32_t)
 #undef GET
   return c;
 }
@@ -46,6 +46,7 @@ static py::dict result_dict(BatchResult& r) {
   d["entries"] = r.entries;
   d["iterations"] = r.iterations;
   d["converged"] = r.converged;
+  d["overflow"] = r.overflow;
   d["stats"] = std::vector<double>(r.stats, r.stats + 6);
   d["loss_history"] = r.loss_history;
   d["prep_ms"] = r.prep_ms;

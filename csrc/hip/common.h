@@ -21,9 +21,11 @@ namespace twtml {
 
 constexpr int kWave = 64;
 constexpr int kBlock = 256;          // 4 waves per workgroup
-constexpr int kChunk = 64;           // rows per SELL chunk (one row per lane)
+constexpr int kLanesPerRow = 4;      // a row's entries are dealt round-robin to 4 lanes
+constexpr int kRowsPerChunk = kWave / kLanesPerRow;  // 16 rows per chunk (one wave)
 constexpr int kGroup = 8;            // entries per lane per 16-byte slot load (u16 slots)
-constexpr int kChunkStride = kChunk * kGroup;  // entries per (chunk, group) = 512
+constexpr int kChunkStride = kWave * kGroup;  // entries per (chunk, group) = 512
+constexpr int kMaxRegGroups = 10;    // groups a lane keeps in VGPRs (row nnz <= 320)
 constexpr int kNumNumeric = 4;       // numeric features (MllibHelper.scala:13)
 constexpr int kPadSlots = 64;        // one zero-weight pad slot per lane
 constexpr int kLenBuckets = 4096;    // counting-sort buckets for row length

@@ -84,10 +84,12 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
 
 void LREngine::alloc_prepared() {
   const int64_t R = cfg_.max_rows;
-  const int64_t C = (R + kChunk - 1) / kChunk;
-  int64_t E = 2 * cfg_.max_units + C * kChunkStride + 65536;
+  const int64_t C = (R + kRowsPerChunk - 1) / kRowsPerChunk;
+  const int64_t R16 = C * kRowsPerChunk;
+  int64_t E = 2 * cfg_.max_units + 2 * C * kChunkStride + 65536;
   E = (E + kChunkStride - 1) / kChunkStride * kChunkStride;
   prep_.cap_rows = R;
+  prep_.cap_rows16 = R16;
   prep_.cap_chunks = C;
   prep_.cap_entries = E;
   prep_.kept = dmalloc<int64_t>(size_t(R));
@@ -99,9 +101,9 @@ void LREngine::alloc_prepared() {
   prep_.cbase = dmalloc<int64_t>(size_t(C) + 1);
   prep_.idx = dmalloc<int32_t>(size_t(E));
   prep_.slot = dmalloc<uint32_t>(size_t(E));
-  prep_.y = dmalloc<float>(size_t(C) * kChunk);
-  prep_.num = dmalloc<float>(size_t(C) * 4 * kChunk);
-  prep_.perm = dmalloc<int32_t>(size_t(C) * kChunk);
+  prep_.y = dmalloc<float>(size_t(R16));
+  prep_.num = dmalloc<float>(4 * size_t(R16));
+  prep_.perm = dmalloc<int32_t>(size_t(R16));
   // active-feature flags: Java-hash bigrams are < 2^21 whatever F is
   const int64_t F = cfg_.num_text_features;
   int64_t fl = cfg_.hash_kind == 0 ? std::min<int64_t>(F, int64_t(1) << 21) : F;
@@ -122,12 +124,12 @@ void LREngine::ensure_compact(int64_t ns) {
     TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
     (void)hipFree(sgd_.wc64);
     (void)hipFree(sgd_.wc32);
-    (void)hipFree(sgd_.g32);
+    (void)hipFree(sgd_.g64);
   }
   sgd_.wc64 = dmalloc<double>(size_t(cap));
   sgd_.wc32 = dmalloc<float>(size_t(cap));
-  sgd_.g32 = dmalloc<float>(size_t(cap) + 1);
-  TWTML_HIP_CHECK(hipMemset(sgd_.g32, 0, sizeof(float) * (size_t(cap) + 1)));
+  sgd_.g64 = dmalloc<double>(size_t(cap) + 1);
+  TWTML_HIP_CHECK(hipMemset(sgd_.g64, 0, sizeof(double) * (size_t(cap) + 1)));
   ns_cap_ = cap;
 }
 
@@ -142,7 +144,7 @@ LREngine::~LREngine() {
   void* bufs[] = {prep_.kept, prep_.nnz, prep_.sorted, prep_.blk, prep_.hist, prep_.clen8,
                   prep_.cbase, prep_.idx, prep_.slot, prep_.y, prep_.num, prep_.perm,
                   prep_.flags, prep_.uniq, prep_.slot_of, prep_.ublk, prep_.counters,
-                  sgd_.w64, sgd_.wc64, sgd_.wc32, sgd_.g32, sgd_.red64, sgd_.stats, sgd_.state,
+                  sgd_.w64, sgd_.wc64, sgd_.wc32, sgd_.g64, sgd_.red64, sgd_.stats, sgd_.state,
                   sgd_.loss_hist, sgd_.pred_out, lower_page_, lower_blocks_, n_global_};
   for (void* b : bufs) if (b) (void)hipFree(b);
   if (host_counters_) (void)hipHostFree(host_counters_);
@@ -240,24 +242,14 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   TWTML_HIP_CHECK(hipMemsetAsync(sgd_.state, 0, 8 * sizeof(double), s));
   TWTML_HIP_CHECK(hipMemsetAsync(sgd_.stats, 0, 8 * sizeof(double), s));
   TWTML_HIP_CHECK(hipMemsetAsync(sgd_.red64, 0, 4 * sizeof(double), s));
-  TWTML_HIP_CHECK(hipMemsetAsync(sgd_.g32 + ns, 0, sizeof(float), s));
+  TWTML_HIP_CHECK(hipMemsetAsync(sgd_.g64 + ns, 0, sizeof(double), s));
   TWTML_HIP_CHECK(hipMemsetAsync(sgd_.loss_hist, 0, sizeof(double) * size_t(cfg_.num_iterations + 2), s));
   launch_batch_init(sgd_.state, double(n_glob), s);  // state[5] = m (global kept rows)
   launch_norm2(sgd_.w64, num_weights(), &sgd_.state[4], s);
   launch_gather_w(sgd_, prep_, s);
   TWTML_HIP_CHECK(hipEventRecord(ev_[1], s));
 
-  const int64_t nch = (res.n_kept + kChunk - 1) / kChunk;
-  int grid = cfg_.sgd_grid;
-  if (grid <= 0) {
-    const int64_t lds = 2 * ns * int64_t(sizeof(float));
-    int per_cu = lds > 0 ? int(std::min<int64_t>(4, (160 * 1024) / std::max<int64_t>(lds, 1))) : 4;
-    if (per_cu < 1) per_cu = 1;
-    if (per_cu > 2) per_cu = 2;
-    grid = num_cu_ * per_cu;
-  }
-  grid = int(std::max<int64_t>(1, std::min<int64_t>(grid, (nch + 3) / 4)));
-
+  int grid = cfg_.sgd_grid > 0 ? cfg_.sgd_grid : sgd_iter_grid(ns, res.n_kept, num_cu_);
   SgdParams sp{};
   sp.step_size = cfg_.step_size;
   sp.fraction = cfg_.fraction;
@@ -266,6 +258,7 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   sp.row_offset = row_offset;
   sp.want_pred = want_pred ? 1 : 0;
   sp.sample = cfg_.fraction < 1.0 ? 1 : 0;
+  sp.ablate = cfg_.ablate;
   if (n_glob > 0) {
     for (int i = 1; i <= cfg_.num_iterations; ++i) {
       sp.iteration = i;
@@ -274,7 +267,7 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
         // nothing local to add; still participate in the collectives below
       }
       if (world > 1) {
-        comm_->allreduce(sgd_.g32, size_t(ns + 1), ncclFloat32, ncclSum, s);
+        comm_->allreduce(sgd_.g64, size_t(ns + 1), ncclFloat64, ncclSum, s);
         if (sp.sample) comm_->allreduce(sgd_.red64, 2, ncclFloat64, ncclSum, s);
       }
       launch_sgd_update(sgd_, sp, s);
@@ -297,6 +290,7 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   for (int k = 0; k < 6; ++k) res.stats[k] = host_out_[k];
   const double* st = host_out_ + 8;
   res.converged = st[1] != 0.0;
+  res.overflow = st[7] != 0.0;
   res.iterations = int32_t(st[3]);
   for (int i = 1; i <= res.iterations; ++i) res.loss_history.push_back(host_out_[16 + i]);
   TWTML_HIP_CHECK(hipEventElapsedTime(&res.prep_ms, ev_[0], ev_[1]));
@@ -340,20 +334,23 @@ void LREngine::debug_prepared(std::vector<int64_t>& counters, std::vector<int32_
   counters.resize(4);
   TWTML_HIP_CHECK(hipMemcpy(counters.data(), prep_.counters, 4 * sizeof(int64_t), hipMemcpyDeviceToHost));
   const int64_t nk = counters[0], nu = counters[1], groups = counters[2];
-  const int64_t C = (nk + kChunk - 1) / kChunk;
+  const int64_t C = (nk + kRowsPerChunk - 1) / kRowsPerChunk;
+  const int64_t R = C * kRowsPerChunk;
   clen8.resize(size_t(C));
   cbase.resize(size_t(C));
   idx.resize(size_t(groups * kChunkStride));
-  perm.resize(size_t(C * kChunk));
-  y.resize(size_t(C * kChunk));
-  num.resize(size_t(C * 4 * kChunk));
+  perm.resize(size_t(R));
+  y.resize(size_t(R));
+  num.resize(size_t(4 * R));
   uniq.resize(size_t(nu));
   if (C) {
     TWTML_HIP_CHECK(hipMemcpy(clen8.data(), prep_.clen8, sizeof(int32_t) * size_t(C), hipMemcpyDeviceToHost));
     TWTML_HIP_CHECK(hipMemcpy(cbase.data(), prep_.cbase, sizeof(int64_t) * size_t(C), hipMemcpyDeviceToHost));
-    TWTML_HIP_CHECK(hipMemcpy(perm.data(), prep_.perm, sizeof(int32_t) * size_t(C * kChunk), hipMemcpyDeviceToHost));
-    TWTML_HIP_CHECK(hipMemcpy(y.data(), prep_.y, sizeof(float) * size_t(C * kChunk), hipMemcpyDeviceToHost));
-    TWTML_HIP_CHECK(hipMemcpy(num.data(), prep_.num, sizeof(float) * size_t(C * 4 * kChunk), hipMemcpyDeviceToHost));
+    TWTML_HIP_CHECK(hipMemcpy(perm.data(), prep_.perm, sizeof(int32_t) * size_t(R), hipMemcpyDeviceToHost));
+    TWTML_HIP_CHECK(hipMemcpy(y.data(), prep_.y, sizeof(float) * size_t(R), hipMemcpyDeviceToHost));
+    for (int k = 0; k < 4; ++k)
+      TWTML_HIP_CHECK(hipMemcpy(num.data() + k * R, prep_.num + k * prep_.cap_rows16,
+                                sizeof(float) * size_t(R), hipMemcpyDeviceToHost));
   }
   if (groups)
     TWTML_HIP_CHECK(hipMemcpy(idx.data(), prep_.idx, sizeof(int32_t) * idx.size(), hipMemcpyDeviceToHost));

@@ -36,6 +36,7 @@ struct LRConfig {
   int64_t max_units = (1 << 16) * 281;
   int32_t sgd_grid = 0;       // 0 = auto
   int32_t early_exit_depth = 3;  // host run-ahead (iterations) for early stop
+  int32_t ablate = 0;            // perf diagnostics only (see SgdParams)
 };
 
 struct HostBatch {
@@ -54,6 +55,7 @@ struct BatchResult {
   int64_t n_raw = 0, n_kept = 0, n_kept_global = 0, n_unique = 0, entries = 0;
   int32_t iterations = 0;
   bool converged = false;
+  bool overflow = false;  // a residual hit the fixed-point clamp (diverging model)
   double stats[6] = {0, 0, 0, 0, 0, 0};  // n, sum y, sum y^2, sum p, sum p^2, sum (y-p)^2
   std::vector<double> loss_history;
   std::vector<float> pred;

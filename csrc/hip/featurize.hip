@@ -1,17 +1,20 @@
-// Ingest-side kernels: filter (K3), length sort, SELL-64 layout, bigram
+// Ingest-side kernels: filter (K3), length sort, SELL layout, bigram
 // hashing + numeric features (K1+K2), active-set compaction and remap.
 //
 // Reference semantics: MllibHelper.filtrate / featurize
 // (spark/src/main/scala/com/giorgioinf/twtml/spark/MllibHelper.scala:42-95).
 //
-// Layout produced for the SGD kernels ("SELL-64", length-sorted):
-//   kept rows are sorted by descending bigram count, cut into chunks of 64
-//   rows (one row per lane); chunk c owns clen8[c] groups of 8 entries per
-//   lane; entry j of the row in lane l lives at
-//       (cbase[c] + j/8) * 512 + l * 8 + j % 8
-//   so one 16-byte load gives a lane 8 consecutive u16 slots and a wave
-//   reads 1 KiB contiguous per instruction.  Padding entries point at a
-//   per-lane zero-weight pad slot.
+// Layout produced for the SGD kernels ("SELL-16x4", length-sorted):
+//   kept rows are sorted by descending bigram count and cut into chunks of
+//   16 rows; a chunk is one wave, each row owns 4 consecutive lanes and its
+//   entries are dealt round-robin to them (entry j -> lane 4r + j%4, local
+//   position jj = j/4).  A chunk owns clen8[c] groups; local entry jj of
+//   lane l lives at
+//       (cbase[c] + jj/8) * 512 + l * 8 + jj % 8
+//   so one 16-byte load gives a lane 8 u16 slots and a wave reads 1 KiB
+//   contiguous per instruction.  Padding entries point at a per-lane
+//   zero-weight pad slot.  Row-level arrays (y, num, perm) are indexed by the
+//   sorted position p = 16c + r.
 #include <hip/hip_runtime.h>
 
 #include "../common/unicode_tables.h"
@@ -55,8 +58,14 @@ static void scan_excl(const int64_t* in, int64_t* out, int64_t n, int64_t* total
   hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, s, in, out, n, total);
 }
 
+__device__ __forceinline__ int len_key(int32_t n32) {
+  return kLenBuckets - 1 - (n32 < kLenBuckets - 1 ? n32 : kLenBuckets - 1);
+}
+
 // ---------------------------------------------------------------------------
 // K3 filter: isRetweet && begin <= retweetCount <= end, order-preserving.
+// The per-row bigram count is bucketed into an LDS histogram (descending key)
+// so the global histogram sees one atomic per (block, bucket).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ bool keep_row(const DevRawBatch& b, int64_t r, const FeaturizeParams& fp) {
   if (r >= b.n) return false;
@@ -79,6 +88,8 @@ __global__ __launch_bounds__(kBlock) void k_filter_write(DevRawBatch b, Featuriz
                                                          const int64_t* blk_off, int64_t* kept,
                                                          int32_t* nnz, int64_t* hist) {
   __shared__ int wtot[kBlock / kWave];
+  __shared__ int lhist[kLenBuckets];
+  for (int i = threadIdx.x; i < kLenBuckets; i += kBlock) lhist[i] = 0;
   const int64_t r = int64_t(blockIdx.x) * kBlock + threadIdx.x;
   const bool pred = keep_row(b, r, fp);
   const uint64_t mask = __ballot(pred);
@@ -95,21 +106,37 @@ __global__ __launch_bounds__(kBlock) void k_filter_write(DevRawBatch b, Featuriz
     const int64_t nz = len >= 2 ? len - 1 : len;
     const int32_t n32 = int32_t(nz > 0x7fffffff ? 0x7fffffff : nz);
     nnz[k] = n32;
-    const int key = kLenBuckets - 1 - (n32 < kLenBuckets - 1 ? n32 : kLenBuckets - 1);
-    atomicAdd(reinterpret_cast<unsigned long long*>(&hist[key]), 1ull);
+    atomicAdd(&lhist[len_key(n32)], 1);
   }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kLenBuckets; i += kBlock)
+    if (lhist[i]) atomicAdd(reinterpret_cast<unsigned long long*>(&hist[i]), (unsigned long long)lhist[i]);
 }
 
+// Counting-sort scatter: one global atomic per (block, bucket) reserves a
+// range; rows take positions inside it through LDS counters.
 __global__ __launch_bounds__(kBlock) void k_sort_scatter(const int32_t* nnz, const int64_t* counters,
                                                          int64_t* cursor, int32_t* sorted,
                                                          int64_t cap) {
-  const int64_t n_kept = counters[0];
-  for (int64_t k = int64_t(blockIdx.x) * kBlock + threadIdx.x; k < n_kept && k < cap;
-       k += int64_t(gridDim.x) * kBlock) {
-    const int32_t n32 = nnz[k];
-    const int key = kLenBuckets - 1 - (n32 < kLenBuckets - 1 ? n32 : kLenBuckets - 1);
-    const int64_t pos = int64_t(atomicAdd(reinterpret_cast<unsigned long long*>(&cursor[key]), 1ull));
-    sorted[pos] = int32_t(k);
+  __shared__ int lcnt[kLenBuckets];
+  __shared__ long long lbase[kLenBuckets];
+  const int64_t n_kept = counters[0] < cap ? counters[0] : cap;
+  for (int64_t base = int64_t(blockIdx.x) * kBlock; base < n_kept; base += int64_t(gridDim.x) * kBlock) {
+    for (int i = threadIdx.x; i < kLenBuckets; i += kBlock) lcnt[i] = 0;
+    __syncthreads();
+    const int64_t k = base + threadIdx.x;
+    const bool ok = k < n_kept;
+    const int key = ok ? len_key(nnz[k]) : 0;
+    int rank = 0;
+    if (ok) rank = atomicAdd(&lcnt[key], 1);
+    __syncthreads();
+    for (int i = threadIdx.x; i < kLenBuckets; i += kBlock)
+      if (lcnt[i])
+        lbase[i] = (long long)atomicAdd(reinterpret_cast<unsigned long long*>(&cursor[i]),
+                                        (unsigned long long)lcnt[i]);
+    __syncthreads();
+    if (ok) sorted[lbase[key] + rank] = int32_t(k);
+    __syncthreads();
   }
 }
 
@@ -122,13 +149,13 @@ void launch_filter_sort(const DevRawBatch& b, const DevPrepared& p, const Featur
   hipLaunchKernelGGL(k_filter_write, dim3(nb), dim3(kBlock), 0, s, b, fp, p.blk, p.kept, p.nnz,
                      p.hist);
   scan_excl(p.hist, p.hist, kLenBuckets, nullptr, s);
-  const int g = nb < 2048 ? nb : 2048;
+  const int g = nb < 4096 ? nb : 4096;
   hipLaunchKernelGGL(k_sort_scatter, dim3(g), dim3(kBlock), 0, s, p.nnz, p.counters, p.hist,
                      p.sorted, p.cap_rows);
 }
 
 // ---------------------------------------------------------------------------
-// Chunk layout: groups of 8 entries per lane for every 64-row chunk.
+// Chunk layout: groups of 8 local entries per lane for every 16-row chunk.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_chunk_len(const int32_t* sorted, const int32_t* nnz,
                                                       const int64_t* counters, int64_t cmax,
@@ -137,12 +164,19 @@ __global__ __launch_bounds__(kBlock) void k_chunk_len(const int32_t* sorted, con
   const int lane = lane_id();
   const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = int64_t(gridDim.x) * kBlock / kWave;
-  for (int64_t c = wave; c < cmax; c += nwaves) {
-    const int64_t p = c * kChunk + lane;
-    const int32_t v = p < n_kept ? nnz[sorted[p]] : 0;
-    const int32_t mx = wave_max(v);
-    const int32_t g = (mx + kGroup - 1) / kGroup;
-    if (lane == 0) {
+  // one wave = 4 chunks of 16 rows (lane -> row 16*(4*wave + lane/16) + lane%16)
+  for (int64_t c4 = wave; c4 * 4 < cmax; c4 += nwaves) {
+    const int64_t c = c4 * 4 + lane / kRowsPerChunk;
+    const int64_t p = c * kRowsPerChunk + (lane % kRowsPerChunk);
+    int32_t v = (c < cmax && p < n_kept) ? nnz[sorted[p]] : 0;
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) {  // max within each 16-lane segment
+      const int32_t o = __shfl_xor(v, off, kWave);
+      v = o > v ? o : v;
+    }
+    if ((lane % kRowsPerChunk) == 0 && c < cmax) {
+      const int32_t per_lane = (v + kLanesPerRow - 1) / kLanesPerRow;
+      const int32_t g = (per_lane + kGroup - 1) / kGroup;
       clen8[c] = g;
       clen_scratch[c] = g;
     }
@@ -150,13 +184,14 @@ __global__ __launch_bounds__(kBlock) void k_chunk_len(const int32_t* sorted, con
 }
 
 void launch_chunk_layout(const DevRawBatch& b, const DevPrepared& p, hipStream_t s) {
-  const int64_t cmax = (b.n + kChunk - 1) / kChunk;
+  const int64_t cmax = (b.n + kRowsPerChunk - 1) / kRowsPerChunk;
   if (cmax == 0) {
     TWTML_HIP_CHECK(hipMemsetAsync(p.cbase, 0, sizeof(int64_t), s));
     TWTML_HIP_CHECK(hipMemsetAsync(&p.counters[2], 0, sizeof(int64_t), s));
     return;
   }
-  const int grid = ceil_div(cmax, kBlock / kWave) < 4096 ? ceil_div(cmax, kBlock / kWave) : 4096;
+  int grid = ceil_div((cmax + 3) / 4, kBlock / kWave);
+  if (grid > 4096) grid = 4096;
   hipLaunchKernelGGL(k_chunk_len, dim3(grid), dim3(kBlock), 0, s, p.sorted, p.nnz, p.counters,
                      cmax, p.cbase, p.clen8);
   scan_excl(p.cbase, p.cbase, cmax, &p.counters[2], s);
@@ -213,17 +248,20 @@ __device__ __forceinline__ int64_t term_mod(int64_t h, int64_t F) {
   return m < 0 ? m + F : m;
 }
 
+// One wave per 16-row chunk; the 4 lanes of a row take entries j = t, t+4, ...
 __global__ __launch_bounds__(kBlock) void k_featurize(DevRawBatch b, DevPrepared p, FeaturizeParams fp,
                                                       const uint8_t* lpage, const uint16_t* lblocks,
                                                       int64_t cmax) {
   const int64_t n_kept = p.counters[0];
   const int lane = lane_id();
+  const int r = lane / kLanesPerRow, t = lane % kLanesPerRow;
   const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = int64_t(gridDim.x) * kBlock / kWave;
   const int64_t F = fp.num_text_features;
   const int64_t cap_groups = p.cap_entries / kChunkStride;
-  for (int64_t c = wave; c < cmax; c += nwaves) {
-    const int64_t pos = c * kChunk + lane;
+  const int64_t nch = (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;
+  for (int64_t c = wave; c < nch && c < cmax; c += nwaves) {
+    const int64_t pos = c * kRowsPerChunk + r;
     const bool valid = pos < n_kept;
     const int32_t kidx = valid ? p.sorted[pos] : -1;
     const int64_t row = valid ? p.kept[kidx] : 0;
@@ -237,50 +275,52 @@ __global__ __launch_bounds__(kBlock) void k_featurize(DevRawBatch b, DevPrepared
     const int64_t len = valid ? b.offsets[row + 1] - o : 0;
     const int64_t nz = len >= 2 ? len - 1 : len;
     int32_t* out = p.idx + g0 * kChunkStride + lane * kGroup;
-    uint32_t prev = len > 0 ? lower_dev(b.text[o], lpage, lblocks) : 0;
     const int32_t total = L8 * kGroup;
-    for (int32_t j = 0; j < total; ++j) {
+    for (int32_t jj = 0; jj < total; ++jj) {
+      const int64_t j = int64_t(jj) * kLanesPerRow + t;
       int32_t v = -1;
       if (j < nz) {
+        const uint32_t u0 = lower_dev(b.text[o + j], lpage, lblocks);
         int64_t h;
         if (len >= 2) {
-          const uint32_t nxt = lower_dev(b.text[o + j + 1], lpage, lblocks);
-          h = fp.hash_kind == 0 ? int64_t(31u * prev + nxt) : int64_t(murmur_term(prev, nxt, 2));
-          prev = nxt;
+          const uint32_t u1 = lower_dev(b.text[o + j + 1], lpage, lblocks);
+          h = fp.hash_kind == 0 ? int64_t(31u * u0 + u1) : int64_t(murmur_term(u0, u1, 2));
         } else {
-          h = fp.hash_kind == 0 ? int64_t(prev) : int64_t(murmur_term(prev, 0, 1));
+          h = fp.hash_kind == 0 ? int64_t(u0) : int64_t(murmur_term(u0, 0, 1));
         }
         const int64_t idx = term_mod(h, F);
         v = int32_t(idx);
         if (idx < p.flag_len) p.flags[idx] = 1;
       }
-      out[(j >> 3) * kChunkStride + (j & 7)] = v;
+      out[(jj >> 3) * kChunkStride + (jj & 7)] = v;
     }
-    const int64_t q = c * kChunk + lane;
-    if (valid) {
-      const int64_t* sc = b.scalars;
-      p.y[q] = float(sc[row]);
-      const double fol = double(sc[1 * b.n + row]), fav = double(sc[2 * b.n + row]);
-      const double fri = double(sc[3 * b.n + row]);
-      const double age = double(fp.now_ms - sc[4 * b.n + row]);
-      p.num[(c * 4 + 0) * kChunk + lane] = float(fol * 1e-12);
-      p.num[(c * 4 + 1) * kChunk + lane] = float(fav * 1e-12);
-      p.num[(c * 4 + 2) * kChunk + lane] = float(fri * 1e-12);
-      p.num[(c * 4 + 3) * kChunk + lane] = float(age * 1e-14);
-    } else {
-      p.y[q] = 0.f;
-      for (int k = 0; k < 4; ++k) p.num[(c * 4 + k) * kChunk + lane] = 0.f;
+    if (t == 0) {
+      const int64_t cap = p.cap_rows16;
+      if (valid) {
+        const int64_t* sc = b.scalars;
+        p.y[pos] = float(sc[row]);
+        const double fol = double(sc[1 * b.n + row]), fav = double(sc[2 * b.n + row]);
+        const double fri = double(sc[3 * b.n + row]);
+        const double age = double(fp.now_ms - sc[4 * b.n + row]);
+        p.num[0 * cap + pos] = float(fol * 1e-12);
+        p.num[1 * cap + pos] = float(fav * 1e-12);
+        p.num[2 * cap + pos] = float(fri * 1e-12);
+        p.num[3 * cap + pos] = float(age * 1e-14);
+      } else {
+        p.y[pos] = 0.f;
+        for (int k = 0; k < 4; ++k) p.num[k * cap + pos] = 0.f;
+      }
+      p.perm[pos] = kidx;
     }
-    p.perm[q] = kidx;
   }
 }
 
 void launch_featurize(const DevRawBatch& b, const DevPrepared& p, const FeaturizeParams& fp,
                       const uint8_t* lpage, const uint16_t* lblocks, hipStream_t s) {
-  const int64_t cmax = (b.n + kChunk - 1) / kChunk;
+  const int64_t cmax = (b.n + kRowsPerChunk - 1) / kRowsPerChunk;
   if (cmax == 0) return;
   int grid = ceil_div(cmax, kBlock / kWave);
-  if (grid > 8192) grid = 8192;
+  if (grid > 16384) grid = 16384;
   hipLaunchKernelGGL(k_featurize, dim3(grid), dim3(kBlock), 0, s, b, p, fp, lpage, lblocks, cmax);
 }
 

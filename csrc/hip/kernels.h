@@ -40,9 +40,9 @@ struct DevPrepared {
   int64_t* cbase;           // [C+1] first group of chunk c (entries = groups*512)
   int32_t* idx;             // [E]   hashed feature index per entry (-1 = pad)
   void* slot;               // [E]   compact slot per entry (u16 or u32)
-  float* y;                 // [C*64] label
-  float* num;               // [C*4*64] numeric features [c][k][lane]
-  int32_t* perm;            // [C*64] kept index of (c, lane), -1 if none
+  float* y;                 // [R16] label at sorted position p
+  float* num;               // [4][R16] numeric features (SoA by sorted position)
+  int32_t* perm;            // [R16] kept index at sorted position p, -1 if none
   // active set
   uint8_t* flags;           // [Fh]
   int32_t* uniq;            // [Fh]  sorted touched feature ids
@@ -50,7 +50,7 @@ struct DevPrepared {
   int64_t* ublk;            // [Fh/4096+2]
   // counters (device): [0]=n_kept [1]=n_unique [2]=groups [3]=error
   int64_t* counters;
-  int64_t cap_rows, cap_entries, cap_chunks, flag_len;
+  int64_t cap_rows, cap_rows16, cap_entries, cap_chunks, flag_len;
 };
 
 struct FeaturizeParams {
@@ -78,7 +78,7 @@ struct DevSgd {
   double* w64;          // [F+4] master weights (fp64)
   double* wc64;         // [NS]  compact master weights
   float* wc32;          // [NS]  compact fp32 copy read by the gradient kernel
-  float* g32;           // [NS+1] gradient accumulator (+ loss at [NS])
+  double* g64;          // [NS+1] gradient accumulator (+ loss at [NS])
   double* red64;        // [4] {loss, m, pad, pad} for sampled iterations
   double* stats;        // [8] n, sum_y, sum_y2, sum_p, sum_p2, sum_e2, -, -
   double* state;        // [8] 0 done 1 converged 2 n_updates 3 iters 4 wrest2 5 m_global 6 wnorm2_full
@@ -98,6 +98,7 @@ struct SgdParams {
   int64_t row_offset;   // global row id of this rank's kept row 0 (sampling)
   int32_t want_pred;
   int32_t sample;       // fraction < 1
+  int32_t ablate;       // perf diagnostics: 1 = skip scatter, 2 = skip gather+scatter
 };
 
 void launch_gather_w(const DevSgd& d, const DevPrepared& p, hipStream_t s);
@@ -106,7 +107,8 @@ void launch_sgd_iter(const DevSgd& d, const DevPrepared& p, const SgdParams& sp,
                      bool u16, int grid, hipStream_t s);
 void launch_sgd_update(const DevSgd& d, const SgdParams& sp, hipStream_t s);
 void launch_scatter_w(const DevSgd& d, const DevPrepared& p, hipStream_t s);
-int sgd_lds_limit_slots();
+int sgd_lds_rep(int64_t ns);
+int sgd_iter_grid(int64_t ns, int64_t n_kept, int num_cu);
 
 // ---------------------------------------------------------------------------
 // K-means (kmeans.hip)

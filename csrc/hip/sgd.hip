@@ -12,25 +12,35 @@
 // features have exactly zero gradient, so the compact iteration is exactly
 // the full-width one; ||w|| adds the constant norm of the untouched part.
 //
-// k_sgd_iter: each workgroup stages the compact fp32 weights in LDS
-// (typically 4-16K slots -> 16-64 KB), streams its SELL-64 chunks (one row per
-// lane, 16-byte slot loads), gathers w from LDS, and scatters r into an LDS
-// gradient (ds_add_f32) -- the hot bigram range never touches global
-// atomics.  The workgroup flushes its non-zero gradient slots once.  At
+// k_sgd_iter_lds (the hot kernel): a 512-thread workgroup stages the compact
+// fp32 weights in LDS, streams its SELL-16x4 chunks (4 lanes per row, the
+// row's slots kept in VGPRs between the forward gather and the backward
+// scatter), and accumulates the gradient in LDS as 64-bit FIXED POINT with
+// ds_add_u64.  Measured on gfx950 (tools/ubench_lds_atomics.hip): ds_add_f32
+// costs ~170 LDS cycles per wave-instruction, ds_add_u64 ~12 and ds_read_b32
+// ~8, so integer accumulation is ~14x faster -- and exact, so a workgroup's
+// partial gradient is independent of the order rows are added in.  Each
+// workgroup flushes its non-zero slots once (fp64 global atomics).  At
 // iteration 1 the same pass yields the prequential predictions and batch
 // statistics (K4 + K7 fused: output op #1 uses the weights before training).
-// k_sgd_update (one workgroup): fp64 master update + norms + convergence flag;
-// every later kernel of the batch early-exits once the flag is set.
+// k_sgd_update (one workgroup): fp64 master update + norms + convergence
+// flag; every later kernel of the batch early-exits once the flag is set.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 
 #include "common.h"
 #include "kernels.h"
 
 namespace twtml {
 
-constexpr int kLdsBytes = 160 * 1024;
-
-int sgd_lds_limit_slots() { return kLdsBytes / (2 * int(sizeof(float))); }
+// Fixed-point scale of the LDS gradient: residuals are added as
+// round(r * 2^24) (resolution 6e-8, finer than fp32 for |r| > 1).  |r| is
+// clamped to 2^26 so a workgroup sum of up to 2^12 rows cannot overflow int64;
+// a clamp raises the overflow flag (state[7]) and the host reports it.
+constexpr float kFixScale = 16777216.0f;        // 2^24
+constexpr double kFixInv = 1.0 / 16777216.0;
+constexpr float kFixClamp = 67108864.0f;        // 2^26
 
 template <typename SlotT>
 struct SlotLoad;
@@ -53,140 +63,280 @@ struct SlotLoad<uint32_t> {
   }
 };
 
-template <typename SlotT, bool STATS, bool SAMPLE, bool LDS>
-__global__ __launch_bounds__(kBlock) void k_sgd_iter(DevSgd d, DevPrepared p, SgdParams sp) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  __shared__ double red_scratch[kBlock / kWave];
-  if (d.state[0] != 0.0) return;  // converged / finished: whole batch is a no-op
-  const int64_t ns = d.ns;
-  float* wl = lds;
-  float* gl = lds + (LDS ? ns : 0);
-  const float* w = LDS ? wl : d.wc32;
-  float* g = LDS ? gl : d.g32;
-  if (LDS) {
-    for (int64_t s = threadIdx.x; s < ns; s += kBlock) {
-      wl[s] = d.wc32[s];
-      gl[s] = 0.f;
-    }
-    __syncthreads();
-  }
-  const int lane = lane_id();
-  const int64_t n_kept = p.counters[0];
-  const int64_t nch = (n_kept + kChunk - 1) / kChunk;
-  const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
-  const int64_t nwaves = int64_t(gridDim.x) * (kBlock / kWave);
-  const SlotT* slot = static_cast<const SlotT*>(p.slot);
-  const float w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3];
+__device__ __forceinline__ void unpack8(const uint4 v, uint32_t (&s)[8]) {
+  s[0] = v.x & 0xFFFF; s[1] = v.x >> 16; s[2] = v.y & 0xFFFF; s[3] = v.y >> 16;
+  s[4] = v.z & 0xFFFF; s[5] = v.z >> 16; s[6] = v.w & 0xFFFF; s[7] = v.w >> 16;
+}
 
+// Per-row epilogue shared by both iteration kernels: residual, stats, preds.
+struct RowAcc {
   float gn0 = 0.f, gn1 = 0.f, gn2 = 0.f, gn3 = 0.f, loss = 0.f;
   double msum = 0.0;
-  double st_n = 0, st_y = 0, st_y2 = 0, st_p = 0, st_p2 = 0, st_e2 = 0;
+  double st[6] = {0, 0, 0, 0, 0, 0};
+};
 
-  for (int64_t c = wave; c < nch; c += nwaves) {
-    const int32_t L8 = p.clen8[c];
-    const SlotT* sl = slot + p.cbase[c] * kChunkStride + lane * kGroup;
-    float dot = 0.f;
-    for (int32_t q = 0; q < L8; ++q) {
-      uint32_t s[8];
-      SlotLoad<SlotT>::load(sl + int64_t(q) * kChunkStride, s);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) dot += w[s[k]];
-    }
-    const int64_t q0 = c * kChunk + lane;
-    const float n0 = p.num[(c * 4 + 0) * kChunk + lane], n1 = p.num[(c * 4 + 1) * kChunk + lane];
-    const float n2 = p.num[(c * 4 + 2) * kChunk + lane], n3 = p.num[(c * 4 + 3) * kChunk + lane];
-    dot += n0 * w0 + n1 * w1 + n2 * w2 + n3 * w3;
-    const bool valid = q0 < n_kept;
-    const float y = p.y[q0];
-    bool in = valid;
-    if (SAMPLE && valid)
-      in = sample_uniform(uint64_t(42 + sp.iteration), uint64_t(sp.row_offset + p.perm[q0])) <
-           sp.fraction;
-    const float r = in ? dot - y : 0.f;
+template <bool STATS, bool SAMPLE>
+__device__ __forceinline__ float row_residual(float dot, int64_t pos, int t, const DevSgd& d,
+                                              const DevPrepared& p, const SgdParams& sp,
+                                              int64_t n_kept, float w0, float w1, float w2,
+                                              float w3, RowAcc& acc) {
+  const bool valid = pos < n_kept;
+  const int64_t cap = p.cap_rows16;
+  const float n0 = p.num[0 * cap + pos], n1 = p.num[1 * cap + pos];
+  const float n2 = p.num[2 * cap + pos], n3 = p.num[3 * cap + pos];
+  dot += n0 * w0 + n1 * w1 + n2 * w2 + n3 * w3;
+  const float y = p.y[pos];
+  bool in = valid;
+  if (SAMPLE && valid)
+    in = sample_uniform(uint64_t(42 + sp.iteration), uint64_t(sp.row_offset + p.perm[pos])) <
+         sp.fraction;
+  const float r = in ? dot - y : 0.f;
+  if (t == 0) {  // one lane per row owns the row-level accumulators
     if (STATS && valid) {
       const double pr = round_half_away(double(dot));
-      if (sp.want_pred) d.pred_out[p.perm[q0]] = float(pr);
+      if (sp.want_pred) d.pred_out[p.perm[pos]] = float(pr);
       const double yd = double(y), e = yd - pr;
-      st_n += 1.0; st_y += yd; st_y2 += yd * yd; st_p += pr; st_p2 += pr * pr; st_e2 += e * e;
+      acc.st[0] += 1.0; acc.st[1] += yd; acc.st[2] += yd * yd;
+      acc.st[3] += pr; acc.st[4] += pr * pr; acc.st[5] += e * e;
     }
-    if (__any(r != 0.f)) {
-      for (int32_t q = 0; q < L8; ++q) {
-        uint32_t s[8];
-        SlotLoad<SlotT>::load(sl + int64_t(q) * kChunkStride, s);
-        if (r != 0.f) {
-#pragma unroll
-          for (int k = 0; k < 8; ++k) atomicAdd(&g[s[k]], r);
-        }
-      }
-    }
-    gn0 += r * n0; gn1 += r * n1; gn2 += r * n2; gn3 += r * n3;
-    loss += r * r;
-    msum += in ? 1.0 : 0.0;
+    acc.gn0 += r * n0; acc.gn1 += r * n1; acc.gn2 += r * n2; acc.gn3 += r * n3;
+    acc.loss += r * r;
+    acc.msum += in ? 1.0 : 0.0;
   }
+  return r;
+}
 
-  // --- workgroup reductions of the scalar partials -> one atomic each
-  const double b0 = block_sum<double>(gn0, red_scratch);
-  const double b1 = block_sum<double>(gn1, red_scratch);
-  const double b2 = block_sum<double>(gn2, red_scratch);
-  const double b3 = block_sum<double>(gn3, red_scratch);
-  const double bl = block_sum<double>(0.5 * double(loss), red_scratch);
+template <bool STATS, bool SAMPLE>
+__device__ __forceinline__ void flush_scalars(const DevSgd& d, const RowAcc& acc, double* scratch) {
+  const double b0 = block_sum<double>(acc.gn0, scratch);
+  const double b1 = block_sum<double>(acc.gn1, scratch);
+  const double b2 = block_sum<double>(acc.gn2, scratch);
+  const double b3 = block_sum<double>(acc.gn3, scratch);
+  const double bl = block_sum<double>(0.5 * double(acc.loss), scratch);
   double bm = 0.0;
-  if (SAMPLE) bm = block_sum<double>(msum, red_scratch);
+  if (SAMPLE) bm = block_sum<double>(acc.msum, scratch);
   double bs[6] = {0, 0, 0, 0, 0, 0};
-  if (STATS) {
-    bs[0] = block_sum<double>(st_n, red_scratch);
-    bs[1] = block_sum<double>(st_y, red_scratch);
-    bs[2] = block_sum<double>(st_y2, red_scratch);
-    bs[3] = block_sum<double>(st_p, red_scratch);
-    bs[4] = block_sum<double>(st_p2, red_scratch);
-    bs[5] = block_sum<double>(st_e2, red_scratch);
-  }
+  if (STATS)
+    for (int k = 0; k < 6; ++k) bs[k] = block_sum<double>(acc.st[k], scratch);
   if (threadIdx.x == 0) {
-    atomicAdd(&d.g32[0], float(b0));
-    atomicAdd(&d.g32[1], float(b1));
-    atomicAdd(&d.g32[2], float(b2));
-    atomicAdd(&d.g32[3], float(b3));
-    atomicAdd(&d.g32[ns], float(bl));
+    atomicAdd(&d.g64[0], b0);
+    atomicAdd(&d.g64[1], b1);
+    atomicAdd(&d.g64[2], b2);
+    atomicAdd(&d.g64[3], b3);
+    atomicAdd(&d.g64[d.ns], bl);
     if (SAMPLE) atomicAdd(&d.red64[1], bm);
     if (STATS)
       for (int k = 0; k < 6; ++k) atomicAdd(&d.stats[k], bs[k]);
   }
-  if (LDS) {
-    __syncthreads();
-    const int64_t hi = kNumNumeric + d.n_unique;  // pads are never flushed
-    for (int64_t s = kNumNumeric + threadIdx.x; s < hi; s += kBlock) {
-      const float v = gl[s];
-      if (v != 0.f) atomicAdd(&d.g32[s], v);
+}
+
+__device__ __forceinline__ unsigned long long to_fix(float r, bool& clamped) {
+  float v = r * kFixScale;
+  const float lim = kFixClamp * kFixScale;
+  if (fabsf(v) > lim) {
+    clamped = true;
+    v = v > 0.f ? lim : -lim;
+  }
+  return (unsigned long long)(long long)__float2ll_rn(v);
+}
+
+// ---------------------------------------------------------------------------
+// Fast path: u16 slots, LDS weights + REP replicated fixed-point gradients.
+// ---------------------------------------------------------------------------
+constexpr int kIterBlock = 512;
+
+template <bool STATS, bool SAMPLE, int REP>
+__global__ __launch_bounds__(kIterBlock) void k_sgd_iter_lds(DevSgd d, DevPrepared p, SgdParams sp) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  __shared__ double scratch[kIterBlock / kWave];
+  if (d.state[0] != 0.0) return;  // converged / finished: the rest of the batch is a no-op
+  const int64_t ns = d.ns;        // multiple of 64
+  float* wl = lds;
+  unsigned long long* gl = reinterpret_cast<unsigned long long*>(lds + ns);
+  for (int64_t s = threadIdx.x; s < ns; s += kIterBlock) wl[s] = d.wc32[s];
+  for (int64_t s = threadIdx.x; s < ns * REP; s += kIterBlock) gl[s] = 0ull;
+  __syncthreads();
+  const int lane = lane_id();
+  const int r = lane / kLanesPerRow, t = lane % kLanesPerRow;
+  const int rep = lane % REP;
+  const int64_t n_kept = p.counters[0];
+  const int64_t nch = (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;
+  const int64_t wave = (int64_t(blockIdx.x) * kIterBlock + threadIdx.x) / kWave;
+  const int64_t nwaves = int64_t(gridDim.x) * (kIterBlock / kWave);
+  const uint16_t* slot = static_cast<const uint16_t*>(p.slot);
+  const float w0 = wl[0], w1 = wl[1], w2 = wl[2], w3 = wl[3];
+  RowAcc acc;
+  bool clamped = false;
+
+  for (int64_t c = wave; c < nch; c += nwaves) {
+    const int32_t L8 = p.clen8[c];
+    const uint16_t* sl = slot + p.cbase[c] * kChunkStride + lane * kGroup;
+    const int64_t pos = c * kRowsPerChunk + r;
+    if (L8 <= kMaxRegGroups) {
+      uint4 v[kMaxRegGroups];
+#pragma unroll
+      for (int g = 0; g < kMaxRegGroups; ++g)
+        if (g < L8) v[g] = *reinterpret_cast<const uint4*>(sl + int64_t(g) * kChunkStride);
+      float d0 = 0.f, d1 = 0.f;
+#pragma unroll
+      for (int g = 0; g < kMaxRegGroups; ++g) {
+        if (g < L8 && sp.ablate < 2) {
+          uint32_t s[8];
+          unpack8(v[g], s);
+          d0 += wl[s[0]] + wl[s[2]] + wl[s[4]] + wl[s[6]];
+          d1 += wl[s[1]] + wl[s[3]] + wl[s[5]] + wl[s[7]];
+        }
+      }
+      float dot = d0 + d1;
+      if (sp.ablate >= 2) {
+        uint32_t s[8];
+        unpack8(v[0], s);
+        dot += float(s[0] + s[7]) * 1e-30f;  // keep the loads live
+      }
+      dot += __shfl_xor(dot, 1, kWave);
+      dot += __shfl_xor(dot, 2, kWave);
+      const float res = row_residual<STATS, SAMPLE>(dot, pos, t, d, p, sp, n_kept, w0, w1, w2, w3, acc);
+      if (res != 0.f && sp.ablate == 0) {
+        const unsigned long long q = to_fix(res, clamped);
+#pragma unroll
+        for (int g = 0; g < kMaxRegGroups; ++g) {
+          if (g < L8) {
+            uint32_t s[8];
+            unpack8(v[g], s);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) atomicAdd(&gl[s[k] * REP + rep], q);
+          }
+        }
+      }
+    } else {  // very long rows: stream the slots twice
+      float dot = 0.f;
+      for (int32_t g = 0; g < L8; ++g) {
+        uint32_t s[8];
+        unpack8(*reinterpret_cast<const uint4*>(sl + int64_t(g) * kChunkStride), s);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) dot += wl[s[k]];
+      }
+      dot += __shfl_xor(dot, 1, kWave);
+      dot += __shfl_xor(dot, 2, kWave);
+      const float res = row_residual<STATS, SAMPLE>(dot, pos, t, d, p, sp, n_kept, w0, w1, w2, w3, acc);
+      if (res != 0.f) {
+        const unsigned long long q = to_fix(res, clamped);
+        for (int32_t g = 0; g < L8; ++g) {
+          uint32_t s[8];
+          unpack8(*reinterpret_cast<const uint4*>(sl + int64_t(g) * kChunkStride), s);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) atomicAdd(&gl[s[k] * REP + rep], q);
+        }
+      }
     }
+  }
+
+  flush_scalars<STATS, SAMPLE>(d, acc, scratch);
+  if (__any(clamped) && lane == 0) d.state[7] = 1.0;
+  __syncthreads();
+  const int64_t hi = kNumNumeric + d.n_unique;  // pads are never flushed
+  for (int64_t s = kNumNumeric + threadIdx.x; s < hi; s += kIterBlock) {
+    long long v = 0;
+#pragma unroll
+    for (int k = 0; k < REP; ++k) v += (long long)gl[s * REP + k];
+    if (v != 0) atomicAdd(&d.g64[s], double(v) * kFixInv);
   }
 }
 
-template <typename SlotT, bool LDS>
-static void launch_iter_t(const DevSgd& d, const DevPrepared& p, const SgdParams& sp, int grid,
-                          size_t lds, hipStream_t s) {
-  const bool stats = sp.iteration == 1;
-  const bool sample = sp.sample != 0;
-  if (stats && sample)
-    hipLaunchKernelGGL((k_sgd_iter<SlotT, true, true, LDS>), dim3(grid), dim3(kBlock), lds, s, d, p, sp);
-  else if (stats)
-    hipLaunchKernelGGL((k_sgd_iter<SlotT, true, false, LDS>), dim3(grid), dim3(kBlock), lds, s, d, p, sp);
-  else if (sample)
-    hipLaunchKernelGGL((k_sgd_iter<SlotT, false, true, LDS>), dim3(grid), dim3(kBlock), lds, s, d, p, sp);
-  else
-    hipLaunchKernelGGL((k_sgd_iter<SlotT, false, false, LDS>), dim3(grid), dim3(kBlock), lds, s, d, p, sp);
+// Generic path: any slot width, weights read from global (L2), gradient by
+// global fp64 atomics.  Used when the active set exceeds LDS.
+template <typename SlotT, bool STATS, bool SAMPLE>
+__global__ __launch_bounds__(kBlock) void k_sgd_iter_global(DevSgd d, DevPrepared p, SgdParams sp) {
+  __shared__ double scratch[kBlock / kWave];
+  if (d.state[0] != 0.0) return;
+  const float* w = d.wc32;
+  const int lane = lane_id();
+  const int r = lane / kLanesPerRow, t = lane % kLanesPerRow;
+  const int64_t n_kept = p.counters[0];
+  const int64_t nch = (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;
+  const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
+  const int64_t nwaves = int64_t(gridDim.x) * (kBlock / kWave);
+  const SlotT* slot = static_cast<const SlotT*>(p.slot);
+  const float w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3];
+  RowAcc acc;
+  for (int64_t c = wave; c < nch; c += nwaves) {
+    const int32_t L8 = p.clen8[c];
+    const SlotT* sl = slot + p.cbase[c] * kChunkStride + lane * kGroup;
+    const int64_t pos = c * kRowsPerChunk + r;
+    float dot = 0.f;
+    for (int32_t g = 0; g < L8; ++g) {
+      uint32_t s[8];
+      SlotLoad<SlotT>::load(sl + int64_t(g) * kChunkStride, s);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) dot += w[s[k]];
+    }
+    dot += __shfl_xor(dot, 1, kWave);
+    dot += __shfl_xor(dot, 2, kWave);
+    const float res = row_residual<STATS, SAMPLE>(dot, pos, t, d, p, sp, n_kept, w0, w1, w2, w3, acc);
+    if (res != 0.f) {
+      for (int32_t g = 0; g < L8; ++g) {
+        uint32_t s[8];
+        SlotLoad<SlotT>::load(sl + int64_t(g) * kChunkStride, s);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (s[k] >= kNumNumeric && s[k] < kNumNumeric + d.n_unique) atomicAdd(&d.g64[s[k]], double(res));
+      }
+    }
+  }
+  flush_scalars<STATS, SAMPLE>(d, acc, scratch);
+}
+
+// LDS bytes of the fast path for a given replication factor.
+static int64_t lds_bytes(int64_t ns, int rep) {
+  return ns * int64_t(sizeof(float)) + ns * rep * int64_t(sizeof(unsigned long long));
+}
+
+// Replication factor for the LDS gradient (0 = does not fit -> global path).
+int sgd_lds_rep(int64_t ns) {
+  if (lds_bytes(ns, 2) <= 40 * 1024) return 2;
+  if (lds_bytes(ns, 1) <= 160 * 1024 - 2048) return 1;
+  return 0;
+}
+
+template <bool STATS, bool SAMPLE>
+static void launch_iter_t(const DevSgd& d, const DevPrepared& p, const SgdParams& sp, bool u16,
+                          int rep, int grid, hipStream_t s) {
+  if (u16 && rep > 0) {
+    const size_t lds = size_t(lds_bytes(d.ns, rep));
+    if (rep == 2)
+      hipLaunchKernelGGL((k_sgd_iter_lds<STATS, SAMPLE, 2>), dim3(grid), dim3(kIterBlock), lds, s, d, p, sp);
+    else
+      hipLaunchKernelGGL((k_sgd_iter_lds<STATS, SAMPLE, 1>), dim3(grid), dim3(kIterBlock), lds, s, d, p, sp);
+  } else if (u16) {
+    hipLaunchKernelGGL((k_sgd_iter_global<uint16_t, STATS, SAMPLE>), dim3(grid * 2), dim3(kBlock), 0, s, d, p, sp);
+  } else {
+    hipLaunchKernelGGL((k_sgd_iter_global<uint32_t, STATS, SAMPLE>), dim3(grid * 2), dim3(kBlock), 0, s, d, p, sp);
+  }
+}
+
+int sgd_iter_grid(int64_t ns, int64_t n_kept, int num_cu) {
+  const int rep = sgd_lds_rep(ns);
+  int per_cu = 2;
+  if (rep > 0) {
+    const int64_t lds = lds_bytes(ns, rep) + 1024;
+    per_cu = int(std::min<int64_t>(4, (160 * 1024) / lds));
+    if (per_cu < 1) per_cu = 1;
+  }
+  const int64_t nch = (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;
+  const int64_t waves_per_wg = kIterBlock / kWave;
+  int64_t g = std::min<int64_t>(int64_t(num_cu) * per_cu, (nch + waves_per_wg - 1) / waves_per_wg);
+  return int(g < 1 ? 1 : g);
 }
 
 void launch_sgd_iter(const DevSgd& d, const DevPrepared& p, const SgdParams& sp, int64_t /*groups*/,
                      bool u16, int grid, hipStream_t s) {
-  const bool lds_ok = d.ns <= sgd_lds_limit_slots() - 64;
-  const size_t lds = lds_ok ? size_t(2 * d.ns) * sizeof(float) : 0;
-  if (u16) {
-    if (lds_ok) launch_iter_t<uint16_t, true>(d, p, sp, grid, lds, s);
-    else launch_iter_t<uint16_t, false>(d, p, sp, grid, lds, s);
-  } else {
-    if (lds_ok) launch_iter_t<uint32_t, true>(d, p, sp, grid, lds, s);
-    else launch_iter_t<uint32_t, false>(d, p, sp, grid, lds, s);
-  }
+  const int rep = u16 ? sgd_lds_rep(d.ns) : 0;
+  const bool stats = sp.iteration == 1;
+  const bool sample = sp.sample != 0;
+  if (stats && sample) launch_iter_t<true, true>(d, p, sp, u16, rep, grid, s);
+  else if (stats) launch_iter_t<true, false>(d, p, sp, u16, rep, grid, s);
+  else if (sample) launch_iter_t<false, true>(d, p, sp, u16, rep, grid, s);
+  else launch_iter_t<false, false>(d, p, sp, u16, rep, grid, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -198,21 +348,21 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp) {
   const int tid = threadIdx.x;
   const int64_t hi = kNumNumeric + d.n_unique;
   const double m = sp.sample ? d.red64[1] : d.state[5];
-  const double loss = double(d.g32[d.ns]);
+  const double loss = d.g64[d.ns];
   double ds = 0.0, ws = 0.0;
   if (m > 0.0) {
     const double alpha = sp.step_size / sqrt(double(sp.iteration));
     for (int64_t s = tid; s < hi; s += 1024) {
-      const double step = alpha * (double(d.g32[s]) / m);
+      const double step = alpha * (d.g64[s] / m);
       const double wn = d.wc64[s] - step;
       d.wc64[s] = wn;
       d.wc32[s] = float(wn);
-      d.g32[s] = 0.f;
+      d.g64[s] = 0.0;
       ds += step * step;
       ws += wn * wn;
     }
   } else {
-    for (int64_t s = tid; s < hi; s += 1024) d.g32[s] = 0.f;
+    for (int64_t s = tid; s < hi; s += 1024) d.g64[s] = 0.0;
   }
   // block reduce (1024 threads = 16 waves)
   ds = wave_sum(ds);
@@ -242,7 +392,7 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp) {
     }
     d.state[3] = double(sp.iteration);
     if (sp.iteration >= sp.num_iterations) d.state[0] = 1.0;
-    d.g32[d.ns] = 0.f;
+    d.g64[d.ns] = 0.0;
     d.red64[0] = 0.0;
     d.red64[1] = 0.0;
   }
@@ -265,7 +415,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_w(DevSgd d, const int32_t* un
     else if (s < kNumNumeric + d.n_unique) v = d.w64[uniq[s - kNumNumeric]];
     d.wc64[s] = v;
     d.wc32[s] = float(v);
-    d.g32[s] = 0.f;
+    d.g64[s] = 0.0;
     acc += v * v;
   }
   acc = block_sum(acc, scratch);
@@ -308,11 +458,10 @@ void launch_scatter_w(const DevSgd& d, const DevPrepared& p, hipStream_t s) {
   hipLaunchKernelGGL(k_scatter_w, dim3(grid), dim3(kBlock), 0, s, d, p.uniq);
 }
 
-}  // namespace twtml
-
-namespace twtml {
 __global__ void k_batch_init(double* state, double m_global) { state[5] = m_global; }
+
 void launch_batch_init(double* state, double m_global, hipStream_t s) {
   hipLaunchKernelGGL(k_batch_init, dim3(1), dim3(1), 0, s, state, m_global);
 }
+
 }  // namespace twtml

@@ -24,18 +24,21 @@ def _engine(F, hash="java", **kw):
 
 
 def _rows_from_debug(dbg):
-    """Per kept row (kept order) -> sorted multiset of hashed feature ids."""
+    """Per kept row (kept order) -> sorted multiset of hashed feature ids.
+
+    SELL-16x4 layout: chunk c = 16 rows, row r owns lanes 4r..4r+3.
+    """
     nk = int(dbg["counters"][0])
     idx, clen8, cbase, perm = dbg["idx"], dbg["clen8"], dbg["cbase"], dbg["perm"]
     rows = [None] * nk
     for c in range(clen8.shape[0]):
         g0, L8 = int(cbase[c]), int(clen8[c])
         block = idx[g0 * 512:(g0 + L8) * 512].reshape(L8, 64, 8)
-        for lane in range(64):
-            k = int(perm[c * 64 + lane])
+        for r in range(16):
+            k = int(perm[c * 16 + r])
             if k < 0:
                 continue
-            v = block[:, lane, :].reshape(-1)
+            v = block[:, 4 * r:4 * r + 4, :].reshape(-1)
             rows[k] = np.sort(v[v >= 0])
     return rows
 
@@ -62,13 +65,13 @@ def test_featurize_matches_oracle(hip_module, F, hash):
     nk = fb.n
     y = np.zeros(nk, np.float32)
     num = np.zeros((nk, 4), np.float32)
-    perm, C = dbg["perm"], dbg["clen8"].shape[0]
-    for c in range(C):
-        for lane in range(64):
-            k = int(perm[c * 64 + lane])
-            if k >= 0:
-                y[k] = dbg["y"][c * 64 + lane]
-                num[k] = dbg["num"][(c * 4 + np.arange(4)) * 64 + lane]
+    perm = dbg["perm"]
+    R = perm.shape[0]
+    for pos in range(R):
+        k = int(perm[pos])
+        if k >= 0:
+            y[k] = dbg["y"][pos]
+            num[k] = dbg["num"][np.arange(4) * R + pos]
     np.testing.assert_array_equal(y, fb.y.astype(np.float32))
     want_num = fb.X[:, F:F + 4].toarray()
     np.testing.assert_allclose(num, want_num, rtol=2e-7, atol=0)

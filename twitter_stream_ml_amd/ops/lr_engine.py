@@ -49,6 +49,7 @@ class LRDeviceConfig:
     max_rows: int = 1 << 16
     max_units: int = (1 << 16) * 281
     sgd_grid: int = 0
+    ablate: int = 0          # perf diagnostics only (1: no scatter, 2: no gather/scatter)
 
     def as_dict(self) -> Dict[str, object]:
         return {
@@ -65,6 +66,7 @@ class LRDeviceConfig:
             "max_rows": int(self.max_rows),
             "max_units": int(self.max_units),
             "sgd_grid": int(self.sgd_grid),
+            "ablate": int(self.ablate),
         }
 
 
