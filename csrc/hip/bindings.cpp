@@ -77,17 +77,26 @@ PYBIND11_MODULE(_twtml_hip, m) {
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
   m.def("rccl_version", &rccl_version);
 
-  py::class_<Comm, std::shared_ptr<Comm>>(m, "Comm")
-      .def(py::init([](py::bytes uid, int rank, int world, int device) {
-             std::string s = uid;
-             py::gil_scoped_release nogil;
-             return std::make_shared<Comm>(s, rank, world, device);
-           }),
-           py::arg("unique_id"), py::arg("rank"), py::arg("world"), py::arg("device"))
+  py::class_<Comm, std::shared_ptr<Comm>>(m, "CommBase")
       .def_property_readonly("rank", &Comm::rank)
       .def_property_readonly("world", &Comm::world)
+      .def_property_readonly("kind", &Comm::kind)
       .def("abort", &Comm::abort)
       .def("check", &Comm::check_async);
+  // RCCL communicator (one process per GPU)
+  m.def("Comm", [](py::bytes uid, int rank, int world, int device) {
+        std::string s = uid;
+        py::gil_scoped_release nogil;
+        return std::shared_ptr<Comm>(std::make_shared<RcclComm>(s, rank, world, device));
+      },
+      py::arg("unique_id"), py::arg("rank"), py::arg("world"), py::arg("device"));
+  // In-process loopback group: N engines on threads of one process (tests)
+  py::class_<LoopbackHub, std::shared_ptr<LoopbackHub>>(m, "LoopbackGroup")
+      .def(py::init<int>(), py::arg("world"))
+      .def("comm", [](std::shared_ptr<LoopbackHub> hub, int rank) {
+        if (rank < 0 || rank >= hub->world()) throw std::invalid_argument("rank out of range");
+        return std::shared_ptr<Comm>(std::make_shared<LoopbackComm>(hub, rank));
+      });
 
   py::class_<HostBatch, std::shared_ptr<HostBatch>>(m, "HostBatch")
       .def(py::init<int64_t, int64_t>(), py::arg("max_rows"), py::arg("max_units"))

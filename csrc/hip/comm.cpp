@@ -1,6 +1,7 @@
 #include "comm.h"
 
 #include <cstring>
+#include <functional>
 #include <stdexcept>
 
 #include "common.h"
@@ -27,8 +28,10 @@ std::string rccl_version() {
   return std::to_string(v);
 }
 
-Comm::Comm(const std::string& unique_id, int rank, int world, int device)
-    : rank_(rank), world_(world) {
+// ---------------------------------------------------------------------------
+RcclComm::RcclComm(const std::string& unique_id, int rank, int world, int device) {
+  rank_ = rank;
+  world_ = world;
   if (unique_id.size() != NCCL_UNIQUE_ID_BYTES)
     throw std::invalid_argument("ncclUniqueId must be 128 bytes");
   if (world < 1 || rank < 0 || rank >= world) throw std::invalid_argument("bad rank/world");
@@ -38,32 +41,117 @@ Comm::Comm(const std::string& unique_id, int rank, int world, int device)
   TWTML_NCCL_CHECK(ncclCommInitRank(&comm_, world, id, rank));
 }
 
-Comm::~Comm() {
+RcclComm::~RcclComm() {
   if (comm_) ncclCommDestroy(comm_);
 }
 
-void Comm::allreduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t s) {
+void RcclComm::allreduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t s) {
   if (world_ == 1 || count == 0) return;
   TWTML_NCCL_CHECK(ncclAllReduce(buf, buf, count, dt, op, comm_, s));
 }
 
-void Comm::broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t s) {
+void RcclComm::broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t s) {
   if (world_ == 1 || count == 0) return;
   TWTML_NCCL_CHECK(ncclBroadcast(buf, buf, count, dt, root, comm_, s));
 }
 
-void Comm::check_async() const {
+void RcclComm::check_async() const {
   ncclResult_t r = ncclSuccess;
   TWTML_NCCL_CHECK(ncclCommGetAsyncError(comm_, &r));
   if (r != ncclSuccess && r != ncclInProgress)
     throw std::runtime_error(std::string("RCCL async error: ") + ncclGetErrorString(r));
 }
 
-void Comm::abort() {
+void RcclComm::abort() {
   if (comm_) {
     ncclCommAbort(comm_);
     comm_ = nullptr;
   }
+}
+
+// ---------------------------------------------------------------------------
+static size_t dt_size(ncclDataType_t dt) {
+  switch (dt) {
+    case ncclInt8: case ncclUint8: return 1;
+    case ncclFloat16: case ncclBfloat16: return 2;
+    case ncclInt32: case ncclUint32: case ncclFloat32: return 4;
+    case ncclInt64: case ncclUint64: case ncclFloat64: return 8;
+    default: throw std::invalid_argument("loopback: unsupported dtype");
+  }
+}
+
+template <typename T>
+static void reduce_into(T* acc, const T* x, size_t n, ncclRedOp_t op) {
+  for (size_t i = 0; i < n; ++i) {
+    switch (op) {
+      case ncclSum: acc[i] = T(acc[i] + x[i]); break;
+      case ncclMax: acc[i] = acc[i] > x[i] ? acc[i] : x[i]; break;
+      case ncclMin: acc[i] = acc[i] < x[i] ? acc[i] : x[i]; break;
+      default: throw std::invalid_argument("loopback: unsupported op");
+    }
+  }
+}
+
+void LoopbackHub::arrive_and_wait(int rank, void* buf, const std::function<void()>& leader_work) {
+  std::unique_lock<std::mutex> lk(m_);
+  const unsigned long long gen = generation_;
+  bufs_[size_t(rank)] = buf;
+  if (++arrived_ == world_) {
+    leader_work();
+    arrived_ = 0;
+    ++generation_;
+    cv_.notify_all();
+  } else {
+    cv_.wait(lk, [&] { return generation_ != gen; });
+  }
+}
+
+void LoopbackHub::allreduce(int rank, void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op) {
+  const size_t bytes = count * dt_size(dt);
+  arrive_and_wait(rank, buf, [&] {
+    std::vector<unsigned char> acc(bytes), tmp(bytes);
+    TWTML_HIP_CHECK(hipMemcpy(acc.data(), bufs_[0], bytes, hipMemcpyDeviceToHost));
+    for (int r = 1; r < world_; ++r) {
+      TWTML_HIP_CHECK(hipMemcpy(tmp.data(), bufs_[size_t(r)], bytes, hipMemcpyDeviceToHost));
+      switch (dt) {
+        case ncclUint8: reduce_into(acc.data(), tmp.data(), count, op); break;
+        case ncclInt32: reduce_into(reinterpret_cast<int32_t*>(acc.data()), reinterpret_cast<int32_t*>(tmp.data()), count, op); break;
+        case ncclInt64: reduce_into(reinterpret_cast<int64_t*>(acc.data()), reinterpret_cast<int64_t*>(tmp.data()), count, op); break;
+        case ncclFloat32: reduce_into(reinterpret_cast<float*>(acc.data()), reinterpret_cast<float*>(tmp.data()), count, op); break;
+        case ncclFloat64: reduce_into(reinterpret_cast<double*>(acc.data()), reinterpret_cast<double*>(tmp.data()), count, op); break;
+        default: throw std::invalid_argument("loopback: unsupported dtype");
+      }
+    }
+    for (int r = 0; r < world_; ++r)
+      TWTML_HIP_CHECK(hipMemcpy(bufs_[size_t(r)], acc.data(), bytes, hipMemcpyHostToDevice));
+  });
+}
+
+void LoopbackHub::broadcast(int rank, void* buf, size_t count, ncclDataType_t dt, int root) {
+  const size_t bytes = count * dt_size(dt);
+  arrive_and_wait(rank, buf, [&] {
+    std::vector<unsigned char> acc(bytes);
+    TWTML_HIP_CHECK(hipMemcpy(acc.data(), bufs_[size_t(root)], bytes, hipMemcpyDeviceToHost));
+    for (int r = 0; r < world_; ++r)
+      TWTML_HIP_CHECK(hipMemcpy(bufs_[size_t(r)], acc.data(), bytes, hipMemcpyHostToDevice));
+  });
+}
+
+LoopbackComm::LoopbackComm(std::shared_ptr<LoopbackHub> hub, int rank) : hub_(std::move(hub)) {
+  rank_ = rank;
+  world_ = hub_->world();
+}
+
+void LoopbackComm::allreduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t s) {
+  if (world_ == 1 || count == 0) return;
+  TWTML_HIP_CHECK(hipStreamSynchronize(s));
+  hub_->allreduce(rank_, buf, count, dt, op);
+}
+
+void LoopbackComm::broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t s) {
+  if (world_ == 1 || count == 0) return;
+  TWTML_HIP_CHECK(hipStreamSynchronize(s));
+  hub_->broadcast(rank_, buf, count, dt, root);
 }
 
 }  // namespace twtml

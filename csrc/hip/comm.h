@@ -1,38 +1,87 @@
-// RCCL communicator (one process per GPU; xGMI on an MI355X node).
+// Collective communicators for the engines (one process per GPU).
 //
-// Replaces the reference's Spark treeAggregate/broadcast traffic (SURVEY §2.5
-// CS1-CS10) with device-side collectives issued on the engine's compute
-// stream: the packed [gradient | loss] buffer is all-reduced in place every
-// GD iteration, the batch statistics once per batch.  The communicator is
+// RcclComm replaces the reference's Spark treeAggregate/broadcast traffic
+//  with device-side RCCL collectives issued on the
+// engine's compute stream: the packed [gradient | loss] buffer is all-reduced
+// in place every GD iteration, the batch statistics once per batch.  It is
 // bootstrapped from an ncclUniqueId that rank 0 creates and torch.distributed
 // broadcasts (parallel/dist.py).
+//
+// LoopbackComm is a test double: N engines in ONE process (threads), possibly
+// on the same GPU, reduce through host memory.  RCCL refuses two ranks on one
+// device, so this is how the data-parallel engine path is exercised on a
+// single-GPU machine (tests/test_gpu_dp_loopback.py).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <condition_variable>
+#include <functional>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <vector>
 
 namespace twtml {
 
 class Comm {
  public:
-  Comm(const std::string& unique_id, int rank, int world, int device);
-  ~Comm();
-  Comm(const Comm&) = delete;
-  Comm& operator=(const Comm&) = delete;
-
-  void allreduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t s);
-  void broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t s);
-  void check_async() const;
-  void abort();
-
+  virtual ~Comm() = default;
+  virtual void allreduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t s) = 0;
+  virtual void broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t s) = 0;
+  virtual void check_async() const {}
+  virtual void abort() {}
+  virtual std::string kind() const = 0;
   int rank() const { return rank_; }
   int world() const { return world_; }
 
+ protected:
+  int rank_ = 0, world_ = 1;
+};
+
+class RcclComm final : public Comm {
+ public:
+  RcclComm(const std::string& unique_id, int rank, int world, int device);
+  ~RcclComm() override;
+  RcclComm(const RcclComm&) = delete;
+  RcclComm& operator=(const RcclComm&) = delete;
+  void allreduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t s) override;
+  void broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t s) override;
+  void check_async() const override;
+  void abort() override;
+  std::string kind() const override { return "rccl"; }
+
  private:
   ncclComm_t comm_ = nullptr;
-  int rank_ = 0, world_ = 1;
+};
+
+class LoopbackHub {
+ public:
+  explicit LoopbackHub(int world) : world_(world), bufs_(size_t(world), nullptr) {}
+  // Blocking collective: every rank calls it with its device buffer.
+  void allreduce(int rank, void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op);
+  void broadcast(int rank, void* buf, size_t count, ncclDataType_t dt, int root);
+  int world() const { return world_; }
+
+ private:
+  void arrive_and_wait(int rank, void* buf, const std::function<void()>& leader_work);
+  int world_;
+  std::mutex m_;
+  std::condition_variable cv_;
+  int arrived_ = 0;
+  unsigned long long generation_ = 0;
+  std::vector<void*> bufs_;
+};
+
+class LoopbackComm final : public Comm {
+ public:
+  LoopbackComm(std::shared_ptr<LoopbackHub> hub, int rank);
+  void allreduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t s) override;
+  void broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t s) override;
+  std::string kind() const override { return "loopback"; }
+
+ private:
+  std::shared_ptr<LoopbackHub> hub_;
 };
 
 std::string rccl_unique_id();

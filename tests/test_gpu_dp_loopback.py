@@ -1,0 +1,92 @@
+"""Data-parallel engine path on one GPU via the in-process loopback communicator.
+
+RCCL refuses two ranks on the same device, so the DP orchestration of the
+engine (flag MAX all-reduce for the active-feature union, per-rank kept counts
+and sampling offsets, per-iteration gradient all-reduce, stats all-reduce,
+early exit agreement) is exercised with N engines on N threads of one
+process, reducing through host memory.  DP over shards must equal the
+single-engine run on the concatenated batch.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+from twitter_stream_ml_amd.sources.synthetic import SynthConfig, generate_batch
+
+pytestmark = pytest.mark.gpu
+NOW = 1_700_000_000_000
+
+
+def _cfg(F, **kw):
+    from twitter_stream_ml_amd.ops.lr_engine import LRDeviceConfig
+    return LRDeviceConfig(num_text_features=F, max_rows=8192, max_units=8192 * 300, **kw)
+
+
+def _run_dp(world, batches, cfg):
+    from twitter_stream_ml_amd.ops._native import hip
+    from twitter_stream_ml_amd.ops.lr_engine import DeviceLinearRegression
+    group = hip().LoopbackGroup(world)
+    engines = [DeviceLinearRegression(cfg, device=0, comm=group.comm(r)) for r in range(world)]
+    results = [[None] * len(batches) for _ in range(world)]
+    errors = []
+
+    def worker(r):
+        try:
+            for t, full in enumerate(batches):
+                results[r][t] = engines[r].train_batch(full.shard(r, world), want_pred=False)
+        except Exception as e:  # pragma: no cover - surfaced below
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=300)
+    assert not errors, errors
+    return engines, results
+
+
+@pytest.mark.parametrize("world,fraction", [(2, 1.0), (3, 1.0), (2, 0.5)])
+def test_dp_equals_single_engine(hip_module, world, fraction):
+    from twitter_stream_ml_amd.ops.lr_engine import DeviceLinearRegression
+    F = 1 << 20
+    cfg = _cfg(F, fraction=fraction, num_iterations=20)
+    synth = SynthConfig.profile("twitter", seed=33, unicode_fraction=0.2)
+    batches = [generate_batch(synth, t * 3000, 3000, batch_time_ms=NOW + t) for t in range(3)]
+    engines, res = _run_dp(world, batches, cfg)
+    single = DeviceLinearRegression(cfg, device=0)
+    for t, full in enumerate(batches):
+        r1 = single.train_batch(full, want_pred=False)
+        for r in range(world):
+            assert res[r][t]["n_kept_global"] == r1["n_kept"]
+            assert res[r][t]["iterations"] == r1["iterations"]
+            np.testing.assert_allclose(res[r][t]["stats"], r1["stats"], rtol=1e-9)
+            np.testing.assert_allclose(res[r][t]["loss_history"], r1["loss_history"], rtol=1e-6)
+    # after the same 3 batches the replicas equal the single-engine model
+    w1 = single.get_weights()
+    scale = max(np.abs(w1).max(), 1e-12)
+    for r in range(world):
+        np.testing.assert_allclose(engines[r].get_weights(), w1, rtol=1e-4, atol=1e-6 * scale)
+    # replicas are bit-identical across ranks
+    for r in range(1, world):
+        np.testing.assert_array_equal(engines[r].get_weights(), engines[0].get_weights())
+
+
+def test_dp_rank_with_no_rows(hip_module):
+    """A rank whose shard is entirely filtered out still joins every collective."""
+    from twitter_stream_ml_amd.ops.lr_engine import DeviceLinearRegression
+    from twitter_stream_ml_amd.records.batch import RawBatch
+    F = 1000
+    cfg = _cfg(F, num_iterations=10)
+    good = generate_batch(SynthConfig.profile("twitter", seed=4), 0, 2000, batch_time_ms=NOW)
+    bad = generate_batch(SynthConfig.profile("twitter", seed=5, retweet_fraction=0.0), 0, 2000,
+                         batch_time_ms=NOW)
+    full = RawBatch.concat([good, bad])  # shard 1 keeps nothing
+    engines, res = _run_dp(2, [full], cfg)
+    assert res[1][0]["n_kept"] == 0 and res[1][0]["n_kept_global"] == res[0][0]["n_kept"]
+    single = DeviceLinearRegression(cfg, device=0)
+    r1 = single.train_batch(full)
+    assert res[0][0]["iterations"] == r1["iterations"]
+    np.testing.assert_allclose(engines[1].get_weights(), single.get_weights(), rtol=1e-4,
+                               atol=1e-9)
