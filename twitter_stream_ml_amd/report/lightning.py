@@ -1,0 +1,113 @@
+"""REST client for a Lightning visualization server.
+
+Re-implements the slice of the vendored ``lightning-scala`` jar the reference
+uses (``SessionStats.scala:11,31-33,49-52``; endpoints inferred from the jar's
+constant pool):
+
+* ``POST {host}/sessions/`` ``{"name": ...}`` -> ``{"id": ...}`` (createSession;
+  done lazily on first plot, the jar's ``checkSession``)
+* ``POST {host}/sessions/{s}/visualizations/`` ``{"type": "line-streaming",
+  "data": {...}}`` -> ``{"id": ...}``
+* ``POST {host}/sessions/{s}/visualizations/{id}/data/`` ``{"data": {...}}``
+  (append to a streaming viz)
+* embed URL ``{host}/visualizations/{id}/pym``
+
+Optional HTTP basic auth as in the jar.  Default host ``http://localhost:3000``.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Any, Dict, List, Optional, Sequence
+
+import requests
+
+__all__ = ["Lightning", "Visualization", "LightningError"]
+
+
+class LightningError(RuntimeError):
+    pass
+
+
+@dataclass
+class Visualization:
+    lgn: "Lightning"
+    id: str
+    type: str = "line-streaming"
+
+    def append(self, data: Dict[str, Any]) -> Dict[str, Any]:
+        return self.lgn._post(f"/sessions/{self.lgn.session}/visualizations/{self.id}/data/",
+                              {"data": data})
+
+    def get_pym_link(self) -> str:
+        return f"{self.lgn.host}/visualizations/{self.id}/pym"
+
+    getPymLink = get_pym_link
+
+
+class Lightning:
+    def __init__(self, host: str = "http://localhost:3000", auth: Optional[tuple] = None,
+                 timeout: float = 5.0):
+        self.host = (host or "http://localhost:3000").rstrip("/")
+        self.auth = auth
+        self.timeout = timeout
+        self.session: str = ""
+        self._http = requests.Session()
+
+    # ------------------------------------------------------------------
+    def _post(self, path: str, payload: Dict[str, Any]) -> Dict[str, Any]:
+        try:
+            r = self._http.post(self.host + path, json=payload, auth=self.auth, timeout=self.timeout)
+        except requests.RequestException as e:
+            raise LightningError(f"lightning unreachable at {self.host}: {e}") from e
+        if r.status_code >= 400:
+            raise LightningError(f"lightning {path}: HTTP {r.status_code} {r.text[:200]}")
+        try:
+            return r.json()
+        except ValueError:
+            return {}
+
+    def create_session(self, name: str = "") -> str:
+        body = {"name": name} if name else {}
+        res = self._post("/sessions/", body)
+        self.session = str(res.get("id", ""))
+        if not self.session:
+            raise LightningError("lightning did not return a session id")
+        return self.session
+
+    createSession = create_session
+
+    def check_session(self) -> None:
+        if not self.session:
+            self.create_session()
+
+    def plot(self, type: str, data: Dict[str, Any]) -> Visualization:
+        self.check_session()
+        res = self._post(f"/sessions/{self.session}/visualizations/", {"type": type, "data": data})
+        vid = res.get("id")
+        if vid is None:
+            raise LightningError("lightning did not return a visualization id")
+        return Visualization(self, str(vid), type)
+
+    def line_streaming(self, series: Sequence[Sequence[float]], size: Sequence[float] = (),
+                       color: Sequence[Sequence[float]] = (), alpha: Sequence[float] = (),
+                       label: Sequence[int] = (), xaxis: str = "", yaxis: str = "",
+                       viz: Optional[Visualization] = None):
+        data: Dict[str, Any] = {"series": [list(map(float, s)) for s in series]}
+        if size:
+            data["size"] = list(size)
+        if color:
+            data["color"] = [list(c) for c in color]
+        if alpha:
+            data["alpha"] = list(alpha)
+        if label:
+            data["label"] = list(label)
+        if xaxis:
+            data["xaxis"] = xaxis
+        if yaxis:
+            data["yaxis"] = yaxis
+        if viz is None:
+            return self.plot("line-streaming", data)
+        viz.append(data)
+        return viz
+
+    lineStreaming = line_streaming
