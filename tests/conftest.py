@@ -10,8 +10,9 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-if ROOT not in sys.path:
-    sys.path.insert(0, ROOT)
+for _p in (ROOT, os.path.join(ROOT, "tests")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
 os.environ.setdefault("TWTML_CONFIG_PATH", os.path.join(ROOT, "tests", "resources"))
 
 

@@ -1,0 +1,84 @@
+"""End-to-end driver runs on the CPU engine (local[N]) with real report sinks.
+
+The reference has no driver tests; these run the LinearRegression
+and KMeans jobs for a few micro-batches against the in-process twtml-web
+server and a fake Lightning server, and check what reaches both.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from twitter_stream_ml_amd.apps import kmeans as km_app
+from twitter_stream_ml_amd.apps import linear_regression as lr_app
+from twitter_stream_ml_amd.checkpoint import load_kmeans, load_linear_regression
+from twitter_stream_ml_amd.report.api_types import Stats
+from twitter_stream_ml_amd.report.webclient import WebClient
+from twitter_stream_ml_amd.web.main import build_server
+
+from fakes import FakeLightning
+
+
+@pytest.fixture()
+def sinks(tmp_path):
+    lgn = FakeLightning().start()
+    web = build_server(["-nocache"], port=0, host="127.0.0.1",
+                       backup_file=str(tmp_path / "w.json")).start()
+    yield lgn, web
+    web.stop()
+    lgn.stop()
+
+
+def test_linear_regression_driver_cpu(sinks, tmp_path, monkeypatch):
+    lgn, web = sinks
+    metrics = tmp_path / "m.jsonl"
+    monkeypatch.setenv("TWTML_METRICS", str(metrics))
+    ck = tmp_path / "model"
+    rc = lr_app.main(["--master", "local[2]", "--lightning", lgn.url, "--twtweb", web.url,
+                      "--seconds", "0.3", "--sourceRate", "4000", "--numBatches", "3",
+                      "-f", "1000", "--checkpoint", str(ck), "--checkpointInterval", "2"])
+    assert rc == 0
+    recs = [json.loads(l) for l in open(metrics)]
+    assert len(recs) == 3 and all(r["batch"] > 0 for r in recs)
+    assert recs[-1]["count"] == sum(r["batch"] for r in recs)
+    # twtml-web got Config (viz from Lightning) and the last batch's Stats
+    cfg = WebClient(web.url).config()
+    assert cfg.host == lgn.url and len(cfg.viz) == 1
+    st = WebClient(web.url).stats()
+    assert st.count == recs[-1]["count"] and st.batch == recs[-1]["batch"]
+    assert st.mse == int(recs[-1]["mse"])
+    # Lightning: session + viz creation + one append per batch (4 series)
+    appends = lgn.appends()
+    assert len(appends) == 3 and len(appends[0]["data"]["series"]) == 4
+    w, b = load_linear_regression(str(ck))
+    assert w.shape == (1004,) and b == 0.0 and np.abs(w).max() > 0
+
+
+def test_linear_regression_driver_resume_and_dead_sinks(tmp_path, monkeypatch):
+    metrics = tmp_path / "m.jsonl"
+    monkeypatch.setenv("TWTML_METRICS", str(metrics))
+    ck = tmp_path / "model"
+    args = ["--master", "local[1]", "--lightning", "http://127.0.0.1:9",
+            "--twtweb", "http://127.0.0.1:9", "--seconds", "0.2", "--sourceRate", "3000",
+            "--numBatches", "2", "--checkpoint", str(ck)]
+    assert lr_app.main(args) == 0            # unreachable report servers never stop training
+    w1, _ = load_linear_regression(str(ck))
+    assert lr_app.main(args + ["--resume", str(ck)]) == 0
+    w2, _ = load_linear_regression(str(ck))
+    assert not np.array_equal(w1, w2)
+
+
+def test_kmeans_driver_cpu(sinks, tmp_path, monkeypatch):
+    lgn, web = sinks
+    (tmp_path / "application.conf").write_text(
+        f'lightning="{lgn.url}"\ntwtweb="{web.url}"\n')
+    monkeypatch.setenv("TWTML_CONFIG_PATH", str(tmp_path))
+    ck = tmp_path / "km"
+    rc = km_app.main(["--seconds", "0.3", "--sourceRate", "3000", "--numBatches", "3",
+                      "--checkpoint", str(ck), "--report"])
+    assert rc == 0
+    c, w = load_kmeans(str(ck))
+    assert c.shape == (3, 2) and w is not None and w.sum() > 0
+    assert any(p == "/sessions/" for (_, p, _) in lgn.calls)
+    assert WebClient(web.url).stats().count > 0

@@ -1,0 +1,76 @@
+"""Multi-process data parallelism on CPU (gloo, world_size 2 and 3).
+
+Mirrors what one process per GPU does on an MI355X node (SURVEY §2.4 DP row):
+every rank owns a shard of each micro-batch, the per-iteration gradient (and
+counts/statistics) are all-reduced, and the replicated model must equal the
+single-process model trained on the concatenated batch.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out_dir, fraction):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from twitter_stream_ml_amd.models.kmeans import CpuKMeans, kmeans_features
+    from twitter_stream_ml_amd.models.linear_regression import CpuLinearRegression, CpuLRConfig
+    from twitter_stream_ml_amd.parallel import dist as D
+    from twitter_stream_ml_amd.sources.synthetic import SynthConfig, generate_batch
+    info = D.init_distributed(backend="gloo")
+    red = D.allreduce_fn()
+    cfg = CpuLRConfig(num_text_features=1 << 12, num_iterations=15, fraction=fraction)
+    lr = CpuLinearRegression(cfg, allreduce=red, rank=info.rank, world=info.world)
+    km = CpuKMeans(5, 2, allreduce=red, seed=3)
+    synth = SynthConfig.profile("twitter", seed=17)
+    res = []
+    for t in range(3):
+        full = generate_batch(synth, t * 1500, 1500, batch_time_ms=1_700_000_000_000)
+        shard = full.shard(info.rank, info.world)
+        r = lr.train_batch(shard)
+        X, _ = kmeans_features(shard)
+        km.update_batch(X)
+        res.append((r["iterations"], r["n_kept_global"], r["stats"]))
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), w=lr.get_weights(), c=km.state.centers,
+             cw=km.state.weights, meta=np.array([x[0] for x in res] + [x[1] for x in res]),
+             stats=np.array([x[2] for x in res]))
+    D.barrier()
+    D.shutdown()
+
+
+@pytest.mark.parametrize("world,fraction", [(2, 1.0), (3, 0.7)])
+def test_cpu_dp_equals_single_process(tmp_path, world, fraction):
+    port = _free_port()
+    mp.start_processes(_worker, args=(world, port, str(tmp_path), fraction), nprocs=world,
+                       join=True, start_method="spawn")
+    from twitter_stream_ml_amd.models.kmeans import CpuKMeans, kmeans_features
+    from twitter_stream_ml_amd.models.linear_regression import CpuLinearRegression, CpuLRConfig
+    from twitter_stream_ml_amd.sources.synthetic import SynthConfig, generate_batch
+    lr = CpuLinearRegression(CpuLRConfig(num_text_features=1 << 12, num_iterations=15,
+                                         fraction=fraction))
+    km = CpuKMeans(5, 2, seed=3)
+    synth = SynthConfig.profile("twitter", seed=17)
+    iters, kept, stats = [], [], []
+    for t in range(3):
+        full = generate_batch(synth, t * 1500, 1500, batch_time_ms=1_700_000_000_000)
+        r = lr.train_batch(full)
+        km.update_batch(kmeans_features(full)[0])
+        iters.append(r["iterations"]); kept.append(r["n_kept_global"]); stats.append(r["stats"])
+    for rank in range(world):
+        d = np.load(tmp_path / f"r{rank}.npz")
+        np.testing.assert_array_equal(d["meta"], np.array(iters + kept))
+        np.testing.assert_allclose(d["stats"], np.array(stats), rtol=1e-12)
+        np.testing.assert_allclose(d["w"], lr.get_weights(), rtol=1e-9, atol=1e-15)
+        np.testing.assert_allclose(d["c"], km.state.centers, rtol=1e-9, atol=1e-12)
+        np.testing.assert_allclose(d["cw"], km.state.weights, rtol=1e-12)

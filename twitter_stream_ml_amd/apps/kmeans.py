@@ -1,0 +1,153 @@
+"""twtml-spark KMeans driver (``KMeans.scala:15-170``).
+
+Reference behaviour: streaming k-means with ``k = 3`` on 2-d points
+``[retweetCount, followersCount]`` of every retweet (no range filter),
+``setHalfLife(5, "batches")``, ``setRandomCenters(2, 0.0)``, 5 s batches; per
+non-empty batch ``count += n``, ``StandardScaler(false, true).fit(rdd)
+.transform(rdd)``, ``latestModel.update(scaled, decayFactor, timeUnit)``, then
+collect x/y/centers/predictions and debug-log them.  It creates a Lightning
+session named ``twitter-stream-ml-kmeans`` but plots nothing (all plotting and
+web stats are commented out, ``KMeans.scala:89-131``).
+
+Like the reference it reads ``lightning``/``twtweb`` from ``ConfigFactory.load``
+and ignores the LR flags; extension flags select the engine and the k=1024
+configuration: ``--master``, ``--k``, ``--textDims`` (hashed bigram dims
+appended to the 2 numeric features), ``--seconds``, ``--numBatches``,
+``--source``, ``--sourceRate``, ``--batchSize``, ``--checkpoint``, ``--report``
+(post Stats/plot like the LR job).
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import sys
+from typing import List, Optional
+
+import numpy as np
+
+from ..config.arguments import parse_master
+from ..config.hocon import ConfigFactory, load_java_opts
+from ..models.kmeans import CpuKMeans, StreamingKMeansModel, kmeans_features
+from ..runtime.streaming import StreamingContext
+from ..sources import make_source
+from ..utils.logging import setup_logging
+
+__all__ = ["main", "KMeansJob", "build_kmeans_engine"]
+
+log = logging.getLogger("com.giorgioinf.twtml.spark.KMeans")
+APP_NAME = "twitter-stream-ml-kmeans"
+
+
+def parse_args(argv: List[str]) -> argparse.Namespace:
+    ap = argparse.ArgumentParser(prog="twtml-kmeans")
+    ap.add_argument("--master", "-m", default="local[*]")
+    ap.add_argument("--k", type=int, default=3)
+    ap.add_argument("--textDims", type=int, default=0)
+    ap.add_argument("--halfLife", type=float, default=5.0)
+    ap.add_argument("--seconds", type=float, default=5.0)
+    ap.add_argument("--numBatches", type=int, default=0)
+    ap.add_argument("--batchSize", type=int, default=0)
+    ap.add_argument("--source", default="synthetic")
+    ap.add_argument("--sourceRate", type=float, default=50.0)
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--checkpoint", default="")
+    ap.add_argument("--report", action="store_true")
+    return ap.parse_args(argv)
+
+
+def build_kmeans_engine(args, dim: int, rank: int, world: int):
+    spec = parse_master(args.master)
+    if spec.is_gpu:
+        from ..ops.kmeans_engine import DeviceKMeans, KMDeviceConfig
+        from ..parallel.dist import make_rccl_comm
+        dev = spec.devices[rank] if spec.devices else rank
+        rows = max(65536, args.batchSize)
+        cfg = KMDeviceConfig(k=args.k, text_dims=args.textDims, half_life=args.halfLife,
+                             max_rows=rows, max_units=rows * 290, seed=args.seed)
+        return DeviceKMeans(cfg, device=dev, comm=make_rccl_comm(dev) if world > 1 else None)
+    from ..parallel.dist import allreduce_fn
+    return CpuKMeans(args.k, dim, half_life=args.halfLife, init_weight=0.0, seed=args.seed,
+                     allreduce=allreduce_fn())
+
+
+class KMeansJob:
+    def __init__(self, engine, text_dims: int = 0, session=None, rank: int = 0):
+        self.engine = engine
+        self.text_dims = text_dims
+        self.session = session
+        self.rank = rank
+        self.count = 0
+        self.batches = 0
+        self.last = None
+
+    def on_batch(self, rdd, time_ms: int) -> None:
+        raw = rdd.raw
+        if hasattr(self.engine, "update_raw"):
+            res = self.engine.update_raw(raw)                 # fused device pipeline
+        else:
+            X, _ = kmeans_features(raw, self.text_dims)
+            res = self.engine.update_batch(X)
+        self.last = res
+        if res["n"] == 0:
+            return
+        self.batches += 1
+        self.count += res["n"]
+        centers, weights = self.engine.get_state()
+        if log.isEnabledFor(logging.DEBUG):
+            scaled = res.get("scaled")
+            log.debug("\n\tmodelx: %s\n\tmodely: %s\n\tdatax: %s\n\tdatay: %s\n\tpred: %s",
+                      centers[:, 0].tolist(), centers[:, 1].tolist(),
+                      [] if scaled is None else scaled[:20, 0].tolist(),
+                      [] if scaled is None else scaled[:20, 1].tolist(),
+                      np.asarray(res.get("pred", []))[:20].tolist())
+        if self.session is not None and self.rank == 0:
+            self.session.web_stats_only(self.count, res["n"])
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    setup_logging()
+    rest = load_java_opts(list(sys.argv[1:] if argv is None else argv))
+    args = parse_args(rest)
+    log.info("Loading application config...")
+    conf = ConfigFactory.load()
+    lgn_host = conf.getString("lightning")
+    web_host = conf.getString("twtweb")
+    from ..parallel.dist import init_distributed
+    info = init_distributed(backend="nccl" if parse_master(args.master).is_gpu else "gloo")
+    dim = 2 + args.textDims
+    log.info("Initializing Streaming Spark Context...")
+    ssc = StreamingContext(args.seconds, batch_size=args.batchSize, num_batches=args.numBatches,
+                           app_name=APP_NAME)
+    log.info("Initializing Twitter stream...")
+    engine = build_kmeans_engine(args, dim, info.rank, info.world)
+    stream = ssc.twitterStream(make_source(args.source, rate=args.sourceRate, seed=args.seed,
+                                           shard=info.rank, num_shards=info.world))
+    session = None
+    if info.rank == 0:
+        log.info("Initializing Lightning graph session...")
+        from ..report.lightning import Lightning, LightningError
+        try:
+            Lightning(lgn_host).create_session(APP_NAME)
+        except LightningError as e:
+            log.warning("lightning unavailable: %s", e)
+        if args.report:
+            from ..report.session_stats import SessionStats
+            session = SessionStats(lgn_host, web_host).open()
+    job = KMeansJob(engine, args.textDims, session, info.rank)
+    stream.foreachRDD(job.on_batch)
+    log.info("Initialization complete.")
+    ssc.start()
+    try:
+        ssc.awaitTermination()
+    except KeyboardInterrupt:
+        pass
+    finally:
+        ssc.stop()
+        if args.checkpoint and info.rank == 0:
+            c, w = engine.get_state()
+            StreamingKMeansModel(c, w).save(args.checkpoint)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

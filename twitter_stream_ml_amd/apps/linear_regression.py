@@ -1,0 +1,191 @@
+"""twtml-spark LinearRegression driver (``LinearRegression.scala:10-94``).
+
+Flow kept from the reference:
+
+1. parse ``ConfArguments`` (app name ``twitter-stream-ml-linear-regression``);
+2. open the report session (Lightning plot + twtml-web Config);
+3. ``MllibHelper.reset(conf)``; model with ``numIterations``/``stepSize``/
+   ``miniBatchFraction`` and zero initial weights of size ``F + 4``;
+4. streaming context with ``seconds`` batches over the tweet source, stream
+   ``filter(filtrate).map(featurize).cache()``;
+5. per batch, output op #1: prequential predict with the current model,
+   ``count``/``batch``/``stdev``/``mse`` (rounded with ``Utils.round``),
+   debug logs, ``session.update``; output op #2: ``model.trainOn(stream)``;
+6. start and block.
+
+Engines: ``--master local[N]`` runs the fp64 CPU engine; ``--master rocm...``
+the MI355X engine, which executes filter, featurize, op #1 and op #2 of a
+batch in one fused device pipeline — op #1 still sees the weights of batch
+t-1 (the stats come out of GD iteration 1, computed before any update).
+Data parallel runs start one process per GPU (``torch.distributed.run``);
+every rank reads its own shard of the stream and rank 0 reports.
+
+Extensions (long flags only): ``--source``, ``--batchSize``, ``--numBatches``,
+``--hash``, ``--checkpoint``/``--checkpointInterval``, ``--resume``,
+``--plotPoints``, ``--metrics FILE`` (via env ``TWTML_METRICS``).
+"""
+from __future__ import annotations
+
+import logging
+import math
+import os
+import sys
+from typing import List, Optional
+
+import numpy as np
+
+from ..config.arguments import ConfArguments
+from ..config.hocon import load_java_opts
+from ..models.linear_regression import CpuLinearRegression, CpuLRConfig, LinearRegressionModel
+from ..models.mllib_helper import MllibHelper
+from ..oracle.mllib import round_half_up
+from ..records.batch import RETWEET_COUNT
+from ..report.session_stats import SessionStats
+from ..runtime.streaming import StreamingContext
+from ..sources import make_source
+from ..utils.logging import setup_logging
+from ..utils.metrics import MetricsLogger
+
+__all__ = ["main", "build_engine", "LinearRegressionJob"]
+
+log = logging.getLogger("com.giorgioinf.twtml.spark.LinearRegression")
+APP_NAME = "twitter-stream-ml-linear-regression"
+
+
+def build_engine(conf: ConfArguments, rank: int, world: int, device: Optional[int] = None,
+                 max_rows: int = 0):
+    """CPU (local[N]) or MI355X (rocm...) engine for this process."""
+    spec = conf.master_spec()
+    F = conf.effectiveNumTextFeatures
+    if spec.is_gpu:
+        from ..ops.lr_engine import DeviceLinearRegression, LRDeviceConfig
+        from ..parallel.dist import make_rccl_comm
+        dev = device if device is not None else (spec.devices[rank] if spec.devices else rank)
+        rows = max_rows or max(65536, int(conf.batchSize or 0))
+        cfg = LRDeviceConfig(num_text_features=F, hash=conf.hash, step_size=conf.stepSize,
+                             num_iterations=conf.numIterations, fraction=conf.miniBatchFraction,
+                             begin=conf.numRetweetBegin, end=conf.numRetweetEnd,
+                             max_rows=rows, max_units=rows * 290)
+        return DeviceLinearRegression(cfg, device=dev, comm=make_rccl_comm(dev) if world > 1 else None)
+    from ..parallel.dist import allreduce_fn
+    cfg = CpuLRConfig(num_text_features=F, hash=conf.hash, step_size=conf.stepSize,
+                      num_iterations=conf.numIterations, fraction=conf.miniBatchFraction,
+                      begin=conf.numRetweetBegin, end=conf.numRetweetEnd)
+    return CpuLinearRegression(cfg, allreduce=allreduce_fn(), rank=rank, world=world)
+
+
+class LinearRegressionJob:
+    """The driver's per-batch logic, reusable from tests and the CLI."""
+
+    def __init__(self, conf: ConfArguments, engine, session: Optional[SessionStats] = None,
+                 rank: int = 0, metrics: Optional[MetricsLogger] = None):
+        self.conf = conf
+        self.engine = engine
+        self.session = session
+        self.rank = rank
+        self.count = 0                 # the "count" accumulator
+        self.batches = 0
+        self.metrics = metrics or MetricsLogger(None)
+        self.last = None
+
+    def on_batch(self, rdd, time_ms: int) -> None:
+        raw = rdd.raw
+        res = self.engine.train_batch(raw, want_pred=True)     # op #1 then op #2
+        self.last = res
+        self.batches += 1
+        batch = int(res["n_kept_global"])
+        if batch == 0:
+            log.debug("batch: 0")
+            self.metrics.log(batch_time_ms=time_ms, raw=raw.n, batch=0)
+            return
+        self.count += batch
+        n, sy, sy2, sp, sp2, se2 = res["stats"]
+        my, mp = sy / n, sp / n
+        try:
+            real_sd = round_half_up(math.sqrt(max(sy2 / n - my * my, 0.0)))
+            pred_sd = round_half_up(math.sqrt(max(sp2 / n - mp * mp, 0.0)))
+            mse = round_half_up(se2 / n)
+        except ValueError as e:  # Utils.round on NaN/Inf: the model diverged
+            log.error("batch %d: model diverged (%s); skipping report", self.batches, e)
+            return
+        mask = self._kept_mask(raw)
+        real = raw.scalars[RETWEET_COUNT][mask].astype(np.float64)
+        pred = np.asarray(res["pred"], np.float64) if res.get("pred") is not None else np.zeros(0)
+        if log.isEnabledFor(logging.DEBUG):
+            log.debug("count: %d", self.count)
+            log.debug("batch: %d,  mse: %d", batch, int(mse))
+            log.debug("stdev (real, pred): (%d, %d)", int(real_sd), int(pred_sd))
+            log.debug("value (real, pred): %s ...",
+                      [(float(a), float(b)) for a, b in zip(real[:10], pred[:10])])
+        self.metrics.log(batch_time_ms=time_ms, raw=raw.n, batch=batch, count=self.count,
+                         mse=mse, realStdev=real_sd, predStdev=pred_sd,
+                         iterations=res["iterations"], converged=bool(res["converged"]),
+                         prep_ms=res.get("prep_ms", 0.0), train_ms=res.get("train_ms", 0.0))
+        if self.session is not None and self.rank == 0:
+            self.session.update(self.count, batch, mse, real_sd, pred_sd, real, pred)
+        self._maybe_checkpoint()
+
+    def _kept_mask(self, raw):
+        rc = raw.scalars[RETWEET_COUNT]
+        return (raw.is_retweet != 0) & (rc >= self.conf.numRetweetBegin) & (rc <= self.conf.numRetweetEnd)
+
+    def _maybe_checkpoint(self, force: bool = False) -> None:
+        c = self.conf
+        if self.rank != 0 or not c.checkpoint:
+            return
+        if force or (c.checkpointInterval > 0 and self.batches % c.checkpointInterval == 0):
+            LinearRegressionModel(self.engine.get_weights(), 0.0).save(c.checkpoint)
+            log.info("checkpoint written to %s after %d batches", c.checkpoint, self.batches)
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    setup_logging()
+    args = load_java_opts(list(sys.argv[1:] if argv is None else argv))
+    log.info("Parsing applications arguments")
+    conf = ConfArguments().setAppName(APP_NAME).parse(args)
+
+    from ..parallel.dist import init_distributed
+    spec = conf.master_spec()
+    info = init_distributed(backend="nccl" if spec.is_gpu else "gloo")
+    rank, world = info.rank, info.world
+
+    session = None
+    if rank == 0:
+        log.info("Initializing session stats...")
+        session = SessionStats.from_conf(conf).open()
+
+    log.info("Initializing Spark Machine Learning Model...")
+    MllibHelper.reset(conf)
+    engine = build_engine(conf, rank, world)
+    w0 = np.zeros(engine.num_weights)                      # Vectors.zeros(numFeatures)
+    if conf.resume:
+        w0 = LinearRegressionModel.load(conf.resume).weights
+        log.info("resumed %d weights from %s", w0.shape[0], conf.resume)
+    engine.set_weights(w0)
+
+    log.info("Initializing Streaming Spark Context... %s sec/batch", conf.seconds)
+    ssc = StreamingContext(conf.seconds, batch_size=conf.batchSize, num_batches=conf.numBatches,
+                           app_name=conf.appName())
+    log.info("Initializing Twitter stream...")
+    stream = ssc.twitterStream(make_source(conf.source, rate=conf.sourceRate, seed=conf.seed,
+                                           shard=rank, num_shards=world)).cache()
+    job = LinearRegressionJob(conf, engine, session, rank,
+                              MetricsLogger(os.environ.get("TWTML_METRICS")))
+    log.info("Initializing prediction model...")
+    stream.foreachRDD(job.on_batch)   # op #1 (stats) + op #2 (trainOn), prequential order
+    ssc.start()
+    log.info("Initialization complete.")
+    try:
+        ssc.awaitTermination()
+    except KeyboardInterrupt:
+        pass
+    finally:
+        ssc.stop()
+        job._maybe_checkpoint(force=bool(conf.checkpoint))
+        if session is not None:
+            session.close()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -294,7 +294,13 @@ Usage: twtml-spark [options]
             set_property("twitter4j.oauth." + attr, value)
         elif attr in ("lightning", "twtweb"):
             setattr(self, attr, value)
-        elif attr in ("seconds", "numIterations", "numRetweetBegin", "numRetweetEnd",
+        elif attr == "seconds":
+            # extension: sub-second intervals ("0.5"); integers parse as in Scala
+            v = _java_int(value) if value.strip().lstrip("+-").isdigit() else float(value)
+            if v <= 0:
+                raise ValueError(value)
+            self.seconds = v
+        elif attr in ("numIterations", "numRetweetBegin", "numRetweetEnd",
                       "numTextFeatures"):
             setattr(self, attr, _java_int(value))
         elif attr in ("stepSize", "miniBatchFraction"):

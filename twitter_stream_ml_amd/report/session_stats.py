@@ -104,6 +104,18 @@ class SessionStats:
                 pass
             self._q.put_nowait(push)
 
+    def web_stats_only(self, count: int, batch: int) -> None:
+        """``Try(web.stats(count))`` of the k-means job (commented out in the
+        reference at ``KMeans.scala:116``; enabled with ``--report``)."""
+        job = lambda: self._try(lambda: self.web.stats(int(count), int(batch), 0, 0, 0))  # noqa: E731
+        if self._async:
+            try:
+                self._q.put_nowait(job)
+            except queue.Full:
+                pass
+        else:
+            job()
+
     def _series(self, batch: int, real_sd: float, pred_sd: float, real, pred) -> List[List[float]]:
         real = np.asarray(real, dtype=np.float64)
         pred = np.asarray(pred, dtype=np.float64)

@@ -1,1 +1,21 @@
-"""sources"""
+"""Tweet sources: synthetic (seeded C++ generator), JSONL replay, live Twitter stub."""
+from .replay import JsonlReplaySource, write_jsonl
+from .synthetic import SynthConfig, SyntheticTweetSource, generate_batch, generate_into
+from .twitter import TwitterSource, TwitterUnavailable
+
+__all__ = ["JsonlReplaySource", "write_jsonl", "SynthConfig", "SyntheticTweetSource",
+           "generate_batch", "generate_into", "TwitterSource", "TwitterUnavailable",
+           "make_source"]
+
+
+def make_source(spec: str, rate: float = 0.0, seed: int = 1, profile: str = "twitter",
+                shard: int = 0, num_shards: int = 1):
+    """``--source`` value -> source object."""
+    if spec in ("", "synthetic"):
+        return SyntheticTweetSource(SynthConfig.profile(profile, seed=seed), rate=rate,
+                                    shard=shard, num_shards=num_shards)
+    if spec.startswith("replay:"):
+        return JsonlReplaySource(spec[len("replay:"):], rate=rate)
+    if spec == "twitter":
+        return TwitterSource()
+    raise ValueError(f"unknown source {spec!r}")
