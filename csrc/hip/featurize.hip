@@ -58,6 +58,10 @@ static void scan_excl(const int64_t* in, int64_t* out, int64_t n, int64_t* total
   hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, s, in, out, n, total);
 }
 
+void scan_excl_launch(const int64_t* in, int64_t* out, int64_t n, int64_t* total, hipStream_t s) {
+  scan_excl(in, out, n, total, s);
+}
+
 __device__ __forceinline__ int len_key(int32_t n32) {
   return kLenBuckets - 1 - (n32 < kLenBuckets - 1 ? n32 : kLenBuckets - 1);
 }
@@ -152,6 +156,17 @@ void launch_filter_sort(const DevRawBatch& b, const DevPrepared& p, const Featur
   const int g = nb < 4096 ? nb : 4096;
   hipLaunchKernelGGL(k_sort_scatter, dim3(g), dim3(kBlock), 0, s, p.nnz, p.counters, p.hist,
                      p.sorted, p.cap_rows);
+}
+
+// Filter + order-preserving compaction only (k-means: no length sort needed).
+void launch_filter_only(const DevRawBatch& b, const DevPrepared& p, const FeaturizeParams& fp,
+                        hipStream_t s) {
+  const int nb = ceil_div(b.n > 0 ? b.n : 1, kBlock);
+  TWTML_HIP_CHECK(hipMemsetAsync(p.hist, 0, sizeof(int64_t) * (kLenBuckets + 1), s));
+  hipLaunchKernelGGL(k_filter_count, dim3(nb), dim3(kBlock), 0, s, b, fp, p.blk);
+  scan_excl(p.blk, p.blk, nb, &p.counters[0], s);
+  hipLaunchKernelGGL(k_filter_write, dim3(nb), dim3(kBlock), 0, s, b, fp, p.blk, p.kept, p.nnz,
+                     p.hist);
 }
 
 // ---------------------------------------------------------------------------

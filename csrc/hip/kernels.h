@@ -110,25 +110,6 @@ void launch_scatter_w(const DevSgd& d, const DevPrepared& p, hipStream_t s);
 int sgd_lds_rep(int64_t ns);
 int sgd_iter_grid(int64_t ns, int64_t n_kept, int num_cu);
 
-// ---------------------------------------------------------------------------
-// K-means (kmeans.hip)
-struct DevKMeans {
-  const float* x;       // [n][d] points (row-major, fp32)
-  int64_t n;
-  int32_t d, k;
-  float* centers;       // [k][d] fp32 (copy of fp64 master for the distance GEMM)
-  float* cnorm;         // [k]
-  int32_t* labels;      // [n]
-  double* sums;         // [k][d] + counts [k]  (fp64 accumulators)
-  double* moments;      // [2*d+1] scaler moments
-};
-// (k-means launchers are declared by kmeans.hip)
-void launch_scaler_sum(const float* x, int64_t n, int d, double* out_sum, hipStream_t s);
-void launch_scaler_m2(const float* x, int64_t n, int d, const double* sum_n, double* out_m2,
-                      hipStream_t s);
-void launch_scale(float* x, int64_t n, int d, const double* factor, hipStream_t s);
-void launch_center_norms(const float* c, int k, int d, float* cnorm, hipStream_t s);
-void launch_assign(const DevKMeans& km, bool use_mfma, hipStream_t s);
-void launch_cluster_sums(const DevKMeans& km, hipStream_t s);
+// (k-means launchers: kmeans_kernels.h)
 
 }  // namespace twtml

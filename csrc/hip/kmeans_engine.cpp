@@ -1,5 +1,262 @@
+// KMEngine: the streaming k-means micro-batch pipeline (see kmeans.hip).
 #include "kmeans_engine.h"
 
+#include <pybind11/numpy.h>
+#include <pybind11/stl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+
+#include "kmeans_kernels.h"
+
+namespace py = pybind11;
+
 namespace twtml {
-void bind_kmeans(pybind11::module_& m) { (void)m; }
+
+template <typename T>
+static T* km_alloc(size_t n) {
+  void* p = nullptr;
+  TWTML_HIP_CHECK(hipMalloc(&p, std::max<size_t>(1, n) * sizeof(T)));
+  return static_cast<T*>(p);
+}
+
+static int pad_dim(int d) {
+  for (int p : {2, 4, 8, 16, 32, 64, 128})
+    if (d <= p) return p;
+  return d;
+}
+
+KMEngine::KMEngine(int device, const KMConfig& cfg, std::shared_ptr<Comm> comm)
+    : device_(device), cfg_(cfg), comm_(std::move(comm)) {
+  if (cfg_.k < 1) throw std::invalid_argument("k must be >= 1");
+  // the feature kernel keeps a per-wave bigram histogram in LDS (4 waves x 4 B)
+  if (cfg_.text_dims < 0 || cfg_.text_dims > 4000)
+    throw std::invalid_argument("text_dims must be in [0, 4000]");
+  if (cfg_.max_rows <= 0 || cfg_.max_rows >= (int64_t(1) << 31)) throw std::invalid_argument("bad max_rows");
+  d_ = 2 + cfg_.text_dims;
+  dp_ = pad_dim(d_);
+  TWTML_HIP_CHECK(hipSetDevice(device_));
+  TWTML_HIP_CHECK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
+  TWTML_HIP_CHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
+  for (auto& s : slots_) {
+    s.text = km_alloc<uint16_t>(size_t(cfg_.max_units) + 8);
+    s.offsets = km_alloc<int64_t>(size_t(cfg_.max_rows) + 1);
+    s.is_rt = km_alloc<uint8_t>(size_t(cfg_.max_rows));
+    s.scalars = km_alloc<int64_t>(5 * size_t(cfg_.max_rows));
+    TWTML_HIP_CHECK(hipEventCreateWithFlags(&s.h2d_done, hipEventDisableTiming));
+    TWTML_HIP_CHECK(hipEventCreateWithFlags(&s.consumed, hipEventDisableTiming));
+  }
+  const int64_t R = cfg_.max_rows;
+  prep_.cap_rows = R;
+  prep_.kept = km_alloc<int64_t>(size_t(R));
+  prep_.nnz = km_alloc<int32_t>(size_t(R));
+  prep_.blk = km_alloc<int64_t>(size_t(R / kBlock + 2));
+  prep_.hist = km_alloc<int64_t>(kLenBuckets + 1);
+  prep_.counters = km_alloc<int64_t>(8);
+  X_ = km_alloc<float>(size_t(R) * size_t(dp_));
+  const size_t k = size_t(cfg_.k), d = size_t(d_);
+  centers_ = km_alloc<double>(k * d);
+  weights_ = km_alloc<double>(k);
+  sums_ = km_alloc<double>(k * d + k);
+  mom_ = km_alloc<double>(2 * d + 2);
+  stdv_ = km_alloc<double>(d);
+  c32_ = km_alloc<float>(k * size_t(dp_));
+  cnorm_ = km_alloc<float>(k);
+  labels_ = km_alloc<int32_t>(size_t(R));
+  order_ = km_alloc<int32_t>(size_t(R));
+  lhist_ = km_alloc<int64_t>(k + 1);
+  TWTML_HIP_CHECK(hipMemset(centers_, 0, sizeof(double) * k * d));
+  TWTML_HIP_CHECK(hipMemset(weights_, 0, sizeof(double) * k));
+  upload_lower_tables(compute_, &lower_page_, &lower_blocks_);
+  TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_out_), sizeof(double) * (4 + d),
+                                hipHostMallocDefault));
+  TWTML_HIP_CHECK(hipEventCreate(&ev0_));
+  TWTML_HIP_CHECK(hipEventCreate(&ev1_));
+  launch_km_centers32(centers_, cfg_.k, d_, dp_, c32_, cnorm_, compute_);
+  TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
+}
+
+KMEngine::~KMEngine() {
+  (void)hipSetDevice(device_);
+  (void)hipDeviceSynchronize();
+  for (auto& s : slots_) {
+    (void)hipFree(s.text); (void)hipFree(s.offsets); (void)hipFree(s.is_rt); (void)hipFree(s.scalars);
+    (void)hipEventDestroy(s.h2d_done); (void)hipEventDestroy(s.consumed);
+  }
+  void* bufs[] = {prep_.kept, prep_.nnz, prep_.blk, prep_.hist, prep_.counters, X_, centers_,
+                  weights_, sums_, mom_, stdv_, c32_, cnorm_, labels_, order_, lhist_,
+                  lower_page_, lower_blocks_};
+  for (void* b : bufs) if (b) (void)hipFree(b);
+  if (host_out_) (void)hipHostFree(host_out_);
+  (void)hipEventDestroy(ev0_);
+  (void)hipEventDestroy(ev1_);
+  (void)hipStreamDestroy(compute_);
+  (void)hipStreamDestroy(copy_);
+}
+
+void KMEngine::submit(const HostBatch& hb, int64_t n, int64_t units, int slot) {
+  if (slot < 0 || slot > 1) throw std::invalid_argument("slot must be 0 or 1");
+  if (n < 0 || n > cfg_.max_rows || n > hb.max_rows) throw std::invalid_argument("rows exceed capacity");
+  if (units < 0 || units > cfg_.max_units || units > hb.max_units)
+    throw std::invalid_argument("text units exceed capacity");
+  if (n > 0 && hb.offsets[n] != units) throw std::invalid_argument("offsets[n] != units");
+  TWTML_HIP_CHECK(hipSetDevice(device_));
+  Slot& s = slots_[slot];
+  if (s.used) TWTML_HIP_CHECK(hipStreamWaitEvent(copy_, s.consumed, 0));
+  if (units > 0)
+    TWTML_HIP_CHECK(hipMemcpyAsync(s.text, hb.text, sizeof(uint16_t) * size_t(units), hipMemcpyHostToDevice, copy_));
+  TWTML_HIP_CHECK(hipMemcpyAsync(s.offsets, hb.offsets, sizeof(int64_t) * size_t(n + 1), hipMemcpyHostToDevice, copy_));
+  if (n > 0) {
+    TWTML_HIP_CHECK(hipMemcpyAsync(s.is_rt, hb.is_rt, size_t(n), hipMemcpyHostToDevice, copy_));
+    TWTML_HIP_CHECK(hipMemcpyAsync(s.scalars, hb.scalars, sizeof(int64_t) * 5 * size_t(n), hipMemcpyHostToDevice, copy_));
+  }
+  TWTML_HIP_CHECK(hipEventRecord(s.h2d_done, copy_));
+  s.n = n;
+  s.units = units;
+  s.used = true;
+}
+
+KMResult KMEngine::process(int slot, bool want_labels) {
+  if (slot < 0 || slot > 1) throw std::invalid_argument("slot must be 0 or 1");
+  TWTML_HIP_CHECK(hipSetDevice(device_));
+  Slot& sl = slots_[slot];
+  hipStream_t s = compute_;
+  const int world = comm_ ? comm_->world() : 1;
+  const int k = cfg_.k, d = d_;
+  KMResult res;
+  res.n_raw = sl.n;
+  TWTML_HIP_CHECK(hipStreamWaitEvent(s, sl.h2d_done, 0));
+  TWTML_HIP_CHECK(hipEventRecord(ev0_, s));
+  DevRawBatch b{sl.text, sl.offsets, sl.is_rt, sl.scalars, sl.n, sl.units};
+  FeaturizeParams fp{1, 0, 1, 0, 0, 0, 0};   // filter: isRetweet only (KMeans.scala:77-80)
+  TWTML_HIP_CHECK(hipMemsetAsync(prep_.counters, 0, 8 * sizeof(int64_t), s));
+  launch_filter_only(b, prep_, fp, s);
+  launch_km_features(b, prep_.kept, prep_.counters, X_, dp_, cfg_.text_dims, lower_page_,
+                     lower_blocks_, cfg_.max_rows, s);
+  TWTML_HIP_CHECK(hipEventRecord(sl.consumed, s));
+  // scaler pass 1: n and column sums (global)
+  TWTML_HIP_CHECK(hipMemsetAsync(mom_, 0, sizeof(double) * size_t(2 * d + 2), s));
+  launch_km_moments(X_, prep_.counters, d, dp_, 0, mom_, mom_, cfg_.max_rows, s);
+  if (world > 1) comm_->allreduce(mom_, size_t(d + 1), ncclFloat64, ncclSum, s);
+  TWTML_HIP_CHECK(hipMemcpyAsync(host_out_, mom_, sizeof(double), hipMemcpyDeviceToHost, s));
+  TWTML_HIP_CHECK(hipMemcpyAsync(host_out_ + 1, prep_.counters, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  TWTML_HIP_CHECK(hipStreamSynchronize(s));
+  res.n_global = int64_t(host_out_[0] + 0.5);
+  int64_t nl;
+  std::memcpy(&nl, host_out_ + 1, sizeof(int64_t));
+  res.n_local = nl;
+  if (res.n_global == 0) {                  // if (rdd.count > 0) { ... }
+    TWTML_HIP_CHECK(hipEventRecord(ev1_, s));
+    TWTML_HIP_CHECK(hipStreamSynchronize(s));
+    return res;
+  }
+  if (cfg_.scale) {
+    launch_km_moments(X_, prep_.counters, d, dp_, 1, mom_, mom_ + d + 1, cfg_.max_rows, s);
+    if (world > 1) comm_->allreduce(mom_ + d + 1, size_t(d), ncclFloat64, ncclSum, s);
+    launch_km_scale(X_, prep_.counters, d, dp_, mom_, mom_ + d + 1, stdv_, cfg_.max_rows, s);
+  }
+  // K8 assignment with the current centres, K9 sums, K10 update.  The
+  // near-tie list reuses order_ (consumed before the label sort) and counter 5.
+  auto* refine_cnt = reinterpret_cast<unsigned long long*>(prep_.counters + 5);
+  launch_km_assign(X_, prep_.counters, c32_, cnorm_, centers_, k, d, dp_, labels_, order_,
+                   refine_cnt, cfg_.max_rows, cfg_.mfma != 0, s);
+  TWTML_HIP_CHECK(hipMemsetAsync(sums_, 0, sizeof(double) * (size_t(k) * d + k), s));
+  launch_km_cluster_sums(X_, labels_, prep_.counters, k, d, dp_, lhist_, order_, sums_,
+                         sums_ + size_t(k) * d, cfg_.max_rows, s, &scan_excl_launch);
+  if (world > 1) comm_->allreduce(sums_, size_t(k) * d + k, ncclFloat64, ncclSum, s);
+  launch_km_update(centers_, weights_, sums_, sums_ + size_t(k) * d, k, d, cfg_.decay,
+                   cfg_.points_unit != 0, c32_, cnorm_, dp_, s);
+  if (want_labels)   // KMeans.scala:113 predicts with the updated model
+    launch_km_assign(X_, prep_.counters, c32_, cnorm_, centers_, k, d, dp_, labels_, order_,
+                     refine_cnt, cfg_.max_rows, cfg_.mfma != 0, s);
+  TWTML_HIP_CHECK(hipEventRecord(ev1_, s));
+  if (cfg_.scale)
+    TWTML_HIP_CHECK(hipMemcpyAsync(host_out_ + 4, stdv_, sizeof(double) * size_t(d), hipMemcpyDeviceToHost, s));
+  if (want_labels && res.n_local > 0) {
+    res.labels.resize(size_t(res.n_local));
+    TWTML_HIP_CHECK(hipMemcpyAsync(res.labels.data(), labels_, sizeof(int32_t) * size_t(res.n_local),
+                                   hipMemcpyDeviceToHost, s));
+  }
+  TWTML_HIP_CHECK(hipStreamSynchronize(s));
+  if (comm_) comm_->check_async();
+  if (cfg_.scale) res.std.assign(host_out_ + 4, host_out_ + 4 + d);
+  TWTML_HIP_CHECK(hipEventElapsedTime(&res.ms, ev0_, ev1_));
+  return res;
+}
+
+void KMEngine::set_state(const double* centers, const double* weights) {
+  TWTML_HIP_CHECK(hipSetDevice(device_));
+  TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
+  TWTML_HIP_CHECK(hipMemcpy(centers_, centers, sizeof(double) * size_t(cfg_.k) * d_, hipMemcpyHostToDevice));
+  TWTML_HIP_CHECK(hipMemcpy(weights_, weights, sizeof(double) * size_t(cfg_.k), hipMemcpyHostToDevice));
+  launch_km_centers32(centers_, cfg_.k, d_, dp_, c32_, cnorm_, compute_);
+  TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
+}
+
+void KMEngine::get_state(double* centers, double* weights) const {
+  TWTML_HIP_CHECK(hipSetDevice(device_));
+  TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
+  TWTML_HIP_CHECK(hipMemcpy(centers, centers_, sizeof(double) * size_t(cfg_.k) * d_, hipMemcpyDeviceToHost));
+  TWTML_HIP_CHECK(hipMemcpy(weights, weights_, sizeof(double) * size_t(cfg_.k), hipMemcpyDeviceToHost));
+}
+
+void KMEngine::synchronize() {
+  TWTML_HIP_CHECK(hipSetDevice(device_));
+  TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
+  TWTML_HIP_CHECK(hipStreamSynchronize(copy_));
+}
+
+// ---------------------------------------------------------------------------
+void bind_kmeans(py::module_& m) {
+  py::class_<KMEngine, std::shared_ptr<KMEngine>>(m, "KMEngine")
+      .def(py::init([](int device, const py::dict& d, std::shared_ptr<Comm> comm) {
+             KMConfig c;
+#define GET(name, type) if (d.contains(#name)) c.name = d[#name].cast<type>();
+             GET(k, int32_t) GET(text_dims, int32_t) GET(decay, double) GET(points_unit, int32_t)
+             GET(scale, int32_t) GET(mfma, int32_t) GET(max_rows, int64_t) GET(max_units, int64_t)
+#undef GET
+             py::gil_scoped_release nogil;
+             return std::make_shared<KMEngine>(device, c, comm);
+           }),
+           py::arg("device"), py::arg("config"), py::arg("comm") = nullptr)
+      .def("submit", [](KMEngine& e, const HostBatch& hb, int64_t n, int64_t units, int slot) {
+        py::gil_scoped_release nogil;
+        e.submit(hb, n, units, slot);
+      })
+      .def("process", [](KMEngine& e, int slot, bool want_labels) {
+        KMResult r;
+        {
+          py::gil_scoped_release nogil;
+          r = e.process(slot, want_labels);
+        }
+        py::dict out;
+        out["n_raw"] = r.n_raw;
+        out["n_local"] = r.n_local;
+        out["n"] = r.n_global;
+        out["std"] = r.std;
+        out["ms"] = r.ms;
+        if (!r.labels.empty())
+          out["pred"] = py::array_t<int32_t>(py::ssize_t(r.labels.size()), r.labels.data());
+        else
+          out["pred"] = py::none();
+        return out;
+      }, py::arg("slot"), py::arg("want_labels") = false)
+      .def("set_state", [](KMEngine& e, py::array_t<double, py::array::c_style | py::array::forcecast> c,
+                           py::array_t<double, py::array::c_style | py::array::forcecast> w) {
+        if (c.size() != py::ssize_t(e.k()) * e.d() || w.size() != e.k())
+          throw std::invalid_argument("state shape mismatch");
+        e.set_state(c.data(), w.data());
+      })
+      .def("get_state", [](const KMEngine& e) {
+        py::array_t<double> c({py::ssize_t(e.k()), py::ssize_t(e.d())});
+        py::array_t<double> w(py::ssize_t(e.k()));
+        e.get_state(c.mutable_data(), w.mutable_data());
+        return py::make_tuple(c, w);
+      })
+      .def("synchronize", &KMEngine::synchronize)
+      .def_property_readonly("k", &KMEngine::k)
+      .def_property_readonly("d", &KMEngine::d);
+}
+
 }  // namespace twtml

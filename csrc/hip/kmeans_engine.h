@@ -1,7 +1,75 @@
-// Streaming k-means engine (K8-K11) -- bindings entry point.
+// Streaming k-means engine (K8-K11) on one GPU, RCCL data parallel.
 #pragma once
+#include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
 
+#include <memory>
+#include <vector>
+
+#include "comm.h"
+#include "common.h"
+#include "engine.h"
+#include "kernels.h"
+
 namespace twtml {
+
+struct KMConfig {
+  int32_t k = 3;
+  int32_t text_dims = 0;       // hashed bigram dims appended to [retweetCount, followers]
+  double decay = 0.8705505632961241;  // setHalfLife(5, "batches")
+  int32_t points_unit = 0;     // timeUnit "points"
+  int32_t scale = 1;           // StandardScaler(false, true) per batch
+  int32_t mfma = 1;            // matrix-core assignment (else scalar fp32)
+  int64_t max_rows = 1 << 16;
+  int64_t max_units = (1 << 16) * 281;
+};
+
+struct KMResult {
+  int64_t n_raw = 0, n_local = 0, n_global = 0;
+  std::vector<double> std;     // scaler std per column
+  std::vector<int32_t> labels; // labels of this rank's points (new model) if requested
+  float ms = 0.f;
+};
+
+class KMEngine {
+ public:
+  KMEngine(int device, const KMConfig& cfg, std::shared_ptr<Comm> comm);
+  ~KMEngine();
+  void submit(const HostBatch& hb, int64_t n, int64_t units, int slot);
+  KMResult process(int slot, bool want_labels);
+  void set_state(const double* centers, const double* weights);
+  void get_state(double* centers, double* weights) const;
+  int k() const { return cfg_.k; }
+  int d() const { return d_; }
+  void synchronize();
+
+ private:
+  int device_;
+  KMConfig cfg_;
+  int d_, dp_;
+  std::shared_ptr<Comm> comm_;
+  hipStream_t compute_ = nullptr, copy_ = nullptr;
+  struct Slot {
+    uint16_t* text = nullptr;
+    int64_t* offsets = nullptr;
+    uint8_t* is_rt = nullptr;
+    int64_t* scalars = nullptr;
+    int64_t n = 0, units = 0;
+    hipEvent_t h2d_done = nullptr, consumed = nullptr;
+    bool used = false;
+  } slots_[2];
+  DevPrepared prep_{};
+  float* X_ = nullptr;
+  double *centers_ = nullptr, *weights_ = nullptr, *sums_ = nullptr, *mom_ = nullptr, *stdv_ = nullptr;
+  float *c32_ = nullptr, *cnorm_ = nullptr;
+  int32_t *labels_ = nullptr, *order_ = nullptr;
+  int64_t* lhist_ = nullptr;
+  uint8_t* lower_page_ = nullptr;
+  uint16_t* lower_blocks_ = nullptr;
+  double* host_out_ = nullptr;
+  hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
+};
+
 void bind_kmeans(pybind11::module_& m);
+
 }  // namespace twtml

@@ -1,0 +1,117 @@
+"""Python face of the MI355X streaming k-means engine (``csrc/hip/kmeans_engine.cpp``).
+
+Per micro-batch, on one GPU (``KMeans.scala:77-115``):
+
+1. filter ``isRetweet`` and build dense features ``[retweetCount, followers,
+   hashed bigram counts...]`` straight from the raw UTF-16 batch;
+2. ``StandardScaler(withMean=false, withStd=true)`` fitted on the batch
+   (two-pass, sample std, all-reduced across ranks);
+3. assignment to the *current* centres on the matrix cores
+   (``mfma_f32_32x32x2f32``: ``-2 x·c + |c|^2``, argmin), per-cluster sums by
+   a counting sort over labels, all-reduced;
+4. the decayed centre/weight update with the dying-cluster split on device;
+5. optional prediction with the *updated* model (``:113``).
+
+The engine matches :class:`~twitter_stream_ml_amd.models.kmeans.CpuKMeans`
+(same random initial centres for the same seed) up to fp32 distance rounding.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from ..oracle.mllib import KMeansState, decay_factor_from_half_life
+from ..records.batch import RawBatch
+from ._native import hip
+from .lr_engine import HostBatchView
+
+__all__ = ["KMDeviceConfig", "DeviceKMeans"]
+
+
+@dataclass
+class KMDeviceConfig:
+    k: int = 3
+    text_dims: int = 0
+    half_life: float = 5.0
+    time_unit: str = "batches"
+    init_weight: float = 0.0
+    scale: bool = True
+    mfma: bool = True
+    max_rows: int = 1 << 16
+    max_units: int = (1 << 16) * 281
+    seed: int = 42
+
+    def as_dict(self) -> Dict[str, object]:
+        if self.time_unit not in ("batches", "points"):
+            raise ValueError(f"Invalid time unit for decay: {self.time_unit}")
+        return {
+            "k": int(self.k),
+            "text_dims": int(self.text_dims),
+            "decay": float(decay_factor_from_half_life(self.half_life)),
+            "points_unit": int(self.time_unit == "points"),
+            "scale": int(bool(self.scale)),
+            "mfma": int(bool(self.mfma)),
+            "max_rows": int(self.max_rows),
+            "max_units": int(self.max_units),
+        }
+
+
+class DeviceKMeans:
+    """StreamingKMeans state + fused batch pipeline on one GPU."""
+
+    def __init__(self, cfg: KMDeviceConfig, device: int = 0, comm=None):
+        self.cfg = cfg
+        self.device = int(device)
+        self.dim = 2 + int(cfg.text_dims)
+        self._eng = hip().KMEngine(self.device, cfg.as_dict(), comm)
+        st = KMeansState.random(cfg.k, self.dim, cfg.init_weight, cfg.seed)
+        self.set_state(st.centers, st.weights)
+        self._staging: List[HostBatchView] = []
+
+    # ---- model state (latestModel.clusterCenters / clusterWeights) -------
+    def get_state(self):
+        c, w = self._eng.get_state()
+        return np.asarray(c), np.asarray(w)
+
+    def set_state(self, centers, weights) -> None:
+        c = np.ascontiguousarray(centers, dtype=np.float64)
+        w = np.ascontiguousarray(weights, dtype=np.float64)
+        if c.shape != (self.cfg.k, self.dim) or w.shape != (self.cfg.k,):
+            raise ValueError(f"expected centers ({self.cfg.k}, {self.dim}) and weights "
+                             f"({self.cfg.k},), got {c.shape} / {w.shape}")
+        self._eng.set_state(c, w)
+
+    @property
+    def state(self) -> KMeansState:
+        c, w = self.get_state()
+        return KMeansState(c, w)
+
+    # ---- pipeline ---------------------------------------------------------
+    def staging(self, i: int = 0) -> HostBatchView:
+        while len(self._staging) <= i:
+            self._staging.append(HostBatchView(self.cfg.max_rows, self.cfg.max_units))
+        return self._staging[i]
+
+    def submit(self, hb: HostBatchView, slot: int) -> None:
+        self._eng.submit(hb._hb, int(hb.n), int(hb.units), int(slot))
+
+    def process(self, slot: int, want_pred: bool = True) -> Dict[str, object]:
+        r = self._eng.process(int(slot), bool(want_pred))
+        if r["std"] is not None and len(r["std"]):
+            r["std"] = np.asarray(r["std"])
+        else:
+            r["std"] = None
+        if want_pred and r["pred"] is None:
+            r["pred"] = np.zeros(0, np.int32)
+        return r
+
+    def update_raw(self, raw: RawBatch, want_pred: bool = True, slot: int = 0) -> Dict[str, object]:
+        """Synchronous path used by the KMeans driver: stage, H2D, process."""
+        hb = self.staging(slot).load(raw)
+        self.submit(hb, slot)
+        return self.process(slot, want_pred)
+
+    def synchronize(self) -> None:
+        self._eng.synchronize()
