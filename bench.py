@@ -34,6 +34,10 @@ BASELINE_TWEETS_PER_SEC = None  # the reference publishes no number (BASELINE.md
 def parse_args(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawTextHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--model", choices=["lr", "kmeans"], default="lr",
+                    help="lr: headline config 2/3/5; kmeans: config 4 (StreamingKMeans)")
+    ap.add_argument("--k", type=int, default=1024, help="kmeans clusters")
+    ap.add_argument("--text-dims", type=int, default=62, help="kmeans hashed bigram dims (+2 numeric)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1_000_000, help="raw tweets per GPU per step")
@@ -77,14 +81,21 @@ def main(argv=None) -> int:
     pool_raw = [prelower(generate_batch(synth, i * B, B, batch_time_ms=now_ms))
                 for i in range(args.pool)]
     max_units = max(r.total_units for r in pool_raw) + 1024
-    cfg = LRDeviceConfig(num_text_features=args.features, hash=args.hash, step_size=args.step_size,
-                         num_iterations=args.iters, fraction=1.0, begin=100, end=1000,
-                         max_rows=B, max_units=max_units, sgd_grid=args.sgd_grid,
-                         ablate=args.ablate)
-    eng = DeviceLinearRegression(cfg, device=device, comm=comm)
+    if args.model == "kmeans":
+        from twitter_stream_ml_amd.ops.kmeans_engine import DeviceKMeans, KMDeviceConfig
+        kcfg = KMDeviceConfig(k=args.k, text_dims=args.text_dims, half_life=5.0, max_rows=B,
+                              max_units=max_units, seed=args.seed)
+        eng = DeviceKMeans(kcfg, device=device, comm=comm)
+    else:
+        cfg = LRDeviceConfig(num_text_features=args.features, hash=args.hash,
+                             step_size=args.step_size, num_iterations=args.iters, fraction=1.0,
+                             begin=100, end=1000, max_rows=B, max_units=max_units,
+                             sgd_grid=args.sgd_grid, ablate=args.ablate)
+        eng = DeviceLinearRegression(cfg, device=device, comm=comm)
     pool = [HostBatchView(B, max_units).load(r) for r in pool_raw]
     del pool_raw
     t_gen = time.time() - t_gen
+    is_km = args.model == "kmeans"
 
     total = args.warmup + args.steps
     lat = []
@@ -101,13 +112,17 @@ def main(argv=None) -> int:
             if s + 1 < n_steps:
                 eng.submit(nxt, slot ^ 1)
             sealed_next = time.perf_counter()
-            res = eng.process(slot, now_ms)
+            res = eng.process(slot, want_pred=False) if is_km else eng.process(slot, now_ms)
             done = time.perf_counter()
             if record:
                 lat.append((done - sealed) * 1e3)
-                kept.append(res["n_kept"])
-                iters.append(res["iterations"])
-                stage.append((res["prep_ms"], res["train_ms"]))
+                if is_km:
+                    kept.append(res["n_local"])
+                    stage.append((res["ms"], 0.0))
+                else:
+                    kept.append(res["n_kept"])
+                    iters.append(res["iterations"])
+                    stage.append((res["prep_ms"], res["train_ms"]))
             sealed = sealed_next
             slot ^= 1
 
@@ -126,7 +141,39 @@ def main(argv=None) -> int:
     p50 = D.allreduce_max_scalar(float(np.median(lat)))
     value = tweets / elapsed
     ms = elapsed / args.steps * 1e3
-    if info.is_main:
+    if info.is_main and is_km:
+        out = {
+            "metric": "tweets/sec trained (whole node)",
+            "value": round(value, 1),
+            "unit": "tweets/s",
+            "n_gpus": info.world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic tweet-shaped records (seeded C++ generator), N(0,1) random centres",
+            "config": {
+                "model": f"StreamingKMeans k={args.k}, d={2 + args.text_dims} "
+                         f"([retweetCount, followers] + {args.text_dims} hashed bigram dims), "
+                         "halfLife 5 batches, per-batch StandardScaler",
+                "global_batch": B * info.world,
+                "seq_len": 280,
+                "parallelism": f"dp{info.world}",
+            },
+            "p50_microbatch_latency_ms": round(p50, 3),
+            "trained_tweets_per_step": round(tweets / args.steps, 1),
+            "device_ms_mean": float(np.mean([s[0] for s in stage])) if stage else 0.0,
+            "pool_gen_s": round(t_gen, 2),
+        }
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as fh:
+                fh.write(line + "\n")
+    elif info.is_main:
         out = {
             "metric": "tweets/sec trained (whole node)",
             "value": round(value, 1),

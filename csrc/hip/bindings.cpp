@@ -99,20 +99,20 @@ PYBIND11_MODULE(_twtml_hip, m) {
       });
 
   py::class_<HostBatch, std::shared_ptr<HostBatch>>(m, "HostBatch")
-      .def(py::init<int64_t, int64_t>(), py::arg("max_rows"), py::arg("max_units"))
+      .def(py::init<int64_t, int64_t>(), py::arg("max_rows"), py::arg("max_bytes"))
       .def_readonly("max_rows", &HostBatch::max_rows)
-      .def_readonly("max_units", &HostBatch::max_units)
+      .def_readonly("max_bytes", &HostBatch::max_bytes)
       .def_property_readonly("text", [](py::object self) {
         auto& h = self.cast<HostBatch&>();
-        return view<uint16_t>(h.text, {py::ssize_t(h.max_units)}, self);
+        return view<uint8_t>(h.text, {py::ssize_t(h.max_bytes)}, self);
       })
       .def_property_readonly("offsets", [](py::object self) {
         auto& h = self.cast<HostBatch&>();
         return view<int64_t>(h.offsets, {py::ssize_t(h.max_rows + 1)}, self);
       })
-      .def_property_readonly("is_rt", [](py::object self) {
+      .def_property_readonly("flags", [](py::object self) {
         auto& h = self.cast<HostBatch&>();
-        return view<uint8_t>(h.is_rt, {py::ssize_t(h.max_rows)}, self);
+        return view<uint8_t>(h.flags, {py::ssize_t(h.max_rows)}, self);
       })
       .def_property_readonly("scalars_flat", [](py::object self) {
         auto& h = self.cast<HostBatch&>();
@@ -127,11 +127,11 @@ PYBIND11_MODULE(_twtml_hip, m) {
            }),
            py::arg("device"), py::arg("config"), py::arg("comm") = nullptr)
       .def("submit",
-           [](LREngine& e, const HostBatch& hb, int64_t n, int64_t units, int slot) {
+           [](LREngine& e, const HostBatch& hb, int64_t n, int64_t bytes, int slot) {
              py::gil_scoped_release nogil;
-             e.submit(hb, n, units, slot);
+             e.submit(hb, n, bytes, slot);
            },
-           py::arg("host_batch"), py::arg("n"), py::arg("units"), py::arg("slot"))
+           py::arg("host_batch"), py::arg("n"), py::arg("bytes"), py::arg("slot"))
       .def("process",
            [](LREngine& e, int slot, int64_t now_ms, bool want_pred) {
              BatchResult r;

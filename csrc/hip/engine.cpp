@@ -10,18 +10,19 @@ namespace twtml {
 
 void launch_batch_init(double* state, double m_global, hipStream_t s);
 
-HostBatch::HostBatch(int64_t rows, int64_t units) : max_rows(rows), max_units(units) {
+HostBatch::HostBatch(int64_t rows, int64_t text_bytes) : max_rows(rows), max_bytes(text_bytes) {
+  if (rows < 0 || text_bytes < 0) throw std::invalid_argument("HostBatch: negative capacity");
   auto up = [](size_t x) { return (x + 255) & ~size_t(255); };
-  const size_t t = up(sizeof(uint16_t) * size_t(units));
+  const size_t t = up(size_t(text_bytes));
   const size_t o = up(sizeof(int64_t) * size_t(rows + 1));
   const size_t r = up(size_t(rows));
   const size_t sc = up(sizeof(int64_t) * 5 * size_t(rows));
   bytes = t + o + r + sc;
   TWTML_HIP_CHECK(hipHostMalloc(&base, bytes, hipHostMallocDefault));
   char* p = static_cast<char*>(base);
-  text = reinterpret_cast<uint16_t*>(p);
+  text = reinterpret_cast<uint8_t*>(p);
   offsets = reinterpret_cast<int64_t*>(p + t);
-  is_rt = reinterpret_cast<uint8_t*>(p + t + o);
+  flags = reinterpret_cast<uint8_t*>(p + t + o);
   scalars = reinterpret_cast<int64_t*>(p + t + o + r);
   offsets[0] = 0;
 }
@@ -50,14 +51,7 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
   num_cu_ = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   TWTML_HIP_CHECK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
   TWTML_HIP_CHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
-  for (auto& s : slots_) {
-    s.text = dmalloc<uint16_t>(size_t(cfg_.max_units) + 8);
-    s.offsets = dmalloc<int64_t>(size_t(cfg_.max_rows) + 1);
-    s.is_rt = dmalloc<uint8_t>(size_t(cfg_.max_rows));
-    s.scalars = dmalloc<int64_t>(5 * size_t(cfg_.max_rows));
-    TWTML_HIP_CHECK(hipEventCreateWithFlags(&s.h2d_done, hipEventDisableTiming));
-    TWTML_HIP_CHECK(hipEventCreateWithFlags(&s.consumed, hipEventDisableTiming));
-  }
+  raw_.init(cfg_.max_rows, text_bytes_for_units(cfg_.max_units));
   for (auto& e : ev_) TWTML_HIP_CHECK(hipEventCreate(&e));
   upload_lower_tables(compute_, &lower_page_, &lower_blocks_);
   alloc_prepared();
@@ -136,10 +130,7 @@ void LREngine::ensure_compact(int64_t ns) {
 LREngine::~LREngine() {
   (void)hipSetDevice(device_);
   (void)hipDeviceSynchronize();
-  for (auto& s : slots_) {
-    (void)hipFree(s.text); (void)hipFree(s.offsets); (void)hipFree(s.is_rt); (void)hipFree(s.scalars);
-    (void)hipEventDestroy(s.h2d_done); (void)hipEventDestroy(s.consumed);
-  }
+  raw_.release();
   for (auto& e : ev_) (void)hipEventDestroy(e);
   void* bufs[] = {prep_.kept, prep_.nnz, prep_.sorted, prep_.blk, prep_.hist, prep_.clen8,
                   prep_.cbase, prep_.idx, prep_.slot, prep_.y, prep_.num, prep_.perm,
@@ -153,53 +144,28 @@ LREngine::~LREngine() {
   (void)hipStreamDestroy(copy_);
 }
 
-void LREngine::submit(const HostBatch& hb, int64_t n, int64_t units, int slot) {
-  if (slot < 0 || slot > 1) throw std::invalid_argument("slot must be 0 or 1");
-  if (n < 0 || n > cfg_.max_rows || n > hb.max_rows) throw std::invalid_argument("rows exceed capacity");
-  if (units < 0 || units > cfg_.max_units || units > hb.max_units)
-    throw std::invalid_argument("text units exceed capacity");
-  if (n > 0 && hb.offsets[n] != units) throw std::invalid_argument("offsets[n] != units");
+void LREngine::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot) {
   TWTML_HIP_CHECK(hipSetDevice(device_));
-  Slot& s = slots_[slot];
-  // wait until the compute stream has finished reading this slot
-  if (s.used) TWTML_HIP_CHECK(hipStreamWaitEvent(copy_, s.consumed, 0));
-  if (units > 0)
-    TWTML_HIP_CHECK(hipMemcpyAsync(s.text, hb.text, sizeof(uint16_t) * size_t(units),
-                                   hipMemcpyHostToDevice, copy_));
-  TWTML_HIP_CHECK(hipMemcpyAsync(s.offsets, hb.offsets, sizeof(int64_t) * size_t(n + 1),
-                                 hipMemcpyHostToDevice, copy_));
-  if (n > 0) {
-    TWTML_HIP_CHECK(hipMemcpyAsync(s.is_rt, hb.is_rt, size_t(n), hipMemcpyHostToDevice, copy_));
-    // scalars are packed [5][n] at the start of the host buffer
-    TWTML_HIP_CHECK(hipMemcpyAsync(s.scalars, hb.scalars, sizeof(int64_t) * 5 * size_t(n),
-                                   hipMemcpyHostToDevice, copy_));
-  }
-  TWTML_HIP_CHECK(hipEventRecord(s.h2d_done, copy_));
-  s.n = n;
-  s.units = units;
-  s.used = true;
+  raw_.submit(hb, n, bytes, slot, copy_);
 }
 
 BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
-  if (slot < 0 || slot > 1) throw std::invalid_argument("slot must be 0 or 1");
   TWTML_HIP_CHECK(hipSetDevice(device_));
-  Slot& sl = slots_[slot];
   hipStream_t s = compute_;
   const int world = comm_ ? comm_->world() : 1;
   const int rank = comm_ ? comm_->rank() : 0;
   BatchResult res;
-  res.n_raw = sl.n;
-  TWTML_HIP_CHECK(hipStreamWaitEvent(s, sl.h2d_done, 0));
+  const DevRawBatch b = raw_.acquire(slot, s);
+  res.n_raw = b.n;
   TWTML_HIP_CHECK(hipEventRecord(ev_[0], s));
 
-  DevRawBatch b{sl.text, sl.offsets, sl.is_rt, sl.scalars, sl.n, sl.units};
   FeaturizeParams fp{cfg_.num_text_features, cfg_.hash_kind, cfg_.require_retweet,
                      cfg_.range_filter, cfg_.begin, cfg_.end, now_ms};
   TWTML_HIP_CHECK(hipMemsetAsync(prep_.counters, 0, 8 * sizeof(int64_t), s));
   launch_filter_sort(b, prep_, fp, s);
   launch_chunk_layout(b, prep_, s);
   launch_featurize(b, prep_, fp, lower_page_, lower_blocks_, s);
-  TWTML_HIP_CHECK(hipEventRecord(sl.consumed, s));  // raw slot may be overwritten now
+  raw_.release_slot(slot, s);  // raw slot may be overwritten now
   if (world > 1) comm_->allreduce(prep_.flags, size_t(prep_.flag_len), ncclUint8, ncclMax, s);
   launch_compact_active(prep_, s);
   // global kept count (and per-rank counts for sampling offsets)

@@ -20,6 +20,7 @@
 #include "comm.h"
 #include "common.h"
 #include "kernels.h"
+#include "raw_slots.h"
 
 namespace twtml {
 
@@ -39,17 +40,23 @@ struct LRConfig {
   int32_t ablate = 0;            // perf diagnostics only (see SgdParams)
 };
 
+// Pinned staging buffer of one raw batch in the wire format
+// (csrc/host/wire.h): narrow/wide rows in `text`, byte offsets, per-row
+// flags (bit0 isRetweet, bit1 wide), scalars packed [5][n].
 struct HostBatch {
   void* base = nullptr;
   size_t bytes = 0;
-  uint16_t* text = nullptr;
+  uint8_t* text = nullptr;
   int64_t* offsets = nullptr;
-  uint8_t* is_rt = nullptr;
+  uint8_t* flags = nullptr;
   int64_t* scalars = nullptr;
-  int64_t max_rows = 0, max_units = 0;
-  HostBatch(int64_t rows, int64_t units);
+  int64_t max_rows = 0, max_bytes = 0;
+  HostBatch(int64_t rows, int64_t text_bytes);
   ~HostBatch();
 };
+
+// bytes of device text buffer for `units` UTF-16 units (all rows wide)
+inline int64_t text_bytes_for_units(int64_t units) { return 2 * units + 64; }
 
 struct BatchResult {
   int64_t n_raw = 0, n_kept = 0, n_kept_global = 0, n_unique = 0, entries = 0;
@@ -68,7 +75,7 @@ class LREngine {
   ~LREngine();
 
   // Async H2D of rows [0, n) of a pinned host batch into device slot `slot`.
-  void submit(const HostBatch& hb, int64_t n, int64_t units, int slot);
+  void submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot);
   // Train on the batch in `slot` (blocks until done); stats use w before training.
   BatchResult process(int slot, int64_t now_ms, bool want_pred);
 
@@ -93,15 +100,7 @@ class LREngine {
   LRConfig cfg_;
   std::shared_ptr<Comm> comm_;
   hipStream_t compute_ = nullptr, copy_ = nullptr;
-  struct Slot {
-    uint16_t* text = nullptr;
-    int64_t* offsets = nullptr;
-    uint8_t* is_rt = nullptr;
-    int64_t* scalars = nullptr;
-    int64_t n = 0, units = 0;
-    hipEvent_t h2d_done = nullptr, consumed = nullptr;
-    bool used = false;
-  } slots_[2];
+  RawSlots raw_;
   DevPrepared prep_{};
   DevSgd sgd_{};
   int64_t ns_cap_ = 0;

@@ -73,7 +73,7 @@ __device__ __forceinline__ int len_key(int32_t n32) {
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ bool keep_row(const DevRawBatch& b, int64_t r, const FeaturizeParams& fp) {
   if (r >= b.n) return false;
-  if (fp.require_retweet && !b.is_rt[r]) return false;
+  if (fp.require_retweet && !(b.flags[r] & kRowRetweet)) return false;
   if (fp.range_filter) {
     const int64_t rc = b.scalars[r];
     if (rc < fp.begin || rc > fp.end) return false;
@@ -106,7 +106,7 @@ __global__ __launch_bounds__(kBlock) void k_filter_write(DevRawBatch b, Featuriz
   if (pred) {
     const int64_t k = blk_off[blockIdx.x] + woff + wpre;
     kept[k] = r;
-    const int64_t len = b.offsets[r + 1] - b.offsets[r];
+    const int64_t len = row_text(b, r).len;
     const int64_t nz = len >= 2 ? len - 1 : len;
     const int32_t n32 = int32_t(nz > 0x7fffffff ? 0x7fffffff : nz);
     nnz[k] = n32;
@@ -226,53 +226,77 @@ __device__ __forceinline__ uint32_t mur_h(uint32_t h, uint32_t k) { return rotl3
 
 // Spark-2 murmur3 (hashUnsafeBytes, seed 42) of the UTF-8 bytes of a
 // 1-2 unit Java string (lone surrogates become '?').
+// UTF-8 encoding of one code point, little-endian packed, byte count in *m
+__device__ __forceinline__ uint32_t utf8_pack(uint32_t cp, int* m) {
+  if (cp < 0x80) { *m = 1; return cp; }
+  if (cp < 0x800) { *m = 2; return (0xC0u | (cp >> 6)) | ((0x80u | (cp & 0x3F)) << 8); }
+  if (cp < 0x10000) {
+    *m = 3;
+    return (0xE0u | (cp >> 12)) | ((0x80u | ((cp >> 6) & 0x3F)) << 8) | ((0x80u | (cp & 0x3F)) << 16);
+  }
+  *m = 4;
+  return (0xF0u | (cp >> 18)) | ((0x80u | ((cp >> 12) & 0x3F)) << 8) |
+         ((0x80u | ((cp >> 6) & 0x3F)) << 16) | ((0x80u | (cp & 0x3F)) << 24);
+}
+
+// The UTF-8 bytes (at most 8) live in one 64-bit register: no private array,
+// so nothing spills to scratch.
 __device__ int32_t murmur_term(uint32_t u0, uint32_t u1, int n) {
-  uint8_t b[8];
-  int k = 0;
-  auto put = [&](uint32_t cp) {
-    if (cp < 0x80) { b[k++] = uint8_t(cp); }
-    else if (cp < 0x800) { b[k++] = uint8_t(0xC0 | (cp >> 6)); b[k++] = uint8_t(0x80 | (cp & 0x3F)); }
-    else if (cp < 0x10000) {
-      b[k++] = uint8_t(0xE0 | (cp >> 12)); b[k++] = uint8_t(0x80 | ((cp >> 6) & 0x3F));
-      b[k++] = uint8_t(0x80 | (cp & 0x3F));
-    } else {
-      b[k++] = uint8_t(0xF0 | (cp >> 18)); b[k++] = uint8_t(0x80 | ((cp >> 12) & 0x3F));
-      b[k++] = uint8_t(0x80 | ((cp >> 6) & 0x3F)); b[k++] = uint8_t(0x80 | (cp & 0x3F));
-    }
-  };
+  uint64_t bytes = 0;
+  int k = 0, m = 0;
   const bool hi0 = u0 >= 0xD800 && u0 <= 0xDBFF, sur0 = u0 >= 0xD800 && u0 <= 0xDFFF;
   if (n == 2 && hi0 && u1 >= 0xDC00 && u1 <= 0xDFFF) {
-    put(0x10000u + ((u0 - 0xD800u) << 10) + (u1 - 0xDC00u));
+    bytes = utf8_pack(0x10000u + ((u0 - 0xD800u) << 10) + (u1 - 0xDC00u), &m);
+    k = m;
   } else {
-    put(sur0 ? '?' : u0);
-    if (n == 2) put((u1 >= 0xD800 && u1 <= 0xDFFF) ? '?' : u1);
+    bytes = utf8_pack(sur0 ? uint32_t('?') : u0, &m);
+    k = m;
+    if (n == 2) {
+      bytes |= uint64_t(utf8_pack((u1 >= 0xD800 && u1 <= 0xDFFF) ? uint32_t('?') : u1, &m)) << (8 * k);
+      k += m;
+    }
   }
   uint32_t h = 42u;
-  const int aligned = k - k % 4;
-  for (int i = 0; i < aligned; i += 4)
-    h = mur_h(h, mur_k(uint32_t(b[i]) | (uint32_t(b[i + 1]) << 8) | (uint32_t(b[i + 2]) << 16) |
-                       (uint32_t(b[i + 3]) << 24)));
-  for (int i = aligned; i < k; ++i) h = mur_h(h, mur_k(uint32_t(int32_t(int8_t(b[i])))));
+  const int aligned = k & ~3;
+  if (aligned >= 4) h = mur_h(h, mur_k(uint32_t(bytes)));
+  if (aligned >= 8) h = mur_h(h, mur_k(uint32_t(bytes >> 32)));
+  for (int i = aligned; i < k; ++i) h = mur_h(h, mur_k(uint32_t(int32_t(int8_t(uint8_t(bytes >> (8 * i)))))));
   h ^= uint32_t(k);
   h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
   return int32_t(h);
 }
 
 __device__ __forceinline__ int64_t term_mod(int64_t h, int64_t F) {
+  if (h >= 0 && h < F) return h;                 // java bigrams (< 2^21) with F >= 2^21
+  if (F <= 0x7fffffff && h >= -0x7fffffffLL && h <= 0x7fffffffLL) {   // 32-bit path
+    const int32_t m = int32_t(h) % int32_t(F);
+    return m < 0 ? m + F : m;
+  }
   const int64_t m = h % F;
   return m < 0 ? m + F : m;
 }
+
+// Active-feature flags: ids below kFlagLds are first collected in a per-block
+// LDS bitmap (Java bigram hashes of ASCII text are < 4096, so almost every
+// entry lands here) and flushed once per block; the rest go straight to the
+// byte flags in global memory.
+constexpr int kFlagLds = 1 << 16;
+constexpr int kFlagWords = kFlagLds / 32;
 
 // One wave per 16-row chunk; the 4 lanes of a row take entries j = t, t+4, ...
 __global__ __launch_bounds__(kBlock) void k_featurize(DevRawBatch b, DevPrepared p, FeaturizeParams fp,
                                                       const uint8_t* lpage, const uint16_t* lblocks,
                                                       int64_t cmax) {
+  __shared__ uint32_t fbits[kFlagWords];
+  for (int i = threadIdx.x; i < kFlagWords; i += kBlock) fbits[i] = 0u;
+  __syncthreads();
   const int64_t n_kept = p.counters[0];
   const int lane = lane_id();
   const int r = lane / kLanesPerRow, t = lane % kLanesPerRow;
   const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = int64_t(gridDim.x) * kBlock / kWave;
   const int64_t F = fp.num_text_features;
+  const int64_t lds_lim = p.flag_len < kFlagLds ? p.flag_len : kFlagLds;
   const int64_t cap_groups = p.cap_entries / kChunkStride;
   const int64_t nch = (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;
   for (int64_t c = wave; c < nch && c < cmax; c += nwaves) {
@@ -286,8 +310,9 @@ __global__ __launch_bounds__(kBlock) void k_featurize(DevRawBatch b, DevPrepared
       if (lane == 0) p.counters[3] = 1;  // capacity overflow -> host raises
       continue;
     }
-    const int64_t o = valid ? b.offsets[row] : 0;
-    const int64_t len = valid ? b.offsets[row + 1] - o : 0;
+    RowText rt{0, 0, 0};
+    if (valid) rt = row_text(b, row);
+    const int64_t len = rt.len;
     const int64_t nz = len >= 2 ? len - 1 : len;
     int32_t* out = p.idx + g0 * kChunkStride + lane * kGroup;
     const int32_t total = L8 * kGroup;
@@ -295,17 +320,18 @@ __global__ __launch_bounds__(kBlock) void k_featurize(DevRawBatch b, DevPrepared
       const int64_t j = int64_t(jj) * kLanesPerRow + t;
       int32_t v = -1;
       if (j < nz) {
-        const uint32_t u0 = lower_dev(b.text[o + j], lpage, lblocks);
+        const uint32_t u0 = lower_dev(row_unit(b, rt, j), lpage, lblocks);
         int64_t h;
         if (len >= 2) {
-          const uint32_t u1 = lower_dev(b.text[o + j + 1], lpage, lblocks);
+          const uint32_t u1 = lower_dev(row_unit(b, rt, j + 1), lpage, lblocks);
           h = fp.hash_kind == 0 ? int64_t(31u * u0 + u1) : int64_t(murmur_term(u0, u1, 2));
         } else {
           h = fp.hash_kind == 0 ? int64_t(u0) : int64_t(murmur_term(u0, 0, 1));
         }
         const int64_t idx = term_mod(h, F);
         v = int32_t(idx);
-        if (idx < p.flag_len) p.flags[idx] = 1;
+        if (idx < lds_lim) atomicOr(&fbits[idx >> 5], 1u << (idx & 31));
+        else if (idx < p.flag_len) p.flags[idx] = 1;
       }
       out[(jj >> 3) * kChunkStride + (jj & 7)] = v;
     }
@@ -328,14 +354,25 @@ __global__ __launch_bounds__(kBlock) void k_featurize(DevRawBatch b, DevPrepared
       p.perm[pos] = kidx;
     }
   }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kFlagWords; i += kBlock) {
+    uint32_t bits = fbits[i];
+    while (bits) {
+      const int bit = __builtin_ctz(bits);
+      bits &= bits - 1u;
+      p.flags[int64_t(i) * 32 + bit] = 1;
+    }
+  }
 }
 
 void launch_featurize(const DevRawBatch& b, const DevPrepared& p, const FeaturizeParams& fp,
                       const uint8_t* lpage, const uint16_t* lblocks, hipStream_t s) {
   const int64_t cmax = (b.n + kRowsPerChunk - 1) / kRowsPerChunk;
   if (cmax == 0) return;
+  // ~8 blocks per CU, each sweeping many chunks, so the LDS flag bitmap is
+  // flushed rarely (XCD-agnostic: chunk order is length-sorted anyway)
   int grid = ceil_div(cmax, kBlock / kWave);
-  if (grid > 16384) grid = 16384;
+  if (grid > 2048) grid = 2048;
   hipLaunchKernelGGL(k_featurize, dim3(grid), dim3(kBlock), 0, s, b, p, fp, lpage, lblocks, cmax);
 }
 

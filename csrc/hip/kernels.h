@@ -18,14 +18,37 @@ namespace twtml {
 
 // ---------------------------------------------------------------------------
 // Raw batch on the device (one ingest slot).
+// Raw batch in the wire format (csrc/host/wire.h).
 struct DevRawBatch {
-  const uint16_t* text;     // [units]
-  const int64_t* offsets;   // [n+1]
-  const uint8_t* is_rt;     // [n]
+  const uint8_t* text;      // [bytes] narrow (1 B/unit) or wide (UTF-16LE) rows
+  const int64_t* offsets;   // [n+1] byte offsets
+  const uint8_t* flags;     // [n] bit0 isRetweet, bit1 wide
   const int64_t* scalars;   // [5][n]
   int64_t n;                // rows in this batch (host-known)
-  int64_t units;
+  int64_t bytes;
 };
+
+constexpr uint8_t kRowRetweet = 1;
+constexpr uint8_t kRowWide = 2;
+
+// Row r: byte offset, wide flag and length in UTF-16 units.
+struct RowText {
+  int64_t o, len;
+  int wide;
+};
+
+__device__ __forceinline__ RowText row_text(const DevRawBatch& b, int64_t r) {
+  const int64_t o = b.offsets[r];
+  const int wide = (b.flags[r] & kRowWide) ? 1 : 0;
+  return RowText{o, (b.offsets[r + 1] - o) >> wide, wide};
+}
+
+// UTF-16 unit j of a row (wide rows may be unaligned: assembled from bytes)
+__device__ __forceinline__ uint32_t row_unit(const DevRawBatch& b, const RowText& t, int64_t j) {
+  if (!t.wide) return b.text[t.o + j];
+  const uint8_t* p = b.text + t.o + 2 * j;
+  return uint32_t(p[0]) | (uint32_t(p[1]) << 8);
+}
 
 // Per-batch prepared (SELL-64, length-sorted) sparse features.
 struct DevPrepared {

@@ -49,12 +49,12 @@ __global__ __launch_bounds__(kBlock) void k_km_features(DevRawBatch b, const int
     if (text_dims > 0) {
       for (int j = lane; j < text_dims; j += kWave) h[j] = 0u;
       __builtin_amdgcn_wave_barrier();
-      const int64_t o = b.offsets[row];
-      const int64_t len = b.offsets[row + 1] - o;
+      const RowText rt = row_text(b, row);
+      const int64_t len = rt.len;
       const int64_t nz = len >= 2 ? len - 1 : len;
       for (int64_t j = lane; j < nz; j += kWave) {
-        const uint32_t u0 = km_lower(b.text[o + j], lpage, lblocks);
-        const uint32_t hsh = len >= 2 ? 31u * u0 + km_lower(b.text[o + j + 1], lpage, lblocks) : u0;
+        const uint32_t u0 = km_lower(row_unit(b, rt, j), lpage, lblocks);
+        const uint32_t hsh = len >= 2 ? 31u * u0 + km_lower(row_unit(b, rt, j + 1), lpage, lblocks) : u0;
         atomicAdd(&h[hsh % uint32_t(text_dims)], 1u);
       }
       __builtin_amdgcn_wave_barrier();
@@ -82,58 +82,77 @@ void launch_km_features(const DevRawBatch& b, const int64_t* kept, const int64_t
 // K11: column moments (fp64).  mode 0: sums -> out[1+j] (+ n in out[0]);
 // mode 1: centred squares -> out[j] using mean = sum_n[1+j] / sum_n[0].
 // ---------------------------------------------------------------------------
+// thread -> (row lane rr, column j): consecutive threads read consecutive
+// columns of a row (coalesced); row lanes are reduced in LDS, one fp64
+// atomic per (block, column).
+static int km_cols_pow2(int d) {
+  int cp = 1;
+  while (cp < d && cp < kBlock) cp <<= 1;
+  return cp;
+}
+
 __global__ __launch_bounds__(kBlock) void k_km_moments(const float* X, const int64_t* counters,
-                                                       int d, int dp, int mode, const double* sum_n,
-                                                       double* out) {
+                                                       int d, int dp, int cp, int mode,
+                                                       const double* sum_n, double* out) {
+  __shared__ double red[kBlock];
   const int64_t n = counters[0];
-  // thread -> (row lane, column); columns strided over the block
-  for (int j0 = 0; j0 < d; j0 += kBlock) {
-    const int j = j0 + int(threadIdx.x);
-    if (j >= d) continue;
-    const double mean = mode == 1 && sum_n[0] > 0 ? sum_n[1 + j] / sum_n[0] : 0.0;
+  const int rp = kBlock / cp, rr = threadIdx.x / cp;
+  for (int jb = 0; jb < d; jb += cp) {
+    const int j = jb + int(threadIdx.x) % cp;
     double acc = 0.0;
-    for (int64_t r = blockIdx.x; r < n; r += gridDim.x) {
-      const double v = double(X[r * dp + j]) - mean;
-      acc += mode == 0 ? v : v * v;
+    if (j < d) {
+      const double mean = mode == 1 && sum_n[0] > 0 ? sum_n[1 + j] / sum_n[0] : 0.0;
+      for (int64_t r = int64_t(blockIdx.x) * rp + rr; r < n; r += int64_t(gridDim.x) * rp) {
+        const double v = double(X[r * dp + j]) - mean;
+        acc += mode == 0 ? v : v * v;
+      }
     }
-    atomicAdd(&out[(mode == 0 ? 1 : 0) + j], acc);
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    if (rr == 0 && j < d) {
+      for (int q = 1; q < rp; ++q) acc += red[q * cp + threadIdx.x];
+      atomicAdd(&out[(mode == 0 ? 1 : 0) + j], acc);
+    }
+    __syncthreads();
   }
   if (mode == 0 && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&out[0], double(n));
 }
 
 void launch_km_moments(const float* X, const int64_t* counters, int d, int dp, int mode,
                        const double* sum_n, double* out, int64_t max_rows, hipStream_t s) {
-  int grid = int(max_rows / 64 + 1);
-  if (grid > 2048) grid = 2048;
-  hipLaunchKernelGGL(k_km_moments, dim3(grid), dim3(kBlock), 0, s, X, counters, d, dp, mode, sum_n, out);
+  int grid = int(max_rows / 256 + 1);
+  if (grid > 1024) grid = 1024;
+  hipLaunchKernelGGL(k_km_moments, dim3(grid), dim3(kBlock), 0, s, X, counters, d, dp,
+                     km_cols_pow2(d), mode, sum_n, out);
 }
 
-// factor_j = std_j != 0 ? 1/std_j : 0 with std = sqrt(M2/(n-1)), n < 2 -> 0
-__global__ void k_km_scale(float* X, const int64_t* counters, int d, int dp, const double* sum_n,
-                           const double* m2, double* factor_out) {
-  const int64_t n = counters[0];
+// std_j = sqrt(M2_j / (n-1)) (n < 2 -> 0); factor_j = std_j != 0 ? 1/std_j : 0
+// (StandardScalerModel.transform).  The features stay unscaled in X; every
+// consumer multiplies by the factor on load (fp32 copy for the matrix-core
+// distances, fp64 for sums and the tie refine).  scale == 0 -> factor 1.
+__global__ void k_km_factor(int d, int dp, int scale, const double* sum_n, const double* m2,
+                            double* std_out, double* f64, float* f32) {
   const double cnt = sum_n[0];
-  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n * dp;
-       i += int64_t(gridDim.x) * blockDim.x) {
-    const int j = int(i % dp);
-    if (j >= d) continue;
-    const double var = cnt > 1.0 ? m2[j] / (cnt - 1.0) : 0.0;
-    const double sd = sqrt(var);
-    const double f = sd != 0.0 ? 1.0 / sd : 0.0;
-    X[i] = float(double(X[i]) * f);
-  }
-  if (blockIdx.x == 0)
-    for (int j = threadIdx.x; j < d; j += blockDim.x) {
-      const double var = cnt > 1.0 ? m2[j] / (cnt - 1.0) : 0.0;
-      factor_out[j] = sqrt(var);
+  for (int j = threadIdx.x; j < dp; j += blockDim.x) {
+    double f = 0.0;
+    if (j < d) {
+      if (scale) {
+        const double sd = sqrt(cnt > 1.0 ? m2[j] / (cnt - 1.0) : 0.0);
+        std_out[j] = sd;
+        f = sd != 0.0 ? 1.0 / sd : 0.0;
+      } else {
+        f = 1.0;
+      }
     }
+    f64[j] = f;
+    f32[j] = float(f);
+  }
 }
 
-void launch_km_scale(float* X, const int64_t* counters, int d, int dp, const double* sum_n,
-                     const double* m2, double* std_out, int64_t max_rows, hipStream_t s) {
-  int grid = int((max_rows * dp) / 1024 + 1);
-  if (grid > 8192) grid = 8192;
-  hipLaunchKernelGGL(k_km_scale, dim3(grid), dim3(kBlock), 0, s, X, counters, d, dp, sum_n, m2, std_out);
+void launch_km_factor(int d, int dp, bool scale, const double* sum_n, const double* m2,
+                      double* std_out, double* f64, float* f32, hipStream_t s) {
+  hipLaunchKernelGGL(k_km_factor, dim3(1), dim3(kBlock), 0, s, d, dp, scale ? 1 : 0, sum_n, m2,
+                     std_out, f64, f32);
 }
 
 // ---------------------------------------------------------------------------
@@ -153,11 +172,39 @@ __device__ __forceinline__ float km_tie_margin(float xn, float best) {
   return 1e-5f * (xn + fabsf(best)) + 1e-30f;
 }
 
+// Running best / second (with indices) / third distance of one point.
+struct KmTop3 {
+  float b1 = FLT_MAX, b2 = FLT_MAX, b3 = FLT_MAX;
+  int i1 = 0, i2 = 0;
+  __device__ __forceinline__ void add(float d, int c) {
+    if (d < b1) { b3 = b2; b2 = b1; i2 = i1; b1 = d; i1 = c; }
+    else if (d < b2) { b3 = b2; b2 = d; i2 = c; }
+    else if (d < b3) b3 = d;
+  }
+  // Near-tie routing (refine layout: [0,R) full list, [R,2R) pair points,
+  // [2R,4R) pair centres; cnt[0] full, cnt[1] pairs): when only two centres
+  // are within the margin the fp64 re-decision compares just those two.
+  __device__ __forceinline__ void route(int64_t p, float xn, int32_t* refine, unsigned long long* cnt,
+                                        int64_t R) const {
+    const float m = km_tie_margin(xn, b1);
+    if (b2 - b1 > m) return;
+    if (b3 - b1 <= m) {
+      refine[atomicAdd(&cnt[0], 1ull)] = int32_t(p);
+    } else {
+      const int64_t q = int64_t(atomicAdd(&cnt[1], 1ull));
+      refine[R + q] = int32_t(p);
+      refine[2 * R + 2 * q] = i1;
+      refine[2 * R + 2 * q + 1] = i2;
+    }
+  }
+};
+
 template <int DP>
-__global__ __launch_bounds__(kBlock) void k_km_assign_mfma(const float* X, const int64_t* counters,
+__global__ __launch_bounds__(kBlock) void k_km_assign_mfma(const float* X, const float* fac,
+                                                           const int64_t* counters,
                                                            const float* C, const float* cnorm, int k,
                                                            int32_t* labels, int32_t* refine,
-                                                           unsigned long long* refine_cnt) {
+                                                           unsigned long long* refine_cnt, int64_t R) {
   constexpr int KS = DP / 2;          // MFMA k-steps
   constexpr int LD = DP + 1;          // padded LDS row
   __shared__ float ct[32 * LD];
@@ -169,13 +216,12 @@ __global__ __launch_bounds__(kBlock) void k_km_assign_mfma(const float* X, const
   const int half = lane >> 5;
   float xb[KS];
 #pragma unroll
-  for (int s = 0; s < KS; ++s) xb[s] = p < n ? X[p * DP + 2 * s + half] : 0.f;
+  for (int s = 0; s < KS; ++s) xb[s] = p < n ? X[p * DP + 2 * s + half] * fac[2 * s + half] : 0.f;
   float xn = 0.f;
 #pragma unroll
   for (int s = 0; s < KS; ++s) xn += xb[s] * xb[s];
   xn += __shfl_xor(xn, 32, kWave);
-  float best = FLT_MAX, second = FLT_MAX;
-  int bidx = 0;
+  KmTop3 t;
   for (int c0 = 0; c0 < k; c0 += 32) {
     __syncthreads();
     for (int i = threadIdx.x; i < 32 * DP; i += kBlock) {
@@ -192,54 +238,72 @@ __global__ __launch_bounds__(kBlock) void k_km_assign_mfma(const float* X, const
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int cl = (r & 3) + 8 * (r >> 2) + 4 * half;
-      const float dist = cn[cl] - 2.f * acc[r];
-      if (dist < best) { second = best; best = dist; bidx = c0 + cl; }
-      else if (dist < second) second = dist;
+      t.add(cn[cl] - 2.f * acc[r], c0 + cl);
     }
   }
-  // combine the two lane halves (interleaved centre sets); ties -> lower index
-  const float ob = __shfl_xor(best, 32, kWave);
-  const float os = __shfl_xor(second, 32, kWave);
-  const int oi = __shfl_xor(bidx, 32, kWave);
-  if (ob < best || (ob == best && oi < bidx)) {
-    second = fminf(os, best);
-    best = ob; bidx = oi;
-  } else {
-    second = fminf(second, ob);
-  }
+  // combine the two lane halves (interleaved centre sets).  Exact fp32 ties
+  // fall inside the margin, so the fp64 refine settles them (first index).
+  const float o1 = __shfl_xor(t.b1, 32, kWave), o2 = __shfl_xor(t.b2, 32, kWave);
+  const float o3 = __shfl_xor(t.b3, 32, kWave);
+  const int j1 = __shfl_xor(t.i1, 32, kWave), j2 = __shfl_xor(t.i2, 32, kWave);
   if (half == 0 && p < n) {
-    labels[p] = bidx;
-    if (second - best <= km_tie_margin(xn, best)) refine[atomicAdd(refine_cnt, 1ull)] = int32_t(p);
+    t.add(o1, j1);
+    t.add(o2, j2);
+    t.add(o3, 0);      // can only land in third place
+    labels[p] = t.i1;
+    t.route(p, xn, refine, refine_cnt, R);
   }
 }
 
 // Generic fallback (any width): one thread per point, scalar fp32.
-__global__ __launch_bounds__(kBlock) void k_km_assign_scalar(const float* X, const int64_t* counters,
+__global__ __launch_bounds__(kBlock) void k_km_assign_scalar(const float* X, const float* fac,
+                                                             const int64_t* counters,
                                                              const float* C, const float* cnorm, int k,
                                                              int dp, int32_t* labels, int32_t* refine,
-                                                             unsigned long long* refine_cnt) {
+                                                             unsigned long long* refine_cnt, int64_t R) {
   const int64_t n = counters[0];
   for (int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x; p < n; p += int64_t(gridDim.x) * kBlock) {
-    float best = FLT_MAX, second = FLT_MAX, xn = 0.f;
-    int bi = 0;
-    for (int j = 0; j < dp; ++j) xn += X[p * dp + j] * X[p * dp + j];
+    KmTop3 t;
+    float xn = 0.f;
+    for (int j = 0; j < dp; ++j) xn += (X[p * dp + j] * fac[j]) * (X[p * dp + j] * fac[j]);
     for (int c = 0; c < k; ++c) {
       float dot = 0.f;
-      for (int j = 0; j < dp; ++j) dot += C[int64_t(c) * dp + j] * X[p * dp + j];
-      const float dist = cnorm[c] - 2.f * dot;
-      if (dist < best) { second = best; best = dist; bi = c; }
-      else if (dist < second) second = dist;
+      for (int j = 0; j < dp; ++j) dot += C[int64_t(c) * dp + j] * (X[p * dp + j] * fac[j]);
+      t.add(cnorm[c] - 2.f * dot, c);
     }
-    labels[p] = bi;
-    if (second - best <= km_tie_margin(xn, best)) refine[atomicAdd(refine_cnt, 1ull)] = int32_t(p);
+    labels[p] = t.i1;
+    t.route(p, xn, refine, refine_cnt, R);
   }
 }
 
-// fp64 re-decision of near-ties (e.g. the two halves of a just-split cluster
-// differ by 1e-14 relative, invisible in fp32): one wave per flagged point,
-// direct sum of squared differences against the fp64 centres, first index
-// on exact ties.
-__global__ __launch_bounds__(kBlock) void k_km_refine(const float* X, const int32_t* refine,
+// fp64 re-decision of a two-centre near-tie (typically the two halves of a
+// just-split cluster, 1e-14 apart -- invisible in fp32): thread per point.
+__global__ __launch_bounds__(kBlock) void k_km_refine_pair(const float* X, const double* fac,
+                                                           const int32_t* refine,
+                                                           const unsigned long long* refine_cnt,
+                                                           const double* centers, int d, int dp,
+                                                           int64_t R, int32_t* labels) {
+  const int64_t np = int64_t(refine_cnt[1]);
+  for (int64_t q = int64_t(blockIdx.x) * kBlock + threadIdx.x; q < np; q += int64_t(gridDim.x) * kBlock) {
+    const int64_t p = refine[R + q];
+    const int a = refine[2 * R + 2 * q], b = refine[2 * R + 2 * q + 1];
+    const float* x = X + p * dp;
+    double da = 0.0, db = 0.0;
+    for (int j = 0; j < d; ++j) {
+      const double xj = double(x[j]) * fac[j];
+      const double ta = xj - centers[int64_t(a) * d + j], tb = xj - centers[int64_t(b) * d + j];
+      da += ta * ta;
+      db += tb * tb;
+    }
+    labels[p] = (db < da || (db == da && b < a)) ? b : a;
+  }
+}
+
+// fp64 re-decision when three or more centres are within the margin: one
+// wave per point, direct sum of squared differences against all fp64
+// centres, first index on exact ties.
+__global__ __launch_bounds__(kBlock) void k_km_refine(const float* X, const double* fac,
+                                                      const int32_t* refine,
                                                       const unsigned long long* refine_cnt,
                                                       const double* centers, int k, int d, int dp,
                                                       int32_t* labels) {
@@ -254,7 +318,7 @@ __global__ __launch_bounds__(kBlock) void k_km_refine(const float* X, const int3
     for (int c = lane; c < k; c += kWave) {
       double s = 0.0;
       for (int j = 0; j < d; ++j) {
-        const double t = double(x[j]) - centers[int64_t(c) * d + j];
+        const double t = double(x[j]) * fac[j] - centers[int64_t(c) * d + j];
         s += t * t;
       }
       if (s < best) { best = s; bi = c; }
@@ -269,17 +333,19 @@ __global__ __launch_bounds__(kBlock) void k_km_refine(const float* X, const int3
   }
 }
 
-void launch_km_assign(const float* X, const int64_t* counters, const float* C, const float* cnorm,
-                      const double* centers, int k, int d, int dp, int32_t* labels, int32_t* refine,
-                      unsigned long long* refine_cnt, int64_t max_rows, bool mfma, hipStream_t s) {
-  TWTML_HIP_CHECK(hipMemsetAsync(refine_cnt, 0, sizeof(unsigned long long), s));
+void launch_km_assign(const float* X, const float* f32, const double* f64, const int64_t* counters,
+                      const float* C, const float* cnorm, const double* centers, int k, int d, int dp,
+                      int32_t* labels, int32_t* refine, unsigned long long* refine_cnt,
+                      int64_t max_rows, bool mfma, hipStream_t s) {
+  TWTML_HIP_CHECK(hipMemsetAsync(refine_cnt, 0, 2 * sizeof(unsigned long long), s));
   const int grid_m = int(max_rows / 128 + 1);
+  const int64_t R = max_rows;
   bool done = false;
   if (mfma) {
 #define KM_MFMA(DPV)                                                                                \
   case DPV:                                                                                         \
-    hipLaunchKernelGGL(k_km_assign_mfma<DPV>, dim3(grid_m), dim3(kBlock), 0, s, X, counters, C,     \
-                       cnorm, k, labels, refine, refine_cnt);                                       \
+    hipLaunchKernelGGL(k_km_assign_mfma<DPV>, dim3(grid_m), dim3(kBlock), 0, s, X, f32, counters, C, \
+                       cnorm, k, labels, refine, refine_cnt, R);                                    \
     done = true;                                                                                    \
     break;
     switch (dp) { KM_MFMA(2) KM_MFMA(4) KM_MFMA(8) KM_MFMA(16) KM_MFMA(32) KM_MFMA(64) KM_MFMA(128) default: break; }
@@ -288,24 +354,104 @@ void launch_km_assign(const float* X, const int64_t* counters, const float* C, c
   int grid = int(max_rows / kBlock + 1);
   if (grid > 4096) grid = 4096;
   if (!done)
-    hipLaunchKernelGGL(k_km_assign_scalar, dim3(grid), dim3(kBlock), 0, s, X, counters, C, cnorm, k,
-                       dp, labels, refine, refine_cnt);
-  hipLaunchKernelGGL(k_km_refine, dim3(grid), dim3(kBlock), 0, s, X, refine, refine_cnt, centers, k,
-                     d, dp, labels);
+    hipLaunchKernelGGL(k_km_assign_scalar, dim3(grid), dim3(kBlock), 0, s, X, f32, counters, C, cnorm,
+                       k, dp, labels, refine, refine_cnt, R);
+  const int grid_r = grid < 1024 ? grid : 1024;
+  hipLaunchKernelGGL(k_km_refine_pair, dim3(grid_r), dim3(kBlock), 0, s, X, f64, refine, refine_cnt,
+                     centers, d, dp, R, labels);
+  hipLaunchKernelGGL(k_km_refine, dim3(grid_r), dim3(kBlock), 0, s, X, f64, refine, refine_cnt,
+                     centers, k, d, dp, labels);
 }
 
 // ---------------------------------------------------------------------------
 // K9: counting sort by label + segmented sums with one atomic per label run.
+//
+// Labels are heavily skewed (most points fall in a few clusters), so global
+// per-point atomics serialise on a handful of addresses.  The histogram and
+// the scatter are privatised per block in LDS, and each wave first "peels"
+// its dominant labels with ballots: one LDS atomic per distinct label per
+// round, lane ranks from popcounts.  Blocks then reserve one global range
+// per (block, label).
 // ---------------------------------------------------------------------------
+constexpr int kKmChunk = 4096;      // points per block pass (multiple of kBlock)
+constexpr int kKmLdsBins = 8192;    // k limit for the LDS-privatised path
+
+// Returns this lane's rank among the points with the same label in cnt[label].
+__device__ __forceinline__ uint32_t km_peel_add(uint32_t* cnt, int label, bool active) {
+  const int lane = lane_id();
+  uint64_t rem = __ballot(active);
+  uint32_t mine = 0;
+  for (int it = 0; it < 4 && rem; ++it) {
+    const int leader = __builtin_ctzll(rem);
+    const int L = __shfl(label, leader, kWave);
+    const uint64_t mask = __ballot(active && label == L) & rem;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(&cnt[L], uint32_t(__popcll(mask)));
+    base = __shfl(base, leader, kWave);
+    if ((mask >> lane) & 1ull) mine = base + uint32_t(__popcll(mask & ((1ull << lane) - 1ull)));
+    rem &= ~mask;
+  }
+  if ((rem >> lane) & 1ull) mine = atomicAdd(&cnt[label], 1u);
+  return mine;
+}
+
 __global__ __launch_bounds__(kBlock) void k_km_label_hist(const int32_t* labels, const int64_t* counters,
-                                                          int64_t* hist) {
+                                                          int k, int64_t* hist) {
+  extern __shared__ uint32_t cnt[];
+  const int64_t n = counters[0];
+  for (int c = threadIdx.x; c < k; c += kBlock) cnt[c] = 0u;
+  __syncthreads();
+  for (int64_t base = int64_t(blockIdx.x) * kKmChunk; base < n; base += int64_t(gridDim.x) * kKmChunk)
+    for (int i = threadIdx.x; i < kKmChunk; i += kBlock) {
+      const int64_t p = base + i;
+      km_peel_add(cnt, p < n ? labels[p] : 0, p < n);
+    }
+  __syncthreads();
+  for (int c = threadIdx.x; c < k; c += kBlock)
+    if (cnt[c]) atomicAdd(reinterpret_cast<unsigned long long*>(&hist[c]), (unsigned long long)cnt[c]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_km_label_scatter(const int32_t* labels, const int64_t* counters,
+                                                             int k, int64_t* cursor, int32_t* order) {
+  extern __shared__ uint32_t sh[];
+  uint32_t* cnt = sh;          // [k]
+  uint32_t* rbase = sh + k;    // [k] reserved global base per label
+  const int64_t n = counters[0];
+  for (int64_t base = int64_t(blockIdx.x) * kKmChunk; base < n; base += int64_t(gridDim.x) * kKmChunk) {
+    for (int c = threadIdx.x; c < k; c += kBlock) cnt[c] = 0u;
+    __syncthreads();
+    for (int i = threadIdx.x; i < kKmChunk; i += kBlock) {
+      const int64_t p = base + i;
+      km_peel_add(cnt, p < n ? labels[p] : 0, p < n);
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < k; c += kBlock) {
+      const uint32_t m = cnt[c];
+      rbase[c] = m ? uint32_t(atomicAdd(reinterpret_cast<unsigned long long*>(&cursor[c]),
+                                        (unsigned long long)m)) : 0u;
+      cnt[c] = 0u;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kKmChunk; i += kBlock) {
+      const int64_t p = base + i;
+      const int lab = p < n ? labels[p] : 0;
+      const uint32_t r = km_peel_add(cnt, lab, p < n);
+      if (p < n) order[rbase[lab] + r] = int32_t(p);
+    }
+    __syncthreads();
+  }
+}
+
+// k > kKmLdsBins: plain global atomics
+__global__ __launch_bounds__(kBlock) void k_km_label_hist_g(const int32_t* labels, const int64_t* counters,
+                                                            int64_t* hist) {
   const int64_t n = counters[0];
   for (int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x; p < n; p += int64_t(gridDim.x) * kBlock)
     atomicAdd(reinterpret_cast<unsigned long long*>(&hist[labels[p]]), 1ull);
 }
 
-__global__ __launch_bounds__(kBlock) void k_km_label_scatter(const int32_t* labels, const int64_t* counters,
-                                                             int64_t* cursor, int32_t* order) {
+__global__ __launch_bounds__(kBlock) void k_km_label_scatter_g(const int32_t* labels, const int64_t* counters,
+                                                               int64_t* cursor, int32_t* order) {
   const int64_t n = counters[0];
   for (int64_t p = int64_t(blockIdx.x) * kBlock + threadIdx.x; p < n; p += int64_t(gridDim.x) * kBlock) {
     const int64_t pos = int64_t(atomicAdd(reinterpret_cast<unsigned long long*>(&cursor[labels[p]]), 1ull));
@@ -317,7 +463,8 @@ constexpr int kSegRows = 1024;
 
 // thread = (row lane rr, column j); walks rows rr, rr+RP, ... of its chunk in
 // label order; flushes its running sum whenever the label changes.
-__global__ __launch_bounds__(kBlock) void k_km_segsum(const float* X, const int32_t* labels,
+__global__ __launch_bounds__(kBlock) void k_km_segsum(const float* X, const double* fac,
+                                                      const int32_t* labels,
                                                       const int32_t* order, const int64_t* counters,
                                                       int d, int dp, int cols_pow2, double* sums,
                                                       double* counts) {
@@ -327,6 +474,7 @@ __global__ __launch_bounds__(kBlock) void k_km_segsum(const float* X, const int3
   for (int64_t base = int64_t(blockIdx.x) * kSegRows; base < n; base += int64_t(gridDim.x) * kSegRows)
   for (int j = threadIdx.x % cols_pow2; j < d; j += cols_pow2) {   // column passes (d > 256)
     const int64_t end = base + kSegRows < n ? base + kSegRows : n;
+    const double fj = fac[j];
     int cur = -1;
     double acc = 0.0, cnt = 0.0;
     for (int64_t q = base + rr; q < end; q += rp) {
@@ -339,7 +487,7 @@ __global__ __launch_bounds__(kBlock) void k_km_segsum(const float* X, const int3
         }
         cur = lab; acc = 0.0; cnt = 0.0;
       }
-      if (j < d) acc += double(X[int64_t(p) * dp + j]);
+      acc += double(X[int64_t(p) * dp + j]) * fj;
       cnt += 1.0;
     }
     if (cur >= 0) {
@@ -349,60 +497,124 @@ __global__ __launch_bounds__(kBlock) void k_km_segsum(const float* X, const int3
   }
 }
 
-void launch_km_cluster_sums(const float* X, const int32_t* labels, const int64_t* counters, int k,
+void launch_km_cluster_sums(const float* X, const double* f64, const int32_t* labels,
+                            const int64_t* counters, int k,
                             int d, int dp, int64_t* hist, int32_t* order, double* sums,
                             double* counts, int64_t max_rows, hipStream_t s,
                             void (*scan)(const int64_t*, int64_t*, int64_t, int64_t*, hipStream_t)) {
   TWTML_HIP_CHECK(hipMemsetAsync(hist, 0, sizeof(int64_t) * size_t(k + 1), s));
-  int grid = int(max_rows / kBlock + 1);
-  if (grid > 4096) grid = 4096;
-  hipLaunchKernelGGL(k_km_label_hist, dim3(grid), dim3(kBlock), 0, s, labels, counters, hist);
-  scan(hist, hist, k, nullptr, s);
-  hipLaunchKernelGGL(k_km_label_scatter, dim3(grid), dim3(kBlock), 0, s, labels, counters, hist, order);
-  int cp = 1;
-  while (cp < d && cp < kBlock) cp <<= 1;
+  if (k <= kKmLdsBins) {
+    int grid = int((max_rows + kKmChunk - 1) / kKmChunk);
+    grid = grid < 1 ? 1 : (grid > 1024 ? 1024 : grid);
+    hipLaunchKernelGGL(k_km_label_hist, dim3(grid), dim3(kBlock), sizeof(uint32_t) * size_t(k), s,
+                       labels, counters, k, hist);
+    scan(hist, hist, k, nullptr, s);
+    hipLaunchKernelGGL(k_km_label_scatter, dim3(grid), dim3(kBlock), 2 * sizeof(uint32_t) * size_t(k), s,
+                       labels, counters, k, hist, order);
+  } else {
+    int grid = int(max_rows / kBlock + 1);
+    if (grid > 4096) grid = 4096;
+    hipLaunchKernelGGL(k_km_label_hist_g, dim3(grid), dim3(kBlock), 0, s, labels, counters, hist);
+    scan(hist, hist, k, nullptr, s);
+    hipLaunchKernelGGL(k_km_label_scatter_g, dim3(grid), dim3(kBlock), 0, s, labels, counters, hist, order);
+  }
   int g2 = int(max_rows / kSegRows + 1);
   if (g2 > 4096) g2 = 4096;
-  hipLaunchKernelGGL(k_km_segsum, dim3(g2), dim3(kBlock), 0, s, X, labels, order, counters, d, dp, cp,
-                     sums, counts);
+  hipLaunchKernelGGL(k_km_segsum, dim3(g2), dim3(kBlock), 0, s, X, f64, labels, order, counters, d, dp,
+                     km_cols_pow2(d), sums, counts);
 }
 
 // ---------------------------------------------------------------------------
-// K10: StreamingKMeansModel.update (one workgroup, fp64).
+// K10: StreamingKMeansModel.update (fp64): weights + per-cluster blend
+// factors (one workgroup), centre blend (grid, elementwise), dying-cluster
+// split (one workgroup), fp32 centre copy + norms (wave per centre).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_km_update(double* centers, double* weights, const double* sums,
-                                                    const double* counts, int k, int d, double decay,
-                                                    int points_unit, float* c32, float* cnorm, int dp) {
+__global__ __launch_bounds__(1024) void k_km_weights(double* weights, const double* counts, int k,
+                                                     double decay, int points_unit, double* blend) {
+  __shared__ double red_v[16];
   __shared__ double total;
-  const int t = threadIdx.x;
-  if (t == 0) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  {
     double s = 0.0;
-    for (int c = 0; c < k; ++c) s += counts[c];
-    total = s;
+    for (int c = t; c < k; c += 1024) s += counts[c];
+    s = wave_sum(s);
+    if (lane == 0) red_v[w] = s;
+    __syncthreads();
+    if (t == 0) {
+      double tot = 0.0;
+      for (int q = 0; q < 16; ++q) tot += red_v[q];
+      total = tot;
+    }
+    __syncthreads();
   }
-  __syncthreads();
   const double discount = points_unit ? pow(decay, total) : decay;
   for (int c = t; c < k; c += 1024) {
     const double cnt = counts[c];
     double wgt = weights[c] * discount;
+    double lam = -1.0, a = 0.0;           // lam < 0: cluster untouched this batch
     if (cnt > 0.0) {
       const double upd = wgt + cnt;
-      const double lam = cnt / (upd > 1e-16 ? upd : 1e-16);
-      for (int j = 0; j < d; ++j)
-        centers[int64_t(c) * d + j] = (1.0 - lam) * centers[int64_t(c) * d + j] + (lam / cnt) * sums[int64_t(c) * d + j];
+      lam = cnt / (upd > 1e-16 ? upd : 1e-16);
+      a = lam / cnt;
       wgt = upd;
     }
     weights[c] = wgt;
+    blend[c] = lam;
+    blend[k + c] = a;
   }
-  __syncthreads();
-  if (t == 0) {
+}
+
+// c <- (1 - lam) c + (lam / n) sum   (BLAS.scal + BLAS.axpy order)
+__global__ void k_km_blend(double* centers, const double* sums, const double* blend, int k, int d) {
+  const int64_t total = int64_t(k) * d;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += int64_t(gridDim.x) * blockDim.x) {
+    const int c = int(i / d);
+    const double lam = blend[c];
+    if (lam >= 0.0) centers[i] = (1.0 - lam) * centers[i] + blend[k + c] * sums[i];
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_km_split(double* centers, double* weights, int k, int d) {
+  __shared__ double red_v[2][16];
+  __shared__ int red_i[2][16];
+  __shared__ int sel[2];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  {
     // dying-cluster check: argmax / argmin of the weights, first index on ties
-    // (Scala maxBy/minBy); a sequential scan -- k is at most a few thousand
-    int largest = 0, smallest = 0;
-    for (int c = 1; c < k; ++c) {
-      if (weights[c] > weights[largest]) largest = c;
-      if (weights[c] < weights[smallest]) smallest = c;
+    // (Scala maxBy/minBy) -- strided scan, then wave and block reductions
+    double vmax = -DBL_MAX, vmin = DBL_MAX;
+    int imax = 0x7fffffff, imin = 0x7fffffff;
+    for (int c = t; c < k; c += 1024) {
+      const double v = weights[c];
+      if (v > vmax) { vmax = v; imax = c; }
+      if (v < vmin) { vmin = v; imin = c; }
     }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const double om = __shfl_xor(vmax, off, kWave), on = __shfl_xor(vmin, off, kWave);
+      const int jm = __shfl_xor(imax, off, kWave), jn = __shfl_xor(imin, off, kWave);
+      if (om > vmax || (om == vmax && jm < imax)) { vmax = om; imax = jm; }
+      if (on < vmin || (on == vmin && jn < imin)) { vmin = on; imin = jn; }
+    }
+    if (lane == 0) { red_v[0][w] = vmax; red_i[0][w] = imax; red_v[1][w] = vmin; red_i[1][w] = imin; }
+    __syncthreads();
+    if (t == 0) {
+      for (int q = 1; q < 16; ++q) {
+        if (red_v[0][q] > red_v[0][0] || (red_v[0][q] == red_v[0][0] && red_i[0][q] < red_i[0][0])) {
+          red_v[0][0] = red_v[0][q]; red_i[0][0] = red_i[0][q];
+        }
+        if (red_v[1][q] < red_v[1][0] || (red_v[1][q] == red_v[1][0] && red_i[1][q] < red_i[1][0])) {
+          red_v[1][0] = red_v[1][q]; red_i[1][0] = red_i[1][q];
+        }
+      }
+      sel[0] = red_i[0][0];
+      sel[1] = red_i[1][0];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    const int largest = sel[0], smallest = sel[1];
     const double maxw = weights[largest], minw = weights[smallest];
     if (minw < 1e-8 * maxw) {
       const double wv = (maxw + minw) / 2.0;
@@ -416,40 +628,42 @@ __global__ __launch_bounds__(1024) void k_km_update(double* centers, double* wei
       }
     }
   }
-  __syncthreads();
-  for (int c = t; c < k; c += 1024) {
-    float nrm = 0.f;
-    for (int j = 0; j < dp; ++j) {
-      const float v = j < d ? float(centers[int64_t(c) * d + j]) : 0.f;
-      c32[int64_t(c) * dp + j] = v;
-      nrm += v * v;
-    }
-    cnorm[c] = nrm;
-  }
 }
 
-void launch_km_update(double* centers, double* weights, const double* sums, const double* counts,
-                      int k, int d, double decay, bool points_unit, float* c32, float* cnorm, int dp,
-                      hipStream_t s) {
-  hipLaunchKernelGGL(k_km_update, dim3(1), dim3(1024), 0, s, centers, weights, sums, counts, k, d,
-                     decay, points_unit ? 1 : 0, c32, cnorm, dp);
-}
-
-__global__ void k_km_centers32(const double* centers, int k, int d, int dp, float* c32, float* cnorm) {
-  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < k; c += gridDim.x * blockDim.x) {
+// wave per centre: fp32 copy (row padded to dp) + squared norm
+__global__ __launch_bounds__(kBlock) void k_km_centers32(const double* centers, int k, int d, int dp,
+                                                         float* c32, float* cnorm) {
+  const int lane = lane_id();
+  for (int64_t c = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave; c < k;
+       c += int64_t(gridDim.x) * (kBlock / kWave)) {
     float nrm = 0.f;
-    for (int j = 0; j < dp; ++j) {
-      const float v = j < d ? float(centers[int64_t(c) * d + j]) : 0.f;
-      c32[int64_t(c) * dp + j] = v;
+    for (int j = lane; j < dp; j += kWave) {
+      const float v = j < d ? float(centers[c * d + j]) : 0.f;
+      c32[c * dp + j] = v;
       nrm += v * v;
     }
-    cnorm[c] = nrm;
+    nrm = wave_sum(nrm);
+    if (lane == 0) cnorm[c] = nrm;
   }
 }
 
 void launch_km_centers32(const double* centers, int k, int d, int dp, float* c32, float* cnorm,
                          hipStream_t s) {
-  hipLaunchKernelGGL(k_km_centers32, dim3((k + 255) / 256), dim3(256), 0, s, centers, k, d, dp, c32, cnorm);
+  int grid = (k + 3) / 4;
+  if (grid > 4096) grid = 4096;
+  hipLaunchKernelGGL(k_km_centers32, dim3(grid), dim3(kBlock), 0, s, centers, k, d, dp, c32, cnorm);
+}
+
+void launch_km_update(double* centers, double* weights, const double* sums, const double* counts,
+                      int k, int d, double decay, bool points_unit, double* blend, float* c32,
+                      float* cnorm, int dp, hipStream_t s) {
+  hipLaunchKernelGGL(k_km_weights, dim3(1), dim3(1024), 0, s, weights, counts, k, decay,
+                     points_unit ? 1 : 0, blend);
+  int grid = int((int64_t(k) * d + kBlock - 1) / kBlock);
+  if (grid > 8192) grid = 8192;
+  hipLaunchKernelGGL(k_km_blend, dim3(grid), dim3(kBlock), 0, s, centers, sums, blend, k, d);
+  hipLaunchKernelGGL(k_km_split, dim3(1), dim3(1024), 0, s, centers, weights, k, d);
+  launch_km_centers32(centers, k, d, dp, c32, cnorm, s);
 }
 
 }  // namespace twtml

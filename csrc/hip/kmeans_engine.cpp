@@ -39,14 +39,7 @@ KMEngine::KMEngine(int device, const KMConfig& cfg, std::shared_ptr<Comm> comm)
   TWTML_HIP_CHECK(hipSetDevice(device_));
   TWTML_HIP_CHECK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
   TWTML_HIP_CHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
-  for (auto& s : slots_) {
-    s.text = km_alloc<uint16_t>(size_t(cfg_.max_units) + 8);
-    s.offsets = km_alloc<int64_t>(size_t(cfg_.max_rows) + 1);
-    s.is_rt = km_alloc<uint8_t>(size_t(cfg_.max_rows));
-    s.scalars = km_alloc<int64_t>(5 * size_t(cfg_.max_rows));
-    TWTML_HIP_CHECK(hipEventCreateWithFlags(&s.h2d_done, hipEventDisableTiming));
-    TWTML_HIP_CHECK(hipEventCreateWithFlags(&s.consumed, hipEventDisableTiming));
-  }
+  raw_.init(cfg_.max_rows, text_bytes_for_units(cfg_.max_units));
   const int64_t R = cfg_.max_rows;
   prep_.cap_rows = R;
   prep_.kept = km_alloc<int64_t>(size_t(R));
@@ -61,10 +54,14 @@ KMEngine::KMEngine(int device, const KMConfig& cfg, std::shared_ptr<Comm> comm)
   sums_ = km_alloc<double>(k * d + k);
   mom_ = km_alloc<double>(2 * d + 2);
   stdv_ = km_alloc<double>(d);
+  fac64_ = km_alloc<double>(size_t(dp_));
+  fac32_ = km_alloc<float>(size_t(dp_));
+  blend_ = km_alloc<double>(2 * k);
   c32_ = km_alloc<float>(k * size_t(dp_));
   cnorm_ = km_alloc<float>(k);
   labels_ = km_alloc<int32_t>(size_t(R));
   order_ = km_alloc<int32_t>(size_t(R));
+  refine_ = km_alloc<int32_t>(4 * size_t(R));
   lhist_ = km_alloc<int64_t>(k + 1);
   TWTML_HIP_CHECK(hipMemset(centers_, 0, sizeof(double) * k * d));
   TWTML_HIP_CHECK(hipMemset(weights_, 0, sizeof(double) * k));
@@ -80,12 +77,9 @@ KMEngine::KMEngine(int device, const KMConfig& cfg, std::shared_ptr<Comm> comm)
 KMEngine::~KMEngine() {
   (void)hipSetDevice(device_);
   (void)hipDeviceSynchronize();
-  for (auto& s : slots_) {
-    (void)hipFree(s.text); (void)hipFree(s.offsets); (void)hipFree(s.is_rt); (void)hipFree(s.scalars);
-    (void)hipEventDestroy(s.h2d_done); (void)hipEventDestroy(s.consumed);
-  }
+  raw_.release();
   void* bufs[] = {prep_.kept, prep_.nnz, prep_.blk, prep_.hist, prep_.counters, X_, centers_,
-                  weights_, sums_, mom_, stdv_, c32_, cnorm_, labels_, order_, lhist_,
+                  weights_, sums_, mom_, stdv_, c32_, cnorm_, labels_, order_, refine_, lhist_, fac64_, fac32_, blend_,
                   lower_page_, lower_blocks_};
   for (void* b : bufs) if (b) (void)hipFree(b);
   if (host_out_) (void)hipHostFree(host_out_);
@@ -95,46 +89,26 @@ KMEngine::~KMEngine() {
   (void)hipStreamDestroy(copy_);
 }
 
-void KMEngine::submit(const HostBatch& hb, int64_t n, int64_t units, int slot) {
-  if (slot < 0 || slot > 1) throw std::invalid_argument("slot must be 0 or 1");
-  if (n < 0 || n > cfg_.max_rows || n > hb.max_rows) throw std::invalid_argument("rows exceed capacity");
-  if (units < 0 || units > cfg_.max_units || units > hb.max_units)
-    throw std::invalid_argument("text units exceed capacity");
-  if (n > 0 && hb.offsets[n] != units) throw std::invalid_argument("offsets[n] != units");
+void KMEngine::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot) {
   TWTML_HIP_CHECK(hipSetDevice(device_));
-  Slot& s = slots_[slot];
-  if (s.used) TWTML_HIP_CHECK(hipStreamWaitEvent(copy_, s.consumed, 0));
-  if (units > 0)
-    TWTML_HIP_CHECK(hipMemcpyAsync(s.text, hb.text, sizeof(uint16_t) * size_t(units), hipMemcpyHostToDevice, copy_));
-  TWTML_HIP_CHECK(hipMemcpyAsync(s.offsets, hb.offsets, sizeof(int64_t) * size_t(n + 1), hipMemcpyHostToDevice, copy_));
-  if (n > 0) {
-    TWTML_HIP_CHECK(hipMemcpyAsync(s.is_rt, hb.is_rt, size_t(n), hipMemcpyHostToDevice, copy_));
-    TWTML_HIP_CHECK(hipMemcpyAsync(s.scalars, hb.scalars, sizeof(int64_t) * 5 * size_t(n), hipMemcpyHostToDevice, copy_));
-  }
-  TWTML_HIP_CHECK(hipEventRecord(s.h2d_done, copy_));
-  s.n = n;
-  s.units = units;
-  s.used = true;
+  raw_.submit(hb, n, bytes, slot, copy_);
 }
 
 KMResult KMEngine::process(int slot, bool want_labels) {
-  if (slot < 0 || slot > 1) throw std::invalid_argument("slot must be 0 or 1");
   TWTML_HIP_CHECK(hipSetDevice(device_));
-  Slot& sl = slots_[slot];
   hipStream_t s = compute_;
   const int world = comm_ ? comm_->world() : 1;
   const int k = cfg_.k, d = d_;
   KMResult res;
-  res.n_raw = sl.n;
-  TWTML_HIP_CHECK(hipStreamWaitEvent(s, sl.h2d_done, 0));
+  const DevRawBatch b = raw_.acquire(slot, s);
+  res.n_raw = b.n;
   TWTML_HIP_CHECK(hipEventRecord(ev0_, s));
-  DevRawBatch b{sl.text, sl.offsets, sl.is_rt, sl.scalars, sl.n, sl.units};
   FeaturizeParams fp{1, 0, 1, 0, 0, 0, 0};   // filter: isRetweet only (KMeans.scala:77-80)
   TWTML_HIP_CHECK(hipMemsetAsync(prep_.counters, 0, 8 * sizeof(int64_t), s));
   launch_filter_only(b, prep_, fp, s);
   launch_km_features(b, prep_.kept, prep_.counters, X_, dp_, cfg_.text_dims, lower_page_,
                      lower_blocks_, cfg_.max_rows, s);
-  TWTML_HIP_CHECK(hipEventRecord(sl.consumed, s));
+  raw_.release_slot(slot, s);
   // scaler pass 1: n and column sums (global)
   TWTML_HIP_CHECK(hipMemsetAsync(mom_, 0, sizeof(double) * size_t(2 * d + 2), s));
   launch_km_moments(X_, prep_.counters, d, dp_, 0, mom_, mom_, cfg_.max_rows, s);
@@ -154,22 +128,22 @@ KMResult KMEngine::process(int slot, bool want_labels) {
   if (cfg_.scale) {
     launch_km_moments(X_, prep_.counters, d, dp_, 1, mom_, mom_ + d + 1, cfg_.max_rows, s);
     if (world > 1) comm_->allreduce(mom_ + d + 1, size_t(d), ncclFloat64, ncclSum, s);
-    launch_km_scale(X_, prep_.counters, d, dp_, mom_, mom_ + d + 1, stdv_, cfg_.max_rows, s);
   }
+  launch_km_factor(d, dp_, cfg_.scale != 0, mom_, mom_ + d + 1, stdv_, fac64_, fac32_, s);
   // K8 assignment with the current centres, K9 sums, K10 update.  The
-  // near-tie list reuses order_ (consumed before the label sort) and counter 5.
+  // near-tie lists in refine_, their counts in counters[5..6].
   auto* refine_cnt = reinterpret_cast<unsigned long long*>(prep_.counters + 5);
-  launch_km_assign(X_, prep_.counters, c32_, cnorm_, centers_, k, d, dp_, labels_, order_,
-                   refine_cnt, cfg_.max_rows, cfg_.mfma != 0, s);
+  launch_km_assign(X_, fac32_, fac64_, prep_.counters, c32_, cnorm_, centers_, k, d, dp_, labels_,
+                   refine_, refine_cnt, cfg_.max_rows, cfg_.mfma != 0, s);
   TWTML_HIP_CHECK(hipMemsetAsync(sums_, 0, sizeof(double) * (size_t(k) * d + k), s));
-  launch_km_cluster_sums(X_, labels_, prep_.counters, k, d, dp_, lhist_, order_, sums_,
+  launch_km_cluster_sums(X_, fac64_, labels_, prep_.counters, k, d, dp_, lhist_, order_, sums_,
                          sums_ + size_t(k) * d, cfg_.max_rows, s, &scan_excl_launch);
   if (world > 1) comm_->allreduce(sums_, size_t(k) * d + k, ncclFloat64, ncclSum, s);
   launch_km_update(centers_, weights_, sums_, sums_ + size_t(k) * d, k, d, cfg_.decay,
-                   cfg_.points_unit != 0, c32_, cnorm_, dp_, s);
+                   cfg_.points_unit != 0, blend_, c32_, cnorm_, dp_, s);
   if (want_labels)   // KMeans.scala:113 predicts with the updated model
-    launch_km_assign(X_, prep_.counters, c32_, cnorm_, centers_, k, d, dp_, labels_, order_,
-                     refine_cnt, cfg_.max_rows, cfg_.mfma != 0, s);
+    launch_km_assign(X_, fac32_, fac64_, prep_.counters, c32_, cnorm_, centers_, k, d, dp_, labels_,
+                     refine_, refine_cnt, cfg_.max_rows, cfg_.mfma != 0, s);
   TWTML_HIP_CHECK(hipEventRecord(ev1_, s));
   if (cfg_.scale)
     TWTML_HIP_CHECK(hipMemcpyAsync(host_out_ + 4, stdv_, sizeof(double) * size_t(d), hipMemcpyDeviceToHost, s));
@@ -220,9 +194,9 @@ void bind_kmeans(py::module_& m) {
              return std::make_shared<KMEngine>(device, c, comm);
            }),
            py::arg("device"), py::arg("config"), py::arg("comm") = nullptr)
-      .def("submit", [](KMEngine& e, const HostBatch& hb, int64_t n, int64_t units, int slot) {
+      .def("submit", [](KMEngine& e, const HostBatch& hb, int64_t n, int64_t bytes, int slot) {
         py::gil_scoped_release nogil;
-        e.submit(hb, n, units, slot);
+        e.submit(hb, n, bytes, slot);
       })
       .def("process", [](KMEngine& e, int slot, bool want_labels) {
         KMResult r;

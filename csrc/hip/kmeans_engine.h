@@ -35,7 +35,7 @@ class KMEngine {
  public:
   KMEngine(int device, const KMConfig& cfg, std::shared_ptr<Comm> comm);
   ~KMEngine();
-  void submit(const HostBatch& hb, int64_t n, int64_t units, int slot);
+  void submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot);
   KMResult process(int slot, bool want_labels);
   void set_state(const double* centers, const double* weights);
   void get_state(double* centers, double* weights) const;
@@ -49,20 +49,13 @@ class KMEngine {
   int d_, dp_;
   std::shared_ptr<Comm> comm_;
   hipStream_t compute_ = nullptr, copy_ = nullptr;
-  struct Slot {
-    uint16_t* text = nullptr;
-    int64_t* offsets = nullptr;
-    uint8_t* is_rt = nullptr;
-    int64_t* scalars = nullptr;
-    int64_t n = 0, units = 0;
-    hipEvent_t h2d_done = nullptr, consumed = nullptr;
-    bool used = false;
-  } slots_[2];
+  RawSlots raw_;
   DevPrepared prep_{};
   float* X_ = nullptr;
   double *centers_ = nullptr, *weights_ = nullptr, *sums_ = nullptr, *mom_ = nullptr, *stdv_ = nullptr;
-  float *c32_ = nullptr, *cnorm_ = nullptr;
-  int32_t *labels_ = nullptr, *order_ = nullptr;
+  float *c32_ = nullptr, *cnorm_ = nullptr, *fac32_ = nullptr;
+  double *fac64_ = nullptr, *blend_ = nullptr;
+  int32_t *labels_ = nullptr, *order_ = nullptr, *refine_ = nullptr;
   int64_t* lhist_ = nullptr;
   uint8_t* lower_page_ = nullptr;
   uint16_t* lower_blocks_ = nullptr;

@@ -1,0 +1,84 @@
+#include "raw_slots.h"
+
+#include <algorithm>
+#include <stdexcept>
+
+#include "engine.h"
+
+namespace twtml {
+
+template <typename T>
+static T* slot_alloc(size_t n) {
+  void* p = nullptr;
+  TWTML_HIP_CHECK(hipMalloc(&p, std::max<size_t>(1, n) * sizeof(T)));
+  return static_cast<T*>(p);
+}
+
+int RawSlots::check(int slot) {
+  if (slot < 0 || slot > 1) throw std::invalid_argument("slot must be 0 or 1");
+  return slot;
+}
+
+void RawSlots::init(int64_t max_rows, int64_t max_bytes) {
+  if (max_rows < 0 || max_bytes < 0) throw std::invalid_argument("RawSlots: negative capacity");
+  release();
+  max_rows_ = max_rows;
+  max_bytes_ = max_bytes;
+  for (auto& s : slots_) {
+    s.text = slot_alloc<uint8_t>(size_t(max_bytes) + 16);
+    s.offsets = slot_alloc<int64_t>(size_t(max_rows) + 1);
+    s.flags = slot_alloc<uint8_t>(size_t(max_rows));
+    s.scalars = slot_alloc<int64_t>(5 * size_t(max_rows));
+    TWTML_HIP_CHECK(hipEventCreateWithFlags(&s.h2d_done, hipEventDisableTiming));
+    TWTML_HIP_CHECK(hipEventCreateWithFlags(&s.consumed, hipEventDisableTiming));
+  }
+}
+
+void RawSlots::release() {
+  for (auto& s : slots_) {
+    if (s.text) (void)hipFree(s.text);
+    if (s.offsets) (void)hipFree(s.offsets);
+    if (s.flags) (void)hipFree(s.flags);
+    if (s.scalars) (void)hipFree(s.scalars);
+    if (s.h2d_done) (void)hipEventDestroy(s.h2d_done);
+    if (s.consumed) (void)hipEventDestroy(s.consumed);
+    s = Slot{};
+  }
+}
+
+void RawSlots::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, hipStream_t copy) {
+  Slot& s = slots_[check(slot)];
+  if (n < 0 || n > max_rows_ || n > hb.max_rows) throw std::invalid_argument("rows exceed capacity");
+  if (bytes < 0 || bytes > max_bytes_ || bytes > hb.max_bytes)
+    throw std::invalid_argument("text bytes exceed capacity");
+  if (hb.offsets[0] != 0 || hb.offsets[n] != bytes) throw std::invalid_argument("offsets[n] != bytes");
+  // wait until the compute stream has finished reading this slot
+  if (s.used) TWTML_HIP_CHECK(hipStreamWaitEvent(copy, s.consumed, 0));
+  if (bytes > 0)
+    TWTML_HIP_CHECK(hipMemcpyAsync(s.text, hb.text, size_t(bytes), hipMemcpyHostToDevice, copy));
+  TWTML_HIP_CHECK(hipMemcpyAsync(s.offsets, hb.offsets, sizeof(int64_t) * size_t(n + 1),
+                                 hipMemcpyHostToDevice, copy));
+  if (n > 0) {
+    TWTML_HIP_CHECK(hipMemcpyAsync(s.flags, hb.flags, size_t(n), hipMemcpyHostToDevice, copy));
+    // scalars are packed [5][n] at the start of the host buffer
+    TWTML_HIP_CHECK(hipMemcpyAsync(s.scalars, hb.scalars, sizeof(int64_t) * 5 * size_t(n),
+                                   hipMemcpyHostToDevice, copy));
+  }
+  TWTML_HIP_CHECK(hipEventRecord(s.h2d_done, copy));
+  s.n = n;
+  s.bytes = bytes;
+  s.used = true;
+}
+
+DevRawBatch RawSlots::acquire(int slot, hipStream_t compute) {
+  Slot& s = slots_[check(slot)];
+  if (!s.used) throw std::logic_error("process() on a slot that was never submitted");
+  TWTML_HIP_CHECK(hipStreamWaitEvent(compute, s.h2d_done, 0));
+  return DevRawBatch{s.text, s.offsets, s.flags, s.scalars, s.n, s.bytes};
+}
+
+void RawSlots::release_slot(int slot, hipStream_t compute) {
+  TWTML_HIP_CHECK(hipEventRecord(slots_[check(slot)].consumed, compute));
+}
+
+}  // namespace twtml

@@ -1,0 +1,51 @@
+// Double-buffered device copies of raw wire-format batches (csrc/host/wire.h).
+//
+// submit() enqueues the H2D of a pinned HostBatch on the copy stream into one
+// of two slots; the compute stream waits on that slot's h2d event and
+// records `consumed` once its kernels no longer read the raw bytes, so the
+// next H2D into the slot overlaps the rest of the batch's compute.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "kernels.h"
+
+namespace twtml {
+
+struct HostBatch;
+
+class RawSlots {
+ public:
+  RawSlots() = default;
+  RawSlots(const RawSlots&) = delete;
+  RawSlots& operator=(const RawSlots&) = delete;
+  ~RawSlots() { release(); }
+
+  void init(int64_t max_rows, int64_t max_bytes);
+  void release();
+  // H2D of rows [0, n) / `bytes` text bytes of hb into `slot` on `copy`.
+  void submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, hipStream_t copy);
+  // Make `compute` wait for the slot's H2D; returns the device view.
+  DevRawBatch acquire(int slot, hipStream_t compute);
+  // The compute stream is done reading the slot's raw bytes.
+  void release_slot(int slot, hipStream_t compute);
+  int64_t rows(int slot) const { return slots_[check(slot)].n; }
+  int64_t max_rows() const { return max_rows_; }
+  int64_t max_bytes() const { return max_bytes_; }
+
+ private:
+  static int check(int slot);
+  struct Slot {
+    uint8_t* text = nullptr;
+    int64_t* offsets = nullptr;
+    uint8_t* flags = nullptr;
+    int64_t* scalars = nullptr;
+    int64_t n = 0, bytes = 0;
+    hipEvent_t h2d_done = nullptr, consumed = nullptr;
+    bool used = false;
+  } slots_[2];
+  int64_t max_rows_ = 0, max_bytes_ = 0;
+};
+
+}  // namespace twtml

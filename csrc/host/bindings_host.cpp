@@ -9,6 +9,7 @@
 #include "featurize_cpu.h"
 #include "synth.h"
 #include "unicode_lower.h"
+#include "wire.h"
 
 namespace py = pybind11;
 using namespace twtml;
@@ -116,5 +117,34 @@ PYBIND11_MODULE(_twtml_host, m) {
 
   m.def("term_index", [](Arr<uint16_t> units, int64_t F, const std::string& hash) {
     return term_index(units.data(), int(units.size()), F, hash == "java" ? 0 : 1);
+  });
+
+  m.def("wire_bound", &wire_bound, py::arg("units"), py::arg("rows"));
+  m.def("wire_pack",
+        [](Arr<uint16_t> text, Arr<int64_t> offsets, Arr<uint8_t> is_rt, py::array out,
+           py::array out_offsets, py::array flags, int nthreads) {
+          const int64_t n = int64_t(offsets.size()) - 1;
+          if (n < 0 || is_rt.size() < n) throw std::invalid_argument("offsets / is_rt mismatch");
+          if (n > 0 && offsets.data()[n] > text.size()) throw std::invalid_argument("offsets exceed text");
+          uint8_t* o = mut_ptr<uint8_t>(out, 0, "out");
+          int64_t* oo = mut_ptr<int64_t>(out_offsets, size_t(n) + 1, "out_offsets");
+          uint8_t* f = mut_ptr<uint8_t>(flags, size_t(n), "flags");
+          py::gil_scoped_release nogil;
+          return wire_pack(text.data(), offsets.data(), is_rt.data(), n, o, int64_t(out.size()), oo, f,
+                           nthreads);
+        },
+        py::arg("text"), py::arg("offsets"), py::arg("is_rt"), py::arg("out"), py::arg("out_offsets"),
+        py::arg("flags"), py::arg("nthreads") = 0,
+        "Pack a UTF-16 batch into the narrow/wide wire format; returns bytes written.");
+  m.def("wire_unpack", [](Arr<uint8_t> wire, Arr<int64_t> woff, Arr<uint8_t> flags) {
+    const int64_t n = int64_t(woff.size()) - 1;
+    if (n < 0 || flags.size() < n) throw std::invalid_argument("woff / flags mismatch");
+    const int64_t units = wire_units(woff.data(), flags.data(), n);
+    py::array_t<uint16_t> text(units);
+    py::array_t<int64_t> offsets(n + 1);
+    py::array_t<uint8_t> is_rt(n);
+    wire_unpack(wire.data(), woff.data(), flags.data(), n, text.mutable_data(), offsets.mutable_data(),
+                is_rt.mutable_data());
+    return py::make_tuple(text, offsets, is_rt);
   });
 }

@@ -1,0 +1,100 @@
+#include "wire.h"
+
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+#include <thread>
+#include <vector>
+
+namespace twtml {
+
+namespace {
+
+bool row_narrow(const uint16_t* t, int64_t len) {
+  uint16_t acc = 0;
+  for (int64_t i = 0; i < len; ++i) acc |= t[i];
+  return acc < 256;
+}
+
+template <typename F>
+void parallel_chunks(int64_t n, int threads, F&& fn) {
+  if (threads <= 0) threads = int(std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency())));
+  const int64_t min_rows = 16384;
+  int T = int(std::min<int64_t>(std::min(threads, 64), (n + min_rows - 1) / min_rows));
+  if (T < 1) T = 1;
+  std::vector<std::thread> pool;
+  for (int c = 1; c < T; ++c) pool.emplace_back([&, c] { fn(c, T); });
+  fn(0, T);
+  for (auto& th : pool) th.join();
+}
+
+}  // namespace
+
+int64_t wire_pack(const uint16_t* text, const int64_t* offsets, const uint8_t* is_rt, int64_t n,
+                  uint8_t* out, int64_t out_cap, int64_t* out_offsets, uint8_t* flags, int threads) {
+  out_offsets[0] = 0;
+  if (n <= 0) return 0;
+  // Pass 1: encoding per row, chunk-local byte offsets; pass 2: globalise + copy.
+  // Wide rows need no alignment (the device assembles units from byte pairs).
+  std::vector<int64_t> chunk_bytes(64 + 1, 0);
+  int used = 1;
+  parallel_chunks(n, threads, [&](int c, int T) {
+    used = T;
+    const int64_t r0 = n * c / T, r1 = n * (c + 1) / T;
+    int64_t pos = 0;
+    for (int64_t r = r0; r < r1; ++r) {
+      const int64_t len = offsets[r + 1] - offsets[r];
+      const bool narrow = row_narrow(text + offsets[r], len);
+      flags[r] = uint8_t((is_rt[r] ? kWireRetweet : 0) | (narrow ? 0 : kWireWide));
+      out_offsets[r + 1] = pos + (narrow ? len : 2 * len);   // chunk-local end
+      pos = out_offsets[r + 1];
+    }
+    chunk_bytes[size_t(c) + 1] = pos;
+  });
+  for (int c = 0; c < used; ++c) chunk_bytes[size_t(c) + 1] += chunk_bytes[size_t(c)];
+  const int64_t total = chunk_bytes[size_t(used)];
+  if (total > out_cap) throw std::length_error("wire_pack: output buffer too small");
+  parallel_chunks(n, threads, [&](int c, int T) {
+    const int64_t r0 = n * c / T, r1 = n * (c + 1) / T;
+    const int64_t base = chunk_bytes[size_t(c)];
+    for (int64_t r = r0; r < r1; ++r) out_offsets[r + 1] += base;
+    for (int64_t r = r0; r < r1; ++r) {
+      const int64_t o = r == r0 ? base : out_offsets[r];
+      const uint16_t* src = text + offsets[r];
+      const int64_t len = offsets[r + 1] - offsets[r];
+      uint8_t* dst = out + o;
+      if (flags[r] & kWireWide) {
+        for (int64_t i = 0; i < len; ++i) {
+          dst[2 * i] = uint8_t(src[i] & 0xFF);
+          dst[2 * i + 1] = uint8_t(src[i] >> 8);
+        }
+      } else {
+        for (int64_t i = 0; i < len; ++i) dst[i] = uint8_t(src[i]);
+      }
+    }
+  });
+  return total;
+}
+
+int64_t wire_units(const int64_t* woff, const uint8_t* flags, int64_t n) {
+  int64_t u = 0;
+  for (int64_t r = 0; r < n; ++r) u += (woff[r + 1] - woff[r]) >> ((flags[r] & kWireWide) ? 1 : 0);
+  return u;
+}
+
+void wire_unpack(const uint8_t* wire, const int64_t* woff, const uint8_t* flags, int64_t n,
+                 uint16_t* text, int64_t* offsets, uint8_t* is_rt) {
+  offsets[0] = 0;
+  for (int64_t r = 0; r < n; ++r) {
+    const bool wide = flags[r] & kWireWide;
+    const int64_t len = (woff[r + 1] - woff[r]) >> (wide ? 1 : 0);
+    const uint8_t* src = wire + woff[r];
+    uint16_t* dst = text + offsets[r];
+    for (int64_t i = 0; i < len; ++i)
+      dst[i] = wide ? uint16_t(src[2 * i] | (uint16_t(src[2 * i + 1]) << 8)) : src[i];
+    offsets[r + 1] = offsets[r] + len;
+    is_rt[r] = flags[r] & kWireRetweet;
+  }
+}
+
+}  // namespace twtml

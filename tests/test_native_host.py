@@ -80,3 +80,40 @@ def test_prelower_rewrites_only_special_rows():
     assert changed == 2
     out = [units_to_str(text[offsets[i]:offsets[i + 1]]) for i in range(3)]
     assert out == ["i̇i abc", "plain", "οδος"]
+
+
+def _wire_roundtrip(raw, nthreads=0):
+    h = host()
+    out = np.zeros(h.wire_bound(raw.total_units, raw.n), np.uint8)
+    woff = np.zeros(raw.n + 1, np.int64)
+    flags = np.zeros(raw.n, np.uint8)
+    nb = h.wire_pack(raw.text, raw.offsets, raw.is_retweet, out, woff, flags, nthreads)
+    assert woff[raw.n] == nb
+    text, offsets, is_rt = h.wire_unpack(out[:nb], woff, flags)
+    np.testing.assert_array_equal(text, raw.text)
+    np.testing.assert_array_equal(offsets, raw.offsets)
+    np.testing.assert_array_equal(is_rt, raw.is_retweet)
+    lens = np.diff(raw.offsets)
+    wide = (flags & 2) != 0
+    np.testing.assert_array_equal(np.diff(woff), np.where(wide, 2 * lens, lens))
+    for r in range(min(raw.n, 200)):                       # narrow <=> every unit < 256
+        u = raw.text[raw.offsets[r]:raw.offsets[r + 1]]
+        assert bool(wide[r]) == bool(u.size and u.max() >= 256)
+    return nb
+
+
+@pytest.mark.parametrize("n,threads", [(0, 0), (1, 0), (777, 1), (70_000, 0), (70_000, 5)])
+def test_wire_pack_roundtrip(n, threads):
+    raw = generate_batch(SynthConfig(seed=9, unicode_fraction=0.4, special_fraction=0.05), 0, n)
+    nb = _wire_roundtrip(raw, threads)
+    assert nb <= 2 * raw.total_units
+
+
+@settings(max_examples=50, deadline=None)
+@given(st.lists(st.text(max_size=12), min_size=1, max_size=20))
+def test_wire_pack_arbitrary_text(texts):
+    units = [utf16_units(t) for t in texts]
+    offsets = np.concatenate([[0], np.cumsum([len(u) for u in units])]).astype(np.int64)
+    text = np.concatenate(units).astype(np.uint16) if offsets[-1] else np.zeros(0, np.uint16)
+    raw = RawBatch(text, offsets, np.arange(len(texts)) % 2, np.zeros((5, len(texts)), np.int64), 0)
+    _wire_roundtrip(raw)

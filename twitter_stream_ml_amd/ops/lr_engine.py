@@ -71,25 +71,29 @@ class LRDeviceConfig:
 
 
 class HostBatchView:
-    """Pinned host staging buffer with numpy views (zero-copy for H2D)."""
+    """Pinned host staging buffer in the wire format, with numpy views.
+
+    ``load`` pre-lowers the special rows, then packs the UTF-16 batch into
+    narrow (Latin-1, 1 byte/unit) / wide (UTF-16LE) rows with the native
+    multi-threaded packer (``csrc/host/wire.cpp``): typical tweet text
+    crosses PCIe at half the UTF-16 size.
+    """
 
     def __init__(self, max_rows: int, max_units: int):
-        self._hb = hip().HostBatch(int(max_rows), int(max_units))
+        self.max_units = int(max_units)
+        self._hb = hip().HostBatch(int(max_rows), int(host().wire_bound(self.max_units, int(max_rows))))
         self.text = self._hb.text
         self.offsets = self._hb.offsets
-        self.is_rt = self._hb.is_rt
+        self.flags = self._hb.flags
         self.scalars_flat = self._hb.scalars_flat
         self.n = 0
         self.units = 0
+        self.bytes = 0
         self.batch_time_ms = 0
 
     @property
     def max_rows(self) -> int:
         return self._hb.max_rows
-
-    @property
-    def max_units(self) -> int:
-        return self._hb.max_units
 
     def scalars(self) -> np.ndarray:
         return self.scalars_flat[:5 * self.n].reshape(5, self.n)
@@ -100,16 +104,16 @@ class HostBatchView:
         if n > self.max_rows or u > self.max_units:
             raise ValueError(f"batch ({n} rows, {u} units) exceeds staging capacity "
                              f"({self.max_rows}, {self.max_units})")
-        self.text[:u] = raw.text
-        self.offsets[:n + 1] = raw.offsets
-        self.is_rt[:n] = raw.is_retweet
+        self.bytes = int(host().wire_pack(raw.text, raw.offsets, raw.is_retweet, self.text,
+                                          self.offsets, self.flags))
         self.scalars_flat[:5 * n] = raw.scalars.reshape(-1)
         self.n, self.units, self.batch_time_ms = n, u, raw.batch_time_ms
         return self
 
     def as_raw(self) -> RawBatch:
-        return RawBatch(self.text[:self.units].copy(), self.offsets[:self.n + 1].copy(),
-                        self.is_rt[:self.n].copy(), self.scalars().copy(), self.batch_time_ms)
+        text, offsets, is_rt = host().wire_unpack(self.text[:self.bytes], self.offsets[:self.n + 1],
+                                                  self.flags[:self.n])
+        return RawBatch(text, offsets, is_rt, self.scalars().copy(), self.batch_time_ms)
 
 
 class DeviceLinearRegression:
@@ -142,7 +146,7 @@ class DeviceLinearRegression:
         return self._staging[i]
 
     def submit(self, hb: HostBatchView, slot: int) -> None:
-        self._eng.submit(hb._hb, int(hb.n), int(hb.units), int(slot))
+        self._eng.submit(hb._hb, int(hb.n), int(hb.bytes), int(slot))
 
     def process(self, slot: int, now_ms: int, want_pred: bool = False) -> Dict[str, object]:
         return self._eng.process(int(slot), int(now_ms), bool(want_pred))
