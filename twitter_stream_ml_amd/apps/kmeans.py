@@ -28,9 +28,12 @@ import numpy as np
 from ..config.arguments import parse_master
 from ..config.hocon import ConfigFactory, load_java_opts
 from ..models.kmeans import CpuKMeans, StreamingKMeansModel, kmeans_features
+from ..parallel.dist import barrier, check_replicas
 from ..runtime.streaming import StreamingContext
 from ..sources import make_source
+from ..utils.faults import maybe_inject
 from ..utils.logging import setup_logging
+from ._common import ResumeState, StreamCheckpointer, load_resume_state, make_watchdog
 
 __all__ = ["main", "KMeansJob", "build_kmeans_engine"]
 
@@ -51,6 +54,10 @@ def parse_args(argv: List[str]) -> argparse.Namespace:
     ap.add_argument("--sourceRate", type=float, default=50.0)
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--checkpoint", default="")
+    ap.add_argument("--checkpointInterval", type=int, default=10)
+    ap.add_argument("--resume", default="", help="model dir (warm start) or 'auto'")
+    ap.add_argument("--batchTimeout", type=float, default=0.0)
+    ap.add_argument("--checkReplicas", type=int, default=0)
     ap.add_argument("--report", action="store_true")
     return ap.parse_args(argv)
 
@@ -71,17 +78,52 @@ def build_kmeans_engine(args, dim: int, rank: int, world: int):
 
 
 class KMeansJob:
-    def __init__(self, engine, text_dims: int = 0, session=None, rank: int = 0):
+    def __init__(self, engine, text_dims: int = 0, session=None, rank: int = 0, args=None,
+                 resume: Optional[ResumeState] = None):
         self.engine = engine
         self.text_dims = text_dims
         self.session = session
         self.rank = rank
-        self.count = 0
-        self.batches = 0
+        resume = resume or ResumeState()
+        self.count = resume.count
+        self.batches = resume.batches      # stream batches seen (incl. empty ones)
+        self.records = resume.records
         self.last = None
+        ckpt = getattr(args, "checkpoint", "") if args is not None else ""
+        interval = getattr(args, "checkpointInterval", 0) if args is not None else 0
+        self.check_every = getattr(args, "checkReplicas", 0) if args is not None else 0
+        self.checkpointer = StreamCheckpointer(
+            ckpt, interval, rank,
+            lambda path, prog: StreamingKMeansModel(*self.engine.get_state()).save(path, prog),
+            barrier)
+        self.watchdog = make_watchdog(getattr(args, "batchTimeout", 0.0) if args is not None else 0.0,
+                                      getattr(engine, "comm", None))
 
     def on_batch(self, rdd, time_ms: int) -> None:
         raw = rdd.raw
+        maybe_inject(self.rank, self.batches + 1)
+        if self.watchdog is not None:
+            self.watchdog.arm()
+        try:
+            self._step(raw)
+            self.batches += 1
+            self.records += raw.n
+            if self.check_every > 0 and self.batches % self.check_every == 0:
+                check_replicas(np.concatenate([a.ravel() for a in self.engine.get_state()]),
+                               "k-means state")
+            self.checkpointer.after_batch(self.batches, self.records, self.count)
+        finally:
+            if self.watchdog is not None:
+                self.watchdog.disarm()
+
+    def final_checkpoint(self) -> None:
+        self.checkpointer.after_batch(self.batches, self.records, self.count, force=True)
+
+    def close(self) -> None:
+        if self.watchdog is not None:
+            self.watchdog.close()
+
+    def _step(self, raw) -> None:
         if hasattr(self.engine, "update_raw"):
             res = self.engine.update_raw(raw)                 # fused device pipeline
         else:
@@ -90,7 +132,6 @@ class KMeansJob:
         self.last = res
         if res["n"] == 0:
             return
-        self.batches += 1
         self.count += res["n"]
         centers, weights = self.engine.get_state()
         if log.isEnabledFor(logging.DEBUG):
@@ -115,13 +156,24 @@ def main(argv: Optional[List[str]] = None) -> int:
     from ..parallel.dist import init_distributed
     info = init_distributed(backend="nccl" if parse_master(args.master).is_gpu else "gloo")
     dim = 2 + args.textDims
+    engine = build_kmeans_engine(args, dim, info.rank, info.world)
+    resume = load_resume_state(args.resume, args.checkpoint, info.rank)
+    if resume.path:
+        model = StreamingKMeansModel.load(resume.path)
+        engine.set_state(model.clusterCenters, model.clusterWeights)
+        log.info("resumed k-means state from %s (batch %d)", resume.path, resume.batches)
+    remaining = args.numBatches
+    if args.numBatches and resume.batches:
+        remaining = max(0, args.numBatches - resume.batches)
+        if remaining == 0:
+            return 0
     log.info("Initializing Streaming Spark Context...")
-    ssc = StreamingContext(args.seconds, batch_size=args.batchSize, num_batches=args.numBatches,
+    ssc = StreamingContext(args.seconds, batch_size=args.batchSize, num_batches=remaining,
                            app_name=APP_NAME)
     log.info("Initializing Twitter stream...")
-    engine = build_kmeans_engine(args, dim, info.rank, info.world)
     stream = ssc.twitterStream(make_source(args.source, rate=args.sourceRate, seed=args.seed,
-                                           shard=info.rank, num_shards=info.world))
+                                           shard=info.rank, num_shards=info.world,
+                                           start=resume.records))
     session = None
     if info.rank == 0:
         log.info("Initializing Lightning graph session...")
@@ -133,19 +185,23 @@ def main(argv: Optional[List[str]] = None) -> int:
         if args.report:
             from ..report.session_stats import SessionStats
             session = SessionStats(lgn_host, web_host).open()
-    job = KMeansJob(engine, args.textDims, session, info.rank)
+    job = KMeansJob(engine, args.textDims, session, info.rank, args, resume)
     stream.foreachRDD(job.on_batch)
     log.info("Initialization complete.")
     ssc.start()
+    failed = False
     try:
         ssc.awaitTermination()
     except KeyboardInterrupt:
         pass
+    except BaseException:
+        failed = True
+        raise
     finally:
         ssc.stop()
-        if args.checkpoint and info.rank == 0:
-            c, w = engine.get_state()
-            StreamingKMeansModel(c, w).save(args.checkpoint)
+        if not failed:
+            job.final_checkpoint()
+        job.close()
     return 0
 
 

@@ -38,6 +38,9 @@ from ..config.arguments import ConfArguments
 from ..config.hocon import load_java_opts
 from ..models.linear_regression import CpuLinearRegression, CpuLRConfig, LinearRegressionModel
 from ..models.mllib_helper import MllibHelper
+from ..parallel.dist import barrier, check_replicas, gather_to_main
+from ..utils.faults import maybe_inject
+from ._common import ResumeState, StreamCheckpointer, load_resume_state, make_watchdog
 from ..oracle.mllib import round_half_up
 from ..records.batch import RETWEET_COUNT
 from ..report.session_stats import SessionStats
@@ -78,21 +81,44 @@ class LinearRegressionJob:
     """The driver's per-batch logic, reusable from tests and the CLI."""
 
     def __init__(self, conf: ConfArguments, engine, session: Optional[SessionStats] = None,
-                 rank: int = 0, metrics: Optional[MetricsLogger] = None):
+                 rank: int = 0, metrics: Optional[MetricsLogger] = None,
+                 resume: Optional[ResumeState] = None, world: int = 1):
         self.conf = conf
         self.engine = engine
         self.session = session
         self.rank = rank
-        self.count = 0                 # the "count" accumulator
-        self.batches = 0
+        self.world = world
+        resume = resume or ResumeState()
+        self.count = resume.count      # the "count" accumulator
+        self.batches = resume.batches  # stream batches trained into the model
+        self.records = resume.records  # source records this rank consumed
         self.metrics = metrics or MetricsLogger(None)
         self.last = None
+        self.checkpointer = StreamCheckpointer(
+            conf.checkpoint, conf.checkpointInterval, rank,
+            lambda path, prog: LinearRegressionModel(self.engine.get_weights(), 0.0).save(path, prog),
+            barrier)
+        self.watchdog = make_watchdog(conf.batchTimeout, getattr(engine, "comm", None))
 
     def on_batch(self, rdd, time_ms: int) -> None:
         raw = rdd.raw
+        maybe_inject(self.rank, self.batches + 1)
+        if self.watchdog is not None:
+            self.watchdog.arm()
         res = self.engine.train_batch(raw, want_pred=True)     # op #1 then op #2
         self.last = res
         self.batches += 1
+        self.records += raw.n
+        try:
+            self._report(raw, res, time_ms)
+            if self.conf.checkReplicas > 0 and self.batches % self.conf.checkReplicas == 0:
+                check_replicas(self.engine.get_weights(), "LR weights")
+            self.checkpointer.after_batch(self.batches, self.records, self.count)
+        finally:
+            if self.watchdog is not None:
+                self.watchdog.disarm()
+
+    def _report(self, raw, res, time_ms: int) -> None:
         batch = int(res["n_kept_global"])
         if batch == 0:
             log.debug("batch: 0")
@@ -111,6 +137,9 @@ class LinearRegressionJob:
         mask = self._kept_mask(raw)
         real = raw.scalars[RETWEET_COUNT][mask].astype(np.float64)
         pred = np.asarray(res["pred"], np.float64) if res.get("pred") is not None else np.zeros(0)
+        real_all, pred_all = real, pred
+        if self.world > 1:   # CS7: real.toArray / pred.toArray are collected to the driver
+            real_all, pred_all = gather_to_main(real), gather_to_main(pred)
         if log.isEnabledFor(logging.DEBUG):
             log.debug("count: %d", self.count)
             log.debug("batch: %d,  mse: %d", batch, int(mse))
@@ -122,20 +151,18 @@ class LinearRegressionJob:
                          iterations=res["iterations"], converged=bool(res["converged"]),
                          prep_ms=res.get("prep_ms", 0.0), train_ms=res.get("train_ms", 0.0))
         if self.session is not None and self.rank == 0:
-            self.session.update(self.count, batch, mse, real_sd, pred_sd, real, pred)
-        self._maybe_checkpoint()
+            self.session.update(self.count, batch, mse, real_sd, pred_sd, real_all, pred_all)
 
     def _kept_mask(self, raw):
         rc = raw.scalars[RETWEET_COUNT]
         return (raw.is_retweet != 0) & (rc >= self.conf.numRetweetBegin) & (rc <= self.conf.numRetweetEnd)
 
-    def _maybe_checkpoint(self, force: bool = False) -> None:
-        c = self.conf
-        if self.rank != 0 or not c.checkpoint:
-            return
-        if force or (c.checkpointInterval > 0 and self.batches % c.checkpointInterval == 0):
-            LinearRegressionModel(self.engine.get_weights(), 0.0).save(c.checkpoint)
-            log.info("checkpoint written to %s after %d batches", c.checkpoint, self.batches)
+    def final_checkpoint(self) -> None:
+        self.checkpointer.after_batch(self.batches, self.records, self.count, force=True)
+
+    def close(self) -> None:
+        if self.watchdog is not None:
+            self.watchdog.close()
 
 
 def main(argv: Optional[List[str]] = None) -> int:
@@ -158,30 +185,45 @@ def main(argv: Optional[List[str]] = None) -> int:
     MllibHelper.reset(conf)
     engine = build_engine(conf, rank, world)
     w0 = np.zeros(engine.num_weights)                      # Vectors.zeros(numFeatures)
-    if conf.resume:
-        w0 = LinearRegressionModel.load(conf.resume).weights
-        log.info("resumed %d weights from %s", w0.shape[0], conf.resume)
+    resume = load_resume_state(conf.resume, conf.checkpoint, rank)
+    if resume.path:
+        w0 = LinearRegressionModel.load(resume.path).weights
+        log.info("resumed %d weights from %s (batch %d, %d records consumed)", w0.shape[0],
+                 resume.path, resume.batches, resume.records)
     engine.set_weights(w0)
+    remaining = conf.numBatches
+    if conf.numBatches and resume.batches:
+        remaining = max(0, conf.numBatches - resume.batches)
+        if remaining == 0:
+            log.info("checkpoint already holds %d batches; nothing to do", resume.batches)
+            return 0
 
     log.info("Initializing Streaming Spark Context... %s sec/batch", conf.seconds)
-    ssc = StreamingContext(conf.seconds, batch_size=conf.batchSize, num_batches=conf.numBatches,
+    ssc = StreamingContext(conf.seconds, batch_size=conf.batchSize, num_batches=remaining,
                            app_name=conf.appName())
     log.info("Initializing Twitter stream...")
     stream = ssc.twitterStream(make_source(conf.source, rate=conf.sourceRate, seed=conf.seed,
-                                           shard=rank, num_shards=world)).cache()
+                                           shard=rank, num_shards=world,
+                                           start=resume.records)).cache()
     job = LinearRegressionJob(conf, engine, session, rank,
-                              MetricsLogger(os.environ.get("TWTML_METRICS")))
+                              MetricsLogger(os.environ.get("TWTML_METRICS")), resume, world)
     log.info("Initializing prediction model...")
     stream.foreachRDD(job.on_batch)   # op #1 (stats) + op #2 (trainOn), prequential order
     ssc.start()
     log.info("Initialization complete.")
+    failed = False
     try:
         ssc.awaitTermination()
     except KeyboardInterrupt:
         pass
+    except BaseException:
+        failed = True
+        raise
     finally:
         ssc.stop()
-        job._maybe_checkpoint(force=bool(conf.checkpoint))
+        if not failed:
+            job.final_checkpoint()
+        job.close()
         if session is not None:
             session.close()
     return 0

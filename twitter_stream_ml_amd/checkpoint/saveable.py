@@ -25,7 +25,7 @@ import json
 import os
 import shutil
 import tempfile
-from typing import Optional, Tuple
+from typing import Dict, Optional, Tuple
 
 import numpy as np
 import pyarrow as pa
@@ -59,7 +59,13 @@ def _from_udt(d: dict) -> np.ndarray:
     return out
 
 
-def _write_dir(path: str, metadata: dict, table: pa.Table, extra: Optional[dict] = None) -> None:
+def _write_dir(path: str, metadata: dict, table: pa.Table,
+               streaming: Optional[Dict[str, dict]] = None) -> None:
+    """Write a Saveable directory atomically (tmp dir + rename).
+
+    ``streaming`` holds extension JSON files (cluster weights, stream
+    progress) under ``<path>/streaming/`` -- MLlib loaders ignore them.
+    """
     parent = os.path.dirname(os.path.abspath(path)) or "."
     os.makedirs(parent, exist_ok=True)
     tmp = tempfile.mkdtemp(prefix=".twtml-ckpt-", dir=parent)
@@ -71,10 +77,11 @@ def _write_dir(path: str, metadata: dict, table: pa.Table, extra: Optional[dict]
         open(os.path.join(tmp, "metadata", "_SUCCESS"), "w").close()
         pq.write_table(table, os.path.join(tmp, "data", "part-00000.parquet"))
         open(os.path.join(tmp, "data", "_SUCCESS"), "w").close()
-        if extra:
+        if streaming:
             os.makedirs(os.path.join(tmp, "streaming"))
-            with open(os.path.join(tmp, "streaming", "weights.json"), "w") as fh:
-                json.dump(extra, fh)
+            for name, obj in streaming.items():
+                with open(os.path.join(tmp, "streaming", name), "w") as fh:
+                    json.dump(obj, fh)
         if os.path.exists(path):
             old = path + ".old"
             shutil.rmtree(old, ignore_errors=True)
@@ -104,11 +111,13 @@ def _read_data(path: str) -> pa.Table:
     return pa.concat_tables([pq.read_table(os.path.join(d, f)) for f in files])
 
 
-def save_linear_regression(path: str, weights: np.ndarray, intercept: float = 0.0) -> None:
+def save_linear_regression(path: str, weights: np.ndarray, intercept: float = 0.0,
+                           progress: Optional[dict] = None) -> None:
     w = np.asarray(weights, dtype=np.float64)
     schema = pa.schema([pa.field("weights", vector_udt_type()), pa.field("intercept", pa.float64())])
     table = pa.Table.from_pylist([{"weights": _dense(w), "intercept": float(intercept)}], schema)
-    _write_dir(path, {"class": LR_CLASS, "version": "1.0", "numFeatures": int(w.shape[0])}, table)
+    _write_dir(path, {"class": LR_CLASS, "version": "1.0", "numFeatures": int(w.shape[0])}, table,
+               {"progress.json": progress} if progress else None)
 
 
 def load_linear_regression(path: str) -> Tuple[np.ndarray, float]:
@@ -122,12 +131,17 @@ def load_linear_regression(path: str) -> Tuple[np.ndarray, float]:
     return w, float(rows[0]["intercept"])
 
 
-def save_kmeans(path: str, centers: np.ndarray, weights: Optional[np.ndarray] = None) -> None:
+def save_kmeans(path: str, centers: np.ndarray, weights: Optional[np.ndarray] = None,
+                progress: Optional[dict] = None) -> None:
     c = np.asarray(centers, dtype=np.float64)
     schema = pa.schema([pa.field("id", pa.int32()), pa.field("point", vector_udt_type())])
     table = pa.Table.from_pylist([{"id": i, "point": _dense(c[i])} for i in range(c.shape[0])], schema)
-    extra = {"clusterWeights": np.asarray(weights, np.float64).tolist()} if weights is not None else None
-    _write_dir(path, {"class": KMEANS_CLASS, "version": "1.0", "k": int(c.shape[0])}, table, extra)
+    files: Dict[str, dict] = {}
+    if weights is not None:
+        files["weights.json"] = {"clusterWeights": np.asarray(weights, np.float64).tolist()}
+    if progress:
+        files["progress.json"] = progress
+    _write_dir(path, {"class": KMEANS_CLASS, "version": "1.0", "k": int(c.shape[0])}, table, files)
 
 
 def load_kmeans(path: str) -> Tuple[np.ndarray, Optional[np.ndarray]]:
@@ -142,3 +156,12 @@ def load_kmeans(path: str) -> Tuple[np.ndarray, Optional[np.ndarray]]:
         with open(wpath) as fh:
             weights = np.asarray(json.load(fh)["clusterWeights"], np.float64)
     return centers, weights
+
+
+def load_progress(path: str) -> Optional[dict]:
+    """Stream progress stored with a model (``{"batches": t, ...}``) or None."""
+    p = os.path.join(path, "streaming", "progress.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as fh:
+        return json.load(fh)

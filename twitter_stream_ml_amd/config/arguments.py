@@ -17,7 +17,8 @@ ConfArguments.scala:6-164``) kept here:
 Extensions for the MI355X engine are long flags only (the reference's 16
 short letters keep their meaning): ``--source``, ``--batchSize``,
 ``--numBatches``, ``--hash``, ``--checkpoint``, ``--checkpointInterval``,
-``--resume``, ``--sourceRate``, ``--plotPoints``, ``--legacyNumTextFeatures``.
+``--resume``, ``--sourceRate``, ``--plotPoints``, ``--legacyNumTextFeatures``,
+``--batchTimeout``, ``--checkReplicas``.
 The master accepts, besides Spark's ``local``, ``local[N]``, ``local[*]``
 (CPU plumbing engine, fp64), the device masters ``rocm``, ``rocm[N]``,
 ``rocm[*]`` and ``rocm:0,1,...`` (HIP engine, one process per GPU).
@@ -134,6 +135,8 @@ _EXT_FLAGS = {
     "--resume": ("resume", str),
     "--plotPoints": ("plotPoints", int),
     "--seed": ("seed", int),
+    "--batchTimeout": ("batchTimeout", float),
+    "--checkReplicas": ("checkReplicas", int),
 }
 
 _FLAG_LOOKUP = {}
@@ -185,6 +188,8 @@ class ConfArguments:
         self.resume = ""
         self.plotPoints = c.getInt("plotPoints") if c.hasPath("plotPoints") else 0
         self.seed = 42
+        self.batchTimeout = 0.0
+        self.checkReplicas = 0
 
         self.usage = f"""
 Usage: python -m twitter_stream_ml_amd.apps.linear_regression
@@ -216,7 +221,11 @@ Usage: twtml-spark [options]
   --numBatches <stop after N batches, 0 = never>  Default: 0
   --hash <java|murmur3>                           Default: {self.hash}
   --checkpoint <dir>  --checkpointInterval <n>    Default: off / {self.checkpointInterval}
-  --resume <dir>                                  warm start from an MLlib model dir
+  --resume <dir|auto>                             warm start from an MLlib model dir
+                                                  (auto: the --checkpoint dir if present,
+                                                  continuing its stream position)
+  --batchTimeout <seconds>                        abort the process if a batch hangs (0 = off)
+  --checkReplicas <n>                             verify DP replicas agree every n batches
   --plotPoints <n>                                points per Lightning append (0 = all)
   --legacyNumTextFeatures                         reproduce the reference bug: ignore -f
   """
@@ -295,9 +304,10 @@ Usage: twtml-spark [options]
         elif attr in ("lightning", "twtweb"):
             setattr(self, attr, value)
         elif attr == "seconds":
-            # extension: sub-second intervals ("0.5"); integers parse as in Scala
+            # extension: sub-second intervals ("0.5"); integers parse as in Scala;
+            # 0 = no timer, batches are sealed by --batchSize alone
             v = _java_int(value) if value.strip().lstrip("+-").isdigit() else float(value)
-            if v <= 0:
+            if v < 0:
                 raise ValueError(value)
             self.seconds = v
         elif attr in ("numIterations", "numRetweetBegin", "numRetweetEnd",

@@ -121,9 +121,9 @@ class StreamingKMeansModel:
         self.state, labels = kmeans_update(self.state, X, decayFactor, timeUnit, allreduce)
         return self
 
-    def save(self, path: str) -> None:
+    def save(self, path: str, progress: Optional[dict] = None) -> None:
         from ..checkpoint.saveable import save_kmeans
-        save_kmeans(path, self.state.centers, self.state.weights)
+        save_kmeans(path, self.state.centers, self.state.weights, progress)
 
     @classmethod
     def load(cls, path: str) -> "StreamingKMeansModel":

@@ -57,9 +57,9 @@ class LinearRegressionModel:
         arr = np.asarray(x, dtype=np.float64)
         return arr @ self.weights + self.intercept
 
-    def save(self, path: str) -> None:
+    def save(self, path: str, progress: Optional[dict] = None) -> None:
         from ..checkpoint.saveable import save_linear_regression
-        save_linear_regression(path, self.weights, self.intercept)
+        save_linear_regression(path, self.weights, self.intercept, progress)
 
     @classmethod
     def load(cls, path: str) -> "LinearRegressionModel":

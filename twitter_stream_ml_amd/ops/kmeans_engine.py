@@ -65,6 +65,7 @@ class DeviceKMeans:
         self.cfg = cfg
         self.device = int(device)
         self.dim = 2 + int(cfg.text_dims)
+        self.comm = comm
         self._eng = hip().KMEngine(self.device, cfg.as_dict(), comm)
         st = KMeansState.random(cfg.k, self.dim, cfg.init_weight, cfg.seed)
         self.set_state(st.centers, st.weights)

@@ -122,6 +122,7 @@ class DeviceLinearRegression:
     def __init__(self, cfg: LRDeviceConfig, device: int = 0, comm=None):
         self.cfg = cfg
         self.device = int(device)
+        self.comm = comm
         self._eng = hip().LREngine(self.device, cfg.as_dict(), comm)
         self._staging: List[HostBatchView] = []
 

@@ -24,7 +24,8 @@ from typing import Callable, Optional
 import numpy as np
 
 __all__ = ["DistInfo", "init_distributed", "dist_info", "make_rccl_comm", "allreduce_fn",
-           "barrier", "allreduce_max_scalar", "allreduce_sum_scalar", "shutdown"]
+           "barrier", "allreduce_max_scalar", "allreduce_sum_scalar", "shutdown",
+           "check_replicas", "replica_digest", "ReplicaDivergence", "gather_to_main"]
 
 
 @dataclass(frozen=True)
@@ -130,6 +131,64 @@ def allreduce_max_scalar(x: float) -> float:
 
 def allreduce_sum_scalar(x: float) -> float:
     return _reduce_scalar(x, "sum")
+
+
+class ReplicaDivergence(RuntimeError):
+    """Data-parallel replicas of the model no longer agree bit for bit."""
+
+
+def replica_digest(arr: np.ndarray) -> int:
+    """64-bit digest of an array's bytes (order-sensitive, exact)."""
+    import hashlib
+    h = hashlib.blake2b(np.ascontiguousarray(arr).tobytes(), digest_size=8)
+    return int.from_bytes(h.digest(), "little", signed=True)
+
+
+def check_replicas(arr: np.ndarray, what: str = "model") -> None:
+    """Race/divergence detector: all ranks must hold identical
+    replicas.  MIN and MAX all-reduces of a digest differ iff any rank
+    disagrees; raises :class:`ReplicaDivergence` on every rank."""
+    info = dist_info()
+    if info.world <= 1:
+        return
+    import torch
+    import torch.distributed as dist
+    d = replica_digest(arr)
+    dev = "cuda" if info.backend == "nccl" else "cpu"
+    lo = torch.tensor([d], dtype=torch.int64, device=dev)
+    hi = lo.clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    if int(lo.item()) != int(hi.item()):
+        raise ReplicaDivergence(f"{what} replicas diverged across ranks (digest on rank "
+                                f"{info.rank}: {d:#x})")
+
+
+def gather_to_main(arr: np.ndarray) -> Optional[np.ndarray]:
+    """Concatenate every rank's 1-D float64 array on rank 0 (None elsewhere).
+
+    CS7/CS11: the reference ``collect``s the batch's real/predicted values to
+    the driver for the Lightning plot; here each rank's shard is gathered
+    once per batch, off the training path."""
+    info = dist_info()
+    a = np.ascontiguousarray(arr, dtype=np.float64).reshape(-1)
+    if info.world <= 1:
+        return a
+    import torch
+    import torch.distributed as dist
+    dev = "cuda" if info.backend == "nccl" else "cpu"
+    n = torch.tensor([a.shape[0]], dtype=torch.int64, device=dev)
+    sizes = [torch.zeros_like(n) for _ in range(info.world)]
+    dist.all_gather(sizes, n)
+    sizes = [int(s.item()) for s in sizes]
+    m = max(sizes) if sizes else 0
+    buf = torch.zeros(max(m, 1), dtype=torch.float64, device=dev)
+    buf[:a.shape[0]] = torch.from_numpy(a).to(dev)
+    parts = [torch.zeros_like(buf) for _ in range(info.world)]
+    dist.all_gather(parts, buf)   # all_gather: supported by gloo and RCCL alike
+    if info.rank != 0:
+        return None
+    return np.concatenate([p[:s].cpu().numpy() for p, s in zip(parts, sizes)])
 
 
 def shutdown() -> None:

@@ -12,7 +12,14 @@ Semantics kept from Spark Streaming 1.6:
   ``foreachRDD(predict+stats)`` registered before ``model.trainOn(stream)``
   sees the model of batch t-1 and training then consumes batch t
   (prequential test-then-train, ``LinearRegression.scala:53-86``);
-* batches that take longer than the interval queue up (scheduling delay).
+* batches that take longer than the interval queue up (scheduling delay);
+  with ``max_pending`` the receiver stops pulling while that many sealed
+  batches wait (backpressure, ``spark.streaming.backpressure.enabled``).
+
+Size-sealed batches (``batch_size > 0``, ``batch_seconds <= 0``) contain
+exactly ``batch_size`` records in source order, so a stream position is just
+"records consumed" (``records_done``) -- what checkpoints store for an exact
+resume after a failure.
 
 ``DStream`` transformations (``filter``/``map``/``cache``) are lazy per batch;
 an output operation receives an :class:`RDD`.  ``run_batches`` drives the same
@@ -151,7 +158,7 @@ class ReceiverDStream(DStream):
 
 class StreamingContext:
     def __init__(self, batch_seconds: float = 5.0, batch_size: int = 0, num_batches: int = 0,
-                 app_name: str = "", poll_chunk: int = 4096):
+                 app_name: str = "", poll_chunk: int = 4096, max_pending: int = 8):
         if batch_seconds <= 0 and batch_size <= 0:
             raise ValueError("need batch_seconds > 0 or batch_size > 0")
         self.batch_seconds = float(batch_seconds)
@@ -159,6 +166,8 @@ class StreamingContext:
         self.num_batches = int(num_batches)
         self.app_name = app_name
         self.poll_chunk = poll_chunk
+        self.max_pending = int(max_pending)
+        self.records_done = 0            # records of all processed batches (stream position)
         self._outputs: List[tuple] = []
         self._inputs: List[ReceiverDStream] = []
         self._buffer: List[RawBatch] = []
@@ -169,6 +178,7 @@ class StreamingContext:
         self._done = threading.Event()
         self._threads: List[threading.Thread] = []
         self.batches_done = 0
+        self._sealed = 0
         self.batch_infos: List[BatchInfo] = []
         self.error: Optional[BaseException] = None
         self.on_batch_completed: List[Callable[[BatchInfo], None]] = []
@@ -196,6 +206,7 @@ class StreamingContext:
             fn(rdd, batch.batch_time_ms) if with_time else fn(rdd)
         info.processing_end_s = time.monotonic()
         self.batches_done += 1
+        self.records_done += batch.n
         self.batch_infos.append(info)
         for cb in self.on_batch_completed:
             cb(info)
@@ -218,8 +229,21 @@ class StreamingContext:
     def _receiver_loop(self, stream: ReceiverDStream) -> None:
         src = stream.source
         while not self._stop.is_set():
+            if self.num_batches and self._sealed >= self.num_batches:
+                self._stop.wait(0.05)           # all requested batches are sealed
+                continue
+            if self.max_pending > 0 and self._jobs.qsize() >= self.max_pending:
+                self._stop.wait(0.005)          # backpressure: executor is behind
+                continue
+            want = self.poll_chunk
+            if self.batch_size > 0:             # never overfill: exact-size batches
+                with self._lock:
+                    want = min(want, self.batch_size - self._buffered)
+                if want <= 0:
+                    self._seal()
+                    continue
             try:
-                chunk = src.poll(self.poll_chunk, now_ms=int(time.time() * 1000))
+                chunk = src.poll(want, now_ms=int(time.time() * 1000))
             except Exception as e:  # receiver restart semantics: log and retry
                 log.warning("receiver error, restarting: %s", e)
                 time.sleep(0.5)
@@ -234,8 +258,11 @@ class StreamingContext:
                 time.sleep(0.01)
 
     def _seal(self) -> None:
+        if self.num_batches and self._sealed >= self.num_batches:
+            return                              # never seal past the requested count
         with self._lock:
             parts, self._buffer, self._buffered = self._buffer, [], 0
+            self._sealed += 1
         t_ms = int(time.time() * 1000)
         batch = RawBatch.concat(parts, t_ms) if parts else RawBatch.empty(t_ms)
         batch.batch_time_ms = t_ms

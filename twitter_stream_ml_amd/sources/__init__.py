@@ -9,13 +9,14 @@ __all__ = ["JsonlReplaySource", "write_jsonl", "SynthConfig", "SyntheticTweetSou
 
 
 def make_source(spec: str, rate: float = 0.0, seed: int = 1, profile: str = "twitter",
-                shard: int = 0, num_shards: int = 1):
-    """``--source`` value -> source object."""
+                shard: int = 0, num_shards: int = 1, start: int = 0):
+    """``--source`` value -> source object; ``start`` = records already consumed."""
     if spec in ("", "synthetic"):
         return SyntheticTweetSource(SynthConfig.profile(profile, seed=seed), rate=rate,
-                                    shard=shard, num_shards=num_shards)
+                                    shard=shard, num_shards=num_shards, start=start)
     if spec.startswith("replay:"):
-        return JsonlReplaySource(spec[len("replay:"):], rate=rate)
+        return JsonlReplaySource(spec[len("replay:"):], rate=rate, skip=start, shard=shard,
+                                 num_shards=num_shards)
     if spec == "twitter":
         return TwitterSource()
     raise ValueError(f"unknown source {spec!r}")
