@@ -161,6 +161,13 @@ def build_all(force: bool = False, verbose: bool = False, hip: bool = True) -> N
         build_hip(force, verbose)
 
 
+def main(argv=None) -> int:
+    """``twtml-build [--force] [-v] [--host-only]``: compile the in-tree extensions."""
+    argv = sys.argv[1:] if argv is None else argv
+    build_all(force="--force" in argv, verbose="-v" in argv or "--verbose" in argv,
+              hip="--host-only" not in argv)
+    return 0
+
+
 if __name__ == "__main__":
-    build_all(force="--force" in sys.argv, verbose="-v" in sys.argv or "--verbose" in sys.argv,
-              hip="--host-only" not in sys.argv)
+    sys.exit(main())

@@ -1,4 +1,4 @@
-"""Tweet sources: synthetic (seeded C++ generator), JSONL replay, live Twitter stub."""
+"""Tweet sources: synthetic (seeded C++ generator), JSONL replay, live Twitter stream."""
 from .replay import JsonlReplaySource, write_jsonl
 from .synthetic import SynthConfig, SyntheticTweetSource, generate_batch, generate_into
 from .twitter import TwitterSource, TwitterUnavailable
@@ -18,5 +18,5 @@ def make_source(spec: str, rate: float = 0.0, seed: int = 1, profile: str = "twi
         return JsonlReplaySource(spec[len("replay:"):], rate=rate, skip=start, shard=shard,
                                  num_shards=num_shards)
     if spec == "twitter":
-        return TwitterSource()
+        return TwitterSource().start()          # fails fast without OAuth keys
     raise ValueError(f"unknown source {spec!r}")
