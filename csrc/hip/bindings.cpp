@@ -32,7 +32,7 @@ static LRConfig lr_config(const py::dict& d) {
   GET(num_iterations, int32_t) GET(fraction, double) GET(tol, double) GET(begin, int64_t)
   GET(end, int64_t) GET(require_retweet, int32_t) GET(range_filter, int32_t)
   GET(max_rows, int64_t) GET(max_units, int64_t) GET(sgd_grid, int32_t)
-  GET(early_exit_depth, int32_t) GET(ablate, int32_t)
+  GET(early_exit_depth, int32_t) GET(ablate, int32_t) GET(dedup, int32_t)
 #undef GET
   return c;
 }
@@ -164,6 +164,15 @@ PYBIND11_MODULE(_twtml_hip, m) {
         d["y"] = py::array_t<float>(py::ssize_t(y.size()), y.data());
         d["num"] = py::array_t<float>(py::ssize_t(num.size()), num.data());
         d["uniq"] = py::array_t<int32_t>(py::ssize_t(uniq.size()), uniq.data());
+        return d;
+      })
+      .def("debug_merged", [](const LREngine& e) {
+        std::vector<int32_t> slot, cnt, clen8d;
+        e.debug_merged(slot, cnt, clen8d);
+        py::dict d;
+        d["slot"] = py::array_t<int32_t>(py::ssize_t(slot.size()), slot.data());
+        d["cnt"] = py::array_t<int32_t>(py::ssize_t(cnt.size()), cnt.data());
+        d["clen8d"] = py::array_t<int32_t>(py::ssize_t(clen8d.size()), clen8d.data());
         return d;
       })
       .def("set_step", &LREngine::set_step)

@@ -92,6 +92,8 @@ void LREngine::alloc_prepared() {
   prep_.blk = dmalloc<int64_t>(size_t(R / kBlock + 2));
   prep_.hist = dmalloc<int64_t>(kLenBuckets + 1);
   prep_.clen8 = dmalloc<int32_t>(size_t(C) + 1);
+  prep_.clen8d = dmalloc<int32_t>(size_t(C) + 1);
+  prep_.cnt = dmalloc<uint16_t>(size_t(E));
   prep_.cbase = dmalloc<int64_t>(size_t(C) + 1);
   prep_.idx = dmalloc<int32_t>(size_t(E));
   prep_.slot = dmalloc<uint32_t>(size_t(E));
@@ -133,6 +135,7 @@ LREngine::~LREngine() {
   raw_.release();
   for (auto& e : ev_) (void)hipEventDestroy(e);
   void* bufs[] = {prep_.kept, prep_.nnz, prep_.sorted, prep_.blk, prep_.hist, prep_.clen8,
+                  prep_.clen8d, prep_.cnt,
                   prep_.cbase, prep_.idx, prep_.slot, prep_.y, prep_.num, prep_.perm,
                   prep_.flags, prep_.uniq, prep_.slot_of, prep_.ublk, prep_.counters,
                   sgd_.w64, sgd_.wc64, sgd_.wc32, sgd_.g64, sgd_.red64, sgd_.stats, sgd_.state,
@@ -205,6 +208,8 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   sgd_.n_unique = nU;
   const bool u16 = ns <= 65536;
   launch_remap(prep_, res.entries, nU, u16, s);
+  prep_.dedup = (cfg_.dedup && u16 && dedup_supported(ns)) ? 1 : 0;
+  if (prep_.dedup) launch_dedup(prep_, ns, kNumNumeric + nU, res.n_kept, s);
   TWTML_HIP_CHECK(hipMemsetAsync(sgd_.state, 0, 8 * sizeof(double), s));
   TWTML_HIP_CHECK(hipMemsetAsync(sgd_.stats, 0, 8 * sizeof(double), s));
   TWTML_HIP_CHECK(hipMemsetAsync(sgd_.red64, 0, 4 * sizeof(double), s));
@@ -225,6 +230,8 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   sp.want_pred = want_pred ? 1 : 0;
   sp.sample = cfg_.fraction < 1.0 ? 1 : 0;
   sp.ablate = cfg_.ablate;
+  // entries one workgroup can add into a slot: its share of the chunks (x2 for imbalance)
+  sp.fix_lim = sgd_fix_limit(2 * (res.entries / std::max(1, grid)) + 65536);
   if (n_glob > 0) {
     for (int i = 1; i <= cfg_.num_iterations; ++i) {
       sp.iteration = i;
@@ -289,6 +296,27 @@ void LREngine::synchronize() {
   TWTML_HIP_CHECK(hipSetDevice(device_));
   TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
   TWTML_HIP_CHECK(hipStreamSynchronize(copy_));
+}
+
+void LREngine::debug_merged(std::vector<int32_t>& slot, std::vector<int32_t>& cnt,
+                            std::vector<int32_t>& clen8d) const {
+  TWTML_HIP_CHECK(hipSetDevice(device_));
+  TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
+  slot.clear(); cnt.clear(); clen8d.clear();
+  if (!prep_.dedup) return;
+  int64_t counters[4];
+  TWTML_HIP_CHECK(hipMemcpy(counters, prep_.counters, sizeof(counters), hipMemcpyDeviceToHost));
+  const int64_t C = (counters[0] + kRowsPerChunk - 1) / kRowsPerChunk;
+  const int64_t E = counters[2] * kChunkStride;
+  std::vector<uint16_t> s16(static_cast<size_t>(E)), c16(static_cast<size_t>(E));
+  clen8d.resize(size_t(C));
+  if (E) {
+    TWTML_HIP_CHECK(hipMemcpy(s16.data(), prep_.slot, sizeof(uint16_t) * size_t(E), hipMemcpyDeviceToHost));
+    TWTML_HIP_CHECK(hipMemcpy(c16.data(), prep_.cnt, sizeof(uint16_t) * size_t(E), hipMemcpyDeviceToHost));
+  }
+  if (C) TWTML_HIP_CHECK(hipMemcpy(clen8d.data(), prep_.clen8d, sizeof(int32_t) * size_t(C), hipMemcpyDeviceToHost));
+  slot.assign(s16.begin(), s16.end());
+  cnt.assign(c16.begin(), c16.end());
 }
 
 void LREngine::debug_prepared(std::vector<int64_t>& counters, std::vector<int32_t>& clen8,

@@ -38,6 +38,7 @@ struct LRConfig {
   int32_t sgd_grid = 0;       // 0 = auto
   int32_t early_exit_depth = 3;  // host run-ahead (iterations) for early stop
   int32_t ablate = 0;            // perf diagnostics only (see SgdParams)
+  int32_t dedup = 0;             // merge repeated bigrams of a row into counts
 };
 
 // Pinned staging buffer of one raw batch in the wire format
@@ -91,6 +92,9 @@ class LREngine {
                       std::vector<int64_t>& cbase, std::vector<int32_t>& idx,
                       std::vector<int32_t>& perm, std::vector<float>& y,
                       std::vector<float>& num, std::vector<int32_t>& uniq);
+  // Merged (slot, count) layout the iteration kernels read (empty if not merged).
+  void debug_merged(std::vector<int32_t>& slot, std::vector<int32_t>& cnt,
+                    std::vector<int32_t>& clen8d) const;
 
  private:
   void alloc_prepared();

@@ -283,16 +283,34 @@ __device__ __forceinline__ int64_t term_mod(int64_t h, int64_t F) {
 constexpr int kFlagLds = 1 << 16;
 constexpr int kFlagWords = kFlagLds / 32;
 
-// One wave per 16-row chunk; the 4 lanes of a row take entries j = t, t+4, ...
+// Latin-1 lower-casing in closed form (narrow rows): A-Z and U+00C0..U+00DE
+// except U+00D7 map to +0x20; nothing else in 0..255 changes under
+// Character.toLowerCase.
+__device__ __forceinline__ uint32_t lower_latin1(uint32_t c) {
+  return ((c - 'A' <= 'Z' - 'A') || (c - 0xC0u <= 0xDEu - 0xC0u && c != 0xD7u)) ? c + 32u : c;
+}
+
+constexpr int kStageWords = 160;                 // 640 B per staged row (>= 280 wide units)
+constexpr int kFeatWaves = kBlock / kWave;
+
+// One wave per 16-row chunk.  Per chunk the wave first resolves the 16 rows'
+// metadata (lanes 0..15), then stages the rows' bytes into LDS with up to 48
+// independent aligned dword loads in flight -- one memory latency per chunk
+// instead of one per bigram (byte loads from global memory may alias the
+// output stores, which serialised the old per-entry loop).  The 4 lanes of a
+// row then take entries j = t, t+4, ... from LDS and write 8 entries per
+// lane with two 16-byte stores.  Rows too long to stage read global memory.
 __global__ __launch_bounds__(kBlock) void k_featurize(DevRawBatch b, DevPrepared p, FeaturizeParams fp,
                                                       const uint8_t* lpage, const uint16_t* lblocks,
                                                       int64_t cmax) {
   __shared__ uint32_t fbits[kFlagWords];
+  __shared__ uint32_t stage[kFeatWaves][kRowsPerChunk * kStageWords];
   for (int i = threadIdx.x; i < kFlagWords; i += kBlock) fbits[i] = 0u;
   __syncthreads();
   const int64_t n_kept = p.counters[0];
   const int lane = lane_id();
   const int r = lane / kLanesPerRow, t = lane % kLanesPerRow;
+  uint32_t* st = stage[threadIdx.x / kWave];
   const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = int64_t(gridDim.x) * kBlock / kWave;
   const int64_t F = fp.num_text_features;
@@ -300,41 +318,97 @@ __global__ __launch_bounds__(kBlock) void k_featurize(DevRawBatch b, DevPrepared
   const int64_t cap_groups = p.cap_entries / kChunkStride;
   const int64_t nch = (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;
   for (int64_t c = wave; c < nch && c < cmax; c += nwaves) {
-    const int64_t pos = c * kRowsPerChunk + r;
-    const bool valid = pos < n_kept;
-    const int32_t kidx = valid ? p.sorted[pos] : -1;
-    const int64_t row = valid ? p.kept[kidx] : 0;
     const int32_t L8 = p.clen8[c];
     const int64_t g0 = p.cbase[c];
     if (g0 + L8 > cap_groups) {
       if (lane == 0) p.counters[3] = 1;  // capacity overflow -> host raises
       continue;
     }
-    RowText rt{0, 0, 0};
-    if (valid) rt = row_text(b, row);
-    const int64_t len = rt.len;
+    // 1. row metadata: lane l resolves row (l & 15)
+    const int64_t mpos = c * kRowsPerChunk + (lane & 15);
+    const bool mvalid = mpos < n_kept;
+    const int32_t mkidx = mvalid ? p.sorted[mpos] : -1;
+    const int64_t mrow = mvalid ? p.kept[mkidx] : 0;
+    int64_t mo = 0, mbytes = 0;
+    int mwide = 0;
+    if (mvalid) {
+      mo = b.offsets[mrow];
+      mbytes = b.offsets[mrow + 1] - mo;
+      mwide = (b.flags[mrow] & kRowWide) ? 1 : 0;
+    }
+    const int64_t ma = mo & ~int64_t(3);
+    const int mob = int(mo - ma);
+    const int mndw = int((mob + mbytes + 3) >> 2);
+    const int mstaged = mndw <= kStageWords ? mndw : 0;
+    // 2. stage all 16 rows (loads first, then LDS writes)
+    uint32_t tmp[kRowsPerChunk][3];
+#pragma unroll
+    for (int q = 0; q < kRowsPerChunk; ++q) {
+      const int64_t qa = __shfl(ma, q, kWave);
+      const int qn = __shfl(mstaged, q, kWave);
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(b.text + qa);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) tmp[q][k] = (lane + kWave * k < qn) ? src[lane + kWave * k] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < kRowsPerChunk; ++q)
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        if (lane + kWave * k < kStageWords) st[q * kStageWords + lane + kWave * k] = tmp[q][k];
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+    // 3. bigrams of row r, entries j = t, t+4, ...
+    const int64_t pos = c * kRowsPerChunk + r;
+    const bool valid = pos < n_kept;
+    const int32_t kidx = __shfl(mkidx, r, kWave);
+    const int64_t row = __shfl(mrow, r, kWave);
+    const int wide = __shfl(mwide, r, kWave);
+    const int staged = __shfl(mstaged, r, kWave);
+    const int ob = __shfl(mob, r, kWave);
+    const RowText rt{__shfl(mo, r, kWave), __shfl(mbytes, r, kWave) >> wide, wide};
+    const int64_t len = valid ? rt.len : 0;
     const int64_t nz = len >= 2 ? len - 1 : len;
+    const uint8_t* sb = reinterpret_cast<const uint8_t*>(st + r * kStageWords) + ob;
+    auto unit = [&](int64_t j) -> uint32_t {
+      if (staged) {
+        if (!wide) return lower_latin1(sb[j]);
+        return lower_dev(uint32_t(sb[2 * j]) | (uint32_t(sb[2 * j + 1]) << 8), lpage, lblocks);
+      }
+      return lower_dev(row_unit(b, rt, j), lpage, lblocks);
+    };
     int32_t* out = p.idx + g0 * kChunkStride + lane * kGroup;
     const int32_t total = L8 * kGroup;
-    for (int32_t jj = 0; jj < total; ++jj) {
-      const int64_t j = int64_t(jj) * kLanesPerRow + t;
-      int32_t v = -1;
-      if (j < nz) {
-        const uint32_t u0 = lower_dev(row_unit(b, rt, j), lpage, lblocks);
-        int64_t h;
-        if (len >= 2) {
-          const uint32_t u1 = lower_dev(row_unit(b, rt, j + 1), lpage, lblocks);
-          h = fp.hash_kind == 0 ? int64_t(31u * u0 + u1) : int64_t(murmur_term(u0, u1, 2));
-        } else {
-          h = fp.hash_kind == 0 ? int64_t(u0) : int64_t(murmur_term(u0, 0, 1));
+    for (int32_t jj0 = 0; jj0 < total; jj0 += kGroup) {
+      int32_t v[kGroup];
+#pragma unroll
+      for (int k = 0; k < kGroup; ++k) {
+        const int64_t j = int64_t(jj0 + k) * kLanesPerRow + t;
+        v[k] = -1;
+        if (j < nz) {
+          const uint32_t u0 = unit(j);
+          int64_t h;
+          if (len >= 2) {
+            const uint32_t u1 = unit(j + 1);
+            h = fp.hash_kind == 0 ? int64_t(31u * u0 + u1) : int64_t(murmur_term(u0, u1, 2));
+          } else {
+            h = fp.hash_kind == 0 ? int64_t(u0) : int64_t(murmur_term(u0, 0, 1));
+          }
+          const int64_t idx = term_mod(h, F);
+          v[k] = int32_t(idx);
+          if (idx < lds_lim) {
+            // hot ids are flagged early: a (broadcast) read skips the atomic
+            const uint32_t bit = 1u << (idx & 31);
+            if (!(fbits[idx >> 5] & bit)) atomicOr(&fbits[idx >> 5], bit);
+          } else if (idx < p.flag_len) {
+            p.flags[idx] = 1;
+          }
         }
-        const int64_t idx = term_mod(h, F);
-        v = int32_t(idx);
-        if (idx < lds_lim) atomicOr(&fbits[idx >> 5], 1u << (idx & 31));
-        else if (idx < p.flag_len) p.flags[idx] = 1;
       }
-      out[(jj >> 3) * kChunkStride + (jj & 7)] = v;
+      int4* dst = reinterpret_cast<int4*>(out + (jj0 >> 3) * kChunkStride);
+      dst[0] = make_int4(v[0], v[1], v[2], v[3]);
+      dst[1] = make_int4(v[4], v[5], v[6], v[7]);
     }
+    __builtin_amdgcn_wave_barrier();   // LDS reads of this chunk precede the next staging
     if (t == 0) {
       const int64_t cap = p.cap_rows16;
       if (valid) {
@@ -483,6 +557,111 @@ void launch_remap(const DevPrepared& p, int64_t entries, int64_t n_unique, bool 
   else
     hipLaunchKernelGGL(k_remap<uint32_t>, dim3(grid), dim3(kBlock), 0, s, p.idx, p.slot_of,
                        static_cast<uint32_t*>(p.slot), entries, pad_base);
+}
+
+// ---------------------------------------------------------------------------
+// Per-row duplicate merging (u16 slots, small active sets).  HashingTF gives a
+// term its count; the SELL rows hold one entry per bigram occurrence, and
+// short texts repeat bigrams a lot ("the ... the").  One wave per chunk walks
+// its 16 rows one at a time with all 64 lanes: an LDS tag array (seen[slot] =
+// row tag; tags are unique per row, so it is never cleared) elects one owner
+// per distinct slot, an LDS counter array counts occurrences, and owners are
+// compacted in entry order (ballot prefix) with their counts.  Chunk lengths
+// shrink accordingly (clen8d); every GD iteration then touches each
+// (row, term) once.
+// ---------------------------------------------------------------------------
+constexpr int kDedupWaves = 2;
+
+__device__ __forceinline__ int64_t sell_addr(int r, int64_t j) {
+  const int64_t m = j >> 2;
+  return (m >> 3) * kChunkStride + (4 * r + int(j & 3)) * kGroup + (m & 7);
+}
+
+__global__ __launch_bounds__(kDedupWaves * kWave) void k_dedup(DevPrepared p, int64_t ns, int64_t pad_base) {
+  extern __shared__ uint32_t dsm[];
+  const int w = threadIdx.x / kWave, lane = lane_id();
+  uint32_t* seen = dsm + int64_t(w) * 2 * ns;
+  uint32_t* cnt = seen + ns;
+  for (int64_t s = lane; s < ns; s += kWave) seen[s] = 0u;
+  __threadfence_block();
+  __builtin_amdgcn_wave_barrier();
+  const int64_t n_kept = p.counters[0];
+  const int64_t nch = (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;
+  const int64_t wave = (int64_t(blockIdx.x) * kDedupWaves + w);
+  const int64_t nwaves = int64_t(gridDim.x) * kDedupWaves;
+  uint16_t* slot = static_cast<uint16_t*>(p.slot);
+  // a row has L8 * 32 entries -> L8 / 2 per lane; rows up to kMaxRegGroups
+  // groups (what the iteration kernel keeps in registers) are merged
+  constexpr int kMaxPer = (kMaxRegGroups + 1) / 2;
+  for (int64_t c = wave; c < nch; c += nwaves) {
+    const int32_t L8 = p.clen8[c];
+    const int64_t base = p.cbase[c] * kChunkStride;
+    uint16_t* sl = slot + base;
+    uint16_t* cn = p.cnt + base;
+    if (L8 > 2 * kMaxPer) {   // very long rows: keep as they are, count 1
+      for (int64_t e = lane; e < int64_t(L8) * kChunkStride; e += kWave) cn[e] = sl[e] < pad_base ? 1 : 0;
+      if (lane == 0) p.clen8d[c] = L8;
+      continue;
+    }
+    const int per = (L8 * 32 + kWave - 1) / kWave;        // entries per lane for one row
+    int32_t maxn = 0;
+    for (int r = 0; r < kRowsPerChunk; ++r) {
+      const uint32_t tag = uint32_t(c * kRowsPerChunk + r + 1);
+      uint32_t s[kMaxPer];
+      bool own[kMaxPer];
+#pragma unroll
+      for (int i = 0; i < kMaxPer; ++i) {
+        const int64_t j = lane + int64_t(kWave) * i;
+        s[i] = (i < per && j < int64_t(L8) * 32) ? sl[sell_addr(r, j)] : 0xFFFFu;
+        own[i] = false;
+        if (s[i] < pad_base) {
+          own[i] = atomicExch(&seen[s[i]], tag) != tag;
+          if (own[i]) cnt[s[i]] = 0u;
+        }
+      }
+      __threadfence_block();
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int i = 0; i < kMaxPer; ++i)
+        if (s[i] < pad_base) atomicAdd(&cnt[s[i]], 1u);
+      __threadfence_block();
+      __builtin_amdgcn_wave_barrier();
+      int32_t n_own = 0;
+#pragma unroll
+      for (int i = 0; i < kMaxPer; ++i) {
+        const uint64_t m = __ballot(own[i]);
+        if (own[i]) {
+          const int64_t jn = n_own + __popcll(m & ((1ull << lane) - 1ull));
+          const int64_t a = sell_addr(r, jn);
+          const uint32_t k = cnt[s[i]];
+          sl[a] = uint16_t(s[i]);
+          cn[a] = uint16_t(k < 65535u ? k : 65535u);
+        }
+        n_own += __popcll(m);
+      }
+      // pads after the merged entries (per-lane pad slot, count 0)
+      for (int64_t j = n_own + lane; j < int64_t(L8) * 32; j += kWave) {
+        const int64_t a = sell_addr(r, j);
+        sl[a] = uint16_t(pad_base + ((4 * r + (j & 3)) & 63));
+        cn[a] = 0;
+      }
+      maxn = n_own > maxn ? n_own : maxn;
+      __threadfence_block();
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (lane == 0) p.clen8d[c] = (maxn + 31) / 32;   // 32 entries per row-group (4 lanes x 8)
+  }
+}
+
+bool dedup_supported(int64_t ns) { return ns <= 8192; }
+
+void launch_dedup(const DevPrepared& p, int64_t ns, int64_t pad_base, int64_t n_kept, hipStream_t s) {
+  const int64_t nch = (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;
+  if (nch == 0) return;
+  int grid = int((nch + kDedupWaves - 1) / kDedupWaves);
+  if (grid > 4096) grid = 4096;
+  const size_t lds = size_t(kDedupWaves) * 2 * size_t(ns) * sizeof(uint32_t);
+  hipLaunchKernelGGL(k_dedup, dim3(grid), dim3(kDedupWaves * kWave), lds, s, p, ns, pad_base);
 }
 
 // ---------------------------------------------------------------------------

@@ -71,6 +71,11 @@ struct DevPrepared {
   int32_t* uniq;            // [Fh]  sorted touched feature ids
   int32_t* slot_of;         // [Fh]  feature id -> slot (valid for touched ids)
   int64_t* ublk;            // [Fh/4096+2]
+  // per-row duplicate merging (HashingTF term counts): slots rewritten in
+  // place as (slot, count) with the count in `cnt`, chunk lengths in clen8d
+  uint16_t* cnt;            // [E]   term count per entry (0 = pad); valid if dedup
+  int32_t* clen8d;          // [C]   groups per lane after merging
+  int32_t dedup;            // 1: iteration kernels use cnt / clen8d
   // counters (device): [0]=n_kept [1]=n_unique [2]=groups [3]=error
   int64_t* counters;
   int64_t cap_rows, cap_rows16, cap_entries, cap_chunks, flag_len;
@@ -94,6 +99,9 @@ void launch_featurize(const DevRawBatch& b, const DevPrepared& p, const Featuriz
                       const uint8_t* lower_page, const uint16_t* lower_blocks, hipStream_t s);
 void launch_compact_active(const DevPrepared& p, hipStream_t s);
 void launch_remap(const DevPrepared& p, int64_t entries, int64_t n_unique, bool u16, hipStream_t s);
+// per-row duplicate merging for u16 slot spaces up to 8192 slots
+bool dedup_supported(int64_t ns);
+void launch_dedup(const DevPrepared& p, int64_t ns, int64_t pad_base, int64_t n_kept, hipStream_t s);
 
 // ---------------------------------------------------------------------------
 // SGD on the compact active set.
@@ -122,7 +130,12 @@ struct SgdParams {
   int32_t want_pred;
   int32_t sample;       // fraction < 1
   int32_t ablate;       // perf diagnostics: 1 = skip scatter, 2 = skip gather+scatter
+  float fix_lim;        // |r| * 2^24 clamp so a workgroup's int64 slot sums cannot overflow
 };
+
+// Fixed-point clamp for a launch: every slot of a workgroup receives at most
+// `entries_per_wg` contributions, each |q| <= lim, so lim * entries < 2^62.
+float sgd_fix_limit(int64_t entries_per_wg);
 
 void launch_gather_w(const DevSgd& d, const DevPrepared& p, hipStream_t s);
 void launch_norm2(const double* v, int64_t n, double* out, hipStream_t s);

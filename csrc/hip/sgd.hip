@@ -37,8 +37,9 @@ namespace twtml {
 
 // Fixed-point scale of the LDS gradient: residuals are added as
 // round(r * 2^24) (resolution 6e-8, finer than fp32 for |r| > 1).  |r| is
-// clamped to 2^26 so a workgroup sum of up to 2^12 rows cannot overflow int64;
-// a clamp raises the overflow flag (state[7]) and the host reports it.
+// clamped (at most 2^26, tighter when a workgroup sees more entries, see
+// sgd_fix_limit) so a workgroup's int64 slot sums cannot overflow; a clamp
+// raises the overflow flag (state[7]) and the host reports it.
 constexpr float kFixScale = 16777216.0f;        // 2^24
 constexpr double kFixInv = 1.0 / 16777216.0;
 constexpr float kFixClamp = 67108864.0f;        // 2^26
@@ -131,9 +132,14 @@ __device__ __forceinline__ void flush_scalars(const DevSgd& d, const RowAcc& acc
   }
 }
 
-__device__ __forceinline__ unsigned long long to_fix(float r, bool& clamped) {
+float sgd_fix_limit(int64_t entries_per_wg) {
+  const double e = double(entries_per_wg < 1 ? 1 : entries_per_wg);
+  const double lim = std::min(double(kFixClamp) * double(kFixScale), 4.611686018427388e18 / e);
+  return float(lim * 0.999);
+}
+
+__device__ __forceinline__ unsigned long long to_fix(float r, bool& clamped, float lim) {
   float v = r * kFixScale;
-  const float lim = kFixClamp * kFixScale;
   if (fabsf(v) > lim) {
     clamped = true;
     v = v > 0.f ? lim : -lim;
@@ -144,9 +150,11 @@ __device__ __forceinline__ unsigned long long to_fix(float r, bool& clamped) {
 // ---------------------------------------------------------------------------
 // Fast path: u16 slots, LDS weights + REP replicated fixed-point gradients.
 // ---------------------------------------------------------------------------
-constexpr int kIterBlock = 512;
+constexpr int kIterBlock = 1024;
 
-template <bool STATS, bool SAMPLE, int REP>
+// CNT: entries carry HashingTF term counts (p.cnt, merged duplicates, chunk
+// lengths p.clen8d); otherwise every entry counts once.
+template <bool STATS, bool SAMPLE, int REP, bool CNT>
 __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_lds(DevSgd d, DevPrepared p, SgdParams sp) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   __shared__ double scratch[kIterBlock / kWave];
@@ -170,22 +178,36 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_lds(DevSgd d, DevPrepar
   bool clamped = false;
 
   for (int64_t c = wave; c < nch; c += nwaves) {
-    const int32_t L8 = p.clen8[c];
-    const uint16_t* sl = slot + p.cbase[c] * kChunkStride + lane * kGroup;
+    const int32_t L8 = CNT ? p.clen8d[c] : p.clen8[c];
+    const int64_t off = p.cbase[c] * kChunkStride + lane * kGroup;
+    const uint16_t* sl = slot + off;
     const int64_t pos = c * kRowsPerChunk + r;
     if (L8 <= kMaxRegGroups) {
       uint4 v[kMaxRegGroups];
+      uint4 cv[CNT ? kMaxRegGroups : 1];
 #pragma unroll
       for (int g = 0; g < kMaxRegGroups; ++g)
-        if (g < L8) v[g] = *reinterpret_cast<const uint4*>(sl + int64_t(g) * kChunkStride);
+        if (g < L8) {
+          v[g] = *reinterpret_cast<const uint4*>(sl + int64_t(g) * kChunkStride);
+          if (CNT) cv[g] = *reinterpret_cast<const uint4*>(p.cnt + off + int64_t(g) * kChunkStride);
+        }
       float d0 = 0.f, d1 = 0.f;
 #pragma unroll
       for (int g = 0; g < kMaxRegGroups; ++g) {
         if (g < L8 && sp.ablate < 2) {
           uint32_t s[8];
           unpack8(v[g], s);
-          d0 += wl[s[0]] + wl[s[2]] + wl[s[4]] + wl[s[6]];
-          d1 += wl[s[1]] + wl[s[3]] + wl[s[5]] + wl[s[7]];
+          if (CNT) {
+            uint32_t k[8];
+            unpack8(cv[g], k);
+            d0 += wl[s[0]] * float(k[0]) + wl[s[2]] * float(k[2]) + wl[s[4]] * float(k[4]) +
+                  wl[s[6]] * float(k[6]);
+            d1 += wl[s[1]] * float(k[1]) + wl[s[3]] * float(k[3]) + wl[s[5]] * float(k[5]) +
+                  wl[s[7]] * float(k[7]);
+          } else {
+            d0 += wl[s[0]] + wl[s[2]] + wl[s[4]] + wl[s[6]];
+            d1 += wl[s[1]] + wl[s[3]] + wl[s[5]] + wl[s[7]];
+          }
         }
       }
       float dot = d0 + d1;
@@ -198,18 +220,25 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_lds(DevSgd d, DevPrepar
       dot += __shfl_xor(dot, 2, kWave);
       const float res = row_residual<STATS, SAMPLE>(dot, pos, t, d, p, sp, n_kept, w0, w1, w2, w3, acc);
       if (res != 0.f && sp.ablate == 0) {
-        const unsigned long long q = to_fix(res, clamped);
+        const unsigned long long q = to_fix(res, clamped, sp.fix_lim);
 #pragma unroll
         for (int g = 0; g < kMaxRegGroups; ++g) {
           if (g < L8) {
             uint32_t s[8];
             unpack8(v[g], s);
+            if (CNT) {
+              uint32_t k[8];
+              unpack8(cv[g], k);
 #pragma unroll
-            for (int k = 0; k < 8; ++k) atomicAdd(&gl[s[k] * REP + rep], q);
+              for (int e = 0; e < 8; ++e) atomicAdd(&gl[s[e] * REP + rep], q * (unsigned long long)k[e]);
+            } else {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) atomicAdd(&gl[s[e] * REP + rep], q);
+            }
           }
         }
       }
-    } else {  // very long rows: stream the slots twice
+    } else {  // very long rows: stream the slots twice (never merged: count 1)
       float dot = 0.f;
       for (int32_t g = 0; g < L8; ++g) {
         uint32_t s[8];
@@ -221,7 +250,7 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_lds(DevSgd d, DevPrepar
       dot += __shfl_xor(dot, 2, kWave);
       const float res = row_residual<STATS, SAMPLE>(dot, pos, t, d, p, sp, n_kept, w0, w1, w2, w3, acc);
       if (res != 0.f) {
-        const unsigned long long q = to_fix(res, clamped);
+        const unsigned long long q = to_fix(res, clamped, sp.fix_lim);
         for (int32_t g = 0; g < L8; ++g) {
           uint32_t s[8];
           unpack8(*reinterpret_cast<const uint4*>(sl + int64_t(g) * kChunkStride), s);
@@ -321,12 +350,16 @@ static void launch_iter_t(const DevSgd& d, const DevPrepared& p, const SgdParams
                           int rep, int grid, hipStream_t s) {
   if (u16 && rep > 0) {
     const size_t lds = size_t(lds_bytes(d.ns, rep));
+#define TWTML_ITER(R, C) \
+  hipLaunchKernelGGL((k_sgd_iter_lds<STATS, SAMPLE, R, C>), dim3(grid), dim3(kIterBlock), lds, s, d, p, sp)
+    const bool cnt = p.dedup != 0;
     switch (rep) {
-      case 8: hipLaunchKernelGGL((k_sgd_iter_lds<STATS, SAMPLE, 8>), dim3(grid), dim3(kIterBlock), lds, s, d, p, sp); break;
-      case 4: hipLaunchKernelGGL((k_sgd_iter_lds<STATS, SAMPLE, 4>), dim3(grid), dim3(kIterBlock), lds, s, d, p, sp); break;
-      case 2: hipLaunchKernelGGL((k_sgd_iter_lds<STATS, SAMPLE, 2>), dim3(grid), dim3(kIterBlock), lds, s, d, p, sp); break;
-      default: hipLaunchKernelGGL((k_sgd_iter_lds<STATS, SAMPLE, 1>), dim3(grid), dim3(kIterBlock), lds, s, d, p, sp); break;
+      case 8: if (cnt) TWTML_ITER(8, true); else TWTML_ITER(8, false); break;
+      case 4: if (cnt) TWTML_ITER(4, true); else TWTML_ITER(4, false); break;
+      case 2: if (cnt) TWTML_ITER(2, true); else TWTML_ITER(2, false); break;
+      default: if (cnt) TWTML_ITER(1, true); else TWTML_ITER(1, false); break;
     }
+#undef TWTML_ITER
   } else if (u16) {
     hipLaunchKernelGGL((k_sgd_iter_global<uint16_t, STATS, SAMPLE>), dim3(grid * 2), dim3(kBlock), 0, s, d, p, sp);
   } else {

@@ -77,10 +77,10 @@ def test_featurize_matches_oracle(hip_module, F, hash):
     np.testing.assert_allclose(num, want_num, rtol=2e-7, atol=0)
 
 
-@pytest.mark.parametrize("F", [1000, 1 << 20])
-def test_sgd_matches_oracle_over_batches(hip_module, F):
+@pytest.mark.parametrize("F,dedup", [(1000, False), (1 << 20, False), (1000, True)])
+def test_sgd_matches_oracle_over_batches(hip_module, F, dedup):
     cfg = SynthConfig.profile("twitter", seed=5, unicode_fraction=0.1)
-    eng = _engine(F, step_size=0.005, num_iterations=50)
+    eng = _engine(F, step_size=0.005, num_iterations=50, dedup=dedup)
     w = np.zeros(F + 4)
     for t in range(4):
         raw = generate_batch(cfg, t * 2500, 2500, batch_time_ms=NOW + t * 5000)
@@ -130,3 +130,39 @@ def test_empty_and_filtered_out_batch(hip_module):
     res = eng.train_batch(raw)
     assert res["n_kept"] == 0 and res["iterations"] == 0
     assert np.all(eng.get_weights() == 0)
+
+
+def test_merged_counts_match_hashingtf(hip_module):
+    """Per-row duplicate merging: (slot, count) entries == HashingTF term counts."""
+    F = 1000
+    cfg = SynthConfig.profile("twitter", seed=12, unicode_fraction=0.2)
+    raw = generate_batch(cfg, 0, 3000, batch_time_ms=NOW)
+    eng = _engine(F, "java", dedup=True)
+    eng.train_batch(raw, want_pred=False)
+    dbg = eng._eng.debug_prepared()
+    mg = eng._eng.debug_merged()
+    assert mg["clen8d"].shape[0] > 0, "merging should be active for a small active set"
+    assert np.all(mg["clen8d"] <= dbg["clen8"])
+    uniq = np.sort(dbg["uniq"])
+    nU = uniq.shape[0]
+    fb = featurize_batch(raw, F, 100, 1000, now_ms=NOW)
+    Xt = fb.X[:, :F].tocsr()
+    perm, cbase = dbg["perm"], dbg["cbase"]
+    slot, cnt = mg["slot"], mg["cnt"]
+    for c in range(mg["clen8d"].shape[0]):
+        g0, L8 = int(cbase[c]), int(mg["clen8d"][c])
+        blk_s = slot[g0 * 512:(g0 + L8) * 512].reshape(L8, 64, 8)
+        blk_c = cnt[g0 * 512:(g0 + L8) * 512].reshape(L8, 64, 8)
+        for r in range(16):
+            k = int(perm[c * 16 + r])
+            if k < 0:
+                continue
+            s = blk_s[:, 4 * r:4 * r + 4, :].reshape(-1)
+            n = blk_c[:, 4 * r:4 * r + 4, :].reshape(-1)
+            real = (s >= 4) & (s < 4 + nU) & (n > 0)
+            ids = uniq[s[real] - 4]
+            assert np.unique(ids).shape[0] == ids.shape[0], f"row {k} not merged"
+            got = dict(zip(ids.tolist(), n[real].tolist()))
+            a, b = Xt.indptr[k], Xt.indptr[k + 1]
+            want = dict(zip(Xt.indices[a:b].tolist(), Xt.data[a:b].astype(int).tolist()))
+            assert got == want, f"row {k}"
