@@ -3,6 +3,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
@@ -73,6 +75,10 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
   TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_out_),
                                 (32 + size_t(std::max(1, cfg_.num_iterations))) * sizeof(double),
                                 hipHostMallocDefault));
+  TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_flags_),
+                                (2 + size_t(std::max(1, cfg_.num_iterations))) * sizeof(double),
+                                hipHostMallocMapped | hipHostMallocCoherent));
+  TWTML_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&sgd_.host_flags), host_flags_, 0));
   TWTML_HIP_CHECK(hipDeviceSynchronize());
 }
 
@@ -143,6 +149,8 @@ LREngine::~LREngine() {
   for (void* b : bufs) if (b) (void)hipFree(b);
   if (host_counters_) (void)hipHostFree(host_counters_);
   if (host_out_) (void)hipHostFree(host_out_);
+  if (host_flags_) (void)hipHostFree(host_flags_);
+  for (auto e : iter_events_) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(compute_);
   (void)hipStreamDestroy(copy_);
 }
@@ -233,7 +241,28 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   // entries one workgroup can add into a slot: its share of the chunks (x2 for imbalance)
   sp.fix_lim = sgd_fix_limit(2 * (res.entries / std::max(1, grid)) + 65536);
   if (n_glob > 0) {
+    // Host-side early stop: the convergence flag (state[0]) of iteration i is
+    // copied to pinned memory behind an event; the host keeps at most
+    // `depth` iterations queued ahead and stops enqueueing once the flag of
+    // an earlier iteration is set.  The flag derives from all-reduced values,
+    // so every rank stops at the same iteration and the collectives match.
+    const int depth = std::max(1, cfg_.early_exit_depth);
+    const int iters = cfg_.num_iterations;
+    if (int(iter_events_.size()) < iters + 1) {
+      for (int k = int(iter_events_.size()); k < iters + 1; ++k) {
+        hipEvent_t e;
+        TWTML_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        iter_events_.push_back(e);
+      }
+    }
     for (int i = 1; i <= cfg_.num_iterations; ++i) {
+      if (i > depth) {
+        const int j = i - depth;                       // flag after iteration j
+        TWTML_HIP_CHECK(hipEventSynchronize(iter_events_[size_t(j)]));
+        if (std::getenv("TWTML_DEBUG_EARLY"))
+          std::fprintf(stderr, "early-stop check i=%d j=%d flag=%g\n", i, j, host_flags_[j]);
+        if (host_flags_[j] != 0.0) break;
+      }
       sp.iteration = i;
       if (res.n_kept > 0) launch_sgd_iter(sgd_, prep_, sp, host_counters_[2], u16, grid, s);
       else if (i == 1 || sp.sample) {
@@ -243,7 +272,8 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
         comm_->allreduce(sgd_.g64, size_t(ns + 1), ncclFloat64, ncclSum, s);
         if (sp.sample) comm_->allreduce(sgd_.red64, 2, ncclFloat64, ncclSum, s);
       }
-      launch_sgd_update(sgd_, sp, s);
+      launch_sgd_update(sgd_, sp, s);   // writes host_flags_[i] (zero copy)
+      TWTML_HIP_CHECK(hipEventRecord(iter_events_[size_t(i)], s));
     }
     launch_scatter_w(sgd_, prep_, s);
   }

@@ -112,6 +112,8 @@ class LREngine {
   uint16_t* lower_blocks_ = nullptr;
   int64_t* host_counters_ = nullptr;  // pinned [8]
   double* host_out_ = nullptr;        // pinned [16 + iters]
+  double* host_flags_ = nullptr;      // pinned [iters + 1] convergence flag per iteration
+  std::vector<hipEvent_t> iter_events_;
   int64_t* n_global_ = nullptr;       // device [world + 1]
   hipEvent_t ev_[4] = {nullptr, nullptr, nullptr, nullptr};
   int num_cu_ = 256;

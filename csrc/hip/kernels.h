@@ -115,6 +115,7 @@ struct DevSgd {
   double* state;        // [8] 0 done 1 converged 2 n_updates 3 iters 4 wrest2 5 m_global 6 wnorm2_full
   double* loss_hist;    // [max_iters+1]
   float* pred_out;      // [R] rounded predictions in kept order (optional)
+  double* host_flags;   // [max_iters+1] pinned host memory: done flag after each update
   int64_t F;
   int64_t ns;           // 4 + n_unique + pads (rounded)
   int64_t n_unique;

@@ -445,6 +445,10 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp) {
     }
     d.state[3] = double(sp.iteration);
     if (sp.iteration >= sp.num_iterations) d.state[0] = 1.0;
+    if (d.host_flags) {               // zero-copy early-stop signal to the host
+      d.host_flags[sp.iteration] = d.state[0];
+      __threadfence_system();
+    }
     d.g64[d.ns] = 0.0;
     d.red64[0] = 0.0;
     d.red64[1] = 0.0;
