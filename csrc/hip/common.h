@@ -82,6 +82,18 @@ __device__ __forceinline__ double round_half_away(double x) {
   const double t = trunc(x);
   return fabs(x - t) >= 0.5 ? t + (x > 0 ? 1.0 : -1.0) : t;
 }
+
+// x mod d for 32-bit x and a runtime divisor, without an integer division
+// (Lemire, Kaser & Kurz 2019: M = floor((2^64 - 1) / d) + 1, then
+// mod = hi64((M * x mod 2^64) * d)).  One 64-bit division per thread setup.
+struct FastMod32 {
+  uint64_t M = 1;
+  uint32_t d = 1;
+  __device__ __forceinline__ explicit FastMod32(uint32_t div) : M(~0ull / div + 1ull), d(div) {}
+  __device__ __forceinline__ uint32_t mod(uint32_t x) const {
+    return uint32_t(__umul64hi(M * uint64_t(x), uint64_t(d)));
+  }
+};
 #endif
 
 inline int ceil_div(long long a, long long b) { return int((a + b - 1) / b); }

@@ -20,6 +20,7 @@
 #include "../common/unicode_tables.h"
 #include "common.h"
 #include "kernels.h"
+#include "text_stage.h"
 
 namespace twtml {
 
@@ -215,10 +216,6 @@ void launch_chunk_layout(const DevRawBatch& b, const DevPrepared& p, hipStream_t
 // ---------------------------------------------------------------------------
 // K1 + K2: lower-case, bigram hash, numeric features, active-set flags.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t lower_dev(uint32_t c, const uint8_t* page, const uint16_t* blocks) {
-  if (c < 128) return (c >= 'A' && c <= 'Z') ? c + 32 : c;
-  return (c + blocks[page[c >> 8] * 256 + (c & 255)]) & 0xFFFFu;
-}
 
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
 __device__ __forceinline__ uint32_t mur_k(uint32_t k) { return rotl32(k * 0xCC9E2D51u, 15) * 0x1B873593u; }
@@ -266,11 +263,14 @@ __device__ int32_t murmur_term(uint32_t u0, uint32_t u1, int n) {
   return int32_t(h);
 }
 
-__device__ __forceinline__ int64_t term_mod(int64_t h, int64_t F) {
+// nonNegativeMod(h, F).  Hashes are 32-bit (Java hashCode / murmur3), so with
+// F < 2^32 the reduction is a multiply-high (FastMod32), not a division.
+__device__ __forceinline__ int64_t term_mod(int64_t h, int64_t F, const FastMod32& fm, bool f32) {
   if (h >= 0 && h < F) return h;                 // java bigrams (< 2^21) with F >= 2^21
-  if (F <= 0x7fffffff && h >= -0x7fffffffLL && h <= 0x7fffffffLL) {   // 32-bit path
-    const int32_t m = int32_t(h) % int32_t(F);
-    return m < 0 ? m + F : m;
+  if (f32 && h >= -0xffffffffLL && h <= 0xffffffffLL) {
+    if (h >= 0) return fm.mod(uint32_t(h));
+    const uint32_t r = fm.mod(uint32_t(-h));
+    return r == 0 ? 0 : F - r;
   }
   const int64_t m = h % F;
   return m < 0 ? m + F : m;
@@ -283,14 +283,6 @@ __device__ __forceinline__ int64_t term_mod(int64_t h, int64_t F) {
 constexpr int kFlagLds = 1 << 16;
 constexpr int kFlagWords = kFlagLds / 32;
 
-// Latin-1 lower-casing in closed form (narrow rows): A-Z and U+00C0..U+00DE
-// except U+00D7 map to +0x20; nothing else in 0..255 changes under
-// Character.toLowerCase.
-__device__ __forceinline__ uint32_t lower_latin1(uint32_t c) {
-  return ((c - 'A' <= 'Z' - 'A') || (c - 0xC0u <= 0xDEu - 0xC0u && c != 0xD7u)) ? c + 32u : c;
-}
-
-constexpr int kStageWords = 160;                 // 640 B per staged row (>= 280 wide units)
 constexpr int kFeatWaves = kBlock / kWave;
 
 // One wave per 16-row chunk.  Per chunk the wave first resolves the 16 rows'
@@ -304,7 +296,7 @@ __global__ __launch_bounds__(kBlock) void k_featurize(DevRawBatch b, DevPrepared
                                                       const uint8_t* lpage, const uint16_t* lblocks,
                                                       int64_t cmax) {
   __shared__ uint32_t fbits[kFlagWords];
-  __shared__ uint32_t stage[kFeatWaves][kRowsPerChunk * kStageWords];
+  __shared__ uint32_t stage[kFeatWaves][kRowsPerChunk * kStageStride];
   for (int i = threadIdx.x; i < kFlagWords; i += kBlock) fbits[i] = 0u;
   __syncthreads();
   const int64_t n_kept = p.counters[0];
@@ -314,6 +306,8 @@ __global__ __launch_bounds__(kBlock) void k_featurize(DevRawBatch b, DevPrepared
   const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = int64_t(gridDim.x) * kBlock / kWave;
   const int64_t F = fp.num_text_features;
+  const bool f32 = F <= 0xffffffffLL;
+  const FastMod32 fm(f32 ? uint32_t(F) : 1u);
   const int64_t lds_lim = p.flag_len < kFlagLds ? p.flag_len : kFlagLds;
   const int64_t cap_groups = p.cap_entries / kChunkStride;
   const int64_t nch = (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;
@@ -324,58 +318,21 @@ __global__ __launch_bounds__(kBlock) void k_featurize(DevRawBatch b, DevPrepared
       if (lane == 0) p.counters[3] = 1;  // capacity overflow -> host raises
       continue;
     }
-    // 1. row metadata: lane l resolves row (l & 15)
+    // 1. row metadata (lane l resolves row l & 15), 2. stage the 16 rows
     const int64_t mpos = c * kRowsPerChunk + (lane & 15);
     const bool mvalid = mpos < n_kept;
     const int32_t mkidx = mvalid ? p.sorted[mpos] : -1;
-    const int64_t mrow = mvalid ? p.kept[mkidx] : 0;
-    int64_t mo = 0, mbytes = 0;
-    int mwide = 0;
-    if (mvalid) {
-      mo = b.offsets[mrow];
-      mbytes = b.offsets[mrow + 1] - mo;
-      mwide = (b.flags[mrow] & kRowWide) ? 1 : 0;
-    }
-    const int64_t ma = mo & ~int64_t(3);
-    const int mob = int(mo - ma);
-    const int mndw = int((mob + mbytes + 3) >> 2);
-    const int mstaged = mndw <= kStageWords ? mndw : 0;
-    // 2. stage all 16 rows (loads first, then LDS writes)
-    uint32_t tmp[kRowsPerChunk][3];
-#pragma unroll
-    for (int q = 0; q < kRowsPerChunk; ++q) {
-      const int64_t qa = __shfl(ma, q, kWave);
-      const int qn = __shfl(mstaged, q, kWave);
-      const uint32_t* src = reinterpret_cast<const uint32_t*>(b.text + qa);
-#pragma unroll
-      for (int k = 0; k < 3; ++k) tmp[q][k] = (lane + kWave * k < qn) ? src[lane + kWave * k] : 0u;
-    }
-#pragma unroll
-    for (int q = 0; q < kRowsPerChunk; ++q)
-#pragma unroll
-      for (int k = 0; k < 3; ++k)
-        if (lane + kWave * k < kStageWords) st[q * kStageWords + lane + kWave * k] = tmp[q][k];
-    __threadfence_block();
-    __builtin_amdgcn_wave_barrier();
+    const StageMeta meta = stage_meta(b, mvalid, mvalid ? p.kept[mkidx] : 0);
+    stage_rows(b, meta, st, lane);
     // 3. bigrams of row r, entries j = t, t+4, ...
     const int64_t pos = c * kRowsPerChunk + r;
     const bool valid = pos < n_kept;
     const int32_t kidx = __shfl(mkidx, r, kWave);
-    const int64_t row = __shfl(mrow, r, kWave);
-    const int wide = __shfl(mwide, r, kWave);
-    const int staged = __shfl(mstaged, r, kWave);
-    const int ob = __shfl(mob, r, kWave);
-    const RowText rt{__shfl(mo, r, kWave), __shfl(mbytes, r, kWave) >> wide, wide};
-    const int64_t len = valid ? rt.len : 0;
+    const int64_t row = __shfl(meta.row, r, kWave);
+    const StagedRow sr = staged_row(meta, st, r);
+    const int64_t len = valid ? sr.rt.len : 0;
     const int64_t nz = len >= 2 ? len - 1 : len;
-    const uint8_t* sb = reinterpret_cast<const uint8_t*>(st + r * kStageWords) + ob;
-    auto unit = [&](int64_t j) -> uint32_t {
-      if (staged) {
-        if (!wide) return lower_latin1(sb[j]);
-        return lower_dev(uint32_t(sb[2 * j]) | (uint32_t(sb[2 * j + 1]) << 8), lpage, lblocks);
-      }
-      return lower_dev(row_unit(b, rt, j), lpage, lblocks);
-    };
+    auto unit = [&](int64_t j) -> uint32_t { return sr.unit(b, j, lpage, lblocks); };
     int32_t* out = p.idx + g0 * kChunkStride + lane * kGroup;
     const int32_t total = L8 * kGroup;
     for (int32_t jj0 = 0; jj0 < total; jj0 += kGroup) {
@@ -393,7 +350,7 @@ __global__ __launch_bounds__(kBlock) void k_featurize(DevRawBatch b, DevPrepared
           } else {
             h = fp.hash_kind == 0 ? int64_t(u0) : int64_t(murmur_term(u0, 0, 1));
           }
-          const int64_t idx = term_mod(h, F);
+          const int64_t idx = term_mod(h, F, fm, f32);
           v[k] = int32_t(idx);
           if (idx < lds_lim) {
             // hot ids are flagged early: a (broadcast) read skips the atomic

@@ -20,6 +20,7 @@
 #include "common.h"
 #include "kernels.h"
 #include "kmeans_kernels.h"
+#include "text_stage.h"
 
 namespace twtml {
 
@@ -68,9 +69,85 @@ __global__ __launch_bounds__(kBlock) void k_km_features(DevRawBatch b, const int
   }
 }
 
+// Chunked variant (text_dims <= kKmChunkDims): a wave takes 16 consecutive
+// kept rows, stages their text in LDS (text_stage.h), 4 lanes per row build
+// the row's bigram histogram in LDS, and the wave writes the 16 contiguous
+// feature rows with coalesced stores.
+constexpr int kKmChunkDims = 256;
+
+__global__ __launch_bounds__(kBlock) void k_km_features_chunk(DevRawBatch b, const int64_t* kept,
+                                                              const int64_t* counters, float* X,
+                                                              int dp, int text_dims,
+                                                              const uint8_t* lpage,
+                                                              const uint16_t* lblocks) {
+  extern __shared__ uint32_t smem[];
+  const int lane = lane_id(), w = threadIdx.x / kWave;
+  const int tdp = text_dims > 0 ? text_dims : 1;
+  uint32_t* st = smem + w * (kRowsPerChunk * kStageStride + kRowsPerChunk * tdp);
+  uint32_t* hist = st + kRowsPerChunk * kStageStride;     // [16][text_dims]
+  const int64_t n_kept = counters[0];
+  const int64_t nch = (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;
+  const FastMod32 fm{static_cast<uint32_t>(tdp)};
+  for (int64_t c = int64_t(blockIdx.x) * kKmFeatWaves + w; c < nch;
+       c += int64_t(gridDim.x) * kKmFeatWaves) {
+    const int64_t mk = c * kRowsPerChunk + (lane & 15);
+    const bool mvalid = mk < n_kept;
+    const int64_t mrow = mvalid ? kept[mk] : 0;
+    const float mx0 = mvalid ? float(b.scalars[0 * b.n + mrow]) : 0.f;   // retweetCount
+    const float mx1 = mvalid ? float(b.scalars[1 * b.n + mrow]) : 0.f;   // followersCount
+    if (text_dims > 0) {
+      const StageMeta meta = stage_meta(b, mvalid, mrow);
+      for (int i = lane; i < kRowsPerChunk * text_dims; i += kWave) hist[i] = 0u;
+      stage_rows(b, meta, st, lane);                // includes the fence + wave barrier
+      // rows one at a time with all 64 lanes (short per-lane chains)
+      for (int q = 0; q < kRowsPerChunk; ++q) {
+        const StagedRow sr = staged_row(meta, st, q);
+        const bool valid = c * kRowsPerChunk + q < n_kept;
+        const int64_t len = valid ? sr.rt.len : 0;
+        const int64_t nz = len >= 2 ? len - 1 : len;
+        uint32_t* h = hist + q * text_dims;
+        for (int64_t j = lane; j < nz; j += kWave) {
+          const uint32_t u0 = sr.unit(b, j, lpage, lblocks);
+          const uint32_t hsh = len >= 2 ? 31u * u0 + sr.unit(b, j + 1, lpage, lblocks) : u0;
+          atomicAdd(&h[fm.mod(hsh)], 1u);
+        }
+      }
+      __threadfence_block();
+      __builtin_amdgcn_wave_barrier();
+    }
+    // 16 consecutive rows x dp floats, contiguous in X
+    const int64_t k0 = c * kRowsPerChunk;
+    const int nrows = int(n_kept - k0 < kRowsPerChunk ? n_kept - k0 : kRowsPerChunk);
+    float* xc = X + k0 * dp;
+    for (int i = lane; i < nrows * dp; i += kWave) {
+      const int q = i / dp, col = i - q * dp;
+      if (col < 2) continue;                      // scalar columns below
+      xc[i] = col < 2 + text_dims ? float(hist[q * text_dims + col - 2]) : 0.f;
+    }
+    // scalar columns (lanes 0..15 own row lane & 15)
+    if (lane < nrows) {
+      xc[int64_t(lane) * dp + 0] = mx0;
+      xc[int64_t(lane) * dp + 1] = mx1;
+    }
+    __builtin_amdgcn_wave_barrier();   // LDS reuse by the next chunk
+  }
+}
+
 void launch_km_features(const DevRawBatch& b, const int64_t* kept, const int64_t* counters,
                         float* X, int dp, int text_dims, const uint8_t* lpage,
                         const uint16_t* lblocks, int64_t max_rows, hipStream_t s) {
+  if (text_dims <= kKmChunkDims) {
+    const int64_t nch = (max_rows + kRowsPerChunk - 1) / kRowsPerChunk;
+    int grid = int((nch + kKmFeatWaves - 1) / kKmFeatWaves);
+    if (grid < 1) grid = 1;
+    if (grid > 2048) grid = 2048;
+    const size_t lds = size_t(kKmFeatWaves) *
+                       (size_t(kRowsPerChunk) * kStageStride + size_t(kRowsPerChunk) *
+                        size_t(text_dims > 0 ? text_dims : 1)) * sizeof(uint32_t);
+    hipLaunchKernelGGL(k_km_features_chunk, dim3(grid), dim3(kBlock), lds, s, b, kept, counters, X,
+                       dp, text_dims, lpage, lblocks);
+    return;
+  }
   int grid = ceil_div(max_rows > 0 ? max_rows : 1, kKmFeatWaves);
   if (grid > 8192) grid = 8192;
   const size_t lds = size_t(kKmFeatWaves) * size_t(text_dims > 0 ? text_dims : 1) * sizeof(uint32_t);
