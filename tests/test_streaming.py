@@ -1,0 +1,86 @@
+"""Streaming runtime (U13/U14 semantics): sealing, ordering, backpressure, DStream ops."""
+import threading
+import time
+
+import numpy as np
+
+from twitter_stream_ml_amd.records.batch import RawBatch
+from twitter_stream_ml_amd.runtime.streaming import StreamingContext
+from twitter_stream_ml_amd.sources.synthetic import SynthConfig, SyntheticTweetSource, generate_batch
+
+
+def test_size_sealed_batches_are_exact_and_in_source_order():
+    src = SyntheticTweetSource(SynthConfig(seed=3), rate=0.0)
+    ssc = StreamingContext(0, batch_size=1000, num_batches=4, poll_chunk=300)
+    seen = []
+    ssc.receiverStream(src).foreachRDD(lambda rdd: seen.append(rdd.raw))
+    ssc.start()
+    assert ssc.awaitTermination(30)
+    ssc.stop()
+    assert [b.n for b in seen] == [1000] * 4
+    assert ssc.records_done == 4000 and ssc.batches_done == 4
+    full = generate_batch(SynthConfig(seed=3), 0, 4000)
+    got = RawBatch.concat(seen)
+    np.testing.assert_array_equal(got.text, full.text)
+    np.testing.assert_array_equal(got.scalars[:4], full.scalars[:4])   # createdAt follows the clock
+
+
+def test_output_ops_run_sequentially_in_registration_order():
+    src = SyntheticTweetSource(SynthConfig(seed=1), rate=0.0)
+    ssc = StreamingContext(0, batch_size=200, num_batches=3)
+    log = []
+    stream = ssc.receiverStream(src).cache()
+    stream.foreachRDD(lambda rdd, t: log.append(("stats", rdd.count())))
+    stream.foreachRDD(lambda rdd: log.append(("train", rdd.count())))
+    ssc.start()
+    ssc.awaitTermination(30)
+    ssc.stop()
+    assert log == [("stats", 200), ("train", 200)] * 3
+
+
+def test_backpressure_bounds_pending_batches():
+    src = SyntheticTweetSource(SynthConfig(seed=2), rate=0.0)
+    ssc = StreamingContext(0, batch_size=100, num_batches=12, max_pending=2)
+    gate = threading.Event()
+    max_q = []
+
+    def slow(rdd):
+        max_q.append(ssc._jobs.qsize())
+        gate.wait(0.05)
+
+    ssc.receiverStream(src).foreachRDD(slow)
+    ssc.start()
+    ssc.awaitTermination(30)
+    ssc.stop()
+    assert ssc.batches_done == 12
+    assert max(max_q) <= 2
+
+
+def test_interval_sealing_and_scheduling_delay():
+    src = SyntheticTweetSource(SynthConfig(seed=4), rate=2000.0)
+    ssc = StreamingContext(0.2, num_batches=3)
+    sizes = []
+    ssc.receiverStream(src).foreachRDD(lambda rdd: sizes.append(rdd.raw.n))
+    t0 = time.time()
+    ssc.start()
+    ssc.awaitTermination(30)
+    ssc.stop()
+    assert len(sizes) == 3 and time.time() - t0 >= 0.55
+    assert all(150 <= s <= 700 for s in sizes[1:]), sizes       # ~400 records per 0.2 s
+    assert all(i.scheduling_delay_ms >= 0 for i in ssc.batch_infos)
+
+
+def test_dstream_transformations_are_lazy_per_batch():
+    ssc = StreamingContext(1.0)
+    raw = generate_batch(SynthConfig(seed=5), 0, 500)
+
+    class Src:
+        def poll(self, n, now_ms=None):
+            return raw
+
+    stream = ssc.receiverStream(Src())
+    counted = []
+    retweets = stream.filter(lambda s: s.isRetweet())
+    retweets.map(lambda s: s.getRetweetCount()).foreachRDD(lambda rdd: counted.append(rdd.count()))
+    ssc.run_batches(2)
+    assert counted == [int(raw.is_retweet.sum())] * 2
