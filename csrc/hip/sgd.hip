@@ -12,7 +12,7 @@
 // features have exactly zero gradient, so the compact iteration is exactly
 // the full-width one; ||w|| adds the constant norm of the untouched part.
 //
-// k_sgd_iter_lds (the hot kernel): a 512-thread workgroup stages the compact
+// k_sgd_iter_lds (the hot kernel): a 1024-thread workgroup stages the compact
 // fp32 weights in LDS, streams its SELL-16x4 chunks (4 lanes per row, the
 // row's slots kept in VGPRs between the forward gather and the backward
 // scatter), and accumulates the gradient in LDS as 64-bit FIXED POINT with
