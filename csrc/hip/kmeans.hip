@@ -258,20 +258,23 @@ struct KmTop3 {
     else if (d < b2) { b3 = b2; b2 = d; i2 = c; }
     else if (d < b3) b3 = d;
   }
-  // Near-tie routing (refine layout: [0,R) full list, [R,2R) pair points,
-  // [2R,4R) pair centres; cnt[0] full, cnt[1] pairs): when only two centres
-  // are within the margin the fp64 re-decision compares just those two.
+  // Near-tie routing (refine layout: [0,R) full list, [R,2R) candidate
+  // points, [2R,6R) up to 4 candidate centres per point, -1 padded; cnt[0]
+  // full, cnt[1] candidate lists): when only two centres are within the
+  // margin the fp64 re-decision compares just those two.
   __device__ __forceinline__ void route(int64_t p, float xn, int32_t* refine, unsigned long long* cnt,
                                         int64_t R) const {
-    const float m = km_tie_margin(xn, b1);
+    route_m(p, km_tie_margin(xn, b1), refine, cnt, R);
+  }
+  __device__ __forceinline__ void route_m(int64_t p, float m, int32_t* refine, unsigned long long* cnt,
+                                          int64_t R) const {
     if (b2 - b1 > m) return;
     if (b3 - b1 <= m) {
       refine[atomicAdd(&cnt[0], 1ull)] = int32_t(p);
     } else {
       const int64_t q = int64_t(atomicAdd(&cnt[1], 1ull));
       refine[R + q] = int32_t(p);
-      refine[2 * R + 2 * q] = i1;
-      refine[2 * R + 2 * q + 1] = i2;
+      reinterpret_cast<int4*>(refine + 2 * R)[q] = make_int4(i1, i2, -1, -1);
     }
   }
 };
@@ -332,6 +335,182 @@ __global__ __launch_bounds__(kBlock) void k_km_assign_mfma(const float* X, const
   }
 }
 
+// ---------------------------------------------------------------------------
+// K8 on the bf16 matrix cores with split operands ("bf16x3"): x = xh + xl and
+// c = ch + cl in bf16 (hi = rne(x), lo = rne(x - hi)), and x.c ~ xh.ch +
+// xh.cl + xl.ch with v_mfma_f32_32x32x16_bf16 (fp32 accumulate).  Relative
+// error of each product <= ~3 * 2^-18, so |dist error| <= ~1.1e-5 (|x|^2 +
+// |c|^2); near ties inside a 1e-4 margin go to the fp64 refine like the fp32
+// path.  3 bf16 MFMAs (K=16) replace 8 fp32 MFMAs (K=2) per 16 feature dims.
+//
+// No LDS and no barriers: the centres are split once per launch into
+// ready-made A fragments ([tile][kb][hi|lo][lane][8 bf16], 1 KB per wave
+// load, L2-resident), and each wave sweeps them for NB x 32 points held in
+// VGPRs.  The epilogue keeps a sorted top-4 of packed keys -- the distance
+// with its low `lbits` mantissa bits replaced by the centre index -- so an
+// insertion is v_min + 3 x v_med3 with no index bookkeeping (5 VALU per
+// distance with the fma and bfi, vs ~14 for compare/select chains).  The key
+// quantisation (2^(lbits-23) relative) is added to the tie margin.
+// ---------------------------------------------------------------------------
+using bf16x8 = __attribute__((ext_vector_type(8))) short;
+
+__device__ __forceinline__ uint16_t km_f2bf(float x) {
+  uint32_t u = __float_as_uint(x);
+  u += 0x7FFFu + ((u >> 16) & 1u);   // round to nearest even
+  return uint16_t(u >> 16);
+}
+__device__ __forceinline__ float km_bf2f(uint16_t h) { return __uint_as_float(uint32_t(h) << 16); }
+
+constexpr int kKmKeyBitsMax = 12;   // k <= 4096 on the packed-key path
+
+// thread per (tile, kb, lane) fragment: 8 hi + 8 lo bf16; padded centres are
+// zero with |c|^2 = FLT_MAX so they never win.
+__global__ __launch_bounds__(kBlock) void k_km_split_bf16(const float* C, const float* cnorm, int k,
+                                                          int dp, int ntiles, uint16_t* frag,
+                                                          float* cnp) {
+  const int KB = dp / 16;
+  const int64_t nfrag = int64_t(ntiles) * KB * kWave;
+  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < nfrag;
+       i += int64_t(gridDim.x) * kBlock) {
+    const int lane = int(i % kWave), kb = int((i / kWave) % KB);
+    const int64_t tile = i / (int64_t(kWave) * KB);
+    const int64_t row = tile * 32 + (lane & 31);
+    const int col0 = 16 * kb + 8 * (lane >> 5);
+    bf16x8 hi, lo;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = row < k ? C[row * dp + col0 + j] : 0.f;
+      const uint16_t h = km_f2bf(v);
+      hi[j] = short(h);
+      lo[j] = short(km_f2bf(v - km_bf2f(h)));
+    }
+    bf16x8* f = reinterpret_cast<bf16x8*>(frag) + ((tile * KB + kb) * 2) * kWave + lane;
+    f[0] = hi;
+    f[kWave] = lo;
+  }
+  for (int64_t c = int64_t(blockIdx.x) * kBlock + threadIdx.x; c < int64_t(ntiles) * 32;
+       c += int64_t(gridDim.x) * kBlock)
+    cnp[c] = c < k ? cnorm[c] : FLT_MAX;
+}
+
+struct KmKeys4 {           // sorted b[0] <= b[1] <= b[2] <= b[3]
+  float b[4] = {FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX};
+  __device__ __forceinline__ void add(float key) {
+    const float n3 = __builtin_amdgcn_fmed3f(b[2], b[3], key);
+    const float n2 = __builtin_amdgcn_fmed3f(b[1], b[2], key);
+    const float n1 = __builtin_amdgcn_fmed3f(b[0], b[1], key);
+    b[0] = fminf(b[0], key);
+    b[1] = n1;
+    b[2] = n2;
+    b[3] = n3;
+  }
+};
+
+template <int DP, int NB>
+__global__ __launch_bounds__(kBlock) void k_km_assign_bf16x3(const float* X, const float* fac,
+                                                             const int64_t* counters,
+                                                             const uint16_t* frag, const float* cnp,
+                                                             int ntiles, int lbits, int32_t* labels,
+                                                             int32_t* refine,
+                                                             unsigned long long* refine_cnt, int64_t R) {
+  static_assert(DP % 16 == 0, "bf16x3 path needs DP % 16 == 0");
+  constexpr int KB = DP / 16;
+  const int lane = lane_id(), h = lane >> 5;
+  const int64_t n = counters[0];
+  const int64_t p0 = ((int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave) * (32 * NB);
+  if (p0 >= n) return;                                  // wave-uniform
+  bf16x8 xh[NB][KB], xl[NB][KB];
+  float xn[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const int64_t p = p0 + 32 * b + (lane & 31);
+    xn[b] = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+      const int col = 16 * kb + 8 * h;
+      float v[8];
+      if (p < n) {
+        const float4 a = *reinterpret_cast<const float4*>(X + p * DP + col);
+        const float4 c = *reinterpret_cast<const float4*>(X + p * DP + col + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = c.x; v[5] = c.y; v[6] = c.z; v[7] = c.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float x = v[j] * fac[col + j];
+        xn[b] += x * x;
+        const uint16_t hi = km_f2bf(x);
+        xh[b][kb][j] = short(hi);
+        xl[b][kb][j] = short(km_f2bf(x - km_bf2f(hi)));
+      }
+    }
+    xn[b] += __shfl_xor(xn[b], 32, kWave);
+  }
+  const uint32_t imask = (1u << lbits) - 1u;
+  KmKeys4 t[NB];
+  const bf16x8* F = reinterpret_cast<const bf16x8*>(frag) + lane;
+  for (int tile = 0; tile < ntiles; ++tile) {
+    bf16x8 ah[KB], al[KB];
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+      ah[kb] = F[((int64_t(tile) * KB + kb) * 2) * kWave];
+      al[kb] = F[((int64_t(tile) * KB + kb) * 2 + 1) * kWave];
+    }
+    float cn[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 c = *reinterpret_cast<const float4*>(cnp + tile * 32 + 8 * q + 4 * h);
+      cn[4 * q] = c.x; cn[4 * q + 1] = c.y; cn[4 * q + 2] = c.z; cn[4 * q + 3] = c.w;
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      f32x16 acc = {};
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[kb], xh[b][kb], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[kb], xl[b][kb], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[kb], xh[b][kb], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const uint32_t idx = uint32_t(tile * 32 + (r & 3) + 8 * (r >> 2) + 4 * h);
+        const float dist = fmaf(-2.f, acc[r], cn[r]);
+        t[b].add(__uint_as_float((__float_as_uint(dist) & ~imask) | idx));
+      }
+    }
+  }
+  const float q = ldexpf(1.f, lbits - 21);   // 4 key quanta, relative
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    float o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = __shfl_xor(t[b].b[j], 32, kWave);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) t[b].add(o[j]);
+    const int64_t p = p0 + 32 * b + (lane & 31);
+    if (h != 0 || p >= n) continue;
+    const float* k4 = t[b].b;
+    const int i1 = int(__float_as_uint(k4[0]) & imask);
+    labels[p] = i1;
+    const float m = 1e-4f * (3.f * xn[b] + fabsf(k4[0]) + cnp[i1]) + q * fabsf(k4[0]) + 1e-30f;
+    if (k4[1] - k4[0] > m) continue;
+    if (k4[3] - k4[0] <= m) {
+      refine[atomicAdd(&refine_cnt[0], 1ull)] = int32_t(p);
+    } else {
+      const int64_t qn = int64_t(atomicAdd(&refine_cnt[1], 1ull));
+      refine[R + qn] = int32_t(p);
+      int4 cand;
+      cand.x = i1;
+      cand.y = int(__float_as_uint(k4[1]) & imask);
+      cand.z = k4[2] - k4[0] <= m ? int(__float_as_uint(k4[2]) & imask) : -1;
+      cand.w = -1;
+      reinterpret_cast<int4*>(refine + 2 * R)[qn] = cand;
+    }
+  }
+}
+
 // Generic fallback (any width): one thread per point, scalar fp32.
 __global__ __launch_bounds__(kBlock) void k_km_assign_scalar(const float* X, const float* fac,
                                                              const int64_t* counters,
@@ -353,9 +532,10 @@ __global__ __launch_bounds__(kBlock) void k_km_assign_scalar(const float* X, con
   }
 }
 
-// fp64 re-decision of a two-centre near-tie (typically the two halves of a
-// just-split cluster, 1e-14 apart -- invisible in fp32): thread per point.
-__global__ __launch_bounds__(kBlock) void k_km_refine_pair(const float* X, const double* fac,
+// fp64 re-decision among a short candidate list (2-3 centres; typically the
+// two halves of a just-split cluster, 1e-14 apart -- invisible in fp32):
+// thread per point, first index on exact ties.
+__global__ __launch_bounds__(kBlock) void k_km_refine_cand(const float* X, const double* fac,
                                                            const int32_t* refine,
                                                            const unsigned long long* refine_cnt,
                                                            const double* centers, int d, int dp,
@@ -363,16 +543,21 @@ __global__ __launch_bounds__(kBlock) void k_km_refine_pair(const float* X, const
   const int64_t np = int64_t(refine_cnt[1]);
   for (int64_t q = int64_t(blockIdx.x) * kBlock + threadIdx.x; q < np; q += int64_t(gridDim.x) * kBlock) {
     const int64_t p = refine[R + q];
-    const int a = refine[2 * R + 2 * q], b = refine[2 * R + 2 * q + 1];
+    const int4 c4 = reinterpret_cast<const int4*>(refine + 2 * R)[q];
+    const int cand[4] = {c4.x, c4.y, c4.z, c4.w};
     const float* x = X + p * dp;
-    double da = 0.0, db = 0.0;
-    for (int j = 0; j < d; ++j) {
-      const double xj = double(x[j]) * fac[j];
-      const double ta = xj - centers[int64_t(a) * d + j], tb = xj - centers[int64_t(b) * d + j];
-      da += ta * ta;
-      db += tb * tb;
+    double best = DBL_MAX;
+    int bi = 0x7fffffff;
+    for (int i = 0; i < 4 && cand[i] >= 0; ++i) {
+      const double* c = centers + int64_t(cand[i]) * d;
+      double s = 0.0;
+      for (int j = 0; j < d; ++j) {
+        const double t = double(x[j]) * fac[j] - c[j];
+        s += t * t;
+      }
+      if (s < best || (s == best && cand[i] < bi)) { best = s; bi = cand[i]; }
     }
-    labels[p] = (db < da || (db == da && b < a)) ? b : a;
+    labels[p] = bi;
   }
 }
 
@@ -413,12 +598,31 @@ __global__ __launch_bounds__(kBlock) void k_km_refine(const float* X, const doub
 void launch_km_assign(const float* X, const float* f32, const double* f64, const int64_t* counters,
                       const float* C, const float* cnorm, const double* centers, int k, int d, int dp,
                       int32_t* labels, int32_t* refine, unsigned long long* refine_cnt,
-                      int64_t max_rows, bool mfma, hipStream_t s) {
+                      uint16_t* frag, float* cnp, int64_t max_rows, bool mfma, bool bf16,
+                      hipStream_t s) {
   TWTML_HIP_CHECK(hipMemsetAsync(refine_cnt, 0, 2 * sizeof(unsigned long long), s));
   const int grid_m = int(max_rows / 128 + 1);
   const int64_t R = max_rows;
   bool done = false;
-  if (mfma) {
+  const int ntiles = (k + 31) / 32;
+  int lbits = 1;
+  while ((1 << lbits) < ntiles * 32) ++lbits;
+  if (mfma && bf16 && dp >= 16 && dp <= 128 && lbits <= kKmKeyBitsMax) {
+    int gs = int((int64_t(ntiles) * (dp / 16) * kWave + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_km_split_bf16, dim3(gs < 1024 ? gs : 1024), dim3(kBlock), 0, s, C, cnorm, k,
+                       dp, ntiles, frag, cnp);
+#define KM_BF16(DPV, NBV)                                                                          \
+  case DPV: {                                                                                      \
+    const int64_t waves = (max_rows + 32 * NBV - 1) / (32 * NBV);                                  \
+    hipLaunchKernelGGL((k_km_assign_bf16x3<DPV, NBV>), dim3(int((waves + 3) / 4)), dim3(kBlock), 0, \
+                       s, X, f32, counters, frag, cnp, ntiles, lbits, labels, refine, refine_cnt, R); \
+    done = true;                                                                                   \
+    break;                                                                                         \
+  }
+    switch (dp) { KM_BF16(16, 2) KM_BF16(32, 2) KM_BF16(64, 2) KM_BF16(128, 1) default: break; }
+#undef KM_BF16
+  }
+  if (mfma && !done) {
 #define KM_MFMA(DPV)                                                                                \
   case DPV:                                                                                         \
     hipLaunchKernelGGL(k_km_assign_mfma<DPV>, dim3(grid_m), dim3(kBlock), 0, s, X, f32, counters, C, \
@@ -434,7 +638,7 @@ void launch_km_assign(const float* X, const float* f32, const double* f64, const
     hipLaunchKernelGGL(k_km_assign_scalar, dim3(grid), dim3(kBlock), 0, s, X, f32, counters, C, cnorm,
                        k, dp, labels, refine, refine_cnt, R);
   const int grid_r = grid < 1024 ? grid : 1024;
-  hipLaunchKernelGGL(k_km_refine_pair, dim3(grid_r), dim3(kBlock), 0, s, X, f64, refine, refine_cnt,
+  hipLaunchKernelGGL(k_km_refine_cand, dim3(grid_r), dim3(kBlock), 0, s, X, f64, refine, refine_cnt,
                      centers, d, dp, R, labels);
   hipLaunchKernelGGL(k_km_refine, dim3(grid_r), dim3(kBlock), 0, s, X, f64, refine, refine_cnt,
                      centers, k, d, dp, labels);

@@ -5,6 +5,8 @@
 #include <pybind11/stl.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
@@ -61,7 +63,9 @@ KMEngine::KMEngine(int device, const KMConfig& cfg, std::shared_ptr<Comm> comm)
   cnorm_ = km_alloc<float>(k);
   labels_ = km_alloc<int32_t>(size_t(R));
   order_ = km_alloc<int32_t>(size_t(R));
-  refine_ = km_alloc<int32_t>(4 * size_t(R));
+  refine_ = km_alloc<int32_t>(6 * size_t(R));
+  frag_ = km_alloc<uint16_t>(km_frag_elems(cfg_.k, dp_));
+  cnp_ = km_alloc<float>(size_t((cfg_.k + 31) / 32) * 32);
   lhist_ = km_alloc<int64_t>(k + 1);
   TWTML_HIP_CHECK(hipMemset(centers_, 0, sizeof(double) * k * d));
   TWTML_HIP_CHECK(hipMemset(weights_, 0, sizeof(double) * k));
@@ -79,7 +83,7 @@ KMEngine::~KMEngine() {
   (void)hipDeviceSynchronize();
   raw_.release();
   void* bufs[] = {prep_.kept, prep_.nnz, prep_.blk, prep_.hist, prep_.counters, X_, centers_,
-                  weights_, sums_, mom_, stdv_, c32_, cnorm_, labels_, order_, refine_, lhist_, fac64_, fac32_, blend_,
+                  weights_, sums_, mom_, stdv_, c32_, cnorm_, labels_, order_, refine_, frag_, cnp_, lhist_, fac64_, fac32_, blend_,
                   lower_page_, lower_blocks_};
   for (void* b : bufs) if (b) (void)hipFree(b);
   if (host_out_) (void)hipHostFree(host_out_);
@@ -134,7 +138,18 @@ KMResult KMEngine::process(int slot, bool want_labels) {
   // near-tie lists in refine_, their counts in counters[5..6].
   auto* refine_cnt = reinterpret_cast<unsigned long long*>(prep_.counters + 5);
   launch_km_assign(X_, fac32_, fac64_, prep_.counters, c32_, cnorm_, centers_, k, d, dp_, labels_,
-                   refine_, refine_cnt, cfg_.max_rows, cfg_.mfma != 0, s);
+                   refine_, refine_cnt, frag_, cnp_, cfg_.max_rows, cfg_.mfma != 0, cfg_.mfma == 1, s);
+  // TWTML_DEBUG_KM=1: per-assignment near-tie counts (synchronises the stream)
+  static const bool debug = std::getenv("TWTML_DEBUG_KM") != nullptr;
+  auto debug_refine = [&](const char* what) {
+    if (!debug) return;
+    unsigned long long c[2];
+    TWTML_HIP_CHECK(hipMemcpyAsync(c, refine_cnt, sizeof(c), hipMemcpyDeviceToHost, s));
+    TWTML_HIP_CHECK(hipStreamSynchronize(s));
+    std::fprintf(stderr, "[km] %s: n=%lld refine full=%llu candidates=%llu\n", what,
+                 static_cast<long long>(res.n_local), c[0], c[1]);
+  };
+  debug_refine("update");
   TWTML_HIP_CHECK(hipMemsetAsync(sums_, 0, sizeof(double) * (size_t(k) * d + k), s));
   launch_km_cluster_sums(X_, fac64_, labels_, prep_.counters, k, d, dp_, lhist_, order_, sums_,
                          sums_ + size_t(k) * d, cfg_.max_rows, s, &scan_excl_launch);
@@ -143,7 +158,8 @@ KMResult KMEngine::process(int slot, bool want_labels) {
                    cfg_.points_unit != 0, blend_, c32_, cnorm_, dp_, s);
   if (want_labels)   // KMeans.scala:113 predicts with the updated model
     launch_km_assign(X_, fac32_, fac64_, prep_.counters, c32_, cnorm_, centers_, k, d, dp_, labels_,
-                     refine_, refine_cnt, cfg_.max_rows, cfg_.mfma != 0, s);
+                     refine_, refine_cnt, frag_, cnp_, cfg_.max_rows, cfg_.mfma != 0, cfg_.mfma == 1, s);
+  if (want_labels) debug_refine("predict");
   TWTML_HIP_CHECK(hipEventRecord(ev1_, s));
   if (cfg_.scale)
     TWTML_HIP_CHECK(hipMemcpyAsync(host_out_ + 4, stdv_, sizeof(double) * size_t(d), hipMemcpyDeviceToHost, s));

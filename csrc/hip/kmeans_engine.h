@@ -19,7 +19,9 @@ struct KMConfig {
   double decay = 0.8705505632961241;  // setHalfLife(5, "batches")
   int32_t points_unit = 0;     // timeUnit "points"
   int32_t scale = 1;           // StandardScaler(false, true) per batch
-  int32_t mfma = 1;            // matrix-core assignment (else scalar fp32)
+  // matrix-core assignment: 1 = bf16x3 split MFMA where 16 <= dp <= 128 and
+  // k <= 4096 (fp32 MFMA otherwise), 2 = fp32 MFMA only, 0 = scalar fp32
+  int32_t mfma = 1;
   int64_t max_rows = 1 << 16;
   int64_t max_units = (1 << 16) * 281;
 };
@@ -56,6 +58,8 @@ class KMEngine {
   float *c32_ = nullptr, *cnorm_ = nullptr, *fac32_ = nullptr;
   double *fac64_ = nullptr, *blend_ = nullptr;
   int32_t *labels_ = nullptr, *order_ = nullptr, *refine_ = nullptr;
+  uint16_t* frag_ = nullptr;           // bf16x3 centre fragments
+  float* cnp_ = nullptr;               // |c|^2 padded to 32-centre tiles
   int64_t* lhist_ = nullptr;
   uint8_t* lower_page_ = nullptr;
   uint16_t* lower_blocks_ = nullptr;

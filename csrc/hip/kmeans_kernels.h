@@ -16,12 +16,16 @@ void launch_km_moments(const float* X, const int64_t* counters, int d, int dp, i
 // scaler factors (X itself stays unscaled; consumers multiply on load)
 void launch_km_factor(int d, int dp, bool scale, const double* sum_n, const double* m2,
                       double* std_out, double* f64, float* f32, hipStream_t s);
-// fp32 (MFMA or scalar) argmin; near-ties re-decided in fp64 against `centers`
-// (refine: scratch of 4 * max_rows ints; refine_cnt: 2 device counters)
+// MFMA (bf16x3 or fp32) or scalar argmin; near-ties re-decided in fp64
+// against `centers` (refine: scratch of 6 * max_rows ints; refine_cnt: 2
+// device counters; frag / cnp: bf16x3 scratch of km_frag_elems(k, dp) u16 and
+// round_up(k, 32) floats)
 void launch_km_assign(const float* X, const float* f32, const double* f64, const int64_t* counters,
                       const float* C, const float* cnorm, const double* centers, int k, int d, int dp,
                       int32_t* labels, int32_t* refine, unsigned long long* refine_cnt,
-                      int64_t max_rows, bool mfma, hipStream_t s);
+                      uint16_t* frag, float* cnp, int64_t max_rows, bool mfma, bool bf16,
+                      hipStream_t s);
+inline size_t km_frag_elems(int k, int dp) { return size_t((k + 31) / 32) * 32 * size_t(dp) * 2; }
 void launch_km_cluster_sums(const float* X, const double* f64, const int32_t* labels,
                             const int64_t* counters, int k,
                             int d, int dp, int64_t* hist, int32_t* order, double* sums,

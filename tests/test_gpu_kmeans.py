@@ -46,11 +46,13 @@ def _check_state(dev, cpu, rtol=2e-5):
     np.testing.assert_allclose(c, cpu.state.centers, rtol=rtol, atol=rtol * scale)
 
 
-@pytest.mark.parametrize("k,text_dims,mfma", [(3, 0, True), (3, 0, False), (5, 8, True),
-                                              (64, 30, True), (1024, 0, True), (200, 126, True)])
-def test_kmeans_matches_cpu(hip_module, k, text_dims, mfma):
+@pytest.mark.parametrize("k,text_dims,mfma,precision", [
+    (3, 0, True, "fp32"), (3, 0, False, "fp32"), (5, 8, True, "fp32"), (64, 30, True, "bf16x3"),
+    (64, 30, True, "fp32"), (1024, 0, True, "fp32"), (200, 126, True, "bf16x3"),
+    (1024, 14, True, "bf16x3")])
+def test_kmeans_matches_cpu(hip_module, k, text_dims, mfma, precision):
     from twitter_stream_ml_amd.ops.kmeans_engine import DeviceKMeans
-    dev = DeviceKMeans(_cfg(k, text_dims, mfma=mfma, seed=5), device=0)
+    dev = DeviceKMeans(_cfg(k, text_dims, mfma=mfma, precision=precision, seed=5), device=0)
     cpu = CpuKMeans(k, 2 + text_dims, seed=5)
     c0, w0 = dev.get_state()
     np.testing.assert_array_equal(c0, cpu.state.centers)

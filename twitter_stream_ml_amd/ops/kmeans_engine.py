@@ -6,9 +6,10 @@ Per micro-batch, on one GPU (``KMeans.scala:77-115``):
    hashed bigram counts...]`` straight from the raw UTF-16 batch;
 2. ``StandardScaler(withMean=false, withStd=true)`` fitted on the batch
    (two-pass, sample std, all-reduced across ranks);
-3. assignment to the *current* centres on the matrix cores
-   (``mfma_f32_32x32x2f32``: ``-2 x·c + |c|^2``, argmin), per-cluster sums by
-   a counting sort over labels, all-reduced;
+3. assignment to the *current* centres on the matrix cores (``-2 x·c +
+   |c|^2``, argmin): split-bf16 ``mfma_f32_32x32x16_bf16`` x3 for d >= 16,
+   ``mfma_f32_32x32x2f32`` below, near ties re-decided in fp64; per-cluster
+   sums by a counting sort over labels, all-reduced;
 4. the decayed centre/weight update with the dying-cluster split on device;
 5. optional prediction with the *updated* model (``:113``).
 
@@ -39,6 +40,9 @@ class KMDeviceConfig:
     init_weight: float = 0.0
     scale: bool = True
     mfma: bool = True
+    # matrix-core precision of the distances: "bf16x3" (split bf16 operands,
+    # 3 MFMAs, ~1e-5 relative; used when d pads to >= 16) or "fp32"
+    precision: str = "bf16x3"
     max_rows: int = 1 << 16
     max_units: int = (1 << 16) * 281
     seed: int = 42
@@ -52,7 +56,7 @@ class KMDeviceConfig:
             "decay": float(decay_factor_from_half_life(self.half_life)),
             "points_unit": int(self.time_unit == "points"),
             "scale": int(bool(self.scale)),
-            "mfma": int(bool(self.mfma)),
+            "mfma": 0 if not self.mfma else (1 if self.precision == "bf16x3" else 2),
             "max_rows": int(self.max_rows),
             "max_units": int(self.max_units),
         }
