@@ -95,7 +95,8 @@ KMEngine::~KMEngine() {
 
 void KMEngine::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot) {
   TWTML_HIP_CHECK(hipSetDevice(device_));
-  raw_.submit(hb, n, bytes, slot, copy_);
+  // features read only retweetCount and followersCount (scalar rows 0, 1)
+  raw_.submit(hb, n, bytes, slot, copy_, 2);
 }
 
 KMResult KMEngine::process(int slot, bool want_labels) {

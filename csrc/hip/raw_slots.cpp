@@ -46,8 +46,10 @@ void RawSlots::release() {
   }
 }
 
-void RawSlots::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, hipStream_t copy) {
+void RawSlots::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, hipStream_t copy,
+                      int scalar_cols) {
   Slot& s = slots_[check(slot)];
+  if (scalar_cols < 1 || scalar_cols > 5) throw std::invalid_argument("scalar_cols must be in [1, 5]");
   if (n < 0 || n > max_rows_ || n > hb.max_rows) throw std::invalid_argument("rows exceed capacity");
   if (bytes < 0 || bytes > max_bytes_ || bytes > hb.max_bytes)
     throw std::invalid_argument("text bytes exceed capacity");
@@ -60,8 +62,9 @@ void RawSlots::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, h
                                  hipMemcpyHostToDevice, copy));
   if (n > 0) {
     TWTML_HIP_CHECK(hipMemcpyAsync(s.flags, hb.flags, size_t(n), hipMemcpyHostToDevice, copy));
-    // scalars are packed [5][n] at the start of the host buffer
-    TWTML_HIP_CHECK(hipMemcpyAsync(s.scalars, hb.scalars, sizeof(int64_t) * 5 * size_t(n),
+    // scalars are packed [5][n] at the start of the host buffer; consumers
+    // that read only the leading columns ship only those
+    TWTML_HIP_CHECK(hipMemcpyAsync(s.scalars, hb.scalars, sizeof(int64_t) * scalar_cols * size_t(n),
                                    hipMemcpyHostToDevice, copy));
   }
   TWTML_HIP_CHECK(hipEventRecord(s.h2d_done, copy));

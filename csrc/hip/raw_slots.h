@@ -25,7 +25,9 @@ class RawSlots {
   void init(int64_t max_rows, int64_t max_bytes);
   void release();
   // H2D of rows [0, n) / `bytes` text bytes of hb into `slot` on `copy`.
-  void submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, hipStream_t copy);
+  // scalar_cols: leading [5][n] scalar columns to copy (the rest stay stale)
+  void submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, hipStream_t copy,
+              int scalar_cols = 5);
   // Make `compute` wait for the slot's H2D; returns the device view.
   DevRawBatch acquire(int slot, hipStream_t compute);
   // The compute stream is done reading the slot's raw bytes.
