@@ -51,6 +51,7 @@ def parse_args(argv=None):
     ap.add_argument("--ablate", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--tol", type=float, default=1e-3, help=argparse.SUPPRESS)
     ap.add_argument("--dedup", type=int, default=0, help="merge repeated bigrams per row (1/0)")
+    ap.add_argument("--hybrid", type=int, default=1, help="dense 4-bit counts for hot bigrams (1/0)")
     ap.add_argument("--json-out", default="")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args(argv)
@@ -92,7 +93,8 @@ def main(argv=None) -> int:
         cfg = LRDeviceConfig(num_text_features=args.features, hash=args.hash,
                              step_size=args.step_size, num_iterations=args.iters, fraction=1.0,
                              begin=100, end=1000, max_rows=B, max_units=max_units,
-                             sgd_grid=args.sgd_grid, ablate=args.ablate, tol=args.tol, dedup=bool(args.dedup))
+                             sgd_grid=args.sgd_grid, ablate=args.ablate, tol=args.tol, dedup=bool(args.dedup),
+                             hybrid=bool(args.hybrid))
         eng = DeviceLinearRegression(cfg, device=device, comm=comm)
     pool = [HostBatchView(B, max_units).load(r) for r in pool_raw]
     del pool_raw

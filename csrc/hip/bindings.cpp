@@ -32,7 +32,7 @@ static LRConfig lr_config(const py::dict& d) {
   GET(num_iterations, int32_t) GET(fraction, double) GET(tol, double) GET(begin, int64_t)
   GET(end, int64_t) GET(require_retweet, int32_t) GET(range_filter, int32_t)
   GET(max_rows, int64_t) GET(max_units, int64_t) GET(sgd_grid, int32_t)
-  GET(early_exit_depth, int32_t) GET(ablate, int32_t) GET(dedup, int32_t)
+  GET(early_exit_depth, int32_t) GET(ablate, int32_t) GET(dedup, int32_t) GET(hybrid, int32_t)
 #undef GET
   return c;
 }
@@ -173,6 +173,17 @@ PYBIND11_MODULE(_twtml_hip, m) {
         d["slot"] = py::array_t<int32_t>(py::ssize_t(slot.size()), slot.data());
         d["cnt"] = py::array_t<int32_t>(py::ssize_t(cnt.size()), cnt.data());
         d["clen8d"] = py::array_t<int32_t>(py::ssize_t(clen8d.size()), clen8d.data());
+        return d;
+      })
+      .def("debug_hybrid", [](const LREngine& e) {
+        std::vector<int32_t> hot_slot, clen8c, cslot;
+        std::vector<uint32_t> hot_dense;
+        e.debug_hybrid(hot_slot, hot_dense, clen8c, cslot);
+        py::dict d;
+        d["hot_slot"] = py::array_t<int32_t>(py::ssize_t(hot_slot.size()), hot_slot.data());
+        d["hot_dense"] = py::array_t<uint32_t>(py::ssize_t(hot_dense.size()), hot_dense.data());
+        d["clen8c"] = py::array_t<int32_t>(py::ssize_t(clen8c.size()), clen8c.data());
+        d["cslot"] = py::array_t<int32_t>(py::ssize_t(cslot.size()), cslot.data());
         return d;
       })
       .def("set_step", &LREngine::set_step)

@@ -100,6 +100,12 @@ void LREngine::alloc_prepared() {
   prep_.clen8 = dmalloc<int32_t>(size_t(C) + 1);
   prep_.clen8d = dmalloc<int32_t>(size_t(C) + 1);
   prep_.cnt = dmalloc<uint16_t>(size_t(E));
+  prep_.cslot = dmalloc<uint16_t>(size_t(E));
+  prep_.hot_dense = dmalloc<uint32_t>(size_t(C) * kWave * 4);
+  prep_.clen8c = dmalloc<int32_t>(size_t(C) + 1);
+  prep_.hot_slot = dmalloc<int32_t>(kHot);
+  prep_.hot_of = dmalloc<uint8_t>(kMaxHybridSlots);
+  prep_.slot_hist = dmalloc<uint32_t>(kMaxHybridSlots);
   prep_.cbase = dmalloc<int64_t>(size_t(C) + 1);
   prep_.idx = dmalloc<int32_t>(size_t(E));
   prep_.slot = dmalloc<uint32_t>(size_t(E));
@@ -141,7 +147,8 @@ LREngine::~LREngine() {
   raw_.release();
   for (auto& e : ev_) (void)hipEventDestroy(e);
   void* bufs[] = {prep_.kept, prep_.nnz, prep_.sorted, prep_.blk, prep_.hist, prep_.clen8,
-                  prep_.clen8d, prep_.cnt,
+                  prep_.clen8d, prep_.cnt, prep_.cslot, prep_.hot_dense, prep_.clen8c,
+                  prep_.hot_slot, prep_.hot_of, prep_.slot_hist,
                   prep_.cbase, prep_.idx, prep_.slot, prep_.y, prep_.num, prep_.perm,
                   prep_.flags, prep_.uniq, prep_.slot_of, prep_.ublk, prep_.counters,
                   sgd_.w64, sgd_.wc64, sgd_.wc32, sgd_.g64, sgd_.red64, sgd_.stats, sgd_.state,
@@ -215,8 +222,11 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   sgd_.ns = ns;
   sgd_.n_unique = nU;
   const bool u16 = ns <= 65536;
-  launch_remap(prep_, res.entries, nU, u16, s);
-  prep_.dedup = (cfg_.dedup && u16 && dedup_supported(ns)) ? 1 : 0;
+  const bool dedup = cfg_.dedup && u16 && dedup_supported(ns);
+  prep_.hybrid = (!dedup && cfg_.hybrid && u16 && res.n_kept > 0 && sgd_hybrid_fits(ns)) ? 1 : 0;
+  if (prep_.hybrid) launch_remap_hybrid(prep_, res.entries, ns, kNumNumeric + nU, num_cu_, s);
+  else launch_remap(prep_, res.entries, nU, u16, s);
+  prep_.dedup = dedup ? 1 : 0;
   if (prep_.dedup) launch_dedup(prep_, ns, kNumNumeric + nU, res.n_kept, s);
   TWTML_HIP_CHECK(hipMemsetAsync(sgd_.state, 0, 8 * sizeof(double), s));
   TWTML_HIP_CHECK(hipMemsetAsync(sgd_.stats, 0, 8 * sizeof(double), s));
@@ -347,6 +357,30 @@ void LREngine::debug_merged(std::vector<int32_t>& slot, std::vector<int32_t>& cn
   if (C) TWTML_HIP_CHECK(hipMemcpy(clen8d.data(), prep_.clen8d, sizeof(int32_t) * size_t(C), hipMemcpyDeviceToHost));
   slot.assign(s16.begin(), s16.end());
   cnt.assign(c16.begin(), c16.end());
+}
+
+void LREngine::debug_hybrid(std::vector<int32_t>& hot_slot, std::vector<uint32_t>& hot_dense,
+                            std::vector<int32_t>& clen8c, std::vector<int32_t>& cslot) const {
+  TWTML_HIP_CHECK(hipSetDevice(device_));
+  TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
+  hot_slot.clear(); hot_dense.clear(); clen8c.clear(); cslot.clear();
+  if (!prep_.hybrid) return;
+  int64_t counters[4];
+  TWTML_HIP_CHECK(hipMemcpy(counters, prep_.counters, sizeof(counters), hipMemcpyDeviceToHost));
+  const int64_t C = (counters[0] + kRowsPerChunk - 1) / kRowsPerChunk;
+  const int64_t E = counters[2] * kChunkStride;
+  hot_slot.resize(kHot);
+  hot_dense.resize(size_t(C) * kWave * 4);
+  clen8c.resize(size_t(C));
+  std::vector<uint16_t> c16(static_cast<size_t>(E));
+  TWTML_HIP_CHECK(hipMemcpy(hot_slot.data(), prep_.hot_slot, sizeof(int32_t) * kHot, hipMemcpyDeviceToHost));
+  if (C) {
+    TWTML_HIP_CHECK(hipMemcpy(hot_dense.data(), prep_.hot_dense, sizeof(uint32_t) * hot_dense.size(),
+                              hipMemcpyDeviceToHost));
+    TWTML_HIP_CHECK(hipMemcpy(clen8c.data(), prep_.clen8c, sizeof(int32_t) * size_t(C), hipMemcpyDeviceToHost));
+  }
+  if (E) TWTML_HIP_CHECK(hipMemcpy(c16.data(), prep_.cslot, sizeof(uint16_t) * size_t(E), hipMemcpyDeviceToHost));
+  cslot.assign(c16.begin(), c16.end());
 }
 
 void LREngine::debug_prepared(std::vector<int64_t>& counters, std::vector<int32_t>& clen8,

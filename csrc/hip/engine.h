@@ -39,6 +39,7 @@ struct LRConfig {
   int32_t early_exit_depth = 3;  // host run-ahead (iterations) for early stop
   int32_t ablate = 0;            // perf diagnostics only (see SgdParams)
   int32_t dedup = 0;             // merge repeated bigrams of a row into counts
+  int32_t hybrid = 1;            // dense 4-bit counts for the batch's hottest slots (hot_split.hip)
 };
 
 // Pinned staging buffer of one raw batch in the wire format
@@ -95,6 +96,9 @@ class LREngine {
   // Merged (slot, count) layout the iteration kernels read (empty if not merged).
   void debug_merged(std::vector<int32_t>& slot, std::vector<int32_t>& cnt,
                     std::vector<int32_t>& clen8d) const;
+  // Hybrid dense-hot layout of the last batch (empty if not used).
+  void debug_hybrid(std::vector<int32_t>& hot_slot, std::vector<uint32_t>& hot_dense,
+                    std::vector<int32_t>& clen8c, std::vector<int32_t>& cslot) const;
 
  private:
   void alloc_prepared();

@@ -1,0 +1,259 @@
+// Hybrid dense-hot layout of the SGD slot stream, built by the remap pass.
+//
+// A GD iteration streams every (row, bigram) entry of the batch twice (dot
+// product, then gradient), and on tweet text the bigram distribution is very
+// skewed: on the bench data the 128 most frequent of ~1.4K active bigrams
+// carry 81 % of all entries.  Those hot slots are stored per row as 4-bit
+// counts -- 128 nibbles = 64 B per row, 16 B per lane of the SELL-16x4 chunk
+// -- and only the remaining cold entries stay in a SELL stream.  The hot
+// gradient then accumulates in VGPRs instead of contended LDS atomics
+// (sgd.hip, k_sgd_iter_hyb).  A hot id whose count in a row exceeds 15 stays
+// cold for that row (every occurrence in its own lane), so the layout is
+// exact for any text and a lane never holds more cold entries than before.
+//
+//   k_slot_hist      sampled slot histogram (every 32nd 8-entry group of idx)
+//   k_hot_select     top-kHot by binary search on the count threshold
+//   k_remap_hybrid   replaces k_remap: one wave per 16-row chunk maps hashed
+//                    ids to slots, counts hot slots per row in LDS, and writes
+//                    the 4-bit hot counts plus each lane's cold entries
+//
+// Chunks with rows too long for the register-resident pass (L8 >
+// kMaxRegGroups) get the plain u16 layout and clen8c = -1.
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace twtml {
+
+namespace {
+
+constexpr int kHistBlock = 1024;
+constexpr int kHistStride = 32;            // sample every 32nd 8-entry group
+constexpr int kSplitWaves = 4;
+
+// LDS hand-off between the lanes of one wave (no other wave touches the
+// region): drain this wave's LDS traffic, then re-converge.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__global__ __launch_bounds__(kHistBlock) void k_slot_hist(const int32_t* idx, const int32_t* slot_of,
+                                                          int64_t n8, int64_t pad_base, uint32_t* hist) {
+  extern __shared__ uint32_t h[];
+  for (int64_t s = threadIdx.x; s < pad_base; s += kHistBlock) h[s] = 0u;
+  __syncthreads();
+  for (int64_t i = int64_t(blockIdx.x) * kHistBlock + threadIdx.x; i * kHistStride < n8;
+       i += int64_t(gridDim.x) * kHistBlock) {
+    const int4* src = reinterpret_cast<const int4*>(idx + i * kHistStride * 8);
+    const int4 a = src[0], b = src[1];
+    const int32_t v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (v[e] >= 0) atomicAdd(&h[kNumNumeric + slot_of[v[e]]], 1u);
+  }
+  __syncthreads();
+  for (int64_t s = threadIdx.x; s < pad_base; s += kHistBlock)
+    if (h[s]) atomicAdd(&hist[s], h[s]);
+}
+
+// Top-kHot slots by sampled count: the largest threshold T with at least
+// kHot slots counting >= T (binary search, block-wide counts), then slots
+// above T and the first ties at T get ids.  Zero counts are never hot.
+__global__ __launch_bounds__(1024) void k_hot_select(const uint32_t* hist, int64_t ns, int64_t pad_base,
+                                                     uint8_t* hot_of, int32_t* hot_slot) {
+  __shared__ int32_t part[1024 / kWave];
+  __shared__ uint32_t n_gt, n_eq;
+  const int tid = threadIdx.x;
+  auto count_ge = [&](uint32_t T) {
+    int32_t c = 0;
+    for (int64_t s = kNumNumeric + tid; s < pad_base; s += 1024) c += hist[s] >= T ? 1 : 0;
+    c = wave_sum(c);
+    __syncthreads();
+    if (lane_id() == 0) part[tid / kWave] = c;
+    __syncthreads();
+    int32_t t = 0;
+    for (int k = 0; k < 1024 / kWave; ++k) t += part[k];
+    return t;
+  };
+  uint32_t lo = 1, hi = 0;   // answer in [lo, hi]: count_ge(lo) >= kHot
+  {
+    uint32_t m = 0;
+    for (int64_t s = kNumNumeric + tid; s < pad_base; s += 1024) m = max(m, hist[s]);
+    m = wave_max(m);
+    __syncthreads();
+    if (lane_id() == 0) part[tid / kWave] = int32_t(m);
+    __syncthreads();
+    for (int k = 0; k < 1024 / kWave; ++k) hi = max(hi, uint32_t(part[k]));
+  }
+  uint32_t T = 1;
+  if (hi >= 1 && count_ge(1) > kHot) {
+    while (lo < hi) {            // largest T with count_ge(T) >= kHot
+      const uint32_t mid = lo + (hi - lo + 1) / 2;
+      if (count_ge(mid) >= kHot) lo = mid; else hi = mid - 1;
+    }
+    T = lo;
+  }
+  // T = 1 with <= kHot non-zero slots: every non-zero slot is hot
+  const int32_t above = count_ge(T + 1);            // strictly above T: < kHot
+  const uint32_t need_eq = uint32_t(kHot - above);
+  if (tid == 0) { n_gt = 0; n_eq = 0; }
+  for (int h = tid; h < kHot; h += 1024) hot_slot[h] = int32_t(pad_base);   // unused ids
+  __syncthreads();
+  for (int64_t s = tid; s < ns; s += 1024) {
+    uint32_t h = 0xFFu;
+    if (s >= kNumNumeric && s < pad_base) {
+      const uint32_t c = hist[s];
+      if (c > T) {
+        const uint32_t k = atomicAdd(&n_gt, 1u);
+        if (k < uint32_t(kHot)) h = k;
+      } else if (c == T && c > 0u) {
+        const uint32_t k = atomicAdd(&n_eq, 1u);
+        if (k < need_eq) h = uint32_t(above) + k;
+      }
+    }
+    hot_of[s] = uint8_t(h);
+    if (h != 0xFFu) hot_slot[h] = int32_t(s);
+  }
+}
+
+__device__ __forceinline__ uint32_t pack2(uint32_t a, uint32_t b) { return a | (b << 16); }
+
+__global__ __launch_bounds__(kSplitWaves * kWave) void k_remap_hybrid(DevPrepared p, int64_t ns,
+                                                                      int64_t pad_base) {
+  __shared__ uint8_t hot_of[kMaxHybridSlots];
+  __shared__ uint32_t cnt[kSplitWaves][kRowsPerChunk * kHot / 2];   // u16 counts, 2 per word
+  for (int64_t s = threadIdx.x; s < ns; s += kSplitWaves * kWave) hot_of[s] = p.hot_of[s];
+  __syncthreads();
+  const int lane = lane_id();
+  const int w = __builtin_amdgcn_readfirstlane(int(threadIdx.x) / kWave);
+  const int r = lane / kLanesPerRow, t = lane % kLanesPerRow;
+  const int64_t n_kept = p.counters[0];
+  const int64_t nch = (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;
+  const int64_t wave = int64_t(blockIdx.x) * kSplitWaves + w;
+  const int64_t nwaves = int64_t(gridDim.x) * kSplitWaves;
+  uint32_t* cw = cnt[w];
+  uint32_t* crow = cw + r * (kHot / 2);
+  const uint32_t pad = uint32_t(pad_base + lane);
+  uint16_t* plain = static_cast<uint16_t*>(p.slot);
+
+  for (int64_t c = wave; c < nch; c += nwaves) {
+    const int32_t L8 = p.clen8[c];
+    const int64_t off = p.cbase[c] * kChunkStride + lane * kGroup;
+    if (L8 > kMaxRegGroups) {   // plain layout (as k_remap)
+      for (int32_t g = 0; g < L8; ++g) {
+        const int4* src = reinterpret_cast<const int4*>(p.idx + off + int64_t(g) * kChunkStride);
+        const int4 a = src[0], b = src[1];
+        const int32_t v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        uint32_t o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = v[e] >= 0 ? uint32_t(kNumNumeric + p.slot_of[v[e]]) : pad;
+        *reinterpret_cast<uint4*>(plain + off + int64_t(g) * kChunkStride) =
+            make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7]));
+      }
+      if (lane == 0) p.clen8c[c] = -1;
+      continue;
+    }
+    for (int i = lane; i < kRowsPerChunk * kHot / 2; i += kWave) cw[i] = 0u;
+    wave_lds_sync();
+    // pass 1: slots into registers (u16 pairs), hot counts per row in LDS
+    uint32_t sv[kMaxRegGroups][4];
+#pragma unroll
+    for (int g = 0; g < kMaxRegGroups; ++g) {
+      if (g < L8) {
+        const int4* src = reinterpret_cast<const int4*>(p.idx + off + int64_t(g) * kChunkStride);
+        const int4 a = src[0], b = src[1];
+        const int32_t v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        uint32_t o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          o[e] = v[e] >= 0 ? uint32_t(kNumNumeric + p.slot_of[v[e]]) : pad;
+          const uint32_t h = v[e] >= 0 ? uint32_t(hot_of[o[e]]) : 0xFFu;
+          if (h != 0xFFu) atomicAdd(&crow[h >> 1], 1u << ((h & 1u) * 16));
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sv[g][q] = pack2(o[2 * q], o[2 * q + 1]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sv[g][q] = 0u;
+      }
+    }
+    wave_lds_sync();
+    // dense part: this lane's 32 hot ids of its row; counts > 15 stay cold
+    uint32_t nib[4] = {0u, 0u, 0u, 0u};
+    {
+      const uint4* c4 = reinterpret_cast<const uint4*>(crow + 16 * t);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint4 cv = c4[j];
+        const uint32_t ws[4] = {cv.x, cv.y, cv.z, cv.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            const uint32_t n = (ws[k] >> (16 * hh)) & 0xFFFFu;
+            const int i = 8 * j + 2 * k + hh;          // hot id 32t + i
+            if (n <= 15u) nib[i >> 3] |= n << (4 * (i & 7));
+          }
+        }
+      }
+    }
+    reinterpret_cast<uint4*>(p.hot_dense)[c * kWave + lane] = make_uint4(nib[0], nib[1], nib[2], nib[3]);
+    // pass 2: this lane's cold entries (in order) -> its own cold groups
+    uint64_t lo = 0, hi = 0;   // 8-entry shift register
+    int32_t n = 0, gout = 0;
+    uint16_t* dst = p.cslot + off;
+    auto push = [&](uint32_t s) {
+      lo = (lo >> 16) | (hi << 48);
+      hi = (hi >> 16) | (uint64_t(s) << 48);
+      if (++n == kGroup) {
+        *reinterpret_cast<uint4*>(dst + int64_t(gout) * kChunkStride) =
+            make_uint4(uint32_t(lo), uint32_t(lo >> 32), uint32_t(hi), uint32_t(hi >> 32));
+        ++gout;
+        n = 0;
+      }
+    };
+#pragma unroll
+    for (int g = 0; g < kMaxRegGroups; ++g) {
+      if (g >= L8) continue;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint32_t s = (sv[g][e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
+        if (s >= uint32_t(pad_base)) continue;
+        const uint32_t h = hot_of[s];
+        bool cold = h == 0xFFu;
+        if (!cold) cold = ((crow[h >> 1] >> ((h & 1u) * 16)) & 0xFFFFu) > 15u;
+        if (cold) push(s);
+      }
+    }
+    const int32_t mine = gout + (n > 0 ? 1 : 0);
+    const int32_t L8c = wave_max(mine);
+    while (gout < L8c) push(pad);
+    if (lane == 0) p.clen8c[c] = L8c;
+    wave_lds_sync();   // the next chunk clears / refills this wave's LDS
+  }
+}
+
+}  // namespace
+
+void launch_remap_hybrid(const DevPrepared& p, int64_t entries, int64_t ns, int64_t pad_base, int num_cu,
+                         hipStream_t s) {
+  if (ns > kMaxHybridSlots) throw std::invalid_argument("hybrid layout: too many active slots");
+  if (entries == 0) return;
+  TWTML_HIP_CHECK(hipMemsetAsync(p.slot_hist, 0, sizeof(uint32_t) * size_t(ns), s));
+  const int64_t n8 = entries / kGroup;
+  int gh = int((n8 / kHistStride + kHistBlock - 1) / kHistBlock);
+  gh = std::max(1, std::min(gh, num_cu));
+  hipLaunchKernelGGL(k_slot_hist, dim3(gh), dim3(kHistBlock), size_t(pad_base) * sizeof(uint32_t), s,
+                     p.idx, p.slot_of, n8, pad_base, p.slot_hist);
+  hipLaunchKernelGGL(k_hot_select, dim3(1), dim3(1024), 0, s, p.slot_hist, ns, pad_base, p.hot_of,
+                     p.hot_slot);
+  const int64_t cmax = (p.cap_rows + kRowsPerChunk - 1) / kRowsPerChunk;
+  int grid = int(std::min<int64_t>(int64_t(num_cu) * 16, (cmax + kSplitWaves - 1) / kSplitWaves));
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(k_remap_hybrid, dim3(grid), dim3(kSplitWaves * kWave), 0, s, p, ns, pad_base);
+}
+
+}  // namespace twtml

@@ -76,6 +76,15 @@ struct DevPrepared {
   uint16_t* cnt;            // [E]   term count per entry (0 = pad); valid if dedup
   int32_t* clen8d;          // [C]   groups per lane after merging
   int32_t dedup;            // 1: iteration kernels use cnt / clen8d
+  // hybrid dense-hot layout (hot_split.hip): the kHot most frequent slots of
+  // the batch become 4-bit counts per row, the rest a cold SELL stream
+  uint32_t* hot_dense;      // [C][64] uint4: lane (row r, quarter t) = 32 nibbles, hot ids 32t..32t+31
+  uint16_t* cslot;          // [E]   cold slots (+ count overflow), same chunk bases as slot
+  int32_t* clen8c;          // [C]   cold groups per lane; -1 = chunk left in the plain layout
+  int32_t* hot_slot;        // [kHot] slot of hot id h (a zero-weight pad slot when unused)
+  uint8_t* hot_of;          // [kMaxHybridSlots] hot id of a slot (0xFF = cold)
+  uint32_t* slot_hist;      // [kMaxHybridSlots] sampled slot frequencies
+  int32_t hybrid;           // 1: iteration kernels use the hybrid layout
   // counters (device): [0]=n_kept [1]=n_unique [2]=groups [3]=error
   int64_t* counters;
   int64_t cap_rows, cap_rows16, cap_entries, cap_chunks, flag_len;
@@ -102,6 +111,14 @@ void launch_remap(const DevPrepared& p, int64_t entries, int64_t n_unique, bool 
 // per-row duplicate merging for u16 slot spaces up to 8192 slots
 bool dedup_supported(int64_t ns);
 void launch_dedup(const DevPrepared& p, int64_t ns, int64_t pad_base, int64_t n_kept, hipStream_t s);
+
+// Hybrid dense-hot layout (u16 slot spaces up to kMaxHybridSlots), in place
+// of launch_remap: sampled slot histogram -> top-kHot selection -> per chunk
+// 4-bit hot counts + each lane's cold entries (hot_split.hip).
+constexpr int kHot = 128;
+constexpr int kMaxHybridSlots = 16384;
+void launch_remap_hybrid(const DevPrepared& p, int64_t entries, int64_t ns, int64_t pad_base, int num_cu,
+                         hipStream_t s);
 
 // ---------------------------------------------------------------------------
 // SGD on the compact active set.
@@ -145,6 +162,8 @@ void launch_sgd_iter(const DevSgd& d, const DevPrepared& p, const SgdParams& sp,
 void launch_sgd_update(const DevSgd& d, const SgdParams& sp, hipStream_t s);
 void launch_scatter_w(const DevSgd& d, const DevPrepared& p, hipStream_t s);
 int sgd_lds_rep(int64_t ns);
+// the hybrid iteration kernel's LDS (gradient replicas + hot partials) fits
+bool sgd_hybrid_fits(int64_t ns);
 int sgd_iter_grid(int64_t ns, int64_t n_kept, int num_cu);
 
 // (k-means launchers: kmeans_kernels.h)

@@ -77,17 +77,26 @@ struct RowAcc {
   double st[6] = {0, 0, 0, 0, 0, 0};
 };
 
-template <bool STATS, bool SAMPLE>
-__device__ __forceinline__ float row_residual(float dot, int64_t pos, int t, const DevSgd& d,
-                                              const DevPrepared& p, const SgdParams& sp,
-                                              int64_t n_kept, float w0, float w1, float w2,
-                                              float w3, RowAcc& acc) {
-  const bool valid = pos < n_kept;
+// Row-level inputs (numeric features + label), loadable ahead of the dot.
+struct RowIn {
+  float n0, n1, n2, n3, y;
+};
+
+__device__ __forceinline__ RowIn row_in(const DevPrepared& p, int64_t pos) {
   const int64_t cap = p.cap_rows16;
-  const float n0 = p.num[0 * cap + pos], n1 = p.num[1 * cap + pos];
-  const float n2 = p.num[2 * cap + pos], n3 = p.num[3 * cap + pos];
+  return RowIn{p.num[0 * cap + pos], p.num[1 * cap + pos], p.num[2 * cap + pos],
+               p.num[3 * cap + pos], p.y[pos]};
+}
+
+template <bool STATS, bool SAMPLE>
+__device__ __forceinline__ float row_residual(float dot, const RowIn& ri, int64_t pos, int t,
+                                              const DevSgd& d, const DevPrepared& p,
+                                              const SgdParams& sp, int64_t n_kept, float w0, float w1,
+                                              float w2, float w3, RowAcc& acc) {
+  const bool valid = pos < n_kept;
+  const float n0 = ri.n0, n1 = ri.n1, n2 = ri.n2, n3 = ri.n3;
   dot += n0 * w0 + n1 * w1 + n2 * w2 + n3 * w3;
-  const float y = p.y[pos];
+  const float y = ri.y;
   bool in = valid;
   if (SAMPLE && valid)
     in = sample_uniform(uint64_t(42 + sp.iteration), uint64_t(sp.row_offset + p.perm[pos])) <
@@ -106,6 +115,14 @@ __device__ __forceinline__ float row_residual(float dot, int64_t pos, int t, con
     acc.msum += in ? 1.0 : 0.0;
   }
   return r;
+}
+
+template <bool STATS, bool SAMPLE>
+__device__ __forceinline__ float row_residual(float dot, int64_t pos, int t, const DevSgd& d,
+                                              const DevPrepared& p, const SgdParams& sp,
+                                              int64_t n_kept, float w0, float w1, float w2,
+                                              float w3, RowAcc& acc) {
+  return row_residual<STATS, SAMPLE>(dot, row_in(p, pos), pos, t, d, p, sp, n_kept, w0, w1, w2, w3, acc);
 }
 
 template <bool STATS, bool SAMPLE>
@@ -170,18 +187,33 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_lds(DevSgd d, DevPrepar
   const int rep = lane % REP;
   const int64_t n_kept = p.counters[0];
   const int64_t nch = (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;
-  const int64_t wave = (int64_t(blockIdx.x) * kIterBlock + threadIdx.x) / kWave;
+  const int64_t wave = int64_t(blockIdx.x) * (kIterBlock / kWave) +
+                       __builtin_amdgcn_readfirstlane(int(threadIdx.x) / kWave);   // wave-uniform
   const int64_t nwaves = int64_t(gridDim.x) * (kIterBlock / kWave);
   const uint16_t* slot = static_cast<const uint16_t*>(p.slot);
   const float w0 = wl[0], w1 = wl[1], w2 = wl[2], w3 = wl[3];
   RowAcc acc;
   bool clamped = false;
 
-  for (int64_t c = wave; c < nch; c += nwaves) {
-    const int32_t L8 = CNT ? p.clen8d[c] : p.clen8[c];
-    const int64_t off = p.cbase[c] * kChunkStride + lane * kGroup;
+  // chunk metadata for 64 chunks at a time in lanes (see k_sgd_iter_hyb)
+  const int32_t* __restrict__ clen = CNT ? p.clen8d : p.clen8;
+  int32_t md_l8 = 0;
+  int64_t md_cb = 0;
+  int k = 0;
+  for (int64_t c = wave; c < nch; c += nwaves, ++k) {
+    if ((k & (kWave - 1)) == 0) {
+      const int64_t cc = c + int64_t(lane) * nwaves;
+      md_l8 = cc < nch ? clen[cc] : 0;
+      md_cb = cc < nch ? p.cbase[cc] : 0;
+    }
+    const int kl = k & (kWave - 1);
+    const int32_t L8 = __builtin_amdgcn_readlane(md_l8, kl);
+    const int64_t cb = int64_t(uint32_t(__builtin_amdgcn_readlane(int32_t(md_cb), kl))) |
+                       (int64_t(__builtin_amdgcn_readlane(int32_t(md_cb >> 32), kl)) << 32);
+    const int64_t off = cb * kChunkStride + lane * kGroup;
     const uint16_t* sl = slot + off;
     const int64_t pos = c * kRowsPerChunk + r;
+    const RowIn ri = row_in(p, pos);
     if (L8 <= kMaxRegGroups) {
       uint4 v[kMaxRegGroups];
       uint4 cv[CNT ? kMaxRegGroups : 1];
@@ -218,7 +250,7 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_lds(DevSgd d, DevPrepar
       }
       dot += __shfl_xor(dot, 1, kWave);
       dot += __shfl_xor(dot, 2, kWave);
-      const float res = row_residual<STATS, SAMPLE>(dot, pos, t, d, p, sp, n_kept, w0, w1, w2, w3, acc);
+      const float res = row_residual<STATS, SAMPLE>(dot, ri, pos, t, d, p, sp, n_kept, w0, w1, w2, w3, acc);
       if (res != 0.f && sp.ablate == 0) {
         const unsigned long long q = to_fix(res, clamped, sp.fix_lim);
 #pragma unroll
@@ -248,7 +280,7 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_lds(DevSgd d, DevPrepar
       }
       dot += __shfl_xor(dot, 1, kWave);
       dot += __shfl_xor(dot, 2, kWave);
-      const float res = row_residual<STATS, SAMPLE>(dot, pos, t, d, p, sp, n_kept, w0, w1, w2, w3, acc);
+      const float res = row_residual<STATS, SAMPLE>(dot, ri, pos, t, d, p, sp, n_kept, w0, w1, w2, w3, acc);
       if (res != 0.f) {
         const unsigned long long q = to_fix(res, clamped, sp.fix_lim);
         for (int32_t g = 0; g < L8; ++g) {
@@ -270,6 +302,212 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_lds(DevSgd d, DevPrepar
 #pragma unroll
     for (int k = 0; k < REP; ++k) v += (long long)gl[s * REP + k];
     if (v != 0) atomicAdd(&d.g64[s], double(v) * kFixInv);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Hybrid dense-hot path (layout: hot_split.hip).  Per chunk a lane reads its
+// row's 32 hot counts (16 B: 4-bit counts of hot ids 32t..32t+31) and the
+// row-balanced cold groups.  Hot weights are read from LDS with b128 loads
+// (broadcast across the 16 lanes of a quarter), the hot gradient accumulates
+// in VGPRs (fp32 per lane, fp64 across waves); only cold entries use the LDS
+// fixed-point gradient.  Chunks left
+// in the plain layout (clen8c < 0) take the plain route.
+// ---------------------------------------------------------------------------
+constexpr int kMaxColdGroups = 4;   // cold groups kept in VGPRs (cold row <= 128)
+constexpr int kHotPerLane = kHot / kLanesPerRow;   // 32
+
+// wq: this lane's 32 hot weights in LDS (quarter t, 16-B aligned, stride 36
+// floats so the four quarters' b128 reads hit different banks)
+constexpr int kHotLdsStride = kHotPerLane + 4;
+
+__device__ __forceinline__ float hot_dot(const uint4 hv, const float* wq) {
+  const uint32_t hw[4] = {hv.x, hv.y, hv.z, hv.w};
+  float a = 0.f, b = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 lo = reinterpret_cast<const float4*>(wq)[2 * q];
+    const float4 hi = reinterpret_cast<const float4*>(wq)[2 * q + 1];
+    const float wv[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+#pragma unroll
+    for (int k = 0; k < 8; k += 2) {
+      a += float((hw[q] >> (4 * k)) & 15u) * wv[k];
+      b += float((hw[q] >> (4 * k + 4)) & 15u) * wv[k + 1];
+    }
+  }
+  return a + b;
+}
+
+__device__ __forceinline__ void hot_grad(const uint4 hv, float res, float (&gh)[kHotPerLane]) {
+  const uint32_t hw[4] = {hv.x, hv.y, hv.z, hv.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) gh[8 * q + k] += res * float((hw[q] >> (4 * k)) & 15u);
+}
+
+template <bool STATS, bool SAMPLE, int REP>
+__global__ __launch_bounds__(kIterBlock) void k_sgd_iter_hyb(DevSgd d, DevPrepared p, SgdParams sp) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  __shared__ double scratch[kIterBlock / kWave];
+  __shared__ float hsum[kIterBlock / kWave][kHot];
+  __shared__ __attribute__((aligned(16))) float whl[kLanesPerRow * kHotLdsStride];
+  if (d.state[0] != 0.0) return;
+  const int64_t ns = d.ns;
+  float* wl = lds;
+  unsigned long long* gl = reinterpret_cast<unsigned long long*>(lds + ns);
+  for (int64_t s = threadIdx.x; s < ns; s += kIterBlock) wl[s] = d.wc32[s];
+  for (int64_t s = threadIdx.x; s < ns * REP; s += kIterBlock) gl[s] = 0ull;
+  for (int h = threadIdx.x; h < kHot; h += kIterBlock)
+    whl[(h / kHotPerLane) * kHotLdsStride + h % kHotPerLane] = d.wc32[p.hot_slot[h]];
+  __syncthreads();
+  const int lane = lane_id();
+  const int w = __builtin_amdgcn_readfirstlane(int(threadIdx.x) / kWave);   // wave-uniform
+  const int r = lane / kLanesPerRow, t = lane % kLanesPerRow;
+  const int rep = lane % REP;
+  const int64_t n_kept = p.counters[0];
+  const int64_t nch = (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;
+  const int64_t wave = int64_t(blockIdx.x) * (kIterBlock / kWave) + w;
+  const int64_t nwaves = int64_t(gridDim.x) * (kIterBlock / kWave);
+  const uint16_t* slot = static_cast<const uint16_t*>(p.slot);
+  const uint4* hdense = reinterpret_cast<const uint4*>(p.hot_dense);
+  const int32_t* __restrict__ clen8c = p.clen8c;
+  const int64_t* __restrict__ cbase = p.cbase;
+  const float w0 = wl[0], w1 = wl[1], w2 = wl[2], w3 = wl[3];
+  const float* wq = whl + t * kHotLdsStride;
+  float gh[kHotPerLane];
+#pragma unroll
+  for (int i = 0; i < kHotPerLane; ++i) gh[i] = 0.f;
+  RowAcc acc;
+  bool clamped = false;
+
+  // Chunk metadata for 64 of this wave's chunks at a time, lane i holding
+  // the i-th (one load round trip per 64 chunks; read back with v_readlane
+  // into SGPRs).  Row inputs and hot counts are issued before the cold
+  // stream, so a chunk costs one memory round trip.
+  int32_t md_l8 = 0;
+  int64_t md_cb = 0;
+  int k = 0;
+  for (int64_t c = wave; c < nch; c += nwaves, ++k) {
+    if ((k & (kWave - 1)) == 0) {
+      const int64_t cc = c + int64_t(lane) * nwaves;
+      md_l8 = cc < nch ? clen8c[cc] : 0;
+      md_cb = cc < nch ? cbase[cc] : 0;
+    }
+    const int kl = k & (kWave - 1);
+    const int32_t L8c = __builtin_amdgcn_readlane(md_l8, kl);
+    const int64_t cb = int64_t(uint32_t(__builtin_amdgcn_readlane(int32_t(md_cb), kl))) |
+                       (int64_t(__builtin_amdgcn_readlane(int32_t(md_cb >> 32), kl)) << 32);
+    const int64_t pos = c * kRowsPerChunk + r;
+    const int64_t off = cb * kChunkStride + lane * kGroup;
+    const RowIn ri = row_in(p, pos);
+    if (L8c >= 0) {
+      const uint4 hv = hdense[c * kWave + lane];
+      const uint16_t* sl = p.cslot + off;
+      const bool reg = L8c <= kMaxColdGroups;
+      uint4 v[kMaxColdGroups];
+      if (reg) {
+#pragma unroll
+        for (int g = 0; g < kMaxColdGroups; ++g)
+          if (g < L8c) v[g] = *reinterpret_cast<const uint4*>(sl + int64_t(g) * kChunkStride);
+      }
+      float d0 = hot_dot(hv, wq), d1 = 0.f;
+      if (reg) {
+#pragma unroll
+        for (int g = 0; g < kMaxColdGroups; ++g)
+          if (g < L8c) {
+            uint32_t s[8];
+            unpack8(v[g], s);
+            d0 += wl[s[0]] + wl[s[2]] + wl[s[4]] + wl[s[6]];
+            d1 += wl[s[1]] + wl[s[3]] + wl[s[5]] + wl[s[7]];
+          }
+      } else {
+        for (int32_t g = 0; g < L8c; ++g) {
+          uint32_t s[8];
+          unpack8(*reinterpret_cast<const uint4*>(sl + int64_t(g) * kChunkStride), s);
+          d0 += wl[s[0]] + wl[s[2]] + wl[s[4]] + wl[s[6]];
+          d1 += wl[s[1]] + wl[s[3]] + wl[s[5]] + wl[s[7]];
+        }
+      }
+      float dot = d0 + d1;
+      dot += __shfl_xor(dot, 1, kWave);
+      dot += __shfl_xor(dot, 2, kWave);
+      const float res = row_residual<STATS, SAMPLE>(dot, ri, pos, t, d, p, sp, n_kept, w0, w1, w2, w3, acc);
+      if (res != 0.f) {
+        // opaque copy: re-extract the counts instead of keeping 32 converted
+        // floats live across the residual (register pressure)
+        uint4 hg = hv;
+        asm volatile("" : "+v"(hg.x), "+v"(hg.y), "+v"(hg.z), "+v"(hg.w));
+        hot_grad(hg, res, gh);
+        const unsigned long long q = to_fix(res, clamped, sp.fix_lim);
+        if (reg) {
+#pragma unroll
+          for (int g = 0; g < kMaxColdGroups; ++g)
+            if (g < L8c) {
+              uint32_t s[8];
+              unpack8(v[g], s);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) atomicAdd(&gl[s[e] * REP + rep], q);
+            }
+        } else {
+          for (int32_t g = 0; g < L8c; ++g) {
+            uint32_t s[8];
+            unpack8(*reinterpret_cast<const uint4*>(sl + int64_t(g) * kChunkStride), s);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) atomicAdd(&gl[s[e] * REP + rep], q);
+          }
+        }
+      }
+    } else {  // plain layout: every entry (hot ones too) through the LDS gradient
+      const int32_t L8 = p.clen8[c];
+      const uint16_t* sl = slot + off;
+      float dot = 0.f;
+      for (int32_t g = 0; g < L8; ++g) {
+        uint32_t s[8];
+        unpack8(*reinterpret_cast<const uint4*>(sl + int64_t(g) * kChunkStride), s);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) dot += wl[s[k]];
+      }
+      dot += __shfl_xor(dot, 1, kWave);
+      dot += __shfl_xor(dot, 2, kWave);
+      const float res = row_residual<STATS, SAMPLE>(dot, ri, pos, t, d, p, sp, n_kept, w0, w1, w2, w3, acc);
+      if (res != 0.f) {
+        const unsigned long long q = to_fix(res, clamped, sp.fix_lim);
+        for (int32_t g = 0; g < L8; ++g) {
+          uint32_t s[8];
+          unpack8(*reinterpret_cast<const uint4*>(sl + int64_t(g) * kChunkStride), s);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) atomicAdd(&gl[s[k] * REP + rep], q);
+        }
+      }
+    }
+  }
+
+  flush_scalars<STATS, SAMPLE>(d, acc, scratch);
+  if (__any(clamped) && lane == 0) d.state[7] = 1.0;
+  // hot gradient: sum the 16 lanes of each quarter t, then the 16 waves
+#pragma unroll
+  for (int i = 0; i < kHotPerLane; ++i) {
+    float v = gh[i];
+    v += __shfl_xor(v, 4, kWave);
+    v += __shfl_xor(v, 8, kWave);
+    v += __shfl_xor(v, 16, kWave);
+    v += __shfl_xor(v, 32, kWave);
+    if (lane < kLanesPerRow) hsum[w][kHotPerLane * lane + i] = v;
+  }
+  __syncthreads();
+  const int64_t hi = kNumNumeric + d.n_unique;  // pads are never flushed
+  for (int64_t s = kNumNumeric + threadIdx.x; s < hi; s += kIterBlock) {
+    long long v = 0;
+#pragma unroll
+    for (int k = 0; k < REP; ++k) v += (long long)gl[s * REP + k];
+    if (v != 0) atomicAdd(&d.g64[s], double(v) * kFixInv);
+  }
+  for (int h = threadIdx.x; h < kHot; h += kIterBlock) {
+    double v = 0.0;
+    for (int k = 0; k < kIterBlock / kWave; ++k) v += double(hsum[k][h]);
+    const int32_t s = p.hot_slot[h];
+    if (v != 0.0 && s < hi) atomicAdd(&d.g64[s], v);
   }
 }
 
@@ -345,10 +583,27 @@ int sgd_lds_rep(int64_t ns) {
   return 0;
 }
 
+bool sgd_hybrid_fits(int64_t ns) {
+  const int rep = sgd_lds_rep(ns);
+  const int64_t statics = int64_t(kIterBlock / kWave) * (kHot * int64_t(sizeof(float)) + int64_t(sizeof(double)));
+  return ns <= kMaxHybridSlots && rep > 0 && lds_bytes(ns, rep) + statics <= 160 * 1024 - 1024;
+}
+
 template <bool STATS, bool SAMPLE>
 static void launch_iter_t(const DevSgd& d, const DevPrepared& p, const SgdParams& sp, bool u16,
                           int rep, int grid, hipStream_t s) {
-  if (u16 && rep > 0) {
+  if (u16 && rep > 0 && p.hybrid) {
+    const size_t lds = size_t(lds_bytes(d.ns, rep));
+#define TWTML_HYB(R) \
+  hipLaunchKernelGGL((k_sgd_iter_hyb<STATS, SAMPLE, R>), dim3(grid), dim3(kIterBlock), lds, s, d, p, sp)
+    switch (rep) {
+      case 8: TWTML_HYB(8); break;
+      case 4: TWTML_HYB(4); break;
+      case 2: TWTML_HYB(2); break;
+      default: TWTML_HYB(1); break;
+    }
+#undef TWTML_HYB
+  } else if (u16 && rep > 0) {
     const size_t lds = size_t(lds_bytes(d.ns, rep));
 #define TWTML_ITER(R, C) \
   hipLaunchKernelGGL((k_sgd_iter_lds<STATS, SAMPLE, R, C>), dim3(grid), dim3(kIterBlock), lds, s, d, p, sp)

@@ -77,10 +77,11 @@ def test_featurize_matches_oracle(hip_module, F, hash):
     np.testing.assert_allclose(num, want_num, rtol=2e-7, atol=0)
 
 
-@pytest.mark.parametrize("F,dedup", [(1000, False), (1 << 20, False), (1000, True)])
-def test_sgd_matches_oracle_over_batches(hip_module, F, dedup):
+@pytest.mark.parametrize("F,dedup,hybrid", [(1000, False, True), (1 << 20, False, True),
+                                             (1000, True, False), (1000, False, False)])
+def test_sgd_matches_oracle_over_batches(hip_module, F, dedup, hybrid):
     cfg = SynthConfig.profile("twitter", seed=5, unicode_fraction=0.1)
-    eng = _engine(F, step_size=0.005, num_iterations=50, dedup=dedup)
+    eng = _engine(F, step_size=0.005, num_iterations=50, dedup=dedup, hybrid=hybrid)
     w = np.zeros(F + 4)
     for t in range(4):
         raw = generate_batch(cfg, t * 2500, 2500, batch_time_ms=NOW + t * 5000)
@@ -166,3 +167,72 @@ def test_merged_counts_match_hashingtf(hip_module):
             a, b = Xt.indptr[k], Xt.indptr[k + 1]
             want = dict(zip(Xt.indices[a:b].tolist(), Xt.data[a:b].astype(int).tolist()))
             assert got == want, f"row {k}"
+
+
+def _with_repeats(raw, every=7, text="ha" * 40):
+    """Replace every `every`-th text so some bigrams repeat > 15 times in a row."""
+    from twitter_stream_ml_amd.records.batch import RawBatch, utf16_units
+    texts = [text if i % every == 0 else raw.text_of(i) for i in range(raw.n)]
+    units = [utf16_units(t) for t in texts]
+    off = np.zeros(raw.n + 1, np.int64)
+    off[1:] = np.cumsum([u.shape[0] for u in units])
+    return RawBatch(np.concatenate(units), off, raw.is_retweet, raw.scalars, raw.batch_time_ms)
+
+
+@pytest.mark.parametrize("repeats", [False, True])
+def test_hybrid_layout_matches_hashingtf(hip_module, repeats):
+    """Hybrid layout: 4-bit hot counts + cold SELL entries == HashingTF term counts."""
+    F = 1000
+    cfg = SynthConfig.profile("twitter", seed=14, unicode_fraction=0.2)
+    raw = generate_batch(cfg, 0, 4000, batch_time_ms=NOW)
+    if repeats:
+        raw = _with_repeats(raw)
+    eng = _engine(F, "java", hybrid=True)
+    eng.train_batch(raw, want_pred=False)
+    dbg = eng._eng.debug_prepared()
+    hy = eng._eng.debug_hybrid()
+    assert hy["clen8c"].shape[0] > 0, "hybrid layout should be active for a small active set"
+    uniq = np.sort(dbg["uniq"])
+    nU = uniq.shape[0]
+    hot_slot = hy["hot_slot"]
+    real_hot = (hot_slot >= 4) & (hot_slot < 4 + nU)
+    assert real_hot.sum() == min(128, nU)
+    assert np.unique(hot_slot[real_hot]).shape[0] == real_hot.sum()
+    fb = featurize_batch(raw, F, 100, 1000, now_ms=NOW)
+    Xt = fb.X[:, :F].tocsr()
+    perm, cbase, clen8 = dbg["perm"], dbg["cbase"], dbg["clen8"]
+    dense = hy["hot_dense"].reshape(-1, 64, 4)
+    cslot = hy["cslot"]
+    big = 0
+    for c in range(hy["clen8c"].shape[0]):
+        L8c = int(hy["clen8c"][c])
+        assert 0 <= L8c <= int(clen8[c])
+        g0 = int(cbase[c])
+        blk = cslot[g0 * 512:(g0 + L8c) * 512].reshape(L8c, 64, 8)
+        for r in range(16):
+            k = int(perm[c * 16 + r])
+            if k < 0:
+                continue
+            got = {}
+            for t in range(4):
+                words = dense[c, 4 * r + t]
+                for i in range(32):
+                    n = (int(words[i // 8]) >> (4 * (i % 8))) & 15
+                    if n:
+                        fid = int(uniq[hot_slot[32 * t + i] - 4])
+                        got[fid] = got.get(fid, 0) + n
+            sl = blk[:, 4 * r:4 * r + 4, :].reshape(-1)
+            sl = sl[(sl >= 4) & (sl < 4 + nU)]
+            for fid in uniq[sl - 4].tolist():
+                got[fid] = got.get(fid, 0) + 1
+            a, b = Xt.indptr[k], Xt.indptr[k + 1]
+            want = dict(zip(Xt.indices[a:b].tolist(), Xt.data[a:b].astype(int).tolist()))
+            big += sum(1 for v in want.values() if v > 15)
+            assert got == want, f"row {k}"
+    if repeats:
+        assert big > 0, "test data should exercise the > 15 count overflow"
+    # the hybrid iteration trains like the plain one
+    plain = _engine(F, "java", hybrid=False)
+    plain.train_batch(raw, want_pred=False)
+    wh, wp = eng.get_weights(), plain.get_weights()
+    np.testing.assert_allclose(wh, wp, rtol=1e-4, atol=1e-6 * np.abs(wp).max())

@@ -55,6 +55,8 @@ class LRDeviceConfig:
     # Measured on MI355X (1M-tweet batches, 35 iterations): -7% per iteration
     # but the merge pass costs more than it saves, so it is off by default.
     dedup: bool = False
+    # dense 4-bit counts for the batch's 128 hottest bigrams (csrc/hip/hot_split.hip)
+    hybrid: bool = True
 
     def as_dict(self) -> Dict[str, object]:
         return {
@@ -73,6 +75,7 @@ class LRDeviceConfig:
             "sgd_grid": int(self.sgd_grid),
             "ablate": int(self.ablate),
             "dedup": int(bool(self.dedup)),
+            "hybrid": int(bool(self.hybrid)),
         }
 
 
