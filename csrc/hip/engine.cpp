@@ -65,6 +65,7 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
   sgd_.stats = dmalloc<double>(8);
   sgd_.state = dmalloc<double>(8);
   sgd_.loss_hist = dmalloc<double>(size_t(std::max(1, cfg_.num_iterations)) + 2);
+  sgd_.itrec = dmalloc<double>((size_t(std::max(1, cfg_.num_iterations)) + 2) * kRecStride);
   sgd_.pred_out = dmalloc<float>(size_t(cfg_.max_rows));
   TWTML_HIP_CHECK(hipMemset(sgd_.red64, 0, 4 * sizeof(double)));
   ensure_compact(4096);
@@ -125,6 +126,16 @@ void LREngine::alloc_prepared() {
   prep_.counters = dmalloc<int64_t>(8);
 }
 
+void LREngine::ensure_part(int64_t n) {
+  if (n <= part_cap_) return;
+  if (sgd_.part) {
+    TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
+    (void)hipFree(sgd_.part);
+  }
+  part_cap_ = std::max<int64_t>(n, part_cap_ * 2);
+  sgd_.part = dmalloc<double>(size_t(part_cap_));
+}
+
 void LREngine::ensure_compact(int64_t ns) {
   if (ns <= ns_cap_) return;
   int64_t cap = std::max<int64_t>(ns, ns_cap_ * 2);
@@ -152,7 +163,7 @@ LREngine::~LREngine() {
                   prep_.cbase, prep_.idx, prep_.slot, prep_.y, prep_.num, prep_.perm,
                   prep_.flags, prep_.uniq, prep_.slot_of, prep_.ublk, prep_.counters,
                   sgd_.w64, sgd_.wc64, sgd_.wc32, sgd_.g64, sgd_.red64, sgd_.stats, sgd_.state,
-                  sgd_.loss_hist, sgd_.pred_out, lower_page_, lower_blocks_, n_global_};
+                  sgd_.loss_hist, sgd_.pred_out, sgd_.part, sgd_.itrec, lower_page_, lower_blocks_, n_global_};
   for (void* b : bufs) if (b) (void)hipFree(b);
   if (host_counters_) (void)hipHostFree(host_counters_);
   if (host_out_) (void)hipHostFree(host_out_);
@@ -239,6 +250,9 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   TWTML_HIP_CHECK(hipEventRecord(ev_[1], s));
 
   int grid = cfg_.sgd_grid > 0 ? cfg_.sgd_grid : sgd_iter_grid(ns, res.n_kept, num_cu_);
+  sgd_.pstride = sgd_part_stride(ns);
+  sgd_.nparts = sgd_partials(ns, u16, grid);
+  ensure_part(int64_t(sgd_.nparts) * sgd_.pstride);
   SgdParams sp{};
   sp.step_size = cfg_.step_size;
   sp.fraction = cfg_.fraction;
@@ -251,12 +265,14 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   // entries one workgroup can add into a slot: its share of the chunks (x2 for imbalance)
   sp.fix_lim = sgd_fix_limit(2 * (res.entries / std::max(1, grid)) + 65536);
   if (n_glob > 0) {
-    // Host-side early stop: the convergence flag (state[0]) of iteration i is
-    // copied to pinned memory behind an event; the host keeps at most
-    // `depth` iterations queued ahead and stops enqueueing once the flag of
-    // an earlier iteration is set.  The flag derives from all-reduced values,
-    // so every rank stops at the same iteration and the collectives match.
-    const int depth = std::max(1, cfg_.early_exit_depth);
+    // Host-side early stop: the convergence test of update j runs in the
+    // prologue of iteration j+1's gradient kernel, which copies its verdict
+    // to pinned memory (zero copy); an event after that kernel lets the host
+    // keep at most `depth` iterations queued and stop enqueueing once an
+    // earlier verdict is set.  Verdicts derive from all-reduced values in a
+    // fixed summation order, so every rank stops at the same iteration and
+    // the collectives match.
+    const int depth = std::max(2, cfg_.early_exit_depth);
     const int iters = cfg_.num_iterations;
     if (int(iter_events_.size()) < iters + 1) {
       for (int k = int(iter_events_.size()); k < iters + 1; ++k) {
@@ -265,26 +281,30 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
         iter_events_.push_back(e);
       }
     }
-    for (int i = 1; i <= cfg_.num_iterations; ++i) {
+    std::fill(host_flags_, host_flags_ + iters + 2, 0.0);
+    // single GPU with partial rows: the update kernel reduces them itself
+    const bool fused = world == 1 && sgd_.nparts > 0;
+    for (int i = 1; i <= iters; ++i) {
       if (i > depth) {
-        const int j = i - depth;                       // flag after iteration j
+        const int j = i - depth;                       // verdict after update j
         TWTML_HIP_CHECK(hipEventSynchronize(iter_events_[size_t(j)]));
         if (std::getenv("TWTML_DEBUG_EARLY"))
           std::fprintf(stderr, "early-stop check i=%d j=%d flag=%g\n", i, j, host_flags_[j]);
         if (host_flags_[j] != 0.0) break;
       }
       sp.iteration = i;
-      if (res.n_kept > 0) launch_sgd_iter(sgd_, prep_, sp, host_counters_[2], u16, grid, s);
-      else if (i == 1 || sp.sample) {
-        // nothing local to add; still participate in the collectives below
-      }
+      // every rank launches the gradient kernel (an empty shard writes zero
+      // partials) so every rank runs the convergence prologue
+      launch_sgd_iter(sgd_, prep_, sp, host_counters_[2], u16, grid, s);
+      if (i > 1) TWTML_HIP_CHECK(hipEventRecord(iter_events_[size_t(i - 1)], s));
       if (world > 1) {
+        launch_sgd_reduce(sgd_, sp, s);
         comm_->allreduce(sgd_.g64, size_t(ns + 1), ncclFloat64, ncclSum, s);
-        if (sp.sample) comm_->allreduce(sgd_.red64, 2, ncclFloat64, ncclSum, s);
+        if (sp.sample) comm_->allreduce(sgd_.red64 + 2 * (i & 1), 2, ncclFloat64, ncclSum, s);
       }
-      launch_sgd_update(sgd_, sp, s);   // writes host_flags_[i] (zero copy)
-      TWTML_HIP_CHECK(hipEventRecord(iter_events_[size_t(i)], s));
+      launch_sgd_update(sgd_, sp, fused ? sgd_.nparts : 0, s);
     }
+    launch_sgd_finish(sgd_, sp, s);
     launch_scatter_w(sgd_, prep_, s);
   }
   TWTML_HIP_CHECK(hipEventRecord(ev_[2], s));

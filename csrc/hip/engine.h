@@ -103,6 +103,7 @@ class LREngine {
  private:
   void alloc_prepared();
   void ensure_compact(int64_t ns);
+  void ensure_part(int64_t n);
 
   int device_;
   LRConfig cfg_;
@@ -112,6 +113,7 @@ class LREngine {
   DevPrepared prep_{};
   DevSgd sgd_{};
   int64_t ns_cap_ = 0;
+  int64_t part_cap_ = 0;
   uint8_t* lower_page_ = nullptr;
   uint16_t* lower_blocks_ = nullptr;
   int64_t* host_counters_ = nullptr;  // pinned [8]

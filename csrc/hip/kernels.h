@@ -133,10 +133,23 @@ struct DevSgd {
   double* loss_hist;    // [max_iters+1]
   float* pred_out;      // [R] rounded predictions in kept order (optional)
   double* host_flags;   // [max_iters+1] pinned host memory: done flag after each update
+  double* part;         // [nparts][pstride] per-workgroup partial gradients (LDS paths)
+  double* itrec;        // [max_iters+2][kRecStride] per-iteration update records
   int64_t F;
   int64_t ns;           // 4 + n_unique + pads (rounded)
   int64_t n_unique;
+  int64_t pstride;      // ns + 64: slots, then loss, m, 6 batch stats (see sgd_part_stride)
+  int32_t nparts;       // partial rows written by the last iteration launch (0 = global path)
 };
+
+// Iteration record: [0] updates so far, [1] m, [2] update workgroups,
+// [kRecHead + 2w] ||dw||^2 and ||w||^2 partials of update workgroup w.
+constexpr int kMaxUpdGrid = 256;
+constexpr int kRecHead = 8;
+constexpr int kRecStride = kRecHead + 2 * kMaxUpdGrid;
+
+// Partial-row stride for a compact space of ns slots (multiple of 64).
+constexpr int64_t sgd_part_stride(int64_t ns) { return ns + 64; }
 
 struct SgdParams {
   double step_size;
@@ -147,7 +160,9 @@ struct SgdParams {
   int64_t row_offset;   // global row id of this rank's kept row 0 (sampling)
   int32_t want_pred;
   int32_t sample;       // fraction < 1
-  int32_t ablate;       // perf diagnostics: 1 = skip scatter, 2 = skip gather+scatter
+  int32_t ablate;       // perf diagnostics: 1 = skip scatter, 2 = skip gather+scatter,
+                        // hybrid only: 3 = skip hot grad, 4 = skip hot dot, 5 = skip cold scatter,
+                        // 6 = loads only, 7 = no chunks (fixed cost)
   float fix_lim;        // |r| * 2^24 clamp so a workgroup's int64 slot sums cannot overflow
 };
 
@@ -159,7 +174,15 @@ void launch_gather_w(const DevSgd& d, const DevPrepared& p, hipStream_t s);
 void launch_norm2(const double* v, int64_t n, double* out, hipStream_t s);
 void launch_sgd_iter(const DevSgd& d, const DevPrepared& p, const SgdParams& sp, int64_t groups,
                      bool u16, int grid, hipStream_t s);
-void launch_sgd_update(const DevSgd& d, const SgdParams& sp, hipStream_t s);
+// Partial rows an iteration launch of `grid` workgroups writes (0: the
+// generic path accumulates straight into g64).
+int sgd_partials(int64_t ns, bool u16, int grid);
+// g64 (+ loss, m, stats) += sum of the d.nparts partial rows
+void launch_sgd_reduce(const DevSgd& d, const SgdParams& sp, hipStream_t s);
+// nparts > 0: sums the partial rows itself (single GPU, no separate reduce)
+void launch_sgd_update(const DevSgd& d, const SgdParams& sp, int nparts, hipStream_t s);
+// after the GD loop: convergence of the last update -> state
+void launch_sgd_finish(const DevSgd& d, const SgdParams& sp, hipStream_t s);
 void launch_scatter_w(const DevSgd& d, const DevPrepared& p, hipStream_t s);
 int sgd_lds_rep(int64_t ns);
 // the hybrid iteration kernel's LDS (gradient replicas + hot partials) fits

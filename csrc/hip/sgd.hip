@@ -44,6 +44,12 @@ constexpr float kFixScale = 16777216.0f;        // 2^24
 constexpr double kFixInv = 1.0 / 16777216.0;
 constexpr float kFixClamp = 67108864.0f;        // 2^26
 
+// Iteration record i (k_sgd_update -> convergence test) and the sampled row
+// count of iteration i (double-buffered by parity: iteration i+1's count is
+// zeroed while iteration i's is still being read).
+__device__ __forceinline__ double* sgd_rec(const DevSgd& d, int it) { return d.itrec + int64_t(it) * kRecStride; }
+__device__ __forceinline__ double* sgd_red_m(const DevSgd& d, int it) { return d.red64 + 2 * (it & 1) + 1; }
+
 template <typename SlotT>
 struct SlotLoad;
 
@@ -126,7 +132,7 @@ __device__ __forceinline__ float row_residual(float dot, int64_t pos, int t, con
 }
 
 template <bool STATS, bool SAMPLE>
-__device__ __forceinline__ void flush_scalars(const DevSgd& d, const RowAcc& acc, double* scratch) {
+__device__ __forceinline__ void flush_scalars(const DevSgd& d, const RowAcc& acc, double* scratch, int it) {
   const double b0 = block_sum<double>(acc.gn0, scratch);
   const double b1 = block_sum<double>(acc.gn1, scratch);
   const double b2 = block_sum<double>(acc.gn2, scratch);
@@ -143,10 +149,52 @@ __device__ __forceinline__ void flush_scalars(const DevSgd& d, const RowAcc& acc
     atomicAdd(&d.g64[2], b2);
     atomicAdd(&d.g64[3], b3);
     atomicAdd(&d.g64[d.ns], bl);
-    if (SAMPLE) atomicAdd(&d.red64[1], bm);
+    if (SAMPLE) atomicAdd(sgd_red_m(d, it), bm);
     if (STATS)
       for (int k = 0; k < 6; ++k) atomicAdd(&d.stats[k], bs[k]);
   }
+}
+
+// Workgroup epilogue without contended atomics.  Every workgroup writes one
+// partial row (plain stores) that k_sgd_reduce sums in a fixed order:
+//   cols 0..3 numeric gradients, 4..hi-1 text slots, hi..ns-1 pads (0),
+//   ns loss, ns+1 sampled row count, ns+2..ns+7 batch stats (STATS).
+// (256 workgroups adding into the same fp64 addresses serialise at the
+// memory-side atomic units: ~10-20 us per launch on MI355X, measured.)
+constexpr int kPartVals = 12;
+
+template <bool STATS, bool SAMPLE>
+__device__ __forceinline__ void part_scalars(const DevSgd& d, const RowAcc& acc,
+                                             double (*wsc)[kPartVals], double* prow) {
+  double v[kPartVals] = {double(acc.gn0), double(acc.gn1), double(acc.gn2), double(acc.gn3),
+                         0.5 * double(acc.loss), acc.msum, acc.st[0], acc.st[1], acc.st[2],
+                         acc.st[3], acc.st[4], acc.st[5]};
+  constexpr int nv = STATS ? kPartVals : (SAMPLE ? 6 : 5);
+  const int w = threadIdx.x / kWave;
+#pragma unroll
+  for (int k = 0; k < nv; ++k) v[k] = wave_sum(v[k]);
+  if (lane_id() == 0) {
+#pragma unroll
+    for (int k = 0; k < nv; ++k) wsc[w][k] = v[k];
+  }
+  __syncthreads();
+  const int tid = threadIdx.x;
+  if (tid < kPartVals) {
+    double t = 0.0;
+    if (tid < nv)
+      for (int k = 0; k < int(blockDim.x) / kWave; ++k) t += wsc[k][tid];
+    prow[tid < kNumNumeric ? int64_t(tid) : d.ns + (tid - kNumNumeric)] = t;
+  }
+}
+
+// Text-slot columns of a partial row: the REP fixed-point replicas summed
+// (+ the hot total of a hot slot).
+template <int REP>
+__device__ __forceinline__ double part_slot(const unsigned long long* gl, int64_t s) {
+  long long v = 0;
+#pragma unroll
+  for (int k = 0; k < REP; ++k) v += (long long)gl[s * REP + k];
+  return double(v) * kFixInv;
 }
 
 float sgd_fix_limit(int64_t entries_per_wg) {
@@ -171,11 +219,55 @@ constexpr int kIterBlock = 1024;
 
 // CNT: entries carry HashingTF term counts (p.cnt, merged duplicates, chunk
 // lengths p.clen8d); otherwise every entry counts once.
+// Convergence after update `it`, evaluated by one wave (lane-parallel loads,
+// fixed-order DPP reduction): identical in every caller.
+__device__ bool sgd_converged_wave(const DevSgd& d, int it, double tol) {
+  const double* rec = sgd_rec(d, it);
+  const int nw = int(rec[2]);
+  double ds = 0.0, ws = 0.0;
+  for (int k = lane_id(); k < nw; k += kWave) {
+    ds += rec[kRecHead + 2 * k];
+    ws += rec[kRecHead + 2 * k + 1];
+  }
+  ds = wave_sum(ds);
+  ws = wave_sum(ws);
+  if (!(rec[1] > 0.0) || rec[0] < 2.0) return false;   // no update this iteration / first update
+  double rest = d.state[4] - d.state[6];
+  if (rest < 0.0) rest = 0.0;
+  const double wnorm = sqrt(ws + rest);
+  return sqrt(ds) < tol * (wnorm > 1.0 ? wnorm : 1.0);
+}
+
+// Iteration-kernel prologue: true when the batch is finished (the caller
+// returns).  Called by every thread; `flag` is a workgroup-shared int.
+__device__ bool sgd_stop(const DevSgd& d, const SgdParams& sp, int* flag) {
+  if (threadIdx.x < kWave) {
+    bool stop = d.state[0] != 0.0;
+    if (!stop && sp.iteration > 1) {
+      stop = sgd_converged_wave(d, sp.iteration - 1, sp.tol);
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (stop) {
+          d.state[0] = 1.0;
+          d.state[1] = 1.0;
+        }
+        if (d.host_flags) {           // zero-copy early-stop signal to the host
+          d.host_flags[sp.iteration - 1] = stop ? 1.0 : 0.0;
+          __threadfence_system();
+        }
+      }
+    }
+    if (threadIdx.x == 0) *flag = stop ? 1 : 0;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
 template <bool STATS, bool SAMPLE, int REP, bool CNT>
 __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_lds(DevSgd d, DevPrepared p, SgdParams sp) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  __shared__ double scratch[kIterBlock / kWave];
-  if (d.state[0] != 0.0) return;  // converged / finished: the rest of the batch is a no-op
+  __shared__ double wsc[kIterBlock / kWave][kPartVals];
+  __shared__ int stop_flag;
+  if (sgd_stop(d, sp, &stop_flag)) return;  // converged / finished: the rest of the batch is a no-op
   const int64_t ns = d.ns;        // multiple of 64
   float* wl = lds;
   unsigned long long* gl = reinterpret_cast<unsigned long long*>(lds + ns);
@@ -293,16 +385,12 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_lds(DevSgd d, DevPrepar
     }
   }
 
-  flush_scalars<STATS, SAMPLE>(d, acc, scratch);
   if (__any(clamped) && lane == 0) d.state[7] = 1.0;
-  __syncthreads();
-  const int64_t hi = kNumNumeric + d.n_unique;  // pads are never flushed
-  for (int64_t s = kNumNumeric + threadIdx.x; s < hi; s += kIterBlock) {
-    long long v = 0;
-#pragma unroll
-    for (int k = 0; k < REP; ++k) v += (long long)gl[s * REP + k];
-    if (v != 0) atomicAdd(&d.g64[s], double(v) * kFixInv);
-  }
+  double* prow = d.part + int64_t(blockIdx.x) * d.pstride;
+  part_scalars<STATS, SAMPLE>(d, acc, wsc, prow);   // includes the block barrier
+  const int64_t hi = kNumNumeric + d.n_unique;      // pads are never flushed
+  for (int64_t s = kNumNumeric + threadIdx.x; s < ns; s += kIterBlock)
+    prow[s] = s < hi ? part_slot<REP>(gl, s) : 0.0;
 }
 
 // ---------------------------------------------------------------------------
@@ -349,10 +437,11 @@ __device__ __forceinline__ void hot_grad(const uint4 hv, float res, float (&gh)[
 template <bool STATS, bool SAMPLE, int REP>
 __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_hyb(DevSgd d, DevPrepared p, SgdParams sp) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  __shared__ double scratch[kIterBlock / kWave];
+  __shared__ double wsc[kIterBlock / kWave][kPartVals];
   __shared__ float hsum[kIterBlock / kWave][kHot];
   __shared__ __attribute__((aligned(16))) float whl[kLanesPerRow * kHotLdsStride];
-  if (d.state[0] != 0.0) return;
+  __shared__ int stop_flag;
+  if (sgd_stop(d, sp, &stop_flag)) return;
   const int64_t ns = d.ns;
   float* wl = lds;
   unsigned long long* gl = reinterpret_cast<unsigned long long*>(lds + ns);
@@ -366,7 +455,7 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_hyb(DevSgd d, DevPrepar
   const int r = lane / kLanesPerRow, t = lane % kLanesPerRow;
   const int rep = lane % REP;
   const int64_t n_kept = p.counters[0];
-  const int64_t nch = (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;
+  const int64_t nch = sp.ablate == 7 ? 0 : (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;  // 7: fixed cost
   const int64_t wave = int64_t(blockIdx.x) * (kIterBlock / kWave) + w;
   const int64_t nwaves = int64_t(gridDim.x) * (kIterBlock / kWave);
   const uint16_t* slot = static_cast<const uint16_t*>(p.slot);
@@ -411,7 +500,18 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_hyb(DevSgd d, DevPrepar
         for (int g = 0; g < kMaxColdGroups; ++g)
           if (g < L8c) v[g] = *reinterpret_cast<const uint4*>(sl + int64_t(g) * kChunkStride);
       }
-      float d0 = hot_dot(hv, wq), d1 = 0.f;
+      if (sp.ablate == 6) {  // loads only: memory floor of the chunk stream
+        uint32_t x = hv.x ^ hv.y ^ hv.z ^ hv.w ^ __float_as_uint(ri.y + ri.n0 + ri.n1 + ri.n2 + ri.n3);
+        if (reg) {
+#pragma unroll
+          for (int g = 0; g < kMaxColdGroups; ++g)
+            if (g < L8c) x ^= v[g].x ^ v[g].y ^ v[g].z ^ v[g].w;
+        }
+        acc.loss += float(x & 1u);
+        continue;
+      }
+      // ablate 4: no hot dot (counts still loaded)
+      float d0 = sp.ablate == 4 ? __uint_as_float(hv.x & 1u) : hot_dot(hv, wq), d1 = 0.f;
       if (reg) {
 #pragma unroll
         for (int g = 0; g < kMaxColdGroups; ++g)
@@ -438,7 +538,8 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_hyb(DevSgd d, DevPrepar
         // floats live across the residual (register pressure)
         uint4 hg = hv;
         asm volatile("" : "+v"(hg.x), "+v"(hg.y), "+v"(hg.z), "+v"(hg.w));
-        hot_grad(hg, res, gh);
+        if (sp.ablate != 1 && sp.ablate != 3) hot_grad(hg, res, gh);   // ablate 3: no hot grad
+        if (sp.ablate == 1 || sp.ablate == 5) continue;                 // 1/5: no cold scatter
         const unsigned long long q = to_fix(res, clamped, sp.fix_lim);
         if (reg) {
 #pragma unroll
@@ -483,9 +584,8 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_hyb(DevSgd d, DevPrepar
     }
   }
 
-  flush_scalars<STATS, SAMPLE>(d, acc, scratch);
   if (__any(clamped) && lane == 0) d.state[7] = 1.0;
-  // hot gradient: sum the 16 lanes of each quarter t, then the 16 waves
+  // hot gradient: sum the 16 lanes of each quarter t (per wave), into LDS
 #pragma unroll
   for (int i = 0; i < kHotPerLane; ++i) {
     float v = gh[i];
@@ -495,19 +595,21 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_hyb(DevSgd d, DevPrepar
     v += __shfl_xor(v, 32, kWave);
     if (lane < kLanesPerRow) hsum[w][kHotPerLane * lane + i] = v;
   }
-  __syncthreads();
-  const int64_t hi = kNumNumeric + d.n_unique;  // pads are never flushed
-  for (int64_t s = kNumNumeric + threadIdx.x; s < hi; s += kIterBlock) {
-    long long v = 0;
-#pragma unroll
-    for (int k = 0; k < REP; ++k) v += (long long)gl[s * REP + k];
-    if (v != 0) atomicAdd(&d.g64[s], double(v) * kFixInv);
-  }
-  for (int h = threadIdx.x; h < kHot; h += kIterBlock) {
+  double* prow = d.part + int64_t(blockIdx.x) * d.pstride;
+  part_scalars<STATS, SAMPLE>(d, acc, wsc, prow);   // includes the block barrier
+  const int64_t hi = kNumNumeric + d.n_unique;      // pads are never flushed
+  for (int64_t s = kNumNumeric + threadIdx.x; s < ns; s += kIterBlock) {
     double v = 0.0;
-    for (int k = 0; k < kIterBlock / kWave; ++k) v += double(hsum[k][h]);
-    const int32_t s = p.hot_slot[h];
-    if (v != 0.0 && s < hi) atomicAdd(&d.g64[s], v);
+    if (s < hi) {
+      v = part_slot<REP>(gl, s);
+      const uint32_t h = p.hot_of[s];
+      if (h != 0xFFu) {
+        double hv = 0.0;
+        for (int k = 0; k < kIterBlock / kWave; ++k) hv += double(hsum[k][h]);
+        v += hv;
+      }
+    }
+    prow[s] = v;
   }
 }
 
@@ -516,7 +618,8 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_hyb(DevSgd d, DevPrepar
 template <typename SlotT, bool STATS, bool SAMPLE>
 __global__ __launch_bounds__(kBlock) void k_sgd_iter_global(DevSgd d, DevPrepared p, SgdParams sp) {
   __shared__ double scratch[kBlock / kWave];
-  if (d.state[0] != 0.0) return;
+  __shared__ int stop_flag;
+  if (sgd_stop(d, sp, &stop_flag)) return;
   const float* w = d.wc32;
   const int lane = lane_id();
   const int r = lane / kLanesPerRow, t = lane % kLanesPerRow;
@@ -551,7 +654,7 @@ __global__ __launch_bounds__(kBlock) void k_sgd_iter_global(DevSgd d, DevPrepare
       }
     }
   }
-  flush_scalars<STATS, SAMPLE>(d, acc, scratch);
+  flush_scalars<STATS, SAMPLE>(d, acc, scratch, sp.iteration);
 }
 
 // LDS bytes of the fast path for a given replication factor.
@@ -647,71 +750,185 @@ void launch_sgd_iter(const DevSgd& d, const DevPrepared& p, const SgdParams& sp,
   else launch_iter_t<false, false>(d, p, sp, u16, rep, grid, s);
 }
 
+int sgd_partials(int64_t ns, bool u16, int grid) {
+  return (u16 && sgd_lds_rep(ns) > 0) ? grid : 0;
+}
+
 // ---------------------------------------------------------------------------
-// SimpleUpdater + convergence test (one workgroup, fp64 master weights).
+// Per-iteration protocol (no grid-wide barrier, no contended atomics):
+//
+//   k_sgd_iter_*  (iteration i)  prologue: converged after update i-1?  ->
+//                 every workgroup decides from record i-1 (fixed-order sums,
+//                 so all workgroups -- and all DP ranks -- agree); workgroup
+//                 0 publishes state[0..1] and the host flag.  Then one
+//                 partial gradient row per workgroup.
+//   [k_sgd_reduce + RCCL all-reduce of g64 when DP]
+//   k_sgd_update  (iteration i)  multi-workgroup: sums the partial rows of
+//                 64 columns (world 1) or reads the all-reduced g64,
+//                 SimpleUpdater on them, per-workgroup ||dw||^2, ||w||^2
+//                 into record i.
+//   k_sgd_finish  after the loop: convergence of the last update.
+//
+// MLlib semantics: the update of iteration i is applied, then
+// ||w_i - w_{i-1}|| < tol * max(||w_i||, 1) (from the second update on) ends
+// the loop, i.e. the weights after the converging update are kept.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp) {
-  __shared__ double scratch[16];
-  if (d.state[0] != 0.0) return;
-  const int tid = threadIdx.x;
-  const int64_t hi = kNumNumeric + d.n_unique;
-  const double m = sp.sample ? d.red64[1] : d.state[5];
-  const double loss = d.g64[d.ns];
-  double ds = 0.0, ws = 0.0;
-  if (m > 0.0) {
-    const double alpha = sp.step_size / sqrt(double(sp.iteration));
-    for (int64_t s = tid; s < hi; s += 1024) {
-      const double step = alpha * (d.g64[s] / m);
-      const double wn = d.wc64[s] - step;
-      d.wc64[s] = wn;
-      d.wc32[s] = float(wn);
-      d.g64[s] = 0.0;
-      ds += step * step;
-      ws += wn * wn;
-    }
-  } else {
-    for (int64_t s = tid; s < hi; s += 1024) d.g64[s] = 0.0;
+
+// ---------------------------------------------------------------------------
+// Cross-workgroup reduction of the partial rows (DP: before the all-reduce):
+// 64 columns per workgroup, 16 row strides per column, fixed summation order.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double part_col_sum(const DevSgd& d, int64_t col, int j, int nparts) {
+  double a[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) a[k] = 0.0;
+  const double* src = d.part + col;
+  const int64_t ps = d.pstride;
+  int64_t g = j;
+  // 16 independent loads in flight (a dependent add chain would serialise
+  // one memory latency per partial row)
+  for (; g + 15 * 16 < nparts; g += 16 * 16) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) a[k] += src[(g + 16 * k) * ps];
   }
-  // block reduce (1024 threads = 16 waves)
-  ds = wave_sum(ds);
-  ws = wave_sum(ws);
-  const int w = tid / kWave;
-  if (lane_id() == 0) scratch[w] = ds;
+#pragma unroll
+  for (int k = 0; k < 16; ++k)
+    if (g + 16 * k < nparts) a[k] += src[(g + 16 * k) * ps];
+  double t = 0.0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) t += a[k];
+  return t;
+}
+
+__global__ __launch_bounds__(1024) void k_sgd_reduce(DevSgd d, SgdParams sp) {
+  __shared__ double red[16][65];
+  if (d.state[0] != 0.0) return;
+  const int c = threadIdx.x & 63, j = threadIdx.x >> 6;
+  const int64_t col = int64_t(blockIdx.x) * 64 + c;
+  const int64_t ncols = d.ns + kPartVals - kNumNumeric;
+  red[j][c] = col < ncols ? part_col_sum(d, col, j, d.nparts) : 0.0;
   __syncthreads();
-  double dsum = 0.0;
-  for (int k = 0; k < 16; ++k) dsum += scratch[k];
-  __syncthreads();
-  if (lane_id() == 0) scratch[w] = ws;
-  __syncthreads();
-  double wsum = 0.0;
-  for (int k = 0; k < 16; ++k) wsum += scratch[k];
-  if (tid == 0) {
-    if (m > 0.0) {
-      d.loss_hist[sp.iteration] = loss / m;
-      const double nupd = d.state[2] + 1.0;
-      d.state[2] = nupd;
-      double rest = d.state[4] - d.state[6];
-      if (rest < 0.0) rest = 0.0;
-      const double wnorm = sqrt(wsum + rest);
-      if (nupd >= 2.0 && sqrt(dsum) < sp.tol * (wnorm > 1.0 ? wnorm : 1.0)) {
-        d.state[0] = 1.0;
-        d.state[1] = 1.0;
-      }
-    }
-    d.state[3] = double(sp.iteration);
-    if (sp.iteration >= sp.num_iterations) d.state[0] = 1.0;
-    if (d.host_flags) {               // zero-copy early-stop signal to the host
-      d.host_flags[sp.iteration] = d.state[0];
-      __threadfence_system();
-    }
-    d.g64[d.ns] = 0.0;
-    d.red64[0] = 0.0;
-    d.red64[1] = 0.0;
+  if (j == 0 && col < ncols) {
+    double v = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v += red[k][c];
+    if (col <= d.ns) d.g64[col] = v;                     // slots, then the loss at [ns]
+    else if (col == d.ns + 1) *sgd_red_m(d, sp.iteration) = v;   // sampled row count
+    else d.stats[col - d.ns - 2] += v;                   // batch stats (iteration 1)
   }
 }
 
-void launch_sgd_update(const DevSgd& d, const SgdParams& sp, hipStream_t s) {
-  hipLaunchKernelGGL(k_sgd_update, dim3(1), dim3(1024), 0, s, d, sp);
+void launch_sgd_reduce(const DevSgd& d, const SgdParams& sp, hipStream_t s) {
+  if (d.nparts <= 0) return;
+  const int grid = int((d.ns + kPartVals - kNumNumeric + 63) / 64);
+  hipLaunchKernelGGL(k_sgd_reduce, dim3(grid), dim3(1024), 0, s, d, sp);
+}
+
+// ---------------------------------------------------------------------------
+// SimpleUpdater (fp64 master weights), 64 columns per workgroup tile.
+// nparts > 0: the column gradients are the sums of the partial rows (single
+// GPU); nparts == 0: g64 holds them (all-reduced, or the generic path).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int nparts) {
+  __shared__ double red[16][65];
+  __shared__ double wsc[16][2];
+  __shared__ double m_sh;
+  if (d.state[0] != 0.0) return;
+  const int tid = threadIdx.x, c = tid & 63, j = tid >> 6;
+  const int it = sp.iteration;
+  const int64_t ns = d.ns, hi = kNumNumeric + d.n_unique;
+  const int64_t ncols = ns + kPartVals - kNumNumeric;
+  // m: global kept rows, or the sampled row count of this iteration
+  if (tid < kWave) {
+    double m = d.state[5];
+    if (sp.sample) {
+      m = *sgd_red_m(d, it);
+      if (nparts > 0) {
+        double t = 0.0;
+        for (int g = tid; g < nparts; g += kWave) t += d.part[int64_t(g) * d.pstride + ns + 1];
+        m += wave_sum(t);
+      }
+    }
+    if (tid == 0) m_sh = m;
+  }
+  __syncthreads();
+  const double m = m_sh;
+  const double alpha = sp.step_size / sqrt(double(it));
+  double ds = 0.0, ws = 0.0;
+  for (int64_t tile = blockIdx.x; tile * 64 < ncols; tile += gridDim.x) {
+    const int64_t col = tile * 64 + c;
+    if (nparts > 0) {
+      red[j][c] = col < ncols ? part_col_sum(d, col, j, nparts) : 0.0;
+      __syncthreads();
+    }
+    if (j == 0 && col < ncols) {
+      double g = col <= ns ? d.g64[col] : 0.0;
+      if (nparts > 0) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) g += red[k][c];
+      }
+      if (col < hi) {
+        if (m > 0.0) {
+          const double step = alpha * (g / m);
+          const double wn = d.wc64[col] - step;
+          d.wc64[col] = wn;
+          d.wc32[col] = float(wn);
+          ds += step * step;
+          ws += wn * wn;
+        }
+        d.g64[col] = 0.0;
+      } else if (col == ns) {
+        if (m > 0.0) d.loss_hist[it] = g / m;
+        d.g64[ns] = 0.0;
+      } else if (col >= ns + 2 && nparts > 0) {
+        d.stats[col - ns - 2] += g;     // batch stats (iteration 1, single GPU)
+      }
+    }
+    if (nparts > 0) __syncthreads();
+  }
+  ds = wave_sum(ds);
+  ws = wave_sum(ws);
+  if (lane_id() == 0) {
+    wsc[tid / kWave][0] = ds;
+    wsc[tid / kWave][1] = ws;
+  }
+  __syncthreads();
+  double* rec = sgd_rec(d, it);
+  if (tid < 2) {
+    double t = 0.0;
+    for (int k = 0; k < 16; ++k) t += wsc[k][tid];
+    rec[kRecHead + 2 * blockIdx.x + tid] = t;
+  }
+  if (blockIdx.x == 0 && tid == 0) {
+    const double nupd = (it > 1 ? sgd_rec(d, it - 1)[0] : 0.0) + (m > 0.0 ? 1.0 : 0.0);
+    rec[0] = nupd;
+    rec[1] = m;
+    rec[2] = double(gridDim.x);
+    d.state[2] = nupd;
+    d.state[3] = double(it);
+    *sgd_red_m(d, it + 1) = 0.0;      // the next iteration's sampled count accumulates from 0
+  }
+}
+
+void launch_sgd_update(const DevSgd& d, const SgdParams& sp, int nparts, hipStream_t s) {
+  const int64_t tiles = (d.ns + kPartVals - kNumNumeric + 63) / 64;
+  const int grid = int(std::min<int64_t>(tiles, kMaxUpdGrid));
+  hipLaunchKernelGGL(k_sgd_update, dim3(grid), dim3(1024), 0, s, d, sp, nparts);
+}
+
+// Convergence of the last update (the loop ended without a prologue seeing it).
+__global__ void k_sgd_finish(DevSgd d, SgdParams sp) {
+  if (threadIdx.x >= kWave || d.state[0] != 0.0) return;
+  const int last = int(d.state[3]);
+  const bool conv = last >= 1 && sgd_converged_wave(d, last, sp.tol);
+  if (threadIdx.x == 0) {
+    d.state[0] = 1.0;
+    if (conv) d.state[1] = 1.0;
+  }
+}
+
+void launch_sgd_finish(const DevSgd& d, const SgdParams& sp, hipStream_t s) {
+  hipLaunchKernelGGL(k_sgd_finish, dim3(1), dim3(kWave), 0, s, d, sp);
 }
 
 // ---------------------------------------------------------------------------

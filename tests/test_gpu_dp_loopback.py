@@ -61,7 +61,11 @@ def test_dp_equals_single_engine(hip_module, world, fraction):
         for r in range(world):
             assert res[r][t]["n_kept_global"] == r1["n_kept"]
             assert res[r][t]["iterations"] == r1["iterations"]
-            np.testing.assert_allclose(res[r][t]["stats"], r1["stats"], rtol=1e-9)
+            # n, sum y, sum y^2 exactly; the rounded-prediction moments may
+            # differ by a rare half-way rounding flip (fp32 forward, weights
+            # equal to ~1e-15 but summed in a different order)
+            np.testing.assert_allclose(res[r][t]["stats"][:3], r1["stats"][:3], rtol=1e-12)
+            np.testing.assert_allclose(res[r][t]["stats"][3:], r1["stats"][3:], rtol=1e-5)
             np.testing.assert_allclose(res[r][t]["loss_history"], r1["loss_history"], rtol=1e-6)
     # after the same 3 batches the replicas equal the single-engine model
     w1 = single.get_weights()
