@@ -99,6 +99,7 @@ void LREngine::alloc_prepared() {
   prep_.blk = dmalloc<int64_t>(size_t(R / kBlock + 2));
   prep_.hist = dmalloc<int64_t>(kLenBuckets + 1);
   prep_.clen8 = dmalloc<int32_t>(size_t(C) + 1);
+  prep_.cfast = dmalloc<uint8_t>(size_t(C) + 1);
   prep_.clen8d = dmalloc<int32_t>(size_t(C) + 1);
   prep_.cnt = dmalloc<uint16_t>(size_t(E));
   prep_.cslot = dmalloc<uint16_t>(size_t(E));
@@ -157,7 +158,7 @@ LREngine::~LREngine() {
   (void)hipDeviceSynchronize();
   raw_.release();
   for (auto& e : ev_) (void)hipEventDestroy(e);
-  void* bufs[] = {prep_.kept, prep_.nnz, prep_.sorted, prep_.blk, prep_.hist, prep_.clen8,
+  void* bufs[] = {prep_.kept, prep_.nnz, prep_.sorted, prep_.blk, prep_.hist, prep_.clen8, prep_.cfast,
                   prep_.clen8d, prep_.cnt, prep_.cslot, prep_.hot_dense, prep_.clen8c,
                   prep_.hot_slot, prep_.hot_of, prep_.slot_hist,
                   prep_.cbase, prep_.idx, prep_.slot, prep_.y, prep_.num, prep_.perm,

@@ -63,8 +63,20 @@ void scan_excl_launch(const int64_t* in, int64_t* out, int64_t n, int64_t* total
   scan_excl(in, out, n, total, s);
 }
 
-__device__ __forceinline__ int len_key(int32_t n32) {
-  return kLenBuckets - 1 - (n32 < kLenBuckets - 1 ? n32 : kLenBuckets - 1);
+// nnz[k] carries the row's bigram count in bits 0..29 and the wide (UTF-16
+// wire) flag in bit 30.  Sort key: narrow rows first, then wide rows, each
+// by descending length, so a chunk mixes narrow and wide rows at most once
+// (the narrow fast featurizer takes whole chunks).
+constexpr int32_t kNnzWide = 1 << 30;
+constexpr int32_t kNnzMask = kNnzWide - 1;
+constexpr int kHalfBuckets = kLenBuckets / 2;
+// Narrow fast featurizer: bigrams per lane (row quarter) it can hold in VGPRs
+constexpr int kFastMaxQ = 72;
+
+__device__ __forceinline__ int len_key(int32_t v) {
+  const int32_t n32 = v & kNnzMask;
+  const int k = kHalfBuckets - 1 - (n32 < kHalfBuckets - 1 ? n32 : kHalfBuckets - 1);
+  return (v & kNnzWide) ? kHalfBuckets + k : k;
 }
 
 // ---------------------------------------------------------------------------
@@ -107,9 +119,9 @@ __global__ __launch_bounds__(kBlock) void k_filter_write(DevRawBatch b, Featuriz
   if (pred) {
     const int64_t k = blk_off[blockIdx.x] + woff + wpre;
     kept[k] = r;
-    const int64_t len = row_text(b, r).len;
-    const int64_t nz = len >= 2 ? len - 1 : len;
-    const int32_t n32 = int32_t(nz > 0x7fffffff ? 0x7fffffff : nz);
+    const RowText rt = row_text(b, r);
+    const int64_t nz = rt.len >= 2 ? rt.len - 1 : rt.len;
+    const int32_t n32 = int32_t(nz > kNnzMask ? kNnzMask : nz) | (rt.wide ? kNnzWide : 0);
     nnz[k] = n32;
     atomicAdd(&lhist[len_key(n32)], 1);
   }
@@ -175,7 +187,8 @@ void launch_filter_only(const DevRawBatch& b, const DevPrepared& p, const Featur
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_chunk_len(const int32_t* sorted, const int32_t* nnz,
                                                       const int64_t* counters, int64_t cmax,
-                                                      int64_t* clen_scratch, int32_t* clen8) {
+                                                      int64_t* clen_scratch, int32_t* clen8,
+                                                      uint8_t* cfast) {
   const int64_t n_kept = counters[0];
   const int lane = lane_id();
   const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
@@ -184,17 +197,20 @@ __global__ __launch_bounds__(kBlock) void k_chunk_len(const int32_t* sorted, con
   for (int64_t c4 = wave; c4 * 4 < cmax; c4 += nwaves) {
     const int64_t c = c4 * 4 + lane / kRowsPerChunk;
     const int64_t p = c * kRowsPerChunk + (lane % kRowsPerChunk);
-    int32_t v = (c < cmax && p < n_kept) ? nnz[sorted[p]] : 0;
+    const int32_t raw = (c < cmax && p < n_kept) ? nnz[sorted[p]] : 0;
+    int32_t v = raw & kNnzMask, wide = raw & kNnzWide;
 #pragma unroll
-    for (int off = 8; off > 0; off >>= 1) {  // max within each 16-lane segment
+    for (int off = 8; off > 0; off >>= 1) {  // max / any within each 16-lane segment
       const int32_t o = __shfl_xor(v, off, kWave);
       v = o > v ? o : v;
+      wide |= __shfl_xor(wide, off, kWave);
     }
     if ((lane % kRowsPerChunk) == 0 && c < cmax) {
       const int32_t per_lane = (v + kLanesPerRow - 1) / kLanesPerRow;
       const int32_t g = (per_lane + kGroup - 1) / kGroup;
       clen8[c] = g;
       clen_scratch[c] = g;
+      cfast[c] = (!wide && per_lane <= kFastMaxQ) ? 1 : 0;
     }
   }
 }
@@ -209,7 +225,7 @@ void launch_chunk_layout(const DevRawBatch& b, const DevPrepared& p, hipStream_t
   int grid = ceil_div((cmax + 3) / 4, kBlock / kWave);
   if (grid > 4096) grid = 4096;
   hipLaunchKernelGGL(k_chunk_len, dim3(grid), dim3(kBlock), 0, s, p.sorted, p.nnz, p.counters,
-                     cmax, p.cbase, p.clen8);
+                     cmax, p.cbase, p.clen8, p.cfast);
   scan_excl(p.cbase, p.cbase, cmax, &p.counters[2], s);
 }
 
@@ -285,6 +301,52 @@ constexpr int kFlagWords = kFlagLds / 32;
 
 constexpr int kFeatWaves = kBlock / kWave;
 
+// K2 (label + 4 numeric features, MllibHelper.scala:58-71) and the kept
+// index of sorted position pos.
+__device__ __forceinline__ void row_scalars(const DevRawBatch& b, const DevPrepared& p,
+                                            const FeaturizeParams& fp, int64_t pos, bool valid,
+                                            int64_t row, int32_t kidx) {
+  const int64_t cap = p.cap_rows16;
+  if (valid) {
+    const int64_t* sc = b.scalars;
+    p.y[pos] = float(sc[row]);
+    const double fol = double(sc[1 * b.n + row]), fav = double(sc[2 * b.n + row]);
+    const double fri = double(sc[3 * b.n + row]);
+    const double age = double(fp.now_ms - sc[4 * b.n + row]);
+    p.num[0 * cap + pos] = float(fol * 1e-12);
+    p.num[1 * cap + pos] = float(fav * 1e-12);
+    p.num[2 * cap + pos] = float(fri * 1e-12);
+    p.num[3 * cap + pos] = float(age * 1e-14);
+  } else {
+    p.y[pos] = 0.f;
+    for (int k = 0; k < 4; ++k) p.num[k * cap + pos] = 0.f;
+  }
+  p.perm[pos] = kidx;
+}
+
+// Flag an active feature id (LDS bitmap below lds_lim, byte flags above).
+__device__ __forceinline__ void flag_id(uint32_t* fbits, const DevPrepared& p, int64_t idx,
+                                        int64_t lds_lim) {
+  if (idx < lds_lim) {
+    // hot ids are flagged early: a (broadcast) read skips the atomic
+    const uint32_t bit = 1u << (idx & 31);
+    if (!(fbits[idx >> 5] & bit)) atomicOr(&fbits[idx >> 5], bit);
+  } else if (idx < p.flag_len) {
+    p.flags[idx] = 1;
+  }
+}
+
+__device__ __forceinline__ void flush_flag_bits(const uint32_t* fbits, const DevPrepared& p) {
+  for (int i = threadIdx.x; i < kFlagWords; i += kBlock) {
+    uint32_t bits = fbits[i];
+    while (bits) {
+      const int bit = __builtin_ctz(bits);
+      bits &= bits - 1u;
+      p.flags[int64_t(i) * 32 + bit] = 1;
+    }
+  }
+}
+
 // One wave per 16-row chunk.  Per chunk the wave first resolves the 16 rows'
 // metadata (lanes 0..15), then stages the rows' bytes into LDS with up to 48
 // independent aligned dword loads in flight -- one memory latency per chunk
@@ -312,6 +374,7 @@ __global__ __launch_bounds__(kBlock) void k_featurize(DevRawBatch b, DevPrepared
   const int64_t cap_groups = p.cap_entries / kChunkStride;
   const int64_t nch = (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;
   for (int64_t c = wave; c < nch && c < cmax; c += nwaves) {
+    if (p.cfast[c]) continue;            // k_featurize_narrow's chunk
     const int32_t L8 = p.clen8[c];
     const int64_t g0 = p.cbase[c];
     if (g0 + L8 > cap_groups) {
@@ -352,13 +415,7 @@ __global__ __launch_bounds__(kBlock) void k_featurize(DevRawBatch b, DevPrepared
           }
           const int64_t idx = term_mod(h, F, fm, f32);
           v[k] = int32_t(idx);
-          if (idx < lds_lim) {
-            // hot ids are flagged early: a (broadcast) read skips the atomic
-            const uint32_t bit = 1u << (idx & 31);
-            if (!(fbits[idx >> 5] & bit)) atomicOr(&fbits[idx >> 5], bit);
-          } else if (idx < p.flag_len) {
-            p.flags[idx] = 1;
-          }
+          flag_id(fbits, p, idx, lds_lim);
         }
       }
       int4* dst = reinterpret_cast<int4*>(out + (jj0 >> 3) * kChunkStride);
@@ -366,34 +423,140 @@ __global__ __launch_bounds__(kBlock) void k_featurize(DevRawBatch b, DevPrepared
       dst[1] = make_int4(v[4], v[5], v[6], v[7]);
     }
     __builtin_amdgcn_wave_barrier();   // LDS reads of this chunk precede the next staging
-    if (t == 0) {
-      const int64_t cap = p.cap_rows16;
-      if (valid) {
-        const int64_t* sc = b.scalars;
-        p.y[pos] = float(sc[row]);
-        const double fol = double(sc[1 * b.n + row]), fav = double(sc[2 * b.n + row]);
-        const double fri = double(sc[3 * b.n + row]);
-        const double age = double(fp.now_ms - sc[4 * b.n + row]);
-        p.num[0 * cap + pos] = float(fol * 1e-12);
-        p.num[1 * cap + pos] = float(fav * 1e-12);
-        p.num[2 * cap + pos] = float(fri * 1e-12);
-        p.num[3 * cap + pos] = float(age * 1e-14);
-      } else {
-        p.y[pos] = 0.f;
-        for (int k = 0; k < 4; ++k) p.num[k * cap + pos] = 0.f;
-      }
-      p.perm[pos] = kidx;
-    }
+    if (t == 0) row_scalars(b, p, fp, pos, valid, row, kidx);
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < kFlagWords; i += kBlock) {
-    uint32_t bits = fbits[i];
-    while (bits) {
-      const int bit = __builtin_ctz(bits);
-      bits &= bits - 1u;
-      p.flags[int64_t(i) * 32 + bit] = 1;
+  flush_flag_bits(fbits, p);
+}
+
+// ---------------------------------------------------------------------------
+// Narrow fast path (chunks whose 16 rows are all Latin-1 on the wire and
+// hold <= kFastMaxQ bigrams per lane): each of a row's 4 lanes takes a
+// CONTIGUOUS quarter of the row's bigrams (the SGD kernels only need every
+// entry of a row in one of its 4 lanes), so a lane's text is one byte range:
+// at most 5 dwordx4 loads, realigned with v_alignbyte, lower-cased four
+// bytes per SWAR step and hashed straight from VGPRs.  No LDS staging (LDS
+// holds only the flag bitmap), so occupancy is register-bound, and every
+// chunk costs two memory round trips (row metadata, then text).
+// ---------------------------------------------------------------------------
+constexpr int kFastDw = 20;     // dwords loaded per lane (80 B >= 3 + kFastMaxQ + 1)
+constexpr int kFastAl = 19;     // realigned dwords (76 chars >= kFastMaxQ + 1)
+static_assert(kFastAl * 4 >= kFastMaxQ + 1, "realigned window too small");
+
+// Character.toLowerCase on four Latin-1 bytes: A-Z and U+00C0..U+00DE except
+// U+00D7 gain 0x20.  Per byte on its low 7 bits (no carries between bytes).
+__device__ __forceinline__ uint32_t lower4_latin1(uint32_t x) {
+  const uint32_t hb = x & 0x80808080u;
+  const uint32_t x7 = x & 0x7F7F7F7Fu;
+  const uint32_t ge41 = x7 + 0x3F3F3F3Fu;              // bit 7: x7 >= 0x41
+  const uint32_t gt5a = x7 + 0x25252525u;              // bit 7: x7 >= 0x5B
+  const uint32_t ge40 = x7 + 0x40404040u;              // bit 7: x7 >= 0x40
+  const uint32_t gt5e = x7 + 0x21212121u;              // bit 7: x7 >= 0x5F
+  const uint32_t x57 = (x7 ^ 0x57575757u) + 0x7F7F7F7Fu;  // bit 7: x7 != 0x57
+  const uint32_t lo = ~hb & ge41 & ~gt5a;
+  const uint32_t hi = hb & ge40 & ~gt5e & x57;
+  return x + (((lo | hi) & 0x80808080u) >> 2);
+}
+
+__device__ __forceinline__ uint32_t byte_of(const uint32_t (&a)[kFastAl], int k) {
+  return (a[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+}
+
+__global__ __launch_bounds__(kBlock) void k_featurize_narrow(DevRawBatch b, DevPrepared p,
+                                                             FeaturizeParams fp, int64_t cmax) {
+  __shared__ uint32_t fbits[kFlagWords];
+  for (int i = threadIdx.x; i < kFlagWords; i += kBlock) fbits[i] = 0u;
+  __syncthreads();
+  const int64_t n_kept = p.counters[0];
+  const int lane = lane_id();
+  const int r = lane / kLanesPerRow, t = lane % kLanesPerRow;
+  const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
+  const int64_t nwaves = int64_t(gridDim.x) * kBlock / kWave;
+  const int64_t F = fp.num_text_features;
+  const bool f32 = F <= 0xffffffffLL;
+  const FastMod32 fm(f32 ? uint32_t(F) : 1u);
+  // Java hashes of Latin-1 bigrams are < 31*255+256 = 8161: no reduction
+  const bool direct = fp.hash_kind == 0 && F > 8160;
+  const int64_t lds_lim = p.flag_len < kFlagLds ? p.flag_len : kFlagLds;
+  const int64_t cap_groups = p.cap_entries / kChunkStride;
+  const int64_t nch = (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;
+  for (int64_t c = wave; c < nch && c < cmax; c += nwaves) {
+    if (!p.cfast[c]) continue;
+    const int32_t L8 = p.clen8[c];
+    const int64_t g0 = p.cbase[c];
+    if (g0 + L8 > cap_groups) {
+      if (lane == 0) p.counters[3] = 1;  // capacity overflow -> host raises
+      continue;
     }
+    // row metadata: lane l resolves row l & 15
+    const int64_t mpos = c * kRowsPerChunk + (lane & 15);
+    const bool mvalid = mpos < n_kept;
+    const int32_t mkidx = mvalid ? p.sorted[mpos] : -1;
+    const int64_t mrow = mvalid ? p.kept[mkidx] : 0;
+    const int64_t mo = mvalid ? b.offsets[mrow] : 0;
+    const int64_t mlen = mvalid ? b.offsets[mrow + 1] - mo : 0;
+    const int64_t pos = c * kRowsPerChunk + r;
+    const bool valid = pos < n_kept;
+    const int32_t kidx = __shfl(mkidx, r, kWave);
+    const int64_t row = __shfl(mrow, r, kWave);
+    const int64_t o = __shfl(mo, r, kWave);
+    const int32_t len = valid ? int32_t(__shfl(mlen, r, kWave)) : 0;
+    const int32_t nz = len >= 2 ? len - 1 : len;
+    const int32_t q = (nz + kLanesPerRow - 1) / kLanesPerRow;
+    const int32_t e0 = t * q;
+    const int32_t my = nz - e0 < 0 ? 0 : (nz - e0 < q ? nz - e0 : q);
+    // text bytes [o + e0, o + e0 + my + 1): dword-aligned window
+    const int64_t start = o + e0;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(b.text + (start & ~int64_t(3)));
+    const uint32_t sh = uint32_t(start & 3);
+    const int32_t need = int32_t(sh) + my + 1;          // bytes of the window used
+    uint32_t d[kFastDw];
+#pragma unroll
+    for (int i = 0; i < kFastDw; i += 4) {
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (my > 0 && 4 * i < need) __builtin_memcpy(&v, src + i, 16);
+      d[i] = v.x; d[i + 1] = v.y; d[i + 2] = v.z; d[i + 3] = v.w;
+    }
+    // wave-uniform bound on the characters any lane uses
+    int32_t mw = my;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const int32_t x = __shfl_xor(mw, off, kWave);
+      mw = x > mw ? x : mw;
+    }
+    mw = __builtin_amdgcn_readfirstlane(mw);
+    uint32_t a[kFastAl];
+#pragma unroll
+    for (int i = 0; i < kFastAl; ++i)
+      a[i] = (4 * i <= mw) ? lower4_latin1(__builtin_amdgcn_alignbyte(d[i + 1], d[i], sh)) : 0u;
+    int32_t* out = p.idx + g0 * kChunkStride + lane * kGroup;
+#pragma unroll
+    for (int g = 0; g < kFastMaxQ / kGroup; ++g) {
+      if (g >= L8) break;                               // wave-uniform
+      int32_t v[kGroup];
+#pragma unroll
+      for (int k = 0; k < kGroup; ++k) {
+        const int e = g * kGroup + k;
+        const uint32_t u0 = byte_of(a, e), u1 = byte_of(a, e + 1);
+        int64_t idx;
+        if (direct) {
+          idx = len >= 2 ? int64_t(31u * u0 + u1) : int64_t(u0);
+        } else {
+          const int64_t h = fp.hash_kind == 0 ? (len >= 2 ? int64_t(31u * u0 + u1) : int64_t(u0))
+                                              : int64_t(murmur_term(u0, u1, len >= 2 ? 2 : 1));
+          idx = term_mod(h, F, fm, f32);
+        }
+        v[k] = e < my ? int32_t(idx) : -1;
+        if (e < my) flag_id(fbits, p, idx, lds_lim);
+      }
+      int4* dst = reinterpret_cast<int4*>(out + g * kChunkStride);
+      dst[0] = make_int4(v[0], v[1], v[2], v[3]);
+      dst[1] = make_int4(v[4], v[5], v[6], v[7]);
+    }
+    if (t == 0) row_scalars(b, p, fp, pos, valid, row, kidx);
   }
+  __syncthreads();
+  flush_flag_bits(fbits, p);
 }
 
 void launch_featurize(const DevRawBatch& b, const DevPrepared& p, const FeaturizeParams& fp,
@@ -404,6 +567,7 @@ void launch_featurize(const DevRawBatch& b, const DevPrepared& p, const Featuriz
   // flushed rarely (XCD-agnostic: chunk order is length-sorted anyway)
   int grid = ceil_div(cmax, kBlock / kWave);
   if (grid > 2048) grid = 2048;
+  hipLaunchKernelGGL(k_featurize_narrow, dim3(grid), dim3(kBlock), 0, s, b, p, fp, cmax);
   hipLaunchKernelGGL(k_featurize, dim3(grid), dim3(kBlock), 0, s, b, p, fp, lpage, lblocks, cmax);
 }
 

@@ -60,6 +60,7 @@ struct DevPrepared {
   int64_t* hist;            // [kLenBuckets+1]
   // chunk layout
   int32_t* clen8;           // [C]   groups of 8 entries per lane in chunk c
+  uint8_t* cfast;           // [C]   1: all rows narrow and short (k_featurize_narrow)
   int64_t* cbase;           // [C+1] first group of chunk c (entries = groups*512)
   int32_t* idx;             // [E]   hashed feature index per entry (-1 = pad)
   void* slot;               // [E]   compact slot per entry (u16 or u32)

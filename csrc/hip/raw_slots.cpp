@@ -25,7 +25,7 @@ void RawSlots::init(int64_t max_rows, int64_t max_bytes) {
   max_rows_ = max_rows;
   max_bytes_ = max_bytes;
   for (auto& s : slots_) {
-    s.text = slot_alloc<uint8_t>(size_t(max_bytes) + 16);
+    s.text = slot_alloc<uint8_t>(size_t(max_bytes) + 128);   // slack: featurize over-reads <= 80 B
     s.offsets = slot_alloc<int64_t>(size_t(max_rows) + 1);
     s.flags = slot_alloc<uint8_t>(size_t(max_rows));
     s.scalars = slot_alloc<int64_t>(5 * size_t(max_rows));
