@@ -10,7 +10,7 @@
 
 namespace twtml {
 
-void launch_batch_init(double* state, double m_global, hipStream_t s);
+void launch_batch_init(const DevSgd& d, double m_global, int n_loss, hipStream_t s);
 
 HostBatch::HostBatch(int64_t rows, int64_t text_bytes) : max_rows(rows), max_bytes(text_bytes) {
   if (rows < 0 || text_bytes < 0) throw std::invalid_argument("HostBatch: negative capacity");
@@ -108,6 +108,7 @@ void LREngine::alloc_prepared() {
   prep_.hot_slot = dmalloc<int32_t>(kHot);
   prep_.hot_of = dmalloc<uint8_t>(kMaxHybridSlots);
   prep_.slot_hist = dmalloc<uint32_t>(kMaxHybridSlots);
+  prep_.code = dmalloc<uint16_t>(8192);
   prep_.cbase = dmalloc<int64_t>(size_t(C) + 1);
   prep_.idx = dmalloc<int32_t>(size_t(E));
   prep_.slot = dmalloc<uint32_t>(size_t(E));
@@ -125,6 +126,39 @@ void LREngine::alloc_prepared() {
   prep_.slot_of = dmalloc<int32_t>(size_t(fl));
   prep_.ublk = dmalloc<int64_t>(size_t(fl / 4096) + 2);
   prep_.counters = dmalloc<int64_t>(8);
+}
+
+// Opt-in (TWTML_PERSIST=1): measured on MI355X the two grid barriers plus
+// the uncached-memory round trips per iteration (~18 us) cost as much as the
+// per-iteration kernel launches they replace (profiles/README.md), and
+// rocprofv3 kernel tracing does not survive the cooperative launch.
+bool LREngine::persist_enabled() {
+  const char* e = std::getenv("TWTML_PERSIST");
+  return e && e[0] == '1';
+}
+
+void LREngine::ensure_coh(int grid, int64_t ns) {
+  const int64_t need_part = int64_t(grid) * sgd_part_stride(ns);
+  if (coh_.bar && need_part <= coh_part_cap_ && ns <= coh_ns_cap_ && grid <= coh_grid_cap_) return;
+  if (coh_.bar) {
+    TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
+    (void)hipFree(coh_.part);
+    (void)hipFree(coh_.w32);
+    (void)hipFree(coh_.norms);
+    (void)hipFree(coh_.bar);
+  }
+  coh_part_cap_ = std::max<int64_t>(need_part, coh_part_cap_ * 2);
+  coh_ns_cap_ = std::max<int64_t>(ns, coh_ns_cap_ * 2);
+  coh_grid_cap_ = std::max(grid, coh_grid_cap_);
+  auto uc = [](size_t bytes) {
+    void* ptr = nullptr;
+    TWTML_HIP_CHECK(hipExtMallocWithFlags(&ptr, std::max<size_t>(bytes, 256), hipDeviceMallocUncached));
+    return ptr;
+  };
+  coh_.part = static_cast<double*>(uc(sizeof(double) * size_t(coh_part_cap_)));
+  coh_.w32 = static_cast<float*>(uc(sizeof(float) * size_t(coh_ns_cap_)));
+  coh_.norms = static_cast<double*>(uc(sizeof(double) * 4 * size_t(coh_grid_cap_)));
+  coh_.bar = static_cast<GridBar*>(uc(sizeof(GridBar)));
 }
 
 void LREngine::ensure_part(int64_t n) {
@@ -160,11 +194,11 @@ LREngine::~LREngine() {
   for (auto& e : ev_) (void)hipEventDestroy(e);
   void* bufs[] = {prep_.kept, prep_.nnz, prep_.sorted, prep_.blk, prep_.hist, prep_.clen8, prep_.cfast,
                   prep_.clen8d, prep_.cnt, prep_.cslot, prep_.hot_dense, prep_.clen8c,
-                  prep_.hot_slot, prep_.hot_of, prep_.slot_hist,
+                  prep_.hot_slot, prep_.hot_of, prep_.slot_hist, prep_.code,
                   prep_.cbase, prep_.idx, prep_.slot, prep_.y, prep_.num, prep_.perm,
                   prep_.flags, prep_.uniq, prep_.slot_of, prep_.ublk, prep_.counters,
                   sgd_.w64, sgd_.wc64, sgd_.wc32, sgd_.g64, sgd_.red64, sgd_.stats, sgd_.state,
-                  sgd_.loss_hist, sgd_.pred_out, sgd_.part, sgd_.itrec, lower_page_, lower_blocks_, n_global_};
+                  sgd_.loss_hist, sgd_.pred_out, sgd_.part, sgd_.itrec, coh_.part, coh_.w32, coh_.norms, coh_.bar, gd_tdbg_, lower_page_, lower_blocks_, n_global_};
   for (void* b : bufs) if (b) (void)hipFree(b);
   if (host_counters_) (void)hipHostFree(host_counters_);
   if (host_out_) (void)hipHostFree(host_out_);
@@ -191,7 +225,7 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
 
   FeaturizeParams fp{cfg_.num_text_features, cfg_.hash_kind, cfg_.require_retweet,
                      cfg_.range_filter, cfg_.begin, cfg_.end, now_ms};
-  TWTML_HIP_CHECK(hipMemsetAsync(prep_.counters, 0, 8 * sizeof(int64_t), s));
+  launch_prep_init(prep_, n_global_, world + 2, s);
   launch_filter_sort(b, prep_, fp, s);
   launch_chunk_layout(b, prep_, s);
   launch_featurize(b, prep_, fp, lower_page_, lower_blocks_, s);
@@ -199,7 +233,6 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   if (world > 1) comm_->allreduce(prep_.flags, size_t(prep_.flag_len), ncclUint8, ncclMax, s);
   launch_compact_active(prep_, s);
   // global kept count (and per-rank counts for sampling offsets)
-  TWTML_HIP_CHECK(hipMemsetAsync(n_global_, 0, sizeof(int64_t) * size_t(world + 2), s));
   TWTML_HIP_CHECK(hipMemcpyAsync(n_global_ + 1 + rank, prep_.counters, sizeof(int64_t),
                                  hipMemcpyDeviceToDevice, s));
   if (world > 1) comm_->allreduce(n_global_ + 1, size_t(world), ncclInt64, ncclSum, s);
@@ -240,12 +273,7 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   else launch_remap(prep_, res.entries, nU, u16, s);
   prep_.dedup = dedup ? 1 : 0;
   if (prep_.dedup) launch_dedup(prep_, ns, kNumNumeric + nU, res.n_kept, s);
-  TWTML_HIP_CHECK(hipMemsetAsync(sgd_.state, 0, 8 * sizeof(double), s));
-  TWTML_HIP_CHECK(hipMemsetAsync(sgd_.stats, 0, 8 * sizeof(double), s));
-  TWTML_HIP_CHECK(hipMemsetAsync(sgd_.red64, 0, 4 * sizeof(double), s));
-  TWTML_HIP_CHECK(hipMemsetAsync(sgd_.g64 + ns, 0, sizeof(double), s));
-  TWTML_HIP_CHECK(hipMemsetAsync(sgd_.loss_hist, 0, sizeof(double) * size_t(cfg_.num_iterations + 2), s));
-  launch_batch_init(sgd_.state, double(n_glob), s);  // state[5] = m (global kept rows)
+  launch_batch_init(sgd_, double(n_glob), cfg_.num_iterations + 2, s);  // state[5] = m (global kept rows)
   launch_norm2(sgd_.w64, num_weights(), &sgd_.state[4], s);
   launch_gather_w(sgd_, prep_, s);
   TWTML_HIP_CHECK(hipEventRecord(ev_[1], s));
@@ -285,7 +313,37 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
     std::fill(host_flags_, host_flags_ + iters + 2, 0.0);
     // single GPU with partial rows: the update kernel reduces them itself
     const bool fused = world == 1 && sgd_.nparts > 0;
-    for (int i = 1; i <= iters; ++i) {
+    // single GPU, hybrid layout: iterations 2..N in one persistent kernel
+    const int pgrid = (world == 1 && iters >= 2 && persist_enabled())
+                          ? sgd_persistent_grid(sgd_, prep_, u16, sp.sample != 0, num_cu_) : 0;
+    if (pgrid > 0) {
+      ensure_coh(pgrid, ns);
+      sp.iteration = 1;
+      launch_sgd_iter(sgd_, prep_, sp, host_counters_[2], u16, grid, s);
+      launch_sgd_update(sgd_, sp, sgd_.nparts, s);
+      TWTML_HIP_CHECK(hipMemsetAsync(coh_.bar, 0, sizeof(GridBar), s));
+      const bool timing = std::getenv("TWTML_GD_TIMING") != nullptr;
+      if (timing && !gd_tdbg_) gd_tdbg_ = dmalloc<uint64_t>(size_t(iters + 2) * 8);
+      coh_.tdbg = timing ? gd_tdbg_ : nullptr;
+      if (timing) TWTML_HIP_CHECK(hipMemsetAsync(gd_tdbg_, 0, sizeof(uint64_t) * size_t(iters + 2) * 8, s));
+      launch_sgd_persistent(sgd_, prep_, sp, coh_, 2, pgrid, s);
+      if (timing) {   // phase times of workgroup 0 (100 MHz clock): init pass barA update barB conv
+        std::vector<uint64_t> tb(size_t(iters + 2) * 8);
+        TWTML_HIP_CHECK(hipMemcpyAsync(tb.data(), gd_tdbg_, tb.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        TWTML_HIP_CHECK(hipStreamSynchronize(s));
+        double acc[6] = {0, 0, 0, 0, 0, 0};
+        int n = 0;
+        for (int i = 2; i <= iters; ++i) {
+          const uint64_t* t = tb.data() + size_t(i) * 8;
+          if (t[6] == 0) break;
+          for (int k = 0; k < 6; ++k) acc[k] += double(t[k + 1] - t[k]) * 0.01;
+          ++n;
+        }
+        if (n) std::fprintf(stderr, "gd timing (us/iter, %d iters): init %.2f pass %.2f barA %.2f update %.2f barB %.2f conv %.2f\n",
+                            n, acc[0] / n, acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n);
+      }
+    }
+    for (int i = 1; pgrid == 0 && i <= iters; ++i) {
       if (i > depth) {
         const int j = i - depth;                       // verdict after update j
         TWTML_HIP_CHECK(hipEventSynchronize(iter_events_[size_t(j)]));
@@ -324,7 +382,8 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   for (int k = 0; k < 6; ++k) res.stats[k] = host_out_[k];
   const double* st = host_out_ + 8;
   res.converged = st[1] != 0.0;
-  res.overflow = st[7] != 0.0;
+  res.overflow = st[7] == 1.0;
+  if (st[7] == 2.0) throw std::runtime_error("persistent GD kernel: grid barrier timed out");
   res.iterations = int32_t(st[3]);
   for (int i = 1; i <= res.iterations; ++i) res.loss_history.push_back(host_out_[16 + i]);
   TWTML_HIP_CHECK(hipEventElapsedTime(&res.prep_ms, ev_[0], ev_[1]));

@@ -104,6 +104,8 @@ class LREngine {
   void alloc_prepared();
   void ensure_compact(int64_t ns);
   void ensure_part(int64_t n);
+  void ensure_coh(int grid, int64_t ns);
+  static bool persist_enabled();
 
   int device_;
   LRConfig cfg_;
@@ -114,6 +116,10 @@ class LREngine {
   DevSgd sgd_{};
   int64_t ns_cap_ = 0;
   int64_t part_cap_ = 0;
+  DevCoh coh_{};
+  int64_t coh_part_cap_ = 0, coh_ns_cap_ = 0;
+  int coh_grid_cap_ = 0;
+  uint64_t* gd_tdbg_ = nullptr;
   uint8_t* lower_page_ = nullptr;
   uint16_t* lower_blocks_ = nullptr;
   int64_t* host_counters_ = nullptr;  // pinned [8]

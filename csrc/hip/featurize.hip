@@ -17,6 +17,8 @@
 //   sorted position p = 16c + r.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "../common/unicode_tables.h"
 #include "common.h"
 #include "kernels.h"
@@ -25,17 +27,39 @@
 namespace twtml {
 
 // ---------------------------------------------------------------------------
-// Generic single-workgroup exclusive scan (int64), in-place safe.
+// Generic single-workgroup exclusive scan (int64), in-place safe.  A tile of
+// 1024 x kScanPer elements is loaded coalesced into LDS (thread t takes
+// elements t, t+1024, ...: one memory latency per tile), then each thread
+// scans kScanPer consecutive LDS elements, the thread totals are scanned
+// with wave shuffles + one LDS pass, and the tile is stored coalesced.
+// (A thread reading its consecutive elements straight from global memory
+// makes every load instruction touch 64 cache lines: 16 us per tile.)
 // ---------------------------------------------------------------------------
+constexpr int kScanPer = 8;
+constexpr int kScanTile = 1024 * kScanPer;
+
 __global__ __launch_bounds__(1024) void k_scan_excl(const int64_t* in, int64_t* out, int64_t n,
                                                     int64_t* total) {
+  __shared__ int64_t tile_v[kScanTile + kScanTile / 32];   // +1 word per 32: fewer bank conflicts
   __shared__ int64_t wsum[16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  auto at = [](int i) { return i + (i >> 5); };
   int64_t carry = 0;
-  for (int64_t base = 0; base < n; base += 1024) {
-    const int64_t i = base + tid;
-    const int64_t v = i < n ? in[i] : 0;
-    int64_t x = v;
+  for (int64_t base = 0; base < n; base += kScanTile) {
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+      const int64_t i = base + k * 1024 + tid;
+      tile_v[at(k * 1024 + tid)] = i < n ? in[i] : 0;
+    }
+    __syncthreads();
+    int64_t v[kScanPer];
+    int64_t tsum = 0;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+      v[k] = tile_v[at(tid * kScanPer + k)];
+      tsum += v[k];
+    }
+    int64_t x = tsum;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
       const int64_t y = __shfl_up(x, off, 64);
@@ -43,13 +67,26 @@ __global__ __launch_bounds__(1024) void k_scan_excl(const int64_t* in, int64_t* 
     }
     if (lane == 63) wsum[w] = x;
     __syncthreads();
-    int64_t woff = 0, tile = 0;
+    int64_t woff = 0, tot = 0;
+#pragma unroll
     for (int k = 0; k < 16; ++k) {
-      if (k < w) woff += wsum[k];
-      tile += wsum[k];
+      const int64_t ws = wsum[k];
+      woff += k < w ? ws : 0;
+      tot += ws;
     }
-    if (i < n) out[i] = carry + woff + x - v;
-    carry += tile;
+    int64_t run = carry + woff + x - tsum;   // exclusive prefix of this thread's first element
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+      tile_v[at(tid * kScanPer + k)] = run;
+      run += v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+      const int64_t i = base + k * 1024 + tid;
+      if (i < n) out[i] = tile_v[at(k * 1024 + tid)];
+    }
+    carry += tot;
     __syncthreads();
   }
   if (tid == 0 && total) *total = carry;
@@ -94,91 +131,143 @@ __device__ __forceinline__ bool keep_row(const DevRawBatch& b, int64_t r, const 
   return true;
 }
 
-__global__ __launch_bounds__(kBlock) void k_filter_count(DevRawBatch b, FeaturizeParams fp,
-                                                         int64_t* blk) {
-  const int64_t r = int64_t(blockIdx.x) * kBlock + threadIdx.x;
-  const int c = __syncthreads_count(keep_row(b, r, fp));
-  if (threadIdx.x == 0) blk[blockIdx.x] = c;
+// Rows are processed in segments of kSegRows (1024 threads x 4 consecutive
+// rows): ~250 workgroups per 1M-row batch, so the global histogram / cursor
+// atomics are ~250 per bucket instead of ~4000 (same-address atomics
+// serialise at the memory-side atomic units).
+constexpr int kSegThreads = 1024;
+constexpr int kSegPer = 4;
+constexpr int kSegRows = kSegThreads * kSegPer;
+
+__global__ __launch_bounds__(kSegThreads) void k_filter_count(DevRawBatch b, FeaturizeParams fp,
+                                                              int64_t* blk) {
+  const int64_t r0 = int64_t(blockIdx.x) * kSegRows + int64_t(threadIdx.x) * kSegPer;
+  __shared__ int wtot[kSegThreads / kWave];
+  int c = 0;
+#pragma unroll
+  for (int k = 0; k < kSegPer; ++k) c += keep_row(b, r0 + k, fp) ? 1 : 0;
+  const int t = wave_sum(c);
+  if (lane_id() == 0) wtot[threadIdx.x / kWave] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t tot = 0;
+    for (int k = 0; k < kSegThreads / kWave; ++k) tot += wtot[k];
+    blk[blockIdx.x] = tot;
+  }
 }
 
-__global__ __launch_bounds__(kBlock) void k_filter_write(DevRawBatch b, FeaturizeParams fp,
-                                                         const int64_t* blk_off, int64_t* kept,
-                                                         int32_t* nnz, int64_t* hist) {
-  __shared__ int wtot[kBlock / kWave];
+__global__ __launch_bounds__(kSegThreads) void k_filter_write(DevRawBatch b, FeaturizeParams fp,
+                                                              const int64_t* blk_off, int64_t* kept,
+                                                              int32_t* nnz, int64_t* hist) {
+  __shared__ int wtot[kSegThreads / kWave];
   __shared__ int lhist[kLenBuckets];
-  for (int i = threadIdx.x; i < kLenBuckets; i += kBlock) lhist[i] = 0;
-  const int64_t r = int64_t(blockIdx.x) * kBlock + threadIdx.x;
-  const bool pred = keep_row(b, r, fp);
-  const uint64_t mask = __ballot(pred);
+  for (int i = threadIdx.x; i < kLenBuckets; i += kSegThreads) lhist[i] = 0;
+  const int64_t r0 = int64_t(blockIdx.x) * kSegRows + int64_t(threadIdx.x) * kSegPer;
+  bool pred[kSegPer];
+  int c = 0;
+#pragma unroll
+  for (int k = 0; k < kSegPer; ++k) {
+    pred[k] = keep_row(b, r0 + k, fp);
+    c += pred[k] ? 1 : 0;
+  }
+  // exclusive prefix of c over the block (rows stay in source order)
   const int lane = lane_id(), w = threadIdx.x / kWave;
-  const int wpre = __popcll(mask & ((1ull << lane) - 1ull));
-  if (lane == 0) wtot[w] = __popcll(mask);
+  int x = c;
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    const int y = __shfl_up(x, off, kWave);
+    if (lane >= off) x += y;
+  }
+  if (lane == kWave - 1) wtot[w] = x;
   __syncthreads();
   int woff = 0;
   for (int k = 0; k < w; ++k) woff += wtot[k];
-  if (pred) {
-    const int64_t k = blk_off[blockIdx.x] + woff + wpre;
-    kept[k] = r;
+  int64_t pos = blk_off[blockIdx.x] + woff + x - c;
+#pragma unroll
+  for (int k = 0; k < kSegPer; ++k) {
+    if (!pred[k]) continue;
+    const int64_t r = r0 + k;
+    kept[pos] = r;
     const RowText rt = row_text(b, r);
     const int64_t nz = rt.len >= 2 ? rt.len - 1 : rt.len;
     const int32_t n32 = int32_t(nz > kNnzMask ? kNnzMask : nz) | (rt.wide ? kNnzWide : 0);
-    nnz[k] = n32;
+    nnz[pos] = n32;
     atomicAdd(&lhist[len_key(n32)], 1);
+    ++pos;
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < kLenBuckets; i += kBlock)
+  for (int i = threadIdx.x; i < kLenBuckets; i += kSegThreads)
     if (lhist[i]) atomicAdd(reinterpret_cast<unsigned long long*>(&hist[i]), (unsigned long long)lhist[i]);
 }
 
-// Counting-sort scatter: one global atomic per (block, bucket) reserves a
+// Counting-sort scatter: one global atomic per (segment, bucket) reserves a
 // range; rows take positions inside it through LDS counters.
-__global__ __launch_bounds__(kBlock) void k_sort_scatter(const int32_t* nnz, const int64_t* counters,
-                                                         int64_t* cursor, int32_t* sorted,
-                                                         int64_t cap) {
+__global__ __launch_bounds__(kSegThreads) void k_sort_scatter(const int32_t* nnz, const int64_t* counters,
+                                                              int64_t* cursor, int32_t* sorted,
+                                                              int64_t cap) {
   __shared__ int lcnt[kLenBuckets];
   __shared__ long long lbase[kLenBuckets];
   const int64_t n_kept = counters[0] < cap ? counters[0] : cap;
-  for (int64_t base = int64_t(blockIdx.x) * kBlock; base < n_kept; base += int64_t(gridDim.x) * kBlock) {
-    for (int i = threadIdx.x; i < kLenBuckets; i += kBlock) lcnt[i] = 0;
+  for (int64_t base = int64_t(blockIdx.x) * kSegRows; base < n_kept; base += int64_t(gridDim.x) * kSegRows) {
+    for (int i = threadIdx.x; i < kLenBuckets; i += kSegThreads) lcnt[i] = 0;
     __syncthreads();
-    const int64_t k = base + threadIdx.x;
-    const bool ok = k < n_kept;
-    const int key = ok ? len_key(nnz[k]) : 0;
-    int rank = 0;
-    if (ok) rank = atomicAdd(&lcnt[key], 1);
+    int key[kSegPer], rank[kSegPer];
+#pragma unroll
+    for (int k = 0; k < kSegPer; ++k) {
+      const int64_t q = base + int64_t(threadIdx.x) * kSegPer + k;
+      key[k] = q < n_kept ? len_key(nnz[q]) : -1;
+    }
+#pragma unroll
+    for (int k = 0; k < kSegPer; ++k) rank[k] = key[k] >= 0 ? atomicAdd(&lcnt[key[k]], 1) : 0;
     __syncthreads();
-    for (int i = threadIdx.x; i < kLenBuckets; i += kBlock)
+    for (int i = threadIdx.x; i < kLenBuckets; i += kSegThreads)
       if (lcnt[i])
         lbase[i] = (long long)atomicAdd(reinterpret_cast<unsigned long long*>(&cursor[i]),
                                         (unsigned long long)lcnt[i]);
     __syncthreads();
-    if (ok) sorted[lbase[key] + rank] = int32_t(k);
+#pragma unroll
+    for (int k = 0; k < kSegPer; ++k)
+      if (key[k] >= 0) sorted[lbase[key[k]] + rank[k]] = int32_t(base + int64_t(threadIdx.x) * kSegPer + k);
     __syncthreads();
   }
 }
 
+// Per-batch zeroing of the small prep buffers in one launch (instead of a
+// hipMemsetAsync per buffer): counters, length histogram, DP kept counts,
+// hybrid slot histogram.
+__global__ __launch_bounds__(1024) void k_prep_init(DevPrepared p, int64_t* n_global, int ng) {
+  const int64_t i = int64_t(blockIdx.x) * 1024 + threadIdx.x;
+  if (i < 8) p.counters[i] = 0;
+  if (i < kLenBuckets + 1) p.hist[i] = 0;
+  if (i < ng) n_global[i] = 0;
+  if (i < kMaxHybridSlots) p.slot_hist[i] = 0u;
+}
+
+void launch_prep_init(const DevPrepared& p, int64_t* n_global, int ng, hipStream_t s) {
+  const int64_t n = std::max<int64_t>(kLenBuckets + 1, kMaxHybridSlots);
+  hipLaunchKernelGGL(k_prep_init, dim3(ceil_div(n, 1024)), dim3(1024), 0, s, p, n_global, ng);
+}
+
 void launch_filter_sort(const DevRawBatch& b, const DevPrepared& p, const FeaturizeParams& fp,
                         hipStream_t s) {
-  const int nb = ceil_div(b.n > 0 ? b.n : 1, kBlock);
-  TWTML_HIP_CHECK(hipMemsetAsync(p.hist, 0, sizeof(int64_t) * (kLenBuckets + 1), s));
-  hipLaunchKernelGGL(k_filter_count, dim3(nb), dim3(kBlock), 0, s, b, fp, p.blk);
+  const int nb = ceil_div(b.n > 0 ? b.n : 1, kSegRows);
+  hipLaunchKernelGGL(k_filter_count, dim3(nb), dim3(kSegThreads), 0, s, b, fp, p.blk);
   scan_excl(p.blk, p.blk, nb, &p.counters[0], s);
-  hipLaunchKernelGGL(k_filter_write, dim3(nb), dim3(kBlock), 0, s, b, fp, p.blk, p.kept, p.nnz,
+  hipLaunchKernelGGL(k_filter_write, dim3(nb), dim3(kSegThreads), 0, s, b, fp, p.blk, p.kept, p.nnz,
                      p.hist);
   scan_excl(p.hist, p.hist, kLenBuckets, nullptr, s);
-  const int g = nb < 4096 ? nb : 4096;
-  hipLaunchKernelGGL(k_sort_scatter, dim3(g), dim3(kBlock), 0, s, p.nnz, p.counters, p.hist,
+  hipLaunchKernelGGL(k_sort_scatter, dim3(nb), dim3(kSegThreads), 0, s, p.nnz, p.counters, p.hist,
                      p.sorted, p.cap_rows);
 }
 
 // Filter + order-preserving compaction only (k-means: no length sort needed).
 void launch_filter_only(const DevRawBatch& b, const DevPrepared& p, const FeaturizeParams& fp,
                         hipStream_t s) {
-  const int nb = ceil_div(b.n > 0 ? b.n : 1, kBlock);
+  const int nb = ceil_div(b.n > 0 ? b.n : 1, kSegRows);
   TWTML_HIP_CHECK(hipMemsetAsync(p.hist, 0, sizeof(int64_t) * (kLenBuckets + 1), s));
-  hipLaunchKernelGGL(k_filter_count, dim3(nb), dim3(kBlock), 0, s, b, fp, p.blk);
+  hipLaunchKernelGGL(k_filter_count, dim3(nb), dim3(kSegThreads), 0, s, b, fp, p.blk);
   scan_excl(p.blk, p.blk, nb, &p.counters[0], s);
-  hipLaunchKernelGGL(k_filter_write, dim3(nb), dim3(kBlock), 0, s, b, fp, p.blk, p.kept, p.nnz,
+  hipLaunchKernelGGL(k_filter_write, dim3(nb), dim3(kSegThreads), 0, s, b, fp, p.blk, p.kept, p.nnz,
                      p.hist);
 }
 

@@ -121,11 +121,52 @@ __global__ __launch_bounds__(1024) void k_hot_select(const uint32_t* hist, int64
 
 __device__ __forceinline__ uint32_t pack2(uint32_t a, uint32_t b) { return a | (b << 16); }
 
+constexpr int kCntStride = kHot / 2 + 4;
+// Hashed ids below kCodeIds (every Java-hash bigram of Latin-1 text) are
+// remapped through an LDS table of 16-bit codes: 0x8000 | hot id, or the
+// compact slot.  Larger ids read slot_of / hot_of from global memory.
+constexpr int kCodeIds = 8192;
+constexpr uint32_t kCodeHot = 0x8000u;
+
+// code[id] for id < kCodeIds (0xFFFF: id not active in this batch; never
+// looked up, but slot_of is only defined for active ids -- checked via uniq)
+__global__ __launch_bounds__(1024) void k_code_table(DevPrepared p, uint16_t* code) {
+  const int id = blockIdx.x * 1024 + threadIdx.x;
+  if (id >= kCodeIds) return;
+  const int64_t nU = p.counters[1];
+  uint32_t c = 0xFFFFu;
+  if (id < p.flag_len) {
+    const int32_t u = p.slot_of[id];
+    if (u >= 0 && u < nU && p.uniq[u] == id) {
+      const uint32_t sl = uint32_t(kNumNumeric + u);
+      const uint32_t h = p.hot_of[sl];
+      c = h != 0xFFu ? (kCodeHot | h) : sl;
+    }
+  }
+  code[id] = uint16_t(c);
+}
+
+__device__ __forceinline__ uint32_t id_code(const uint16_t* lcode, const DevPrepared& p, int32_t id) {
+  if (id < kCodeIds) return lcode[id];
+  const uint32_t sl = uint32_t(kNumNumeric + p.slot_of[id]);
+  const uint32_t h = p.hot_of[sl];
+  return h != 0xFFu ? (kCodeHot | h) : sl;
+}
+
+// One wave per 16-row chunk (SELL-16x4 input layout of featurize):
+//   pass 1  ids -> codes; hot ids counted per row (LDS u16 pairs), cold
+//           slots stored straight to this lane's cold stream (in order)
+//   dense   this lane's 32 hot ids of its row as 4-bit counts
+//   rare    a hot id counting > 15 in a row: its entries are re-read and
+//           appended cold (each stays in the lane that held it)
+//   pad     every lane's cold stream padded to the chunk's max group count
 __global__ __launch_bounds__(kSplitWaves * kWave) void k_remap_hybrid(DevPrepared p, int64_t ns,
-                                                                      int64_t pad_base) {
-  __shared__ uint8_t hot_of[kMaxHybridSlots];
-  __shared__ uint32_t cnt[kSplitWaves][kRowsPerChunk * kHot / 2];   // u16 counts, 2 per word
-  for (int64_t s = threadIdx.x; s < ns; s += kSplitWaves * kWave) hot_of[s] = p.hot_of[s];
+                                                                      int64_t pad_base,
+                                                                      const uint16_t* code) {
+  __shared__ uint16_t lcode[kCodeIds];
+  __shared__ uint32_t cnt[kSplitWaves][kRowsPerChunk * kCntStride];
+  for (int i = threadIdx.x; i < kCodeIds / 8; i += kSplitWaves * kWave)
+    reinterpret_cast<uint4*>(lcode)[i] = reinterpret_cast<const uint4*>(code)[i];
   __syncthreads();
   const int lane = lane_id();
   const int w = __builtin_amdgcn_readfirstlane(int(threadIdx.x) / kWave);
@@ -135,17 +176,18 @@ __global__ __launch_bounds__(kSplitWaves * kWave) void k_remap_hybrid(DevPrepare
   const int64_t wave = int64_t(blockIdx.x) * kSplitWaves + w;
   const int64_t nwaves = int64_t(gridDim.x) * kSplitWaves;
   uint32_t* cw = cnt[w];
-  uint32_t* crow = cw + r * (kHot / 2);
+  uint32_t* crow = cw + r * kCntStride;
   const uint32_t pad = uint32_t(pad_base + lane);
   uint16_t* plain = static_cast<uint16_t*>(p.slot);
 
   for (int64_t c = wave; c < nch; c += nwaves) {
     const int32_t L8 = p.clen8[c];
     const int64_t off = p.cbase[c] * kChunkStride + lane * kGroup;
+    const int32_t* src = p.idx + off;
     if (L8 > kMaxRegGroups) {   // plain layout (as k_remap)
       for (int32_t g = 0; g < L8; ++g) {
-        const int4* src = reinterpret_cast<const int4*>(p.idx + off + int64_t(g) * kChunkStride);
-        const int4 a = src[0], b = src[1];
+        const int4* s4 = reinterpret_cast<const int4*>(src + int64_t(g) * kChunkStride);
+        const int4 a = s4[0], b = s4[1];
         const int32_t v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
         uint32_t o[8];
 #pragma unroll
@@ -156,33 +198,34 @@ __global__ __launch_bounds__(kSplitWaves * kWave) void k_remap_hybrid(DevPrepare
       if (lane == 0) p.clen8c[c] = -1;
       continue;
     }
-    for (int i = lane; i < kRowsPerChunk * kHot / 2; i += kWave) cw[i] = 0u;
+    for (int i = lane; i < kRowsPerChunk * kCntStride; i += kWave) cw[i] = 0u;
     wave_lds_sync();
-    // pass 1: slots into registers (u16 pairs), hot counts per row in LDS
-    uint32_t sv[kMaxRegGroups][4];
+    uint16_t* dst = p.cslot + off;
+    int32_t k = 0;   // cold entries of this lane so far
+    auto put = [&](uint32_t sl) {
+      dst[int64_t(k >> 3) * kChunkStride + (k & 7)] = uint16_t(sl);
+      ++k;
+    };
+    for (int32_t g = 0; g < L8; ++g) {
+      const int4* s4 = reinterpret_cast<const int4*>(src + int64_t(g) * kChunkStride);
+      const int4 a = s4[0], b = s4[1];
+      const int32_t v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 #pragma unroll
-    for (int g = 0; g < kMaxRegGroups; ++g) {
-      if (g < L8) {
-        const int4* src = reinterpret_cast<const int4*>(p.idx + off + int64_t(g) * kChunkStride);
-        const int4 a = src[0], b = src[1];
-        const int32_t v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-        uint32_t o[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          o[e] = v[e] >= 0 ? uint32_t(kNumNumeric + p.slot_of[v[e]]) : pad;
-          const uint32_t h = v[e] >= 0 ? uint32_t(hot_of[o[e]]) : 0xFFu;
-          if (h != 0xFFu) atomicAdd(&crow[h >> 1], 1u << ((h & 1u) * 16));
+      for (int e = 0; e < 8; ++e) {
+        if (v[e] < 0) continue;
+        const uint32_t cd = id_code(lcode, p, v[e]);
+        if (cd & kCodeHot) {
+          const uint32_t h = cd & 0xFFu;
+          atomicAdd(&crow[h >> 1], 1u << ((h & 1u) * 16));
+        } else {
+          put(cd);
         }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) sv[g][q] = pack2(o[2 * q], o[2 * q + 1]);
-      } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) sv[g][q] = 0u;
       }
     }
     wave_lds_sync();
     // dense part: this lane's 32 hot ids of its row; counts > 15 stay cold
     uint32_t nib[4] = {0u, 0u, 0u, 0u};
+    bool ovf = false;
     {
       const uint4* c4 = reinterpret_cast<const uint4*>(crow + 16 * t);
 #pragma unroll
@@ -190,47 +233,38 @@ __global__ __launch_bounds__(kSplitWaves * kWave) void k_remap_hybrid(DevPrepare
         const uint4 cv = c4[j];
         const uint32_t ws[4] = {cv.x, cv.y, cv.z, cv.w};
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int q = 0; q < 4; ++q) {
 #pragma unroll
           for (int hh = 0; hh < 2; ++hh) {
-            const uint32_t n = (ws[k] >> (16 * hh)) & 0xFFFFu;
-            const int i = 8 * j + 2 * k + hh;          // hot id 32t + i
+            const uint32_t n = (ws[q] >> (16 * hh)) & 0xFFFFu;
+            const int i = 8 * j + 2 * q + hh;          // hot id 32t + i
             if (n <= 15u) nib[i >> 3] |= n << (4 * (i & 7));
+            else ovf = true;
           }
         }
       }
     }
     reinterpret_cast<uint4*>(p.hot_dense)[c * kWave + lane] = make_uint4(nib[0], nib[1], nib[2], nib[3]);
-    // pass 2: this lane's cold entries (in order) -> its own cold groups
-    uint64_t lo = 0, hi = 0;   // 8-entry shift register
-    int32_t n = 0, gout = 0;
-    uint16_t* dst = p.cslot + off;
-    auto push = [&](uint32_t s) {
-      lo = (lo >> 16) | (hi << 48);
-      hi = (hi >> 16) | (uint64_t(s) << 48);
-      if (++n == kGroup) {
-        *reinterpret_cast<uint4*>(dst + int64_t(gout) * kChunkStride) =
-            make_uint4(uint32_t(lo), uint32_t(lo >> 32), uint32_t(hi), uint32_t(hi >> 32));
-        ++gout;
-        n = 0;
-      }
-    };
+    if (__any(ovf)) {   // rare: a hot bigram more than 15 times in one row
+      for (int32_t g = 0; g < L8; ++g) {
+        const int4* s4 = reinterpret_cast<const int4*>(src + int64_t(g) * kChunkStride);
+        const int4 a = s4[0], b = s4[1];
+        const int32_t v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 #pragma unroll
-    for (int g = 0; g < kMaxRegGroups; ++g) {
-      if (g >= L8) continue;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const uint32_t s = (sv[g][e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
-        if (s >= uint32_t(pad_base)) continue;
-        const uint32_t h = hot_of[s];
-        bool cold = h == 0xFFu;
-        if (!cold) cold = ((crow[h >> 1] >> ((h & 1u) * 16)) & 0xFFFFu) > 15u;
-        if (cold) push(s);
+        for (int e = 0; e < 8; ++e) {
+          if (v[e] < 0) continue;
+          const uint32_t cd = id_code(lcode, p, v[e]);
+          if (!(cd & kCodeHot)) continue;
+          const uint32_t h = cd & 0xFFu;
+          if (((crow[h >> 1] >> ((h & 1u) * 16)) & 0xFFFFu) > 15u) put(uint32_t(p.hot_slot[h]));
+        }
       }
     }
-    const int32_t mine = gout + (n > 0 ? 1 : 0);
-    const int32_t L8c = wave_max(mine);
-    while (gout < L8c) push(pad);
+    const int32_t L8c = wave_max((k + kGroup - 1) / kGroup);
+    while (k < L8c * kGroup && (k & 7)) put(pad);           // finish the partial group
+    for (int32_t g = k >> 3; g < L8c; ++g)                    // whole pad groups
+      *reinterpret_cast<uint4*>(dst + int64_t(g) * kChunkStride) =
+          make_uint4(pack2(pad, pad), pack2(pad, pad), pack2(pad, pad), pack2(pad, pad));
     if (lane == 0) p.clen8c[c] = L8c;
     wave_lds_sync();   // the next chunk clears / refills this wave's LDS
   }
@@ -242,7 +276,7 @@ void launch_remap_hybrid(const DevPrepared& p, int64_t entries, int64_t ns, int6
                          hipStream_t s) {
   if (ns > kMaxHybridSlots) throw std::invalid_argument("hybrid layout: too many active slots");
   if (entries == 0) return;
-  TWTML_HIP_CHECK(hipMemsetAsync(p.slot_hist, 0, sizeof(uint32_t) * size_t(ns), s));
+  // slot_hist was zeroed by launch_prep_init
   const int64_t n8 = entries / kGroup;
   int gh = int((n8 / kHistStride + kHistBlock - 1) / kHistBlock);
   gh = std::max(1, std::min(gh, num_cu));
@@ -250,10 +284,12 @@ void launch_remap_hybrid(const DevPrepared& p, int64_t entries, int64_t ns, int6
                      p.idx, p.slot_of, n8, pad_base, p.slot_hist);
   hipLaunchKernelGGL(k_hot_select, dim3(1), dim3(1024), 0, s, p.slot_hist, ns, pad_base, p.hot_of,
                      p.hot_slot);
+  hipLaunchKernelGGL(k_code_table, dim3(kCodeIds / 1024), dim3(1024), 0, s, p, p.code);
   const int64_t cmax = (p.cap_rows + kRowsPerChunk - 1) / kRowsPerChunk;
-  int grid = int(std::min<int64_t>(int64_t(num_cu) * 16, (cmax + kSplitWaves - 1) / kSplitWaves));
+  // persistent-style grid (each workgroup loads the 16 KB code table once)
+  int grid = int(std::min<int64_t>(int64_t(num_cu) * 4, (cmax + kSplitWaves - 1) / kSplitWaves));
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL(k_remap_hybrid, dim3(grid), dim3(kSplitWaves * kWave), 0, s, p, ns, pad_base);
+  hipLaunchKernelGGL(k_remap_hybrid, dim3(grid), dim3(kSplitWaves * kWave), 0, s, p, ns, pad_base, p.code);
 }
 
 }  // namespace twtml

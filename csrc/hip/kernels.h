@@ -84,6 +84,7 @@ struct DevPrepared {
   int32_t* clen8c;          // [C]   cold groups per lane; -1 = chunk left in the plain layout
   int32_t* hot_slot;        // [kHot] slot of hot id h (a zero-weight pad slot when unused)
   uint8_t* hot_of;          // [kMaxHybridSlots] hot id of a slot (0xFF = cold)
+  uint16_t* code;           // [8192] remap code of small hashed ids (hot_split.hip)
   uint32_t* slot_hist;      // [kMaxHybridSlots] sampled slot frequencies
   int32_t hybrid;           // 1: iteration kernels use the hybrid layout
   // counters (device): [0]=n_kept [1]=n_unique [2]=groups [3]=error
@@ -102,6 +103,9 @@ struct FeaturizeParams {
 
 void upload_lower_tables(hipStream_t s, uint8_t** d_page, uint16_t** d_blocks);
 
+// zero counters, length histogram, n_global[0..ng) and the hybrid slot
+// histogram (before launch_filter_sort)
+void launch_prep_init(const DevPrepared& p, int64_t* n_global, int ng, hipStream_t s);
 void launch_filter_sort(const DevRawBatch& b, const DevPrepared& p, const FeaturizeParams& fp,
                         hipStream_t s);
 void launch_chunk_layout(const DevRawBatch& b, const DevPrepared& p, hipStream_t s);
@@ -143,6 +147,25 @@ struct DevSgd {
   int32_t nparts;       // partial rows written by the last iteration launch (0 = global path)
 };
 
+// Grid barrier of the persistent GD kernel (uncached memory): per-XCD-group
+// arrival counters (64 B apart), global counter, generation, error flag.
+struct GridBar {
+  uint32_t cnt[8 * 16];
+  uint32_t gcnt, pad0[15];
+  uint32_t gen, pad1[15];
+  uint32_t err, pad2[15];
+};
+
+constexpr int kMaxPersistGrid = 512;
+// Cross-workgroup buffers of the persistent GD kernel (hipDeviceMallocUncached)
+struct DevCoh {
+  double* part;     // [G][pstride] partial rows
+  float* w32;       // [ns] compact fp32 weights after each update
+  double* norms;    // [2][G][2] per-workgroup ||dw||^2, ||w||^2 (iteration parity)
+  GridBar* bar;
+  uint64_t* tdbg;   // optional [iters][8] s_memrealtime stamps of workgroup 0 (TWTML_GD_TIMING)
+};
+
 // Iteration record: [0] updates so far, [1] m, [2] update workgroups,
 // [kRecHead + 2w] ||dw||^2 and ||w||^2 partials of update workgroup w.
 constexpr int kMaxUpdGrid = 256;
@@ -182,6 +205,11 @@ int sgd_partials(int64_t ns, bool u16, int grid);
 void launch_sgd_reduce(const DevSgd& d, const SgdParams& sp, hipStream_t s);
 // nparts > 0: sums the partial rows itself (single GPU, no separate reduce)
 void launch_sgd_update(const DevSgd& d, const SgdParams& sp, int nparts, hipStream_t s);
+// persistent loop for iterations it_first..N (single GPU); grid from
+// sgd_persistent_grid (0 = use the per-iteration kernels)
+int sgd_persistent_grid(const DevSgd& d, const DevPrepared& p, bool u16, bool sample, int num_cu);
+void launch_sgd_persistent(const DevSgd& d, const DevPrepared& p, const SgdParams& sp, const DevCoh& coh,
+                           int it_first, int grid, hipStream_t s);
 // after the GD loop: convergence of the last update -> state
 void launch_sgd_finish(const DevSgd& d, const SgdParams& sp, hipStream_t s);
 void launch_scatter_w(const DevSgd& d, const DevPrepared& p, hipStream_t s);

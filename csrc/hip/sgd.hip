@@ -434,22 +434,14 @@ __device__ __forceinline__ void hot_grad(const uint4 hv, float res, float (&gh)[
     for (int k = 0; k < 8; ++k) gh[8 * q + k] += res * float((hw[q] >> (4 * k)) & 15u);
 }
 
+// One pass of the hybrid gradient over this workgroup's chunks (LDS already
+// holds the weights wl / hot weights whl and a zeroed gradient gl); ends by
+// writing the workgroup's partial row prow (includes block barriers).
 template <bool STATS, bool SAMPLE, int REP>
-__global__ __launch_bounds__(kIterBlock) void k_sgd_iter_hyb(DevSgd d, DevPrepared p, SgdParams sp) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  __shared__ double wsc[kIterBlock / kWave][kPartVals];
-  __shared__ float hsum[kIterBlock / kWave][kHot];
-  __shared__ __attribute__((aligned(16))) float whl[kLanesPerRow * kHotLdsStride];
-  __shared__ int stop_flag;
-  if (sgd_stop(d, sp, &stop_flag)) return;
+__device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, const SgdParams& sp,
+                                         const float* wl, unsigned long long* gl, const float* whl,
+                                         float (*hsum)[kHot], double (*wsc)[kPartVals], double* prow) {
   const int64_t ns = d.ns;
-  float* wl = lds;
-  unsigned long long* gl = reinterpret_cast<unsigned long long*>(lds + ns);
-  for (int64_t s = threadIdx.x; s < ns; s += kIterBlock) wl[s] = d.wc32[s];
-  for (int64_t s = threadIdx.x; s < ns * REP; s += kIterBlock) gl[s] = 0ull;
-  for (int h = threadIdx.x; h < kHot; h += kIterBlock)
-    whl[(h / kHotPerLane) * kHotLdsStride + h % kHotPerLane] = d.wc32[p.hot_slot[h]];
-  __syncthreads();
   const int lane = lane_id();
   const int w = __builtin_amdgcn_readfirstlane(int(threadIdx.x) / kWave);   // wave-uniform
   const int r = lane / kLanesPerRow, t = lane % kLanesPerRow;
@@ -595,7 +587,6 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_hyb(DevSgd d, DevPrepar
     v += __shfl_xor(v, 32, kWave);
     if (lane < kLanesPerRow) hsum[w][kHotPerLane * lane + i] = v;
   }
-  double* prow = d.part + int64_t(blockIdx.x) * d.pstride;
   part_scalars<STATS, SAMPLE>(d, acc, wsc, prow);   // includes the block barrier
   const int64_t hi = kNumNumeric + d.n_unique;      // pads are never flushed
   for (int64_t s = kNumNumeric + threadIdx.x; s < ns; s += kIterBlock) {
@@ -611,6 +602,201 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_hyb(DevSgd d, DevPrepar
     }
     prow[s] = v;
   }
+}
+
+
+// Weights -> LDS (fp32 compact weights, hot weights in hot order) and a
+// zeroed fixed-point gradient; ends with a block barrier.
+// Loads of data other workgroups wrote during the persistent kernel:
+// device-scope (sc1) so they are not served from this CU's (non-coherent) L1.
+template <typename T>
+__device__ __forceinline__ T ld_coh(const T* ptr) {
+  return __hip_atomic_load(ptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Slots >= hi (pads) get weight 0 whatever wsrc holds there.
+template <int REP>
+__device__ __forceinline__ void hyb_lds_init(const DevPrepared& p, const float* wsrc, int64_t ns,
+                                             int64_t hi, float* wl, unsigned long long* gl, float* whl) {
+  for (int64_t s = threadIdx.x; s < ns; s += kIterBlock) wl[s] = s < hi ? ld_coh(wsrc + s) : 0.f;
+  for (int64_t s = threadIdx.x; s < ns * REP; s += kIterBlock) gl[s] = 0ull;
+  __syncthreads();
+  for (int h = threadIdx.x; h < kHot; h += kIterBlock)
+    whl[(h / kHotPerLane) * kHotLdsStride + h % kHotPerLane] = wl[p.hot_slot[h]];
+  __syncthreads();
+}
+
+template <bool STATS, bool SAMPLE, int REP>
+__global__ __launch_bounds__(kIterBlock) void k_sgd_iter_hyb(DevSgd d, DevPrepared p, SgdParams sp) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  __shared__ double wsc[kIterBlock / kWave][kPartVals];
+  __shared__ float hsum[kIterBlock / kWave][kHot];
+  __shared__ __attribute__((aligned(16))) float whl[kLanesPerRow * kHotLdsStride];
+  __shared__ int stop_flag;
+  if (sgd_stop(d, sp, &stop_flag)) return;
+  float* wl = lds;
+  unsigned long long* gl = reinterpret_cast<unsigned long long*>(lds + d.ns);
+  hyb_lds_init<REP>(p, d.wc32, d.ns, kNumNumeric + d.n_unique, wl, gl, whl);
+  hyb_pass<STATS, SAMPLE, REP>(d, p, sp, wl, gl, whl, hsum, wsc, d.part + int64_t(blockIdx.x) * d.pstride);
+}
+
+// ---------------------------------------------------------------------------
+// Persistent GD loop (single GPU, hybrid layout, iterations 2..N).
+//
+// One workgroup per CU for the whole loop, so the ~25 us of per-iteration
+// launch / prologue / epilogue / update-kernel overhead of the multi-kernel
+// path disappears.  Per iteration:
+//   pass      gradient over the workgroup's chunks -> partial row (UC memory)
+//   barrier A
+//   update    workgroup b owns ~ns/G columns: fixed-order sum of the G
+//             partial rows, SimpleUpdater, fp32 copy -> UC memory, norms
+//   barrier B
+//   converged?  every workgroup sums the G norm partials in the same order
+//             (identical verdicts), MLlib test as k_sgd_update/sgd_stop.
+// Cross-workgroup data lives in uncached (hipDeviceMallocUncached) memory,
+// so the barriers need no L2 write-back / invalidate (a device-scope fence
+// on MI355X writes back the XCD's whole L2 -- measured, see profiles/).
+// The grid barrier is hierarchical: one arrival counter per XCD group
+// (blockIdx % 8), the last arriver of a group bumps the global counter, the
+// last group publishes the generation.  Spins are bounded: a stuck barrier
+// raises bar->err and every workgroup leaves the loop.
+// ---------------------------------------------------------------------------
+__device__ bool grid_sync(GridBar* gb, uint32_t target, int* flag) {
+  __builtin_amdgcn_s_waitcnt(0);   // this thread's UC stores have completed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t G = gridDim.x, x = blockIdx.x & 7u;
+    const uint32_t nx = (G - x + 7u) / 8u;
+    const uint32_t ng = G < 8u ? G : 8u;
+    if (atomicAdd(&gb->cnt[x * 16], 1u) + 1u == target * nx)
+      if (atomicAdd(&gb->gcnt, 1u) + 1u == target * ng)
+        __hip_atomic_store(&gb->gen, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int ok = 1;
+    uint32_t spins = 0;
+    while (__hip_atomic_load(&gb->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (__hip_atomic_load(&gb->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) { ok = 0; break; }
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 25)) {
+        __hip_atomic_store(&gb->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+    }
+    *flag = ok;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
+template <int REP>
+__global__ __launch_bounds__(kIterBlock) void k_sgd_gd_hyb(DevSgd d, DevPrepared p, SgdParams sp,
+                                                           DevCoh coh, int it_first) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  __shared__ double wsc[kIterBlock / kWave][kPartVals];
+  __shared__ float hsum[kIterBlock / kWave][kHot];
+  __shared__ __attribute__((aligned(16))) float whl[kLanesPerRow * kHotLdsStride];
+  __shared__ double red[kIterBlock / kWave][2];
+  __shared__ int flag, conv_sh;
+  const int64_t ns = d.ns, hi = kNumNumeric + d.n_unique;
+  float* wl = lds;
+  unsigned long long* gl = reinterpret_cast<unsigned long long*>(lds + ns);
+  const int G = int(gridDim.x), b = int(blockIdx.x);
+  const int lane = lane_id(), w = int(threadIdx.x) / kWave;
+  const double m = d.state[5];
+  double rest = d.state[4] - d.state[6];
+  if (rest < 0.0) rest = 0.0;
+  // update columns of this workgroup: index k in [0, hi] -> column k (< hi) or the loss (ns)
+  const int64_t nk = hi + 1, cpw = (nk + G - 1) / G;
+  const int64_t k0 = int64_t(b) * cpw, k1 = k0 + cpw < nk ? k0 + cpw : nk;
+  double* prow = coh.part + int64_t(b) * d.pstride;
+  uint32_t gen = 0;
+  int it = it_first;
+  uint64_t* tst = nullptr;
+  auto stamp = [&](int k) {
+    if (tst && b == 0 && threadIdx.x == 0) tst[k] = __builtin_amdgcn_s_memrealtime();
+  };
+  for (;; ++it) {
+    sp.iteration = it;
+    tst = coh.tdbg ? coh.tdbg + int64_t(it) * 8 : nullptr;
+    stamp(0);
+    hyb_lds_init<REP>(p, it == it_first ? d.wc32 : coh.w32, ns, hi, wl, gl, whl);
+    stamp(1);
+    hyb_pass<false, false, REP>(d, p, sp, wl, gl, whl, hsum, wsc, prow);
+    stamp(2);
+    if (!grid_sync(coh.bar, ++gen, &flag)) break;
+    stamp(3);
+    // ---- update of this workgroup's columns (one wave per column)
+    const double alpha = sp.step_size / sqrt(double(it));
+    double ds = 0.0, ws = 0.0;
+    for (int64_t k = k0 + w; k < k1; k += kIterBlock / kWave) {
+      const int64_t col = k < hi ? k : ns;
+      // the G partials of this column, all loads in flight at once
+      double a[kMaxPersistGrid / kWave];
+#pragma unroll
+      for (int q = 0; q < kMaxPersistGrid / kWave; ++q) {
+        const int j = lane + q * kWave;
+        a[q] = j < G ? ld_coh(coh.part + int64_t(j) * d.pstride + col) : 0.0;
+      }
+      double g = 0.0;
+#pragma unroll
+      for (int q = 0; q < kMaxPersistGrid / kWave; ++q) g += a[q];
+      g = wave_sum(g);
+      if (lane == 0) {
+        if (col < hi) {
+          const double step = alpha * (g / m);
+          const double wn = d.wc64[col] - step;
+          d.wc64[col] = wn;
+          coh.w32[col] = float(wn);
+          ds += step * step;
+          ws += wn * wn;
+        } else {
+          d.loss_hist[it] = g / m;
+        }
+      }
+    }
+    if (lane == 0) {
+      red[w][0] = ds;
+      red[w][1] = ws;
+    }
+    __syncthreads();
+    double* nrm = coh.norms + int64_t(it & 1) * 2 * G;
+    if (threadIdx.x < 2) {
+      double t = 0.0;
+      for (int k = 0; k < kIterBlock / kWave; ++k) t += red[k][threadIdx.x];
+      nrm[2 * b + threadIdx.x] = t;
+    }
+    stamp(4);
+    if (!grid_sync(coh.bar, ++gen, &flag)) break;
+    stamp(5);
+    // ---- convergence (every workgroup, same fixed-order sums)
+    if (threadIdx.x < kWave) {
+      double dsum = 0.0, wsum = 0.0;
+      for (int j = lane; j < G; j += kWave) {
+        dsum += ld_coh(nrm + 2 * j);
+        wsum += ld_coh(nrm + 2 * j + 1);
+      }
+      dsum = wave_sum(dsum);
+      wsum = wave_sum(wsum);
+      const double wnorm = sqrt(wsum + rest);
+      const bool conv = sqrt(dsum) < sp.tol * (wnorm > 1.0 ? wnorm : 1.0);   // it >= 2: second update on
+      if (threadIdx.x == 0) conv_sh = conv ? 1 : 0;
+    }
+    __syncthreads();
+    stamp(6);
+    const bool conv = conv_sh != 0;
+    if (conv || it >= sp.num_iterations) {
+      if (b == 0 && threadIdx.x == 0) {
+        d.state[0] = 1.0;
+        if (conv) d.state[1] = 1.0;
+        d.state[2] = double(it);
+        d.state[3] = double(it);
+      }
+      break;
+    }
+  }
+  if (b == 0 && threadIdx.x == 0 &&
+      __hip_atomic_load(&coh.bar->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)
+    d.state[7] = 2.0;   // barrier timeout: reported by the host
 }
 
 // Generic path: any slot width, weights read from global (L2), gradient by
@@ -752,6 +938,45 @@ void launch_sgd_iter(const DevSgd& d, const DevPrepared& p, const SgdParams& sp,
 
 int sgd_partials(int64_t ns, bool u16, int grid) {
   return (u16 && sgd_lds_rep(ns) > 0) ? grid : 0;
+}
+
+// Persistent loop: the grid it needs (0 = not applicable: generic / plain
+// layout, sampling, or a workgroup per CU does not fit).
+int sgd_persistent_grid(const DevSgd& d, const DevPrepared& p, bool u16, bool sample, int num_cu) {
+  if (!u16 || sample || !p.hybrid) return 0;
+  const int rep = sgd_lds_rep(d.ns);
+  if (rep <= 0) return 0;
+  const size_t lds = size_t(lds_bytes(d.ns, rep));
+  int per_cu = 0;
+  hipError_t e = hipSuccess;
+  switch (rep) {
+    case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sgd_gd_hyb<8>, kIterBlock, lds); break;
+    case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sgd_gd_hyb<4>, kIterBlock, lds); break;
+    case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sgd_gd_hyb<2>, kIterBlock, lds); break;
+    default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sgd_gd_hyb<1>, kIterBlock, lds); break;
+  }
+  if (e != hipSuccess || per_cu < 1 || num_cu > kMaxPersistGrid) return 0;
+  return num_cu;   // one workgroup per CU (co-resident by construction, cooperative launch checks)
+}
+
+void launch_sgd_persistent(const DevSgd& d, const DevPrepared& p, const SgdParams& sp, const DevCoh& coh,
+                           int it_first, int grid, hipStream_t s) {
+  const int rep = sgd_lds_rep(d.ns);
+  const unsigned lds = unsigned(lds_bytes(d.ns, rep));
+  SgdParams spc = sp;
+  DevSgd dc = d;
+  DevPrepared pc = p;
+  DevCoh cc = coh;
+  int itf = it_first;
+  void* args[] = {&dc, &pc, &spc, &cc, &itf};
+  const void* fn = nullptr;
+  switch (rep) {
+    case 8: fn = reinterpret_cast<const void*>(k_sgd_gd_hyb<8>); break;
+    case 4: fn = reinterpret_cast<const void*>(k_sgd_gd_hyb<4>); break;
+    case 2: fn = reinterpret_cast<const void*>(k_sgd_gd_hyb<2>); break;
+    default: fn = reinterpret_cast<const void*>(k_sgd_gd_hyb<1>); break;
+  }
+  TWTML_HIP_CHECK(hipLaunchCooperativeKernel(fn, dim3(grid), dim3(kIterBlock), args, lds, s));
 }
 
 // ---------------------------------------------------------------------------
@@ -987,10 +1212,21 @@ void launch_scatter_w(const DevSgd& d, const DevPrepared& p, hipStream_t s) {
   hipLaunchKernelGGL(k_scatter_w, dim3(grid), dim3(kBlock), 0, s, d, p.uniq);
 }
 
-__global__ void k_batch_init(double* state, double m_global) { state[5] = m_global; }
+// Per-batch SGD state in one launch: state (m = global kept rows at [5]),
+// batch stats, sampled counts, the loss slot g64[ns] and the loss history.
+__global__ void k_batch_init(DevSgd d, double m_global, int n_loss) {
+  const int i = threadIdx.x;
+  if (i < 8) {
+    d.state[i] = i == 5 ? m_global : 0.0;
+    d.stats[i] = 0.0;
+  }
+  if (i < 4) d.red64[i] = 0.0;
+  if (i == 0) d.g64[d.ns] = 0.0;
+  for (int k = i; k < n_loss; k += blockDim.x) d.loss_hist[k] = 0.0;
+}
 
-void launch_batch_init(double* state, double m_global, hipStream_t s) {
-  hipLaunchKernelGGL(k_batch_init, dim3(1), dim3(1), 0, s, state, m_global);
+void launch_batch_init(const DevSgd& d, double m_global, int n_loss, hipStream_t s) {
+  hipLaunchKernelGGL(k_batch_init, dim3(1), dim3(256), 0, s, d, m_global, n_loss);
 }
 
 }  // namespace twtml
