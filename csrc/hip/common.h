@@ -40,6 +40,31 @@ __device__ __forceinline__ T wave_sum(T v) {
   return v;
 }
 
+// fp32 wave sum on the VALU (no LDS permute traffic): DPP quad permutes and
+// row rotates inside each 16-lane row, then the four row totals through
+// v_readlane.  Every lane returns the total.  (The gfx950
+// v_permlane{16,32}_swap builtins are avoided: with both operands the same
+// value the compiler read one swap result twice -- wrong sums, measured.)
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float rdlane(float v, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+// per-row sum over the 4 lanes of each quad-column: lanes j, j+4, j+8, j+12 of a row
+__device__ __forceinline__ float row_sum_mod4(float v) {
+  v += dpp_mov<0x124>(v);   // row_ror:4
+  v += dpp_mov<0x128>(v);   // row_ror:8
+  return v;
+}
+__device__ __forceinline__ float wave_sum_f32(float v) {
+  v += dpp_mov<0xB1>(v);    // quad_perm [1,0,3,2]: lane ^ 1
+  v += dpp_mov<0x4E>(v);    // quad_perm [2,3,0,1]: lane ^ 2
+  v = row_sum_mod4(v);      // every lane: its 16-lane row total
+  return (rdlane(v, 0) + rdlane(v, 16)) + (rdlane(v, 32) + rdlane(v, 48));
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_max(T v) {
 #pragma unroll

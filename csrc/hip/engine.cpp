@@ -7,6 +7,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
+#include <thread>
 
 namespace twtml {
 
@@ -132,6 +133,26 @@ void LREngine::alloc_prepared() {
 // the uncached-memory round trips per iteration (~18 us) cost as much as the
 // per-iteration kernel launches they replace (profiles/README.md), and
 // rocprofv3 kernel tracing does not survive the cooperative launch.
+// Host side of the early stop: spin (with back-off) on the zero-copy verdict
+// of update j, which iteration j+1's gradient kernel publishes in its
+// prologue.  Bounded: the stream is synchronised as a fallback so a kernel
+// fault surfaces as a HIP error instead of a hang.
+double LREngine::wait_flag(int j) {
+  volatile double* f = host_flags_ + j;
+  for (int spin = 0; spin < (1 << 22); ++spin) {
+    const double v = *f;
+    if (v >= 0.0) {
+      if (std::getenv("TWTML_DEBUG_EARLY")) std::fprintf(stderr, "early-stop check j=%d flag=%g\n", j, v);
+      return v;
+    }
+    if (spin > 4096) std::this_thread::yield();
+  }
+  TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
+  const double v = *f;
+  if (v < 0.0) throw std::runtime_error("GD early-stop verdict never published");
+  return v;
+}
+
 bool LREngine::persist_enabled() {
   const char* e = std::getenv("TWTML_PERSIST");
   return e && e[0] == '1';
@@ -198,7 +219,7 @@ LREngine::~LREngine() {
                   prep_.cbase, prep_.idx, prep_.slot, prep_.y, prep_.num, prep_.perm,
                   prep_.flags, prep_.uniq, prep_.slot_of, prep_.ublk, prep_.counters,
                   sgd_.w64, sgd_.wc64, sgd_.wc32, sgd_.g64, sgd_.red64, sgd_.stats, sgd_.state,
-                  sgd_.loss_hist, sgd_.pred_out, sgd_.part, sgd_.itrec, coh_.part, coh_.w32, coh_.norms, coh_.bar, gd_tdbg_, lower_page_, lower_blocks_, n_global_};
+                  sgd_.loss_hist, sgd_.pred_out, sgd_.part, sgd_.itrec, coh_.part, coh_.w32, coh_.norms, coh_.bar, gd_tdbg_, iter_tdbg_, lower_page_, lower_blocks_, n_global_};
   for (void* b : bufs) if (b) (void)hipFree(b);
   if (host_counters_) (void)hipHostFree(host_counters_);
   if (host_out_) (void)hipHostFree(host_out_);
@@ -310,7 +331,7 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
         iter_events_.push_back(e);
       }
     }
-    std::fill(host_flags_, host_flags_ + iters + 2, 0.0);
+    std::fill(host_flags_, host_flags_ + iters + 2, -1.0);   // -1: verdict not published yet
     // single GPU with partial rows: the update kernel reduces them itself
     const bool fused = world == 1 && sgd_.nparts > 0;
     // single GPU, hybrid layout: iterations 2..N in one persistent kernel
@@ -343,19 +364,19 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
                             n, acc[0] / n, acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n);
       }
     }
+    const bool itime = std::getenv("TWTML_ITER_TIMING") != nullptr;
+    if (itime && !iter_tdbg_) iter_tdbg_ = dmalloc<uint64_t>(size_t(iters + 2) * 16);
+    sgd_.tdbg = itime ? iter_tdbg_ : nullptr;
+    if (itime) TWTML_HIP_CHECK(hipMemsetAsync(iter_tdbg_, 0, sizeof(uint64_t) * size_t(iters + 2) * 16, s));
     for (int i = 1; pgrid == 0 && i <= iters; ++i) {
       if (i > depth) {
         const int j = i - depth;                       // verdict after update j
-        TWTML_HIP_CHECK(hipEventSynchronize(iter_events_[size_t(j)]));
-        if (std::getenv("TWTML_DEBUG_EARLY"))
-          std::fprintf(stderr, "early-stop check i=%d j=%d flag=%g\n", i, j, host_flags_[j]);
-        if (host_flags_[j] != 0.0) break;
+        if (wait_flag(j) != 0.0) break;
       }
       sp.iteration = i;
       // every rank launches the gradient kernel (an empty shard writes zero
       // partials) so every rank runs the convergence prologue
       launch_sgd_iter(sgd_, prep_, sp, host_counters_[2], u16, grid, s);
-      if (i > 1) TWTML_HIP_CHECK(hipEventRecord(iter_events_[size_t(i - 1)], s));
       if (world > 1) {
         launch_sgd_reduce(sgd_, sp, s);
         comm_->allreduce(sgd_.g64, size_t(ns + 1), ncclFloat64, ncclSum, s);
@@ -365,6 +386,23 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
     }
     launch_sgd_finish(sgd_, sp, s);
     launch_scatter_w(sgd_, prep_, s);
+    if (itime) {   // iteration-kernel phases (us): stop-check, lds init, chunks, hot reduce, scalars, slots
+      std::vector<uint64_t> tb(size_t(iters + 2) * 16);
+      TWTML_HIP_CHECK(hipMemcpyAsync(tb.data(), iter_tdbg_, tb.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+      TWTML_HIP_CHECK(hipStreamSynchronize(s));
+      for (int which = 0; which < 2; ++which) {
+        double acc[6] = {0, 0, 0, 0, 0, 0};
+        int n = 0;
+        for (int i = 2; i <= iters; ++i) {
+          const uint64_t* t = tb.data() + (size_t(i) * 2 + size_t(which)) * 8;
+          if (t[6] == 0) continue;
+          for (int k = 0; k < 6; ++k) acc[k] += double(t[k + 1] - t[k]) * 0.01;
+          ++n;
+        }
+        if (n) std::fprintf(stderr, "iter timing wg %s (us, %d iters): stop %.2f init %.2f chunks %.2f hotred %.2f scalars %.2f slots %.2f\n",
+                            which ? "last" : "0", n, acc[0] / n, acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n);
+      }
+    }
   }
   TWTML_HIP_CHECK(hipEventRecord(ev_[2], s));
   if (world > 1) comm_->allreduce(sgd_.stats, 6, ncclFloat64, ncclSum, s);

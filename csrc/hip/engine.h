@@ -106,6 +106,7 @@ class LREngine {
   void ensure_part(int64_t n);
   void ensure_coh(int grid, int64_t ns);
   static bool persist_enabled();
+  double wait_flag(int j);
 
   int device_;
   LRConfig cfg_;
@@ -120,6 +121,7 @@ class LREngine {
   int64_t coh_part_cap_ = 0, coh_ns_cap_ = 0;
   int coh_grid_cap_ = 0;
   uint64_t* gd_tdbg_ = nullptr;
+  uint64_t* iter_tdbg_ = nullptr;
   uint8_t* lower_page_ = nullptr;
   uint16_t* lower_blocks_ = nullptr;
   int64_t* host_counters_ = nullptr;  // pinned [8]

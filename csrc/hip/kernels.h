@@ -140,6 +140,7 @@ struct DevSgd {
   double* host_flags;   // [max_iters+1] pinned host memory: done flag after each update
   double* part;         // [nparts][pstride] per-workgroup partial gradients (LDS paths)
   double* itrec;        // [max_iters+2][kRecStride] per-iteration update records
+  uint64_t* tdbg;       // optional phase stamps (TWTML_ITER_TIMING): [iter][wg 0 / last][8]
   int64_t F;
   int64_t ns;           // 4 + n_unique + pads (rounded)
   int64_t n_unique;

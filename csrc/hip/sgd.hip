@@ -166,13 +166,18 @@ constexpr int kPartVals = 12;
 template <bool STATS, bool SAMPLE>
 __device__ __forceinline__ void part_scalars(const DevSgd& d, const RowAcc& acc,
                                              double (*wsc)[kPartVals], double* prow) {
-  double v[kPartVals] = {double(acc.gn0), double(acc.gn1), double(acc.gn2), double(acc.gn3),
-                         0.5 * double(acc.loss), acc.msum, acc.st[0], acc.st[1], acc.st[2],
+  double v[kPartVals] = {0.0, 0.0, 0.0, 0.0, 0.0, acc.msum, acc.st[0], acc.st[1], acc.st[2],
                          acc.st[3], acc.st[4], acc.st[5]};
   constexpr int nv = STATS ? kPartVals : (SAMPLE ? 6 : 5);
   const int w = threadIdx.x / kWave;
+  // the per-lane fp32 partials reduce on the VALU (DPP); fp64 from here on
+  v[0] = double(wave_sum_f32(acc.gn0));
+  v[1] = double(wave_sum_f32(acc.gn1));
+  v[2] = double(wave_sum_f32(acc.gn2));
+  v[3] = double(wave_sum_f32(acc.gn3));
+  v[4] = 0.5 * double(wave_sum_f32(acc.loss));
 #pragma unroll
-  for (int k = 0; k < nv; ++k) v[k] = wave_sum(v[k]);
+  for (int k = 5; k < nv; ++k) v[k] = wave_sum(v[k]);
   if (lane_id() == 0) {
 #pragma unroll
     for (int k = 0; k < nv; ++k) wsc[w][k] = v[k];
@@ -240,21 +245,23 @@ __device__ bool sgd_converged_wave(const DevSgd& d, int it, double tol) {
 
 // Iteration-kernel prologue: true when the batch is finished (the caller
 // returns).  Called by every thread; `flag` is a workgroup-shared int.
+// Also publishes the verdict for update i-1 to the host (zero-copy pinned
+// memory, initialised to -1 by the host): the host polls it to stop
+// enqueueing iterations, without a per-iteration event in the stream.
 __device__ bool sgd_stop(const DevSgd& d, const SgdParams& sp, int* flag) {
   if (threadIdx.x < kWave) {
-    bool stop = d.state[0] != 0.0;
-    if (!stop && sp.iteration > 1) {
+    const bool done = d.state[0] != 0.0;
+    bool stop = done;
+    if (!done && sp.iteration > 1) {
       stop = sgd_converged_wave(d, sp.iteration - 1, sp.tol);
-      if (blockIdx.x == 0 && threadIdx.x == 0) {
-        if (stop) {
-          d.state[0] = 1.0;
-          d.state[1] = 1.0;
-        }
-        if (d.host_flags) {           // zero-copy early-stop signal to the host
-          d.host_flags[sp.iteration - 1] = stop ? 1.0 : 0.0;
-          __threadfence_system();
-        }
+      if (stop && blockIdx.x == 0 && threadIdx.x == 0) {
+        d.state[0] = 1.0;
+        d.state[1] = 1.0;
       }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0 && d.host_flags && sp.iteration > 1) {
+      __hip_atomic_store(&d.host_flags[sp.iteration - 1], stop ? 1.0 : 0.0, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
     }
     if (threadIdx.x == 0) *flag = stop ? 1 : 0;
   }
@@ -402,6 +409,7 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_lds(DevSgd d, DevPrepar
 // fixed-point gradient.  Chunks left
 // in the plain layout (clen8c < 0) take the plain route.
 // ---------------------------------------------------------------------------
+constexpr int kHotRows = kWave / 16;  // 16-lane rows per wave (hot-gradient partials per wave)
 constexpr int kMaxColdGroups = 4;   // cold groups kept in VGPRs (cold row <= 128)
 constexpr int kHotPerLane = kHot / kLanesPerRow;   // 32
 
@@ -409,45 +417,109 @@ constexpr int kHotPerLane = kHot / kLanesPerRow;   // 32
 // floats so the four quarters' b128 reads hit different banks)
 constexpr int kHotLdsStride = kHotPerLane + 4;
 
-__device__ __forceinline__ float hot_dot(const uint4 hv, const float* wq) {
+// Hot weights as 4 signed base-128 digits of a 28-bit fixed-point value
+// (w ~= S * 2^-27 * (d0 2^21 + d1 2^14 + d2 2^7 + d3), S = max |w_hot| of
+// the pass): the forward dot of a lane's 32 hot counts is 32
+// v_dot4_i32_iu8 (4 counts x 4 digits each, exact int32), not 96 VALU ops
+// of extract / convert / fma.  Quantisation error <= S * 2^-28 per weight.
+// LDS per lane quarter t (kHotLdsStride dwords): dword (d*4 + q)*2 + half
+// packs digit d of the 4 hot ids held in the even (half 0) / odd (half 1)
+// nibbles of the lane's count dword q; dwords 32..35 hold the 4 digit scales.
+// (Counts 0..15 are valid signed bytes, so the signed v_dot4_i32_i8 serves.)
+__device__ __forceinline__ void nib_split(uint32_t x, uint32_t& lo, uint32_t& hi) {
+  lo = x & 0x0F0F0F0Fu;           // nibbles 0,2,4,6 -> bytes 0..3
+  hi = (x >> 4) & 0x0F0F0F0Fu;    // nibbles 1,3,5,7 -> bytes 0..3
+}
+
+__device__ __forceinline__ float hot_dot(const uint4 hv, const uint32_t* wq) {
   const uint32_t hw[4] = {hv.x, hv.y, hv.z, hv.w};
-  float a = 0.f, b = 0.f;
+  int acc[4] = {0, 0, 0, 0};
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const float4 lo = reinterpret_cast<const float4*>(wq)[2 * q];
-    const float4 hi = reinterpret_cast<const float4*>(wq)[2 * q + 1];
-    const float wv[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  for (int d = 0; d < 4; ++d) {
+    const uint4 a = reinterpret_cast<const uint4*>(wq)[2 * d];       // q 0,1
+    const uint4 b = reinterpret_cast<const uint4*>(wq)[2 * d + 1];   // q 2,3
+    const uint32_t dg[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 #pragma unroll
-    for (int k = 0; k < 8; k += 2) {
-      a += float((hw[q] >> (4 * k)) & 15u) * wv[k];
-      b += float((hw[q] >> (4 * k + 4)) & 15u) * wv[k + 1];
+    for (int q = 0; q < 4; ++q) {
+      uint32_t lo, hi;
+      nib_split(hw[q], lo, hi);
+      acc[d] = __builtin_amdgcn_sdot4(int(lo), int(dg[2 * q]), acc[d], false);
+      acc[d] = __builtin_amdgcn_sdot4(int(hi), int(dg[2 * q + 1]), acc[d], false);
     }
   }
-  return a + b;
+  const float4 sc = reinterpret_cast<const float4*>(wq)[8];
+  return float(acc[0]) * sc.x + float(acc[1]) * sc.y + float(acc[2]) * sc.z + float(acc[3]) * sc.w;
 }
 
-__device__ __forceinline__ void hot_grad(const uint4 hv, float res, float (&gh)[kHotPerLane]) {
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// gh[j] accumulates hot ids (2j, 2j+1) of the lane's quarter: counts convert
+// straight from bytes (v_cvt_f32_ubyteN) and pairs update with v_pk_fma_f32.
+__device__ __forceinline__ void hot_grad(const uint4 hv, float res, f32x2 (&gh)[kHotPerLane / 2]) {
   const uint32_t hw[4] = {hv.x, hv.y, hv.z, hv.w};
+  const f32x2 r2 = {res, res};
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
+  for (int q = 0; q < 4; ++q) {
+    uint32_t lo, hi;
+    nib_split(hw[q], lo, hi);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) gh[8 * q + k] += res * float((hw[q] >> (4 * k)) & 15u);
+    for (int i = 0; i < 4; ++i) {
+      const f32x2 c = {float((lo >> (8 * i)) & 0xFFu), float((hi >> (8 * i)) & 0xFFu)};
+      gh[4 * q + i] = __builtin_elementwise_fma(c, r2, gh[4 * q + i]);
+    }
+  }
 }
 
-// One pass of the hybrid gradient over this workgroup's chunks (LDS already
-// holds the weights wl / hot weights whl and a zeroed gradient gl); ends by
-// writing the workgroup's partial row prow (includes block barriers).
+// Build the digit table of the pass from the LDS weights (one wave; the
+// caller synchronises).  Hot id h: quarter t = h / 32, count dword
+// q = (h % 32) / 8, nibble k = h % 8 -> half = k & 1, byte i = k >> 1.
+__device__ __forceinline__ void hot_digits(const DevPrepared& p, const float* wl, uint32_t* whl) {
+  const int lane = lane_id();
+  const float wa = wl[p.hot_slot[lane]], wb = wl[p.hot_slot[lane + kWave]];
+  float S = fmaxf(fabsf(wa), fabsf(wb));
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) S = fmaxf(S, __shfl_xor(S, off, kWave));
+  const float inv = S > 0.f ? 134217728.0f / S : 0.f;   // 2^27 / S
+  uint8_t* bytes = reinterpret_cast<uint8_t*>(whl);
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int h = lane + u * kWave;
+    int32_t W = int32_t(rintf((u ? wb : wa) * inv));
+    int32_t dg[4];
+#pragma unroll
+    for (int d = 3; d > 0; --d) {   // balanced base-128 digits, least significant first
+      const int32_t x = ((W + 64) & 127) - 64;
+      dg[d] = x;
+      W = (W - x) >> 7;
+    }
+    dg[0] = W;                       // |W| <= 2^27 -> |d0| <= 64
+    const int t = h / 32, q = (h % 32) / 8, k = h % 8;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      bytes[(t * kHotLdsStride + (d * 4 + q) * 2 + (k & 1)) * 4 + (k >> 1)] = uint8_t(int8_t(dg[d]));
+  }
+  if (lane < kLanesPerRow) {
+    float* sc = reinterpret_cast<float*>(whl + lane * kHotLdsStride + 32);
+    const float s0 = S * (1.0f / 64.0f);   // S * 2^-27 * 2^21
+    sc[0] = s0;
+    sc[1] = s0 * (1.0f / 128.0f);
+    sc[2] = s0 * (1.0f / 16384.0f);
+    sc[3] = s0 * (1.0f / 2097152.0f);
+  }
+}
+
 template <bool STATS, bool SAMPLE, int REP>
 __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, const SgdParams& sp,
-                                         const float* wl, unsigned long long* gl, const float* whl,
-                                         float (*hsum)[kHot], double (*wsc)[kPartVals], double* prow) {
+                                         const float* wl, unsigned long long* gl, const uint32_t* whl,
+                                         float (*hsum)[kHot], double (*wsc)[kPartVals], double* prow,
+                                         uint64_t* tst = nullptr) {
   const int64_t ns = d.ns;
   const int lane = lane_id();
   const int w = __builtin_amdgcn_readfirstlane(int(threadIdx.x) / kWave);   // wave-uniform
   const int r = lane / kLanesPerRow, t = lane % kLanesPerRow;
   const int rep = lane % REP;
   const int64_t n_kept = p.counters[0];
-  const int64_t nch = sp.ablate == 7 ? 0 : (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;  // 7: fixed cost
+  const int64_t nch = sp.ablate % 10 == 7 ? 0 : (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;  // 7: fixed cost
   const int64_t wave = int64_t(blockIdx.x) * (kIterBlock / kWave) + w;
   const int64_t nwaves = int64_t(gridDim.x) * (kIterBlock / kWave);
   const uint16_t* slot = static_cast<const uint16_t*>(p.slot);
@@ -455,10 +527,10 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
   const int32_t* __restrict__ clen8c = p.clen8c;
   const int64_t* __restrict__ cbase = p.cbase;
   const float w0 = wl[0], w1 = wl[1], w2 = wl[2], w3 = wl[3];
-  const float* wq = whl + t * kHotLdsStride;
-  float gh[kHotPerLane];
+  const uint32_t* wq = whl + t * kHotLdsStride;
+  f32x2 gh[kHotPerLane / 2];
 #pragma unroll
-  for (int i = 0; i < kHotPerLane; ++i) gh[i] = 0.f;
+  for (int i = 0; i < kHotPerLane / 2; ++i) gh[i] = f32x2{0.f, 0.f};
   RowAcc acc;
   bool clamped = false;
 
@@ -469,11 +541,22 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
   int32_t md_l8 = 0;
   int64_t md_cb = 0;
   int k = 0;
-  for (int64_t c = wave; c < nch; c += nwaves, ++k) {
+  // chunk order: round robin over all waves, or (ablate >= 10, experiment)
+  // a contiguous block per workgroup interleaved over its waves
+  const bool blocked = sp.ablate >= 10;
+  const int abl = blocked ? sp.ablate - 10 : sp.ablate;
+  int64_t c0 = wave, cstep = nwaves, cend = nch;
+  if (blocked) {
+    const int64_t G = gridDim.x;
+    c0 = nch * int64_t(blockIdx.x) / G + w;
+    cend = nch * (int64_t(blockIdx.x) + 1) / G;
+    cstep = kIterBlock / kWave;
+  }
+  for (int64_t c = c0; c < cend; c += cstep, ++k) {
     if ((k & (kWave - 1)) == 0) {
-      const int64_t cc = c + int64_t(lane) * nwaves;
-      md_l8 = cc < nch ? clen8c[cc] : 0;
-      md_cb = cc < nch ? cbase[cc] : 0;
+      const int64_t cc = c + int64_t(lane) * cstep;
+      md_l8 = cc < cend ? clen8c[cc] : 0;
+      md_cb = cc < cend ? cbase[cc] : 0;
     }
     const int kl = k & (kWave - 1);
     const int32_t L8c = __builtin_amdgcn_readlane(md_l8, kl);
@@ -492,7 +575,7 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
         for (int g = 0; g < kMaxColdGroups; ++g)
           if (g < L8c) v[g] = *reinterpret_cast<const uint4*>(sl + int64_t(g) * kChunkStride);
       }
-      if (sp.ablate == 6) {  // loads only: memory floor of the chunk stream
+      if (abl == 6) {  // loads only: memory floor of the chunk stream
         uint32_t x = hv.x ^ hv.y ^ hv.z ^ hv.w ^ __float_as_uint(ri.y + ri.n0 + ri.n1 + ri.n2 + ri.n3);
         if (reg) {
 #pragma unroll
@@ -503,7 +586,7 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
         continue;
       }
       // ablate 4: no hot dot (counts still loaded)
-      float d0 = sp.ablate == 4 ? __uint_as_float(hv.x & 1u) : hot_dot(hv, wq), d1 = 0.f;
+      float d0 = abl == 4 ? __uint_as_float(hv.x & 1u) : hot_dot(hv, wq), d1 = 0.f;
       if (reg) {
 #pragma unroll
         for (int g = 0; g < kMaxColdGroups; ++g)
@@ -530,8 +613,8 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
         // floats live across the residual (register pressure)
         uint4 hg = hv;
         asm volatile("" : "+v"(hg.x), "+v"(hg.y), "+v"(hg.z), "+v"(hg.w));
-        if (sp.ablate != 1 && sp.ablate != 3) hot_grad(hg, res, gh);   // ablate 3: no hot grad
-        if (sp.ablate == 1 || sp.ablate == 5) continue;                 // 1/5: no cold scatter
+        if (abl != 1 && abl != 3) hot_grad(hg, res, gh);   // ablate 3: no hot grad
+        if (abl == 1 || abl == 5) continue;                 // 1/5: no cold scatter
         const unsigned long long q = to_fix(res, clamped, sp.fix_lim);
         if (reg) {
 #pragma unroll
@@ -576,18 +659,20 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
     }
   }
 
+  if (tst) tst[3] = __builtin_amdgcn_s_memrealtime();
   if (__any(clamped) && lane == 0) d.state[7] = 1.0;
   // hot gradient: sum the 16 lanes of each quarter t (per wave), into LDS
+  // per 16-lane row (DPP), the four row partials of each hot id go to LDS
+  // and the slot loop adds the 4 x 16 of them
+  float* hrow = hsum[w * kHotRows + lane / 16];
 #pragma unroll
   for (int i = 0; i < kHotPerLane; ++i) {
-    float v = gh[i];
-    v += __shfl_xor(v, 4, kWave);
-    v += __shfl_xor(v, 8, kWave);
-    v += __shfl_xor(v, 16, kWave);
-    v += __shfl_xor(v, 32, kWave);
-    if (lane < kLanesPerRow) hsum[w][kHotPerLane * lane + i] = v;
+    const float v = row_sum_mod4((i & 1) ? gh[i >> 1].y : gh[i >> 1].x);
+    if ((lane & 15) < kLanesPerRow) hrow[kHotPerLane * (lane & 3) + i] = v;
   }
+  if (tst) tst[4] = __builtin_amdgcn_s_memrealtime();
   part_scalars<STATS, SAMPLE>(d, acc, wsc, prow);   // includes the block barrier
+  if (tst) tst[5] = __builtin_amdgcn_s_memrealtime();
   const int64_t hi = kNumNumeric + d.n_unique;      // pads are never flushed
   for (int64_t s = kNumNumeric + threadIdx.x; s < ns; s += kIterBlock) {
     double v = 0.0;
@@ -596,7 +681,7 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
       const uint32_t h = p.hot_of[s];
       if (h != 0xFFu) {
         double hv = 0.0;
-        for (int k = 0; k < kIterBlock / kWave; ++k) hv += double(hsum[k][h]);
+        for (int k = 0; k < kIterBlock / kWave * kHotRows; ++k) hv += double(hsum[k][h]);
         v += hv;
       }
     }
@@ -617,12 +702,11 @@ __device__ __forceinline__ T ld_coh(const T* ptr) {
 // Slots >= hi (pads) get weight 0 whatever wsrc holds there.
 template <int REP>
 __device__ __forceinline__ void hyb_lds_init(const DevPrepared& p, const float* wsrc, int64_t ns,
-                                             int64_t hi, float* wl, unsigned long long* gl, float* whl) {
+                                             int64_t hi, float* wl, unsigned long long* gl, uint32_t* whl) {
   for (int64_t s = threadIdx.x; s < ns; s += kIterBlock) wl[s] = s < hi ? ld_coh(wsrc + s) : 0.f;
   for (int64_t s = threadIdx.x; s < ns * REP; s += kIterBlock) gl[s] = 0ull;
   __syncthreads();
-  for (int h = threadIdx.x; h < kHot; h += kIterBlock)
-    whl[(h / kHotPerLane) * kHotLdsStride + h % kHotPerLane] = wl[p.hot_slot[h]];
+  if (threadIdx.x < kWave) hot_digits(p, wl, whl);
   __syncthreads();
 }
 
@@ -630,14 +714,21 @@ template <bool STATS, bool SAMPLE, int REP>
 __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_hyb(DevSgd d, DevPrepared p, SgdParams sp) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   __shared__ double wsc[kIterBlock / kWave][kPartVals];
-  __shared__ float hsum[kIterBlock / kWave][kHot];
-  __shared__ __attribute__((aligned(16))) float whl[kLanesPerRow * kHotLdsStride];
+  __shared__ float hsum[kIterBlock / kWave * kHotRows][kHot];
+  __shared__ __attribute__((aligned(16))) uint32_t whl[kLanesPerRow * kHotLdsStride];
   __shared__ int stop_flag;
+  uint64_t* tst = nullptr;
+  if (d.tdbg && threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1))
+    tst = d.tdbg + (int64_t(sp.iteration) * 2 + (blockIdx.x == 0 ? 0 : 1)) * 8;
+  if (tst) tst[0] = __builtin_amdgcn_s_memrealtime();
   if (sgd_stop(d, sp, &stop_flag)) return;
+  if (tst) tst[1] = __builtin_amdgcn_s_memrealtime();
   float* wl = lds;
   unsigned long long* gl = reinterpret_cast<unsigned long long*>(lds + d.ns);
   hyb_lds_init<REP>(p, d.wc32, d.ns, kNumNumeric + d.n_unique, wl, gl, whl);
-  hyb_pass<STATS, SAMPLE, REP>(d, p, sp, wl, gl, whl, hsum, wsc, d.part + int64_t(blockIdx.x) * d.pstride);
+  if (tst) tst[2] = __builtin_amdgcn_s_memrealtime();
+  hyb_pass<STATS, SAMPLE, REP>(d, p, sp, wl, gl, whl, hsum, wsc, d.part + int64_t(blockIdx.x) * d.pstride, tst);
+  if (tst) tst[6] = __builtin_amdgcn_s_memrealtime();
 }
 
 // ---------------------------------------------------------------------------
@@ -693,8 +784,8 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_gd_hyb(DevSgd d, DevPrepared
                                                            DevCoh coh, int it_first) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   __shared__ double wsc[kIterBlock / kWave][kPartVals];
-  __shared__ float hsum[kIterBlock / kWave][kHot];
-  __shared__ __attribute__((aligned(16))) float whl[kLanesPerRow * kHotLdsStride];
+  __shared__ float hsum[kIterBlock / kWave * kHotRows][kHot];
+  __shared__ __attribute__((aligned(16))) uint32_t whl[kLanesPerRow * kHotLdsStride];
   __shared__ double red[kIterBlock / kWave][2];
   __shared__ int flag, conv_sh;
   const int64_t ns = d.ns, hi = kNumNumeric + d.n_unique;
