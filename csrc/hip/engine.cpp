@@ -365,9 +365,9 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
       }
     }
     const bool itime = std::getenv("TWTML_ITER_TIMING") != nullptr;
-    if (itime && !iter_tdbg_) iter_tdbg_ = dmalloc<uint64_t>(size_t(iters + 2) * 16);
+    if (itime && !iter_tdbg_) iter_tdbg_ = dmalloc<uint64_t>(4096 + size_t(iters + 2) * 32);
     sgd_.tdbg = itime ? iter_tdbg_ : nullptr;
-    if (itime) TWTML_HIP_CHECK(hipMemsetAsync(iter_tdbg_, 0, sizeof(uint64_t) * size_t(iters + 2) * 16, s));
+    if (itime) TWTML_HIP_CHECK(hipMemsetAsync(iter_tdbg_, 0, sizeof(uint64_t) * (4096 + size_t(iters + 2) * 32), s));
     for (int i = 1; pgrid == 0 && i <= iters; ++i) {
       if (i > depth) {
         const int j = i - depth;                       // verdict after update j
@@ -387,7 +387,7 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
     launch_sgd_finish(sgd_, sp, s);
     launch_scatter_w(sgd_, prep_, s);
     if (itime) {   // iteration-kernel phases (us): stop-check, lds init, chunks, hot reduce, scalars, slots
-      std::vector<uint64_t> tb(size_t(iters + 2) * 16);
+      std::vector<uint64_t> tb(4096 + size_t(iters + 2) * 32);
       TWTML_HIP_CHECK(hipMemcpyAsync(tb.data(), iter_tdbg_, tb.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
       TWTML_HIP_CHECK(hipStreamSynchronize(s));
       for (int which = 0; which < 2; ++which) {
@@ -401,6 +401,15 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
         }
         if (n) std::fprintf(stderr, "iter timing wg %s (us, %d iters): stop %.2f init %.2f chunks %.2f hotred %.2f scalars %.2f slots %.2f\n",
                             which ? "last" : "0", n, acc[0] / n, acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n);
+      }
+      {   // wave end spread inside WG 0, iteration 10
+        const int i = std::min(10, iters);
+        const uint64_t* t0 = tb.data() + (size_t(i) * 2) * 8;
+        const uint64_t* we = tb.data() + 4096 + size_t(i) * 32;
+        std::fprintf(stderr, "wave ends (us after kernel start) / chunks, WG 0 it %d:", i);
+        for (int w = 0; w < 16; ++w)
+          std::fprintf(stderr, " %.1f/%d", double(we[2 * w] - t0[0]) * 0.01, int(we[2 * w + 1]));
+        std::fprintf(stderr, "\n");
       }
     }
   }

@@ -660,6 +660,11 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
   }
 
   if (tst) tst[3] = __builtin_amdgcn_s_memrealtime();
+  if (d.tdbg && blockIdx.x == 0 && lane == 0) {   // per-wave end of the chunk loop (WG 0)
+    uint64_t* we = d.tdbg + 4096 + int64_t(sp.iteration) * 32 + w * 2;
+    we[0] = __builtin_amdgcn_s_memrealtime();
+    we[1] = uint64_t(k);
+  }
   if (__any(clamped) && lane == 0) d.state[7] = 1.0;
   // hot gradient: sum the 16 lanes of each quarter t (per wave), into LDS
   // per 16-lane row (DPP), the four row partials of each hot id go to LDS
