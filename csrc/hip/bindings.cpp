@@ -63,6 +63,7 @@ static py::dict result_dict(BatchResult& r) {
 
 PYBIND11_MODULE(_twtml_hip, m) {
   m.doc() = "twtml MI355X engine: HIP/CDNA4 kernels, micro-batch engines, RCCL";
+  m.attr("RAW_SLOTS") = kRawSlots;   // device raw-batch slots per engine (submit/process)
 
   m.def("device_count", []() {
     int n = 0;

@@ -1,13 +1,13 @@
 // MI355X micro-batch engine for StreamingLinearRegressionWithSGD.
 //
 // One engine per process/GPU.  A micro-batch flows:
-//   pinned host RawBatch --(copy stream, async H2D)--> device slot (x2)
+//   pinned host RawBatch --(copy stream, async H2D)--> device slot (x3)
 //   compute stream: filter -> length sort -> featurize -> [RCCL max of the
 //   active-feature flags] -> compact -> remap -> gather w ->
 //   numIterations x ( fused predict/gradient kernel -> [RCCL all-reduce of
 //   the packed gradient] -> fp64 update + convergence ) -> scatter w
-// Two device slots let batch t+1's H2D overlap batch t's training (SURVEY
-// §2.4 "Ingest || compute pipelining").  Output op #1 (prequential stats)
+// Three device slots let the H2D of batches t+1 and t+2 overlap batch t's
+// training (SURVEY §2.4 "Ingest || compute pipelining").  Output op #1 (prequential stats)
 // is fused into iteration 1, so it sees the weights before training on the
 // batch (LinearRegression.scala:53-86 ordering).
 #pragma once

@@ -15,7 +15,7 @@ static T* slot_alloc(size_t n) {
 }
 
 int RawSlots::check(int slot) {
-  if (slot < 0 || slot > 1) throw std::invalid_argument("slot must be 0 or 1");
+  if (slot < 0 || slot >= kRawSlots) throw std::invalid_argument("slot must be in [0, kRawSlots)");
   return slot;
 }
 

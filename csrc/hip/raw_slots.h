@@ -1,9 +1,13 @@
-// Double-buffered device copies of raw wire-format batches (csrc/host/wire.h).
+// Triple-buffered device copies of raw wire-format batches (csrc/host/wire.h).
 //
 // submit() enqueues the H2D of a pinned HostBatch on the copy stream into one
-// of two slots; the compute stream waits on that slot's h2d event and
+// of kRawSlots slots; the compute stream waits on that slot's h2d event and
 // records `consumed` once its kernels no longer read the raw bytes, so the
-// next H2D into the slot overlaps the rest of the batch's compute.
+// next H2D into the slot overlaps the rest of the batch's compute.  With three
+// slots the host can keep two batches queued ahead of the one being trained,
+// so the PCIe copy engine never idles while the host waits for a batch's
+// results (double buffering only starts batch t+1's copy once batch t-1 has
+// returned to the host).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -14,6 +18,8 @@
 namespace twtml {
 
 struct HostBatch;
+
+constexpr int kRawSlots = 3;
 
 class RawSlots {
  public:
@@ -46,7 +52,7 @@ class RawSlots {
     int64_t n = 0, bytes = 0;
     hipEvent_t h2d_done = nullptr, consumed = nullptr;
     bool used = false;
-  } slots_[2];
+  } slots_[kRawSlots];
   int64_t max_rows_ = 0, max_bytes_ = 0;
 };
 

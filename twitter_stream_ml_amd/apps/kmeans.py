@@ -187,6 +187,8 @@ def main(argv: Optional[List[str]] = None) -> int:
             session = SessionStats(lgn_host, web_host).open()
     job = KMeansJob(engine, args.textDims, session, info.rank, args, resume)
     stream.foreachRDD(job.on_batch)
+    if hasattr(engine, "prefetch"):   # device engine: H2D of queued batches overlaps training
+        ssc.add_prefetch(engine.prefetch)
     log.info("Initialization complete.")
     ssc.start()
     failed = False

@@ -209,6 +209,8 @@ def main(argv: Optional[List[str]] = None) -> int:
                               MetricsLogger(os.environ.get("TWTML_METRICS")), resume, world)
     log.info("Initializing prediction model...")
     stream.foreachRDD(job.on_batch)   # op #1 (stats) + op #2 (trainOn), prequential order
+    if hasattr(engine, "prefetch"):   # device engine: H2D of queued batches overlaps training
+        ssc.add_prefetch(engine.prefetch)
     ssc.start()
     log.info("Initialization complete.")
     failed = False

@@ -26,6 +26,7 @@ import numpy as np
 from ..oracle.mllib import KMeansState, decay_factor_from_half_life
 from ..records.batch import RawBatch
 from ._native import hip
+from .ingest import SlotPipeline
 from .lr_engine import HostBatchView
 
 __all__ = ["KMDeviceConfig", "DeviceKMeans"]
@@ -74,6 +75,9 @@ class DeviceKMeans:
         st = KMeansState.random(cfg.k, self.dim, cfg.init_weight, cfg.seed)
         self.set_state(st.centers, st.weights)
         self._staging: List[HostBatchView] = []
+        self.raw_slots = int(hip().RAW_SLOTS)
+        self._pipe = SlotPipeline(self.raw_slots, lambda s, raw: self.staging(s).load(raw),
+                                  self.submit, self.synchronize)
 
     # ---- model state (latestModel.clusterCenters / clusterWeights) -------
     def get_state(self):
@@ -112,11 +116,13 @@ class DeviceKMeans:
             r["pred"] = np.zeros(0, np.int32)
         return r
 
-    def update_raw(self, raw: RawBatch, want_pred: bool = True, slot: int = 0) -> Dict[str, object]:
-        """Synchronous path used by the KMeans driver: stage, H2D, process."""
-        hb = self.staging(slot).load(raw)
-        self.submit(hb, slot)
-        return self.process(slot, want_pred)
+    def prefetch(self, raw: RawBatch) -> bool:
+        """Stage + async H2D of a queued future batch (overlaps the current one)."""
+        return self._pipe.prefetch(raw)
+
+    def update_raw(self, raw: RawBatch, want_pred: bool = True) -> Dict[str, object]:
+        """One micro-batch: uses its prefetched slot, else stages + H2D now."""
+        return self.process(self._pipe.take(raw), want_pred)
 
     def synchronize(self) -> None:
         self._eng.synchronize()

@@ -22,6 +22,7 @@ import numpy as np
 
 from ..records.batch import RETWEET_COUNT, RawBatch
 from ._native import hip, host
+from .ingest import SlotPipeline
 
 __all__ = ["LRDeviceConfig", "DeviceLinearRegression", "prelower", "HostBatchView"]
 
@@ -134,6 +135,9 @@ class DeviceLinearRegression:
         self.comm = comm
         self._eng = hip().LREngine(self.device, cfg.as_dict(), comm)
         self._staging: List[HostBatchView] = []
+        self.raw_slots = int(hip().RAW_SLOTS)
+        self._pipe = SlotPipeline(self.raw_slots, lambda s, raw: self.staging(s).load(raw),
+                                  self.submit, self.synchronize)
 
     # ---- weights (MLlib setInitialWeights / latestModel.weights) ---------
     @property
@@ -161,11 +165,13 @@ class DeviceLinearRegression:
     def process(self, slot: int, now_ms: int, want_pred: bool = False) -> Dict[str, object]:
         return self._eng.process(int(slot), int(now_ms), bool(want_pred))
 
-    def train_batch(self, raw: RawBatch, want_pred: bool = True, slot: int = 0) -> Dict[str, object]:
-        """Synchronous convenience path: stage, H2D, process."""
-        hb = self.staging(slot).load(raw)
-        self.submit(hb, slot)
-        return self.process(slot, raw.batch_time_ms, want_pred)
+    def prefetch(self, raw: RawBatch) -> bool:
+        """Stage + async H2D of a queued future batch (overlaps the current one)."""
+        return self._pipe.prefetch(raw)
+
+    def train_batch(self, raw: RawBatch, want_pred: bool = True) -> Dict[str, object]:
+        """Train on one micro-batch: uses its prefetched slot, else stages + H2D now."""
+        return self.process(self._pipe.take(raw), raw.batch_time_ms, want_pred)
 
     def synchronize(self) -> None:
         self._eng.synchronize()

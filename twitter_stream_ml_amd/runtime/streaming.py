@@ -12,6 +12,10 @@ Semantics kept from Spark Streaming 1.6:
   ``foreachRDD(predict+stats)`` registered before ``model.trainOn(stream)``
   sees the model of batch t-1 and training then consumes batch t
   (prequential test-then-train, ``LinearRegression.scala:53-86``);
+* ingest overlaps compute: before a batch's output ops run, the sealed
+  batches queued behind it are handed to the registered prefetch hooks
+  (``add_prefetch``; a device engine stages them and starts their H2D on a
+  side stream), the receiver-on-its-own-core overlap of the reference;
 * batches that take longer than the interval queue up (scheduling delay);
   with ``max_pending`` the receiver stops pulling while that many sealed
   batches wait (backpressure, ``spark.streaming.backpressure.enabled``).
@@ -182,6 +186,8 @@ class StreamingContext:
         self.batch_infos: List[BatchInfo] = []
         self.error: Optional[BaseException] = None
         self.on_batch_completed: List[Callable[[BatchInfo], None]] = []
+        self._prefetch: List[Callable[[RawBatch], Any]] = []
+        self.prefetch_depth = 2
 
     # ---- graph construction --------------------------------------------------
     def receiverStream(self, source) -> ReceiverDStream:
@@ -196,6 +202,21 @@ class StreamingContext:
 
     def _register(self, stream: DStream, fn: Callable[..., Any], with_time: bool) -> None:
         self._outputs.append((stream, fn, with_time))
+
+    def add_prefetch(self, fn: Callable[[RawBatch], Any]) -> None:
+        """Register ``fn(batch)``, called for sealed batches still queued behind
+        the one about to run (at most ``prefetch_depth``, oldest first; a batch
+        may be offered more than once, hooks must be idempotent)."""
+        self._prefetch.append(fn)
+
+    def _prefetch_upcoming(self) -> None:
+        if not self._prefetch or self.prefetch_depth <= 0:
+            return
+        with self._jobs.mutex:
+            upcoming = [it[0] for it in list(self._jobs.queue)[:self.prefetch_depth] if it is not None]
+        for b in upcoming:
+            for fn in self._prefetch:
+                fn(b)
 
     # ---- execution -----------------------------------------------------------
     def run_batch(self, batch: RawBatch, info: Optional[BatchInfo] = None) -> BatchInfo:
@@ -289,6 +310,7 @@ class StreamingContext:
                 if item is None:
                     break
                 batch, info = item
+                self._prefetch_upcoming()
                 self.run_batch(batch, info)
                 if self.num_batches and self.batches_done >= self.num_batches:
                     self._stop.set()
