@@ -118,6 +118,19 @@ PYBIND11_MODULE(_twtml_hip, m) {
       .def_property_readonly("scalars_flat", [](py::object self) {
         auto& h = self.cast<HostBatch&>();
         return view<int64_t>(h.scalars, {py::ssize_t(5 * h.max_rows)}, self);
+      })
+      .def("pack_scalars", [](HostBatch& h, int64_t n) {
+        py::gil_scoped_release nogil;
+        h.pack_scalars(n);
+      }, py::arg("n"))
+      .def_property_readonly("scalar_wire", [](const HostBatch& h) {
+        py::dict d;   // wire encoding of the last pack_scalars (tests / diagnostics)
+        std::vector<int64_t> off(h.soff, h.soff + kScalarCols + 1), base(h.sbase, h.sbase + kScalarCols);
+        d["offsets"] = off;
+        d["base"] = base;
+        d["wide_mask"] = h.swide;
+        d["rows"] = h.spacked_n;
+        return d;
       });
 
   py::class_<LREngine, std::shared_ptr<LREngine>>(m, "LREngine")

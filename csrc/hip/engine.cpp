@@ -20,14 +20,53 @@ HostBatch::HostBatch(int64_t rows, int64_t text_bytes) : max_rows(rows), max_byt
   const size_t o = up(sizeof(int64_t) * size_t(rows + 1));
   const size_t r = up(size_t(rows));
   const size_t sc = up(sizeof(int64_t) * 5 * size_t(rows));
-  bytes = t + o + r + sc;
+  bytes = t + o + r + 2 * sc;
   TWTML_HIP_CHECK(hipHostMalloc(&base, bytes, hipHostMallocDefault));
   char* p = static_cast<char*>(base);
   text = reinterpret_cast<uint8_t*>(p);
   offsets = reinterpret_cast<int64_t*>(p + t);
   flags = reinterpret_cast<uint8_t*>(p + t + o);
   scalars = reinterpret_cast<int64_t*>(p + t + o + r);
+  spack = reinterpret_cast<uint8_t*>(p + t + o + r + sc);
   offsets[0] = 0;
+}
+
+void HostBatch::pack_scalars(int64_t n) {
+  if (n < 0 || n > max_rows) throw std::invalid_argument("pack_scalars: bad row count");
+  int64_t lo[kScalarCols], hi[kScalarCols];
+  auto range = [&](int c) {
+    const int64_t* v = scalars + int64_t(c) * n;
+    int64_t a = n ? v[0] : 0, b = a;
+    for (int64_t i = 1; i < n; ++i) { a = std::min(a, v[i]); b = std::max(b, v[i]); }
+    lo[c] = a;
+    hi[c] = b;
+  };
+  std::vector<std::thread> th;
+  for (int c = 0; c < kScalarCols; ++c) th.emplace_back(range, c);
+  for (auto& x : th) x.join();
+  th.clear();
+  swide = 0;
+  soff[0] = 0;
+  for (int c = 0; c < kScalarCols; ++c) {
+    // range test in unsigned arithmetic (hi - lo may overflow int64)
+    const bool narrow = uint64_t(hi[c]) - uint64_t(lo[c]) <= uint64_t(UINT32_MAX);
+    if (!narrow) swide |= 1 << c;
+    sbase[c] = narrow ? lo[c] : 0;
+    soff[c + 1] = soff[c] + (narrow ? 4 : 8) * n;
+  }
+  auto put = [&](int c) {
+    const int64_t* v = scalars + int64_t(c) * n;
+    if (swide & (1 << c)) {
+      std::memcpy(spack + soff[c], v, sizeof(int64_t) * size_t(n));
+    } else {
+      uint32_t* o = reinterpret_cast<uint32_t*>(spack + soff[c]);
+      const uint64_t b = uint64_t(sbase[c]);
+      for (int64_t i = 0; i < n; ++i) o[i] = uint32_t(uint64_t(v[i]) - b);
+    }
+  };
+  for (int c = 0; c < kScalarCols; ++c) th.emplace_back(put, c);
+  for (auto& x : th) x.join();
+  spacked_n = n;
 }
 
 HostBatch::~HostBatch() {

@@ -44,7 +44,8 @@ struct LRConfig {
 
 // Pinned staging buffer of one raw batch in the wire format
 // (csrc/host/wire.h): narrow/wide rows in `text`, byte offsets, per-row
-// flags (bit0 isRetweet, bit1 wide), scalars packed [5][n].
+// flags (bit0 isRetweet, bit1 wide), scalars [5][n] int64 (the record
+// values), and their wire encoding (`spack`, see DevRawBatch in kernels.h).
 struct HostBatch {
   void* base = nullptr;
   size_t bytes = 0;
@@ -52,9 +53,16 @@ struct HostBatch {
   int64_t* offsets = nullptr;
   uint8_t* flags = nullptr;
   int64_t* scalars = nullptr;
+  uint8_t* spack = nullptr;            // packed columns, column c at soff[c]
+  int64_t soff[kScalarCols + 1] = {};  // byte offsets; soff[c+1]-soff[c] = 4n or 8n
+  int64_t sbase[kScalarCols] = {};
+  int32_t swide = 0;                   // bit c: column c is int64 on the wire
+  int64_t spacked_n = -1;              // rows of the last pack_scalars (-1: none)
   int64_t max_rows = 0, max_bytes = 0;
   HostBatch(int64_t rows, int64_t text_bytes);
   ~HostBatch();
+  // Encode scalars[:, :n] into spack (one thread per column).
+  void pack_scalars(int64_t n);
 };
 
 // bytes of device text buffer for `units` UTF-16 units (all rows wide)

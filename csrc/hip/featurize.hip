@@ -125,7 +125,7 @@ __device__ __forceinline__ bool keep_row(const DevRawBatch& b, int64_t r, const 
   if (r >= b.n) return false;
   if (fp.require_retweet && !(b.flags[r] & kRowRetweet)) return false;
   if (fp.range_filter) {
-    const int64_t rc = b.scalars[r];
+    const int64_t rc = raw_scalar(b, 0, r);
     if (rc < fp.begin || rc > fp.end) return false;
   }
   return true;
@@ -397,11 +397,10 @@ __device__ __forceinline__ void row_scalars(const DevRawBatch& b, const DevPrepa
                                             int64_t row, int32_t kidx) {
   const int64_t cap = p.cap_rows16;
   if (valid) {
-    const int64_t* sc = b.scalars;
-    p.y[pos] = float(sc[row]);
-    const double fol = double(sc[1 * b.n + row]), fav = double(sc[2 * b.n + row]);
-    const double fri = double(sc[3 * b.n + row]);
-    const double age = double(fp.now_ms - sc[4 * b.n + row]);
+    p.y[pos] = float(raw_scalar(b, 0, row));
+    const double fol = double(raw_scalar(b, 1, row)), fav = double(raw_scalar(b, 2, row));
+    const double fri = double(raw_scalar(b, 3, row));
+    const double age = double(fp.now_ms - raw_scalar(b, 4, row));
     p.num[0 * cap + pos] = float(fol * 1e-12);
     p.num[1 * cap + pos] = float(fav * 1e-12);
     p.num[2 * cap + pos] = float(fri * 1e-12);

@@ -19,14 +19,32 @@ namespace twtml {
 // ---------------------------------------------------------------------------
 // Raw batch on the device (one ingest slot).
 // Raw batch in the wire format (csrc/host/wire.h).
+//
+// Scalar columns (retweetCount, followers, favourites, friends, createdAt) are
+// int64 in the record; on the wire a column whose batch range fits 32 bits is
+// a u32 offset from a per-batch base (HostBatch::pack_scalars), halving their
+// PCIe bytes on real and synthetic streams (counts are small, createdAt spans
+// far less than 49 days within a batch); a column that does not fit ships as
+// int64.  Exact either way.
+constexpr int kScalarCols = 5;
+
 struct DevRawBatch {
   const uint8_t* text;      // [bytes] narrow (1 B/unit) or wide (UTF-16LE) rows
   const int64_t* offsets;   // [n+1] byte offsets
   const uint8_t* flags;     // [n] bit0 isRetweet, bit1 wide
-  const int64_t* scalars;   // [5][n]
+  const uint8_t* scol[kScalarCols];   // column c: u32[n] (+ sbase[c]) or int64[n]
+  int64_t sbase[kScalarCols];
+  int32_t swide;            // bit c: column c ships as int64
   int64_t n;                // rows in this batch (host-known)
   int64_t bytes;
 };
+
+// Scalar column c of raw row r (c is a compile-time constant at every call
+// site, so the width test is one scalar branch).
+__device__ __forceinline__ int64_t raw_scalar(const DevRawBatch& b, int c, int64_t r) {
+  if (b.swide & (1 << c)) return reinterpret_cast<const int64_t*>(b.scol[c])[r];
+  return b.sbase[c] + int64_t(reinterpret_cast<const uint32_t*>(b.scol[c])[r]);
+}
 
 constexpr uint8_t kRowRetweet = 1;
 constexpr uint8_t kRowWide = 2;

@@ -62,8 +62,8 @@ __global__ __launch_bounds__(kBlock) void k_km_features(DevRawBatch b, const int
       for (int j = lane; j < text_dims; j += kWave) xr[2 + j] = float(h[j]);
     }
     if (lane == 0) {
-      xr[0] = float(b.scalars[0 * b.n + row]);   // retweetCount
-      xr[1] = float(b.scalars[1 * b.n + row]);   // followersCount
+      xr[0] = float(raw_scalar(b, 0, row));   // retweetCount
+      xr[1] = float(raw_scalar(b, 1, row));   // followersCount
     }
     for (int j = 2 + text_dims + lane; j < dp; j += kWave) xr[j] = 0.f;
   }
@@ -93,8 +93,8 @@ __global__ __launch_bounds__(kBlock) void k_km_features_chunk(DevRawBatch b, con
     const int64_t mk = c * kRowsPerChunk + (lane & 15);
     const bool mvalid = mk < n_kept;
     const int64_t mrow = mvalid ? kept[mk] : 0;
-    const float mx0 = mvalid ? float(b.scalars[0 * b.n + mrow]) : 0.f;   // retweetCount
-    const float mx1 = mvalid ? float(b.scalars[1 * b.n + mrow]) : 0.f;   // followersCount
+    const float mx0 = mvalid ? float(raw_scalar(b, 0, mrow)) : 0.f;   // retweetCount
+    const float mx1 = mvalid ? float(raw_scalar(b, 1, mrow)) : 0.f;   // followersCount
     if (text_dims > 0) {
       const StageMeta meta = stage_meta(b, mvalid, mrow);
       for (int i = lane; i < kRowsPerChunk * text_dims; i += kWave) hist[i] = 0u;

@@ -54,6 +54,7 @@ void RawSlots::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, h
   if (bytes < 0 || bytes > max_bytes_ || bytes > hb.max_bytes)
     throw std::invalid_argument("text bytes exceed capacity");
   if (hb.offsets[0] != 0 || hb.offsets[n] != bytes) throw std::invalid_argument("offsets[n] != bytes");
+  if (n > 0 && hb.spacked_n != n) throw std::logic_error("HostBatch scalars not packed for this row count");
   // wait until the compute stream has finished reading this slot
   if (s.used) TWTML_HIP_CHECK(hipStreamWaitEvent(copy, s.consumed, 0));
   if (bytes > 0)
@@ -62,12 +63,17 @@ void RawSlots::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, h
                                  hipMemcpyHostToDevice, copy));
   if (n > 0) {
     TWTML_HIP_CHECK(hipMemcpyAsync(s.flags, hb.flags, size_t(n), hipMemcpyHostToDevice, copy));
-    // scalars are packed [5][n] at the start of the host buffer; consumers
-    // that read only the leading columns ship only those
-    TWTML_HIP_CHECK(hipMemcpyAsync(s.scalars, hb.scalars, sizeof(int64_t) * scalar_cols * size_t(n),
+    // wire-encoded columns are consecutive, so the leading scalar_cols of
+    // them are one contiguous copy
+    TWTML_HIP_CHECK(hipMemcpyAsync(s.scalars, hb.spack, size_t(hb.soff[scalar_cols]),
                                    hipMemcpyHostToDevice, copy));
   }
   TWTML_HIP_CHECK(hipEventRecord(s.h2d_done, copy));
+  for (int c = 0; c < kScalarCols; ++c) {
+    s.soff[c] = hb.soff[c];
+    s.sbase[c] = hb.sbase[c];
+  }
+  s.swide = hb.swide;
   s.n = n;
   s.bytes = bytes;
   s.used = true;
@@ -77,7 +83,19 @@ DevRawBatch RawSlots::acquire(int slot, hipStream_t compute) {
   Slot& s = slots_[check(slot)];
   if (!s.used) throw std::logic_error("process() on a slot that was never submitted");
   TWTML_HIP_CHECK(hipStreamWaitEvent(compute, s.h2d_done, 0));
-  return DevRawBatch{s.text, s.offsets, s.flags, s.scalars, s.n, s.bytes};
+  DevRawBatch b{};
+  b.text = s.text;
+  b.offsets = s.offsets;
+  b.flags = s.flags;
+  const uint8_t* sc = reinterpret_cast<const uint8_t*>(s.scalars);
+  for (int c = 0; c < kScalarCols; ++c) {
+    b.scol[c] = sc + s.soff[c];
+    b.sbase[c] = s.sbase[c];
+  }
+  b.swide = s.swide;
+  b.n = s.n;
+  b.bytes = s.bytes;
+  return b;
 }
 
 void RawSlots::release_slot(int slot, hipStream_t compute) {

@@ -31,7 +31,8 @@ class RawSlots {
   void init(int64_t max_rows, int64_t max_bytes);
   void release();
   // H2D of rows [0, n) / `bytes` text bytes of hb into `slot` on `copy`.
-  // scalar_cols: leading [5][n] scalar columns to copy (the rest stay stale)
+  // scalar_cols: leading scalar columns to copy (the rest stay stale); the
+  // batch's scalars must have been encoded with hb.pack_scalars(n)
   void submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, hipStream_t copy,
               int scalar_cols = 5);
   // Make `compute` wait for the slot's H2D; returns the device view.
@@ -48,7 +49,10 @@ class RawSlots {
     uint8_t* text = nullptr;
     int64_t* offsets = nullptr;
     uint8_t* flags = nullptr;
-    int64_t* scalars = nullptr;
+    int64_t* scalars = nullptr;       // wire-encoded scalar columns (bytes)
+    int64_t soff[kScalarCols] = {};
+    int64_t sbase[kScalarCols] = {};
+    int32_t swide = 0;
     int64_t n = 0, bytes = 0;
     hipEvent_t h2d_done = nullptr, consumed = nullptr;
     bool used = false;

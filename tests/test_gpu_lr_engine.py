@@ -43,12 +43,19 @@ def _rows_from_debug(dbg):
     return rows
 
 
-@pytest.mark.parametrize("F,hash", [(1000, "java"), (1 << 20, "java"), (1 << 20, "murmur3")])
-def test_featurize_matches_oracle(hip_module, F, hash):
+@pytest.mark.parametrize("F,hash,wide", [(1000, "java", False), (1 << 20, "java", False),
+                                         (1 << 20, "murmur3", False), (1000, "java", True)])
+def test_featurize_matches_oracle(hip_module, F, hash, wide):
     cfg = SynthConfig.profile("twitter", seed=11, special_fraction=0.05, unicode_fraction=0.3)
     raw = generate_batch(cfg, 0, 3000, batch_time_ms=NOW)
+    if wide:   # followers / createdAt ranges beyond 32 bits: those columns ship as int64
+        raw.scalars[1, 5] = (1 << 40) + 7
+        raw.scalars[4, 9] = 0
     eng = _engine(F, hash)
     eng.train_batch(raw, want_pred=True)
+    sw = eng._staging[0]._hb.scalar_wire
+    assert sw["rows"] == raw.n
+    assert sw["wide_mask"] == (0b10010 if wide else 0), sw
     dbg = eng._eng.debug_prepared()
     fb = featurize_batch(raw, F, 100, 1000, now_ms=NOW, hash=hash)
     assert int(dbg["counters"][0]) == fb.n

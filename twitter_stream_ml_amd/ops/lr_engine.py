@@ -86,7 +86,8 @@ class HostBatchView:
     ``load`` pre-lowers the special rows, then packs the UTF-16 batch into
     narrow (Latin-1, 1 byte/unit) / wide (UTF-16LE) rows with the native
     multi-threaded packer (``csrc/host/wire.cpp``): typical tweet text
-    crosses PCIe at half the UTF-16 size.
+    crosses PCIe at half the UTF-16 size.  The five int64 scalar columns
+    ship as u32 offsets from a per-batch base when their range fits (exact).
     """
 
     def __init__(self, max_rows: int, max_units: int):
@@ -117,6 +118,7 @@ class HostBatchView:
         self.bytes = int(host().wire_pack(raw.text, raw.offsets, raw.is_retweet, self.text,
                                           self.offsets, self.flags))
         self.scalars_flat[:5 * n] = raw.scalars.reshape(-1)
+        self._hb.pack_scalars(n)   # u32 + per-batch base where a column's range fits
         self.n, self.units, self.batch_time_ms = n, u, raw.batch_time_ms
         return self
 
