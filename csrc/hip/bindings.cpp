@@ -32,7 +32,7 @@ static LRConfig lr_config(const py::dict& d) {
   GET(num_iterations, int32_t) GET(fraction, double) GET(tol, double) GET(begin, int64_t)
   GET(end, int64_t) GET(require_retweet, int32_t) GET(range_filter, int32_t)
   GET(max_rows, int64_t) GET(max_units, int64_t) GET(sgd_grid, int32_t)
-  GET(early_exit_depth, int32_t) GET(ablate, int32_t) GET(dedup, int32_t) GET(hybrid, int32_t)
+  GET(early_exit_depth, int32_t) GET(ablate, int32_t) GET(dedup, int32_t) GET(hybrid, int32_t) GET(lazy_idx, int32_t)
 #undef GET
   return c;
 }

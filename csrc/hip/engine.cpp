@@ -155,6 +155,7 @@ void LREngine::alloc_prepared() {
   prep_.y = dmalloc<float>(size_t(R16));
   prep_.num = dmalloc<float>(4 * size_t(R16));
   prep_.perm = dmalloc<int32_t>(size_t(R16));
+  prep_.rtext = dmalloc<int64_t>(size_t(R16));
   // active-feature flags: Java-hash bigrams are < 2^21 whatever F is
   const int64_t F = cfg_.num_text_features;
   int64_t fl = cfg_.hash_kind == 0 ? std::min<int64_t>(F, int64_t(1) << 21) : F;
@@ -255,7 +256,7 @@ LREngine::~LREngine() {
   void* bufs[] = {prep_.kept, prep_.nnz, prep_.sorted, prep_.blk, prep_.hist, prep_.clen8, prep_.cfast,
                   prep_.clen8d, prep_.cnt, prep_.cslot, prep_.hot_dense, prep_.clen8c,
                   prep_.hot_slot, prep_.hot_of, prep_.slot_hist, prep_.code,
-                  prep_.cbase, prep_.idx, prep_.slot, prep_.y, prep_.num, prep_.perm,
+                  prep_.cbase, prep_.idx, prep_.slot, prep_.y, prep_.num, prep_.perm, prep_.rtext,
                   prep_.flags, prep_.uniq, prep_.slot_of, prep_.ublk, prep_.counters,
                   sgd_.w64, sgd_.wc64, sgd_.wc32, sgd_.g64, sgd_.red64, sgd_.stats, sgd_.state,
                   sgd_.loss_hist, sgd_.pred_out, sgd_.part, sgd_.itrec, coh_.part, coh_.w32, coh_.norms, coh_.bar, gd_tdbg_, iter_tdbg_, lower_page_, lower_blocks_, n_global_};
@@ -288,8 +289,12 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   launch_prep_init(prep_, n_global_, world + 2, s);
   launch_filter_sort(b, prep_, fp, s);
   launch_chunk_layout(b, prep_, s);
+  // lazy ids: only the histogram's sample chunks keep their hashed ids; the
+  // hybrid remap re-reads the (still resident) raw text for the rest
+  const bool lazy = cfg_.lazy_idx && cfg_.hybrid && !cfg_.dedup;
+  fp.idx_mode = lazy ? 1 : 0;
   launch_featurize(b, prep_, fp, lower_page_, lower_blocks_, s);
-  raw_.release_slot(slot, s);  // raw slot may be overwritten now
+  if (!lazy) raw_.release_slot(slot, s);  // raw slot may be overwritten now
   if (world > 1) comm_->allreduce(prep_.flags, size_t(prep_.flag_len), ncclUint8, ncclMax, s);
   launch_compact_active(prep_, s);
   // global kept count (and per-rank counts for sampling offsets)
@@ -329,8 +334,10 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   const bool u16 = ns <= 65536;
   const bool dedup = cfg_.dedup && u16 && dedup_supported(ns);
   prep_.hybrid = (!dedup && cfg_.hybrid && u16 && res.n_kept > 0 && sgd_hybrid_fits(ns)) ? 1 : 0;
-  if (prep_.hybrid) launch_remap_hybrid(prep_, res.entries, ns, kNumNumeric + nU, num_cu_, s);
+  if (lazy && !prep_.hybrid) launch_featurize_fast_ids(b, prep_, fp, s);   // every id after all
+  if (prep_.hybrid) launch_remap_hybrid(prep_, res.entries, ns, kNumNumeric + nU, num_cu_, b, fp, lazy, s);
   else launch_remap(prep_, res.entries, nU, u16, s);
+  if (lazy) raw_.release_slot(slot, s);
   prep_.dedup = dedup ? 1 : 0;
   if (prep_.dedup) launch_dedup(prep_, ns, kNumNumeric + nU, res.n_kept, s);
   launch_batch_init(sgd_, double(n_glob), cfg_.num_iterations + 2, s);  // state[5] = m (global kept rows)

@@ -40,6 +40,7 @@ struct LRConfig {
   int32_t ablate = 0;            // perf diagnostics only (see SgdParams)
   int32_t dedup = 0;             // merge repeated bigrams of a row into counts
   int32_t hybrid = 1;            // dense 4-bit counts for the batch's hottest slots (hot_split.hip)
+  int32_t lazy_idx = 1;          // hybrid: fast chunks' ids re-derived from text by the remap
 };
 
 // Pinned staging buffer of one raw batch in the wire format

@@ -22,6 +22,7 @@
 #include "../common/unicode_tables.h"
 #include "common.h"
 #include "kernels.h"
+#include "narrow_text.h"
 #include "text_stage.h"
 
 namespace twtml {
@@ -107,8 +108,6 @@ void scan_excl_launch(const int64_t* in, int64_t* out, int64_t n, int64_t* total
 constexpr int32_t kNnzWide = 1 << 30;
 constexpr int32_t kNnzMask = kNnzWide - 1;
 constexpr int kHalfBuckets = kLenBuckets / 2;
-// Narrow fast featurizer: bigrams per lane (row quarter) it can hold in VGPRs
-constexpr int kFastMaxQ = 72;
 
 __device__ __forceinline__ int len_key(int32_t v) {
   const int32_t n32 = v & kNnzMask;
@@ -322,65 +321,6 @@ void launch_chunk_layout(const DevRawBatch& b, const DevPrepared& p, hipStream_t
 // K1 + K2: lower-case, bigram hash, numeric features, active-set flags.
 // ---------------------------------------------------------------------------
 
-__device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
-__device__ __forceinline__ uint32_t mur_k(uint32_t k) { return rotl32(k * 0xCC9E2D51u, 15) * 0x1B873593u; }
-__device__ __forceinline__ uint32_t mur_h(uint32_t h, uint32_t k) { return rotl32(h ^ k, 13) * 5u + 0xE6546B64u; }
-
-// Spark-2 murmur3 (hashUnsafeBytes, seed 42) of the UTF-8 bytes of a
-// 1-2 unit Java string (lone surrogates become '?').
-// UTF-8 encoding of one code point, little-endian packed, byte count in *m
-__device__ __forceinline__ uint32_t utf8_pack(uint32_t cp, int* m) {
-  if (cp < 0x80) { *m = 1; return cp; }
-  if (cp < 0x800) { *m = 2; return (0xC0u | (cp >> 6)) | ((0x80u | (cp & 0x3F)) << 8); }
-  if (cp < 0x10000) {
-    *m = 3;
-    return (0xE0u | (cp >> 12)) | ((0x80u | ((cp >> 6) & 0x3F)) << 8) | ((0x80u | (cp & 0x3F)) << 16);
-  }
-  *m = 4;
-  return (0xF0u | (cp >> 18)) | ((0x80u | ((cp >> 12) & 0x3F)) << 8) |
-         ((0x80u | ((cp >> 6) & 0x3F)) << 16) | ((0x80u | (cp & 0x3F)) << 24);
-}
-
-// The UTF-8 bytes (at most 8) live in one 64-bit register: no private array,
-// so nothing spills to scratch.
-__device__ int32_t murmur_term(uint32_t u0, uint32_t u1, int n) {
-  uint64_t bytes = 0;
-  int k = 0, m = 0;
-  const bool hi0 = u0 >= 0xD800 && u0 <= 0xDBFF, sur0 = u0 >= 0xD800 && u0 <= 0xDFFF;
-  if (n == 2 && hi0 && u1 >= 0xDC00 && u1 <= 0xDFFF) {
-    bytes = utf8_pack(0x10000u + ((u0 - 0xD800u) << 10) + (u1 - 0xDC00u), &m);
-    k = m;
-  } else {
-    bytes = utf8_pack(sur0 ? uint32_t('?') : u0, &m);
-    k = m;
-    if (n == 2) {
-      bytes |= uint64_t(utf8_pack((u1 >= 0xD800 && u1 <= 0xDFFF) ? uint32_t('?') : u1, &m)) << (8 * k);
-      k += m;
-    }
-  }
-  uint32_t h = 42u;
-  const int aligned = k & ~3;
-  if (aligned >= 4) h = mur_h(h, mur_k(uint32_t(bytes)));
-  if (aligned >= 8) h = mur_h(h, mur_k(uint32_t(bytes >> 32)));
-  for (int i = aligned; i < k; ++i) h = mur_h(h, mur_k(uint32_t(int32_t(int8_t(uint8_t(bytes >> (8 * i)))))));
-  h ^= uint32_t(k);
-  h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
-  return int32_t(h);
-}
-
-// nonNegativeMod(h, F).  Hashes are 32-bit (Java hashCode / murmur3), so with
-// F < 2^32 the reduction is a multiply-high (FastMod32), not a division.
-__device__ __forceinline__ int64_t term_mod(int64_t h, int64_t F, const FastMod32& fm, bool f32) {
-  if (h >= 0 && h < F) return h;                 // java bigrams (< 2^21) with F >= 2^21
-  if (f32 && h >= -0xffffffffLL && h <= 0xffffffffLL) {
-    if (h >= 0) return fm.mod(uint32_t(h));
-    const uint32_t r = fm.mod(uint32_t(-h));
-    return r == 0 ? 0 : F - r;
-  }
-  const int64_t m = h % F;
-  return m < 0 ? m + F : m;
-}
-
 // Active-feature flags: ids below kFlagLds are first collected in a per-block
 // LDS bitmap (Java bigram hashes of ASCII text are < 4096, so almost every
 // entry lands here) and flushed once per block; the rest go straight to the
@@ -527,44 +467,25 @@ __global__ __launch_bounds__(kBlock) void k_featurize(DevRawBatch b, DevPrepared
 // holds only the flag bitmap), so occupancy is register-bound, and every
 // chunk costs two memory round trips (row metadata, then text).
 // ---------------------------------------------------------------------------
-constexpr int kFastDw = 20;     // dwords loaded per lane (80 B >= 3 + kFastMaxQ + 1)
-constexpr int kFastAl = 19;     // realigned dwords (76 chars >= kFastMaxQ + 1)
-static_assert(kFastAl * 4 >= kFastMaxQ + 1, "realigned window too small");
-
-// Character.toLowerCase on four Latin-1 bytes: A-Z and U+00C0..U+00DE except
-// U+00D7 gain 0x20.  Per byte on its low 7 bits (no carries between bytes).
-__device__ __forceinline__ uint32_t lower4_latin1(uint32_t x) {
-  const uint32_t hb = x & 0x80808080u;
-  const uint32_t x7 = x & 0x7F7F7F7Fu;
-  const uint32_t ge41 = x7 + 0x3F3F3F3Fu;              // bit 7: x7 >= 0x41
-  const uint32_t gt5a = x7 + 0x25252525u;              // bit 7: x7 >= 0x5B
-  const uint32_t ge40 = x7 + 0x40404040u;              // bit 7: x7 >= 0x40
-  const uint32_t gt5e = x7 + 0x21212121u;              // bit 7: x7 >= 0x5F
-  const uint32_t x57 = (x7 ^ 0x57575757u) + 0x7F7F7F7Fu;  // bit 7: x7 != 0x57
-  const uint32_t lo = ~hb & ge41 & ~gt5a;
-  const uint32_t hi = hb & ge40 & ~gt5e & x57;
-  return x + (((lo | hi) & 0x80808080u) >> 2);
-}
-
-__device__ __forceinline__ uint32_t byte_of(const uint32_t (&a)[kFastAl], int k) {
-  return (a[k >> 2] >> (8 * (k & 3))) & 0xFFu;
-}
-
+// idx_mode (FeaturizeParams): 0 writes every entry's hashed id; 1 (lazy)
+// writes ids only for the chunks the hot-slot histogram samples -- the hybrid
+// remap re-derives the rest from the text (narrow_text.h); 2 writes every id
+// but no flags / numeric features (fallback when the batch cannot use the
+// hybrid layout after a lazy pass).
 __global__ __launch_bounds__(kBlock) void k_featurize_narrow(DevRawBatch b, DevPrepared p,
                                                              FeaturizeParams fp, int64_t cmax) {
   __shared__ uint32_t fbits[kFlagWords];
-  for (int i = threadIdx.x; i < kFlagWords; i += kBlock) fbits[i] = 0u;
-  __syncthreads();
+  const bool flags = fp.idx_mode != 2;
+  if (flags) {
+    for (int i = threadIdx.x; i < kFlagWords; i += kBlock) fbits[i] = 0u;
+    __syncthreads();
+  }
   const int64_t n_kept = p.counters[0];
   const int lane = lane_id();
-  const int r = lane / kLanesPerRow, t = lane % kLanesPerRow;
+  const int t = lane % kLanesPerRow;
   const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
   const int64_t nwaves = int64_t(gridDim.x) * kBlock / kWave;
-  const int64_t F = fp.num_text_features;
-  const bool f32 = F <= 0xffffffffLL;
-  const FastMod32 fm(f32 ? uint32_t(F) : 1u);
-  // Java hashes of Latin-1 bigrams are < 31*255+256 = 8161: no reduction
-  const bool direct = fp.hash_kind == 0 && F > 8160;
+  const NarrowHash nh(fp);
   const int64_t lds_lim = p.flag_len < kFlagLds ? p.flag_len : kFlagLds;
   const int64_t cap_groups = p.cap_entries / kChunkStride;
   const int64_t nch = (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;
@@ -576,47 +497,12 @@ __global__ __launch_bounds__(kBlock) void k_featurize_narrow(DevRawBatch b, DevP
       if (lane == 0) p.counters[3] = 1;  // capacity overflow -> host raises
       continue;
     }
-    // row metadata: lane l resolves row l & 15
-    const int64_t mpos = c * kRowsPerChunk + (lane & 15);
-    const bool mvalid = mpos < n_kept;
-    const int32_t mkidx = mvalid ? p.sorted[mpos] : -1;
-    const int64_t mrow = mvalid ? p.kept[mkidx] : 0;
-    const int64_t mo = mvalid ? b.offsets[mrow] : 0;
-    const int64_t mlen = mvalid ? b.offsets[mrow + 1] - mo : 0;
-    const int64_t pos = c * kRowsPerChunk + r;
-    const bool valid = pos < n_kept;
-    const int32_t kidx = __shfl(mkidx, r, kWave);
-    const int64_t row = __shfl(mrow, r, kWave);
-    const int64_t o = __shfl(mo, r, kWave);
-    const int32_t len = valid ? int32_t(__shfl(mlen, r, kWave)) : 0;
-    const int32_t nz = len >= 2 ? len - 1 : len;
-    const int32_t q = (nz + kLanesPerRow - 1) / kLanesPerRow;
-    const int32_t e0 = t * q;
-    const int32_t my = nz - e0 < 0 ? 0 : (nz - e0 < q ? nz - e0 : q);
-    // text bytes [o + e0, o + e0 + my + 1): dword-aligned window
-    const int64_t start = o + e0;
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(b.text + (start & ~int64_t(3)));
-    const uint32_t sh = uint32_t(start & 3);
-    const int32_t need = int32_t(sh) + my + 1;          // bytes of the window used
-    uint32_t d[kFastDw];
-#pragma unroll
-    for (int i = 0; i < kFastDw; i += 4) {
-      uint4 v = make_uint4(0u, 0u, 0u, 0u);
-      if (my > 0 && 4 * i < need) __builtin_memcpy(&v, src + i, 16);
-      d[i] = v.x; d[i + 1] = v.y; d[i + 2] = v.z; d[i + 3] = v.w;
-    }
-    // wave-uniform bound on the characters any lane uses
-    int32_t mw = my;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      const int32_t x = __shfl_xor(mw, off, kWave);
-      mw = x > mw ? x : mw;
-    }
-    mw = __builtin_amdgcn_readfirstlane(mw);
+    const bool store = fp.idx_mode != 1 || (c % kHistChunks) == 0;   // wave-uniform
+    NarrowLane L;
     uint32_t a[kFastAl];
-#pragma unroll
-    for (int i = 0; i < kFastAl; ++i)
-      a[i] = (4 * i <= mw) ? lower4_latin1(__builtin_amdgcn_alignbyte(d[i + 1], d[i], sh)) : 0u;
+    int64_t rt;
+    narrow_lane_load(b, p, c, n_kept, L, a, &rt);
+    if (fp.idx_mode == 1 && lane < kRowsPerChunk) p.rtext[c * kRowsPerChunk + lane] = rt;
     int32_t* out = p.idx + g0 * kChunkStride + lane * kGroup;
 #pragma unroll
     for (int g = 0; g < kFastMaxQ / kGroup; ++g) {
@@ -625,26 +511,22 @@ __global__ __launch_bounds__(kBlock) void k_featurize_narrow(DevRawBatch b, DevP
 #pragma unroll
       for (int k = 0; k < kGroup; ++k) {
         const int e = g * kGroup + k;
-        const uint32_t u0 = byte_of(a, e), u1 = byte_of(a, e + 1);
-        int64_t idx;
-        if (direct) {
-          idx = len >= 2 ? int64_t(31u * u0 + u1) : int64_t(u0);
-        } else {
-          const int64_t h = fp.hash_kind == 0 ? (len >= 2 ? int64_t(31u * u0 + u1) : int64_t(u0))
-                                              : int64_t(murmur_term(u0, u1, len >= 2 ? 2 : 1));
-          idx = term_mod(h, F, fm, f32);
-        }
-        v[k] = e < my ? int32_t(idx) : -1;
-        if (e < my) flag_id(fbits, p, idx, lds_lim);
+        const int64_t idx = narrow_id(L, a, e, nh);
+        v[k] = e < L.my ? int32_t(idx) : -1;
+        if (flags && e < L.my) flag_id(fbits, p, idx, lds_lim);
       }
-      int4* dst = reinterpret_cast<int4*>(out + g * kChunkStride);
-      dst[0] = make_int4(v[0], v[1], v[2], v[3]);
-      dst[1] = make_int4(v[4], v[5], v[6], v[7]);
+      if (store) {
+        int4* dst = reinterpret_cast<int4*>(out + g * kChunkStride);
+        dst[0] = make_int4(v[0], v[1], v[2], v[3]);
+        dst[1] = make_int4(v[4], v[5], v[6], v[7]);
+      }
     }
-    if (t == 0) row_scalars(b, p, fp, pos, valid, row, kidx);
+    if (flags && t == 0) row_scalars(b, p, fp, L.pos, L.valid, L.row, L.kidx);
   }
-  __syncthreads();
-  flush_flag_bits(fbits, p);
+  if (flags) {
+    __syncthreads();
+    flush_flag_bits(fbits, p);
+  }
 }
 
 void launch_featurize(const DevRawBatch& b, const DevPrepared& p, const FeaturizeParams& fp,
@@ -657,6 +539,15 @@ void launch_featurize(const DevRawBatch& b, const DevPrepared& p, const Featuriz
   if (grid > 2048) grid = 2048;
   hipLaunchKernelGGL(k_featurize_narrow, dim3(grid), dim3(kBlock), 0, s, b, p, fp, cmax);
   hipLaunchKernelGGL(k_featurize, dim3(grid), dim3(kBlock), 0, s, b, p, fp, lpage, lblocks, cmax);
+}
+
+void launch_featurize_fast_ids(const DevRawBatch& b, const DevPrepared& p, FeaturizeParams fp, hipStream_t s) {
+  const int64_t cmax = (b.n + kRowsPerChunk - 1) / kRowsPerChunk;
+  if (cmax == 0) return;
+  fp.idx_mode = 2;
+  int grid = ceil_div(cmax, kBlock / kWave);
+  if (grid > 2048) grid = 2048;
+  hipLaunchKernelGGL(k_featurize_narrow, dim3(grid), dim3(kBlock), 0, s, b, p, fp, cmax);
 }
 
 // ---------------------------------------------------------------------------

@@ -11,7 +11,7 @@
 // cold for that row (every occurrence in its own lane), so the layout is
 // exact for any text and a lane never holds more cold entries than before.
 //
-//   k_slot_hist      sampled slot histogram (every 32nd 8-entry group of idx)
+//   k_slot_hist      sampled slot histogram (every kHistChunks-th chunk of idx)
 //   k_hot_select     top-kHot by binary search on the count threshold
 //   k_remap_hybrid   replaces k_remap: one wave per 16-row chunk maps hashed
 //                    ids to slots, counts hot slots per row in LDS, and writes
@@ -23,13 +23,13 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "narrow_text.h"
 
 namespace twtml {
 
 namespace {
 
 constexpr int kHistBlock = 1024;
-constexpr int kHistStride = 32;            // sample every 32nd 8-entry group
 constexpr int kSplitWaves = 4;
 
 // LDS hand-off between the lanes of one wave (no other wave touches the
@@ -40,19 +40,29 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-__global__ __launch_bounds__(kHistBlock) void k_slot_hist(const int32_t* idx, const int32_t* slot_of,
-                                                          int64_t n8, int64_t pad_base, uint32_t* hist) {
+// One wave per sampled chunk (c % kHistChunks == 0: the lazy featurizer
+// writes ids for exactly those fast chunks), all of its groups.
+__global__ __launch_bounds__(kHistBlock) void k_slot_hist(DevPrepared p, int64_t pad_base, uint32_t* hist) {
   extern __shared__ uint32_t h[];
   for (int64_t s = threadIdx.x; s < pad_base; s += kHistBlock) h[s] = 0u;
   __syncthreads();
-  for (int64_t i = int64_t(blockIdx.x) * kHistBlock + threadIdx.x; i * kHistStride < n8;
-       i += int64_t(gridDim.x) * kHistBlock) {
-    const int4* src = reinterpret_cast<const int4*>(idx + i * kHistStride * 8);
-    const int4 a = src[0], b = src[1];
-    const int32_t v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  const int lane = lane_id();
+  const int64_t n_kept = p.counters[0];
+  const int64_t nsamp = ((n_kept + kRowsPerChunk - 1) / kRowsPerChunk + kHistChunks - 1) / kHistChunks;
+  const int64_t wave = (int64_t(blockIdx.x) * kHistBlock + threadIdx.x) / kWave;
+  const int64_t nwaves = int64_t(gridDim.x) * kHistBlock / kWave;
+  for (int64_t sc = wave; sc < nsamp; sc += nwaves) {
+    const int64_t c = sc * kHistChunks;
+    const int32_t L8 = p.clen8[c];
+    const int32_t* src = p.idx + p.cbase[c] * kChunkStride + lane * kGroup;
+    for (int32_t g = 0; g < L8; ++g) {
+      const int4* s4 = reinterpret_cast<const int4*>(src + int64_t(g) * kChunkStride);
+      const int4 a = s4[0], b = s4[1];
+      const int32_t v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 #pragma unroll
-    for (int e = 0; e < 8; ++e)
-      if (v[e] >= 0) atomicAdd(&h[kNumNumeric + slot_of[v[e]]], 1u);
+      for (int e = 0; e < 8; ++e)
+        if (v[e] >= 0) atomicAdd(&h[kNumNumeric + p.slot_of[v[e]]], 1u);
+    }
   }
   __syncthreads();
   for (int64_t s = threadIdx.x; s < pad_base; s += kHistBlock)
@@ -160,9 +170,13 @@ __device__ __forceinline__ uint32_t id_code(const uint16_t* lcode, const DevPrep
 //   rare    a hot id counting > 15 in a row: its entries are re-read and
 //           appended cold (each stays in the lane that held it)
 //   pad     every lane's cold stream padded to the chunk's max group count
+//   text    (from_text) fast chunks re-derive their ids from the raw text
+//           (narrow_text.h) instead of reading idx
 __global__ __launch_bounds__(kSplitWaves * kWave) void k_remap_hybrid(DevPrepared p, int64_t ns,
                                                                       int64_t pad_base,
-                                                                      const uint16_t* code) {
+                                                                      const uint16_t* code,
+                                                                      DevRawBatch rb, FeaturizeParams fp,
+                                                                      int from_text) {
   __shared__ uint16_t lcode[kCodeIds];
   __shared__ uint32_t cnt[kSplitWaves][kRowsPerChunk * kCntStride];
   for (int i = threadIdx.x; i < kCodeIds / 8; i += kSplitWaves * kWave)
@@ -179,8 +193,13 @@ __global__ __launch_bounds__(kSplitWaves * kWave) void k_remap_hybrid(DevPrepare
   uint32_t* crow = cw + r * kCntStride;
   const uint32_t pad = uint32_t(pad_base + lane);
   uint16_t* plain = static_cast<uint16_t*>(p.slot);
+  const NarrowHash nh(fp);
 
+  // the next chunk's packed row-text words are loaded one chunk ahead
+  int64_t rt_next = (from_text && wave < nch) ? p.rtext[wave * kRowsPerChunk + lane / kLanesPerRow] : 0;
   for (int64_t c = wave; c < nch; c += nwaves) {
+    const int64_t rt = rt_next;
+    if (from_text && c + nwaves < nch) rt_next = p.rtext[(c + nwaves) * kRowsPerChunk + lane / kLanesPerRow];
     const int32_t L8 = p.clen8[c];
     const int64_t off = p.cbase[c] * kChunkStride + lane * kGroup;
     const int32_t* src = p.idx + off;
@@ -206,20 +225,41 @@ __global__ __launch_bounds__(kSplitWaves * kWave) void k_remap_hybrid(DevPrepare
       dst[int64_t(k >> 3) * kChunkStride + (k & 7)] = uint16_t(sl);
       ++k;
     };
-    for (int32_t g = 0; g < L8; ++g) {
-      const int4* s4 = reinterpret_cast<const int4*>(src + int64_t(g) * kChunkStride);
-      const int4 a = s4[0], b = s4[1];
-      const int32_t v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    auto count = [&](uint32_t cd) {
+      if (cd & kCodeHot) {
+        const uint32_t h = cd & 0xFFu;
+        atomicAdd(&crow[h >> 1], 1u << ((h & 1u) * 16));
+      } else {
+        put(cd);
+      }
+    };
+    auto big = [&](uint32_t cd) {   // rare pass: hot ids counting > 15 in the row go cold
+      if (!(cd & kCodeHot)) return;
+      const uint32_t h = cd & 0xFFu;
+      if (((crow[h >> 1] >> ((h & 1u) * 16)) & 0xFFFFu) > 15u) put(uint32_t(p.hot_slot[h]));
+    };
+    const bool text = from_text && p.cfast[c];   // wave-uniform
+    NarrowLane L;
+    uint32_t a[kFastAl];
+    if (text) {
+      narrow_lane_load_rt(rb, c, n_kept, rt, L, a);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        if (v[e] < 0) continue;
-        const uint32_t cd = id_code(lcode, p, v[e]);
-        if (cd & kCodeHot) {
-          const uint32_t h = cd & 0xFFu;
-          atomicAdd(&crow[h >> 1], 1u << ((h & 1u) * 16));
-        } else {
-          put(cd);
+      for (int g = 0; g < kFastMaxQ / kGroup; ++g) {
+        if (g >= L8) break;                               // wave-uniform
+#pragma unroll
+        for (int e8 = 0; e8 < kGroup; ++e8) {
+          const int e = g * kGroup + e8;
+          if (e < L.my) count(id_code(lcode, p, int32_t(narrow_id(L, a, e, nh))));
         }
+      }
+    } else {
+      for (int32_t g = 0; g < L8; ++g) {
+        const int4* s4 = reinterpret_cast<const int4*>(src + int64_t(g) * kChunkStride);
+        const int4 a = s4[0], b = s4[1];
+        const int32_t v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (v[e] >= 0) count(id_code(lcode, p, v[e]));
       }
     }
     wave_lds_sync();
@@ -246,17 +286,26 @@ __global__ __launch_bounds__(kSplitWaves * kWave) void k_remap_hybrid(DevPrepare
     }
     reinterpret_cast<uint4*>(p.hot_dense)[c * kWave + lane] = make_uint4(nib[0], nib[1], nib[2], nib[3]);
     if (__any(ovf)) {   // rare: a hot bigram more than 15 times in one row
-      for (int32_t g = 0; g < L8; ++g) {
-        const int4* s4 = reinterpret_cast<const int4*>(src + int64_t(g) * kChunkStride);
-        const int4 a = s4[0], b = s4[1];
-        const int32_t v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      if (text) {   // reload the text (keeping a[] live here costs registers everywhere)
+        uint32_t a2[kFastAl];
+        narrow_lane_load_rt(rb, c, n_kept, rt, L, a2);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          if (v[e] < 0) continue;
-          const uint32_t cd = id_code(lcode, p, v[e]);
-          if (!(cd & kCodeHot)) continue;
-          const uint32_t h = cd & 0xFFu;
-          if (((crow[h >> 1] >> ((h & 1u) * 16)) & 0xFFFFu) > 15u) put(uint32_t(p.hot_slot[h]));
+        for (int g = 0; g < kFastMaxQ / kGroup; ++g) {
+          if (g >= L8) break;
+#pragma unroll
+          for (int e8 = 0; e8 < kGroup; ++e8) {
+            const int e = g * kGroup + e8;
+            if (e < L.my) big(id_code(lcode, p, int32_t(narrow_id(L, a2, e, nh))));
+          }
+        }
+      } else {
+        for (int32_t g = 0; g < L8; ++g) {
+          const int4* s4 = reinterpret_cast<const int4*>(src + int64_t(g) * kChunkStride);
+          const int4 a = s4[0], b = s4[1];
+          const int32_t v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (v[e] >= 0) big(id_code(lcode, p, v[e]));
         }
       }
     }
@@ -273,23 +322,24 @@ __global__ __launch_bounds__(kSplitWaves * kWave) void k_remap_hybrid(DevPrepare
 }  // namespace
 
 void launch_remap_hybrid(const DevPrepared& p, int64_t entries, int64_t ns, int64_t pad_base, int num_cu,
-                         hipStream_t s) {
+                         const DevRawBatch& b, const FeaturizeParams& fp, bool from_text, hipStream_t s) {
   if (ns > kMaxHybridSlots) throw std::invalid_argument("hybrid layout: too many active slots");
   if (entries == 0) return;
   // slot_hist was zeroed by launch_prep_init
-  const int64_t n8 = entries / kGroup;
-  int gh = int((n8 / kHistStride + kHistBlock - 1) / kHistBlock);
+  const int64_t cmax = (p.cap_rows + kRowsPerChunk - 1) / kRowsPerChunk;
+  const int64_t nsamp = (cmax + kHistChunks - 1) / kHistChunks;
+  int gh = int((nsamp + kHistBlock / kWave - 1) / (kHistBlock / kWave));
   gh = std::max(1, std::min(gh, num_cu));
   hipLaunchKernelGGL(k_slot_hist, dim3(gh), dim3(kHistBlock), size_t(pad_base) * sizeof(uint32_t), s,
-                     p.idx, p.slot_of, n8, pad_base, p.slot_hist);
+                     p, pad_base, p.slot_hist);
   hipLaunchKernelGGL(k_hot_select, dim3(1), dim3(1024), 0, s, p.slot_hist, ns, pad_base, p.hot_of,
                      p.hot_slot);
   hipLaunchKernelGGL(k_code_table, dim3(kCodeIds / 1024), dim3(1024), 0, s, p, p.code);
-  const int64_t cmax = (p.cap_rows + kRowsPerChunk - 1) / kRowsPerChunk;
   // persistent-style grid (each workgroup loads the 16 KB code table once)
   int grid = int(std::min<int64_t>(int64_t(num_cu) * 4, (cmax + kSplitWaves - 1) / kSplitWaves));
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL(k_remap_hybrid, dim3(grid), dim3(kSplitWaves * kWave), 0, s, p, ns, pad_base, p.code);
+  hipLaunchKernelGGL(k_remap_hybrid, dim3(grid), dim3(kSplitWaves * kWave), 0, s, p, ns, pad_base, p.code,
+                     b, fp, from_text ? 1 : 0);
 }
 
 }  // namespace twtml

@@ -85,6 +85,7 @@ struct DevPrepared {
   float* y;                 // [R16] label at sorted position p
   float* num;               // [4][R16] numeric features (SoA by sorted position)
   int32_t* perm;            // [R16] kept index at sorted position p, -1 if none
+  int64_t* rtext;           // [R16] fast chunks: text byte offset * 512 + length of the row at p
   // active set
   uint8_t* flags;           // [Fh]
   int32_t* uniq;            // [Fh]  sorted touched feature ids
@@ -117,6 +118,7 @@ struct FeaturizeParams {
   int32_t range_filter;       // filter: begin <= rtCount <= end
   int64_t begin, end;
   int64_t now_ms;
+  int32_t idx_mode = 0;       // narrow featurizer ids: 0 all, 1 lazy (sampled chunks), 2 all, no flags
 };
 
 void upload_lower_tables(hipStream_t s, uint8_t** d_page, uint16_t** d_blocks);
@@ -129,6 +131,8 @@ void launch_filter_sort(const DevRawBatch& b, const DevPrepared& p, const Featur
 void launch_chunk_layout(const DevRawBatch& b, const DevPrepared& p, hipStream_t s);
 void launch_featurize(const DevRawBatch& b, const DevPrepared& p, const FeaturizeParams& fp,
                       const uint8_t* lower_page, const uint16_t* lower_blocks, hipStream_t s);
+// after a lazy (idx_mode 1) featurize: the ids of every fast chunk (idx_mode 2)
+void launch_featurize_fast_ids(const DevRawBatch& b, const DevPrepared& p, FeaturizeParams fp, hipStream_t s);
 void launch_compact_active(const DevPrepared& p, hipStream_t s);
 void launch_remap(const DevPrepared& p, int64_t entries, int64_t n_unique, bool u16, hipStream_t s);
 // per-row duplicate merging for u16 slot spaces up to 8192 slots
@@ -140,8 +144,10 @@ void launch_dedup(const DevPrepared& p, int64_t ns, int64_t pad_base, int64_t n_
 // 4-bit hot counts + each lane's cold entries (hot_split.hip).
 constexpr int kHot = 128;
 constexpr int kMaxHybridSlots = 16384;
+// from_text: fast chunks were featurized lazily (idx_mode 1); their ids are
+// re-derived from the raw batch b (which must still be resident)
 void launch_remap_hybrid(const DevPrepared& p, int64_t entries, int64_t ns, int64_t pad_base, int num_cu,
-                         hipStream_t s);
+                         const DevRawBatch& b, const FeaturizeParams& fp, bool from_text, hipStream_t s);
 
 // ---------------------------------------------------------------------------
 // SGD on the compact active set.

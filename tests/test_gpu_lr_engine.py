@@ -51,7 +51,7 @@ def test_featurize_matches_oracle(hip_module, F, hash, wide):
     if wide:   # followers / createdAt ranges beyond 32 bits: those columns ship as int64
         raw.scalars[1, 5] = (1 << 40) + 7
         raw.scalars[4, 9] = 0
-    eng = _engine(F, hash)
+    eng = _engine(F, hash, lazy_idx=False)   # every hashed id kept for inspection
     eng.train_batch(raw, want_pred=True)
     sw = eng._staging[0]._hb.scalar_wire
     assert sw["rows"] == raw.n
@@ -186,15 +186,18 @@ def _with_repeats(raw, every=7, text="ha" * 40):
     return RawBatch(np.concatenate(units), off, raw.is_retweet, raw.scalars, raw.batch_time_ms)
 
 
-@pytest.mark.parametrize("repeats", [False, True])
-def test_hybrid_layout_matches_hashingtf(hip_module, repeats):
-    """Hybrid layout: 4-bit hot counts + cold SELL entries == HashingTF term counts."""
-    F = 1000
+@pytest.mark.parametrize("F,hash,repeats,lazy", [(1000, "java", False, True), (1000, "java", True, True),
+                                                 (1 << 20, "java", False, True),
+                                                 (1 << 20, "java", True, False),
+                                                 (1 << 20, "murmur3", False, True)])
+def test_hybrid_layout_matches_hashingtf(hip_module, F, hash, repeats, lazy):
+    """Hybrid layout: 4-bit hot counts + cold SELL entries == HashingTF term counts
+    (lazy: fast chunks' ids re-derived from the text by the remap)."""
     cfg = SynthConfig.profile("twitter", seed=14, unicode_fraction=0.2)
     raw = generate_batch(cfg, 0, 4000, batch_time_ms=NOW)
     if repeats:
         raw = _with_repeats(raw)
-    eng = _engine(F, "java", hybrid=True)
+    eng = _engine(F, hash, hybrid=True, lazy_idx=lazy)
     eng.train_batch(raw, want_pred=False)
     dbg = eng._eng.debug_prepared()
     hy = eng._eng.debug_hybrid()
@@ -205,7 +208,7 @@ def test_hybrid_layout_matches_hashingtf(hip_module, repeats):
     real_hot = (hot_slot >= 4) & (hot_slot < 4 + nU)
     assert real_hot.sum() == min(128, nU)
     assert np.unique(hot_slot[real_hot]).shape[0] == real_hot.sum()
-    fb = featurize_batch(raw, F, 100, 1000, now_ms=NOW)
+    fb = featurize_batch(raw, F, 100, 1000, now_ms=NOW, hash=hash)
     Xt = fb.X[:, :F].tocsr()
     perm, cbase, clen8 = dbg["perm"], dbg["cbase"], dbg["clen8"]
     dense = hy["hot_dense"].reshape(-1, 64, 4)
@@ -239,7 +242,7 @@ def test_hybrid_layout_matches_hashingtf(hip_module, repeats):
     if repeats:
         assert big > 0, "test data should exercise the > 15 count overflow"
     # the hybrid iteration trains like the plain one
-    plain = _engine(F, "java", hybrid=False)
+    plain = _engine(F, hash, hybrid=False)
     plain.train_batch(raw, want_pred=False)
     wh, wp = eng.get_weights(), plain.get_weights()
     np.testing.assert_allclose(wh, wp, rtol=1e-4, atol=1e-6 * np.abs(wp).max())

@@ -58,6 +58,11 @@ class LRDeviceConfig:
     dedup: bool = False
     # dense 4-bit counts for the batch's 128 hottest bigrams (csrc/hip/hot_split.hip)
     hybrid: bool = True
+    # hybrid layout only: the featurizer materialises hashed ids just for the
+    # chunks the hot-slot histogram samples; the remap re-derives the rest
+    # from the raw text (csrc/hip/narrow_text.h).  False keeps every id
+    # (debug_prepared() inspection).
+    lazy_idx: bool = True
 
     def as_dict(self) -> Dict[str, object]:
         return {
@@ -77,6 +82,7 @@ class LRDeviceConfig:
             "ablate": int(self.ablate),
             "dedup": int(bool(self.dedup)),
             "hybrid": int(bool(self.hybrid)),
+            "lazy_idx": int(bool(self.lazy_idx)),
         }
 
 
