@@ -508,11 +508,12 @@ __device__ __forceinline__ void hot_digits(const DevPrepared& p, const float* wl
   }
 }
 
+// wctr: the workgroup's LDS chunk counter, zeroed by hyb_lds_init.
 template <bool STATS, bool SAMPLE, int REP>
 __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, const SgdParams& sp,
                                          const float* wl, unsigned long long* gl, const uint32_t* whl,
                                          float (*hsum)[kHot], double (*wsc)[kPartVals], double* prow,
-                                         uint64_t* tst = nullptr) {
+                                         uint32_t* wctr, uint64_t* tst = nullptr) {
   const int64_t ns = d.ns;
   const int lane = lane_id();
   const int w = __builtin_amdgcn_readfirstlane(int(threadIdx.x) / kWave);   // wave-uniform
@@ -520,8 +521,6 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
   const int rep = lane % REP;
   const int64_t n_kept = p.counters[0];
   const int64_t nch = sp.ablate % 10 == 7 ? 0 : (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;  // 7: fixed cost
-  const int64_t wave = int64_t(blockIdx.x) * (kIterBlock / kWave) + w;
-  const int64_t nwaves = int64_t(gridDim.x) * (kIterBlock / kWave);
   const uint16_t* slot = static_cast<const uint16_t*>(p.slot);
   const uint4* hdense = reinterpret_cast<const uint4*>(p.hot_dense);
   const int32_t* __restrict__ clen8c = p.clen8c;
@@ -534,34 +533,38 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
   RowAcc acc;
   bool clamped = false;
 
-  // Chunk metadata for 64 of this wave's chunks at a time, lane i holding
-  // the i-th (one load round trip per 64 chunks; read back with v_readlane
-  // into SGPRs).  Row inputs and hot counts are issued before the cold
-  // stream, so a chunk costs one memory round trip.
-  int32_t md_l8 = 0;
-  int64_t md_cb = 0;
-  int k = 0;
-  // chunk order: round robin over all waves, or (ablate >= 10, experiment)
-  // a contiguous block per workgroup interleaved over its waves
-  const bool blocked = sp.ablate >= 10;
-  const int abl = blocked ? sp.ablate - 10 : sp.ablate;
-  int64_t c0 = wave, cstep = nwaves, cend = nch;
-  if (blocked) {
-    const int64_t G = gridDim.x;
-    c0 = nch * int64_t(blockIdx.x) / G + w;
-    cend = nch * (int64_t(blockIdx.x) + 1) / G;
-    cstep = kIterBlock / kWave;
+  // Dynamic chunk assignment inside the workgroup: workgroup b owns chunks
+  // b, b + G, b + 2G, ... and its waves take the next one from an LDS
+  // counter.  (A static round robin let the oldest waves, which the SIMD
+  // arbiter favours, finish ~20 us before the youngest -- the tail then ran
+  // at one wave per SIMD.)  The next chunk's index and metadata are fetched
+  // one chunk ahead (scalar loads), so the grab costs no memory round trip.
+  const int abl = sp.ablate;
+  const int64_t G = gridDim.x, b = blockIdx.x;
+  const int64_t nj = nch > b ? (nch - b + G - 1) / G : 0;
+  auto grab = [&]() -> int64_t {
+    uint32_t j = 0;
+    if (lane == 0) j = atomicAdd(wctr, 1u);
+    return int64_t(__builtin_amdgcn_readfirstlane(__shfl(int(j), 0, kWave)));
+  };
+  int k = 0;   // chunks this wave took
+  int64_t j = grab();
+  int32_t L8n = 0;
+  int64_t cbn = 0;
+  if (j < nj) {
+    L8n = clen8c[b + j * G];
+    cbn = cbase[b + j * G];
   }
-  for (int64_t c = c0; c < cend; c += cstep, ++k) {
-    if ((k & (kWave - 1)) == 0) {
-      const int64_t cc = c + int64_t(lane) * cstep;
-      md_l8 = cc < cend ? clen8c[cc] : 0;
-      md_cb = cc < cend ? cbase[cc] : 0;
+  while (j < nj) {
+    const int64_t c = b + j * G;
+    const int32_t L8c = L8n;
+    const int64_t cb = cbn;
+    ++k;
+    j = grab();
+    if (j < nj) {
+      L8n = clen8c[b + j * G];
+      cbn = cbase[b + j * G];
     }
-    const int kl = k & (kWave - 1);
-    const int32_t L8c = __builtin_amdgcn_readlane(md_l8, kl);
-    const int64_t cb = int64_t(uint32_t(__builtin_amdgcn_readlane(int32_t(md_cb), kl))) |
-                       (int64_t(__builtin_amdgcn_readlane(int32_t(md_cb >> 32), kl)) << 32);
     const int64_t pos = c * kRowsPerChunk + r;
     const int64_t off = cb * kChunkStride + lane * kGroup;
     const RowIn ri = row_in(p, pos);
@@ -707,7 +710,9 @@ __device__ __forceinline__ T ld_coh(const T* ptr) {
 // Slots >= hi (pads) get weight 0 whatever wsrc holds there.
 template <int REP>
 __device__ __forceinline__ void hyb_lds_init(const DevPrepared& p, const float* wsrc, int64_t ns,
-                                             int64_t hi, float* wl, unsigned long long* gl, uint32_t* whl) {
+                                             int64_t hi, float* wl, unsigned long long* gl, uint32_t* whl,
+                                             uint32_t* wctr) {
+  if (threadIdx.x == 0) *wctr = 0u;
   for (int64_t s = threadIdx.x; s < ns; s += kIterBlock) wl[s] = s < hi ? ld_coh(wsrc + s) : 0.f;
   for (int64_t s = threadIdx.x; s < ns * REP; s += kIterBlock) gl[s] = 0ull;
   __syncthreads();
@@ -722,6 +727,7 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_hyb(DevSgd d, DevPrepar
   __shared__ float hsum[kIterBlock / kWave * kHotRows][kHot];
   __shared__ __attribute__((aligned(16))) uint32_t whl[kLanesPerRow * kHotLdsStride];
   __shared__ int stop_flag;
+  __shared__ uint32_t wctr;
   uint64_t* tst = nullptr;
   if (d.tdbg && threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1))
     tst = d.tdbg + (int64_t(sp.iteration) * 2 + (blockIdx.x == 0 ? 0 : 1)) * 8;
@@ -730,9 +736,9 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_hyb(DevSgd d, DevPrepar
   if (tst) tst[1] = __builtin_amdgcn_s_memrealtime();
   float* wl = lds;
   unsigned long long* gl = reinterpret_cast<unsigned long long*>(lds + d.ns);
-  hyb_lds_init<REP>(p, d.wc32, d.ns, kNumNumeric + d.n_unique, wl, gl, whl);
+  hyb_lds_init<REP>(p, d.wc32, d.ns, kNumNumeric + d.n_unique, wl, gl, whl, &wctr);
   if (tst) tst[2] = __builtin_amdgcn_s_memrealtime();
-  hyb_pass<STATS, SAMPLE, REP>(d, p, sp, wl, gl, whl, hsum, wsc, d.part + int64_t(blockIdx.x) * d.pstride, tst);
+  hyb_pass<STATS, SAMPLE, REP>(d, p, sp, wl, gl, whl, hsum, wsc, d.part + int64_t(blockIdx.x) * d.pstride, &wctr, tst);
   if (tst) tst[6] = __builtin_amdgcn_s_memrealtime();
 }
 
@@ -793,6 +799,7 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_gd_hyb(DevSgd d, DevPrepared
   __shared__ __attribute__((aligned(16))) uint32_t whl[kLanesPerRow * kHotLdsStride];
   __shared__ double red[kIterBlock / kWave][2];
   __shared__ int flag, conv_sh;
+  __shared__ uint32_t wctr;
   const int64_t ns = d.ns, hi = kNumNumeric + d.n_unique;
   float* wl = lds;
   unsigned long long* gl = reinterpret_cast<unsigned long long*>(lds + ns);
@@ -815,9 +822,9 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_gd_hyb(DevSgd d, DevPrepared
     sp.iteration = it;
     tst = coh.tdbg ? coh.tdbg + int64_t(it) * 8 : nullptr;
     stamp(0);
-    hyb_lds_init<REP>(p, it == it_first ? d.wc32 : coh.w32, ns, hi, wl, gl, whl);
+    hyb_lds_init<REP>(p, it == it_first ? d.wc32 : coh.w32, ns, hi, wl, gl, whl, &wctr);
     stamp(1);
-    hyb_pass<false, false, REP>(d, p, sp, wl, gl, whl, hsum, wsc, prow);
+    hyb_pass<false, false, REP>(d, p, sp, wl, gl, whl, hsum, wsc, prow, &wctr);
     stamp(2);
     if (!grid_sync(coh.bar, ++gen, &flag)) break;
     stamp(3);
