@@ -5,6 +5,7 @@
 #include <stdexcept>
 
 #include "common.h"
+#include "trace.h"
 
 #define TWTML_NCCL_CHECK(expr)                                                                \
   do {                                                                                        \
@@ -47,6 +48,7 @@ RcclComm::~RcclComm() {
 
 void RcclComm::allreduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t s) {
   if (world_ == 1 || count == 0) return;
+  TraceRange tr("twtml.rccl.allreduce");
   TWTML_NCCL_CHECK(ncclAllReduce(buf, buf, count, dt, op, comm_, s));
 }
 

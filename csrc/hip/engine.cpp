@@ -1,5 +1,6 @@
 // LREngine implementation; see engine.h.
 #include "engine.h"
+#include "trace.h"
 
 #include <algorithm>
 #include <cmath>
@@ -270,11 +271,13 @@ LREngine::~LREngine() {
 }
 
 void LREngine::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot) {
+  TraceRange tr("twtml.lr.submit_h2d");
   TWTML_HIP_CHECK(hipSetDevice(device_));
   raw_.submit(hb, n, bytes, slot, copy_);
 }
 
 BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
+  TraceRange tr_batch("twtml.lr.batch");
   TWTML_HIP_CHECK(hipSetDevice(device_));
   hipStream_t s = compute_;
   const int world = comm_ ? comm_->world() : 1;
@@ -284,6 +287,7 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   res.n_raw = b.n;
   TWTML_HIP_CHECK(hipEventRecord(ev_[0], s));
 
+  auto tr_prep = std::make_unique<TraceRange>("twtml.lr.prep");   // filter .. remap
   FeaturizeParams fp{cfg_.num_text_features, cfg_.hash_kind, cfg_.require_retweet,
                      cfg_.range_filter, cfg_.begin, cfg_.end, now_ms};
   launch_prep_init(prep_, n_global_, world + 2, s);
@@ -344,6 +348,8 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   launch_norm2(sgd_.w64, num_weights(), &sgd_.state[4], s);
   launch_gather_w(sgd_, prep_, s);
   TWTML_HIP_CHECK(hipEventRecord(ev_[1], s));
+  tr_prep.reset();
+  TraceRange tr_train("twtml.lr.train");   // GD iterations (host enqueue + early-stop polling)
 
   int grid = cfg_.sgd_grid > 0 ? cfg_.sgd_grid : sgd_iter_grid(ns, res.n_kept, num_cu_);
   sgd_.pstride = sgd_part_stride(ns);

@@ -1,5 +1,6 @@
 // KMEngine: the streaming k-means micro-batch pipeline (see kmeans.hip).
 #include "kmeans_engine.h"
+#include "trace.h"
 
 #include <pybind11/numpy.h>
 #include <pybind11/stl.h>
@@ -94,12 +95,14 @@ KMEngine::~KMEngine() {
 }
 
 void KMEngine::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot) {
+  TraceRange tr("twtml.km.submit_h2d");
   TWTML_HIP_CHECK(hipSetDevice(device_));
   // features read only retweetCount and followersCount (scalar rows 0, 1)
   raw_.submit(hb, n, bytes, slot, copy_, 2);
 }
 
 KMResult KMEngine::process(int slot, bool want_labels) {
+  TraceRange tr("twtml.km.batch");
   TWTML_HIP_CHECK(hipSetDevice(device_));
   hipStream_t s = compute_;
   const int world = comm_ ? comm_->world() : 1;

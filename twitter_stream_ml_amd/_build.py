@@ -149,7 +149,7 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
                  f"-Wl,-rpath,{tl}"]
     else:
         link += [f"-L{ROCM}/lib", "-lamdhip64", "-lrccl", f"-Wl,-rpath,{ROCM}/lib"]
-    link += ["-lpthread"]
+    link += [f"-L{ROCM}/lib", "-lrocprofiler-sdk-roctx", f"-Wl,-rpath,{ROCM}/lib", "-lpthread"]
     _run(link, verbose)
     os.replace(HIP_SO + ".tmp", HIP_SO)
     return HIP_SO
