@@ -108,6 +108,8 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
   sgd_.loss_hist = dmalloc<double>(size_t(std::max(1, cfg_.num_iterations)) + 2);
   sgd_.itrec = dmalloc<double>((size_t(std::max(1, cfg_.num_iterations)) + 2) * kRecStride);
   sgd_.pred_out = dmalloc<float>(size_t(cfg_.max_rows));
+  sgd_.nrm = dmalloc<double>(kNormParts);
+  sgd_.wnorm_next = dmalloc<double>(1);
   TWTML_HIP_CHECK(hipMemset(sgd_.red64, 0, 4 * sizeof(double)));
   ensure_compact(4096);
   const int world = comm_ ? comm_->world() : 1;
@@ -260,7 +262,7 @@ LREngine::~LREngine() {
                   prep_.cbase, prep_.idx, prep_.slot, prep_.y, prep_.num, prep_.perm, prep_.rtext,
                   prep_.flags, prep_.uniq, prep_.slot_of, prep_.ublk, prep_.counters,
                   sgd_.w64, sgd_.wc64, sgd_.wc32, sgd_.g64, sgd_.red64, sgd_.stats, sgd_.state,
-                  sgd_.loss_hist, sgd_.pred_out, sgd_.part, sgd_.itrec, coh_.part, coh_.w32, coh_.norms, coh_.bar, gd_tdbg_, iter_tdbg_, lower_page_, lower_blocks_, n_global_};
+                  sgd_.loss_hist, sgd_.pred_out, sgd_.nrm, sgd_.wnorm_next, sgd_.part, sgd_.itrec, coh_.part, coh_.w32, coh_.norms, coh_.bar, gd_tdbg_, iter_tdbg_, lower_page_, lower_blocks_, n_global_};
   for (void* b : bufs) if (b) (void)hipFree(b);
   if (host_counters_) (void)hipHostFree(host_counters_);
   if (host_out_) (void)hipHostFree(host_out_);
@@ -345,7 +347,13 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   prep_.dedup = dedup ? 1 : 0;
   if (prep_.dedup) launch_dedup(prep_, ns, kNumNumeric + nU, res.n_kept, s);
   launch_batch_init(sgd_, double(n_glob), cfg_.num_iterations + 2, s);  // state[5] = m (global kept rows)
-  launch_norm2(sgd_.w64, num_weights(), &sgd_.state[4], s);
+  if (norm_age_ < 0 || norm_age_ >= kNormRefresh) {
+    launch_norm2(sgd_.w64, num_weights(), &sgd_.state[4], sgd_, s);
+    norm_age_ = 0;
+  } else {
+    launch_norm_carry(sgd_, s);
+  }
+  ++norm_age_;
   launch_gather_w(sgd_, prep_, s);
   TWTML_HIP_CHECK(hipEventRecord(ev_[1], s));
   tr_prep.reset();
@@ -438,6 +446,7 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
     }
     launch_sgd_finish(sgd_, sp, s);
     launch_scatter_w(sgd_, prep_, s);
+    launch_norm_next(sgd_, true, s);
     if (itime) {   // iteration-kernel phases (us): stop-check, lds init, chunks, hot reduce, scalars, slots
       std::vector<uint64_t> tb(4096 + size_t(iters + 2) * 32);
       TWTML_HIP_CHECK(hipMemcpyAsync(tb.data(), iter_tdbg_, tb.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
@@ -465,6 +474,7 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
       }
     }
   }
+  if (n_glob <= 0) launch_norm_next(sgd_, false, s);   // weights unchanged: carry |w|^2 as is
   TWTML_HIP_CHECK(hipEventRecord(ev_[2], s));
   if (world > 1) comm_->allreduce(sgd_.stats, 6, ncclFloat64, ncclSum, s);
   TWTML_HIP_CHECK(hipMemcpyAsync(host_out_, sgd_.stats, 8 * sizeof(double), hipMemcpyDeviceToHost, s));
@@ -495,6 +505,7 @@ void LREngine::set_weights(const double* w, int64_t n) {
   TWTML_HIP_CHECK(hipSetDevice(device_));
   TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
   TWTML_HIP_CHECK(hipMemcpy(sgd_.w64, w, sizeof(double) * size_t(n), hipMemcpyHostToDevice));
+  norm_age_ = -1;   // the carried |w|^2 no longer holds
 }
 
 void LREngine::get_weights(double* w, int64_t n) const {

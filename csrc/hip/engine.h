@@ -125,6 +125,11 @@ class LREngine {
   DevPrepared prep_{};
   DevSgd sgd_{};
   int64_t ns_cap_ = 0;
+  // |w|^2 is carried from batch to batch (|w_rest|^2 + trained active part)
+  // instead of a pass over all F+4 weights (800 MB at F = 1e8); recomputed
+  // after set_weights and every kNormRefresh batches
+  static constexpr int kNormRefresh = 256;
+  int norm_age_ = -1;   // batches since the last full pass (-1: carried value invalid)
   int64_t part_cap_ = 0;
   DevCoh coh_{};
   int64_t coh_part_cap_ = 0, coh_ns_cap_ = 0;

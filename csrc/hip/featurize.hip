@@ -353,14 +353,28 @@ __device__ __forceinline__ void row_scalars(const DevRawBatch& b, const DevPrepa
 }
 
 // Flag an active feature id (LDS bitmap below lds_lim, byte flags above).
+// fcache (murmur3 over a wide F only): a direct-mapped LDS cache of ids this
+// workgroup already flagged, so the ~150 entries per tweet do not each store
+// a byte into a 100 MB flag array -- a tweet batch touches a few thousand
+// distinct ids, almost every lookup hits.
+constexpr int kFlagCache = 4096;
+
 __device__ __forceinline__ void flag_id(uint32_t* fbits, const DevPrepared& p, int64_t idx,
-                                        int64_t lds_lim) {
+                                        int64_t lds_lim, uint32_t* fcache = nullptr) {
   if (idx < lds_lim) {
     // hot ids are flagged early: a (broadcast) read skips the atomic
     const uint32_t bit = 1u << (idx & 31);
     if (!(fbits[idx >> 5] & bit)) atomicOr(&fbits[idx >> 5], bit);
   } else if (idx < p.flag_len) {
-    p.flags[idx] = 1;
+    if (fcache) {
+      uint32_t& e = fcache[uint32_t(idx) & (kFlagCache - 1)];
+      if (e != uint32_t(idx)) {
+        p.flags[idx] = 1;
+        e = uint32_t(idx);   // racing lanes may both store: harmless
+      }
+    } else {
+      p.flags[idx] = 1;
+    }
   }
 }
 
@@ -472,12 +486,17 @@ __global__ __launch_bounds__(kBlock) void k_featurize(DevRawBatch b, DevPrepared
 // remap re-derives the rest from the text (narrow_text.h); 2 writes every id
 // but no flags / numeric features (fallback when the batch cannot use the
 // hybrid layout after a lazy pass).
+template <bool CACHE>
 __global__ __launch_bounds__(kBlock) void k_featurize_narrow(DevRawBatch b, DevPrepared p,
                                                              FeaturizeParams fp, int64_t cmax) {
   __shared__ uint32_t fbits[kFlagWords];
+  __shared__ uint32_t fcache_s[CACHE ? kFlagCache : 1];
+  uint32_t* fcache = CACHE ? fcache_s : nullptr;
   const bool flags = fp.idx_mode != 2;
   if (flags) {
     for (int i = threadIdx.x; i < kFlagWords; i += kBlock) fbits[i] = 0u;
+    if (CACHE)
+      for (int i = threadIdx.x; i < kFlagCache; i += kBlock) fcache_s[i] = 0xFFFFFFFFu;
     __syncthreads();
   }
   const int64_t n_kept = p.counters[0];
@@ -513,7 +532,7 @@ __global__ __launch_bounds__(kBlock) void k_featurize_narrow(DevRawBatch b, DevP
         const int e = g * kGroup + k;
         const int64_t idx = narrow_id(L, a, e, nh);
         v[k] = e < L.my ? int32_t(idx) : -1;
-        if (flags && e < L.my) flag_id(fbits, p, idx, lds_lim);
+        if (flags && e < L.my) flag_id(fbits, p, idx, lds_lim, fcache);
       }
       if (store) {
         int4* dst = reinterpret_cast<int4*>(out + g * kChunkStride);
@@ -537,7 +556,12 @@ void launch_featurize(const DevRawBatch& b, const DevPrepared& p, const Featuriz
   // flushed rarely (XCD-agnostic: chunk order is length-sorted anyway)
   int grid = ceil_div(cmax, kBlock / kWave);
   if (grid > 2048) grid = 2048;
-  hipLaunchKernelGGL(k_featurize_narrow, dim3(grid), dim3(kBlock), 0, s, b, p, fp, cmax);
+  // ids of a Java-hashed Latin-1 bigram are < 8161, always in the LDS bitmap;
+  // murmur3 ids above it get the flag cache
+  if (fp.hash_kind == 1 && p.flag_len > kFlagLds)
+    hipLaunchKernelGGL(k_featurize_narrow<true>, dim3(grid), dim3(kBlock), 0, s, b, p, fp, cmax);
+  else
+    hipLaunchKernelGGL(k_featurize_narrow<false>, dim3(grid), dim3(kBlock), 0, s, b, p, fp, cmax);
   hipLaunchKernelGGL(k_featurize, dim3(grid), dim3(kBlock), 0, s, b, p, fp, lpage, lblocks, cmax);
 }
 
@@ -547,7 +571,7 @@ void launch_featurize_fast_ids(const DevRawBatch& b, const DevPrepared& p, Featu
   fp.idx_mode = 2;
   int grid = ceil_div(cmax, kBlock / kWave);
   if (grid > 2048) grid = 2048;
-  hipLaunchKernelGGL(k_featurize_narrow, dim3(grid), dim3(kBlock), 0, s, b, p, fp, cmax);
+  hipLaunchKernelGGL(k_featurize_narrow<false>, dim3(grid), dim3(kBlock), 0, s, b, p, fp, cmax);
 }
 
 // ---------------------------------------------------------------------------

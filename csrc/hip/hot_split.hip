@@ -156,11 +156,26 @@ __global__ __launch_bounds__(1024) void k_code_table(DevPrepared p, uint16_t* co
   code[id] = uint16_t(c);
 }
 
+// Larger active ids carry their hot id in slot_of itself (k_code_tag:
+// bit 31 hot, bits 16..23 hot id, bits 0..15 compact index), one dependent
+// load per lookup instead of slot_of then hot_of.
+constexpr uint32_t kTagHot = 0x80000000u;
+
+__device__ __forceinline__ uint32_t slot_index(int32_t so) { return uint32_t(so) & 0xFFFFu; }
+
 __device__ __forceinline__ uint32_t id_code(const uint16_t* lcode, const DevPrepared& p, int32_t id) {
   if (id < kCodeIds) return lcode[id];
-  const uint32_t sl = uint32_t(kNumNumeric + p.slot_of[id]);
-  const uint32_t h = p.hot_of[sl];
-  return h != 0xFFu ? (kCodeHot | h) : sl;
+  const uint32_t so = uint32_t(p.slot_of[id]);
+  return (so & kTagHot) ? (kCodeHot | ((so >> 16) & 0xFFu)) : uint32_t(kNumNumeric) + (so & 0xFFFFu);
+}
+
+__global__ __launch_bounds__(1024) void k_code_tag(DevPrepared p, int64_t n_unique) {
+  const int64_t u = int64_t(blockIdx.x) * 1024 + threadIdx.x;
+  if (u >= n_unique) return;
+  const int32_t id = p.uniq[u];
+  if (id < kCodeIds) return;
+  const uint32_t h = p.hot_of[kNumNumeric + u];
+  p.slot_of[id] = int32_t(uint32_t(u) | (h != 0xFFu ? (kTagHot | (h << 16)) : 0u));
 }
 
 // One wave per 16-row chunk (SELL-16x4 input layout of featurize):
@@ -210,7 +225,7 @@ __global__ __launch_bounds__(kSplitWaves * kWave) void k_remap_hybrid(DevPrepare
         const int32_t v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
         uint32_t o[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = v[e] >= 0 ? uint32_t(kNumNumeric + p.slot_of[v[e]]) : pad;
+        for (int e = 0; e < 8; ++e) o[e] = v[e] >= 0 ? uint32_t(kNumNumeric) + slot_index(p.slot_of[v[e]]) : pad;
         *reinterpret_cast<uint4*>(plain + off + int64_t(g) * kChunkStride) =
             make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7]));
       }
@@ -335,6 +350,8 @@ void launch_remap_hybrid(const DevPrepared& p, int64_t entries, int64_t ns, int6
   hipLaunchKernelGGL(k_hot_select, dim3(1), dim3(1024), 0, s, p.slot_hist, ns, pad_base, p.hot_of,
                      p.hot_slot);
   hipLaunchKernelGGL(k_code_table, dim3(kCodeIds / 1024), dim3(1024), 0, s, p, p.code);
+  const int64_t nU = pad_base - kNumNumeric;
+  if (nU > 0) hipLaunchKernelGGL(k_code_tag, dim3(int((nU + 1023) / 1024)), dim3(1024), 0, s, p, nU);
   // persistent-style grid (each workgroup loads the 16 KB code table once)
   int grid = int(std::min<int64_t>(int64_t(num_cu) * 4, (cmax + kSplitWaves - 1) / kSplitWaves));
   if (grid < 1) grid = 1;

@@ -158,7 +158,8 @@ struct DevSgd {
   double* g64;          // [NS+1] gradient accumulator (+ loss at [NS])
   double* red64;        // [4] {loss, m, pad, pad} for sampled iterations
   double* stats;        // [8] n, sum_y, sum_y2, sum_p, sum_p2, sum_e2, -, -
-  double* state;        // [8] 0 done 1 converged 2 n_updates 3 iters 4 wrest2 5 m_global 6 wnorm2_full
+  double* state;        // [8] 0 done 1 converged 2 n_updates 3 iters 4 |w|^2 (all F+4) 5 m_global
+                        //     6 |w_active|^2 at gather (|w_rest|^2 = [4] - [6])
   double* loss_hist;    // [max_iters+1]
   float* pred_out;      // [R] rounded predictions in kept order (optional)
   double* host_flags;   // [max_iters+1] pinned host memory: done flag after each update
@@ -170,7 +171,11 @@ struct DevSgd {
   int64_t n_unique;
   int64_t pstride;      // ns + 64: slots, then loss, m, 6 batch stats (see sgd_part_stride)
   int32_t nparts;       // partial rows written by the last iteration launch (0 = global path)
+  double* nrm;          // [kNormParts] per-block partial squared norms (fixed-order sums)
+  double* wnorm_next;   // [1] |w|^2 after the last batch (state[4] of the next batch)
 };
+
+constexpr int kNormParts = 1024;   // grid cap of the norm / gather / scatter kernels
 
 // Grid barrier of the persistent GD kernel (uncached memory): per-XCD-group
 // arrival counters (64 B apart), global counter, generation, error flag.
@@ -220,7 +225,7 @@ struct SgdParams {
 float sgd_fix_limit(int64_t entries_per_wg);
 
 void launch_gather_w(const DevSgd& d, const DevPrepared& p, hipStream_t s);
-void launch_norm2(const double* v, int64_t n, double* out, hipStream_t s);
+void launch_norm2(const double* v, int64_t n, double* out, const DevSgd& d, hipStream_t s);
 void launch_sgd_iter(const DevSgd& d, const DevPrepared& p, const SgdParams& sp, int64_t groups,
                      bool u16, int grid, hipStream_t s);
 // Partial rows an iteration launch of `grid` workgroups writes (0: the
@@ -238,6 +243,11 @@ void launch_sgd_persistent(const DevSgd& d, const DevPrepared& p, const SgdParam
 // after the GD loop: convergence of the last update -> state
 void launch_sgd_finish(const DevSgd& d, const SgdParams& sp, hipStream_t s);
 void launch_scatter_w(const DevSgd& d, const DevPrepared& p, hipStream_t s);
+// |w|^2 for the next batch: |w_rest|^2 + |w_active after training|^2, from
+// the scatter's block partials (trained) or state[4] unchanged (no rows)
+void launch_norm_next(const DevSgd& d, bool trained, hipStream_t s);
+// state[4] = wnorm_next (instead of a full |w|^2 pass over all F+4 weights)
+void launch_norm_carry(const DevSgd& d, hipStream_t s);
 int sgd_lds_rep(int64_t ns);
 // the hybrid iteration kernel's LDS (gradient replicas + hot partials) fits
 bool sgd_hybrid_fits(int64_t ns);

@@ -1262,6 +1262,25 @@ void launch_sgd_finish(const DevSgd& d, const SgdParams& sp, hipStream_t s) {
 // ---------------------------------------------------------------------------
 // Gather / scatter between full-width fp64 weights and the compact space.
 // ---------------------------------------------------------------------------
+// Squared norms are reduced deterministically: each block writes its partial
+// to d.nrm[blockIdx], one wave adds the partials in a fixed order (DP ranks
+// hold identical weights, so their convergence verdicts must match bit for
+// bit; float atomics would add in arrival order).
+// mode 0: out = sum; 1: out = |w_rest|^2 (state[4] - state[6]) + sum; 2: out = state[4]
+__global__ void k_norm_sum(const double* parts, int n, double* out, const double* state, int mode) {
+  double acc = 0.0;
+  for (int k = lane_id(); k < n; k += kWave) acc += parts[k];
+  acc = wave_sum(acc);
+  if (threadIdx.x == 0) {
+    double base = 0.0;
+    if (mode == 1) {             // rest of the previous batch + active part
+      base = state[4] - state[6];
+      if (base < 0.0) base = 0.0;
+    }
+    *out = mode == 2 ? state[4] : base + acc;
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_gather_w(DevSgd d, const int32_t* uniq) {
   __shared__ double scratch[kBlock / kWave];
   double acc = 0.0;
@@ -1276,43 +1295,66 @@ __global__ __launch_bounds__(kBlock) void k_gather_w(DevSgd d, const int32_t* un
     acc += v * v;
   }
   acc = block_sum(acc, scratch);
-  if (threadIdx.x == 0) atomicAdd(&d.state[6], acc);
+  if (threadIdx.x == 0) d.nrm[blockIdx.x] = acc;
 }
 
-__global__ __launch_bounds__(kBlock) void k_norm2(const double* v, int64_t n, double* out) {
+__global__ __launch_bounds__(kBlock) void k_norm2(const double* v, int64_t n, double* parts) {
   __shared__ double scratch[kBlock / kWave];
   double acc = 0.0;
   for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock)
     acc += v[i] * v[i];
   acc = block_sum(acc, scratch);
-  if (threadIdx.x == 0) atomicAdd(out, acc);
+  if (threadIdx.x == 0) parts[blockIdx.x] = acc;
 }
 
 __global__ __launch_bounds__(kBlock) void k_scatter_w(DevSgd d, const int32_t* uniq) {
+  __shared__ double scratch[kBlock / kWave];
+  double acc = 0.0;
   for (int64_t s = int64_t(blockIdx.x) * kBlock + threadIdx.x; s < kNumNumeric + d.n_unique;
        s += int64_t(gridDim.x) * kBlock) {
-    if (s < kNumNumeric) d.w64[d.F + s] = d.wc64[s];
-    else d.w64[uniq[s - kNumNumeric]] = d.wc64[s];
+    const double v = d.wc64[s];
+    if (s < kNumNumeric) d.w64[d.F + s] = v;
+    else d.w64[uniq[s - kNumNumeric]] = v;
+    acc += v * v;
   }
+  acc = block_sum(acc, scratch);
+  if (threadIdx.x == 0) d.nrm[blockIdx.x] = acc;
+}
+
+static int gather_grid(const DevSgd& d) { return std::max(1, std::min(ceil_div(d.ns, kBlock), kNormParts)); }
+static int scatter_grid(const DevSgd& d) {
+  return std::max(1, std::min(ceil_div(kNumNumeric + d.n_unique, kBlock), kNormParts));
 }
 
 void launch_gather_w(const DevSgd& d, const DevPrepared& p, hipStream_t s) {
-  int grid = ceil_div(d.ns, kBlock);
-  if (grid > 1024) grid = 1024;
+  const int grid = gather_grid(d);
   hipLaunchKernelGGL(k_gather_w, dim3(grid), dim3(kBlock), 0, s, d, p.uniq);
+  hipLaunchKernelGGL(k_norm_sum, dim3(1), dim3(kWave), 0, s, d.nrm, grid, &d.state[6], d.state, 0);
 }
 
-void launch_norm2(const double* v, int64_t n, double* out, hipStream_t s) {
+void launch_norm2(const double* v, int64_t n, double* out, const DevSgd& d, hipStream_t s) {
   int grid = ceil_div(n, kBlock * 8);
-  if (grid > 1024) grid = 1024;
+  if (grid > kNormParts) grid = kNormParts;
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL(k_norm2, dim3(grid), dim3(kBlock), 0, s, v, n, out);
+  hipLaunchKernelGGL(k_norm2, dim3(grid), dim3(kBlock), 0, s, v, n, d.nrm);
+  hipLaunchKernelGGL(k_norm_sum, dim3(1), dim3(kWave), 0, s, d.nrm, grid, out, d.state, 0);
 }
 
 void launch_scatter_w(const DevSgd& d, const DevPrepared& p, hipStream_t s) {
-  int grid = ceil_div(kNumNumeric + d.n_unique, kBlock);
-  if (grid > 1024) grid = 1024;
-  hipLaunchKernelGGL(k_scatter_w, dim3(grid), dim3(kBlock), 0, s, d, p.uniq);
+  hipLaunchKernelGGL(k_scatter_w, dim3(scatter_grid(d)), dim3(kBlock), 0, s, d, p.uniq);
+}
+
+void launch_norm_next(const DevSgd& d, bool trained, hipStream_t s) {
+  hipLaunchKernelGGL(k_norm_sum, dim3(1), dim3(kWave), 0, s, d.nrm, trained ? scatter_grid(d) : 0,
+                     d.wnorm_next, d.state, trained ? 1 : 2);
+}
+
+__global__ void k_norm_carry(DevSgd d) {
+  if (threadIdx.x == 0) d.state[4] = *d.wnorm_next;
+}
+
+void launch_norm_carry(const DevSgd& d, hipStream_t s) {
+  hipLaunchKernelGGL(k_norm_carry, dim3(1), dim3(kWave), 0, s, d);
 }
 
 // Per-batch SGD state in one launch: state (m = global kept rows at [5]),
