@@ -74,6 +74,8 @@ def main(argv=None) -> int:
     info = D.init_distributed()
     device = info.local_rank
     torch.cuda.set_device(device)
+    from twitter_stream_ml_amd.parallel.affinity import bind_local_numa
+    numa_cpus = bind_local_numa(device)   # before the pinned pool is allocated
     comm = D.make_rccl_comm(device)
 
     B = args.batch
@@ -186,6 +188,7 @@ def main(argv=None) -> int:
             "trained_tweets_per_step": round(tweets / args.steps, 1),
             "device_ms_mean": float(np.mean([s[0] for s in stage])) if stage else 0.0,
             "pool_gen_s": round(t_gen, 2),
+            "numa_bound_cpus": len(numa_cpus) if numa_cpus else None,
         }
         line = json.dumps(out)
         print(line, flush=True)
@@ -221,6 +224,7 @@ def main(argv=None) -> int:
             "prep_ms_mean": float(np.mean([s[0] for s in stage])) if stage else 0.0,
             "train_ms_mean": float(np.mean([s[1] for s in stage])) if stage else 0.0,
             "pool_gen_s": round(t_gen, 2),
+            "numa_bound_cpus": len(numa_cpus) if numa_cpus else None,
         }
         line = json.dumps(out)
         print(line, flush=True)

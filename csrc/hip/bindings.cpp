@@ -65,6 +65,11 @@ PYBIND11_MODULE(_twtml_hip, m) {
   m.doc() = "twtml MI355X engine: HIP/CDNA4 kernels, micro-batch engines, RCCL";
   m.attr("RAW_SLOTS") = kRawSlots;   // device raw-batch slots per engine (submit/process)
 
+  m.def("pci_bus_id", [](int device) {
+    char buf[64] = {0};
+    TWTML_HIP_CHECK(hipDeviceGetPCIBusId(buf, int(sizeof(buf)), device));
+    return std::string(buf);
+  }, py::arg("device"));
   m.def("device_count", []() {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;

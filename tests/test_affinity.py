@@ -1,0 +1,57 @@
+"""NUMA-local binding of a GPU rank (parallel/affinity.py) against a fake sysfs."""
+import os
+
+from twitter_stream_ml_amd.parallel.affinity import bind_local_numa, gpu_numa_node, parse_cpulist
+
+
+def _sysfs(tmp_path, bdf="0000:05:00.0", node="1", cpulist="4-7,12"):
+    dev = tmp_path / "bus" / "pci" / "devices" / bdf
+    dev.mkdir(parents=True)
+    (dev / "numa_node").write_text(node + "\n")
+    nd = tmp_path / "devices" / "system" / "node" / f"node{node}"
+    nd.mkdir(parents=True)
+    (nd / "cpulist").write_text(cpulist + "\n")
+    return str(tmp_path)
+
+
+def test_parse_cpulist():
+    assert parse_cpulist("0-3,8,10-11\n") == {0, 1, 2, 3, 8, 10, 11}
+    assert parse_cpulist("") == set()
+
+
+def test_gpu_numa_node(tmp_path):
+    root = _sysfs(tmp_path)
+    assert gpu_numa_node("0000:05:00.0", root) == 1
+    assert gpu_numa_node("0000:06:00.0", root) is None
+
+
+def test_bind_intersects_with_current_affinity(tmp_path, monkeypatch):
+    monkeypatch.delenv("TWTML_NUMA_BIND", raising=False)
+    root = _sysfs(tmp_path)
+    calls = []
+    got = bind_local_numa(3, pci_bus_id=lambda d: "0000:05:00.0", sysfs=root,
+                          setaffinity=lambda pid, cpus: calls.append(set(cpus)),
+                          getaffinity=lambda pid: set(range(0, 10)))
+    assert got == {4, 5, 6, 7} and calls == [{4, 5, 6, 7}]
+
+
+def test_bind_is_best_effort(tmp_path, monkeypatch):
+    monkeypatch.delenv("TWTML_NUMA_BIND", raising=False)
+    root = _sysfs(tmp_path, node="-1")
+    never = lambda pid, cpus: (_ for _ in ()).throw(AssertionError("must not bind"))  # noqa: E731
+    cur = lambda pid: {0, 1}  # noqa: E731
+    assert bind_local_numa(0, lambda d: "0000:05:00.0", root, never, cur) is None    # no NUMA info
+    root2 = _sysfs(tmp_path / "b", cpulist="4-7")
+    assert bind_local_numa(0, lambda d: "0000:05:00.0", root2, never, cur) is None   # cpuset excludes node
+    def boom(d):
+        raise RuntimeError("no device")
+    assert bind_local_numa(0, boom, root2, never, cur) is None
+    monkeypatch.setenv("TWTML_NUMA_BIND", "0")
+    root3 = _sysfs(tmp_path / "c", cpulist="0")
+    assert bind_local_numa(0, lambda d: "0000:05:00.0", root3, never, lambda pid: {0, 1}) is None
+
+
+def test_real_process_affinity_untouched_without_gpu():
+    before = os.sched_getaffinity(0)
+    bind_local_numa(0, pci_bus_id=lambda d: "ffff:ff:ff.f")   # nonexistent device path
+    assert os.sched_getaffinity(0) == before

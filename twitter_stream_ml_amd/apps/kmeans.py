@@ -68,6 +68,8 @@ def build_kmeans_engine(args, dim: int, rank: int, world: int):
         from ..ops.kmeans_engine import DeviceKMeans, KMDeviceConfig
         from ..parallel.dist import make_rccl_comm
         dev = spec.devices[rank] if spec.devices else rank
+        from ..parallel.affinity import bind_local_numa
+        bind_local_numa(dev)   # pinned staging buffers on the GPU's NUMA node
         rows = max(65536, args.batchSize)
         cfg = KMDeviceConfig(k=args.k, text_dims=args.textDims, half_life=args.halfLife,
                              max_rows=rows, max_units=rows * 290, seed=args.seed)

@@ -64,6 +64,8 @@ def build_engine(conf: ConfArguments, rank: int, world: int, device: Optional[in
         from ..ops.lr_engine import DeviceLinearRegression, LRDeviceConfig
         from ..parallel.dist import make_rccl_comm
         dev = device if device is not None else (spec.devices[rank] if spec.devices else rank)
+        from ..parallel.affinity import bind_local_numa
+        bind_local_numa(dev)   # pinned staging buffers on the GPU's NUMA node
         rows = max_rows or max(65536, int(conf.batchSize or 0))
         cfg = LRDeviceConfig(num_text_features=F, hash=conf.hash, step_size=conf.stepSize,
                              num_iterations=conf.numIterations, fraction=conf.miniBatchFraction,

@@ -1,0 +1,86 @@
+"""NUMA-local CPU binding for one-process-per-GPU jobs.
+
+On an 8-GPU MI355X node every rank streams ~190 B per raw tweet from pinned
+host memory over its own PCIe link (~56 GB/s each, ~450 GB/s for the node):
+host DRAM and the socket interconnect sit on that path.  Binding a rank's
+threads to the CPUs of its GPU's NUMA node before it allocates its pinned
+staging buffers keeps those buffers on the local node (Linux first-touch
+policy), so no rank's H2D crosses sockets.  Spark has no equivalent (the
+reference's ingest is 2 tweets/s); this exists for the DP=8
+configuration of BASELINE.json.
+
+``TWTML_NUMA_BIND=0`` disables it.  Every step is best effort: no sysfs
+entry, a single-node machine or a cpuset that excludes the node leaves the
+affinity unchanged.
+"""
+from __future__ import annotations
+
+import os
+from typing import Callable, Optional, Set
+
+__all__ = ["parse_cpulist", "gpu_numa_node", "bind_local_numa"]
+
+SYSFS = "/sys"
+
+
+def parse_cpulist(text: str) -> Set[int]:
+    """Kernel cpulist format: ``0-3,8,10-11``."""
+    out: Set[int] = set()
+    for part in text.strip().split(","):
+        part = part.strip()
+        if not part:
+            continue
+        if "-" in part:
+            a, b = part.split("-", 1)
+            out.update(range(int(a), int(b) + 1))
+        else:
+            out.add(int(part))
+    return out
+
+
+def _read(path: str) -> Optional[str]:
+    try:
+        with open(path) as f:
+            return f.read()
+    except OSError:
+        return None
+
+
+def gpu_numa_node(pci_bus_id: str, sysfs: str = SYSFS) -> Optional[int]:
+    """NUMA node of a PCI device (``0000:05:00.0``), None if unknown."""
+    txt = _read(os.path.join(sysfs, "bus", "pci", "devices", pci_bus_id.lower(), "numa_node"))
+    if txt is None:
+        return None
+    try:
+        node = int(txt.strip())
+    except ValueError:
+        return None
+    return node if node >= 0 else None
+
+
+def bind_local_numa(device: int, pci_bus_id: Optional[Callable[[int], str]] = None,
+                    sysfs: str = SYSFS,
+                    setaffinity: Callable[[int, Set[int]], None] = os.sched_setaffinity,
+                    getaffinity: Callable[[int], Set[int]] = os.sched_getaffinity) -> Optional[Set[int]]:
+    """Restrict the calling thread (and threads it starts later) to the CPUs
+    of ``device``'s NUMA node.  Returns the CPU set, or None if unchanged."""
+    if os.environ.get("TWTML_NUMA_BIND", "1") == "0":
+        return None
+    if pci_bus_id is None:
+        from ..ops._native import hip
+        pci_bus_id = hip().pci_bus_id
+    try:
+        bdf = pci_bus_id(int(device))
+    except Exception:   # noqa: BLE001 -- no device / runtime: keep the affinity
+        return None
+    node = gpu_numa_node(bdf, sysfs)
+    if node is None:
+        return None
+    txt = _read(os.path.join(sysfs, "devices", "system", "node", f"node{node}", "cpulist"))
+    if txt is None:
+        return None
+    cpus = parse_cpulist(txt) & set(getaffinity(0))
+    if not cpus or cpus == set(getaffinity(0)):
+        return None
+    setaffinity(0, cpus)
+    return cpus
