@@ -124,6 +124,10 @@ PYBIND11_MODULE(_twtml_hip, m) {
         auto& h = self.cast<HostBatch&>();
         return view<int64_t>(h.scalars, {py::ssize_t(5 * h.max_rows)}, self);
       })
+      .def("pack_rows", [](HostBatch& h, int64_t n) {
+        py::gil_scoped_release nogil;
+        return h.pack_rows(n);
+      }, py::arg("n"))
       .def("pack_scalars", [](HostBatch& h, int64_t n) {
         py::gil_scoped_release nogil;
         h.pack_scalars(n);

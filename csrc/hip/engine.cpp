@@ -21,7 +21,8 @@ HostBatch::HostBatch(int64_t rows, int64_t text_bytes) : max_rows(rows), max_byt
   const size_t o = up(sizeof(int64_t) * size_t(rows + 1));
   const size_t r = up(size_t(rows));
   const size_t sc = up(sizeof(int64_t) * 5 * size_t(rows));
-  bytes = t + o + r + 2 * sc;
+  const size_t rp = up(sizeof(uint16_t) * size_t(rows));
+  bytes = t + o + r + 2 * sc + rp;
   TWTML_HIP_CHECK(hipHostMalloc(&base, bytes, hipHostMallocDefault));
   char* p = static_cast<char*>(base);
   text = reinterpret_cast<uint8_t*>(p);
@@ -29,6 +30,7 @@ HostBatch::HostBatch(int64_t rows, int64_t text_bytes) : max_rows(rows), max_byt
   flags = reinterpret_cast<uint8_t*>(p + t + o);
   scalars = reinterpret_cast<int64_t*>(p + t + o + r);
   spack = reinterpret_cast<uint8_t*>(p + t + o + r + sc);
+  rowpack = reinterpret_cast<uint16_t*>(p + t + o + r + 2 * sc);
   offsets[0] = 0;
 }
 
@@ -68,6 +70,18 @@ void HostBatch::pack_scalars(int64_t n) {
   for (int c = 0; c < kScalarCols; ++c) th.emplace_back(put, c);
   for (auto& x : th) x.join();
   spacked_n = n;
+}
+
+bool HostBatch::pack_rows(int64_t n) {
+  if (n < 0 || n > max_rows) throw std::invalid_argument("pack_rows: bad row count");
+  rowpacked_n = -1;
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t len = offsets[i + 1] - offsets[i];
+    if (len < 0 || len >= (int64_t(1) << kRowLenBits)) return false;
+    rowpack[i] = uint16_t(len | (int64_t(flags[i] & 3) << kRowLenBits));
+  }
+  rowpacked_n = n;
+  return true;
 }
 
 HostBatch::~HostBatch() {

@@ -59,11 +59,17 @@ struct HostBatch {
   int64_t sbase[kScalarCols] = {};
   int32_t swide = 0;                   // bit c: column c is int64 on the wire
   int64_t spacked_n = -1;              // rows of the last pack_scalars (-1: none)
+  uint16_t* rowpack = nullptr;         // per row: byte length | wire flags << 14
+  int64_t rowpacked_n = -1;            // rows of the last successful pack_rows (-1: none)
   int64_t max_rows = 0, max_bytes = 0;
   HostBatch(int64_t rows, int64_t text_bytes);
   ~HostBatch();
   // Encode scalars[:, :n] into spack (one thread per column).
   void pack_scalars(int64_t n);
+  // Offsets + flags of rows [0, n) as one u16 per row (the device rebuilds
+  // both with a scan): 9 -> 2 bytes per row on PCIe.  False (and the batch
+  // ships offsets + flags as before) if a row has >= 16384 wire bytes.
+  bool pack_rows(int64_t n);
 };
 
 // bytes of device text buffer for `units` UTF-16 units (all rows wide)

@@ -101,6 +101,96 @@ void scan_excl_launch(const int64_t* in, int64_t* out, int64_t n, int64_t* total
   scan_excl(in, out, n, total, s);
 }
 
+// Packed row words -> offsets [n+1] + flags [n], a three-phase scan over
+// tiles of 8192 rows (one 1024-thread block, 8 consecutive rows per thread
+// = one 16-byte load): tile sums, a scan of the ~120 tile sums, then each
+// tile's block-level exclusive scan plus its tile offset.
+constexpr int kRowTile = 8192;
+
+__device__ __forceinline__ void row_words(const uint16_t* rp, int64_t n, int64_t i0, uint32_t (&w)[8]) {
+  if (i0 + 8 <= n) {
+    const uint4 v = *reinterpret_cast<const uint4*>(rp + i0);
+    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      w[2 * k] = d[k] & 0xFFFFu;
+      w[2 * k + 1] = d[k] >> 16;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) w[k] = i0 + k < n ? uint32_t(rp[i0 + k]) : 0u;
+  }
+}
+
+__device__ __forceinline__ int64_t block_excl_scan_1024(int64_t v, int64_t* wsum, int64_t* total) {
+  const int lane = lane_id(), w = threadIdx.x / kWave;
+  int64_t x = v;   // inclusive wave scan
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    const int64_t y = __shfl_up(x, off, kWave);
+    if (lane >= off) x += y;
+  }
+  if (lane == kWave - 1) wsum[w] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t acc = 0;
+    for (int k = 0; k < 1024 / kWave; ++k) {
+      const int64_t t = wsum[k];
+      wsum[k] = acc;
+      acc += t;
+    }
+    *total = acc;
+  }
+  __syncthreads();
+  return wsum[w] + x - v;
+}
+
+__global__ __launch_bounds__(1024) void k_rows_tilesum(const uint16_t* rp, int64_t n, int64_t* tsum) {
+  __shared__ int64_t wsum[1024 / kWave];
+  __shared__ int64_t total;
+  const int64_t i0 = int64_t(blockIdx.x) * kRowTile + int64_t(threadIdx.x) * 8;
+  uint32_t w[8];
+  row_words(rp, n, i0, w);
+  int64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s += w[k] & ((1u << kRowLenBits) - 1u);
+  (void)block_excl_scan_1024(s, wsum, &total);
+  if (threadIdx.x == 0) tsum[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(1024) void k_rows_scan(const uint16_t* rp, int64_t n, const int64_t* tsum,
+                                                    int64_t* offsets, uint8_t* flags) {
+  __shared__ int64_t wsum[1024 / kWave];
+  __shared__ int64_t total;
+  const int64_t i0 = int64_t(blockIdx.x) * kRowTile + int64_t(threadIdx.x) * 8;
+  uint32_t w[8];
+  row_words(rp, n, i0, w);
+  int64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s += w[k] & ((1u << kRowLenBits) - 1u);
+  int64_t o = tsum[blockIdx.x] + block_excl_scan_1024(s, wsum, &total);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    if (i0 + k < n) {
+      offsets[i0 + k] = o;
+      flags[i0 + k] = uint8_t(w[k] >> kRowLenBits);
+    }
+    o += w[k] & ((1u << kRowLenBits) - 1u);
+  }
+}
+
+void launch_unpack_rows(const uint16_t* rowpack, int64_t n, int64_t* offsets, uint8_t* flags, int64_t* tsum,
+                        hipStream_t s) {
+  if (n <= 0) {
+    TWTML_HIP_CHECK(hipMemsetAsync(offsets, 0, sizeof(int64_t), s));
+    return;
+  }
+  const int tiles = int((n + kRowTile - 1) / kRowTile);
+  hipLaunchKernelGGL(k_rows_tilesum, dim3(tiles), dim3(1024), 0, s, rowpack, n, tsum);
+  scan_excl(tsum, tsum, tiles, offsets + n, s);   // offsets[n] = total bytes
+  hipLaunchKernelGGL(k_rows_scan, dim3(tiles), dim3(1024), 0, s, rowpack, n, tsum, offsets, flags);
+}
+
 // nnz[k] carries the row's bigram count in bits 0..29 and the wide (UTF-16
 // wire) flag in bit 30.  Sort key: narrow rows first, then wide rows, each
 // by descending length, so a chunk mixes narrow and wide rows at most once

@@ -48,6 +48,13 @@ __device__ __forceinline__ int64_t raw_scalar(const DevRawBatch& b, int c, int64
 
 constexpr uint8_t kRowRetweet = 1;
 constexpr uint8_t kRowWide = 2;
+// Packed row words on the wire (HostBatch::pack_rows): byte length in the
+// low kRowLenBits bits, the two flag bits above.
+constexpr int kRowLenBits = 14;
+// Rebuild offsets [n+1] (exclusive scan of the lengths) and flags [n] from
+// packed row words on `s`; tsum: scratch of ceil(n / 8192) int64.
+void launch_unpack_rows(const uint16_t* rowpack, int64_t n, int64_t* offsets, uint8_t* flags, int64_t* tsum,
+                        hipStream_t s);
 
 // Row r: byte offset, wide flag and length in UTF-16 units.
 struct RowText {

@@ -29,6 +29,8 @@ void RawSlots::init(int64_t max_rows, int64_t max_bytes) {
     s.offsets = slot_alloc<int64_t>(size_t(max_rows) + 1);
     s.flags = slot_alloc<uint8_t>(size_t(max_rows));
     s.scalars = slot_alloc<int64_t>(5 * size_t(max_rows));
+    s.rowpack = slot_alloc<uint16_t>(size_t(max_rows) + 8);
+    s.tsum = slot_alloc<int64_t>(size_t(max_rows) / 8192 + 2);
     TWTML_HIP_CHECK(hipEventCreateWithFlags(&s.h2d_done, hipEventDisableTiming));
     TWTML_HIP_CHECK(hipEventCreateWithFlags(&s.consumed, hipEventDisableTiming));
   }
@@ -40,6 +42,8 @@ void RawSlots::release() {
     if (s.offsets) (void)hipFree(s.offsets);
     if (s.flags) (void)hipFree(s.flags);
     if (s.scalars) (void)hipFree(s.scalars);
+    if (s.rowpack) (void)hipFree(s.rowpack);
+    if (s.tsum) (void)hipFree(s.tsum);
     if (s.h2d_done) (void)hipEventDestroy(s.h2d_done);
     if (s.consumed) (void)hipEventDestroy(s.consumed);
     s = Slot{};
@@ -59,10 +63,19 @@ void RawSlots::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, h
   if (s.used) TWTML_HIP_CHECK(hipStreamWaitEvent(copy, s.consumed, 0));
   if (bytes > 0)
     TWTML_HIP_CHECK(hipMemcpyAsync(s.text, hb.text, size_t(bytes), hipMemcpyHostToDevice, copy));
-  TWTML_HIP_CHECK(hipMemcpyAsync(s.offsets, hb.offsets, sizeof(int64_t) * size_t(n + 1),
-                                 hipMemcpyHostToDevice, copy));
+  // offsets + flags: one u16 per row when the batch was packed (the compute
+  // stream rebuilds both in acquire), else as they are
+  const bool packed = n > 0 && hb.rowpacked_n == n;
+  if (packed) {
+    TWTML_HIP_CHECK(hipMemcpyAsync(s.rowpack, hb.rowpack, sizeof(uint16_t) * size_t(n),
+                                   hipMemcpyHostToDevice, copy));
+  } else {
+    TWTML_HIP_CHECK(hipMemcpyAsync(s.offsets, hb.offsets, sizeof(int64_t) * size_t(n + 1),
+                                   hipMemcpyHostToDevice, copy));
+  }
   if (n > 0) {
-    TWTML_HIP_CHECK(hipMemcpyAsync(s.flags, hb.flags, size_t(n), hipMemcpyHostToDevice, copy));
+    if (!packed)
+      TWTML_HIP_CHECK(hipMemcpyAsync(s.flags, hb.flags, size_t(n), hipMemcpyHostToDevice, copy));
     // wire-encoded columns are consecutive, so the leading scalar_cols of
     // them are one contiguous copy
     TWTML_HIP_CHECK(hipMemcpyAsync(s.scalars, hb.spack, size_t(hb.soff[scalar_cols]),
@@ -74,6 +87,7 @@ void RawSlots::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, h
     s.sbase[c] = hb.sbase[c];
   }
   s.swide = hb.swide;
+  s.packed = packed;
   s.n = n;
   s.bytes = bytes;
   s.used = true;
@@ -83,6 +97,7 @@ DevRawBatch RawSlots::acquire(int slot, hipStream_t compute) {
   Slot& s = slots_[check(slot)];
   if (!s.used) throw std::logic_error("process() on a slot that was never submitted");
   TWTML_HIP_CHECK(hipStreamWaitEvent(compute, s.h2d_done, 0));
+  if (s.packed) launch_unpack_rows(s.rowpack, s.n, s.offsets, s.flags, s.tsum, compute);
   DevRawBatch b{};
   b.text = s.text;
   b.offsets = s.offsets;

@@ -50,6 +50,9 @@ class RawSlots {
     int64_t* offsets = nullptr;
     uint8_t* flags = nullptr;
     int64_t* scalars = nullptr;       // wire-encoded scalar columns (bytes)
+    uint16_t* rowpack = nullptr;      // packed row words (when the batch shipped them)
+    int64_t* tsum = nullptr;          // unpack scan scratch (per 8192-row tile)
+    bool packed = false;
     int64_t soff[kScalarCols] = {};
     int64_t sbase[kScalarCols] = {};
     int32_t swide = 0;

@@ -43,19 +43,38 @@ def _rows_from_debug(dbg):
     return rows
 
 
-@pytest.mark.parametrize("F,hash,wide", [(1000, "java", False), (1 << 20, "java", False),
-                                         (1 << 20, "murmur3", False), (1000, "java", True)])
-def test_featurize_matches_oracle(hip_module, F, hash, wide):
+def _with_long_row(raw, k=3, n_units=9000):
+    """Row k becomes 9000 Cyrillic units (18000 wire bytes >= 16 KiB)."""
+    from twitter_stream_ml_amd.records.batch import RawBatch, utf16_units
+    texts = ["\u0436" * n_units if i == k else raw.text_of(i) for i in range(raw.n)]
+    units = [utf16_units(t) for t in texts]
+    off = np.zeros(raw.n + 1, np.int64)
+    off[1:] = np.cumsum([u.shape[0] for u in units])
+    return RawBatch(np.concatenate(units), off, raw.is_retweet, raw.scalars, raw.batch_time_ms)
+
+
+@pytest.mark.parametrize("F,hash,wide,longrow", [(1000, "java", False, False), (1 << 20, "java", False, False),
+                                                 (1 << 20, "murmur3", False, False),
+                                                 (1000, "java", True, False), (1 << 20, "java", False, True)])
+def test_featurize_matches_oracle(hip_module, F, hash, wide, longrow):
+    """Featurize == oracle; also covers the wire encodings: wide (int64)
+    scalar columns and the plain-offsets fallback of a >= 16 KiB row."""
     cfg = SynthConfig.profile("twitter", seed=11, special_fraction=0.05, unicode_fraction=0.3)
     raw = generate_batch(cfg, 0, 3000, batch_time_ms=NOW)
     if wide:   # followers / createdAt ranges beyond 32 bits: those columns ship as int64
         raw.scalars[1, 5] = (1 << 40) + 7
         raw.scalars[4, 9] = 0
+    if longrow:
+        raw = _with_long_row(raw)
+        raw.scalars[0, 3] = 500   # keep it: it passes the [100, 1000] filter
+        raw.is_retweet[3] = True
     eng = _engine(F, hash, lazy_idx=False)   # every hashed id kept for inspection
     eng.train_batch(raw, want_pred=True)
-    sw = eng._staging[0]._hb.scalar_wire
+    hb = eng._staging[0]
+    sw = hb._hb.scalar_wire
     assert sw["rows"] == raw.n
     assert sw["wide_mask"] == (0b10010 if wide else 0), sw
+    assert hb.rows_packed == (not longrow)
     dbg = eng._eng.debug_prepared()
     fb = featurize_batch(raw, F, 100, 1000, now_ms=NOW, hash=hash)
     assert int(dbg["counters"][0]) == fb.n

@@ -93,7 +93,9 @@ class HostBatchView:
     narrow (Latin-1, 1 byte/unit) / wide (UTF-16LE) rows with the native
     multi-threaded packer (``csrc/host/wire.cpp``): typical tweet text
     crosses PCIe at half the UTF-16 size.  The five int64 scalar columns
-    ship as u32 offsets from a per-batch base when their range fits (exact).
+    ship as u32 offsets from a per-batch base when their range fits (exact),
+    and a row's byte offset + flags as one u16 (length | flags << 14) that
+    the device scans back into offsets (rows of >= 16 KiB: plain offsets).
     """
 
     def __init__(self, max_rows: int, max_units: int):
@@ -107,6 +109,7 @@ class HostBatchView:
         self.units = 0
         self.bytes = 0
         self.batch_time_ms = 0
+        self.rows_packed = False
 
     @property
     def max_rows(self) -> int:
@@ -125,6 +128,7 @@ class HostBatchView:
                                           self.offsets, self.flags))
         self.scalars_flat[:5 * n] = raw.scalars.reshape(-1)
         self._hb.pack_scalars(n)   # u32 + per-batch base where a column's range fits
+        self.rows_packed = bool(self._hb.pack_rows(n))   # offsets + flags as 2 B per row
         self.n, self.units, self.batch_time_ms = n, u, raw.batch_time_ms
         return self
 
