@@ -137,7 +137,11 @@ PYBIND11_MODULE(_twtml_hip, m) {
         std::vector<int64_t> off(h.soff, h.soff + kScalarCols + 1), base(h.sbase, h.sbase + kScalarCols);
         d["offsets"] = off;
         d["base"] = base;
-        d["wide_mask"] = h.swide;
+        std::vector<int> w(h.sw, h.sw + kScalarCols);
+        d["widths"] = w;
+        int mask = 0;
+        for (int c = 0; c < kScalarCols; ++c) mask |= (h.sw[c] == 8 ? 1 : 0) << c;
+        d["wide_mask"] = mask;
         d["rows"] = h.spacked_n;
         return d;
       });

@@ -48,23 +48,32 @@ void HostBatch::pack_scalars(int64_t n) {
   for (int c = 0; c < kScalarCols; ++c) th.emplace_back(range, c);
   for (auto& x : th) x.join();
   th.clear();
-  swide = 0;
   soff[0] = 0;
   for (int c = 0; c < kScalarCols; ++c) {
-    // range test in unsigned arithmetic (hi - lo may overflow int64)
-    const bool narrow = uint64_t(hi[c]) - uint64_t(lo[c]) <= uint64_t(UINT32_MAX);
-    if (!narrow) swide |= 1 << c;
-    sbase[c] = narrow ? lo[c] : 0;
-    soff[c + 1] = soff[c] + (narrow ? 4 : 8) * n;
+    // range in unsigned arithmetic (hi - lo may overflow int64)
+    const uint64_t span = uint64_t(hi[c]) - uint64_t(lo[c]);
+    const int w = span < (1ull << 8) ? 1 : span < (1ull << 16) ? 2 : span < (1ull << 24) ? 3
+                : span <= uint64_t(UINT32_MAX) ? 4 : 8;
+    sw[c] = uint8_t(w);
+    sbase[c] = w == 8 ? 0 : lo[c];
+    soff[c + 1] = soff[c] + int64_t(w) * n;
   }
   auto put = [&](int c) {
     const int64_t* v = scalars + int64_t(c) * n;
-    if (swide & (1 << c)) {
-      std::memcpy(spack + soff[c], v, sizeof(int64_t) * size_t(n));
-    } else {
-      uint32_t* o = reinterpret_cast<uint32_t*>(spack + soff[c]);
-      const uint64_t b = uint64_t(sbase[c]);
-      for (int64_t i = 0; i < n; ++i) o[i] = uint32_t(uint64_t(v[i]) - b);
+    uint8_t* o = spack + soff[c];
+    const uint64_t b = uint64_t(sbase[c]);
+    switch (sw[c]) {
+      case 8: std::memcpy(o, v, sizeof(int64_t) * size_t(n)); break;
+      case 4: for (int64_t i = 0; i < n; ++i) reinterpret_cast<uint32_t*>(o)[i] = uint32_t(uint64_t(v[i]) - b); break;
+      case 2: for (int64_t i = 0; i < n; ++i) reinterpret_cast<uint16_t*>(o)[i] = uint16_t(uint64_t(v[i]) - b); break;
+      case 1: for (int64_t i = 0; i < n; ++i) o[i] = uint8_t(uint64_t(v[i]) - b); break;
+      default:
+        for (int64_t i = 0; i < n; ++i) {
+          const uint32_t x = uint32_t(uint64_t(v[i]) - b);
+          o[3 * i] = uint8_t(x);
+          o[3 * i + 1] = uint8_t(x >> 8);
+          o[3 * i + 2] = uint8_t(x >> 16);
+        }
     }
   };
   for (int c = 0; c < kScalarCols; ++c) th.emplace_back(put, c);

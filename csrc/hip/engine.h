@@ -55,9 +55,9 @@ struct HostBatch {
   uint8_t* flags = nullptr;
   int64_t* scalars = nullptr;
   uint8_t* spack = nullptr;            // packed columns, column c at soff[c]
-  int64_t soff[kScalarCols + 1] = {};  // byte offsets; soff[c+1]-soff[c] = 4n or 8n
+  int64_t soff[kScalarCols + 1] = {};  // byte offsets; soff[c+1]-soff[c] = sw[c] * n
   int64_t sbase[kScalarCols] = {};
-  int32_t swide = 0;                   // bit c: column c is int64 on the wire
+  uint8_t sw[kScalarCols] = {};        // wire bytes per value (DevRawBatch::sw)
   int64_t spacked_n = -1;              // rows of the last pack_scalars (-1: none)
   uint16_t* rowpack = nullptr;         // per row: byte length | wire flags << 14
   int64_t rowpacked_n = -1;            // rows of the last successful pack_rows (-1: none)

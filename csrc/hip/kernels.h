@@ -21,29 +21,38 @@ namespace twtml {
 // Raw batch in the wire format (csrc/host/wire.h).
 //
 // Scalar columns (retweetCount, followers, favourites, friends, createdAt) are
-// int64 in the record; on the wire a column whose batch range fits 32 bits is
-// a u32 offset from a per-batch base (HostBatch::pack_scalars), halving their
-// PCIe bytes on real and synthetic streams (counts are small, createdAt spans
-// far less than 49 days within a batch); a column that does not fit ships as
-// int64.  Exact either way.
+// int64 in the record; on the wire column c is the offset from a per-batch
+// base in the fewest bytes that hold the batch's range (1, 2, 3 or 4 bytes,
+// little endian), or the raw int64 if the range needs more than 32 bits
+// (HostBatch::pack_scalars).  Counts are small and createdAt spans far less
+// than 49 days within a batch, so a tweet's five scalars take ~14 B instead
+// of 40.  Exact either way.
 constexpr int kScalarCols = 5;
 
 struct DevRawBatch {
   const uint8_t* text;      // [bytes] narrow (1 B/unit) or wide (UTF-16LE) rows
   const int64_t* offsets;   // [n+1] byte offsets
   const uint8_t* flags;     // [n] bit0 isRetweet, bit1 wide
-  const uint8_t* scol[kScalarCols];   // column c: u32[n] (+ sbase[c]) or int64[n]
+  const uint8_t* scol[kScalarCols];   // column c: n values of sw[c] bytes (+ sbase[c])
   int64_t sbase[kScalarCols];
-  int32_t swide;            // bit c: column c ships as int64
+  uint8_t sw[kScalarCols];  // bytes per value: 1..4 (offset from sbase) or 8 (raw int64)
   int64_t n;                // rows in this batch (host-known)
   int64_t bytes;
 };
 
-// Scalar column c of raw row r (c is a compile-time constant at every call
-// site, so the width test is one scalar branch).
+// Scalar column c of raw row r (the width test is wave-uniform).
 __device__ __forceinline__ int64_t raw_scalar(const DevRawBatch& b, int c, int64_t r) {
-  if (b.swide & (1 << c)) return reinterpret_cast<const int64_t*>(b.scol[c])[r];
-  return b.sbase[c] + int64_t(reinterpret_cast<const uint32_t*>(b.scol[c])[r]);
+  const uint8_t* p = b.scol[c];
+  switch (b.sw[c]) {
+    case 8: return reinterpret_cast<const int64_t*>(p)[r];
+    case 4: return b.sbase[c] + int64_t(reinterpret_cast<const uint32_t*>(p)[r]);
+    case 2: return b.sbase[c] + int64_t(reinterpret_cast<const uint16_t*>(p)[r]);
+    case 1: return b.sbase[c] + int64_t(p[r]);
+    default: {   // 3 bytes
+      const uint8_t* q = p + 3 * r;
+      return b.sbase[c] + int64_t(uint32_t(q[0]) | (uint32_t(q[1]) << 8) | (uint32_t(q[2]) << 16));
+    }
+  }
 }
 
 constexpr uint8_t kRowRetweet = 1;

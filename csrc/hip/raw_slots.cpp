@@ -85,8 +85,8 @@ void RawSlots::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, h
   for (int c = 0; c < kScalarCols; ++c) {
     s.soff[c] = hb.soff[c];
     s.sbase[c] = hb.sbase[c];
+    s.sw[c] = hb.sw[c];
   }
-  s.swide = hb.swide;
   s.packed = packed;
   s.n = n;
   s.bytes = bytes;
@@ -106,8 +106,8 @@ DevRawBatch RawSlots::acquire(int slot, hipStream_t compute) {
   for (int c = 0; c < kScalarCols; ++c) {
     b.scol[c] = sc + s.soff[c];
     b.sbase[c] = s.sbase[c];
+    b.sw[c] = s.sw[c];
   }
-  b.swide = s.swide;
   b.n = s.n;
   b.bytes = s.bytes;
   return b;

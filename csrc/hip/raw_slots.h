@@ -55,7 +55,7 @@ class RawSlots {
     bool packed = false;
     int64_t soff[kScalarCols] = {};
     int64_t sbase[kScalarCols] = {};
-    int32_t swide = 0;
+    uint8_t sw[kScalarCols] = {};
     int64_t n = 0, bytes = 0;
     hipEvent_t h2d_done = nullptr, consumed = nullptr;
     bool used = false;
