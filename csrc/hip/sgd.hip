@@ -508,6 +508,10 @@ __device__ __forceinline__ void hot_digits(const DevPrepared& p, const float* wl
   }
 }
 
+__device__ __forceinline__ float sgpr_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+}
+
 // wctr: the workgroup's LDS chunk counter, zeroed by hyb_lds_init.
 template <bool STATS, bool SAMPLE, int REP>
 __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, const SgdParams& sp,
@@ -525,7 +529,9 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
   const uint4* hdense = reinterpret_cast<const uint4*>(p.hot_dense);
   const int32_t* __restrict__ clen8c = p.clen8c;
   const int64_t* __restrict__ cbase = p.cbase;
-  const float w0 = wl[0], w1 = wl[1], w2 = wl[2], w3 = wl[3];
+  // the 4 numeric-feature weights are wave-uniform: SGPRs, not 4 VGPRs (the
+  // chunk loop sits at the 128-VGPR limit of 1024-thread workgroups)
+  const float w0 = sgpr_f(wl[0]), w1 = sgpr_f(wl[1]), w2 = sgpr_f(wl[2]), w3 = sgpr_f(wl[3]);
   const uint32_t* wq = whl + t * kHotLdsStride;
   f32x2 gh[kHotPerLane / 2];
 #pragma unroll
