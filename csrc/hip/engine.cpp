@@ -182,6 +182,7 @@ void LREngine::alloc_prepared() {
   prep_.num = dmalloc<float>(4 * size_t(R16));
   prep_.perm = dmalloc<int32_t>(size_t(R16));
   prep_.rtext = dmalloc<int64_t>(size_t(R16));
+  prep_.scan_tmp = dmalloc<int64_t>(size_t(C) / 8192 + 2);
   // active-feature flags: Java-hash bigrams are < 2^21 whatever F is
   const int64_t F = cfg_.num_text_features;
   int64_t fl = cfg_.hash_kind == 0 ? std::min<int64_t>(F, int64_t(1) << 21) : F;
@@ -282,7 +283,7 @@ LREngine::~LREngine() {
   void* bufs[] = {prep_.kept, prep_.nnz, prep_.sorted, prep_.blk, prep_.hist, prep_.clen8, prep_.cfast,
                   prep_.clen8d, prep_.cnt, prep_.cslot, prep_.hot_dense, prep_.clen8c,
                   prep_.hot_slot, prep_.hot_of, prep_.slot_hist, prep_.code,
-                  prep_.cbase, prep_.idx, prep_.slot, prep_.y, prep_.num, prep_.perm, prep_.rtext,
+                  prep_.cbase, prep_.idx, prep_.slot, prep_.y, prep_.num, prep_.perm, prep_.rtext, prep_.scan_tmp,
                   prep_.flags, prep_.uniq, prep_.slot_of, prep_.ublk, prep_.counters,
                   sgd_.w64, sgd_.wc64, sgd_.wc32, sgd_.g64, sgd_.red64, sgd_.stats, sgd_.state,
                   sgd_.loss_hist, sgd_.pred_out, sgd_.nrm, sgd_.wnorm_next, sgd_.part, sgd_.itrec, coh_.part, coh_.w32, coh_.norms, coh_.bar, gd_tdbg_, iter_tdbg_, lower_page_, lower_blocks_, n_global_};

@@ -39,18 +39,23 @@ namespace twtml {
 constexpr int kScanPer = 8;
 constexpr int kScanTile = 1024 * kScanPer;
 
+// Block b scans [b * span, min(n, (b + 1) * span)) starting from carry_in[b]
+// (0 without carry_in); single block: span = n.
 __global__ __launch_bounds__(1024) void k_scan_excl(const int64_t* in, int64_t* out, int64_t n,
-                                                    int64_t* total) {
+                                                    int64_t* total, const int64_t* carry_in = nullptr,
+                                                    int64_t span = 0) {
   __shared__ int64_t tile_v[kScanTile + kScanTile / 32];   // +1 word per 32: fewer bank conflicts
   __shared__ int64_t wsum[16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   auto at = [](int i) { return i + (i >> 5); };
-  int64_t carry = 0;
-  for (int64_t base = 0; base < n; base += kScanTile) {
+  int64_t carry = carry_in ? carry_in[blockIdx.x] : 0;
+  const int64_t b0 = carry_in ? int64_t(blockIdx.x) * span : 0;
+  const int64_t b1 = carry_in ? (b0 + span < n ? b0 + span : n) : n;
+  for (int64_t base = b0; base < b1; base += kScanTile) {
 #pragma unroll
     for (int k = 0; k < kScanPer; ++k) {
       const int64_t i = base + k * 1024 + tid;
-      tile_v[at(k * 1024 + tid)] = i < n ? in[i] : 0;
+      tile_v[at(k * 1024 + tid)] = i < b1 ? in[i] : 0;
     }
     __syncthreads();
     int64_t v[kScanPer];
@@ -85,16 +90,51 @@ __global__ __launch_bounds__(1024) void k_scan_excl(const int64_t* in, int64_t* 
 #pragma unroll
     for (int k = 0; k < kScanPer; ++k) {
       const int64_t i = base + k * 1024 + tid;
-      if (i < n) out[i] = tile_v[at(k * 1024 + tid)];
+      if (i < b1) out[i] = tile_v[at(k * 1024 + tid)];
     }
     carry += tot;
     __syncthreads();
   }
-  if (tid == 0 && total) *total = carry;
+  if (tid == 0 && total && !carry_in) *total = carry;
+}
+
+// Tile sums for the multi-block scan: block b sums in[b * kScanTile, ...).
+__global__ __launch_bounds__(1024) void k_tile_sum(const int64_t* in, int64_t n, int64_t* tsum) {
+  __shared__ int64_t wsum[16];
+  int64_t v = 0;
+  const int64_t b0 = int64_t(blockIdx.x) * kScanTile;
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    const int64_t i = b0 + k * 1024 + threadIdx.x;
+    v += i < n ? in[i] : 0;
+  }
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t t = 0;
+    for (int k = 0; k < 16; ++k) t += wsum[k];
+    tsum[blockIdx.x] = t;
+  }
 }
 
 static void scan_excl(const int64_t* in, int64_t* out, int64_t n, int64_t* total, hipStream_t s) {
-  hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, s, in, out, n, total);
+  hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, s, in, out, n, total, nullptr, int64_t(0));
+}
+
+// Multi-block exclusive scan (in place safe): tile sums, a single-block scan
+// of them, then every tile scanned from its offset.  tsum: ceil(n / 8192) + 1.
+static void scan_excl_big(const int64_t* in, int64_t* out, int64_t n, int64_t* total, int64_t* tsum,
+                          hipStream_t s) {
+  if (n <= kScanTile) {
+    scan_excl(in, out, n, total, s);
+    return;
+  }
+  const int tiles = int((n + kScanTile - 1) / kScanTile);
+  hipLaunchKernelGGL(k_tile_sum, dim3(tiles), dim3(1024), 0, s, in, n, tsum);
+  scan_excl(tsum, tsum, tiles, total, s);
+  hipLaunchKernelGGL(k_scan_excl, dim3(tiles), dim3(1024), 0, s, in, out, n, nullptr,
+                     static_cast<const int64_t*>(tsum), int64_t(kScanTile));
 }
 
 void scan_excl_launch(const int64_t* in, int64_t* out, int64_t n, int64_t* total, hipStream_t s) {
@@ -404,7 +444,7 @@ void launch_chunk_layout(const DevRawBatch& b, const DevPrepared& p, hipStream_t
   if (grid > 4096) grid = 4096;
   hipLaunchKernelGGL(k_chunk_len, dim3(grid), dim3(kBlock), 0, s, p.sorted, p.nnz, p.counters,
                      cmax, p.cbase, p.clen8, p.cfast);
-  scan_excl(p.cbase, p.cbase, cmax, &p.counters[2], s);
+  scan_excl_big(p.cbase, p.cbase, cmax, &p.counters[2], p.scan_tmp, s);
 }
 
 // ---------------------------------------------------------------------------

@@ -102,6 +102,7 @@ struct DevPrepared {
   float* num;               // [4][R16] numeric features (SoA by sorted position)
   int32_t* perm;            // [R16] kept index at sorted position p, -1 if none
   int64_t* rtext;           // [R16] fast chunks: text byte offset * 512 + length of the row at p
+  int64_t* scan_tmp;        // [C/8192+2] tile sums of the multi-block chunk-base scan
   // active set
   uint8_t* flags;           // [Fh]
   int32_t* uniq;            // [Fh]  sorted touched feature ids
