@@ -13,9 +13,9 @@ step() {  # step <name> <seconds> <cmd...>
   return 0
 }
 [ -z "$SKIP_TESTS" ] && TAIL=12 step pytest_gpu 500 python -m pytest tests -q -m gpu
-step bench_lr 300 python bench.py --steps 10 --warmup 2
-step bench_km 300 python bench.py --model kmeans --steps 10 --warmup 2
-step bench_wide 400 python bench.py --features 100000000 --hash murmur3 --steps 10 --warmup 2
+step bench_lr 300 python bench.py --steps 20 --warmup 3
+step bench_km 300 python bench.py --model kmeans --steps 20 --warmup 3
+step bench_wide 400 python bench.py --features 100000000 --hash murmur3 --steps 20 --warmup 3
 if [ -n "$PROFILE" ]; then
   rm -rf gpurun_out/prof_lr
   step prof_lr 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d gpurun_out/prof_lr -o run -- python bench.py --steps 5 --warmup 1
