@@ -84,13 +84,18 @@ void HostBatch::pack_scalars(int64_t n) {
 bool HostBatch::pack_rows(int64_t n) {
   if (n < 0 || n > max_rows) throw std::invalid_argument("pack_rows: bad row count");
   rowpacked_n = -1;
+  int64_t cesu = 0;
+  bool fits = true;
   for (int64_t i = 0; i < n; ++i) {
     const int64_t len = offsets[i + 1] - offsets[i];
-    if (len < 0 || len >= (int64_t(1) << kRowLenBits)) return false;
-    rowpack[i] = uint16_t(len | (int64_t(flags[i] & 3) << kRowLenBits));
+    cesu += (flags[i] & kRowCesu) ? 1 : 0;
+    if (len < 0 || len >= (int64_t(1) << kRowLenBits)) fits = false;
+    else rowpack[i] = uint16_t(len | (int64_t(flags[i] & 7) << kRowLenBits));
   }
-  rowpacked_n = n;
-  return true;
+  cesu_rows = cesu;
+  rows_scanned_n = n;
+  if (fits) rowpacked_n = n;
+  return fits;
 }
 
 HostBatch::~HostBatch() {

@@ -59,8 +59,10 @@ struct HostBatch {
   int64_t sbase[kScalarCols] = {};
   uint8_t sw[kScalarCols] = {};        // wire bytes per value (DevRawBatch::sw)
   int64_t spacked_n = -1;              // rows of the last pack_scalars (-1: none)
-  uint16_t* rowpack = nullptr;         // per row: byte length | wire flags << 14
+  uint16_t* rowpack = nullptr;         // per row: byte length | wire flags << kRowLenBits
   int64_t rowpacked_n = -1;            // rows of the last successful pack_rows (-1: none)
+  int64_t cesu_rows = 0;               // cesu rows of the last pack_rows (device expands them)
+  int64_t rows_scanned_n = -1;         // rows of the last pack_rows call (fit or not)
   int64_t max_rows = 0, max_bytes = 0;
   HostBatch(int64_t rows, int64_t text_bytes);
   ~HostBatch();
@@ -68,7 +70,8 @@ struct HostBatch {
   void pack_scalars(int64_t n);
   // Offsets + flags of rows [0, n) as one u16 per row (the device rebuilds
   // both with a scan): 9 -> 2 bytes per row on PCIe.  False (and the batch
-  // ships offsets + flags as before) if a row has >= 16384 wire bytes.
+  // ships offsets + flags as before) if a row has >= 8192 wire bytes.
+  // Also counts the cesu rows (either way).
   bool pack_rows(int64_t n);
 };
 

@@ -231,6 +231,72 @@ void launch_unpack_rows(const uint16_t* rowpack, int64_t n, int64_t* offsets, ui
   hipLaunchKernelGGL(k_rows_scan, dim3(tiles), dim3(1024), 0, s, rowpack, n, tsum, offsets, flags);
 }
 
+// ---------------------------------------------------------------------------
+// cesu wire rows (csrc/host/wire.h) -> UTF-16LE rows after the wire bytes.
+// A row of B wire bytes has at most B units, so it expands into
+// [tail + 2 * start, tail + 2 * end): no count or scan pass.  A wave takes
+// 64 rows; lane l owns row l's offsets / flags, and the wave walks the cesu
+// rows among them (ballot) together: 64 bytes per step, a unit starts at
+// every non-continuation byte, its index is the running count plus a
+// popcount of the lead-byte mask below the lane.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t lanes_below() {
+  return (uint64_t(1) << lane_id()) - 1u;
+}
+
+__global__ __launch_bounds__(256) void k_cesu_decode(uint8_t* text, const int64_t* offsets, uint8_t* flags,
+                                                     int64_t n, int64_t tail, int64_t* rstart, int64_t* rend) {
+  const int lane = lane_id();
+  const int64_t wave = (int64_t(blockIdx.x) * 256 + threadIdx.x) / kWave;
+  const int64_t nwaves = int64_t(gridDim.x) * 256 / kWave;
+  for (int64_t g = wave; g * kWave < n; g += nwaves) {
+    const int64_t r = g * kWave + lane;
+    const uint8_t fl = r < n ? flags[r] : 0;
+    const bool mine = r < n && (fl & kRowCesu);
+    int64_t s0 = r < n ? offsets[r] : 0, s1 = r < n ? offsets[r + 1] : 0;
+    uint64_t m = __ballot(mine);
+    while (m) {
+      const int l = __builtin_ctzll(m);
+      m &= m - 1;
+      const int64_t rr = g * kWave + l;
+      const int64_t o = offsets[rr], e = offsets[rr + 1];
+      const int64_t d0 = tail + 2 * o;
+      uint16_t* dst = reinterpret_cast<uint16_t*>(text + d0);
+      int64_t k = 0;
+      for (int64_t i0 = o; i0 < e; i0 += kWave) {
+        const int64_t i = i0 + lane;
+        const uint32_t b0 = i < e ? text[i] : 0x80u;
+        const bool lead = i < e && (b0 & 0xC0u) != 0x80u;
+        const uint64_t lm = __ballot(lead);
+        if (lead) {
+          uint32_t u = b0;
+          if (b0 >= 0xE0u) u = ((b0 & 0x0Fu) << 12) | ((text[i + 1] & 0x3Fu) << 6) | (text[i + 2] & 0x3Fu);
+          else if (b0 >= 0x80u) u = ((b0 & 0x1Fu) << 6) | (text[i + 1] & 0x3Fu);
+          dst[k + __popcll(lm & lanes_below())] = uint16_t(u);
+        }
+        k += __popcll(lm);
+      }
+      if (lane == l) {
+        s0 = d0;
+        s1 = d0 + 2 * k;
+      }
+    }
+    if (r < n) {
+      rstart[r] = s0;
+      rend[r] = s1;
+      if (mine) flags[r] = uint8_t((fl & ~kRowCesu) | kRowWide);
+    }
+  }
+}
+
+void launch_cesu_expand(uint8_t* text, const int64_t* offsets, uint8_t* flags, int64_t n, int64_t tail,
+                        int64_t* rstart, int64_t* rend, hipStream_t s) {
+  if (n <= 0) return;
+  // one wave per 64 rows, ~4 waves per SIMD
+  const int grid = int(std::min<int64_t>((n + 255) / 256, 4096));
+  hipLaunchKernelGGL(k_cesu_decode, dim3(grid), dim3(256), 0, s, text, offsets, flags, n, tail, rstart, rend);
+}
+
 // nnz[k] carries the row's bigram count in bits 0..29 and the wide (UTF-16
 // wire) flag in bit 30.  Sort key: narrow rows first, then wide rows, each
 // by descending length, so a chunk mixes narrow and wide rows at most once

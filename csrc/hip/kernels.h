@@ -31,8 +31,9 @@ constexpr int kScalarCols = 5;
 
 struct DevRawBatch {
   const uint8_t* text;      // [bytes] narrow (1 B/unit) or wide (UTF-16LE) rows
-  const int64_t* offsets;   // [n+1] byte offsets
-  const uint8_t* flags;     // [n] bit0 isRetweet, bit1 wide
+  const int64_t* offsets;   // [n] byte offset where row r starts
+  const int64_t* oend;      // [n] byte offset where it ends (offsets + 1 unless rows were relocated)
+  const uint8_t* flags;     // [n] bit0 isRetweet, bit1 wide (cesu rows are expanded to wide)
   const uint8_t* scol[kScalarCols];   // column c: n values of sw[c] bytes (+ sbase[c])
   int64_t sbase[kScalarCols];
   uint8_t sw[kScalarCols];  // bytes per value: 1..4 (offset from sbase) or 8 (raw int64)
@@ -57,9 +58,15 @@ __device__ __forceinline__ int64_t raw_scalar(const DevRawBatch& b, int c, int64
 
 constexpr uint8_t kRowRetweet = 1;
 constexpr uint8_t kRowWide = 2;
+constexpr uint8_t kRowCesu = 4;   // wire only (csrc/host/wire.h); expanded by launch_cesu_expand
 // Packed row words on the wire (HostBatch::pack_rows): byte length in the
-// low kRowLenBits bits, the two flag bits above.
-constexpr int kRowLenBits = 14;
+// low kRowLenBits bits, the three flag bits above.
+constexpr int kRowLenBits = 13;
+// cesu rows -> UTF-16LE rows behind the wire bytes (row with wire bytes
+// [o, e) -> from byte tail + 2 * o); writes every row's start / end offset
+// and turns the cesu rows' flags wide.  text needs tail + 2 * bytes + 64.
+void launch_cesu_expand(uint8_t* text, const int64_t* offsets, uint8_t* flags, int64_t n, int64_t tail,
+                        int64_t* rstart, int64_t* rend, hipStream_t s);
 // Rebuild offsets [n+1] (exclusive scan of the lengths) and flags [n] from
 // packed row words on `s`; tsum: scratch of ceil(n / 8192) int64.
 void launch_unpack_rows(const uint16_t* rowpack, int64_t n, int64_t* offsets, uint8_t* flags, int64_t* tsum,
@@ -74,7 +81,7 @@ struct RowText {
 __device__ __forceinline__ RowText row_text(const DevRawBatch& b, int64_t r) {
   const int64_t o = b.offsets[r];
   const int wide = (b.flags[r] & kRowWide) ? 1 : 0;
-  return RowText{o, (b.offsets[r + 1] - o) >> wide, wide};
+  return RowText{o, (b.oend[r] - o) >> wide, wide};
 }
 
 // UTF-16 unit j of a row (wide rows may be unaligned: assembled from bytes)

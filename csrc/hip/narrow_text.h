@@ -145,7 +145,7 @@ __device__ __forceinline__ void narrow_lane_load(const DevRawBatch& b, const Dev
   const int32_t mkidx = mvalid ? p.sorted[mpos] : -1;
   const int64_t mrow = mvalid ? p.kept[mkidx] : 0;
   const int64_t mo = mvalid ? b.offsets[mrow] : 0;
-  const int64_t mlen = mvalid ? b.offsets[mrow + 1] - mo : 0;
+  const int64_t mlen = mvalid ? b.oend[mrow] - mo : 0;
   if (rt) *rt = (mo << kRtextShift) | mlen;
   L.pos = c * kRowsPerChunk + r;
   L.valid = L.pos < n_kept;

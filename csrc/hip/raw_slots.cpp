@@ -25,12 +25,16 @@ void RawSlots::init(int64_t max_rows, int64_t max_bytes) {
   max_rows_ = max_rows;
   max_bytes_ = max_bytes;
   for (auto& s : slots_) {
-    s.text = slot_alloc<uint8_t>(size_t(max_bytes) + 128);   // slack: featurize over-reads <= 80 B
+    // wire bytes + cesu rows expanded behind them (UTF-16: at most twice the
+    // wire bytes of those rows); slack: featurize over-reads <= 80 B
+    s.text = slot_alloc<uint8_t>(3 * size_t(max_bytes) + 256);
     s.offsets = slot_alloc<int64_t>(size_t(max_rows) + 1);
     s.flags = slot_alloc<uint8_t>(size_t(max_rows));
     s.scalars = slot_alloc<int64_t>(5 * size_t(max_rows));
     s.rowpack = slot_alloc<uint16_t>(size_t(max_rows) + 8);
     s.tsum = slot_alloc<int64_t>(size_t(max_rows) / 8192 + 2);
+    s.rstart = slot_alloc<int64_t>(size_t(max_rows) + 1);
+    s.rend = slot_alloc<int64_t>(size_t(max_rows) + 1);
     TWTML_HIP_CHECK(hipEventCreateWithFlags(&s.h2d_done, hipEventDisableTiming));
     TWTML_HIP_CHECK(hipEventCreateWithFlags(&s.consumed, hipEventDisableTiming));
   }
@@ -44,6 +48,8 @@ void RawSlots::release() {
     if (s.scalars) (void)hipFree(s.scalars);
     if (s.rowpack) (void)hipFree(s.rowpack);
     if (s.tsum) (void)hipFree(s.tsum);
+    if (s.rstart) (void)hipFree(s.rstart);
+    if (s.rend) (void)hipFree(s.rend);
     if (s.h2d_done) (void)hipEventDestroy(s.h2d_done);
     if (s.consumed) (void)hipEventDestroy(s.consumed);
     s = Slot{};
@@ -59,6 +65,7 @@ void RawSlots::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, h
     throw std::invalid_argument("text bytes exceed capacity");
   if (hb.offsets[0] != 0 || hb.offsets[n] != bytes) throw std::invalid_argument("offsets[n] != bytes");
   if (n > 0 && hb.spacked_n != n) throw std::logic_error("HostBatch scalars not packed for this row count");
+  if (n > 0 && hb.rows_scanned_n != n) throw std::logic_error("HostBatch rows not packed (pack_rows) for this row count");
   // wait until the compute stream has finished reading this slot
   if (s.used) TWTML_HIP_CHECK(hipStreamWaitEvent(copy, s.consumed, 0));
   if (bytes > 0)
@@ -88,6 +95,7 @@ void RawSlots::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, h
     s.sw[c] = hb.sw[c];
   }
   s.packed = packed;
+  s.cesu_rows = n > 0 ? hb.cesu_rows : 0;
   s.n = n;
   s.bytes = bytes;
   s.used = true;
@@ -101,7 +109,14 @@ DevRawBatch RawSlots::acquire(int slot, hipStream_t compute) {
   DevRawBatch b{};
   b.text = s.text;
   b.offsets = s.offsets;
+  b.oend = s.offsets + 1;
   b.flags = s.flags;
+  if (s.cesu_rows > 0) {   // expand cesu rows behind the wire bytes (16-byte aligned)
+    const int64_t tail = (s.bytes + 15) / 16 * 16;
+    launch_cesu_expand(s.text, s.offsets, s.flags, s.n, tail, s.rstart, s.rend, compute);
+    b.offsets = s.rstart;
+    b.oend = s.rend;
+  }
   const uint8_t* sc = reinterpret_cast<const uint8_t*>(s.scalars);
   for (int c = 0; c < kScalarCols; ++c) {
     b.scol[c] = sc + s.soff[c];

@@ -41,6 +41,8 @@ class RawSlots {
   void release_slot(int slot, hipStream_t compute);
   int64_t rows(int slot) const { return slots_[check(slot)].n; }
   int64_t max_rows() const { return max_rows_; }
+  // device text bytes per slot: the wire bytes, then room for cesu rows
+  // expanded to UTF-16 (<= 2 bytes per wire byte)
   int64_t max_bytes() const { return max_bytes_; }
 
  private:
@@ -52,6 +54,9 @@ class RawSlots {
     int64_t* scalars = nullptr;       // wire-encoded scalar columns (bytes)
     uint16_t* rowpack = nullptr;      // packed row words (when the batch shipped them)
     int64_t* tsum = nullptr;          // unpack scan scratch (per 8192-row tile)
+    int64_t* rstart = nullptr;        // cesu batches: row start / end after expansion
+    int64_t* rend = nullptr;
+    int64_t cesu_rows = 0;
     bool packed = false;
     int64_t soff[kScalarCols] = {};
     int64_t sbase[kScalarCols] = {};

@@ -42,7 +42,7 @@ __device__ __forceinline__ StageMeta stage_meta(const DevRawBatch& b, bool valid
   StageMeta m{row, 0, 0, 0, 0, 0, 0};
   if (valid) {
     m.o = b.offsets[row];
-    m.bytes = b.offsets[row + 1] - m.o;
+    m.bytes = b.oend[row] - m.o;
     m.wide = (b.flags[row] & kRowWide) ? 1 : 0;
   }
   m.aligned = m.o & ~int64_t(3);

@@ -135,11 +135,11 @@ PYBIND11_MODULE(_twtml_host, m) {
         },
         py::arg("text"), py::arg("offsets"), py::arg("is_rt"), py::arg("out"), py::arg("out_offsets"),
         py::arg("flags"), py::arg("nthreads") = 0,
-        "Pack a UTF-16 batch into the narrow/wide wire format; returns bytes written.");
+        "Pack a UTF-16 batch into the narrow/cesu/wide wire format; returns bytes written.");
   m.def("wire_unpack", [](Arr<uint8_t> wire, Arr<int64_t> woff, Arr<uint8_t> flags) {
     const int64_t n = int64_t(woff.size()) - 1;
     if (n < 0 || flags.size() < n) throw std::invalid_argument("woff / flags mismatch");
-    const int64_t units = wire_units(woff.data(), flags.data(), n);
+    const int64_t units = wire_units(wire.data(), woff.data(), flags.data(), n);
     py::array_t<uint16_t> text(units);
     py::array_t<int64_t> offsets(n + 1);
     py::array_t<uint8_t> is_rt(n);

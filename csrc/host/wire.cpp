@@ -10,10 +10,22 @@ namespace twtml {
 
 namespace {
 
-bool row_narrow(const uint16_t* t, int64_t len) {
+// Encoding of a row and its wire bytes.
+uint8_t row_kind(const uint16_t* t, int64_t len, int64_t* bytes) {
   uint16_t acc = 0;
   for (int64_t i = 0; i < len; ++i) acc |= t[i];
-  return acc < 256;
+  if (acc < 256) {
+    *bytes = len;
+    return 0;
+  }
+  int64_t c = 0;
+  for (int64_t i = 0; i < len; ++i) c += cesu_len(t[i]);
+  if (c < 2 * len) {
+    *bytes = c;
+    return kWireCesu;
+  }
+  *bytes = 2 * len;
+  return kWireWide;
 }
 
 template <typename F>
@@ -44,9 +56,10 @@ int64_t wire_pack(const uint16_t* text, const int64_t* offsets, const uint8_t* i
     int64_t pos = 0;
     for (int64_t r = r0; r < r1; ++r) {
       const int64_t len = offsets[r + 1] - offsets[r];
-      const bool narrow = row_narrow(text + offsets[r], len);
-      flags[r] = uint8_t((is_rt[r] ? kWireRetweet : 0) | (narrow ? 0 : kWireWide));
-      out_offsets[r + 1] = pos + (narrow ? len : 2 * len);   // chunk-local end
+      int64_t nb = 0;
+      const uint8_t kind = row_kind(text + offsets[r], len, &nb);
+      flags[r] = uint8_t((is_rt[r] ? kWireRetweet : 0) | kind);
+      out_offsets[r + 1] = pos + nb;   // chunk-local end
       pos = out_offsets[r + 1];
     }
     chunk_bytes[size_t(c) + 1] = pos;
@@ -68,6 +81,20 @@ int64_t wire_pack(const uint16_t* text, const int64_t* offsets, const uint8_t* i
           dst[2 * i] = uint8_t(src[i] & 0xFF);
           dst[2 * i + 1] = uint8_t(src[i] >> 8);
         }
+      } else if (flags[r] & kWireCesu) {
+        for (int64_t i = 0; i < len; ++i) {
+          const uint32_t u = src[i];
+          if (u < 0x80) {
+            *dst++ = uint8_t(u);
+          } else if (u < 0x800) {
+            *dst++ = uint8_t(0xC0 | (u >> 6));
+            *dst++ = uint8_t(0x80 | (u & 0x3F));
+          } else {
+            *dst++ = uint8_t(0xE0 | (u >> 12));
+            *dst++ = uint8_t(0x80 | ((u >> 6) & 0x3F));
+            *dst++ = uint8_t(0x80 | (u & 0x3F));
+          }
+        }
       } else {
         for (int64_t i = 0; i < len; ++i) dst[i] = uint8_t(src[i]);
       }
@@ -76,9 +103,19 @@ int64_t wire_pack(const uint16_t* text, const int64_t* offsets, const uint8_t* i
   return total;
 }
 
-int64_t wire_units(const int64_t* woff, const uint8_t* flags, int64_t n) {
+namespace {
+int64_t row_units(const uint8_t* w, int64_t nb, uint8_t fl) {
+  if (fl & kWireWide) return nb >> 1;
+  if (!(fl & kWireCesu)) return nb;
   int64_t u = 0;
-  for (int64_t r = 0; r < n; ++r) u += (woff[r + 1] - woff[r]) >> ((flags[r] & kWireWide) ? 1 : 0);
+  for (int64_t i = 0; i < nb; ++i) u += (w[i] & 0xC0) != 0x80;
+  return u;
+}
+}  // namespace
+
+int64_t wire_units(const uint8_t* wire, const int64_t* woff, const uint8_t* flags, int64_t n) {
+  int64_t u = 0;
+  for (int64_t r = 0; r < n; ++r) u += row_units(wire + woff[r], woff[r + 1] - woff[r], flags[r]);
   return u;
 }
 
@@ -86,14 +123,36 @@ void wire_unpack(const uint8_t* wire, const int64_t* woff, const uint8_t* flags,
                  uint16_t* text, int64_t* offsets, uint8_t* is_rt) {
   offsets[0] = 0;
   for (int64_t r = 0; r < n; ++r) {
-    const bool wide = flags[r] & kWireWide;
-    const int64_t len = (woff[r + 1] - woff[r]) >> (wide ? 1 : 0);
+    const uint8_t fl = flags[r];
+    const int64_t nb = woff[r + 1] - woff[r];
     const uint8_t* src = wire + woff[r];
     uint16_t* dst = text + offsets[r];
-    for (int64_t i = 0; i < len; ++i)
-      dst[i] = wide ? uint16_t(src[2 * i] | (uint16_t(src[2 * i + 1]) << 8)) : src[i];
+    int64_t len = 0;
+    if (fl & kWireWide) {
+      len = nb >> 1;
+      for (int64_t i = 0; i < len; ++i) dst[i] = uint16_t(src[2 * i] | (uint16_t(src[2 * i + 1]) << 8));
+    } else if (fl & kWireCesu) {
+      for (int64_t i = 0; i < nb;) {
+        const uint32_t b0 = src[i];
+        uint32_t u;
+        if (b0 < 0x80) {
+          u = b0;
+          i += 1;
+        } else if (b0 < 0xE0) {
+          u = ((b0 & 0x1F) << 6) | (src[i + 1] & 0x3F);
+          i += 2;
+        } else {
+          u = ((b0 & 0x0F) << 12) | ((src[i + 1] & 0x3F) << 6) | (src[i + 2] & 0x3F);
+          i += 3;
+        }
+        dst[len++] = uint16_t(u);
+      }
+    } else {
+      len = nb;
+      for (int64_t i = 0; i < len; ++i) dst[i] = src[i];
+    }
     offsets[r + 1] = offsets[r] + len;
-    is_rt[r] = flags[r] & kWireRetweet;
+    is_rt[r] = fl & kWireRetweet;
   }
 }
 

@@ -95,10 +95,21 @@ def _wire_roundtrip(raw, nthreads=0):
     np.testing.assert_array_equal(is_rt, raw.is_retweet)
     lens = np.diff(raw.offsets)
     wide = (flags & 2) != 0
-    np.testing.assert_array_equal(np.diff(woff), np.where(wide, 2 * lens, lens))
-    for r in range(min(raw.n, 200)):                       # narrow <=> every unit < 256
+    cesu = (flags & 4) != 0
+    assert not np.any(wide & cesu)
+    narrow = ~(wide | cesu)
+    nbytes = np.diff(woff)
+    np.testing.assert_array_equal(nbytes[wide], 2 * lens[wide])
+    np.testing.assert_array_equal(nbytes[narrow], lens[narrow])
+    assert np.all(nbytes[cesu] < 2 * lens[cesu])           # cesu only when smaller than UTF-16
+    for r in range(min(raw.n, 300)):
         u = raw.text[raw.offsets[r]:raw.offsets[r + 1]]
-        assert bool(wide[r]) == bool(u.size and u.max() >= 256)
+        assert bool(narrow[r]) == (not (u.size and u.max() >= 256))   # narrow <=> every unit < 256
+        if not narrow[r]:   # cesu size: 1 / 2 / 3 bytes per unit
+            c = int(np.where(u < 0x80, 1, np.where(u < 0x800, 2, 3)).sum())
+            assert cesu[r] == (c < 2 * u.size)
+            if cesu[r]:
+                assert nbytes[r] == c
     return nb
 
 
@@ -107,6 +118,22 @@ def test_wire_pack_roundtrip(n, threads):
     raw = generate_batch(SynthConfig(seed=9, unicode_fraction=0.4, special_fraction=0.05), 0, n)
     nb = _wire_roundtrip(raw, threads)
     assert nb <= 2 * raw.total_units
+
+
+def test_wire_cesu_rows_exact_for_any_units():
+    """cesu rows round-trip every UTF-16 unit sequence: lone / swapped
+    surrogates, U+07FF/U+0800 boundaries, emoji pairs, NUL."""
+    from twitter_stream_ml_amd.records.batch import RawBatch
+    rows = [[0x41, 0xD800, 0x42, 0x43, 0x44, 0x45, 0x46], [0xDC00, 0xD800, 0x61, 0x62, 0x63, 0x64],
+            [0x7F, 0x80, 0x7FF, 0x800, 0x61, 0x62, 0x63, 0x64, 0x65, 0x66],
+            [0xD83D, 0xDE00, 0x61, 0x62, 0x63, 0x64, 0x65], [0x0, 0x100, 0x61, 0x62, 0x63],
+            [0x4E2D, 0x6587], [0x61] * 3 + [0xFFFF]]
+    units = [np.array(r, np.uint16) for r in rows]
+    off = np.zeros(len(rows) + 1, np.int64)
+    off[1:] = np.cumsum([u.size for u in units])
+    raw = RawBatch(np.concatenate(units), off, np.ones(len(rows), bool),
+                   np.zeros((5, len(rows)), np.int64), 0)
+    _wire_roundtrip(raw, 1)
 
 
 @settings(max_examples=50, deadline=None)

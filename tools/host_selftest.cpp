@@ -66,7 +66,7 @@ int main(int argc, char** argv) {
   const int64_t bytes = wire_pack(lt.data(), lo.data(), rt.data(), int64_t(n), wire.data(), int64_t(wire.size()),
                                   woff.data(), flags.data(), threads);
   CHECK(bytes > 0 && bytes <= int64_t(wire.size()) && woff[n] == bytes);
-  CHECK(wire_units(woff.data(), flags.data(), int64_t(n)) == lo[n]);
+  CHECK(wire_units(wire.data(), woff.data(), flags.data(), int64_t(n)) == lo[n]);
   std::vector<uint16_t> back(static_cast<size_t>(lo[n]));
   std::vector<int64_t> boff(n + 1);
   std::vector<uint8_t> brt(n);
