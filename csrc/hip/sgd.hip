@@ -1159,16 +1159,38 @@ void launch_sgd_reduce(const DevSgd& d, const SgdParams& sp, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------
-// SimpleUpdater (fp64 master weights), 64 columns per workgroup tile.
+// SimpleUpdater (fp64 master weights), one wave per column: lane j sums the
+// partial rows j, j + 64, ... (all loads in flight) and a DPP wave sum
+// gives the column (fixed order); 16 columns per 1024-thread workgroup, so
+// a ~1.4K-slot batch spreads over ~90 CUs instead of 23.
 // nparts > 0: the column gradients are the sums of the partial rows (single
 // GPU); nparts == 0: g64 holds them (all-reduced, or the generic path).
 // ---------------------------------------------------------------------------
+constexpr int kUpdCols = 1024 / kWave;   // columns (waves) per workgroup
+
+__device__ __forceinline__ double part_col_wave(const DevSgd& d, int64_t col, int nparts) {
+  const int lane = lane_id();
+  const double* src = d.part + col;
+  const int64_t ps = d.pstride;
+  double a[kMaxPersistGrid / kWave];
+#pragma unroll
+  for (int q = 0; q < kMaxPersistGrid / kWave; ++q) {
+    const int g = lane + q * kWave;
+    a[q] = g < nparts ? src[int64_t(g) * ps] : 0.0;
+  }
+  double t = 0.0;
+  for (int g0 = kMaxPersistGrid; g0 < nparts; g0 += kWave)   // grids beyond 512 (not launched today)
+    if (g0 + lane < nparts) t += src[int64_t(g0 + lane) * ps];
+#pragma unroll
+  for (int q = 0; q < kMaxPersistGrid / kWave; ++q) t += a[q];
+  return wave_sum(t);
+}
+
 __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int nparts) {
-  __shared__ double red[16][65];
-  __shared__ double wsc[16][2];
+  __shared__ double wsc[kUpdCols][2];
   __shared__ double m_sh;
   if (d.state[0] != 0.0) return;
-  const int tid = threadIdx.x, c = tid & 63, j = tid >> 6;
+  const int tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
   const int it = sp.iteration;
   const int64_t ns = d.ns, hi = kNumNumeric + d.n_unique;
   const int64_t ncols = ns + kPartVals - kNumNumeric;
@@ -1189,18 +1211,10 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
   const double m = m_sh;
   const double alpha = sp.step_size / sqrt(double(it));
   double ds = 0.0, ws = 0.0;
-  for (int64_t tile = blockIdx.x; tile * 64 < ncols; tile += gridDim.x) {
-    const int64_t col = tile * 64 + c;
-    if (nparts > 0) {
-      red[j][c] = col < ncols ? part_col_sum(d, col, j, nparts) : 0.0;
-      __syncthreads();
-    }
-    if (j == 0 && col < ncols) {
-      double g = col <= ns ? d.g64[col] : 0.0;
-      if (nparts > 0) {
-#pragma unroll
-        for (int k = 0; k < 16; ++k) g += red[k][c];
-      }
+  for (int64_t col = int64_t(blockIdx.x) * kUpdCols + w; col < ncols; col += int64_t(gridDim.x) * kUpdCols) {
+    double g = col <= ns ? d.g64[col] : 0.0;   // wave-uniform load
+    if (nparts > 0) g += part_col_wave(d, col, nparts);
+    if (lane == 0) {
       if (col < hi) {
         if (m > 0.0) {
           const double step = alpha * (g / m);
@@ -1218,19 +1232,16 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
         d.stats[col - ns - 2] += g;     // batch stats (iteration 1, single GPU)
       }
     }
-    if (nparts > 0) __syncthreads();
   }
-  ds = wave_sum(ds);
-  ws = wave_sum(ws);
-  if (lane_id() == 0) {
-    wsc[tid / kWave][0] = ds;
-    wsc[tid / kWave][1] = ws;
+  if (lane == 0) {
+    wsc[w][0] = ds;
+    wsc[w][1] = ws;
   }
   __syncthreads();
   double* rec = sgd_rec(d, it);
   if (tid < 2) {
     double t = 0.0;
-    for (int k = 0; k < 16; ++k) t += wsc[k][tid];
+    for (int k = 0; k < kUpdCols; ++k) t += wsc[k][tid];
     rec[kRecHead + 2 * blockIdx.x + tid] = t;
   }
   if (blockIdx.x == 0 && tid == 0) {
@@ -1245,7 +1256,7 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
 }
 
 void launch_sgd_update(const DevSgd& d, const SgdParams& sp, int nparts, hipStream_t s) {
-  const int64_t tiles = (d.ns + kPartVals - kNumNumeric + 63) / 64;
+  const int64_t tiles = (d.ns + kPartVals - kNumNumeric + kUpdCols - 1) / kUpdCols;
   const int grid = int(std::min<int64_t>(tiles, kMaxUpdGrid));
   hipLaunchKernelGGL(k_sgd_update, dim3(grid), dim3(1024), 0, s, d, sp, nparts);
 }
