@@ -1109,56 +1109,6 @@ void launch_sgd_persistent(const DevSgd& d, const DevPrepared& p, const SgdParam
 // ---------------------------------------------------------------------------
 
 // ---------------------------------------------------------------------------
-// Cross-workgroup reduction of the partial rows (DP: before the all-reduce):
-// 64 columns per workgroup, 16 row strides per column, fixed summation order.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ double part_col_sum(const DevSgd& d, int64_t col, int j, int nparts) {
-  double a[16];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) a[k] = 0.0;
-  const double* src = d.part + col;
-  const int64_t ps = d.pstride;
-  int64_t g = j;
-  // 16 independent loads in flight (a dependent add chain would serialise
-  // one memory latency per partial row)
-  for (; g + 15 * 16 < nparts; g += 16 * 16) {
-#pragma unroll
-    for (int k = 0; k < 16; ++k) a[k] += src[(g + 16 * k) * ps];
-  }
-#pragma unroll
-  for (int k = 0; k < 16; ++k)
-    if (g + 16 * k < nparts) a[k] += src[(g + 16 * k) * ps];
-  double t = 0.0;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) t += a[k];
-  return t;
-}
-
-__global__ __launch_bounds__(1024) void k_sgd_reduce(DevSgd d, SgdParams sp) {
-  __shared__ double red[16][65];
-  if (d.state[0] != 0.0) return;
-  const int c = threadIdx.x & 63, j = threadIdx.x >> 6;
-  const int64_t col = int64_t(blockIdx.x) * 64 + c;
-  const int64_t ncols = d.ns + kPartVals - kNumNumeric;
-  red[j][c] = col < ncols ? part_col_sum(d, col, j, d.nparts) : 0.0;
-  __syncthreads();
-  if (j == 0 && col < ncols) {
-    double v = 0.0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) v += red[k][c];
-    if (col <= d.ns) d.g64[col] = v;                     // slots, then the loss at [ns]
-    else if (col == d.ns + 1) *sgd_red_m(d, sp.iteration) = v;   // sampled row count
-    else d.stats[col - d.ns - 2] += v;                   // batch stats (iteration 1)
-  }
-}
-
-void launch_sgd_reduce(const DevSgd& d, const SgdParams& sp, hipStream_t s) {
-  if (d.nparts <= 0) return;
-  const int grid = int((d.ns + kPartVals - kNumNumeric + 63) / 64);
-  hipLaunchKernelGGL(k_sgd_reduce, dim3(grid), dim3(1024), 0, s, d, sp);
-}
-
-// ---------------------------------------------------------------------------
 // SimpleUpdater (fp64 master weights), one wave per column: lane j sums the
 // partial rows j, j + 64, ... (all loads in flight) and a DPP wave sum
 // gives the column (fixed order); 16 columns per 1024-thread workgroup, so
@@ -1259,6 +1209,28 @@ void launch_sgd_update(const DevSgd& d, const SgdParams& sp, int nparts, hipStre
   const int64_t tiles = (d.ns + kPartVals - kNumNumeric + kUpdCols - 1) / kUpdCols;
   const int grid = int(std::min<int64_t>(tiles, kMaxUpdGrid));
   hipLaunchKernelGGL(k_sgd_update, dim3(grid), dim3(1024), 0, s, d, sp, nparts);
+}
+
+// Cross-workgroup reduction of the partial rows (DP: before the all-reduce)
+// into g64 (+ loss, sampled count, batch stats): one wave per column, fixed
+// summation order.
+__global__ __launch_bounds__(1024) void k_sgd_reduce(DevSgd d, SgdParams sp) {
+  if (d.state[0] != 0.0) return;
+  const int64_t ncols = d.ns + kPartVals - kNumNumeric;
+  const int64_t col = int64_t(blockIdx.x) * kUpdCols + threadIdx.x / kWave;
+  if (col >= ncols) return;   // wave-uniform
+  const double v = part_col_wave(d, col, d.nparts);
+  if (lane_id() == 0) {
+    if (col <= d.ns) d.g64[col] = v;                     // slots, then the loss at [ns]
+    else if (col == d.ns + 1) *sgd_red_m(d, sp.iteration) = v;   // sampled row count
+    else d.stats[col - d.ns - 2] += v;                   // batch stats (iteration 1)
+  }
+}
+
+void launch_sgd_reduce(const DevSgd& d, const SgdParams& sp, hipStream_t s) {
+  if (d.nparts <= 0) return;
+  const int grid = int((d.ns + kPartVals - kNumNumeric + kUpdCols - 1) / kUpdCols);
+  hipLaunchKernelGGL(k_sgd_reduce, dim3(grid), dim3(1024), 0, s, d, sp);
 }
 
 // Convergence of the last update (the loop ended without a prologue seeing it).
