@@ -123,8 +123,8 @@ struct DevPrepared {
   // hybrid dense-hot layout (hot_split.hip): the kHot most frequent slots of
   // the batch become 4-bit counts per row, the rest a cold SELL stream
   uint32_t* hot_dense;      // [C][64] uint4: lane (row r, quarter t) = 32 nibbles, hot ids 32t..32t+31
-  uint16_t* cslot;          // [E]   cold slots (+ count overflow), same chunk bases as slot
-  int32_t* clen8c;          // [C]   cold groups per lane; -1 = chunk left in the plain layout
+  uint16_t* cslot;          // [E]   cold slots (+ count overflow), same chunk bases as slot, kColdGroup groups
+  int32_t* clen8c;          // [C]   cold kColdGroup-entry groups per lane; -1 = chunk left in the plain layout
   int32_t* hot_slot;        // [kHot] slot of hot id h (a zero-weight pad slot when unused)
   uint8_t* hot_of;          // [kMaxHybridSlots] hot id of a slot (0xFF = cold)
   uint16_t* code;           // [8192] remap code of small hashed ids (hot_split.hip)
@@ -167,6 +167,10 @@ void launch_dedup(const DevPrepared& p, int64_t ns, int64_t pad_base, int64_t n_
 // of launch_remap: sampled slot histogram -> top-kHot selection -> per chunk
 // 4-bit hot counts + each lane's cold entries (hot_split.hip).
 constexpr int kHot = 128;
+// Cold stream of the hybrid layout: kColdGroup u16 slots per lane and group
+// (one 8-byte load), kColdStride entries per (chunk, group).
+constexpr int kColdGroup = 4;
+constexpr int kColdStride = 64 * kColdGroup;
 constexpr int kMaxHybridSlots = 16384;
 // from_text: fast chunks were featurized lazily (idx_mode 1); their ids are
 // re-derived from the raw batch b (which must still be resident)

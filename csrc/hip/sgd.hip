@@ -71,6 +71,10 @@ struct SlotLoad<uint32_t> {
   }
 };
 
+__device__ __forceinline__ void unpack4(const uint2 v, uint32_t (&s)[4]) {
+  s[0] = v.x & 0xFFFF; s[1] = v.x >> 16; s[2] = v.y & 0xFFFF; s[3] = v.y >> 16;
+}
+
 __device__ __forceinline__ void unpack8(const uint4 v, uint32_t (&s)[8]) {
   s[0] = v.x & 0xFFFF; s[1] = v.x >> 16; s[2] = v.y & 0xFFFF; s[3] = v.y >> 16;
   s[4] = v.z & 0xFFFF; s[5] = v.z >> 16; s[6] = v.w & 0xFFFF; s[7] = v.w >> 16;
@@ -410,7 +414,7 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_lds(DevSgd d, DevPrepar
 // in the plain layout (clen8c < 0) take the plain route.
 // ---------------------------------------------------------------------------
 constexpr int kHotRows = kWave / 16;  // 16-lane rows per wave (hot-gradient partials per wave)
-constexpr int kMaxColdGroups = 4;   // cold groups kept in VGPRs (cold row <= 128)
+constexpr int kMaxColdGroups = 8;   // cold 4-entry groups kept in VGPRs (32 cold entries per lane)
 constexpr int kHotPerLane = kHot / kLanesPerRow;   // 32
 
 // wq: this lane's 32 hot weights in LDS (quarter t, 16-B aligned, stride 36
@@ -576,20 +580,21 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
     const RowIn ri = row_in(p, pos);
     if (L8c >= 0) {
       const uint4 hv = hdense[c * kWave + lane];
-      const uint16_t* sl = p.cslot + off;
+      // cold stream: L8c groups of kColdGroup slots per lane (hot_split.hip)
+      const uint16_t* sl = p.cslot + cb * kChunkStride + lane * kColdGroup;
       const bool reg = L8c <= kMaxColdGroups;
-      uint4 v[kMaxColdGroups];
+      uint2 v[kMaxColdGroups];
       if (reg) {
 #pragma unroll
         for (int g = 0; g < kMaxColdGroups; ++g)
-          if (g < L8c) v[g] = *reinterpret_cast<const uint4*>(sl + int64_t(g) * kChunkStride);
+          if (g < L8c) v[g] = *reinterpret_cast<const uint2*>(sl + int64_t(g) * kColdStride);
       }
       if (abl == 6) {  // loads only: memory floor of the chunk stream
         uint32_t x = hv.x ^ hv.y ^ hv.z ^ hv.w ^ __float_as_uint(ri.y + ri.n0 + ri.n1 + ri.n2 + ri.n3);
         if (reg) {
 #pragma unroll
           for (int g = 0; g < kMaxColdGroups; ++g)
-            if (g < L8c) x ^= v[g].x ^ v[g].y ^ v[g].z ^ v[g].w;
+            if (g < L8c) x ^= v[g].x ^ v[g].y;
         }
         acc.loss += float(x & 1u);
         continue;
@@ -600,17 +605,17 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
 #pragma unroll
         for (int g = 0; g < kMaxColdGroups; ++g)
           if (g < L8c) {
-            uint32_t s[8];
-            unpack8(v[g], s);
-            d0 += wl[s[0]] + wl[s[2]] + wl[s[4]] + wl[s[6]];
-            d1 += wl[s[1]] + wl[s[3]] + wl[s[5]] + wl[s[7]];
+            uint32_t s[4];
+            unpack4(v[g], s);
+            d0 += wl[s[0]] + wl[s[2]];
+            d1 += wl[s[1]] + wl[s[3]];
           }
       } else {
         for (int32_t g = 0; g < L8c; ++g) {
-          uint32_t s[8];
-          unpack8(*reinterpret_cast<const uint4*>(sl + int64_t(g) * kChunkStride), s);
-          d0 += wl[s[0]] + wl[s[2]] + wl[s[4]] + wl[s[6]];
-          d1 += wl[s[1]] + wl[s[3]] + wl[s[5]] + wl[s[7]];
+          uint32_t s[4];
+          unpack4(*reinterpret_cast<const uint2*>(sl + int64_t(g) * kColdStride), s);
+          d0 += wl[s[0]] + wl[s[2]];
+          d1 += wl[s[1]] + wl[s[3]];
         }
       }
       float dot = d0 + d1;
@@ -629,17 +634,17 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
 #pragma unroll
           for (int g = 0; g < kMaxColdGroups; ++g)
             if (g < L8c) {
-              uint32_t s[8];
-              unpack8(v[g], s);
+              uint32_t s[4];
+              unpack4(v[g], s);
 #pragma unroll
-              for (int e = 0; e < 8; ++e) atomicAdd(&gl[s[e] * REP + rep], q);
+              for (int e = 0; e < 4; ++e) atomicAdd(&gl[s[e] * REP + rep], q);
             }
         } else {
           for (int32_t g = 0; g < L8c; ++g) {
-            uint32_t s[8];
-            unpack8(*reinterpret_cast<const uint4*>(sl + int64_t(g) * kChunkStride), s);
+            uint32_t s[4];
+            unpack4(*reinterpret_cast<const uint2*>(sl + int64_t(g) * kColdStride), s);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) atomicAdd(&gl[s[e] * REP + rep], q);
+            for (int e = 0; e < 4; ++e) atomicAdd(&gl[s[e] * REP + rep], q);
           }
         }
       }

@@ -235,10 +235,10 @@ def test_hybrid_layout_matches_hashingtf(hip_module, F, hash, repeats, lazy):
     cslot = hy["cslot"]
     big = 0
     for c in range(hy["clen8c"].shape[0]):
-        L8c = int(hy["clen8c"][c])
-        assert 0 <= L8c <= int(clen8[c])
+        L4c = int(hy["clen8c"][c])            # cold 4-entry groups per lane
+        assert 0 <= L4c <= 2 * int(clen8[c])
         g0 = int(cbase[c])
-        blk = cslot[g0 * 512:(g0 + L8c) * 512].reshape(L8c, 64, 8)
+        blk = cslot[g0 * 512:g0 * 512 + L4c * 256].reshape(L4c, 64, 4)
         for r in range(16):
             k = int(perm[c * 16 + r])
             if k < 0:
