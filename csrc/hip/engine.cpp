@@ -388,7 +388,7 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   tr_prep.reset();
   TraceRange tr_train("twtml.lr.train");   // GD iterations (host enqueue + early-stop polling)
 
-  int grid = cfg_.sgd_grid > 0 ? cfg_.sgd_grid : sgd_iter_grid(ns, res.n_kept, num_cu_);
+  int grid = cfg_.sgd_grid > 0 ? cfg_.sgd_grid : sgd_iter_grid(ns, res.n_kept, num_cu_, prep_.hybrid != 0);
   sgd_.pstride = sgd_part_stride(ns);
   sgd_.nparts = sgd_partials(ns, u16, grid);
   ensure_part(int64_t(sgd_.nparts) * sgd_.pstride);

@@ -279,7 +279,7 @@ void launch_norm_carry(const DevSgd& d, hipStream_t s);
 int sgd_lds_rep(int64_t ns);
 // the hybrid iteration kernel's LDS (gradient replicas + hot partials) fits
 bool sgd_hybrid_fits(int64_t ns);
-int sgd_iter_grid(int64_t ns, int64_t n_kept, int num_cu);
+int sgd_iter_grid(int64_t ns, int64_t n_kept, int num_cu, bool hybrid);
 
 // (k-means launchers: kmeans_kernels.h)
 

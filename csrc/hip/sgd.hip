@@ -1025,14 +1025,34 @@ static void launch_iter_t(const DevSgd& d, const DevPrepared& p, const SgdParams
   }
 }
 
-int sgd_iter_grid(int64_t ns, int64_t n_kept, int num_cu) {
+// Workgroups of the (non-stats, non-sampled) LDS iteration kernel that fit a
+// CU at once: LDS *and* registers (a 1024-thread workgroup at 122-128 VGPRs
+// is one per CU -- an LDS-only estimate launched 2-3 rounds of workgroups
+// for mid-sized active sets, each round paying the full per-iteration
+// overhead and adding partial rows).
+static int iter_blocks_per_cu(int64_t ns, int rep, bool hybrid) {
+  const size_t lds = size_t(lds_bytes(ns, rep));
+  int n = 0;
+  hipError_t e = hipSuccess;
+#define TWTML_OCC(K) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, K, kIterBlock, lds)
+  switch (rep) {
+    case 8: if (hybrid) TWTML_OCC((k_sgd_iter_hyb<false, false, 8>)); else TWTML_OCC((k_sgd_iter_lds<false, false, 8, false>)); break;
+    case 4: if (hybrid) TWTML_OCC((k_sgd_iter_hyb<false, false, 4>)); else TWTML_OCC((k_sgd_iter_lds<false, false, 4, false>)); break;
+    case 2: if (hybrid) TWTML_OCC((k_sgd_iter_hyb<false, false, 2>)); else TWTML_OCC((k_sgd_iter_lds<false, false, 2, false>)); break;
+    default: if (hybrid) TWTML_OCC((k_sgd_iter_hyb<false, false, 1>)); else TWTML_OCC((k_sgd_iter_lds<false, false, 1, false>)); break;
+  }
+#undef TWTML_OCC
+  if (e != hipSuccess || n < 1) {
+    (void)hipGetLastError();
+    n = 1;
+  }
+  return n;
+}
+
+int sgd_iter_grid(int64_t ns, int64_t n_kept, int num_cu, bool hybrid) {
   const int rep = sgd_lds_rep(ns);
   int per_cu = 2;
-  if (rep > 0) {
-    const int64_t lds = lds_bytes(ns, rep) + 1024;
-    per_cu = int(std::min<int64_t>(4, (160 * 1024) / lds));
-    if (per_cu < 1) per_cu = 1;
-  }
+  if (rep > 0) per_cu = std::min(4, iter_blocks_per_cu(ns, rep, hybrid));
   const int64_t nch = (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;
   const int64_t waves_per_wg = kIterBlock / kWave;
   int64_t g = std::min<int64_t>(int64_t(num_cu) * per_cu, (nch + waves_per_wg - 1) / waves_per_wg);
