@@ -88,7 +88,19 @@ PYBIND11_MODULE(_twtml_hip, m) {
       .def_property_readonly("world", &Comm::world)
       .def_property_readonly("kind", &Comm::kind)
       .def("abort", &Comm::abort)
-      .def("check", &Comm::check_async);
+      .def("check", &Comm::check_async)
+      // In-place fp64 sum over a device buffer on a private stream, then
+      // synchronise: exercises the communicator outside an engine (tests,
+      // link checks).  The engines issue their collectives on their own streams.
+      .def("allreduce_f64", [](Comm& c, uintptr_t dev_ptr, size_t count) {
+        py::gil_scoped_release nogil;
+        hipStream_t s;
+        TWTML_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        c.allreduce(reinterpret_cast<void*>(dev_ptr), count, ncclFloat64, ncclSum, s);
+        TWTML_HIP_CHECK(hipStreamSynchronize(s));
+        TWTML_HIP_CHECK(hipStreamDestroy(s));
+        c.check_async();
+      }, py::arg("dev_ptr"), py::arg("count"));
   // RCCL communicator (one process per GPU)
   m.def("Comm", [](py::bytes uid, int rank, int world, int device) {
         std::string s = uid;
