@@ -21,16 +21,19 @@ HostBatch::HostBatch(int64_t rows, int64_t text_bytes) : max_rows(rows), max_byt
   const size_t o = up(sizeof(int64_t) * size_t(rows + 1));
   const size_t r = up(size_t(rows));
   const size_t sc = up(sizeof(int64_t) * 5 * size_t(rows));
-  const size_t rp = up(sizeof(uint16_t) * size_t(rows));
-  bytes = t + o + r + 2 * sc + rp;
+  const size_t rp = up(sizeof(uint16_t) * size_t(rows) + 16);
+  bytes = rp + t + o + r + 2 * sc;
   TWTML_HIP_CHECK(hipHostMalloc(&base, bytes, hipHostMallocDefault));
+  // [row words | text | offsets | flags | scalars | spack]: the row words of
+  // n rows end right before the text (pack_rows), so both cross PCIe as one copy
   char* p = static_cast<char*>(base);
-  text = reinterpret_cast<uint8_t*>(p);
+  text = reinterpret_cast<uint8_t*>(p + rp);
+  rowpack = reinterpret_cast<uint16_t*>(p);
+  p += rp;
   offsets = reinterpret_cast<int64_t*>(p + t);
   flags = reinterpret_cast<uint8_t*>(p + t + o);
   scalars = reinterpret_cast<int64_t*>(p + t + o + r);
   spack = reinterpret_cast<uint8_t*>(p + t + o + r + sc);
-  rowpack = reinterpret_cast<uint16_t*>(p + t + o + r + 2 * sc);
   offsets[0] = 0;
 }
 
@@ -84,6 +87,7 @@ void HostBatch::pack_scalars(int64_t n) {
 bool HostBatch::pack_rows(int64_t n) {
   if (n < 0 || n > max_rows) throw std::invalid_argument("pack_rows: bad row count");
   rowpacked_n = -1;
+  rowpack = reinterpret_cast<uint16_t*>(text - rowpack_prefix(n));
   int64_t cesu = 0;
   bool fits = true;
   for (int64_t i = 0; i < n; ++i) {

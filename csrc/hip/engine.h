@@ -47,6 +47,10 @@ struct LRConfig {
 // (csrc/host/wire.h): narrow/wide rows in `text`, byte offsets, per-row
 // flags (bit0 isRetweet, bit1 wide), scalars [5][n] int64 (the record
 // values), and their wire encoding (`spack`, see DevRawBatch in kernels.h).
+// Bytes of row words (u16 per row) placed right before a batch's text, on
+// the host and in a device raw slot, so the two are one H2D copy.
+inline size_t rowpack_prefix(int64_t n) { return (sizeof(uint16_t) * size_t(n) + 15) & ~size_t(15); }
+
 struct HostBatch {
   void* base = nullptr;
   size_t bytes = 0;
@@ -59,7 +63,8 @@ struct HostBatch {
   int64_t sbase[kScalarCols] = {};
   uint8_t sw[kScalarCols] = {};        // wire bytes per value (DevRawBatch::sw)
   int64_t spacked_n = -1;              // rows of the last pack_scalars (-1: none)
-  uint16_t* rowpack = nullptr;         // per row: byte length | wire flags << kRowLenBits
+  uint16_t* rowpack = nullptr;         // per row: byte length | wire flags << kRowLenBits;
+                                       // ends rowpack_prefix(n) bytes before `text`
   int64_t rowpacked_n = -1;            // rows of the last successful pack_rows (-1: none)
   int64_t cesu_rows = 0;               // cesu rows of the last pack_rows (device expands them)
   int64_t rows_scanned_n = -1;         // rows of the last pack_rows call (fit or not)

@@ -27,11 +27,12 @@ void RawSlots::init(int64_t max_rows, int64_t max_bytes) {
   for (auto& s : slots_) {
     // wire bytes + cesu rows expanded behind them (UTF-16: at most twice the
     // wire bytes of those rows); slack: featurize over-reads <= 80 B
-    s.text = slot_alloc<uint8_t>(3 * size_t(max_bytes) + 256);
+    const size_t pre = (rowpack_prefix(max_rows) + 255) & ~size_t(255);
+    s.text_base = slot_alloc<uint8_t>(pre + 3 * size_t(max_bytes) + 256);
+    s.text = s.text_base + pre;
     s.offsets = slot_alloc<int64_t>(size_t(max_rows) + 1);
     s.flags = slot_alloc<uint8_t>(size_t(max_rows));
     s.scalars = slot_alloc<int64_t>(5 * size_t(max_rows));
-    s.rowpack = slot_alloc<uint16_t>(size_t(max_rows) + 8);
     s.tsum = slot_alloc<int64_t>(size_t(max_rows) / 8192 + 2);
     s.rstart = slot_alloc<int64_t>(size_t(max_rows) + 1);
     s.rend = slot_alloc<int64_t>(size_t(max_rows) + 1);
@@ -42,11 +43,10 @@ void RawSlots::init(int64_t max_rows, int64_t max_bytes) {
 
 void RawSlots::release() {
   for (auto& s : slots_) {
-    if (s.text) (void)hipFree(s.text);
+    if (s.text_base) (void)hipFree(s.text_base);
     if (s.offsets) (void)hipFree(s.offsets);
     if (s.flags) (void)hipFree(s.flags);
     if (s.scalars) (void)hipFree(s.scalars);
-    if (s.rowpack) (void)hipFree(s.rowpack);
     if (s.tsum) (void)hipFree(s.tsum);
     if (s.rstart) (void)hipFree(s.rstart);
     if (s.rend) (void)hipFree(s.rend);
@@ -68,15 +68,15 @@ void RawSlots::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, h
   if (n > 0 && hb.rows_scanned_n != n) throw std::logic_error("HostBatch rows not packed (pack_rows) for this row count");
   // wait until the compute stream has finished reading this slot
   if (s.used) TWTML_HIP_CHECK(hipStreamWaitEvent(copy, s.consumed, 0));
-  if (bytes > 0)
-    TWTML_HIP_CHECK(hipMemcpyAsync(s.text, hb.text, size_t(bytes), hipMemcpyHostToDevice, copy));
   // offsets + flags: one u16 per row when the batch was packed (the compute
-  // stream rebuilds both in acquire), else as they are
+  // stream rebuilds both in acquire), else as they are.  Packed row words sit
+  // right before the text on both sides and travel with it (below).
   const bool packed = n > 0 && hb.rowpacked_n == n;
-  if (packed) {
-    TWTML_HIP_CHECK(hipMemcpyAsync(s.rowpack, hb.rowpack, sizeof(uint16_t) * size_t(n),
-                                   hipMemcpyHostToDevice, copy));
-  } else {
+  const size_t pre = packed ? rowpack_prefix(n) : 0;
+  if (packed && reinterpret_cast<const uint8_t*>(hb.rowpack) + pre != hb.text)
+    throw std::logic_error("HostBatch row words not adjacent to the text");
+  s.rowpack = reinterpret_cast<uint16_t*>(s.text - pre);
+  if (!packed) {
     TWTML_HIP_CHECK(hipMemcpyAsync(s.offsets, hb.offsets, sizeof(int64_t) * size_t(n + 1),
                                    hipMemcpyHostToDevice, copy));
   }
@@ -88,6 +88,11 @@ void RawSlots::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, h
     TWTML_HIP_CHECK(hipMemcpyAsync(s.scalars, hb.spack, size_t(hb.soff[scalar_cols]),
                                    hipMemcpyHostToDevice, copy));
   }
+  // row words + text last: the small copy goes first, so the gap the copy
+  // engine leaves after a long transfer falls between batches, not inside one
+  if (bytes > 0 || pre > 0)
+    TWTML_HIP_CHECK(hipMemcpyAsync(s.text - pre, hb.text - pre, pre + size_t(bytes),
+                                   hipMemcpyHostToDevice, copy));
   TWTML_HIP_CHECK(hipEventRecord(s.h2d_done, copy));
   for (int c = 0; c < kScalarCols; ++c) {
     s.soff[c] = hb.soff[c];

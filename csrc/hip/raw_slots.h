@@ -48,6 +48,7 @@ class RawSlots {
  private:
   static int check(int slot);
   struct Slot {
+    uint8_t* text_base = nullptr;     // [row words prefix | text] (one H2D copy)
     uint8_t* text = nullptr;
     int64_t* offsets = nullptr;
     uint8_t* flags = nullptr;
