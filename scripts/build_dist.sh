@@ -9,6 +9,6 @@ OUT=dist/twtml-mi355x-$VER
 rm -rf "$OUT" && mkdir -p "$OUT"
 cp -r twitter_stream_ml_amd "$OUT/"
 find "$OUT" -name __pycache__ -prune -exec rm -rf {} +
-cp README.md pyproject.toml Procfile bench.py "$OUT/"
+cp README.md pyproject.toml Procfile app.json bench.py "$OUT/"
 tar -C dist -czf "dist/twtml-mi355x-$VER.tar.gz" "twtml-mi355x-$VER"
 echo "dist/twtml-mi355x-$VER.tar.gz"
