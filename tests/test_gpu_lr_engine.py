@@ -287,3 +287,22 @@ def test_persistent_loop_matches_per_iteration_kernels(hip_module, monkeypatch, 
         np.testing.assert_allclose(r1["loss_history"], r0["loss_history"], rtol=1e-6)
     w0, w1 = out["0"][1], out["1"][1]
     np.testing.assert_allclose(w1, w0, rtol=1e-5, atol=1e-7 * np.abs(w0).max())
+
+
+def test_wide_murmur3_hybrid_matches_plain_remap(hip_module):
+    """F = 1e8 murmur3: the hybrid remap (LDS id cache for wide ids,
+    hot_split.hip:id_code) trains the same model as the plain k_remap path."""
+    from twitter_stream_ml_amd.ops.lr_engine import DeviceLinearRegression, LRDeviceConfig
+    from twitter_stream_ml_amd.sources.synthetic import SynthConfig, generate_batch
+    synth = SynthConfig.profile("twitter", seed=21, unicode_fraction=0.2)
+    batches = [generate_batch(synth, t * 20000, 20000, batch_time_ms=1_700_000_000_000 + t) for t in range(2)]
+    kw = dict(num_text_features=100_000_000, hash="murmur3", max_rows=32768, max_units=32768 * 300,
+              num_iterations=10)
+    a = DeviceLinearRegression(LRDeviceConfig(hybrid=True, **kw), device=0)
+    b = DeviceLinearRegression(LRDeviceConfig(hybrid=False, **kw), device=0)
+    for bt in batches:
+        ra, rb = a.train_batch(bt, want_pred=False), b.train_batch(bt, want_pred=False)
+        assert ra["n_kept"] == rb["n_kept"] and ra["iterations"] == rb["iterations"]
+        np.testing.assert_allclose(ra["loss_history"], rb["loss_history"], rtol=1e-5)
+    wb = b.get_weights()
+    np.testing.assert_allclose(a.get_weights(), wb, rtol=1e-4, atol=1e-6 * max(np.abs(wb).max(), 1e-12))
