@@ -47,6 +47,9 @@ def parse_args(argv=None):
     ap.add_argument("--pool", type=int, default=4, help="pre-generated batches per rank")
     ap.add_argument("--hash", default="java")
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--profile", default="bench", choices=["bench", "wide"],
+                    help="synthetic data: bench (toy ~300-word vocabulary, ~1.4K active bigrams) or "
+                         "wide (realistic 50K-word multi-script vocabulary, ~200K active bigrams)")
     ap.add_argument("--sgd-grid", type=int, default=0)
     ap.add_argument("--ablate", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--tol", type=float, default=1e-3, help=argparse.SUPPRESS)
@@ -79,7 +82,7 @@ def main(argv=None) -> int:
     comm = D.make_rccl_comm(device)
 
     B = args.batch
-    synth = SynthConfig.profile("bench", seed=args.seed + 7919 * info.rank)
+    synth = SynthConfig.profile(args.profile, seed=args.seed + 7919 * info.rank)
     now_ms = synth.now_ms
     # ---- pool of pinned raw batches (generated + host special-row pass)
     t_gen = time.time()

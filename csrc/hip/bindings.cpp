@@ -50,6 +50,8 @@ static py::dict result_dict(BatchResult& r) {
   d["stats"] = std::vector<double>(r.stats, r.stats + 6);
   d["loss_history"] = r.loss_history;
   d["prep_ms"] = r.prep_ms;
+  d["rows_lowered"] = r.rows_lowered;
+  d["rows_narrowed"] = r.rows_narrowed;
   d["train_ms"] = r.train_ms;
   if (!r.pred.empty()) {
     auto* v = new std::vector<float>(std::move(r.pred));
@@ -81,6 +83,14 @@ PYBIND11_MODULE(_twtml_hip, m) {
     return std::string(p.name) + " (" + p.gcnArchName + ", " + std::to_string(p.multiProcessorCount) + " CUs)";
   });
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
+  // Page-lock a host buffer (e.g. a receiver's batch) so submit(ext_text=...)
+  // DMAs straight from it; unregister before the buffer is freed.
+  m.def("host_register", [](uintptr_t ptr, size_t bytes) {
+    TWTML_HIP_CHECK(hipHostRegister(reinterpret_cast<void*>(ptr), bytes, hipHostRegisterDefault));
+  }, py::arg("ptr"), py::arg("bytes"));
+  m.def("host_unregister", [](uintptr_t ptr) {
+    TWTML_HIP_CHECK(hipHostUnregister(reinterpret_cast<void*>(ptr)));
+  }, py::arg("ptr"));
   m.def("rccl_version", &rccl_version);
 
   py::class_<Comm, std::shared_ptr<Comm>>(m, "CommBase")
@@ -144,6 +154,25 @@ PYBIND11_MODULE(_twtml_hip, m) {
         py::gil_scoped_release nogil;
         h.pack_scalars(n);
       }, py::arg("n"))
+      .def("load_utf16",
+           [](HostBatch& h, py::array_t<uint16_t, py::array::c_style> text,
+              py::array_t<int64_t, py::array::c_style> offsets, py::array_t<uint8_t, py::array::c_style> is_rt,
+              py::array_t<int64_t, py::array::c_style> scalars, bool copy_text, int threads) {
+             const int64_t n = int64_t(offsets.size()) - 1;
+             if (n < 0 || is_rt.size() < n || scalars.size() < 5 * n)
+               throw std::invalid_argument("load_utf16: offsets / is_rt / scalars mismatch");
+             if (n > 0 && offsets.data()[n] > text.size()) throw std::invalid_argument("offsets exceed text");
+             py::gil_scoped_release nogil;
+             h.load_utf16(text.data(), offsets.data(), is_rt.data(), scalars.data(), n, copy_text, threads);
+             return n > 0 ? 2 * offsets.data()[n] : int64_t(0);
+           },
+           py::arg("text"), py::arg("offsets"), py::arg("is_rt"), py::arg("scalars"),
+           py::arg("copy_text") = true, py::arg("threads") = 0,
+           "Stage a raw UTF-16 batch (row words, offsets, packed scalars; text copied only if "
+           "copy_text); returns the text bytes.")
+      .def_readonly("utf16", &HostBatch::utf16)
+      .def_readonly("rowpacked_n", &HostBatch::rowpacked_n)
+      .def_readonly("wide_rows", &HostBatch::wide_rows)
       .def_property_readonly("scalar_wire", [](const HostBatch& h) {
         py::dict d;   // wire encoding of the last pack_scalars (tests / diagnostics)
         std::vector<int64_t> off(h.soff, h.soff + kScalarCols + 1), base(h.sbase, h.sbase + kScalarCols);
@@ -166,11 +195,11 @@ PYBIND11_MODULE(_twtml_hip, m) {
            }),
            py::arg("device"), py::arg("config"), py::arg("comm") = nullptr)
       .def("submit",
-           [](LREngine& e, const HostBatch& hb, int64_t n, int64_t bytes, int slot) {
+           [](LREngine& e, const HostBatch& hb, int64_t n, int64_t bytes, int slot, uintptr_t ext_text) {
              py::gil_scoped_release nogil;
-             e.submit(hb, n, bytes, slot);
+             e.submit(hb, n, bytes, slot, reinterpret_cast<const uint8_t*>(ext_text));
            },
-           py::arg("host_batch"), py::arg("n"), py::arg("bytes"), py::arg("slot"))
+           py::arg("host_batch"), py::arg("n"), py::arg("bytes"), py::arg("slot"), py::arg("ext_text") = 0)
       .def("process",
            [](LREngine& e, int slot, int64_t now_ms, bool want_pred) {
              BatchResult r;

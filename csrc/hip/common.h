@@ -75,6 +75,12 @@ __device__ __forceinline__ T wave_max(T v) {
   return v;
 }
 
+__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v |= uint32_t(__shfl_xor(int(v), off, kWave));
+  return v;
+}
+
 // Block-wide sum for kBlock threads; `scratch` needs kBlock/kWave entries.
 template <typename T>
 __device__ __forceinline__ T block_sum(T v, T* scratch) {

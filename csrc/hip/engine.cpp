@@ -37,11 +37,12 @@ HostBatch::HostBatch(int64_t rows, int64_t text_bytes) : max_rows(rows), max_byt
   offsets[0] = 0;
 }
 
-void HostBatch::pack_scalars(int64_t n) {
+void HostBatch::pack_scalars(int64_t n, const int64_t* src) {
   if (n < 0 || n > max_rows) throw std::invalid_argument("pack_scalars: bad row count");
+  if (!src) src = scalars;
   int64_t lo[kScalarCols], hi[kScalarCols];
   auto range = [&](int c) {
-    const int64_t* v = scalars + int64_t(c) * n;
+    const int64_t* v = src + int64_t(c) * n;
     int64_t a = n ? v[0] : 0, b = a;
     for (int64_t i = 1; i < n; ++i) { a = std::min(a, v[i]); b = std::max(b, v[i]); }
     lo[c] = a;
@@ -62,7 +63,7 @@ void HostBatch::pack_scalars(int64_t n) {
     soff[c + 1] = soff[c] + int64_t(w) * n;
   }
   auto put = [&](int c) {
-    const int64_t* v = scalars + int64_t(c) * n;
+    const int64_t* v = src + int64_t(c) * n;
     uint8_t* o = spack + soff[c];
     const uint64_t b = uint64_t(sbase[c]);
     switch (sw[c]) {
@@ -88,18 +89,64 @@ bool HostBatch::pack_rows(int64_t n) {
   if (n < 0 || n > max_rows) throw std::invalid_argument("pack_rows: bad row count");
   rowpacked_n = -1;
   rowpack = reinterpret_cast<uint16_t*>(text - rowpack_prefix(n));
-  int64_t cesu = 0;
+  int64_t cesu = 0, wide = 0;
   bool fits = true;
   for (int64_t i = 0; i < n; ++i) {
     const int64_t len = offsets[i + 1] - offsets[i];
     cesu += (flags[i] & kRowCesu) ? 1 : 0;
+    wide += (flags[i] & kRowWide) ? 1 : 0;
     if (len < 0 || len >= (int64_t(1) << kRowLenBits)) fits = false;
     else rowpack[i] = uint16_t(len | (int64_t(flags[i] & 7) << kRowLenBits));
   }
   cesu_rows = cesu;
+  wide_rows = wide;
+  utf16 = false;
   rows_scanned_n = n;
   if (fits) rowpacked_n = n;
   return fits;
+}
+
+void HostBatch::load_utf16(const uint16_t* t, const int64_t* uoff, const uint8_t* is_rt, const int64_t* sc,
+                           int64_t n, bool copy_text, int threads) {
+  if (n < 0 || n > max_rows) throw std::invalid_argument("load_utf16: bad row count");
+  const int64_t bytes = n > 0 ? 2 * (uoff[n] - uoff[0]) : 0;
+  if (copy_text && bytes > max_bytes) throw std::invalid_argument("load_utf16: text exceeds staging capacity");
+  if (n > 0 && uoff[0] != 0) throw std::invalid_argument("load_utf16: offsets must start at 0");
+  rowpacked_n = -1;
+  rowpack = reinterpret_cast<uint16_t*>(text - rowpack_prefix(n));
+  if (threads <= 0) threads = int(std::min<unsigned>(8, std::max(1u, std::thread::hardware_concurrency())));
+  const int T = int(std::max<int64_t>(1, std::min<int64_t>(threads, (n + 65535) / 65536)));
+  std::vector<uint8_t> fit(size_t(T), 1);
+  auto rows = [&](int c) {
+    const int64_t r0 = n * c / T, r1 = n * (c + 1) / T;
+    bool ok = true;
+    for (int64_t i = r0; i < r1; ++i) {
+      const int64_t len = 2 * (uoff[i + 1] - uoff[i]);
+      const uint8_t f = uint8_t((is_rt[i] ? kRowRetweet : 0) | kRowWide);
+      offsets[i + 1] = 2 * uoff[i + 1];
+      flags[i] = f;
+      if (len < 0 || len >= (int64_t(1) << kRowLenBits)) ok = false;
+      else rowpack[i] = uint16_t(len | (int64_t(f) << kRowLenBits));
+    }
+    fit[size_t(c)] = ok ? 1 : 0;
+    if (copy_text) {   // this thread's share of the text bytes
+      const int64_t b0 = 2 * uoff[r0], b1 = 2 * uoff[r1];
+      if (b1 > b0) std::memcpy(text + b0, reinterpret_cast<const uint8_t*>(t) + b0, size_t(b1 - b0));
+    }
+  };
+  std::vector<std::thread> th;
+  for (int c = 1; c < T; ++c) th.emplace_back(rows, c);
+  rows(0);
+  for (auto& x : th) x.join();
+  offsets[0] = 0;
+  pack_scalars(n, sc);
+  cesu_rows = 0;
+  wide_rows = n;
+  utf16 = true;
+  rows_scanned_n = n;
+  bool all = true;
+  for (auto f : fit) all = all && f;
+  if (all) rowpacked_n = n;
 }
 
 HostBatch::~HostBatch() {
@@ -155,6 +202,7 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
                                 (2 + size_t(std::max(1, cfg_.num_iterations))) * sizeof(double),
                                 hipHostMallocMapped | hipHostMallocCoherent));
   TWTML_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&sgd_.host_flags), host_flags_, 0));
+  TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_norm_), 2 * sizeof(int64_t), hipHostMallocDefault));
   TWTML_HIP_CHECK(hipDeviceSynchronize());
 }
 
@@ -300,15 +348,16 @@ LREngine::~LREngine() {
   if (host_counters_) (void)hipHostFree(host_counters_);
   if (host_out_) (void)hipHostFree(host_out_);
   if (host_flags_) (void)hipHostFree(host_flags_);
+  if (host_norm_) (void)hipHostFree(host_norm_);
   for (auto e : iter_events_) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(compute_);
   (void)hipStreamDestroy(copy_);
 }
 
-void LREngine::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot) {
+void LREngine::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, const uint8_t* ext_text) {
   TraceRange tr("twtml.lr.submit_h2d");
   TWTML_HIP_CHECK(hipSetDevice(device_));
-  raw_.submit(hb, n, bytes, slot, copy_);
+  raw_.submit(hb, n, bytes, slot, copy_, kScalarCols, ext_text);
 }
 
 BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
@@ -342,12 +391,16 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   if (world > 1) comm_->allreduce(n_global_ + 1, size_t(world), ncclInt64, ncclSum, s);
   TWTML_HIP_CHECK(hipMemcpyAsync(host_counters_, prep_.counters, 4 * sizeof(int64_t),
                                  hipMemcpyDeviceToHost, s));
+  TWTML_HIP_CHECK(hipMemcpyAsync(host_norm_, raw_.norm_stats(slot), 2 * sizeof(int64_t),
+                                 hipMemcpyDeviceToHost, s));
   TWTML_HIP_CHECK(hipMemcpyAsync(host_counters_ + 4, n_global_ + 1,
                                  sizeof(int64_t) * size_t(std::min(world, 4)), hipMemcpyDeviceToHost, s));
   std::vector<int64_t> per_rank(size_t(world), 0);
   TWTML_HIP_CHECK(hipStreamSynchronize(s));
   if (host_counters_[3] != 0) throw std::runtime_error("feature buffer capacity exceeded");
   res.n_kept = host_counters_[0];
+  res.rows_lowered = host_norm_[0];
+  res.rows_narrowed = host_norm_[1];
   res.n_unique = host_counters_[1];
   res.entries = host_counters_[2] * kChunkStride;
   int64_t row_offset = 0, n_glob = 0;

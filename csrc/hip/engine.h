@@ -67,12 +67,23 @@ struct HostBatch {
                                        // ends rowpack_prefix(n) bytes before `text`
   int64_t rowpacked_n = -1;            // rows of the last successful pack_rows (-1: none)
   int64_t cesu_rows = 0;               // cesu rows of the last pack_rows (device expands them)
+  int64_t wide_rows = 0;               // wide rows of the last pack_rows (device checks them for
+                                       // special lower-casing, rows.hip)
+  bool utf16 = false;                  // text is plain UTF-16LE (load_utf16): the device narrows
+                                       // Latin-1 rows itself
   int64_t rows_scanned_n = -1;         // rows of the last pack_rows call (fit or not)
   int64_t max_rows = 0, max_bytes = 0;
   HostBatch(int64_t rows, int64_t text_bytes);
   ~HostBatch();
-  // Encode scalars[:, :n] into spack (one thread per column).
-  void pack_scalars(int64_t n);
+  // Encode scalars[:, :n] (or src [5][n]) into spack (one thread per column).
+  void pack_scalars(int64_t n, const int64_t* src = nullptr);
+  // Raw UTF-16 ingest: row words / offsets / flags for `n` rows of UTF-16
+  // text with unit offsets uoff [n+1], scalars from sc [5][n]; the text is
+  // copied into `text` only if copy_text (else it is DMA'd from the caller's
+  // registered buffer by submit).  No per-unit host work besides the copy:
+  // the device narrows Latin-1 rows and lowers special rows (rows.hip).
+  void load_utf16(const uint16_t* t, const int64_t* uoff, const uint8_t* is_rt, const int64_t* sc,
+                  int64_t n, bool copy_text, int threads);
   // Offsets + flags of rows [0, n) as one u16 per row (the device rebuilds
   // both with a scan): 9 -> 2 bytes per row on PCIe.  False (and the batch
   // ships offsets + flags as before) if a row has >= 8192 wire bytes.
@@ -88,6 +99,7 @@ struct BatchResult {
   int32_t iterations = 0;
   bool converged = false;
   bool overflow = false;  // a residual hit the fixed-point clamp (diverging model)
+  int64_t rows_lowered = 0, rows_narrowed = 0;   // device row normalisation (rows.hip)
   double stats[6] = {0, 0, 0, 0, 0, 0};  // n, sum y, sum y^2, sum p, sum p^2, sum (y-p)^2
   std::vector<double> loss_history;
   std::vector<float> pred;
@@ -100,7 +112,7 @@ class LREngine {
   ~LREngine();
 
   // Async H2D of rows [0, n) of a pinned host batch into device slot `slot`.
-  void submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot);
+  void submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, const uint8_t* ext_text = nullptr);
   // Train on the batch in `slot` (blocks until done); stats use w before training.
   BatchResult process(int slot, int64_t now_ms, bool want_pred);
 
@@ -155,6 +167,7 @@ class LREngine {
   int64_t* host_counters_ = nullptr;  // pinned [8]
   double* host_out_ = nullptr;        // pinned [16 + iters]
   double* host_flags_ = nullptr;      // pinned [iters + 1] convergence flag per iteration
+  int64_t* host_norm_ = nullptr;      // pinned [2] rows lowered / narrowed on the device
   std::vector<hipEvent_t> iter_events_;
   int64_t* n_global_ = nullptr;       // device [world + 1]
   hipEvent_t ev_[4] = {nullptr, nullptr, nullptr, nullptr};

@@ -72,6 +72,23 @@ void launch_cesu_expand(uint8_t* text, const int64_t* offsets, uint8_t* flags, i
 void launch_unpack_rows(const uint16_t* rowpack, int64_t n, int64_t* offsets, uint8_t* flags, int64_t* tsum,
                         hipStream_t s);
 
+// Unicode case tables for the special-row full case mapping (rows.hip).
+struct DevCaseTables {
+  const uint32_t* supp_lower = nullptr;    // [n_supp][2] astral code point -> lower case
+  const uint32_t* case_ranges = nullptr;   // [n_ranges][3] lo, hi, class (1 ignorable, 2 cased)
+  int32_t n_supp = 0, n_ranges = 0;
+};
+void upload_case_tables(DevCaseTables* ct);
+void free_case_tables(DevCaseTables* ct);
+// Special-row full case mapping (+ narrowing of Latin-1 rows of UTF-16
+// batches when `narrow`), see rows.hip.  Reads rows at [cur_s, cur_e),
+// writes every row's extents to out_s / out_e (may alias cur_*) and clears
+// the wide flag of narrowed rows.  text needs lower_base + 2 * wire bytes.
+void launch_row_normalize(uint8_t* text, const int64_t* wire_off, const int64_t* cur_s, const int64_t* cur_e,
+                          uint8_t* flags, int64_t* out_s, int64_t* out_e, int64_t n, int64_t tail,
+                          int64_t lower_base, bool narrow, const DevCaseTables& ct, int64_t* stats,
+                          hipStream_t s);
+
 // Row r: byte offset, wide flag and length in UTF-16 units.
 struct RowText {
   int64_t o, len;

@@ -94,11 +94,11 @@ KMEngine::~KMEngine() {
   (void)hipStreamDestroy(copy_);
 }
 
-void KMEngine::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot) {
+void KMEngine::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, const uint8_t* ext_text) {
   TraceRange tr("twtml.km.submit_h2d");
   TWTML_HIP_CHECK(hipSetDevice(device_));
   // features read only retweetCount and followersCount (scalar rows 0, 1)
-  raw_.submit(hb, n, bytes, slot, copy_, 2);
+  raw_.submit(hb, n, bytes, slot, copy_, 2, ext_text);
 }
 
 KMResult KMEngine::process(int slot, bool want_labels) {
@@ -214,10 +214,10 @@ void bind_kmeans(py::module_& m) {
              return std::make_shared<KMEngine>(device, c, comm);
            }),
            py::arg("device"), py::arg("config"), py::arg("comm") = nullptr)
-      .def("submit", [](KMEngine& e, const HostBatch& hb, int64_t n, int64_t bytes, int slot) {
+      .def("submit", [](KMEngine& e, const HostBatch& hb, int64_t n, int64_t bytes, int slot, uintptr_t ext_text) {
         py::gil_scoped_release nogil;
-        e.submit(hb, n, bytes, slot);
-      })
+        e.submit(hb, n, bytes, slot, reinterpret_cast<const uint8_t*>(ext_text));
+      }, py::arg("host_batch"), py::arg("n"), py::arg("bytes"), py::arg("slot"), py::arg("ext_text") = 0)
       .def("process", [](KMEngine& e, int slot, bool want_labels) {
         KMResult r;
         {

@@ -37,7 +37,7 @@ class KMEngine {
  public:
   KMEngine(int device, const KMConfig& cfg, std::shared_ptr<Comm> comm);
   ~KMEngine();
-  void submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot);
+  void submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, const uint8_t* ext_text = nullptr);
   KMResult process(int slot, bool want_labels);
   void set_state(const double* centers, const double* weights);
   void get_state(double* centers, double* weights) const;

@@ -28,7 +28,8 @@ void RawSlots::init(int64_t max_rows, int64_t max_bytes) {
     // wire bytes + cesu rows expanded behind them (UTF-16: at most twice the
     // wire bytes of those rows); slack: featurize over-reads <= 80 B
     const size_t pre = (rowpack_prefix(max_rows) + 255) & ~size_t(255);
-    s.text_base = slot_alloc<uint8_t>(pre + 3 * size_t(max_bytes) + 256);
+    s.text_base = slot_alloc<uint8_t>(pre + 5 * size_t(max_bytes) + 256);
+    s.nstats = slot_alloc<int64_t>(2);
     s.text = s.text_base + pre;
     s.offsets = slot_alloc<int64_t>(size_t(max_rows) + 1);
     s.flags = slot_alloc<uint8_t>(size_t(max_rows));
@@ -39,6 +40,7 @@ void RawSlots::init(int64_t max_rows, int64_t max_bytes) {
     TWTML_HIP_CHECK(hipEventCreateWithFlags(&s.h2d_done, hipEventDisableTiming));
     TWTML_HIP_CHECK(hipEventCreateWithFlags(&s.consumed, hipEventDisableTiming));
   }
+  upload_case_tables(&case_);
 }
 
 void RawSlots::release() {
@@ -50,18 +52,20 @@ void RawSlots::release() {
     if (s.tsum) (void)hipFree(s.tsum);
     if (s.rstart) (void)hipFree(s.rstart);
     if (s.rend) (void)hipFree(s.rend);
+    if (s.nstats) (void)hipFree(s.nstats);
     if (s.h2d_done) (void)hipEventDestroy(s.h2d_done);
     if (s.consumed) (void)hipEventDestroy(s.consumed);
     s = Slot{};
   }
+  free_case_tables(&case_);
 }
 
 void RawSlots::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, hipStream_t copy,
-                      int scalar_cols) {
+                      int scalar_cols, const uint8_t* ext_text) {
   Slot& s = slots_[check(slot)];
   if (scalar_cols < 1 || scalar_cols > 5) throw std::invalid_argument("scalar_cols must be in [1, 5]");
   if (n < 0 || n > max_rows_ || n > hb.max_rows) throw std::invalid_argument("rows exceed capacity");
-  if (bytes < 0 || bytes > max_bytes_ || bytes > hb.max_bytes)
+  if (bytes < 0 || bytes > max_bytes_ || (!ext_text && bytes > hb.max_bytes))
     throw std::invalid_argument("text bytes exceed capacity");
   if (hb.offsets[0] != 0 || hb.offsets[n] != bytes) throw std::invalid_argument("offsets[n] != bytes");
   if (n > 0 && hb.spacked_n != n) throw std::logic_error("HostBatch scalars not packed for this row count");
@@ -90,9 +94,15 @@ void RawSlots::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, h
   }
   // row words + text last: the small copy goes first, so the gap the copy
   // engine leaves after a long transfer falls between batches, not inside one
-  if (bytes > 0 || pre > 0)
+  if (ext_text) {   // row words from the staging buffer, text from the caller's buffer
+    if (pre > 0)
+      TWTML_HIP_CHECK(hipMemcpyAsync(s.text - pre, hb.text - pre, pre, hipMemcpyHostToDevice, copy));
+    if (bytes > 0)
+      TWTML_HIP_CHECK(hipMemcpyAsync(s.text, ext_text, size_t(bytes), hipMemcpyHostToDevice, copy));
+  } else if (bytes > 0 || pre > 0) {
     TWTML_HIP_CHECK(hipMemcpyAsync(s.text - pre, hb.text - pre, pre + size_t(bytes),
                                    hipMemcpyHostToDevice, copy));
+  }
   TWTML_HIP_CHECK(hipEventRecord(s.h2d_done, copy));
   for (int c = 0; c < kScalarCols; ++c) {
     s.soff[c] = hb.soff[c];
@@ -101,6 +111,8 @@ void RawSlots::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, h
   }
   s.packed = packed;
   s.cesu_rows = n > 0 ? hb.cesu_rows : 0;
+  s.wide_rows = n > 0 ? hb.wide_rows : 0;
+  s.utf16 = n > 0 && hb.utf16;
   s.n = n;
   s.bytes = bytes;
   s.used = true;
@@ -116,9 +128,17 @@ DevRawBatch RawSlots::acquire(int slot, hipStream_t compute) {
   b.offsets = s.offsets;
   b.oend = s.offsets + 1;
   b.flags = s.flags;
+  const int64_t tail = (s.bytes + 15) / 16 * 16;
   if (s.cesu_rows > 0) {   // expand cesu rows behind the wire bytes (16-byte aligned)
-    const int64_t tail = (s.bytes + 15) / 16 * 16;
     launch_cesu_expand(s.text, s.offsets, s.flags, s.n, tail, s.rstart, s.rend, compute);
+    b.offsets = s.rstart;
+    b.oend = s.rend;
+  }
+  TWTML_HIP_CHECK(hipMemsetAsync(s.nstats, 0, 2 * sizeof(int64_t), compute));
+  if (s.utf16 || s.cesu_rows > 0 || s.wide_rows > 0) {
+    // special rows -> fully lower-cased UTF-16; UTF-16 batches: Latin-1 rows narrowed
+    launch_row_normalize(s.text, s.offsets, b.offsets, b.oend, s.flags, s.rstart, s.rend, s.n, tail,
+                         tail + 2 * ((s.bytes + 15) / 16 * 16), s.utf16, case_, s.nstats, compute);
     b.offsets = s.rstart;
     b.oend = s.rend;
   }

@@ -33,16 +33,22 @@ class RawSlots {
   // H2D of rows [0, n) / `bytes` text bytes of hb into `slot` on `copy`.
   // scalar_cols: leading scalar columns to copy (the rest stay stale); the
   // batch's scalars must have been encoded with hb.pack_scalars(n)
+  // ext_text: the batch's text bytes live outside hb (a registered host
+  // buffer, e.g. the receiver's UTF-16 batch): DMA'd from there.
   void submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, hipStream_t copy,
-              int scalar_cols = 5);
+              int scalar_cols = 5, const uint8_t* ext_text = nullptr);
   // Make `compute` wait for the slot's H2D; returns the device view.
   DevRawBatch acquire(int slot, hipStream_t compute);
+  // Rows lowered (special full case mapping) / narrowed by the last acquire
+  // of `slot` (device counters, valid once the compute stream passed acquire).
+  const int64_t* norm_stats(int slot) const { return slots_[check(slot)].nstats; }
   // The compute stream is done reading the slot's raw bytes.
   void release_slot(int slot, hipStream_t compute);
   int64_t rows(int slot) const { return slots_[check(slot)].n; }
   int64_t max_rows() const { return max_rows_; }
   // device text bytes per slot: the wire bytes, then room for cesu rows
-  // expanded to UTF-16 (<= 2 bytes per wire byte)
+  // expanded to UTF-16 / narrowed UTF-16 rows (<= 2 bytes per wire byte),
+  // then for lowered special rows (<= 2 bytes per wire byte, rows.hip)
   int64_t max_bytes() const { return max_bytes_; }
 
  private:
@@ -57,8 +63,9 @@ class RawSlots {
     int64_t* tsum = nullptr;          // unpack scan scratch (per 8192-row tile)
     int64_t* rstart = nullptr;        // cesu batches: row start / end after expansion
     int64_t* rend = nullptr;
-    int64_t cesu_rows = 0;
-    bool packed = false;
+    int64_t cesu_rows = 0, wide_rows = 0;
+    int64_t* nstats = nullptr;        // [2] rows lowered / narrowed by row_normalize
+    bool packed = false, utf16 = false;
     int64_t soff[kScalarCols] = {};
     int64_t sbase[kScalarCols] = {};
     uint8_t sw[kScalarCols] = {};
@@ -67,6 +74,7 @@ class RawSlots {
     bool used = false;
   } slots_[kRawSlots];
   int64_t max_rows_ = 0, max_bytes_ = 0;
+  DevCaseTables case_{};
 };
 
 }  // namespace twtml

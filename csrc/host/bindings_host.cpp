@@ -33,6 +33,7 @@ static SynthParams params_from(const py::dict& d) {
   GET(rt_base, double) GET(rt_slope, double) GET(rt_noise, double) GET(rt_tail, double)
   GET(min_len, int32_t) GET(max_len, int32_t) GET(unicode_fraction, double)
   GET(special_fraction, double) GET(now_ms, int64_t) GET(max_age_ms, int64_t)
+  GET(vocab, int32_t) GET(vocab_size, int32_t)
 #undef GET
   return p;
 }

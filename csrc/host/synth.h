@@ -27,6 +27,12 @@ struct SynthParams {
   double special_fraction = 0.002; // P(tweet contains U+0130 / U+03A3 edge cases)
   int64_t now_ms = 1700000000000LL;
   int64_t max_age_ms = 7LL * 24 * 3600 * 1000;
+  // 0: the ~300-word toy vocabulary (1.4K active bigrams per batch);
+  // 1: a realistic multi-script vocabulary of `vocab_size` generated words
+  //    (Latin, accented Latin-1, Cyrillic, Greek, CJK, kana, Hangul, Arabic,
+  //    Devanagari, Thai, Hebrew) plus fresh @handles, hashtags and URL slugs
+  int32_t vocab = 0;
+  int32_t vocab_size = 50000;
 };
 
 // Generate rows [start, start+n) of the stream into caller buffers.

@@ -53,12 +53,16 @@ def _with_long_row(raw, k=3, n_units=9000):
     return RawBatch(np.concatenate(units), off, raw.is_retweet, raw.scalars, raw.batch_time_ms)
 
 
-@pytest.mark.parametrize("F,hash,wide,longrow", [(1000, "java", False, False), (1 << 20, "java", False, False),
-                                                 (1 << 20, "murmur3", False, False),
-                                                 (1000, "java", True, False), (1 << 20, "java", False, True)])
-def test_featurize_matches_oracle(hip_module, F, hash, wide, longrow):
+@pytest.mark.parametrize("F,hash,wide,longrow,ingest", [
+    (1000, "java", False, False, "wire"), (1 << 20, "java", False, False, "wire"),
+    (1 << 20, "murmur3", False, False, "wire"), (1000, "java", True, False, "wire"),
+    (1 << 20, "java", False, True, "wire"),
+    (1 << 20, "java", False, False, "utf16"), (1 << 20, "murmur3", True, True, "utf16")])
+def test_featurize_matches_oracle(hip_module, F, hash, wide, longrow, ingest):
     """Featurize == oracle; also covers the wire encodings: wide (int64)
-    scalar columns and the plain-offsets fallback of a >= 16 KiB row."""
+    scalar columns and the plain-offsets fallback of a >= 16 KiB row, and
+    raw UTF-16 ingest (Latin-1 rows narrowed on the device).  Special rows
+    (5 %) are fully lower-cased on the device (rows.hip), not on the host."""
     cfg = SynthConfig.profile("twitter", seed=11, special_fraction=0.05, unicode_fraction=0.3)
     raw = generate_batch(cfg, 0, 3000, batch_time_ms=NOW)
     if wide:   # followers / createdAt ranges beyond 32 bits: those columns ship as int64
@@ -68,8 +72,11 @@ def test_featurize_matches_oracle(hip_module, F, hash, wide, longrow):
         raw = _with_long_row(raw)
         raw.scalars[0, 3] = 500   # keep it: it passes the [100, 1000] filter
         raw.is_retweet[3] = True
-    eng = _engine(F, hash, lazy_idx=False)   # every hashed id kept for inspection
-    eng.train_batch(raw, want_pred=True)
+    eng = _engine(F, hash, lazy_idx=False, ingest=ingest)   # every hashed id kept for inspection
+    res = eng.train_batch(raw, want_pred=True)
+    assert res["rows_lowered"] > 0
+    if ingest == "utf16":
+        assert res["rows_narrowed"] > 0.5 * raw.n
     hb = eng._staging[0]
     sw = hb._hb.scalar_wire
     assert sw["rows"] == raw.n
@@ -102,6 +109,46 @@ def test_featurize_matches_oracle(hip_module, F, hash, wide, longrow):
     np.testing.assert_array_equal(y, fb.y.astype(np.float32))
     want_num = fb.X[:, F:F + 4].toarray()
     np.testing.assert_allclose(num, want_num, rtol=2e-7, atol=0)
+
+
+_SPECIAL_TEXTS = [
+    "\u0130stanbul", "ŞEHİR", "KIZ İ", "İ", "ΟΔΟΣ", "ΣΟΦΙΑ", "ΛΟΓΟΣ.", "ΣΑΣ", "Σ", "ΑΣ'", "ΑΣ'Β", "ΑΣ\u0308",
+    "α Σ β", "ΑΣ \U00010400", "\U00010400ΣΑ", "\U00010400\U00010401\U00010402 mixed", "\U0001E900\U0001E901",
+    "ΜΑΣ ΤΟΥΣ", "plain ascii then İ", "x\ud801", "\udc00Σ\ud801\udc00", "ab\ud801\ud801\udc00Σ",
+    "caf\u00e9 İ ok", "\U0001F600 emoji Σ",
+]
+
+
+@pytest.mark.parametrize("ingest", ["wire", "utf16"])
+def test_device_special_lowering(hip_module, ingest):
+    """Rows whose lower-casing is not one unit per unit (U+0130 -> 2 units,
+    Final_Sigma context incl. case-ignorables and astral neighbours, astral
+    cased letters, lone surrogates), as narrow / cesu / wide wire rows or raw
+    UTF-16: device featurize == oracle (Java toLowerCase semantics)."""
+    from twitter_stream_ml_amd.records.batch import RawBatch, utf16_units
+    base = generate_batch(SynthConfig.profile("twitter", seed=3), 0, 400, batch_time_ms=NOW)
+    texts = [base.text_of(i) for i in range(base.n)]
+    for j, s in enumerate(_SPECIAL_TEXTS):
+        texts[7 * j] = s
+    units = [utf16_units(s) for s in texts]
+    off = np.zeros(len(texts) + 1, np.int64)
+    off[1:] = np.cumsum([u.shape[0] for u in units])
+    is_rt = np.ones(len(texts), np.uint8)
+    sc = base.scalars.copy()
+    sc[0, :] = 500   # every row passes the filter
+    raw = RawBatch(np.concatenate(units), off, is_rt, sc, NOW)
+    eng = _engine(1 << 20, "murmur3", lazy_idx=False, ingest=ingest)
+    res = eng.train_batch(raw, want_pred=True)
+    assert res["rows_lowered"] >= 18, res["rows_lowered"]
+    dbg = eng._eng.debug_prepared()
+    fb = featurize_batch(raw, 1 << 20, 100, 1000, now_ms=NOW, hash="murmur3")
+    assert int(dbg["counters"][0]) == fb.n == raw.n
+    rows = _rows_from_debug(dbg)
+    Xt = fb.X[:, :1 << 20].tocsr()
+    for k in range(fb.n):
+        s, e = Xt.indptr[k], Xt.indptr[k + 1]
+        want = np.repeat(Xt.indices[s:e], Xt.data[s:e].astype(np.int64))
+        np.testing.assert_array_equal(rows[k], np.sort(want), err_msg=f"row {k}: {texts[k]!r}")
 
 
 @pytest.mark.parametrize("F,dedup,hybrid", [(1000, False, True), (1 << 20, False, True),

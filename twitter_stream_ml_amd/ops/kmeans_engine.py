@@ -104,7 +104,7 @@ class DeviceKMeans:
         return self._staging[i]
 
     def submit(self, hb: HostBatchView, slot: int) -> None:
-        self._eng.submit(hb._hb, int(hb.n), int(hb.bytes), int(slot))
+        self._eng.submit(hb._hb, int(hb.n), int(hb.bytes), int(slot), int(hb.ext_text))
 
     def process(self, slot: int, want_pred: bool = True) -> Dict[str, object]:
         r = self._eng.process(int(slot), bool(want_pred))

@@ -6,12 +6,14 @@ reference runs as ~60 Spark jobs: filter (K3), featurize
 ``LinearRegression.scala:53-81``) and ``numIterations`` steps of
 ``GradientDescent`` (K5+K6, output op #2 ``model.trainOn`` at ``:86``).
 
-Host-side contract: raw batches live in pinned :class:`HostBatch` buffers in
-the wire format (narrow/wide ``text`` bytes, byte ``offsets``, per-row
-``flags``, packed ``[5][n]`` scalars; ``csrc/host/wire.h``).  Rows whose
-lower-casing is not per-UTF-16-unit (U+0130, U+03A3, astral cased letters)
-are rewritten on the host first (:func:`prelower`); everything else is
-lowered on the device.
+Host-side contract: raw batches live in pinned :class:`HostBatch` buffers,
+either in the packed wire format (narrow/cesu/wide ``text`` bytes, row
+words, packed scalars; ``csrc/host/wire.h``) or as plain UTF-16 (``ingest
+="utf16"``: no per-unit host work at all, the text can even be DMA'd
+straight from the receiver's registered buffer).  Lower-casing -- including
+the rows whose full case mapping is not one unit per unit (U+0130, Final
+Sigma, astral cased letters, ``MllibHelper.scala:45``) -- happens on the
+device (``csrc/hip/rows.hip``).
 """
 from __future__ import annotations
 
@@ -24,11 +26,13 @@ from ..records.batch import RETWEET_COUNT, RawBatch
 from ._native import hip, host
 from .ingest import SlotPipeline
 
-__all__ = ["LRDeviceConfig", "DeviceLinearRegression", "prelower", "HostBatchView"]
+__all__ = ["LRDeviceConfig", "DeviceLinearRegression", "prelower", "HostBatchView", "register_host",
+           "unregister_host"]
 
 
 def prelower(raw: RawBatch) -> RawBatch:
-    """Host pre-pass: full-case-map the rare rows the GPU cannot lower per unit."""
+    """Host full case mapping of the special rows (reference / tests only:
+    the device does this itself, ``csrc/hip/rows.hip``)."""
     h = host()
     if h.count_special_rows(raw.text, raw.offsets) == 0:
         return raw
@@ -63,6 +67,10 @@ class LRDeviceConfig:
     # from the raw text (csrc/hip/narrow_text.h).  False keeps every id
     # (debug_prepared() inspection).
     lazy_idx: bool = True
+    # host staging: "wire" packs rows on the host (Latin-1 / cesu / UTF-16,
+    # ~166 B per tweet on PCIe); "utf16" ships plain UTF-16 (~300 B per
+    # tweet) with no per-unit host work -- the device narrows Latin-1 rows
+    ingest: str = "wire"
 
     def as_dict(self) -> Dict[str, object]:
         return {
@@ -87,15 +95,17 @@ class LRDeviceConfig:
 
 
 class HostBatchView:
-    """Pinned host staging buffer in the wire format, with numpy views.
+    """Pinned host staging buffer of one raw batch, with numpy views.
 
-    ``load`` pre-lowers the special rows, then packs the UTF-16 batch into
-    narrow (Latin-1, 1 byte/unit) / wide (UTF-16LE) rows with the native
-    multi-threaded packer (``csrc/host/wire.cpp``): typical tweet text
-    crosses PCIe at half the UTF-16 size.  The five int64 scalar columns
-    ship as u32 offsets from a per-batch base when their range fits (exact),
-    and a row's byte offset + flags as one u16 (length | flags << 14) that
-    the device scans back into offsets (rows of >= 16 KiB: plain offsets).
+    ``load`` packs the UTF-16 batch into narrow (Latin-1, 1 byte/unit) /
+    cesu / wide rows with the native multi-threaded packer
+    (``csrc/host/wire.cpp``): typical tweet text crosses PCIe at half the
+    UTF-16 size.  The five int64 scalar columns ship as 1-4 byte offsets
+    from a per-batch base when their range fits (exact), and a row's byte
+    length + flags as one u16 that the device scans back into offsets.
+    ``load_utf16`` stages only the row words and scalars and leaves the
+    text as UTF-16 (copied, or DMA'd from the caller's buffer by ``submit``).
+    No lower-casing happens on the host in either mode.
     """
 
     def __init__(self, max_rows: int, max_units: int):
@@ -110,6 +120,8 @@ class HostBatchView:
         self.bytes = 0
         self.batch_time_ms = 0
         self.rows_packed = False
+        self.ext_text = 0      # address of an external text buffer (load_utf16(copy_text=False))
+        self._ext_owner = None
 
     @property
     def max_rows(self) -> int:
@@ -118,24 +130,61 @@ class HostBatchView:
     def scalars(self) -> np.ndarray:
         return self.scalars_flat[:5 * self.n].reshape(5, self.n)
 
-    def load(self, raw: RawBatch) -> "HostBatchView":
-        raw = prelower(raw)
+    def _check(self, raw: RawBatch) -> None:
         n, u = raw.n, raw.total_units
         if n > self.max_rows or u > self.max_units:
             raise ValueError(f"batch ({n} rows, {u} units) exceeds staging capacity "
                              f"({self.max_rows}, {self.max_units})")
+
+    def load(self, raw: RawBatch, ingest: str = "wire") -> "HostBatchView":
+        if ingest == "utf16":
+            return self.load_utf16(raw, copy_text=True)
+        if ingest != "wire":
+            raise ValueError(f"unknown ingest mode {ingest!r}")
+        self._check(raw)
+        n, u = raw.n, raw.total_units
         self.bytes = int(host().wire_pack(raw.text, raw.offsets, raw.is_retweet, self.text,
                                           self.offsets, self.flags))
         self.scalars_flat[:5 * n] = raw.scalars.reshape(-1)
         self._hb.pack_scalars(n)   # u32 + per-batch base where a column's range fits
         self.rows_packed = bool(self._hb.pack_rows(n))   # offsets + flags as 2 B per row
         self.n, self.units, self.batch_time_ms = n, u, raw.batch_time_ms
+        self.ext_text, self._ext_owner = 0, None
+        return self
+
+    def load_utf16(self, raw: RawBatch, copy_text: bool = True) -> "HostBatchView":
+        """Raw UTF-16 staging (row words + scalars only; O(rows) host work
+        plus the text copy, which copy_text=False skips: ``submit`` then DMAs
+        the text from ``raw.text`` -- register it with :func:`register_host`)."""
+        self._check(raw)
+        text = np.ascontiguousarray(raw.text, dtype=np.uint16)
+        sc = np.ascontiguousarray(raw.scalars, dtype=np.int64)
+        self.bytes = int(self._hb.load_utf16(text, np.ascontiguousarray(raw.offsets, dtype=np.int64),
+                                             np.ascontiguousarray(raw.is_retweet, dtype=np.uint8), sc,
+                                             bool(copy_text)))
+        self.n, self.units, self.batch_time_ms = raw.n, raw.total_units, raw.batch_time_ms
+        self.rows_packed = int(self._hb.rowpacked_n) == raw.n
+        self.ext_text = 0 if copy_text else int(text.ctypes.data)
+        self._ext_owner = None if copy_text else text   # keeps the DMA source alive
         return self
 
     def as_raw(self) -> RawBatch:
+        if self.ext_text:
+            raise ValueError("text was not staged (load_utf16(copy_text=False))")
         text, offsets, is_rt = host().wire_unpack(self.text[:self.bytes], self.offsets[:self.n + 1],
                                                   self.flags[:self.n])
         return RawBatch(text, offsets, is_rt, self.scalars().copy(), self.batch_time_ms)
+
+
+def register_host(arr: np.ndarray) -> None:
+    """Page-lock a host array so ``submit`` can DMA from it asynchronously."""
+    if arr.nbytes:
+        hip().host_register(int(arr.ctypes.data), int(arr.nbytes))
+
+
+def unregister_host(arr: np.ndarray) -> None:
+    if arr.nbytes:
+        hip().host_unregister(int(arr.ctypes.data))
 
 
 class DeviceLinearRegression:
@@ -148,7 +197,7 @@ class DeviceLinearRegression:
         self._eng = hip().LREngine(self.device, cfg.as_dict(), comm)
         self._staging: List[HostBatchView] = []
         self.raw_slots = int(hip().RAW_SLOTS)
-        self._pipe = SlotPipeline(self.raw_slots, lambda s, raw: self.staging(s).load(raw),
+        self._pipe = SlotPipeline(self.raw_slots, lambda s, raw: self.staging(s).load(raw, cfg.ingest),
                                   self.submit, self.synchronize)
 
     # ---- weights (MLlib setInitialWeights / latestModel.weights) ---------
@@ -172,7 +221,7 @@ class DeviceLinearRegression:
         return self._staging[i]
 
     def submit(self, hb: HostBatchView, slot: int) -> None:
-        self._eng.submit(hb._hb, int(hb.n), int(hb.bytes), int(slot))
+        self._eng.submit(hb._hb, int(hb.n), int(hb.bytes), int(slot), int(hb.ext_text))
 
     def process(self, slot: int, now_ms: int, want_pred: bool = False) -> Dict[str, object]:
         return self._eng.process(int(slot), int(now_ms), bool(want_pred))
