@@ -52,6 +52,8 @@ static py::dict result_dict(BatchResult& r) {
   d["prep_ms"] = r.prep_ms;
   d["rows_lowered"] = r.rows_lowered;
   d["rows_narrowed"] = r.rows_narrowed;
+  d["tiered"] = r.tiered;
+  d["n_near"] = r.n_near;
   d["train_ms"] = r.train_ms;
   if (!r.pred.empty()) {
     auto* v = new std::vector<float>(std::move(r.pred));
@@ -83,6 +85,8 @@ PYBIND11_MODULE(_twtml_hip, m) {
     return std::string(p.name) + " (" + p.gcnArchName + ", " + std::to_string(p.multiProcessorCount) + " CUs)";
   });
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
+  m.def("tier_near_cap", &tier_near_cap, "LDS-resident text slots of the tiered layout");
+  m.def("sgd_hybrid_fits", &sgd_hybrid_fits, py::arg("ns"));
   // Page-lock a host buffer (e.g. a receiver's batch) so submit(ext_text=...)
   // DMAs straight from it; unregister before the buffer is freed.
   m.def("host_register", [](uintptr_t ptr, size_t bytes) {

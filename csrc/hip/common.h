@@ -75,6 +75,14 @@ __device__ __forceinline__ T wave_max(T v) {
   return v;
 }
 
+// LDS hand-off between the lanes of one wave (no other wave touches the
+// region): drain this wave's LDS traffic, then re-converge.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 __device__ __forceinline__ uint32_t wave_or(uint32_t v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v |= uint32_t(__shfl_xor(int(v), off, kWave));

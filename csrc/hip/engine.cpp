@@ -167,6 +167,7 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
   if (cfg_.max_rows >= (int64_t(1) << 31)) throw std::invalid_argument("max_rows must be < 2^31");
   if (cfg_.fraction <= 0.0 || cfg_.fraction > 1.0 + 1e-12)
     throw std::invalid_argument("miniBatchFraction must be in (0, 1]");
+  if (const char* v = std::getenv("TWTML_FORCE_TIERED")) force_tiered_ = v[0] == '1';   // tests
   TWTML_HIP_CHECK(hipSetDevice(device_));
   hipDeviceProp_t prop;
   TWTML_HIP_CHECK(hipGetDeviceProperties(&prop, device_));
@@ -231,6 +232,7 @@ void LREngine::alloc_prepared() {
   prep_.hot_slot = dmalloc<int32_t>(kHot);
   prep_.hot_of = dmalloc<uint8_t>(kMaxHybridSlots);
   prep_.slot_hist = dmalloc<uint32_t>(kMaxHybridSlots);
+  slot_hist_cap_ = kMaxHybridSlots;
   prep_.code = dmalloc<uint16_t>(8192);
   prep_.cbase = dmalloc<int64_t>(size_t(C) + 1);
   prep_.idx = dmalloc<int32_t>(size_t(E));
@@ -253,10 +255,6 @@ void LREngine::alloc_prepared() {
   prep_.counters = dmalloc<int64_t>(8);
 }
 
-// Opt-in (TWTML_PERSIST=1): measured on MI355X the two grid barriers plus
-// the uncached-memory round trips per iteration (~18 us) cost as much as the
-// per-iteration kernel launches they replace (profiles/README.md), and
-// rocprofv3 kernel tracing does not survive the cooperative launch.
 // Host side of the early stop: spin (with back-off) on the zero-copy verdict
 // of update j, which iteration j+1's gradient kernel publishes in its
 // prologue.  Bounded: the stream is synchronised as a fallback so a kernel
@@ -277,33 +275,37 @@ double LREngine::wait_flag(int j) {
   return v;
 }
 
-bool LREngine::persist_enabled() {
-  const char* e = std::getenv("TWTML_PERSIST");
-  return e && e[0] == '1';
-}
-
-void LREngine::ensure_coh(int grid, int64_t ns) {
-  const int64_t need_part = int64_t(grid) * sgd_part_stride(ns);
-  if (coh_.bar && need_part <= coh_part_cap_ && ns <= coh_ns_cap_ && grid <= coh_grid_cap_) return;
-  if (coh_.bar) {
-    TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
-    (void)hipFree(coh_.part);
-    (void)hipFree(coh_.w32);
-    (void)hipFree(coh_.norms);
-    (void)hipFree(coh_.bar);
+// Tiered-layout buffers: per-batch arrays of the nU compact slots (grown on
+// demand) and, at the first tiered batch, the entry-sized far lists / CSC.
+void LREngine::ensure_tier(int64_t n_unique) {
+  if (!prep_.fslot) {
+    const size_t E = size_t(prep_.cap_entries);
+    prep_.fslot = dmalloc<uint32_t>(E);
+    prep_.fcsc_pos = dmalloc<uint32_t>(E);
+    prep_.fcsc_slot = dmalloc<uint32_t>(E);
+    prep_.fcount = dmalloc<int32_t>(size_t(prep_.cap_chunks) + 1);
+    prep_.hist_near = dmalloc<uint32_t>(kMaxHybridSlots);
+    prep_.tparam = dmalloc<int64_t>(4);
+    sgd_.rbuf = dmalloc<float>(size_t(prep_.cap_rows16));
   }
-  coh_part_cap_ = std::max<int64_t>(need_part, coh_part_cap_ * 2);
-  coh_ns_cap_ = std::max<int64_t>(ns, coh_ns_cap_ * 2);
-  coh_grid_cap_ = std::max(grid, coh_grid_cap_);
-  auto uc = [](size_t bytes) {
-    void* ptr = nullptr;
-    TWTML_HIP_CHECK(hipExtMallocWithFlags(&ptr, std::max<size_t>(bytes, 256), hipDeviceMallocUncached));
-    return ptr;
-  };
-  coh_.part = static_cast<double*>(uc(sizeof(double) * size_t(coh_part_cap_)));
-  coh_.w32 = static_cast<float*>(uc(sizeof(float) * size_t(coh_ns_cap_)));
-  coh_.norms = static_cast<double*>(uc(sizeof(double) * 4 * size_t(coh_grid_cap_)));
-  coh_.bar = static_cast<GridBar*>(uc(sizeof(GridBar)));
+  if (n_unique <= prep_.cap_tier) return;
+  TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
+  void* old[] = {prep_.newslot, prep_.slot_fid, prep_.tscan, prep_.tscan_blk, prep_.fhist, prep_.fcur};
+  for (void* p : old) if (p) (void)hipFree(p);
+  const int64_t cap = std::max<int64_t>(n_unique, prep_.cap_tier * 2);
+  prep_.cap_tier = cap;
+  prep_.newslot = dmalloc<int32_t>(size_t(cap));
+  prep_.slot_fid = dmalloc<int32_t>(size_t(cap) + kNumNumeric + 2 * kPadSlots);
+  prep_.tscan = dmalloc<int64_t>(size_t(cap) + 1 + 2048);   // + 4096 u32 count buckets
+  prep_.tscan_blk = dmalloc<int64_t>(size_t(cap) / 8192 + 4);
+  prep_.fhist = dmalloc<uint64_t>(size_t(cap) + 1);
+  prep_.fcur = dmalloc<uint64_t>(size_t(cap) + 1);
+  if (cap + kNumNumeric + 64 > slot_hist_cap_) {
+    (void)hipFree(prep_.slot_hist);
+    slot_hist_cap_ = cap + kNumNumeric + 64;
+    prep_.slot_hist = dmalloc<uint32_t>(size_t(slot_hist_cap_));
+    TWTML_HIP_CHECK(hipMemset(prep_.slot_hist, 0, sizeof(uint32_t) * size_t(slot_hist_cap_)));
+  }
 }
 
 void LREngine::ensure_part(int64_t n) {
@@ -324,11 +326,14 @@ void LREngine::ensure_compact(int64_t ns) {
     (void)hipFree(sgd_.wc64);
     (void)hipFree(sgd_.wc32);
     (void)hipFree(sgd_.g64);
+    (void)hipFree(sgd_.gfix);
   }
   sgd_.wc64 = dmalloc<double>(size_t(cap));
   sgd_.wc32 = dmalloc<float>(size_t(cap));
   sgd_.g64 = dmalloc<double>(size_t(cap) + 1);
+  sgd_.gfix = dmalloc<uint64_t>(size_t(cap));   // far gradients (tiered), kept zeroed by k_sgd_update
   TWTML_HIP_CHECK(hipMemset(sgd_.g64, 0, sizeof(double) * (size_t(cap) + 1)));
+  TWTML_HIP_CHECK(hipMemset(sgd_.gfix, 0, sizeof(uint64_t) * size_t(cap)));
   ns_cap_ = cap;
 }
 
@@ -342,8 +347,11 @@ LREngine::~LREngine() {
                   prep_.hot_slot, prep_.hot_of, prep_.slot_hist, prep_.code,
                   prep_.cbase, prep_.idx, prep_.slot, prep_.y, prep_.num, prep_.perm, prep_.rtext, prep_.scan_tmp,
                   prep_.flags, prep_.uniq, prep_.slot_of, prep_.ublk, prep_.counters,
+                  prep_.fslot, prep_.fcount, prep_.fhist, prep_.fcur, prep_.fcsc_pos, prep_.fcsc_slot,
+                  prep_.newslot, prep_.slot_fid, prep_.tscan, prep_.tscan_blk, prep_.hist_near, prep_.tparam,
+                  sgd_.gfix, sgd_.rbuf,
                   sgd_.w64, sgd_.wc64, sgd_.wc32, sgd_.g64, sgd_.red64, sgd_.stats, sgd_.state,
-                  sgd_.loss_hist, sgd_.pred_out, sgd_.nrm, sgd_.wnorm_next, sgd_.part, sgd_.itrec, coh_.part, coh_.w32, coh_.norms, coh_.bar, gd_tdbg_, iter_tdbg_, lower_page_, lower_blocks_, n_global_};
+                  sgd_.loss_hist, sgd_.pred_out, sgd_.nrm, sgd_.wnorm_next, sgd_.part, sgd_.itrec, iter_tdbg_, lower_page_, lower_blocks_, n_global_};
   for (void* b : bufs) if (b) (void)hipFree(b);
   if (host_counters_) (void)hipHostFree(host_counters_);
   if (host_out_) (void)hipHostFree(host_out_);
@@ -423,12 +431,45 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   ensure_compact(ns);
   sgd_.ns = ns;
   sgd_.n_unique = nU;
-  const bool u16 = ns <= 65536;
-  const bool dedup = cfg_.dedup && u16 && dedup_supported(ns);
-  prep_.hybrid = (!dedup && cfg_.hybrid && u16 && res.n_kept > 0 && sgd_hybrid_fits(ns)) ? 1 : 0;
-  if (lazy && !prep_.hybrid) launch_featurize_fast_ids(b, prep_, fp, s);   // every id after all
-  if (prep_.hybrid) launch_remap_hybrid(prep_, res.entries, ns, kNumNumeric + nU, num_cu_, b, fp, lazy, s);
-  else launch_remap(prep_, res.entries, nU, u16, s);
+  // Active sets beyond LDS take the tiered layout (hot_split.hip / k_far_grad):
+  // decided from the global active set, so every DP rank takes the same path.
+  const bool tiered = !(ns <= 65536 && sgd_hybrid_fits(ns)) || force_tiered_;
+  const bool u16 = ns <= 65536 || tiered;   // tiered: the near streams are u16
+  const bool dedup = cfg_.dedup && !tiered && dedup_supported(ns);
+  prep_.tiered = tiered ? 1 : 0;
+  prep_.hybrid = (tiered || (!dedup && cfg_.hybrid && res.n_kept > 0)) ? 1 : 0;
+  sgd_.nl = ns;
+  sgd_.n_near = nU;
+  sgd_.far_base = kNumNumeric + nU;
+  sgd_.slot_fid = nullptr;
+  if (tiered) {
+    if (near_cap_ <= 0) {
+      near_cap_ = tier_near_cap();
+      if (const char* v = std::getenv("TWTML_NEAR_CAP"))   // tests / tuning: a smaller LDS tier
+        near_cap_ = std::max<int64_t>(64, std::min<int64_t>(near_cap_, std::atoll(v)));
+    }
+    const int64_t n_near = std::min(nU, near_cap_);
+    const int64_t nl = (kNumNumeric + n_near + kPadSlots + 63) / 64 * 64;
+    ensure_tier(nU);
+    prep_.near_end = kNumNumeric + n_near;
+    TWTML_HIP_CHECK(hipMemsetAsync(prep_.slot_hist + kNumNumeric, 0, sizeof(uint32_t) * size_t(nU), s));
+    launch_tier_hist(prep_, nU, num_cu_, s);
+    // every rank numbers the slots from the same (summed) sampled counts
+    if (world > 1) comm_->allreduce(prep_.slot_hist + kNumNumeric, size_t(nU), ncclUint32, ncclSum, s);
+    launch_tier_layout(prep_, res.entries, nU, n_near, ns, nl, num_cu_, b, fp, lazy, s);
+    sgd_.nl = nl;
+    sgd_.n_near = n_near;
+    sgd_.far_base = kNumNumeric + n_near;
+    sgd_.slot_fid = prep_.slot_fid;
+    sgd_.fcsc_pos = prep_.fcsc_pos;
+    sgd_.fcsc_slot = prep_.fcsc_slot;
+    sgd_.far_n = prep_.tparam + 2;
+    res.tiered = true;
+  } else {
+    if (lazy && !prep_.hybrid) launch_featurize_fast_ids(b, prep_, fp, s);   // every id after all
+    if (prep_.hybrid) launch_remap_hybrid(prep_, res.entries, ns, kNumNumeric + nU, num_cu_, b, fp, lazy, s);
+    else launch_remap(prep_, res.entries, nU, u16, s);
+  }
   if (lazy) raw_.release_slot(slot, s);
   prep_.dedup = dedup ? 1 : 0;
   if (prep_.dedup) launch_dedup(prep_, ns, kNumNumeric + nU, res.n_kept, s);
@@ -445,9 +486,11 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   tr_prep.reset();
   TraceRange tr_train("twtml.lr.train");   // GD iterations (host enqueue + early-stop polling)
 
-  int grid = cfg_.sgd_grid > 0 ? cfg_.sgd_grid : sgd_iter_grid(ns, res.n_kept, num_cu_, prep_.hybrid != 0);
-  sgd_.pstride = sgd_part_stride(ns);
-  sgd_.nparts = sgd_partials(ns, u16, grid);
+  const int64_t nl = sgd_.nl;
+  res.n_near = sgd_.n_near;
+  int grid = cfg_.sgd_grid > 0 ? cfg_.sgd_grid : sgd_iter_grid(nl, res.n_kept, num_cu_, prep_.hybrid != 0);
+  sgd_.pstride = sgd_part_stride(nl);
+  sgd_.nparts = sgd_partials(nl, u16, grid);
   ensure_part(int64_t(sgd_.nparts) * sgd_.pstride);
   SgdParams sp{};
   sp.step_size = cfg_.step_size;
@@ -460,6 +503,9 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   sp.ablate = cfg_.ablate;
   // entries one workgroup can add into a slot: its share of the chunks (x2 for imbalance)
   sp.fix_lim = sgd_fix_limit(2 * (res.entries / std::max(1, grid)) + 65536);
+  // far slots sum entries of every workgroup and rank
+  sp.far_lim = sgd_far_limit((res.entries + 65536) * int64_t(world));
+  const int64_t n_far = kNumNumeric + nU - sgd_.far_base;
   if (n_glob > 0) {
     // Host-side early stop: the convergence test of update j runs in the
     // prologue of iteration j+1's gradient kernel, which copies its verdict
@@ -480,41 +526,11 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
     std::fill(host_flags_, host_flags_ + iters + 2, -1.0);   // -1: verdict not published yet
     // single GPU with partial rows: the update kernel reduces them itself
     const bool fused = world == 1 && sgd_.nparts > 0;
-    // single GPU, hybrid layout: iterations 2..N in one persistent kernel
-    const int pgrid = (world == 1 && iters >= 2 && persist_enabled())
-                          ? sgd_persistent_grid(sgd_, prep_, u16, sp.sample != 0, num_cu_) : 0;
-    if (pgrid > 0) {
-      ensure_coh(pgrid, ns);
-      sp.iteration = 1;
-      launch_sgd_iter(sgd_, prep_, sp, host_counters_[2], u16, grid, s);
-      launch_sgd_update(sgd_, sp, sgd_.nparts, s);
-      TWTML_HIP_CHECK(hipMemsetAsync(coh_.bar, 0, sizeof(GridBar), s));
-      const bool timing = std::getenv("TWTML_GD_TIMING") != nullptr;
-      if (timing && !gd_tdbg_) gd_tdbg_ = dmalloc<uint64_t>(size_t(iters + 2) * 8);
-      coh_.tdbg = timing ? gd_tdbg_ : nullptr;
-      if (timing) TWTML_HIP_CHECK(hipMemsetAsync(gd_tdbg_, 0, sizeof(uint64_t) * size_t(iters + 2) * 8, s));
-      launch_sgd_persistent(sgd_, prep_, sp, coh_, 2, pgrid, s);
-      if (timing) {   // phase times of workgroup 0 (100 MHz clock): init pass barA update barB conv
-        std::vector<uint64_t> tb(size_t(iters + 2) * 8);
-        TWTML_HIP_CHECK(hipMemcpyAsync(tb.data(), gd_tdbg_, tb.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-        TWTML_HIP_CHECK(hipStreamSynchronize(s));
-        double acc[6] = {0, 0, 0, 0, 0, 0};
-        int n = 0;
-        for (int i = 2; i <= iters; ++i) {
-          const uint64_t* t = tb.data() + size_t(i) * 8;
-          if (t[6] == 0) break;
-          for (int k = 0; k < 6; ++k) acc[k] += double(t[k + 1] - t[k]) * 0.01;
-          ++n;
-        }
-        if (n) std::fprintf(stderr, "gd timing (us/iter, %d iters): init %.2f pass %.2f barA %.2f update %.2f barB %.2f conv %.2f\n",
-                            n, acc[0] / n, acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n);
-      }
-    }
     const bool itime = std::getenv("TWTML_ITER_TIMING") != nullptr;
     if (itime && !iter_tdbg_) iter_tdbg_ = dmalloc<uint64_t>(4096 + size_t(iters + 2) * 32);
     sgd_.tdbg = itime ? iter_tdbg_ : nullptr;
     if (itime) TWTML_HIP_CHECK(hipMemsetAsync(iter_tdbg_, 0, sizeof(uint64_t) * (4096 + size_t(iters + 2) * 32), s));
-    for (int i = 1; pgrid == 0 && i <= iters; ++i) {
+    for (int i = 1; i <= iters; ++i) {
       if (i > depth) {
         const int j = i - depth;                       // verdict after update j
         if (wait_flag(j) != 0.0) break;
@@ -523,9 +539,12 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
       // every rank launches the gradient kernel (an empty shard writes zero
       // partials) so every rank runs the convergence prologue
       launch_sgd_iter(sgd_, prep_, sp, host_counters_[2], u16, grid, s);
+      if (tiered) launch_far_grad(sgd_, sp, num_cu_, s);
       if (world > 1) {
         launch_sgd_reduce(sgd_, sp, s);
-        comm_->allreduce(sgd_.g64, size_t(ns + 1), ncclFloat64, ncclSum, s);
+        comm_->allreduce(sgd_.g64, size_t(nl + 1), ncclFloat64, ncclSum, s);
+        // far gradients are int64 fixed point: the sum over ranks is exact
+        if (n_far > 0) comm_->allreduce(sgd_.gfix, size_t(n_far), ncclUint64, ncclSum, s);
         if (sp.sample) comm_->allreduce(sgd_.red64 + 2 * (i & 1), 2, ncclFloat64, ncclSum, s);
       }
       launch_sgd_update(sgd_, sp, fused ? sgd_.nparts : 0, s);
@@ -578,7 +597,6 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   const double* st = host_out_ + 8;
   res.converged = st[1] != 0.0;
   res.overflow = st[7] == 1.0;
-  if (st[7] == 2.0) throw std::runtime_error("persistent GD kernel: grid barrier timed out");
   res.iterations = int32_t(st[3]);
   for (int i = 1; i <= res.iterations; ++i) res.loss_history.push_back(host_out_[16 + i]);
   TWTML_HIP_CHECK(hipEventElapsedTime(&res.prep_ms, ev_[0], ev_[1]));

@@ -100,6 +100,8 @@ struct BatchResult {
   bool converged = false;
   bool overflow = false;  // a residual hit the fixed-point clamp (diverging model)
   int64_t rows_lowered = 0, rows_narrowed = 0;   // device row normalisation (rows.hip)
+  bool tiered = false;    // active set beyond LDS: tiered layout (near slots in LDS, far via CSC)
+  int64_t n_near = 0;     // text slots in the LDS tier
   double stats[6] = {0, 0, 0, 0, 0, 0};  // n, sum y, sum y^2, sum p, sum p^2, sum (y-p)^2
   std::vector<double> loss_history;
   std::vector<float> pred;
@@ -139,8 +141,7 @@ class LREngine {
   void alloc_prepared();
   void ensure_compact(int64_t ns);
   void ensure_part(int64_t n);
-  void ensure_coh(int grid, int64_t ns);
-  static bool persist_enabled();
+  void ensure_tier(int64_t n_unique);
   double wait_flag(int j);
 
   int device_;
@@ -157,10 +158,9 @@ class LREngine {
   static constexpr int kNormRefresh = 256;
   int norm_age_ = -1;   // batches since the last full pass (-1: carried value invalid)
   int64_t part_cap_ = 0;
-  DevCoh coh_{};
-  int64_t coh_part_cap_ = 0, coh_ns_cap_ = 0;
-  int coh_grid_cap_ = 0;
-  uint64_t* gd_tdbg_ = nullptr;
+  int64_t near_cap_ = 0;          // tiered layout: LDS-resident text slots (tier_near_cap)
+  bool force_tiered_ = false;     // TWTML_FORCE_TIERED=1: tiered layout for any active set (tests)
+  int64_t slot_hist_cap_ = 0;
   uint64_t* iter_tdbg_ = nullptr;
   uint8_t* lower_page_ = nullptr;
   uint16_t* lower_blocks_ = nullptr;

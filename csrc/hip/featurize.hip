@@ -137,6 +137,10 @@ static void scan_excl_big(const int64_t* in, int64_t* out, int64_t n, int64_t* t
                      static_cast<const int64_t*>(tsum), int64_t(kScanTile));
 }
 
+void launch_scan_excl(const int64_t* in, int64_t* out, int64_t n, int64_t* total, int64_t* tsum, hipStream_t s) {
+  scan_excl_big(in, out, n, total, tsum, s);
+}
+
 void scan_excl_launch(const int64_t* in, int64_t* out, int64_t n, int64_t* total, hipStream_t s) {
   scan_excl(in, out, n, total, s);
 }

@@ -21,6 +21,9 @@
 // kMaxRegGroups) get the plain u16 layout and clen8c = -1.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <stdexcept>
+
 #include "common.h"
 #include "kernels.h"
 #include "narrow_text.h"
@@ -31,14 +34,6 @@ namespace {
 
 constexpr int kHistBlock = 1024;
 constexpr int kSplitWaves = 4;
-
-// LDS hand-off between the lanes of one wave (no other wave touches the
-// region): drain this wave's LDS traffic, then re-converge.
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
 
 // One wave per sampled chunk (c % kHistChunks == 0: the lazy featurizer
 // writes ids for exactly those fast chunks), all of its groups.
@@ -163,10 +158,27 @@ constexpr uint32_t kTagHot = 0x80000000u;
 
 __device__ __forceinline__ uint32_t slot_index(int32_t so) { return uint32_t(so) & 0xFFFFu; }
 
+// Tiered layout: slot_of holds the (renumbered) slot itself, tagged hot
+// (kTagHot | hot id << 16 | slot) or far (kTagFar | slot, 28 bits); the LDS
+// code of a small far id is kCodeFar16 ("look slot_of up").  Codes are 32
+// bit: kCodeHot | hot id, kCodeFar | far slot, or a near slot (< 2^14).
+constexpr uint32_t kTagFar = 0x40000000u;
+constexpr uint32_t kTagSlot = 0x0FFFFFFFu;
+constexpr uint32_t kCodeFar16 = 0x4000u;
+constexpr uint32_t kCodeFar = 0x40000000u;
+static_assert(kMaxHybridSlots <= int(kCodeFar16), "near slots must stay below the far LDS code");
+
+template <bool TIERED>
 __device__ __forceinline__ uint32_t id_code(const uint16_t* lcode, const DevPrepared& p, int32_t id) {
-  if (id < kCodeIds) return lcode[id];
+  if (id < kCodeIds) {
+    const uint32_t c = lcode[id];
+    if (TIERED && c == kCodeFar16) return kCodeFar | (uint32_t(p.slot_of[id]) & kTagSlot);
+    return c;
+  }
   const uint32_t so = uint32_t(p.slot_of[id]);
-  return (so & kTagHot) ? (kCodeHot | ((so >> 16) & 0xFFu)) : uint32_t(kNumNumeric) + (so & 0xFFFFu);
+  if (so & kTagHot) return kCodeHot | ((so >> 16) & 0xFFu);
+  if (TIERED) return (so & kTagFar) ? (kCodeFar | (so & kTagSlot)) : (so & kTagSlot);
+  return uint32_t(kNumNumeric) + (so & 0xFFFFu);
 }
 
 __global__ __launch_bounds__(1024) void k_code_tag(DevPrepared p, int64_t n_unique) {
@@ -193,6 +205,9 @@ __global__ __launch_bounds__(1024) void k_code_tag(DevPrepared p, int64_t n_uniq
 // in 8-entry groups: 37 % of the cold stream was padding).
 //   text    (from_text) fast chunks re-derive their ids from the raw text
 //           (narrow_text.h) instead of reading idx
+//   far     (TIERED) entries of far slots go to the chunk's far list
+//           (row << 28 | slot, at cbase * 512 ..) and count into fhist
+template <bool TIERED>
 __global__ __launch_bounds__(kSplitWaves * kWave) void k_remap_hybrid(DevPrepared p, int64_t ns,
                                                                       int64_t pad_base,
                                                                       const uint16_t* code,
@@ -201,6 +216,7 @@ __global__ __launch_bounds__(kSplitWaves * kWave) void k_remap_hybrid(DevPrepare
   __shared__ uint16_t lcode[kCodeIds];
   __shared__ uint32_t cnt[kSplitWaves][kRowsPerChunk * kCntStride];
   __shared__ uint32_t ccnt[kSplitWaves][kRowsPerChunk];
+  __shared__ uint32_t fcnt[kSplitWaves];
   for (int i = threadIdx.x; i < kCodeIds / 8; i += kSplitWaves * kWave)
     reinterpret_cast<uint4*>(lcode)[i] = reinterpret_cast<const uint4*>(code)[i];
   __syncthreads();
@@ -216,6 +232,7 @@ __global__ __launch_bounds__(kSplitWaves * kWave) void k_remap_hybrid(DevPrepare
   const uint32_t pad = uint32_t(pad_base + lane);
   uint16_t* plain = static_cast<uint16_t*>(p.slot);
   const NarrowHash nh(fp);
+  const uint32_t near_end = uint32_t(p.near_end);
 
   // the next chunk's packed row-text words are loaded one chunk ahead
   int64_t rt_next = (from_text && wave < nch) ? p.rtext[wave * kRowsPerChunk + lane / kLanesPerRow] : 0;
@@ -225,16 +242,44 @@ __global__ __launch_bounds__(kSplitWaves * kWave) void k_remap_hybrid(DevPrepare
     const int32_t L8 = p.clen8[c];
     const int64_t off = p.cbase[c] * kChunkStride + lane * kGroup;
     const int32_t* src = p.idx + off;
+    uint32_t* flist = TIERED ? p.fslot + p.cbase[c] * kChunkStride : nullptr;
+    if (TIERED) {
+      if (lane == 0) fcnt[w] = 0u;
+      wave_lds_sync();
+    }
+    auto far_put = [&](uint32_t cd) {   // TIERED: far entry of row r -> the chunk's far list
+      const uint32_t sl = cd & kTagSlot;
+      const uint32_t k = atomicAdd(&fcnt[w], 1u);
+      flist[k] = (uint32_t(r) << 28) | sl;
+      atomicAdd(reinterpret_cast<unsigned long long*>(&p.fhist[sl - near_end]), 1ull);
+    };
     if (L8 > kMaxRegGroups) {   // plain layout (as k_remap)
       for (int32_t g = 0; g < L8; ++g) {
         const int4* s4 = reinterpret_cast<const int4*>(src + int64_t(g) * kChunkStride);
         const int4 a = s4[0], b = s4[1];
         const int32_t v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
         uint32_t o[8];
+        if constexpr (TIERED) {   // rare (rows of > 320 bigrams): far entries to the far list
+          for (int e = 0; e < 8; ++e) {
+            uint32_t x = pad;
+            if (v[e] >= 0) {
+              const uint32_t cd = id_code<true>(lcode, p, v[e]);
+              if (cd & kCodeFar) far_put(cd);   // far codes carry a 28-bit slot: test first
+              else if (cd & kCodeHot) x = uint32_t(p.hot_slot[cd & 0xFFu]);
+              else x = cd;
+            }
+            o[e] = x;
+          }
+        } else {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = v[e] >= 0 ? uint32_t(kNumNumeric) + slot_index(p.slot_of[v[e]]) : pad;
+          for (int e = 0; e < 8; ++e) o[e] = v[e] >= 0 ? uint32_t(kNumNumeric) + slot_index(p.slot_of[v[e]]) : pad;
+        }
         *reinterpret_cast<uint4*>(plain + off + int64_t(g) * kChunkStride) =
             make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7]));
+      }
+      if (TIERED) {
+        wave_lds_sync();
+        if (lane == 0) p.fcount[c] = int32_t(fcnt[w]);
       }
       if (lane == 0) p.clen8c[c] = -1;
       continue;
@@ -250,7 +295,9 @@ __global__ __launch_bounds__(kSplitWaves * kWave) void k_remap_hybrid(DevPrepare
            (kk % kColdGroup)] = uint16_t(sl);
     };
     auto count = [&](uint32_t cd) {
-      if (cd & kCodeHot) {
+      if (TIERED && (cd & kCodeFar)) {   // far codes carry a 28-bit slot (bit 15 may be set)
+        far_put(cd);
+      } else if (cd & kCodeHot) {
         const uint32_t h = cd & 0xFFu;
         atomicAdd(&crow[h >> 1], 1u << ((h & 1u) * 16));
       } else {
@@ -258,7 +305,7 @@ __global__ __launch_bounds__(kSplitWaves * kWave) void k_remap_hybrid(DevPrepare
       }
     };
     auto big = [&](uint32_t cd) {   // rare pass: hot ids counting > 15 in the row go cold
-      if (!(cd & kCodeHot)) return;
+      if ((TIERED && (cd & kCodeFar)) || !(cd & kCodeHot)) return;
       const uint32_t h = cd & 0xFFu;
       if (((crow[h >> 1] >> ((h & 1u) * 16)) & 0xFFFFu) > 15u) put(uint32_t(p.hot_slot[h]));
     };
@@ -273,7 +320,7 @@ __global__ __launch_bounds__(kSplitWaves * kWave) void k_remap_hybrid(DevPrepare
 #pragma unroll
         for (int e8 = 0; e8 < kGroup; ++e8) {
           const int e = g * kGroup + e8;
-          if (e < L.my) count(id_code(lcode, p, int32_t(narrow_id(L, a, e, nh))));
+          if (e < L.my) count(id_code<TIERED>(lcode, p, int32_t(narrow_id(L, a, e, nh))));
         }
       }
     } else {
@@ -283,7 +330,7 @@ __global__ __launch_bounds__(kSplitWaves * kWave) void k_remap_hybrid(DevPrepare
         const int32_t v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          if (v[e] >= 0) count(id_code(lcode, p, v[e]));
+          if (v[e] >= 0) count(id_code<TIERED>(lcode, p, v[e]));
       }
     }
     wave_lds_sync();
@@ -319,7 +366,7 @@ __global__ __launch_bounds__(kSplitWaves * kWave) void k_remap_hybrid(DevPrepare
 #pragma unroll
           for (int e8 = 0; e8 < kGroup; ++e8) {
             const int e = g * kGroup + e8;
-            if (e < L.my) big(id_code(lcode, p, int32_t(narrow_id(L, a2, e, nh))));
+            if (e < L.my) big(id_code<TIERED>(lcode, p, int32_t(narrow_id(L, a2, e, nh))));
           }
         }
       } else {
@@ -329,11 +376,12 @@ __global__ __launch_bounds__(kSplitWaves * kWave) void k_remap_hybrid(DevPrepare
           const int32_t v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 #pragma unroll
           for (int e = 0; e < 8; ++e)
-            if (v[e] >= 0) big(id_code(lcode, p, v[e]));
+            if (v[e] >= 0) big(id_code<TIERED>(lcode, p, v[e]));
         }
       }
     }
     wave_lds_sync();   // every cold entry of the chunk is counted
+    if (TIERED && lane == 0) p.fcount[c] = int32_t(fcnt[w]);
     const uint32_t rc = ccnt[w][r];
     const int32_t mine = rc > uint32_t(t) ? int32_t((rc - uint32_t(t) + 3u) >> 2) : 0;   // this lane's entries
     const int32_t L4c = wave_max((mine + kColdGroup - 1) / kColdGroup);
@@ -342,6 +390,172 @@ __global__ __launch_bounds__(kSplitWaves * kWave) void k_remap_hybrid(DevPrepare
       own[int64_t(kk / kColdGroup) * kColdStride + kk % kColdGroup] = uint16_t(pad);
     if (lane == 0) p.clen8c[c] = L4c;
     wave_lds_sync();   // the next chunk clears / refills this wave's LDS
+  }
+}
+
+
+// ---------------------------------------------------------------------------
+// Tiered layout (active set beyond LDS).
+// ---------------------------------------------------------------------------
+// Sampled counts of compact slots [lo, hi) (slot_of still holds compact
+// indices): LDS histogram of the range, non-zero bins flushed with one
+// global atomic each.  Multiple ranges = multiple launches.
+constexpr int kTierHistSpan = 32768;
+
+__global__ __launch_bounds__(kHistBlock) void k_tier_hist(DevPrepared p, int64_t lo, int64_t hi) {
+  __shared__ uint32_t h[kTierHistSpan];
+  const int64_t span = hi - lo;
+  for (int64_t i = threadIdx.x; i < span; i += kHistBlock) h[i] = 0u;
+  __syncthreads();
+  const int lane = lane_id();
+  const int64_t n_kept = p.counters[0];
+  const int64_t nsamp = ((n_kept + kRowsPerChunk - 1) / kRowsPerChunk + kHistChunks - 1) / kHistChunks;
+  const int64_t wave = (int64_t(blockIdx.x) * kHistBlock + threadIdx.x) / kWave;
+  const int64_t nwaves = int64_t(gridDim.x) * kHistBlock / kWave;
+  for (int64_t sc = wave; sc < nsamp; sc += nwaves) {
+    const int64_t c = sc * kHistChunks;
+    const int32_t L8 = p.clen8[c];
+    const int32_t* src = p.idx + p.cbase[c] * kChunkStride + lane * kGroup;
+    for (int32_t g = 0; g < L8; ++g) {
+      const int4* s4 = reinterpret_cast<const int4*>(src + int64_t(g) * kChunkStride);
+      const int4 a = s4[0], b = s4[1];
+      const int32_t v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (v[e] >= 0) {
+          const int64_t u = p.slot_of[v[e]] - lo;
+          if (u >= 0 && u < span) atomicAdd(&h[u], 1u);
+        }
+    }
+  }
+  __syncthreads();
+  for (int64_t i = threadIdx.x; i < span; i += kHistBlock)
+    if (h[i]) atomicAdd(&p.slot_hist[kNumNumeric + lo + i], h[i]);
+}
+
+// Count buckets: exact below 2048, then 128 log-spaced buckets per octave
+// (monotone in the count).
+constexpr int kCountBuckets = 4096;
+__device__ __forceinline__ int count_bucket(uint32_t c) {
+  if (c < 2048u) return int(c);
+  const int e = 31 - __builtin_clz(c);                 // >= 11
+  const int b = 2048 + (e - 11) * 128 + int((c >> (e - 7)) & 127u);
+  return b < kCountBuckets ? b : kCountBuckets - 1;
+}
+
+__global__ __launch_bounds__(1024) void k_tier_buckets(const uint32_t* hist, int64_t n, uint32_t* cb) {
+  __shared__ uint32_t lb[kCountBuckets];
+  for (int i = threadIdx.x; i < kCountBuckets; i += 1024) lb[i] = 0u;
+  __syncthreads();
+  for (int64_t u = int64_t(blockIdx.x) * 1024 + threadIdx.x; u < n; u += int64_t(gridDim.x) * 1024)
+    atomicAdd(&lb[count_bucket(hist[u])], 1u);
+  __syncthreads();
+  for (int i = threadIdx.x; i < kCountBuckets; i += 1024)
+    if (lb[i]) atomicAdd(&cb[i], lb[i]);
+}
+
+// Threshold bucket B: the K near slots are every slot in a bucket above B
+// plus the first `need` slots (by compact index) of bucket B.
+__global__ void k_tier_threshold(const uint32_t* cb, int64_t K, int64_t* tparam) {
+  if (threadIdx.x != 0) return;
+  int64_t above = 0;
+  int B = 0;
+  for (int b = kCountBuckets - 1; b >= 0; --b) {
+    if (above + int64_t(cb[b]) >= K) { B = b; break; }
+    above += cb[b];
+  }
+  tparam[0] = B;
+  tparam[1] = K - above;
+}
+
+__global__ __launch_bounds__(1024) void k_tier_eqflag(const uint32_t* hist, int64_t n, const int64_t* tparam,
+                                                      int64_t* flag) {
+  const int B = int(tparam[0]);
+  for (int64_t u = int64_t(blockIdx.x) * 1024 + threadIdx.x; u < n; u += int64_t(gridDim.x) * 1024)
+    flag[u] = count_bucket(hist[u]) == B ? 1 : 0;
+}
+
+// eqrank (scanned) -> near flag, kept in newslot until the numbering pass
+__global__ __launch_bounds__(1024) void k_tier_nearflag(const uint32_t* hist, int64_t n, const int64_t* tparam,
+                                                        int64_t* scan, int32_t* newslot) {
+  const int B = int(tparam[0]);
+  const int64_t need = tparam[1];
+  for (int64_t u = int64_t(blockIdx.x) * 1024 + threadIdx.x; u < n; u += int64_t(gridDim.x) * 1024) {
+    const int b = count_bucket(hist[u]);
+    const bool near = b > B || (b == B && scan[u] < need);
+    newslot[u] = near ? 1 : 0;
+    scan[u] = near ? 1 : 0;
+  }
+}
+
+// near rank (scanned) -> slot numbering: near slots 4.., far from near_end
+__global__ __launch_bounds__(1024) void k_tier_number(DevPrepared p, const uint32_t* hist, int64_t n,
+                                                      const int64_t* scan) {
+  const int64_t near_end = p.near_end;
+  for (int64_t u = int64_t(blockIdx.x) * 1024 + threadIdx.x; u < n; u += int64_t(gridDim.x) * 1024) {
+    const int64_t nr = scan[u];
+    const bool near = p.newslot[u] != 0;
+    const int64_t sl = near ? kNumNumeric + nr : near_end + (u - nr);
+    p.newslot[u] = int32_t(sl);
+    p.slot_fid[sl] = p.uniq[u];
+    if (near) p.hist_near[sl] = hist[u];
+  }
+}
+
+// Codes of small ids (LDS table) and tags of every active id (tiered).
+__global__ __launch_bounds__(1024) void k_code_table_tiered(DevPrepared p, uint16_t* code) {
+  const int id = blockIdx.x * 1024 + threadIdx.x;
+  if (id >= kCodeIds) return;
+  const int64_t nU = p.counters[1];
+  uint32_t c = 0xFFFFu;
+  if (id < p.flag_len) {
+    const int32_t u = p.slot_of[id];
+    if (u >= 0 && u < nU && p.uniq[u] == id) {
+      const int64_t sl = p.newslot[u];
+      if (sl >= p.near_end) {
+        c = kCodeFar16;
+      } else {
+        const uint32_t h = p.hot_of[sl];
+        c = h != 0xFFu ? (kCodeHot | h) : uint32_t(sl);
+      }
+    }
+  }
+  code[id] = uint16_t(c);
+}
+
+__global__ __launch_bounds__(1024) void k_code_tag_tiered(DevPrepared p, int64_t n_unique) {
+  const int64_t u = int64_t(blockIdx.x) * 1024 + threadIdx.x;
+  if (u >= n_unique) return;
+  const int32_t id = p.uniq[u];
+  const uint32_t sl = uint32_t(p.newslot[u]);
+  uint32_t tag;
+  if (int64_t(sl) >= p.near_end) {
+    tag = kTagFar | sl;
+  } else {
+    const uint32_t h = p.hot_of[sl];
+    tag = h != 0xFFu ? (kTagHot | (h << 16) | sl) : sl;
+  }
+  p.slot_of[id] = int32_t(tag);
+}
+
+// Far CSC: every far entry of every chunk list -> its slot's segment.
+__global__ __launch_bounds__(256) void k_far_csc(DevPrepared p) {
+  const int lane = lane_id();
+  const int64_t n_kept = p.counters[0];
+  const int64_t nch = (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;
+  const int64_t wave = (int64_t(blockIdx.x) * 256 + threadIdx.x) / kWave;
+  const int64_t nwaves = int64_t(gridDim.x) * 256 / kWave;
+  const uint32_t near_end = uint32_t(p.near_end);
+  for (int64_t c = wave; c < nch; c += nwaves) {
+    const int32_t fc = p.fcount[c];
+    const uint32_t* fl = p.fslot + p.cbase[c] * kChunkStride;
+    for (int32_t k = lane; k < fc; k += kWave) {
+      const uint32_t e = fl[k];
+      const uint32_t sl = e & kTagSlot;
+      const uint64_t at = atomicAdd(reinterpret_cast<unsigned long long*>(&p.fcur[sl - near_end]), 1ull);
+      p.fcsc_pos[at] = uint32_t(c * kRowsPerChunk + (e >> 28));
+      p.fcsc_slot[at] = sl;
+    }
   }
 }
 
@@ -366,8 +580,73 @@ void launch_remap_hybrid(const DevPrepared& p, int64_t entries, int64_t ns, int6
   // persistent-style grid (each workgroup loads the 16 KB code table once)
   int grid = int(std::min<int64_t>(int64_t(num_cu) * 4, (cmax + kSplitWaves - 1) / kSplitWaves));
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL(k_remap_hybrid, dim3(grid), dim3(kSplitWaves * kWave), 0, s, p, ns, pad_base, p.code,
+  hipLaunchKernelGGL(k_remap_hybrid<false>, dim3(grid), dim3(kSplitWaves * kWave), 0, s, p, ns, pad_base, p.code,
                      b, fp, from_text ? 1 : 0);
+}
+
+
+void launch_tier_hist(const DevPrepared& p, int64_t n_unique, int num_cu, hipStream_t s) {
+  // slot_hist[4 .. 4 + nU) zeroed by the caller
+  const int64_t cmax = (p.cap_rows + kRowsPerChunk - 1) / kRowsPerChunk;
+  const int64_t nsamp = (cmax + kHistChunks - 1) / kHistChunks;
+  int gh = int((nsamp + kHistBlock / kWave - 1) / (kHistBlock / kWave));
+  gh = std::max(1, std::min(gh, num_cu / 2));
+  for (int64_t lo = 0; lo < n_unique; lo += kTierHistSpan)
+    hipLaunchKernelGGL(k_tier_hist, dim3(gh), dim3(kHistBlock), 0, s, p, lo,
+                       std::min<int64_t>(n_unique, lo + kTierHistSpan));
+}
+
+int64_t tier_near_cap() {
+  // LDS slot space 4 + n_near + pads (rounded to 64) must fit the hybrid
+  // kernel plus the tiered kernel's far-dot scratch
+  for (int64_t n = kMaxHybridSlots; n >= 64; n -= 64) {
+    const int64_t nl = (kNumNumeric + n + kPadSlots + 63) / 64 * 64;
+    if (nl <= kMaxHybridSlots && sgd_hybrid_fits(nl)) return n;
+  }
+  return 0;
+}
+
+void launch_tier_layout(const DevPrepared& p, int64_t entries, int64_t n_unique, int64_t n_near, int64_t ns,
+                        int64_t nl, int num_cu, const DevRawBatch& b, const FeaturizeParams& fp, bool from_text,
+                        hipStream_t s) {
+  if (n_unique + kNumNumeric + kPadSlots >= (int64_t(1) << 28)) throw std::invalid_argument("tiered layout: too many active slots");
+  if (nl > kMaxHybridSlots) throw std::invalid_argument("tiered layout: near tier exceeds LDS");
+  const uint32_t* hist = p.slot_hist + kNumNumeric;
+  const int g = int(std::max<int64_t>(1, std::min<int64_t>((n_unique + 1023) / 1024, int64_t(num_cu) * 4)));
+  // count buckets: 4096 u32 after the cap_tier + 1 scan elements of tscan
+  uint32_t* buckets = reinterpret_cast<uint32_t*>(p.tscan + p.cap_tier + 1);
+  TWTML_HIP_CHECK(hipMemsetAsync(buckets, 0, sizeof(uint32_t) * kCountBuckets, s));
+  hipLaunchKernelGGL(k_tier_buckets, dim3(g), dim3(1024), 0, s, hist, n_unique, buckets);
+  hipLaunchKernelGGL(k_tier_threshold, dim3(1), dim3(kWave), 0, s, buckets, n_near, p.tparam);
+  hipLaunchKernelGGL(k_tier_eqflag, dim3(g), dim3(1024), 0, s, hist, n_unique, p.tparam, p.tscan);
+  launch_scan_excl(p.tscan, p.tscan, n_unique, p.tparam + 3, p.tscan_blk, s);
+  hipLaunchKernelGGL(k_tier_nearflag, dim3(g), dim3(1024), 0, s, hist, n_unique, p.tparam, p.tscan, p.newslot);
+  launch_scan_excl(p.tscan, p.tscan, n_unique, p.tparam + 3, p.tscan_blk, s);
+  TWTML_HIP_CHECK(hipMemsetAsync(p.hist_near, 0, sizeof(uint32_t) * kMaxHybridSlots, s));
+  hipLaunchKernelGGL(k_tier_number, dim3(g), dim3(1024), 0, s, p, hist, n_unique, p.tscan);
+  // hot ids among the near slots (new numbering)
+  hipLaunchKernelGGL(k_hot_select, dim3(1), dim3(1024), 0, s, p.hist_near, nl, p.near_end, p.hot_of,
+                     p.hot_slot);
+  hipLaunchKernelGGL(k_code_table_tiered, dim3(kCodeIds / 1024), dim3(1024), 0, s, p, p.code);
+  hipLaunchKernelGGL(k_code_tag_tiered, dim3(int((n_unique + 1023) / 1024)), dim3(1024), 0, s, p, n_unique);
+  const int64_t n_far = kNumNumeric + n_unique - p.near_end;
+  TWTML_HIP_CHECK(hipMemsetAsync(p.fhist, 0, sizeof(uint64_t) * size_t(n_far + 1), s));
+  if (entries > 0) {
+    const int64_t cmax = (p.cap_rows + kRowsPerChunk - 1) / kRowsPerChunk;
+    int grid = int(std::min<int64_t>(int64_t(num_cu) * 4, (cmax + kSplitWaves - 1) / kSplitWaves));
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL(k_remap_hybrid<true>, dim3(grid), dim3(kSplitWaves * kWave), 0, s, p, ns, p.near_end,
+                       p.code, b, fp, from_text ? 1 : 0);
+  }
+  // CSC offsets (exclusive scan of the far counts, in place), cursors, scatter
+  launch_scan_excl(reinterpret_cast<const int64_t*>(p.fhist), reinterpret_cast<int64_t*>(p.fhist), n_far,
+                   p.tparam + 2, p.tscan_blk, s);
+  TWTML_HIP_CHECK(hipMemcpyAsync(p.fcur, p.fhist, sizeof(uint64_t) * size_t(n_far), hipMemcpyDeviceToDevice, s));
+  if (entries > 0) {
+    const int64_t cmax = (p.cap_rows + kRowsPerChunk - 1) / kRowsPerChunk;
+    const int grid = int(std::max<int64_t>(1, std::min<int64_t>((cmax + 3) / 4, int64_t(num_cu) * 8)));
+    hipLaunchKernelGGL(k_far_csc, dim3(grid), dim3(256), 0, s, p);
+  }
 }
 
 }  // namespace twtml

@@ -145,8 +145,28 @@ struct DevPrepared {
   int32_t* hot_slot;        // [kHot] slot of hot id h (a zero-weight pad slot when unused)
   uint8_t* hot_of;          // [kMaxHybridSlots] hot id of a slot (0xFF = cold)
   uint16_t* code;           // [8192] remap code of small hashed ids (hot_split.hip)
-  uint32_t* slot_hist;      // [kMaxHybridSlots] sampled slot frequencies
+  uint32_t* slot_hist;      // [max(kMaxHybridSlots, cap_tier + 64)] sampled slot frequencies
   int32_t hybrid;           // 1: iteration kernels use the hybrid layout
+  // Tiered layout (active sets beyond LDS, tiered.hip): the near_end - 4
+  // most frequent text slots [4, near_end) keep the hybrid layout (hot
+  // counts + LDS cold stream); far slots [near_end, 4 + nU) are per-chunk
+  // lists of (row << 28 | slot) entries for the forward pass plus a
+  // slot-sorted CSC of the same entries for the backward segmented sum.
+  int32_t tiered;
+  int64_t near_end;
+  uint32_t* fslot;          // [E] far entries of chunk c from cbase[c] * 512 on
+  int32_t* fcount;          // [C] far entries per chunk
+  uint64_t* fhist;          // [cap_tier + 1] entries per far slot, scanned in place into CSC offsets
+  uint64_t* fcur;           // [cap_tier] CSC scatter cursors
+  uint32_t* fcsc_pos;       // [E] CSC: sorted position of the entry's row
+  uint32_t* fcsc_slot;      // [E] CSC: far slot of the entry
+  int32_t* newslot;         // [cap_tier] compact index u -> slot
+  int32_t* slot_fid;        // [cap_tier + 64] slot -> feature id
+  int64_t* tscan;           // [cap_tier + 1] scan scratch
+  int64_t* tscan_blk;       // [cap_tier / 8192 + 2]
+  uint32_t* hist_near;      // [kMaxHybridSlots] sampled counts of the near slots (new numbering)
+  int64_t* tparam;          // [4] near threshold T, ties to take, far entries, -
+  int64_t cap_tier;
   // counters (device): [0]=n_kept [1]=n_unique [2]=groups [3]=error
   int64_t* counters;
   int64_t cap_rows, cap_rows16, cap_entries, cap_chunks, flag_len;
@@ -194,6 +214,24 @@ constexpr int kMaxHybridSlots = 16384;
 void launch_remap_hybrid(const DevPrepared& p, int64_t entries, int64_t ns, int64_t pad_base, int num_cu,
                          const DevRawBatch& b, const FeaturizeParams& fp, bool from_text, hipStream_t s);
 
+// Exclusive int64 scan (in place safe); tsum: ceil(n / 8192) + 2 scratch.
+void launch_scan_excl(const int64_t* in, int64_t* out, int64_t n, int64_t* total, int64_t* tsum, hipStream_t s);
+
+// ---------------------------------------------------------------------------
+// Tiered layout (tiered.hip), in place of launch_remap_hybrid when the active
+// set does not fit LDS.  Step 1 (before the DP sum of the histogram):
+// sampled counts of the nU compact slots into slot_hist[4 + u].
+void launch_tier_hist(const DevPrepared& p, int64_t n_unique, int num_cu, hipStream_t s);
+// Step 2: near tier = the n_near most frequent slots (ties by index, so
+// every DP rank numbers slots alike), renumbering, hot ids among the near
+// slots, id codes, then the remap (hybrid streams + far lists) and the far
+// CSC.  ns: 4 + nU + pads; nl: LDS slot space (4 + n_near + pads).
+void launch_tier_layout(const DevPrepared& p, int64_t entries, int64_t n_unique, int64_t n_near, int64_t ns,
+                        int64_t nl, int num_cu, const DevRawBatch& b, const FeaturizeParams& fp, bool from_text,
+                        hipStream_t s);
+// Largest n_near whose LDS slot space 4 + n_near + pads fits the hybrid kernel.
+int64_t tier_near_cap();
+
 // ---------------------------------------------------------------------------
 // SGD on the compact active set.
 struct DevSgd {
@@ -211,6 +249,17 @@ struct DevSgd {
   double* part;         // [nparts][pstride] per-workgroup partial gradients (LDS paths)
   double* itrec;        // [max_iters+2][kRecStride] per-iteration update records
   uint64_t* tdbg;       // optional phase stamps (TWTML_ITER_TIMING): [iter][wg 0 / last][8]
+  // LDS / partial-row slot space: nl slots (= ns unless tiered), text slots
+  // [4, 4 + n_near) in LDS; tiered: far slots [far_base, 4 + n_unique)
+  int64_t nl;
+  int64_t n_near;
+  int64_t far_base;
+  uint64_t* gfix;       // [ns] far gradients, 2^-24 fixed point, by slot - far_base (tiered)
+  float* rbuf;          // [R16] residual per sorted position (tiered backward)
+  const int32_t* slot_fid;   // slot -> feature id (tiered); null: uniq[slot - 4]
+  const uint32_t* fcsc_pos;
+  const uint32_t* fcsc_slot;
+  const int64_t* far_n;      // device: far entries (CSC length)
   int64_t F;
   int64_t ns;           // 4 + n_unique + pads (rounded)
   int64_t n_unique;
@@ -221,25 +270,6 @@ struct DevSgd {
 };
 
 constexpr int kNormParts = 1024;   // grid cap of the norm / gather / scatter kernels
-
-// Grid barrier of the persistent GD kernel (uncached memory): per-XCD-group
-// arrival counters (64 B apart), global counter, generation, error flag.
-struct GridBar {
-  uint32_t cnt[8 * 16];
-  uint32_t gcnt, pad0[15];
-  uint32_t gen, pad1[15];
-  uint32_t err, pad2[15];
-};
-
-constexpr int kMaxPersistGrid = 512;
-// Cross-workgroup buffers of the persistent GD kernel (hipDeviceMallocUncached)
-struct DevCoh {
-  double* part;     // [G][pstride] partial rows
-  float* w32;       // [ns] compact fp32 weights after each update
-  double* norms;    // [2][G][2] per-workgroup ||dw||^2, ||w||^2 (iteration parity)
-  GridBar* bar;
-  uint64_t* tdbg;   // optional [iters][8] s_memrealtime stamps of workgroup 0 (TWTML_GD_TIMING)
-};
 
 // Iteration record: [0] updates so far, [1] m, [2] update workgroups,
 // [kRecHead + 2w] ||dw||^2 and ||w||^2 partials of update workgroup w.
@@ -263,11 +293,14 @@ struct SgdParams {
                         // hybrid only: 3 = skip hot grad, 4 = skip hot dot, 5 = skip cold scatter,
                         // 6 = loads only, 7 = no chunks (fixed cost)
   float fix_lim;        // |r| * 2^24 clamp so a workgroup's int64 slot sums cannot overflow
+  float far_lim;        // |r| * 2^16 clamp of the far (tiered) gradient: batch-wide int64 sums
 };
 
 // Fixed-point clamp for a launch: every slot of a workgroup receives at most
 // `entries_per_wg` contributions, each |q| <= lim, so lim * entries < 2^62.
 float sgd_fix_limit(int64_t entries_per_wg);
+// Far-gradient clamp: `entries_total` entries (all ranks) may add into one slot.
+float sgd_far_limit(int64_t entries_total);
 
 void launch_gather_w(const DevSgd& d, const DevPrepared& p, hipStream_t s);
 void launch_norm2(const double* v, int64_t n, double* out, const DevSgd& d, hipStream_t s);
@@ -280,11 +313,9 @@ int sgd_partials(int64_t ns, bool u16, int grid);
 void launch_sgd_reduce(const DevSgd& d, const SgdParams& sp, hipStream_t s);
 // nparts > 0: sums the partial rows itself (single GPU, no separate reduce)
 void launch_sgd_update(const DevSgd& d, const SgdParams& sp, int nparts, hipStream_t s);
-// persistent loop for iterations it_first..N (single GPU); grid from
-// sgd_persistent_grid (0 = use the per-iteration kernels)
-int sgd_persistent_grid(const DevSgd& d, const DevPrepared& p, bool u16, bool sample, int num_cu);
-void launch_sgd_persistent(const DevSgd& d, const DevPrepared& p, const SgdParams& sp, const DevCoh& coh,
-                           int it_first, int grid, hipStream_t s);
+// Far backward of one iteration: gfix[slot - far_base] += sum of the fixed-
+// point residuals of the slot's entries (CSC segmented sums).
+void launch_far_grad(const DevSgd& d, const SgdParams& sp, int num_cu, hipStream_t s);
 // after the GD loop: convergence of the last update -> state
 void launch_sgd_finish(const DevSgd& d, const SgdParams& sp, hipStream_t s);
 void launch_scatter_w(const DevSgd& d, const DevPrepared& p, hipStream_t s);

@@ -29,6 +29,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <stdexcept>
 
 #include "common.h"
 #include "kernels.h"
@@ -43,33 +44,17 @@ namespace twtml {
 constexpr float kFixScale = 16777216.0f;        // 2^24
 constexpr double kFixInv = 1.0 / 16777216.0;
 constexpr float kFixClamp = 67108864.0f;        // 2^26
+// Far gradients (tiered layout) sum over all of a slot's entries in the
+// batch (all ranks): a coarser 2^-16 scale and a clamp from the batch's
+// entry count keep those int64 sums from overflowing (SgdParams::far_lim).
+constexpr float kFarScale = 65536.0f;           // 2^16
+constexpr double kFarInv = 1.0 / 65536.0;
 
 // Iteration record i (k_sgd_update -> convergence test) and the sampled row
 // count of iteration i (double-buffered by parity: iteration i+1's count is
 // zeroed while iteration i's is still being read).
 __device__ __forceinline__ double* sgd_rec(const DevSgd& d, int it) { return d.itrec + int64_t(it) * kRecStride; }
 __device__ __forceinline__ double* sgd_red_m(const DevSgd& d, int it) { return d.red64 + 2 * (it & 1) + 1; }
-
-template <typename SlotT>
-struct SlotLoad;
-
-template <>
-struct SlotLoad<uint16_t> {
-  __device__ __forceinline__ static void load(const uint16_t* p, uint32_t (&s)[8]) {
-    const uint4 v = *reinterpret_cast<const uint4*>(p);
-    s[0] = v.x & 0xFFFF; s[1] = v.x >> 16; s[2] = v.y & 0xFFFF; s[3] = v.y >> 16;
-    s[4] = v.z & 0xFFFF; s[5] = v.z >> 16; s[6] = v.w & 0xFFFF; s[7] = v.w >> 16;
-  }
-};
-
-template <>
-struct SlotLoad<uint32_t> {
-  __device__ __forceinline__ static void load(const uint32_t* p, uint32_t (&s)[8]) {
-    const uint4 a = reinterpret_cast<const uint4*>(p)[0];
-    const uint4 b = reinterpret_cast<const uint4*>(p)[1];
-    s[0] = a.x; s[1] = a.y; s[2] = a.z; s[3] = a.w; s[4] = b.x; s[5] = b.y; s[6] = b.z; s[7] = b.w;
-  }
-};
 
 __device__ __forceinline__ void unpack4(const uint2 v, uint32_t (&s)[4]) {
   s[0] = v.x & 0xFFFF; s[1] = v.x >> 16; s[2] = v.y & 0xFFFF; s[3] = v.y >> 16;
@@ -135,30 +120,6 @@ __device__ __forceinline__ float row_residual(float dot, int64_t pos, int t, con
   return row_residual<STATS, SAMPLE>(dot, row_in(p, pos), pos, t, d, p, sp, n_kept, w0, w1, w2, w3, acc);
 }
 
-template <bool STATS, bool SAMPLE>
-__device__ __forceinline__ void flush_scalars(const DevSgd& d, const RowAcc& acc, double* scratch, int it) {
-  const double b0 = block_sum<double>(acc.gn0, scratch);
-  const double b1 = block_sum<double>(acc.gn1, scratch);
-  const double b2 = block_sum<double>(acc.gn2, scratch);
-  const double b3 = block_sum<double>(acc.gn3, scratch);
-  const double bl = block_sum<double>(0.5 * double(acc.loss), scratch);
-  double bm = 0.0;
-  if (SAMPLE) bm = block_sum<double>(acc.msum, scratch);
-  double bs[6] = {0, 0, 0, 0, 0, 0};
-  if (STATS)
-    for (int k = 0; k < 6; ++k) bs[k] = block_sum<double>(acc.st[k], scratch);
-  if (threadIdx.x == 0) {
-    atomicAdd(&d.g64[0], b0);
-    atomicAdd(&d.g64[1], b1);
-    atomicAdd(&d.g64[2], b2);
-    atomicAdd(&d.g64[3], b3);
-    atomicAdd(&d.g64[d.ns], bl);
-    if (SAMPLE) atomicAdd(sgd_red_m(d, it), bm);
-    if (STATS)
-      for (int k = 0; k < 6; ++k) atomicAdd(&d.stats[k], bs[k]);
-  }
-}
-
 // Workgroup epilogue without contended atomics.  Every workgroup writes one
 // partial row (plain stores) that k_sgd_reduce sums in a fixed order:
 //   cols 0..3 numeric gradients, 4..hi-1 text slots, hi..ns-1 pads (0),
@@ -192,7 +153,7 @@ __device__ __forceinline__ void part_scalars(const DevSgd& d, const RowAcc& acc,
     double t = 0.0;
     if (tid < nv)
       for (int k = 0; k < int(blockDim.x) / kWave; ++k) t += wsc[k][tid];
-    prow[tid < kNumNumeric ? int64_t(tid) : d.ns + (tid - kNumNumeric)] = t;
+    prow[tid < kNumNumeric ? int64_t(tid) : d.nl + (tid - kNumNumeric)] = t;
   }
 }
 
@@ -204,6 +165,11 @@ __device__ __forceinline__ double part_slot(const unsigned long long* gl, int64_
 #pragma unroll
   for (int k = 0; k < REP; ++k) v += (long long)gl[s * REP + k];
   return double(v) * kFixInv;
+}
+
+float sgd_far_limit(int64_t entries_total) {
+  const double e = double(entries_total < 1 ? 1 : entries_total);
+  return float(std::min(double(kFixClamp) * double(kFarScale), 4.611686018427388e18 / e) * 0.999);
 }
 
 float sgd_fix_limit(int64_t entries_per_wg) {
@@ -279,7 +245,7 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_lds(DevSgd d, DevPrepar
   __shared__ double wsc[kIterBlock / kWave][kPartVals];
   __shared__ int stop_flag;
   if (sgd_stop(d, sp, &stop_flag)) return;  // converged / finished: the rest of the batch is a no-op
-  const int64_t ns = d.ns;        // multiple of 64
+  const int64_t ns = d.nl;        // multiple of 64 (== d.ns: the plain path is never tiered)
   float* wl = lds;
   unsigned long long* gl = reinterpret_cast<unsigned long long*>(lds + ns);
   for (int64_t s = threadIdx.x; s < ns; s += kIterBlock) wl[s] = d.wc32[s];
@@ -413,7 +379,6 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_lds(DevSgd d, DevPrepar
 // fixed-point gradient.  Chunks left
 // in the plain layout (clen8c < 0) take the plain route.
 // ---------------------------------------------------------------------------
-constexpr int kHotRows = kWave / 16;  // 16-lane rows per wave (hot-gradient partials per wave)
 constexpr int kMaxColdGroups = 8;   // cold 4-entry groups kept in VGPRs (32 cold entries per lane)
 constexpr int kHotPerLane = kHot / kLanesPerRow;   // 32
 
@@ -517,12 +482,15 @@ __device__ __forceinline__ float sgpr_f(float v) {
 }
 
 // wctr: the workgroup's LDS chunk counter, zeroed by hyb_lds_init.
-template <bool STATS, bool SAMPLE, int REP>
+// TIERED: the chunk's far entries (p.fslot list, weights from global memory)
+// join the row dots through the per-wave LDS row sums fdot, and every row's
+// residual goes to d.rbuf for the far backward (k_far_grad).
+template <bool STATS, bool SAMPLE, int REP, bool TIERED>
 __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, const SgdParams& sp,
                                          const float* wl, unsigned long long* gl, const uint32_t* whl,
                                          float (*hsum)[kHot], double (*wsc)[kPartVals], double* prow,
-                                         uint32_t* wctr, uint64_t* tst = nullptr) {
-  const int64_t ns = d.ns;
+                                         uint32_t* wctr, float (*fdot)[kRowsPerChunk], uint64_t* tst = nullptr) {
+  const int64_t ns = d.nl;
   const int lane = lane_id();
   const int w = __builtin_amdgcn_readfirstlane(int(threadIdx.x) / kWave);   // wave-uniform
   const int r = lane / kLanesPerRow, t = lane % kLanesPerRow;
@@ -559,25 +527,42 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
   };
   int k = 0;   // chunks this wave took
   int64_t j = grab();
-  int32_t L8n = 0;
+  int32_t L8n = 0, fcn = 0;
   int64_t cbn = 0;
   if (j < nj) {
     L8n = clen8c[b + j * G];
     cbn = cbase[b + j * G];
+    if (TIERED) fcn = p.fcount[b + j * G];
   }
   while (j < nj) {
     const int64_t c = b + j * G;
-    const int32_t L8c = L8n;
+    const int32_t L8c = L8n, fc = fcn;
     const int64_t cb = cbn;
     ++k;
     j = grab();
     if (j < nj) {
       L8n = clen8c[b + j * G];
       cbn = cbase[b + j * G];
+      if (TIERED) fcn = p.fcount[b + j * G];
     }
     const int64_t pos = c * kRowsPerChunk + r;
     const int64_t off = cb * kChunkStride + lane * kGroup;
     const RowIn ri = row_in(p, pos);
+    // far entries of the chunk: their row sums land in lane t == 0 of the row
+    float far = 0.f;
+    if (TIERED && fc > 0) {   // wave-uniform
+      float* fd = fdot[w];
+      if (lane < kRowsPerChunk) fd[lane] = 0.f;
+      wave_lds_sync();
+      const uint32_t* fl = p.fslot + cb * kChunkStride;
+      for (int32_t k0 = 0; k0 < fc; k0 += kWave)
+        if (k0 + lane < fc) {
+          const uint32_t e = fl[k0 + lane];
+          atomicAdd(&fd[e >> 28], d.wc32[e & 0x0FFFFFFFu]);
+        }
+      wave_lds_sync();
+      if (t == 0) far = fd[r];
+    }
     if (L8c >= 0) {
       const uint4 hv = hdense[c * kWave + lane];
       // cold stream: L8c groups of kColdGroup slots per lane (hot_split.hip)
@@ -600,7 +585,7 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
         continue;
       }
       // ablate 4: no hot dot (counts still loaded)
-      float d0 = abl == 4 ? __uint_as_float(hv.x & 1u) : hot_dot(hv, wq), d1 = 0.f;
+      float d0 = abl == 4 ? __uint_as_float(hv.x & 1u) : hot_dot(hv, wq), d1 = far;
       if (reg) {
 #pragma unroll
         for (int g = 0; g < kMaxColdGroups; ++g)
@@ -622,6 +607,7 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
       dot += __shfl_xor(dot, 1, kWave);
       dot += __shfl_xor(dot, 2, kWave);
       const float res = row_residual<STATS, SAMPLE>(dot, ri, pos, t, d, p, sp, n_kept, w0, w1, w2, w3, acc);
+      if (TIERED && t == 0) d.rbuf[pos] = res;
       if (res != 0.f) {
         // opaque copy: re-extract the counts instead of keeping 32 converted
         // floats live across the residual (register pressure)
@@ -651,7 +637,7 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
     } else {  // plain layout: every entry (hot ones too) through the LDS gradient
       const int32_t L8 = p.clen8[c];
       const uint16_t* sl = slot + off;
-      float dot = 0.f;
+      float dot = far;
       for (int32_t g = 0; g < L8; ++g) {
         uint32_t s[8];
         unpack8(*reinterpret_cast<const uint4*>(sl + int64_t(g) * kChunkStride), s);
@@ -661,6 +647,7 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
       dot += __shfl_xor(dot, 1, kWave);
       dot += __shfl_xor(dot, 2, kWave);
       const float res = row_residual<STATS, SAMPLE>(dot, ri, pos, t, d, p, sp, n_kept, w0, w1, w2, w3, acc);
+      if (TIERED && t == 0) d.rbuf[pos] = res;
       if (res != 0.f) {
         const unsigned long long q = to_fix(res, clamped, sp.fix_lim);
         for (int32_t g = 0; g < L8; ++g) {
@@ -683,16 +670,18 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
   // hot gradient: sum the 16 lanes of each quarter t (per wave), into LDS
   // per 16-lane row (DPP), the four row partials of each hot id go to LDS
   // and the slot loop adds the 4 x 16 of them
-  float* hrow = hsum[w * kHotRows + lane / 16];
+  float* hrow = hsum[w];
 #pragma unroll
   for (int i = 0; i < kHotPerLane; ++i) {
-    const float v = row_sum_mod4((i & 1) ? gh[i >> 1].y : gh[i >> 1].x);
-    if ((lane & 15) < kLanesPerRow) hrow[kHotPerLane * (lane & 3) + i] = v;
+    float v = row_sum_mod4((i & 1) ? gh[i >> 1].y : gh[i >> 1].x);
+    v += __shfl_xor(v, 16, kWave);   // the wave's four 16-lane rows
+    v += __shfl_xor(v, 32, kWave);
+    if (lane < kLanesPerRow) hrow[kHotPerLane * lane + i] = v;
   }
   if (tst) tst[4] = __builtin_amdgcn_s_memrealtime();
   part_scalars<STATS, SAMPLE>(d, acc, wsc, prow);   // includes the block barrier
   if (tst) tst[5] = __builtin_amdgcn_s_memrealtime();
-  const int64_t hi = kNumNumeric + d.n_unique;      // pads are never flushed
+  const int64_t hi = d.far_base;                    // pads (and far slots) are never flushed
   for (int64_t s = kNumNumeric + threadIdx.x; s < ns; s += kIterBlock) {
     double v = 0.0;
     if (s < hi) {
@@ -700,7 +689,7 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
       const uint32_t h = p.hot_of[s];
       if (h != 0xFFu) {
         double hv = 0.0;
-        for (int k = 0; k < kIterBlock / kWave * kHotRows; ++k) hv += double(hsum[k][h]);
+        for (int k = 0; k < kIterBlock / kWave; ++k) hv += double(hsum[k][h]);
         v += hv;
       }
     }
@@ -711,12 +700,6 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
 
 // Weights -> LDS (fp32 compact weights, hot weights in hot order) and a
 // zeroed fixed-point gradient; ends with a block barrier.
-// Loads of data other workgroups wrote during the persistent kernel:
-// device-scope (sc1) so they are not served from this CU's (non-coherent) L1.
-template <typename T>
-__device__ __forceinline__ T ld_coh(const T* ptr) {
-  return __hip_atomic_load(ptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // Slots >= hi (pads) get weight 0 whatever wsrc holds there.
 template <int REP>
@@ -724,18 +707,19 @@ __device__ __forceinline__ void hyb_lds_init(const DevPrepared& p, const float* 
                                              int64_t hi, float* wl, unsigned long long* gl, uint32_t* whl,
                                              uint32_t* wctr) {
   if (threadIdx.x == 0) *wctr = 0u;
-  for (int64_t s = threadIdx.x; s < ns; s += kIterBlock) wl[s] = s < hi ? ld_coh(wsrc + s) : 0.f;
+  for (int64_t s = threadIdx.x; s < ns; s += kIterBlock) wl[s] = s < hi ? wsrc[s] : 0.f;
   for (int64_t s = threadIdx.x; s < ns * REP; s += kIterBlock) gl[s] = 0ull;
   __syncthreads();
   if (threadIdx.x < kWave) hot_digits(p, wl, whl);
   __syncthreads();
 }
 
-template <bool STATS, bool SAMPLE, int REP>
+template <bool STATS, bool SAMPLE, int REP, bool TIERED>
 __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_hyb(DevSgd d, DevPrepared p, SgdParams sp) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   __shared__ double wsc[kIterBlock / kWave][kPartVals];
-  __shared__ float hsum[kIterBlock / kWave * kHotRows][kHot];
+  __shared__ float hsum[kIterBlock / kWave][kHot];
+  __shared__ float fdot[TIERED ? kIterBlock / kWave : 1][kRowsPerChunk];
   __shared__ __attribute__((aligned(16))) uint32_t whl[kLanesPerRow * kHotLdsStride];
   __shared__ int stop_flag;
   __shared__ uint32_t wctr;
@@ -746,215 +730,12 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_hyb(DevSgd d, DevPrepar
   if (sgd_stop(d, sp, &stop_flag)) return;
   if (tst) tst[1] = __builtin_amdgcn_s_memrealtime();
   float* wl = lds;
-  unsigned long long* gl = reinterpret_cast<unsigned long long*>(lds + d.ns);
-  hyb_lds_init<REP>(p, d.wc32, d.ns, kNumNumeric + d.n_unique, wl, gl, whl, &wctr);
+  unsigned long long* gl = reinterpret_cast<unsigned long long*>(lds + d.nl);
+  hyb_lds_init<REP>(p, d.wc32, d.nl, d.far_base, wl, gl, whl, &wctr);
   if (tst) tst[2] = __builtin_amdgcn_s_memrealtime();
-  hyb_pass<STATS, SAMPLE, REP>(d, p, sp, wl, gl, whl, hsum, wsc, d.part + int64_t(blockIdx.x) * d.pstride, &wctr, tst);
+  hyb_pass<STATS, SAMPLE, REP, TIERED>(d, p, sp, wl, gl, whl, hsum, wsc, d.part + int64_t(blockIdx.x) * d.pstride,
+                                       &wctr, fdot, tst);
   if (tst) tst[6] = __builtin_amdgcn_s_memrealtime();
-}
-
-// ---------------------------------------------------------------------------
-// Persistent GD loop (single GPU, hybrid layout, iterations 2..N).
-//
-// One workgroup per CU for the whole loop, so the ~25 us of per-iteration
-// launch / prologue / epilogue / update-kernel overhead of the multi-kernel
-// path disappears.  Per iteration:
-//   pass      gradient over the workgroup's chunks -> partial row (UC memory)
-//   barrier A
-//   update    workgroup b owns ~ns/G columns: fixed-order sum of the G
-//             partial rows, SimpleUpdater, fp32 copy -> UC memory, norms
-//   barrier B
-//   converged?  every workgroup sums the G norm partials in the same order
-//             (identical verdicts), MLlib test as k_sgd_update/sgd_stop.
-// Cross-workgroup data lives in uncached (hipDeviceMallocUncached) memory,
-// so the barriers need no L2 write-back / invalidate (a device-scope fence
-// on MI355X writes back the XCD's whole L2 -- measured, see profiles/).
-// The grid barrier is hierarchical: one arrival counter per XCD group
-// (blockIdx % 8), the last arriver of a group bumps the global counter, the
-// last group publishes the generation.  Spins are bounded: a stuck barrier
-// raises bar->err and every workgroup leaves the loop.
-// ---------------------------------------------------------------------------
-__device__ bool grid_sync(GridBar* gb, uint32_t target, int* flag) {
-  __builtin_amdgcn_s_waitcnt(0);   // this thread's UC stores have completed
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t G = gridDim.x, x = blockIdx.x & 7u;
-    const uint32_t nx = (G - x + 7u) / 8u;
-    const uint32_t ng = G < 8u ? G : 8u;
-    if (atomicAdd(&gb->cnt[x * 16], 1u) + 1u == target * nx)
-      if (atomicAdd(&gb->gcnt, 1u) + 1u == target * ng)
-        __hip_atomic_store(&gb->gen, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int ok = 1;
-    uint32_t spins = 0;
-    while (__hip_atomic_load(&gb->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      if (__hip_atomic_load(&gb->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) { ok = 0; break; }
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 25)) {
-        __hip_atomic_store(&gb->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = 0;
-        break;
-      }
-    }
-    *flag = ok;
-  }
-  __syncthreads();
-  return *flag != 0;
-}
-
-template <int REP>
-__global__ __launch_bounds__(kIterBlock) void k_sgd_gd_hyb(DevSgd d, DevPrepared p, SgdParams sp,
-                                                           DevCoh coh, int it_first) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  __shared__ double wsc[kIterBlock / kWave][kPartVals];
-  __shared__ float hsum[kIterBlock / kWave * kHotRows][kHot];
-  __shared__ __attribute__((aligned(16))) uint32_t whl[kLanesPerRow * kHotLdsStride];
-  __shared__ double red[kIterBlock / kWave][2];
-  __shared__ int flag, conv_sh;
-  __shared__ uint32_t wctr;
-  const int64_t ns = d.ns, hi = kNumNumeric + d.n_unique;
-  float* wl = lds;
-  unsigned long long* gl = reinterpret_cast<unsigned long long*>(lds + ns);
-  const int G = int(gridDim.x), b = int(blockIdx.x);
-  const int lane = lane_id(), w = int(threadIdx.x) / kWave;
-  const double m = d.state[5];
-  double rest = d.state[4] - d.state[6];
-  if (rest < 0.0) rest = 0.0;
-  // update columns of this workgroup: index k in [0, hi] -> column k (< hi) or the loss (ns)
-  const int64_t nk = hi + 1, cpw = (nk + G - 1) / G;
-  const int64_t k0 = int64_t(b) * cpw, k1 = k0 + cpw < nk ? k0 + cpw : nk;
-  double* prow = coh.part + int64_t(b) * d.pstride;
-  uint32_t gen = 0;
-  int it = it_first;
-  uint64_t* tst = nullptr;
-  auto stamp = [&](int k) {
-    if (tst && b == 0 && threadIdx.x == 0) tst[k] = __builtin_amdgcn_s_memrealtime();
-  };
-  for (;; ++it) {
-    sp.iteration = it;
-    tst = coh.tdbg ? coh.tdbg + int64_t(it) * 8 : nullptr;
-    stamp(0);
-    hyb_lds_init<REP>(p, it == it_first ? d.wc32 : coh.w32, ns, hi, wl, gl, whl, &wctr);
-    stamp(1);
-    hyb_pass<false, false, REP>(d, p, sp, wl, gl, whl, hsum, wsc, prow, &wctr);
-    stamp(2);
-    if (!grid_sync(coh.bar, ++gen, &flag)) break;
-    stamp(3);
-    // ---- update of this workgroup's columns (one wave per column)
-    const double alpha = sp.step_size / sqrt(double(it));
-    double ds = 0.0, ws = 0.0;
-    for (int64_t k = k0 + w; k < k1; k += kIterBlock / kWave) {
-      const int64_t col = k < hi ? k : ns;
-      // the G partials of this column, all loads in flight at once
-      double a[kMaxPersistGrid / kWave];
-#pragma unroll
-      for (int q = 0; q < kMaxPersistGrid / kWave; ++q) {
-        const int j = lane + q * kWave;
-        a[q] = j < G ? ld_coh(coh.part + int64_t(j) * d.pstride + col) : 0.0;
-      }
-      double g = 0.0;
-#pragma unroll
-      for (int q = 0; q < kMaxPersistGrid / kWave; ++q) g += a[q];
-      g = wave_sum(g);
-      if (lane == 0) {
-        if (col < hi) {
-          const double step = alpha * (g / m);
-          const double wn = d.wc64[col] - step;
-          d.wc64[col] = wn;
-          coh.w32[col] = float(wn);
-          ds += step * step;
-          ws += wn * wn;
-        } else {
-          d.loss_hist[it] = g / m;
-        }
-      }
-    }
-    if (lane == 0) {
-      red[w][0] = ds;
-      red[w][1] = ws;
-    }
-    __syncthreads();
-    double* nrm = coh.norms + int64_t(it & 1) * 2 * G;
-    if (threadIdx.x < 2) {
-      double t = 0.0;
-      for (int k = 0; k < kIterBlock / kWave; ++k) t += red[k][threadIdx.x];
-      nrm[2 * b + threadIdx.x] = t;
-    }
-    stamp(4);
-    if (!grid_sync(coh.bar, ++gen, &flag)) break;
-    stamp(5);
-    // ---- convergence (every workgroup, same fixed-order sums)
-    if (threadIdx.x < kWave) {
-      double dsum = 0.0, wsum = 0.0;
-      for (int j = lane; j < G; j += kWave) {
-        dsum += ld_coh(nrm + 2 * j);
-        wsum += ld_coh(nrm + 2 * j + 1);
-      }
-      dsum = wave_sum(dsum);
-      wsum = wave_sum(wsum);
-      const double wnorm = sqrt(wsum + rest);
-      const bool conv = sqrt(dsum) < sp.tol * (wnorm > 1.0 ? wnorm : 1.0);   // it >= 2: second update on
-      if (threadIdx.x == 0) conv_sh = conv ? 1 : 0;
-    }
-    __syncthreads();
-    stamp(6);
-    const bool conv = conv_sh != 0;
-    if (conv || it >= sp.num_iterations) {
-      if (b == 0 && threadIdx.x == 0) {
-        d.state[0] = 1.0;
-        if (conv) d.state[1] = 1.0;
-        d.state[2] = double(it);
-        d.state[3] = double(it);
-      }
-      break;
-    }
-  }
-  if (b == 0 && threadIdx.x == 0 &&
-      __hip_atomic_load(&coh.bar->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)
-    d.state[7] = 2.0;   // barrier timeout: reported by the host
-}
-
-// Generic path: any slot width, weights read from global (L2), gradient by
-// global fp64 atomics.  Used when the active set exceeds LDS.
-template <typename SlotT, bool STATS, bool SAMPLE>
-__global__ __launch_bounds__(kBlock) void k_sgd_iter_global(DevSgd d, DevPrepared p, SgdParams sp) {
-  __shared__ double scratch[kBlock / kWave];
-  __shared__ int stop_flag;
-  if (sgd_stop(d, sp, &stop_flag)) return;
-  const float* w = d.wc32;
-  const int lane = lane_id();
-  const int r = lane / kLanesPerRow, t = lane % kLanesPerRow;
-  const int64_t n_kept = p.counters[0];
-  const int64_t nch = (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;
-  const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave;
-  const int64_t nwaves = int64_t(gridDim.x) * (kBlock / kWave);
-  const SlotT* slot = static_cast<const SlotT*>(p.slot);
-  const float w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3];
-  RowAcc acc;
-  for (int64_t c = wave; c < nch; c += nwaves) {
-    const int32_t L8 = p.clen8[c];
-    const SlotT* sl = slot + p.cbase[c] * kChunkStride + lane * kGroup;
-    const int64_t pos = c * kRowsPerChunk + r;
-    float dot = 0.f;
-    for (int32_t g = 0; g < L8; ++g) {
-      uint32_t s[8];
-      SlotLoad<SlotT>::load(sl + int64_t(g) * kChunkStride, s);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) dot += w[s[k]];
-    }
-    dot += __shfl_xor(dot, 1, kWave);
-    dot += __shfl_xor(dot, 2, kWave);
-    const float res = row_residual<STATS, SAMPLE>(dot, pos, t, d, p, sp, n_kept, w0, w1, w2, w3, acc);
-    if (res != 0.f) {
-      for (int32_t g = 0; g < L8; ++g) {
-        uint32_t s[8];
-        SlotLoad<SlotT>::load(sl + int64_t(g) * kChunkStride, s);
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if (s[k] >= kNumNumeric && s[k] < kNumNumeric + d.n_unique) atomicAdd(&d.g64[s[k]], double(res));
-      }
-    }
-  }
-  flush_scalars<STATS, SAMPLE>(d, acc, scratch, sp.iteration);
 }
 
 // LDS bytes of the fast path for a given replication factor.
@@ -988,7 +769,11 @@ int sgd_lds_rep(int64_t ns) {
 
 bool sgd_hybrid_fits(int64_t ns) {
   const int rep = sgd_lds_rep(ns);
-  const int64_t statics = int64_t(kIterBlock / kWave) * (kHot * int64_t(sizeof(float)) + int64_t(sizeof(double)));
+  // static LDS of k_sgd_iter_hyb<.., TIERED>: wsc, hsum, fdot per wave + whl, flags
+  const int64_t statics = int64_t(kIterBlock / kWave) *
+                              (kPartVals * int64_t(sizeof(double)) + kHot * int64_t(sizeof(float)) +
+                               kRowsPerChunk * int64_t(sizeof(float))) +
+                          kLanesPerRow * kHotLdsStride * int64_t(sizeof(uint32_t)) + 64;
   return ns <= kMaxHybridSlots && rep > 0 && lds_bytes(ns, rep) + statics <= 160 * 1024 - 1024;
 }
 
@@ -996,18 +781,19 @@ template <bool STATS, bool SAMPLE>
 static void launch_iter_t(const DevSgd& d, const DevPrepared& p, const SgdParams& sp, bool u16,
                           int rep, int grid, hipStream_t s) {
   if (u16 && rep > 0 && p.hybrid) {
-    const size_t lds = size_t(lds_bytes(d.ns, rep));
-#define TWTML_HYB(R) \
-  hipLaunchKernelGGL((k_sgd_iter_hyb<STATS, SAMPLE, R>), dim3(grid), dim3(kIterBlock), lds, s, d, p, sp)
+    const size_t lds = size_t(lds_bytes(d.nl, rep));
+#define TWTML_HYB(R, T) \
+  hipLaunchKernelGGL((k_sgd_iter_hyb<STATS, SAMPLE, R, T>), dim3(grid), dim3(kIterBlock), lds, s, d, p, sp)
+    const bool tiered = p.tiered != 0;
     switch (rep) {
-      case 8: TWTML_HYB(8); break;
-      case 4: TWTML_HYB(4); break;
-      case 2: TWTML_HYB(2); break;
-      default: TWTML_HYB(1); break;
+      case 8: if (tiered) TWTML_HYB(8, true); else TWTML_HYB(8, false); break;
+      case 4: if (tiered) TWTML_HYB(4, true); else TWTML_HYB(4, false); break;
+      case 2: if (tiered) TWTML_HYB(2, true); else TWTML_HYB(2, false); break;
+      default: if (tiered) TWTML_HYB(1, true); else TWTML_HYB(1, false); break;
     }
 #undef TWTML_HYB
   } else if (u16 && rep > 0) {
-    const size_t lds = size_t(lds_bytes(d.ns, rep));
+    const size_t lds = size_t(lds_bytes(d.nl, rep));
 #define TWTML_ITER(R, C) \
   hipLaunchKernelGGL((k_sgd_iter_lds<STATS, SAMPLE, R, C>), dim3(grid), dim3(kIterBlock), lds, s, d, p, sp)
     const bool cnt = p.dedup != 0;
@@ -1018,10 +804,8 @@ static void launch_iter_t(const DevSgd& d, const DevPrepared& p, const SgdParams
       default: if (cnt) TWTML_ITER(1, true); else TWTML_ITER(1, false); break;
     }
 #undef TWTML_ITER
-  } else if (u16) {
-    hipLaunchKernelGGL((k_sgd_iter_global<uint16_t, STATS, SAMPLE>), dim3(grid * 2), dim3(kBlock), 0, s, d, p, sp);
   } else {
-    hipLaunchKernelGGL((k_sgd_iter_global<uint32_t, STATS, SAMPLE>), dim3(grid * 2), dim3(kBlock), 0, s, d, p, sp);
+    throw std::logic_error("launch_sgd_iter: active set exceeds LDS (the tiered path handles it)");
   }
 }
 
@@ -1036,10 +820,10 @@ static int iter_blocks_per_cu(int64_t ns, int rep, bool hybrid) {
   hipError_t e = hipSuccess;
 #define TWTML_OCC(K) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, K, kIterBlock, lds)
   switch (rep) {
-    case 8: if (hybrid) TWTML_OCC((k_sgd_iter_hyb<false, false, 8>)); else TWTML_OCC((k_sgd_iter_lds<false, false, 8, false>)); break;
-    case 4: if (hybrid) TWTML_OCC((k_sgd_iter_hyb<false, false, 4>)); else TWTML_OCC((k_sgd_iter_lds<false, false, 4, false>)); break;
-    case 2: if (hybrid) TWTML_OCC((k_sgd_iter_hyb<false, false, 2>)); else TWTML_OCC((k_sgd_iter_lds<false, false, 2, false>)); break;
-    default: if (hybrid) TWTML_OCC((k_sgd_iter_hyb<false, false, 1>)); else TWTML_OCC((k_sgd_iter_lds<false, false, 1, false>)); break;
+    case 8: if (hybrid) TWTML_OCC((k_sgd_iter_hyb<false, false, 8, true>)); else TWTML_OCC((k_sgd_iter_lds<false, false, 8, false>)); break;
+    case 4: if (hybrid) TWTML_OCC((k_sgd_iter_hyb<false, false, 4, true>)); else TWTML_OCC((k_sgd_iter_lds<false, false, 4, false>)); break;
+    case 2: if (hybrid) TWTML_OCC((k_sgd_iter_hyb<false, false, 2, true>)); else TWTML_OCC((k_sgd_iter_lds<false, false, 2, false>)); break;
+    default: if (hybrid) TWTML_OCC((k_sgd_iter_hyb<false, false, 1, true>)); else TWTML_OCC((k_sgd_iter_lds<false, false, 1, false>)); break;
   }
 #undef TWTML_OCC
   if (e != hipSuccess || n < 1) {
@@ -1061,7 +845,7 @@ int sgd_iter_grid(int64_t ns, int64_t n_kept, int num_cu, bool hybrid) {
 
 void launch_sgd_iter(const DevSgd& d, const DevPrepared& p, const SgdParams& sp, int64_t /*groups*/,
                      bool u16, int grid, hipStream_t s) {
-  const int rep = u16 ? sgd_lds_rep(d.ns) : 0;
+  const int rep = u16 ? sgd_lds_rep(d.nl) : 0;
   const bool stats = sp.iteration == 1;
   const bool sample = sp.sample != 0;
   if (stats && sample) launch_iter_t<true, true>(d, p, sp, u16, rep, grid, s);
@@ -1072,45 +856,6 @@ void launch_sgd_iter(const DevSgd& d, const DevPrepared& p, const SgdParams& sp,
 
 int sgd_partials(int64_t ns, bool u16, int grid) {
   return (u16 && sgd_lds_rep(ns) > 0) ? grid : 0;
-}
-
-// Persistent loop: the grid it needs (0 = not applicable: generic / plain
-// layout, sampling, or a workgroup per CU does not fit).
-int sgd_persistent_grid(const DevSgd& d, const DevPrepared& p, bool u16, bool sample, int num_cu) {
-  if (!u16 || sample || !p.hybrid) return 0;
-  const int rep = sgd_lds_rep(d.ns);
-  if (rep <= 0) return 0;
-  const size_t lds = size_t(lds_bytes(d.ns, rep));
-  int per_cu = 0;
-  hipError_t e = hipSuccess;
-  switch (rep) {
-    case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sgd_gd_hyb<8>, kIterBlock, lds); break;
-    case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sgd_gd_hyb<4>, kIterBlock, lds); break;
-    case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sgd_gd_hyb<2>, kIterBlock, lds); break;
-    default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sgd_gd_hyb<1>, kIterBlock, lds); break;
-  }
-  if (e != hipSuccess || per_cu < 1 || num_cu > kMaxPersistGrid) return 0;
-  return num_cu;   // one workgroup per CU (co-resident by construction, cooperative launch checks)
-}
-
-void launch_sgd_persistent(const DevSgd& d, const DevPrepared& p, const SgdParams& sp, const DevCoh& coh,
-                           int it_first, int grid, hipStream_t s) {
-  const int rep = sgd_lds_rep(d.ns);
-  const unsigned lds = unsigned(lds_bytes(d.ns, rep));
-  SgdParams spc = sp;
-  DevSgd dc = d;
-  DevPrepared pc = p;
-  DevCoh cc = coh;
-  int itf = it_first;
-  void* args[] = {&dc, &pc, &spc, &cc, &itf};
-  const void* fn = nullptr;
-  switch (rep) {
-    case 8: fn = reinterpret_cast<const void*>(k_sgd_gd_hyb<8>); break;
-    case 4: fn = reinterpret_cast<const void*>(k_sgd_gd_hyb<4>); break;
-    case 2: fn = reinterpret_cast<const void*>(k_sgd_gd_hyb<2>); break;
-    default: fn = reinterpret_cast<const void*>(k_sgd_gd_hyb<1>); break;
-  }
-  TWTML_HIP_CHECK(hipLaunchCooperativeKernel(fn, dim3(grid), dim3(kIterBlock), args, lds, s));
 }
 
 // ---------------------------------------------------------------------------
@@ -1142,22 +887,23 @@ void launch_sgd_persistent(const DevSgd& d, const DevPrepared& p, const SgdParam
 // GPU); nparts == 0: g64 holds them (all-reduced, or the generic path).
 // ---------------------------------------------------------------------------
 constexpr int kUpdCols = 1024 / kWave;   // columns (waves) per workgroup
+constexpr int kPartLoads = 512;          // partial rows a lane loads at once
 
 __device__ __forceinline__ double part_col_wave(const DevSgd& d, int64_t col, int nparts) {
   const int lane = lane_id();
   const double* src = d.part + col;
   const int64_t ps = d.pstride;
-  double a[kMaxPersistGrid / kWave];
+  double a[kPartLoads / kWave];
 #pragma unroll
-  for (int q = 0; q < kMaxPersistGrid / kWave; ++q) {
+  for (int q = 0; q < kPartLoads / kWave; ++q) {
     const int g = lane + q * kWave;
     a[q] = g < nparts ? src[int64_t(g) * ps] : 0.0;
   }
   double t = 0.0;
-  for (int g0 = kMaxPersistGrid; g0 < nparts; g0 += kWave)   // grids beyond 512 (not launched today)
+  for (int g0 = kPartLoads; g0 < nparts; g0 += kWave)   // grids beyond 512 (not launched today)
     if (g0 + lane < nparts) t += src[int64_t(g0 + lane) * ps];
 #pragma unroll
-  for (int q = 0; q < kMaxPersistGrid / kWave; ++q) t += a[q];
+  for (int q = 0; q < kPartLoads / kWave; ++q) t += a[q];
   return wave_sum(t);
 }
 
@@ -1167,7 +913,7 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
   if (d.state[0] != 0.0) return;
   const int tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
   const int it = sp.iteration;
-  const int64_t ns = d.ns, hi = kNumNumeric + d.n_unique;
+  const int64_t ns = d.nl, hi = d.far_base;   // partial-row columns; near text slots end at far_base
   const int64_t ncols = ns + kPartVals - kNumNumeric;
   // m: global kept rows, or the sampled row count of this iteration
   if (tid < kWave) {
@@ -1176,7 +922,7 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
       m = *sgd_red_m(d, it);
       if (nparts > 0) {
         double t = 0.0;
-        for (int g = tid; g < nparts; g += kWave) t += d.part[int64_t(g) * d.pstride + ns + 1];
+        for (int g = tid; g < nparts; g += kWave) t += d.part[int64_t(g) * d.pstride + ns + 1];   // ns = nl
         m += wave_sum(t);
       }
     }
@@ -1208,6 +954,30 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
       }
     }
   }
+  // tiered: far slots [far_base, 4 + n_unique), one thread per slot, from
+  // the fixed-point far gradient (k_far_grad / all-reduced), re-zeroed here
+  const int64_t n_far = kNumNumeric + d.n_unique - d.far_base;
+  if (n_far > 0) {
+    double fds = 0.0, fws = 0.0;
+    const double inv_m = m > 0.0 ? 1.0 / m : 0.0;
+    for (int64_t j = int64_t(blockIdx.x) * 1024 + tid; j < n_far; j += int64_t(gridDim.x) * 1024) {
+      const double g = double((long long)d.gfix[j]) * kFarInv;
+      d.gfix[j] = 0ull;
+      if (m > 0.0) {
+        const int64_t col = d.far_base + j;
+        const double step = alpha * (g * inv_m);
+        const double wn = d.wc64[col] - step;
+        d.wc64[col] = wn;
+        d.wc32[col] = float(wn);
+        fds += step * step;
+        fws += wn * wn;
+      }
+    }
+    fds = wave_sum(fds);
+    fws = wave_sum(fws);
+    ds += fds;   // lane 0 carries the wave's columns (fixed order)
+    ws += fws;
+  }
   if (lane == 0) {
     wsc[w][0] = ds;
     wsc[w][1] = ws;
@@ -1231,8 +1001,9 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
 }
 
 void launch_sgd_update(const DevSgd& d, const SgdParams& sp, int nparts, hipStream_t s) {
-  const int64_t tiles = (d.ns + kPartVals - kNumNumeric + kUpdCols - 1) / kUpdCols;
-  const int grid = int(std::min<int64_t>(tiles, kMaxUpdGrid));
+  const int64_t tiles = (d.nl + kPartVals - kNumNumeric + kUpdCols - 1) / kUpdCols;
+  const int64_t far_tiles = (kNumNumeric + d.n_unique - d.far_base + 1023) / 1024;
+  const int grid = int(std::min<int64_t>(std::max(tiles, far_tiles), kMaxUpdGrid));
   hipLaunchKernelGGL(k_sgd_update, dim3(grid), dim3(1024), 0, s, d, sp, nparts);
 }
 
@@ -1241,20 +1012,20 @@ void launch_sgd_update(const DevSgd& d, const SgdParams& sp, int nparts, hipStre
 // summation order.
 __global__ __launch_bounds__(1024) void k_sgd_reduce(DevSgd d, SgdParams sp) {
   if (d.state[0] != 0.0) return;
-  const int64_t ncols = d.ns + kPartVals - kNumNumeric;
+  const int64_t ncols = d.nl + kPartVals - kNumNumeric;
   const int64_t col = int64_t(blockIdx.x) * kUpdCols + threadIdx.x / kWave;
   if (col >= ncols) return;   // wave-uniform
   const double v = part_col_wave(d, col, d.nparts);
   if (lane_id() == 0) {
-    if (col <= d.ns) d.g64[col] = v;                     // slots, then the loss at [ns]
-    else if (col == d.ns + 1) *sgd_red_m(d, sp.iteration) = v;   // sampled row count
-    else d.stats[col - d.ns - 2] += v;                   // batch stats (iteration 1)
+    if (col <= d.nl) d.g64[col] = v;                     // slots, then the loss at [nl]
+    else if (col == d.nl + 1) *sgd_red_m(d, sp.iteration) = v;   // sampled row count
+    else d.stats[col - d.nl - 2] += v;                   // batch stats (iteration 1)
   }
 }
 
 void launch_sgd_reduce(const DevSgd& d, const SgdParams& sp, hipStream_t s) {
   if (d.nparts <= 0) return;
-  const int grid = int((d.ns + kPartVals - kNumNumeric + kUpdCols - 1) / kUpdCols);
+  const int grid = int((d.nl + kPartVals - kNumNumeric + kUpdCols - 1) / kUpdCols);
   hipLaunchKernelGGL(k_sgd_reduce, dim3(grid), dim3(1024), 0, s, d, sp);
 }
 
@@ -1271,6 +1042,54 @@ __global__ void k_sgd_finish(DevSgd d, SgdParams sp) {
 
 void launch_sgd_finish(const DevSgd& d, const SgdParams& sp, hipStream_t s) {
   hipLaunchKernelGGL(k_sgd_finish, dim3(1), dim3(kWave), 0, s, d, sp);
+}
+
+
+// ---------------------------------------------------------------------------
+// Far backward (tiered layout): the CSC lists every far entry grouped by
+// slot; lane e of the grid takes entry e, converts its row's residual to the
+// 2^-16 fixed point (kFarScale), and a segmented inclusive scan over
+// the wave (segments = runs of equal slot) leaves each run's sum in its last
+// lane, which adds it to gfix[slot - far_base] with one 64-bit integer
+// atomic.  Integer sums are exact, so the result does not depend on the
+// order of entries inside a slot or on which wave adds first: no per-entry
+// float atomics, deterministic across runs and DP ranks.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_far_grad(DevSgd d, SgdParams sp) {
+  if (d.state[0] != 0.0) return;
+  const int64_t n = *d.far_n;
+  const int lane = lane_id();
+  bool clamped = false;
+  const int64_t stride = int64_t(gridDim.x) * 256;
+  for (int64_t e0 = int64_t(blockIdx.x) * 256 + (threadIdx.x & ~(kWave - 1)); e0 < n; e0 += stride) {
+    const int64_t e = e0 + lane;
+    const bool valid = e < n;
+    uint32_t sl = valid ? d.fcsc_slot[e] : 0xFFFFFFFFu;
+    long long q = 0;
+    if (valid) {
+      float v = d.rbuf[d.fcsc_pos[e]] * kFarScale;
+      if (fabsf(v) > sp.far_lim) {
+        clamped = true;
+        v = v > 0.f ? sp.far_lim : -sp.far_lim;
+      }
+      q = __float2ll_rn(v);
+    }
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+      const long long qu = __shfl_up(q, off, kWave);
+      const uint32_t su = uint32_t(__shfl_up(int(sl), off, kWave));
+      if (lane >= off && su == sl) q += qu;
+    }
+    const uint32_t sn = uint32_t(__shfl_down(int(sl), 1, kWave));
+    const bool tail = valid && (lane == kWave - 1 || e + 1 >= n || sn != sl);
+    if (tail && q != 0)
+      atomicAdd(reinterpret_cast<unsigned long long*>(&d.gfix[sl - d.far_base]), (unsigned long long)q);
+  }
+  if (__any(clamped) && lane == 0) d.state[7] = 1.0;
+}
+
+void launch_far_grad(const DevSgd& d, const SgdParams& sp, int num_cu, hipStream_t s) {
+  hipLaunchKernelGGL(k_far_grad, dim3(std::max(1, num_cu * 4)), dim3(256), 0, s, d, sp);
 }
 
 // ---------------------------------------------------------------------------
@@ -1302,7 +1121,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_w(DevSgd d, const int32_t* un
        s += int64_t(gridDim.x) * kBlock) {
     double v = 0.0;
     if (s < kNumNumeric) v = d.w64[d.F + s];
-    else if (s < kNumNumeric + d.n_unique) v = d.w64[uniq[s - kNumNumeric]];
+    else if (s < kNumNumeric + d.n_unique) v = d.w64[d.slot_fid ? d.slot_fid[s] : uniq[s - kNumNumeric]];
     d.wc64[s] = v;
     d.wc32[s] = float(v);
     d.g64[s] = 0.0;
@@ -1328,7 +1147,7 @@ __global__ __launch_bounds__(kBlock) void k_scatter_w(DevSgd d, const int32_t* u
        s += int64_t(gridDim.x) * kBlock) {
     const double v = d.wc64[s];
     if (s < kNumNumeric) d.w64[d.F + s] = v;
-    else d.w64[uniq[s - kNumNumeric]] = v;
+    else d.w64[d.slot_fid ? d.slot_fid[s] : uniq[s - kNumNumeric]] = v;
     acc += v * v;
   }
   acc = block_sum(acc, scratch);
@@ -1380,7 +1199,7 @@ __global__ void k_batch_init(DevSgd d, double m_global, int n_loss) {
     d.stats[i] = 0.0;
   }
   if (i < 4) d.red64[i] = 0.0;
-  if (i == 0) d.g64[d.ns] = 0.0;
+  if (i == 0) d.g64[d.nl] = 0.0;
   for (int k = i; k < n_loss; k += blockDim.x) d.loss_hist[k] = 0.0;
 }
 

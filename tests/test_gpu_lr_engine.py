@@ -315,27 +315,6 @@ def test_hybrid_layout_matches_hashingtf(hip_module, F, hash, repeats, lazy):
     np.testing.assert_allclose(wh, wp, rtol=1e-4, atol=1e-6 * np.abs(wp).max())
 
 
-@pytest.mark.parametrize("F", [1000, 1 << 20])
-def test_persistent_loop_matches_per_iteration_kernels(hip_module, monkeypatch, F):
-    """Iterations 2..N in the persistent kernel (grid barriers over uncached
-    memory) equal the per-iteration kernel path: same iteration counts and
-    convergence, loss history and weights to fp32-summation-order level."""
-    cfg = SynthConfig.profile("bench", seed=21)
-    batches = [generate_batch(cfg, t * 6000, 6000, batch_time_ms=NOW + t) for t in range(3)]
-    out = {}
-    for mode in ("0", "1"):
-        monkeypatch.setenv("TWTML_PERSIST", mode)
-        eng = _engine(F, num_iterations=50)
-        res = [eng.train_batch(b) for b in batches]
-        out[mode] = (res, eng.get_weights())
-    for r0, r1 in zip(out["0"][0], out["1"][0]):
-        assert r0["iterations"] == r1["iterations"] > 2
-        assert r0["converged"] == r1["converged"]
-        np.testing.assert_allclose(r1["loss_history"], r0["loss_history"], rtol=1e-6)
-    w0, w1 = out["0"][1], out["1"][1]
-    np.testing.assert_allclose(w1, w0, rtol=1e-5, atol=1e-7 * np.abs(w0).max())
-
-
 def test_wide_murmur3_hybrid_matches_plain_remap(hip_module):
     """F = 1e8 murmur3: the hybrid remap (LDS id cache for wide ids,
     hot_split.hip:id_code) trains the same model as the plain k_remap path."""

@@ -215,3 +215,27 @@ def test_kmeans_dying_cluster_split_and_ties():
     assert s1.centers[0, 0] > s1.centers[1, 0]
     assert s1.centers[0, 0] - s1.centers[1, 0] == pytest.approx(2e-14 * 1.0, rel=1e-3)
     assert list(find_closest(np.array([[0.0], [0.0]]), np.array([[1.0]]))) == [0]
+
+
+def test_active_column_oracle_equals_full_width():
+    """run_minibatch_sgd_active (touched columns + constant rest norm) takes
+    the same iterates as the full-width MLlib loop, warm-started from a
+    model with weight outside the batch's columns; and the native featurizer
+    equals the Python one."""
+    from twitter_stream_ml_amd.oracle import (featurize_batch, featurize_batch_native,
+                                              run_minibatch_sgd, run_minibatch_sgd_active)
+    from twitter_stream_ml_amd.sources.synthetic import SynthConfig, generate_batch
+    cfg = SynthConfig.profile("wide", seed=4, special_fraction=0.02)
+    F = 1 << 16
+    raw = generate_batch(cfg, 0, 1500, batch_time_ms=1_700_000_000_000)
+    fb = featurize_batch(raw, F, 100, 1000, hash="murmur3")
+    fn = featurize_batch_native(raw, F, 100, 1000, hash="murmur3")
+    assert abs(fb.X - fn.X).max() == 0 and np.array_equal(fb.y, fn.y)
+    rng = np.random.default_rng(1)
+    w0 = rng.standard_normal(F + 4) * 1e-3   # mass outside the touched columns too
+    for tol in (1e-3, 1e-4):
+        a = run_minibatch_sgd(fb.X, fb.y, w0, 0.005, 50, convergence_tol=tol)
+        b = run_minibatch_sgd_active(fb.X, fb.y, w0, 0.005, 50, convergence_tol=tol)
+        assert a.iterations == b.iterations and a.converged == b.converged
+        np.testing.assert_allclose(b.weights, a.weights, rtol=1e-10, atol=1e-13)
+        np.testing.assert_allclose(b.loss_history, a.loss_history, rtol=1e-10)

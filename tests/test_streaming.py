@@ -84,3 +84,24 @@ def test_dstream_transformations_are_lazy_per_batch():
     retweets.map(lambda s: s.getRetweetCount()).foreachRDD(lambda rdd: counted.append(rdd.count()))
     ssc.run_batches(2)
     assert counted == [int(raw.is_retweet.sum())] * 2
+
+
+def test_time_sealed_batches_respect_engine_capacity():
+    """A time-sealed batch never exceeds the engine's staging capacity: the
+    receiver seals early at max_batch_rows / max_batch_units (ADVICE r1:
+    a 5 s batch with more rows than the buffers used to kill the job)."""
+    import time as _t
+    from twitter_stream_ml_amd.runtime.streaming import StreamingContext
+    from twitter_stream_ml_amd.sources.synthetic import SynthConfig, SyntheticTweetSource
+    ssc = StreamingContext(batch_seconds=30.0, num_batches=4, max_batch_rows=5000,
+                           max_batch_units=5000 * 120, poll_chunk=1500)
+    sizes = []
+    ssc.twitterStream(SyntheticTweetSource(SynthConfig(seed=2))).foreachRDD(
+        lambda rdd: sizes.append((rdd.raw.n, rdd.raw.total_units)))
+    ssc.start()
+    t0 = _t.time()
+    assert ssc.awaitTermination(60)
+    ssc.stop()
+    assert len(sizes) == 4 and _t.time() - t0 < 30   # sealed by capacity, not the 30 s timer
+    assert all(0 < n <= 5000 and u <= 5000 * 120 for n, u in sizes), sizes
+    assert ssc.capacity_seals >= 4

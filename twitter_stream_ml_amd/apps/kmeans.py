@@ -170,8 +170,11 @@ def main(argv: Optional[List[str]] = None) -> int:
         if remaining == 0:
             return 0
     log.info("Initializing Streaming Spark Context...")
+    cap = getattr(engine, "cfg", None)   # device engine: staging capacity per batch
     ssc = StreamingContext(args.seconds, batch_size=args.batchSize, num_batches=remaining,
-                           app_name=APP_NAME)
+                           app_name=APP_NAME,
+                           max_batch_rows=int(cap.max_rows) if cap is not None else 0,
+                           max_batch_units=int(cap.max_units) if cap is not None else 0)
     log.info("Initializing Twitter stream...")
     stream = ssc.twitterStream(make_source(args.source, rate=args.sourceRate, seed=args.seed,
                                            shard=info.rank, num_shards=info.world,

@@ -96,6 +96,7 @@ class LinearRegressionJob:
         self.records = resume.records  # source records this rank consumed
         self.metrics = metrics or MetricsLogger(None)
         self.last = None
+        self.overflows = 0   # batches whose gradient hit the fixed-point clamp
         self.checkpointer = StreamCheckpointer(
             conf.checkpoint, conf.checkpointInterval, rank,
             lambda path, prog: LinearRegressionModel(self.engine.get_weights(), 0.0).save(path, prog),
@@ -109,6 +110,12 @@ class LinearRegressionJob:
             self.watchdog.arm()
         res = self.engine.train_batch(raw, want_pred=True)     # op #1 then op #2
         self.last = res
+        if res.get("overflow"):
+            # a residual hit the fixed-point gradient clamp (sgd.hip sgd_fix_limit):
+            # the update no longer follows MLlib exactly -- the model is diverging
+            log.error("batch %d: gradient fixed-point clamp hit (|residual| too large); "
+                      "the model is diverging (stepSize %s too large?)", self.batches + 1, self.conf.stepSize)
+            self.overflows += 1
         self.batches += 1
         self.records += raw.n
         try:
@@ -135,6 +142,8 @@ class LinearRegressionJob:
             mse = round_half_up(se2 / n)
         except ValueError as e:  # Utils.round on NaN/Inf: the model diverged
             log.error("batch %d: model diverged (%s); skipping report", self.batches, e)
+            self.metrics.log(batch_time_ms=time_ms, raw=raw.n, batch=batch, diverged=True,
+                             overflow=bool(res.get("overflow", False)))
             return
         mask = self._kept_mask(raw)
         real = raw.scalars[RETWEET_COUNT][mask].astype(np.float64)
@@ -151,6 +160,7 @@ class LinearRegressionJob:
         self.metrics.log(batch_time_ms=time_ms, raw=raw.n, batch=batch, count=self.count,
                          mse=mse, realStdev=real_sd, predStdev=pred_sd,
                          iterations=res["iterations"], converged=bool(res["converged"]),
+                         overflow=bool(res.get("overflow", False)),
                          prep_ms=res.get("prep_ms", 0.0), train_ms=res.get("train_ms", 0.0))
         if self.session is not None and self.rank == 0:
             self.session.update(self.count, batch, mse, real_sd, pred_sd, real_all, pred_all)
@@ -201,8 +211,11 @@ def main(argv: Optional[List[str]] = None) -> int:
             return 0
 
     log.info("Initializing Streaming Spark Context... %s sec/batch", conf.seconds)
+    cap = getattr(engine, "cfg", None)   # device engines: staging capacity per batch
     ssc = StreamingContext(conf.seconds, batch_size=conf.batchSize, num_batches=remaining,
-                           app_name=conf.appName())
+                           app_name=conf.appName(),
+                           max_batch_rows=int(cap.max_rows) if cap is not None else 0,
+                           max_batch_units=int(cap.max_units) if cap is not None else 0)
     log.info("Initializing Twitter stream...")
     stream = ssc.twitterStream(make_source(conf.source, rate=conf.sourceRate, seed=conf.seed,
                                            shard=rank, num_shards=world,

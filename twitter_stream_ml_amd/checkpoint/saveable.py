@@ -13,11 +13,22 @@ can ``LinearRegressionModel.load(sc, path)`` it [upstream
   k-means (+ ``_SUCCESS``).  ``VectorUDT`` is
   ``struct<type: tinyint, size: int, indices: array<int>, values:
   array<double>>`` with ``type = 1`` (dense; size/indices null) or ``0``
-  (sparse).
+  (sparse: a vector with under 25 % non-zeros -- the usual case for hashed
+  text weights at F = 1e8, where only the touched bigrams ever move).  The
+  footer carries Spark's ``org.apache.spark.sql.parquet.row.metadata``
+  schema JSON with the VectorUDT class, which is what Spark's parquet reader
+  uses to turn the struct back into a ``Vector``.  Loading in real Spark is
+  parity-unpinned (no Spark here); the layout follows upstream
+  ``GLMRegressionModel.SaveLoadV1_0`` / ``VectorUDT.sqlType``.
+
+Vectors are built and read column-wise (numpy <-> arrow buffers), never as
+Python lists: a 1e8-weight model saves and loads in seconds.
 
 Streaming k-means also needs the cluster weights, which ``KMeansModel`` does
 not store; they go to ``<path>/streaming/weights.json`` (extension, ignored
-by Spark).  Writes are atomic (temporary directory + rename).
+by Spark).  Writes replace the directory via rename: a crash between the
+two renames leaves ``<path>.old`` as the last good model, which
+``resolve_resume`` falls back to.
 """
 from __future__ import annotations
 
@@ -47,15 +58,78 @@ def vector_udt_type() -> pa.DataType:
     ])
 
 
-def _dense(v: np.ndarray) -> dict:
-    return {"type": 1, "size": None, "indices": None, "values": np.asarray(v, np.float64).tolist()}
+SPARSE_DENSITY = 0.25   # sparse VectorUDT (type 0) below this fraction of non-zeros
+
+_UDT_JSON = {
+    "type": "udt", "class": "org.apache.spark.mllib.linalg.VectorUDT",
+    "pyClass": "pyspark.mllib.linalg.VectorUDT",
+    "sqlType": {"type": "struct", "fields": [
+        {"name": "type", "type": "byte", "nullable": False, "metadata": {}},
+        {"name": "size", "type": "integer", "nullable": True, "metadata": {}},
+        {"name": "indices", "type": {"type": "array", "elementType": "integer", "containsNull": False},
+         "nullable": True, "metadata": {}},
+        {"name": "values", "type": {"type": "array", "elementType": "double", "containsNull": False},
+         "nullable": True, "metadata": {}}]},
+}
 
 
-def _from_udt(d: dict) -> np.ndarray:
-    if d["type"] == 1:
-        return np.asarray(d["values"], dtype=np.float64)
-    out = np.zeros(int(d["size"]), np.float64)
-    out[np.asarray(d["indices"], np.int64)] = np.asarray(d["values"], np.float64)
+def _spark_row_metadata(fields) -> dict:
+    """Spark's parquet footer schema (``org.apache.spark.sql.parquet.row.metadata``)."""
+    js = {"type": "struct", "fields": [
+        {"name": n, "type": (_UDT_JSON if t == "vector" else t), "nullable": nl, "metadata": {}}
+        for n, t, nl in fields]}
+    return {b"org.apache.spark.sql.parquet.row.metadata": json.dumps(js, separators=(",", ":")).encode()}
+
+
+def _udt_array(vecs, sparse_density: float = SPARSE_DENSITY) -> pa.StructArray:
+    """VectorUDT column of ``vecs`` from numpy buffers (no Python floats)."""
+    types, sizes, size_null = [], [], []
+    iv, io, inull = [], [0], []
+    vv, vo = [], [0]
+    for v in vecs:
+        v = np.asarray(v, dtype=np.float64)
+        nz = np.flatnonzero(v)
+        sparse = v.shape[0] > 0 and nz.shape[0] < sparse_density * v.shape[0]
+        types.append(0 if sparse else 1)
+        sizes.append(v.shape[0] if sparse else 0)
+        size_null.append(not sparse)
+        if sparse:
+            iv.append(nz.astype(np.int32))
+            vv.append(v[nz])
+        else:
+            vv.append(v)
+        inull.append(not sparse)
+        io.append(io[-1] + (nz.shape[0] if sparse else 0))
+        vo.append(vo[-1] + vv[-1].shape[0])
+    i32 = pa.list_(pa.field("element", pa.int32(), nullable=False))
+    f64 = pa.list_(pa.field("element", pa.float64(), nullable=False))
+    ind = pa.ListArray.from_arrays(pa.array(np.asarray(io, np.int32)),
+                                   pa.array(np.concatenate(iv) if iv else np.zeros(0, np.int32)),
+                                   type=i32, mask=pa.array(np.asarray(inull, bool)))
+    if vo[-1] >= 2 ** 31:
+        raise ValueError("VectorUDT column: more than 2^31 values")
+    val = pa.ListArray.from_arrays(pa.array(np.asarray(vo, np.int32)),
+                                   pa.array(np.concatenate(vv) if vv else np.zeros(0)), type=f64)
+    siz = pa.array(np.asarray(sizes, np.int32), mask=np.asarray(size_null, bool))
+    return pa.StructArray.from_arrays([pa.array(np.asarray(types, np.int8)), siz, ind, val],
+                                      fields=list(vector_udt_type()))
+
+
+def _from_udt_column(col: pa.ChunkedArray) -> list:
+    """VectorUDT column -> list of numpy vectors (buffers, not Python lists)."""
+    out = []
+    for chunk in col.chunks:
+        types = chunk.field("type").to_numpy(zero_copy_only=False)
+        sizes = chunk.field("size")
+        inds, vals = chunk.field("indices"), chunk.field("values")
+        for r in range(len(chunk)):
+            v = vals[r].values.to_numpy(zero_copy_only=False).astype(np.float64, copy=False)
+            if int(types[r]) == 1:
+                out.append(np.array(v, dtype=np.float64))
+            else:
+                dense = np.zeros(int(sizes[r].as_py()), np.float64)
+                dense[inds[r].values.to_numpy(zero_copy_only=False).astype(np.int64)] = v
+                out.append(dense)
     return out
 
 
@@ -114,28 +188,32 @@ def _read_data(path: str) -> pa.Table:
 def save_linear_regression(path: str, weights: np.ndarray, intercept: float = 0.0,
                            progress: Optional[dict] = None) -> None:
     w = np.asarray(weights, dtype=np.float64)
-    schema = pa.schema([pa.field("weights", vector_udt_type()), pa.field("intercept", pa.float64())])
-    table = pa.Table.from_pylist([{"weights": _dense(w), "intercept": float(intercept)}], schema)
+    schema = pa.schema([pa.field("weights", vector_udt_type()), pa.field("intercept", pa.float64(), nullable=False)],
+                       metadata=_spark_row_metadata([("weights", "vector", True), ("intercept", "double", False)]))
+    table = pa.Table.from_arrays([_udt_array([w]), pa.array([float(intercept)], pa.float64())], schema=schema)
     _write_dir(path, {"class": LR_CLASS, "version": "1.0", "numFeatures": int(w.shape[0])}, table,
                {"progress.json": progress} if progress else None)
 
 
 def load_linear_regression(path: str) -> Tuple[np.ndarray, float]:
     meta = _read_meta(path, LR_CLASS)
-    rows = _read_data(path).to_pylist()
-    if len(rows) != 1:
-        raise ValueError(f"{path}: expected one data row, found {len(rows)}")
-    w = _from_udt(rows[0]["weights"])
+    t = _read_data(path)
+    if t.num_rows != 1:
+        raise ValueError(f"{path}: expected one data row, found {t.num_rows}")
+    w = _from_udt_column(t.column("weights"))[0]
     if w.shape[0] != int(meta["numFeatures"]):
         raise ValueError(f"{path}: numFeatures {meta['numFeatures']} != {w.shape[0]}")
-    return w, float(rows[0]["intercept"])
+    return w, float(t.column("intercept")[0].as_py())
 
 
 def save_kmeans(path: str, centers: np.ndarray, weights: Optional[np.ndarray] = None,
                 progress: Optional[dict] = None) -> None:
     c = np.asarray(centers, dtype=np.float64)
-    schema = pa.schema([pa.field("id", pa.int32()), pa.field("point", vector_udt_type())])
-    table = pa.Table.from_pylist([{"id": i, "point": _dense(c[i])} for i in range(c.shape[0])], schema)
+    schema = pa.schema([pa.field("id", pa.int32(), nullable=False), pa.field("point", vector_udt_type())],
+                       metadata=_spark_row_metadata([("id", "integer", False), ("point", "vector", True)]))
+    table = pa.Table.from_arrays([pa.array(np.arange(c.shape[0], dtype=np.int32)),
+                                  _udt_array([c[i] for i in range(c.shape[0])], sparse_density=0.0)],
+                                 schema=schema)
     files: Dict[str, dict] = {}
     if weights is not None:
         files["weights.json"] = {"clusterWeights": np.asarray(weights, np.float64).tolist()}
@@ -146,8 +224,11 @@ def save_kmeans(path: str, centers: np.ndarray, weights: Optional[np.ndarray] = 
 
 def load_kmeans(path: str) -> Tuple[np.ndarray, Optional[np.ndarray]]:
     meta = _read_meta(path, KMEANS_CLASS)
-    rows = sorted(_read_data(path).to_pylist(), key=lambda r: r["id"])
-    centers = np.stack([_from_udt(r["point"]) for r in rows]) if rows else np.zeros((0, 0))
+    t = _read_data(path)
+    ids = t.column("id").to_numpy()
+    pts = _from_udt_column(t.column("point"))
+    order = np.argsort(ids, kind="stable")
+    centers = np.stack([pts[i] for i in order]) if len(pts) else np.zeros((0, 0))
     if centers.shape[0] != int(meta["k"]):
         raise ValueError(f"{path}: k {meta['k']} != {centers.shape[0]}")
     wpath = os.path.join(path, "streaming", "weights.json")

@@ -55,6 +55,11 @@ def resolve_resume(resume: str, checkpoint: str) -> Optional[str]:
     if resume == "auto":
         if checkpoint and os.path.isdir(os.path.join(checkpoint, "metadata")):
             return checkpoint
+        # a crash between the two renames of a checkpoint replacement leaves
+        # the previous model at <checkpoint>.old (saveable._write_dir)
+        old = os.path.abspath(checkpoint) + ".old" if checkpoint else ""
+        if old and os.path.isdir(os.path.join(old, "metadata")):
+            return old
         return None
     return resume
 

@@ -19,7 +19,7 @@ from ..models.mllib_helper import NUMBER_SCALES
 from ..records.batch import (CREATED_AT, FAVOURITES, FOLLOWERS, FRIENDS, RETWEET_COUNT,
                              RawBatch, units_to_str)
 
-__all__ = ["FeaturizedBatch", "filter_mask", "featurize_batch", "lowered_units"]
+__all__ = ["FeaturizedBatch", "filter_mask", "featurize_batch", "featurize_batch_native", "lowered_units"]
 
 
 @dataclass
@@ -67,5 +67,31 @@ def featurize_batch(raw: RawBatch, num_text_features: int, begin: int, end: int,
     indices = np.concatenate(idx_parts) if idx_parts else np.zeros(0, np.int64)
     values = np.concatenate(val_parts) if val_parts else np.zeros(0, np.float64)
     X = sp.csr_matrix((values, indices, indptr), shape=(rows.shape[0], F + 4))
+    y = raw.scalars[RETWEET_COUNT, rows].astype(np.float64)
+    return FeaturizedBatch(X, y, rows, F)
+
+
+def featurize_batch_native(raw: RawBatch, num_text_features: int, begin: int, end: int,
+                           now_ms: Optional[int] = None, hash: str = "java",
+                           apply_filter: bool = True) -> FeaturizedBatch:
+    """Same result as :func:`featurize_batch`, with the bigram hashing done by
+    the host C++ featurizer (``csrc/host/featurize_cpu.cpp``: full case
+    mapping of special rows, Java / murmur3 hashing; checked against the
+    Python path in ``tests/test_oracle.py``) -- for oracle runs over
+    bench-sized batches (10^5-10^6 rows)."""
+    from ..ops._native import host
+    F = int(num_text_features)
+    now = raw.batch_time_ms if now_ms is None else int(now_ms)
+    mask = filter_mask(raw, begin, end) if apply_filter else np.ones(raw.n, bool)
+    rows = np.nonzero(mask)[0].astype(np.int64)
+    indptr, indices = host().featurize_rows(raw.text, raw.offsets, rows, F, hash)
+    n = rows.shape[0]
+    T = sp.csr_matrix((np.ones(indices.shape[0]), indices, indptr), shape=(n, F))
+    T.sum_duplicates()   # term counts, sorted indices
+    sc = raw.scalars[:, rows]
+    nums = np.stack([sc[FOLLOWERS] * NUMBER_SCALES[0], sc[FAVOURITES] * NUMBER_SCALES[1],
+                     sc[FRIENDS] * NUMBER_SCALES[2], (now - sc[CREATED_AT]) * NUMBER_SCALES[3]],
+                    axis=1).astype(np.float64)
+    X = sp.hstack([T, sp.csr_matrix(nums)], format="csr")
     y = raw.scalars[RETWEET_COUNT, rows].astype(np.float64)
     return FeaturizedBatch(X, y, rows, F)

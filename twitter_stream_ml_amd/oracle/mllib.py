@@ -35,7 +35,7 @@ import scipy.sparse as sp
 
 __all__ = [
     "round_half_up", "round_half_up_array", "StatCounter", "sgd_uniform",
-    "SGDResult", "run_minibatch_sgd", "least_squares_gradient", "KMeansState",
+    "SGDResult", "run_minibatch_sgd", "run_minibatch_sgd_active", "least_squares_gradient", "KMeansState",
     "find_closest", "kmeans_update", "standard_scaler_fit", "standard_scaler_transform",
     "decay_factor_from_half_life", "CONVERGENCE_TOL",
 ]
@@ -198,6 +198,42 @@ def run_minibatch_sgd(X: sp.csr_matrix, y: np.ndarray, w0: np.ndarray, step_size
                 diff = float(np.linalg.norm(prev - cur))
                 converged = diff < convergence_tol * max(float(np.linalg.norm(cur)), 1.0)
         i += 1
+    res.weights = w
+    res.iterations = i - 1
+    res.converged = converged
+    return res
+
+
+def run_minibatch_sgd_active(X: sp.csr_matrix, y: np.ndarray, w0: np.ndarray, step_size: float,
+                             num_iterations: int, convergence_tol: float = CONVERGENCE_TOL) -> SGDResult:
+    """:func:`run_minibatch_sgd` (miniBatchFraction 1, one rank) on the
+    columns the batch touches.  Untouched columns have a zero gradient, so
+    their weights never move; ``||w||`` adds their constant norm.  Same
+    iterates as the full-width loop (up to fp64 summation order), at a cost
+    independent of the feature width -- the oracle for F = 1e8 batches."""
+    cols = np.unique(X.indices)
+    Xc = X[:, cols].tocsr()
+    w = np.array(w0, dtype=np.float64, copy=True)
+    wc = w[cols].copy()
+    rest2 = max(float(np.dot(w, w)) - float(np.dot(wc, wc)), 0.0)
+    res = SGDResult(w, num_examples=int(y.shape[0]))
+    if y.shape[0] == 0:
+        return res
+    prev = None
+    converged = False
+    i = 1
+    while not converged and i <= num_iterations:
+        diff = Xc @ wc - y
+        g = np.asarray(Xc.T @ diff, dtype=np.float64).reshape(-1)
+        m = int(y.shape[0])
+        res.loss_history.append(float(0.5 * diff @ diff) / m)
+        new = wc - (step_size / math.sqrt(i)) * (g / m)
+        if prev is not None or i > 1:
+            d = float(np.linalg.norm(new - wc))
+            converged = d < convergence_tol * max(math.sqrt(float(new @ new) + rest2), 1.0)
+        prev, wc = wc, new
+        i += 1
+    w[cols] = wc
     res.weights = w
     res.iterations = i - 1
     res.converged = converged

@@ -161,8 +161,18 @@ class ReceiverDStream(DStream):
 
 
 class StreamingContext:
+    """Micro-batch scheduler (Spark's StreamingContext + JobScheduler).
+
+    ``max_batch_rows`` / ``max_batch_units``: capacity of the engine's
+    staging buffers.  A time-sealed batch that would outgrow them is sealed
+    early (the rest of the interval's records start the next batch) instead
+    of failing the job; Spark has no such limit because its batches live in
+    executor memory.
+    """
+
     def __init__(self, batch_seconds: float = 5.0, batch_size: int = 0, num_batches: int = 0,
-                 app_name: str = "", poll_chunk: int = 4096, max_pending: int = 8):
+                 app_name: str = "", poll_chunk: int = 4096, max_pending: int = 8,
+                 max_batch_rows: int = 0, max_batch_units: int = 0):
         if batch_seconds <= 0 and batch_size <= 0:
             raise ValueError("need batch_seconds > 0 or batch_size > 0")
         self.batch_seconds = float(batch_seconds)
@@ -171,6 +181,12 @@ class StreamingContext:
         self.app_name = app_name
         self.poll_chunk = poll_chunk
         self.max_pending = int(max_pending)
+        self.max_batch_rows = int(max_batch_rows)
+        self.max_batch_units = int(max_batch_units)
+        if self.batch_size > 0 and self.max_batch_rows > 0 and self.batch_size > self.max_batch_rows:
+            raise ValueError(f"batch_size {self.batch_size} exceeds the engine capacity {self.max_batch_rows}")
+        self._buffered_units = 0
+        self.capacity_seals = 0          # batches sealed early at the capacity limit
         self.records_done = 0            # records of all processed batches (stream position)
         self._outputs: List[tuple] = []
         self._inputs: List[ReceiverDStream] = []
@@ -263,6 +279,12 @@ class StreamingContext:
                 if want <= 0:
                     self._seal()
                     continue
+            elif self.max_batch_rows > 0:       # time-sealed: stay within capacity
+                with self._lock:
+                    want = min(want, self.max_batch_rows - self._buffered)
+                if want <= 0:
+                    self._capacity_seal()
+                    continue
             try:
                 chunk = src.poll(want, now_ms=int(time.time() * 1000))
             except Exception as e:  # receiver restart semantics: log and retry
@@ -270,19 +292,31 @@ class StreamingContext:
                 time.sleep(0.5)
                 continue
             if chunk.n:
+                if (self.max_batch_units > 0 and self._buffered
+                        and self._buffered_units + chunk.total_units > self.max_batch_units):
+                    self._capacity_seal()       # this chunk starts the next batch
                 with self._lock:
                     self._buffer.append(chunk)
                     self._buffered += chunk.n
+                    self._buffered_units += chunk.total_units
                 if self.batch_size > 0 and self._buffered >= self.batch_size:
                     self._seal()
             else:
                 time.sleep(0.01)
+
+    def _capacity_seal(self) -> None:
+        if self.capacity_seals == 0:
+            log.warning("micro-batch reached the engine capacity (%d rows / %d units): sealed early",
+                        self.max_batch_rows, self.max_batch_units)
+        self.capacity_seals += 1
+        self._seal()
 
     def _seal(self) -> None:
         if self.num_batches and self._sealed >= self.num_batches:
             return                              # never seal past the requested count
         with self._lock:
             parts, self._buffer, self._buffered = self._buffer, [], 0
+            self._buffered_units = 0
             self._sealed += 1
         t_ms = int(time.time() * 1000)
         batch = RawBatch.concat(parts, t_ms) if parts else RawBatch.empty(t_ms)
