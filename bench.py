@@ -12,10 +12,27 @@ One *step* = one micro-batch end to end: H2D of the raw tweets (overlapped
 with the previous batch), filter, lower-case + bigram hashing, prequential
 predict + stats, and up to 50 GD iterations (early exit on convergence, as
 MLlib).  Each rank trains ``--batch`` raw tweets per step (weak scaling).
-Tweets are replayed from a pool of pre-generated pinned batches (the
-generator runs at ~1M tweets/s/core, slower than the GPU consumes them).
 
-Usage:  python bench.py [--gpus N --steps K --warmup W]
+Two ingest modes:
+
+* default (device pipeline): batches are replayed from a pool that was
+  packed into the wire format once (Latin-1 / cesu rows, row words, 1-4 byte
+  scalar columns, ~166 B per tweet); the H2D of every batch is in the timed
+  region, the host packing is not.
+* ``--e2e``: each timed step also stages a fresh batch on the host from the
+  raw UTF-16 records (the pool stands in for the network receiver): a
+  staging thread runs ahead of the GPU by up to two batches.  ``--ingest
+  utf16`` (default) stages row words + packed scalars and DMAs the UTF-16
+  text straight from the receiver's registered buffer (~300 B per tweet on
+  PCIe, the device narrows Latin-1 rows); ``--ingest wire`` runs the host
+  packer on every batch.  Lower-casing, incl. the special rows, is on the
+  device in both modes.
+
+``--profile wide`` replaces the ~300-word toy vocabulary by a realistic
+50K-word multi-script one (~200K active bigrams per batch: the tiered SGD
+layout).
+
+Usage:  python bench.py [--gpus N --steps K --warmup W] [--e2e] [--profile wide]
         (N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
 """
 from __future__ import annotations
@@ -23,7 +40,9 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import queue
 import sys
+import threading
 import time
 
 import numpy as np
@@ -50,14 +69,134 @@ def parse_args(argv=None):
     ap.add_argument("--profile", default="bench", choices=["bench", "wide"],
                     help="synthetic data: bench (toy ~300-word vocabulary, ~1.4K active bigrams) or "
                          "wide (realistic 50K-word multi-script vocabulary, ~200K active bigrams)")
+    ap.add_argument("--e2e", action="store_true",
+                    help="stage every batch on the host inside the timed region (see module doc)")
+    ap.add_argument("--ingest", choices=["utf16", "wire"], default="",
+                    help="host staging of --e2e: utf16 (default; text DMA'd from the receiver buffer) "
+                         "or wire (host packer)")
     ap.add_argument("--sgd-grid", type=int, default=0)
     ap.add_argument("--ablate", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--tol", type=float, default=1e-3, help=argparse.SUPPRESS)
     ap.add_argument("--dedup", type=int, default=0, help="merge repeated bigrams per row (1/0)")
     ap.add_argument("--hybrid", type=int, default=1, help="dense 4-bit counts for hot bigrams (1/0)")
+    ap.add_argument("--comm", choices=["rccl", "gloo"], default="rccl",
+                    help="DP gradient collectives: RCCL over xGMI, or host-staged torch.distributed "
+                         "gloo (lets N ranks share one GPU for testing)")
     ap.add_argument("--json-out", default="")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args(argv)
+
+
+class Runner:
+    """Continuous stream of batches through an engine's raw slots."""
+
+    def __init__(self, eng, is_km: bool, now_ms: int):
+        self.eng, self.is_km, self.now_ms = eng, is_km, now_ms
+        self.lat, self.kept, self.iters, self.stage, self.extra = [], [], [], [], []
+
+    def process(self, slot: int):
+        if self.is_km:
+            return self.eng.process(slot, want_pred=False)
+        return self.eng.process(slot, self.now_ms)
+
+    def record(self, res, sealed: float, done: float) -> None:
+        self.lat.append((done - sealed) * 1e3)
+        if self.is_km:
+            self.kept.append(res["n_local"])
+            self.stage.append((res["ms"], 0.0))
+        else:
+            self.kept.append(res["n_kept"])
+            self.iters.append(res["iterations"])
+            self.stage.append((res["prep_ms"], res["train_ms"]))
+            self.extra.append((res.get("tiered", False), res.get("n_unique", 0), res.get("n_near", 0)))
+
+
+def run_device_pipeline(r: Runner, pool, warmup: int, steps: int, sync):
+    """Pre-packed pool; batch t+depth is submitted (async H2D) before batch t
+    is trained, so the copy engine always has the next batch queued.  Every
+    timed step trains one batch and submits one."""
+    eng = r.eng
+    depth = max(1, min(int(os.environ.get("TWTML_BENCH_DEPTH", "2")), eng.raw_slots - 1))
+    state = {"next": 0, "cur": 0}
+    sealed_at = {}
+
+    def submit_one():
+        i = state["next"]
+        sealed_at[i] = time.perf_counter()
+        eng.submit(pool[i % len(pool)], i % eng.raw_slots)
+        state["next"] = i + 1
+
+    def run(n, record):
+        for _ in range(n):
+            t = state["cur"]
+            submit_one()
+            res = r.process(t % eng.raw_slots)
+            done = time.perf_counter()
+            state["cur"] = t + 1
+            if record:
+                r.record(res, sealed_at.pop(t), done)
+            else:
+                sealed_at.pop(t)
+
+    for _ in range(depth - 1):   # prime: batches 0..depth-2 in flight before step 0
+        submit_one()
+    run(warmup, False)
+    t0, t1 = sync(lambda: run(steps, True))
+    return t0, t1
+
+
+def run_e2e(r: Runner, raws, views, ingest: str, warmup: int, steps: int, sync):
+    """Host staging inside the loop: a staging thread loads raw batch i into
+    the staging buffer of a free raw slot (wire pack or UTF-16 row words +
+    scalars) and submits its H2D, up to raw_slots - 1 batches ahead of the
+    GPU; the main thread trains batches in order."""
+    eng = r.eng
+    total = warmup + steps
+    free: "queue.Queue[int]" = queue.Queue()
+    ready: "queue.Queue" = queue.Queue()
+    for s in range(eng.raw_slots - 1):
+        free.put(s)
+    err = []
+
+    def stager():
+        try:
+            for i in range(total):
+                slot = free.get()
+                sealed = time.perf_counter()
+                raw = raws[i % len(raws)]
+                hb = views[slot]
+                if ingest == "utf16":
+                    hb.load_utf16(raw, copy_text=False)
+                else:
+                    hb.load(raw, "wire")
+                eng.submit(hb, slot)
+                ready.put((slot, sealed, time.perf_counter() - sealed))
+        except BaseException as e:   # surfaced by the main thread
+            err.append(e)
+            ready.put(None)
+
+    th = threading.Thread(target=stager, name="stager", daemon=True)
+    th.start()
+    host_ms = []
+
+    def run(n, record):
+        for _ in range(n):
+            item = ready.get()
+            if item is None:
+                raise err[0]
+            slot, sealed, stage_s = item
+            res = r.process(slot)
+            done = time.perf_counter()
+            free.put(slot)
+            if record:
+                r.record(res, sealed, done)
+                host_ms.append(stage_s * 1e3)
+
+    run(warmup, False)
+    t0, t1 = sync(lambda: run(steps, True))
+    th.join(timeout=60)
+    r.host_stage_ms = float(np.median(host_ms)) if host_ms else 0.0
+    return t0, t1
 
 
 def main(argv=None) -> int:
@@ -65,7 +204,7 @@ def main(argv=None) -> int:
     import torch  # noqa: F401  (binds the HIP runtime before the engine loads)
     from twitter_stream_ml_amd.parallel import dist as D
     from twitter_stream_ml_amd.ops.lr_engine import (DeviceLinearRegression, HostBatchView,
-                                                     LRDeviceConfig, prelower)
+                                                     LRDeviceConfig, register_host)
     from twitter_stream_ml_amd.sources.synthetic import SynthConfig, generate_batch
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
@@ -74,22 +213,23 @@ def main(argv=None) -> int:
             print(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes",
                   file=sys.stderr)
             return 2
-    info = D.init_distributed()
-    device = info.local_rank
+    info = D.init_distributed(backend="gloo" if args.comm == "gloo" else None)
+    n_dev = max(1, torch.cuda.device_count())
+    device = info.local_rank % n_dev   # gloo comm: several ranks may share a GPU
     torch.cuda.set_device(device)
     from twitter_stream_ml_amd.parallel.affinity import bind_local_numa
     numa_cpus = bind_local_numa(device)   # before the pinned pool is allocated
-    comm = D.make_rccl_comm(device)
+    comm = D.make_comm(device, args.comm)
+    ingest = args.ingest or "utf16"
 
     B = args.batch
     synth = SynthConfig.profile(args.profile, seed=args.seed + 7919 * info.rank)
     now_ms = synth.now_ms
-    # ---- pool of pinned raw batches (generated + host special-row pass)
     t_gen = time.time()
-    pool_raw = [prelower(generate_batch(synth, i * B, B, batch_time_ms=now_ms))
-                for i in range(args.pool)]
+    pool_raw = [generate_batch(synth, i * B, B, batch_time_ms=now_ms) for i in range(args.pool)]
     max_units = max(r.total_units for r in pool_raw) + 1024
-    if args.model == "kmeans":
+    is_km = args.model == "kmeans"
+    if is_km:
         from twitter_stream_ml_amd.ops.kmeans_engine import DeviceKMeans, KMDeviceConfig
         kcfg = KMDeviceConfig(k=args.k, text_dims=args.text_dims, half_life=5.0, max_rows=B,
                               max_units=max_units, seed=args.seed)
@@ -99,136 +239,90 @@ def main(argv=None) -> int:
                              step_size=args.step_size, num_iterations=args.iters, fraction=1.0,
                              begin=100, end=1000, max_rows=B, max_units=max_units,
                              sgd_grid=args.sgd_grid, ablate=args.ablate, tol=args.tol, dedup=bool(args.dedup),
-                             hybrid=bool(args.hybrid))
+                             hybrid=bool(args.hybrid), ingest=ingest if args.e2e else "wire")
         eng = DeviceLinearRegression(cfg, device=device, comm=comm)
-    pool = [HostBatchView(B, max_units).load(r) for r in pool_raw]
-    del pool_raw
+    if args.e2e:
+        views = [HostBatchView(B, max_units) for _ in range(eng.raw_slots)]
+        if ingest == "utf16":
+            for r in pool_raw:   # the receiver's buffers: DMA source of the text
+                register_host(r.text)
+    else:
+        pool = [HostBatchView(B, max_units).load(r) for r in pool_raw]
+        del pool_raw
     t_gen = time.time() - t_gen
-    is_km = args.model == "kmeans"
+    runner = Runner(eng, is_km, now_ms)
 
-    total = args.warmup + args.steps
-    lat = []
-    kept = []
-    iters = []
-    stage = []
+    def sync(fn):
+        eng.synchronize()
+        D.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()
+        eng.synchronize()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        D.barrier()
+        return t0, t1
 
-    # Continuous ingest pipeline over the engine's raw slots: batch t+depth
-    # is submitted (async H2D on the copy stream) before batch t is trained,
-    # so the copy engine always has the next batch queued.  Warmup and timed
-    # steps are one stream of batches; every timed step trains one batch and
-    # submits one (the next-but-one), i.e. exactly K batches of compute and K
-    # of H2D fall inside the timed region.
-    depth = max(1, min(int(os.environ.get("TWTML_BENCH_DEPTH", "2")), eng.raw_slots - 1))
-    state = {"next": 0, "cur": 0}
-
-    def submit_one():
-        i = state["next"]
-        eng.submit(pool[i % len(pool)], i % eng.raw_slots)
-        state["next"] = i + 1
-
-    def run(n_steps, record):
-        for s in range(n_steps):
-            t = state["cur"]
-            sealed_at[state["next"]] = time.perf_counter()
-            submit_one()
-            sealed = sealed_at.pop(t)
-            slot = t % eng.raw_slots
-            res = eng.process(slot, want_pred=False) if is_km else eng.process(slot, now_ms)
-            done = time.perf_counter()
-            state["cur"] = t + 1
-            if record:
-                lat.append((done - sealed) * 1e3)
-                if is_km:
-                    kept.append(res["n_local"])
-                    stage.append((res["ms"], 0.0))
-                else:
-                    kept.append(res["n_kept"])
-                    iters.append(res["iterations"])
-                    stage.append((res["prep_ms"], res["train_ms"]))
-
-    sealed_at = {}
-    for _ in range(depth - 1):   # prime: batches 0..depth-2 in flight before step 0
-        sealed_at[state["next"]] = time.perf_counter()
-        submit_one()
-    run(args.warmup, False)
-    eng.synchronize()
-    D.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run(args.steps, True)
-    eng.synchronize()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    D.barrier()
+    if args.e2e:
+        t0, t1 = run_e2e(runner, pool_raw, views, ingest, args.warmup, args.steps, sync)
+    else:
+        t0, t1 = run_device_pipeline(runner, pool, args.warmup, args.steps, sync)
     elapsed = D.allreduce_max_scalar(t1 - t0)
-    tweets = D.allreduce_sum_scalar(float(sum(kept)))
-    p50 = D.allreduce_max_scalar(float(np.median(lat)))
+    tweets = D.allreduce_sum_scalar(float(sum(runner.kept)))
+    p50 = D.allreduce_max_scalar(float(np.median(runner.lat)))
     value = tweets / elapsed
     ms = elapsed / args.steps * 1e3
-    if info.is_main and is_km:
-        out = {
-            "metric": "tweets/sec trained (whole node)",
-            "value": round(value, 1),
-            "unit": "tweets/s",
-            "n_gpus": info.world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "fp32",
-            "data": "synthetic tweet-shaped records (seeded C++ generator), N(0,1) random centres",
-            "config": {
-                "model": f"StreamingKMeans k={args.k}, d={2 + args.text_dims} "
-                         f"([retweetCount, followers] + {args.text_dims} hashed bigram dims), "
-                         "halfLife 5 batches, per-batch StandardScaler",
-                "global_batch": B * info.world,
-                "seq_len": 280,
-                "parallelism": f"dp{info.world}",
-            },
-            "p50_microbatch_latency_ms": round(p50, 3),
-            "trained_tweets_per_step": round(tweets / args.steps, 1),
-            "device_ms_mean": float(np.mean([s[0] for s in stage])) if stage else 0.0,
-            "pool_gen_s": round(t_gen, 2),
-            "numa_bound_cpus": len(numa_cpus) if numa_cpus else None,
+    stage = runner.stage
+    par = f"dp{info.world}" + ("-gloo" if args.comm == "gloo" else "")
+    data = ("synthetic tweet-shaped records (seeded C++ generator, "
+            f"{'realistic 50K-word multi-script' if args.profile == 'wide' else 'toy ~300-word'} vocabulary)")
+    out = {
+        "metric": "tweets/sec trained (whole node)",
+        "value": round(value, 1),
+        "unit": "tweets/s",
+        "n_gpus": info.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": (value / BASELINE_TWEETS_PER_SEC) if BASELINE_TWEETS_PER_SEC else None,
+        "dtype": "fp32",
+    }
+    if is_km:
+        out["data"] = data + ", N(0,1) random centres"
+        out["config"] = {
+            "model": f"StreamingKMeans k={args.k}, d={2 + args.text_dims} "
+                     f"([retweetCount, followers] + {args.text_dims} hashed bigram dims), "
+                     "halfLife 5 batches, per-batch StandardScaler",
+            "global_batch": B * info.world, "seq_len": 280, "parallelism": par,
         }
-        line = json.dumps(out)
-        print(line, flush=True)
-        if args.json_out:
-            with open(args.json_out, "w") as fh:
-                fh.write(line + "\n")
-    elif info.is_main:
-        out = {
-            "metric": "tweets/sec trained (whole node)",
-            "value": round(value, 1),
-            "unit": "tweets/s",
-            "n_gpus": info.world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": (value / BASELINE_TWEETS_PER_SEC) if BASELINE_TWEETS_PER_SEC else None,
-            "dtype": "fp32",
-            "data": "synthetic tweet-shaped records (seeded C++ generator), zero-init weights",
-            "config": {
-                "model": f"StreamingLinearRegressionWithSGD, {args.features}-dim hashed bigrams + 4 numeric",
-                "global_batch": B * info.world,
-                "seq_len": 280,
-                "parallelism": f"dp{info.world}",
-                "numIterations": args.iters,
-                "stepSize": args.step_size,
-                "miniBatchFraction": 1.0,
-            },
-            "p50_microbatch_latency_ms": round(p50, 3),
-            "trained_tweets_per_step": round(tweets / args.steps, 1),
-            "gd_iterations_mean": float(np.mean(iters)) if iters else 0.0,
-            "prep_ms_mean": float(np.mean([s[0] for s in stage])) if stage else 0.0,
-            "train_ms_mean": float(np.mean([s[1] for s in stage])) if stage else 0.0,
-            "pool_gen_s": round(t_gen, 2),
-            "numa_bound_cpus": len(numa_cpus) if numa_cpus else None,
+        out["device_ms_mean"] = float(np.mean([s[0] for s in stage])) if stage else 0.0
+    else:
+        out["data"] = data + ", zero-init weights"
+        out["config"] = {
+            "model": f"StreamingLinearRegressionWithSGD, {args.features}-dim hashed bigrams + 4 numeric",
+            "global_batch": B * info.world, "seq_len": 280, "parallelism": par,
+            "numIterations": args.iters, "stepSize": args.step_size, "miniBatchFraction": 1.0,
+            "hash": args.hash, "profile": args.profile,
         }
+        out["gd_iterations_mean"] = float(np.mean(runner.iters)) if runner.iters else 0.0
+        out["prep_ms_mean"] = float(np.mean([s[0] for s in stage])) if stage else 0.0
+        out["train_ms_mean"] = float(np.mean([s[1] for s in stage])) if stage else 0.0
+        if runner.extra:
+            out["tiered"] = bool(runner.extra[-1][0])
+            out["active_features"] = int(np.mean([e[1] for e in runner.extra]))
+            out["lds_tier_features"] = int(runner.extra[-1][2])
+    out["p50_microbatch_latency_ms"] = round(p50, 3)
+    out["trained_tweets_per_step"] = round(tweets / args.steps, 1)
+    out["ingest"] = (f"e2e-{ingest}: host staging of every batch in the timed region"
+                     if args.e2e else "device pipeline: pre-packed wire pool, H2D in the timed region")
+    if args.e2e:
+        out["host_stage_ms_p50"] = round(getattr(runner, "host_stage_ms", 0.0), 3)
+    out["pool_gen_s"] = round(t_gen, 2)
+    out["numa_bound_cpus"] = len(numa_cpus) if numa_cpus else None
+    if info.is_main:
         line = json.dumps(out)
         print(line, flush=True)
         if args.json_out:

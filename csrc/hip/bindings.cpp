@@ -122,6 +122,36 @@ PYBIND11_MODULE(_twtml_hip, m) {
         return std::shared_ptr<Comm>(std::make_shared<RcclComm>(s, rank, world, device));
       },
       py::arg("unique_id"), py::arg("rank"), py::arg("world"), py::arg("device"));
+  // Host-staged communicator over a Python callback (torch.distributed gloo):
+  // fn(array, op, root) runs the collective in place on a numpy view of the
+  // pinned staging buffer (op 0 sum, 1 max, 2 min, -1 broadcast, -2 all-gather)
+  m.def("HostComm", [](int rank, int world, py::function fn) {
+        // the callable is released with the GIL held, whichever thread drops the comm
+        std::shared_ptr<py::function> f(new py::function(std::move(fn)), [](py::function* p) {
+          py::gil_scoped_acquire g;
+          delete p;
+        });
+        auto cb = [f, world](void* host, size_t count, ncclDataType_t dt, int op, int root) {
+          py::gil_scoped_acquire g;
+          std::string fmt;
+          switch (dt) {
+            case ncclUint8: fmt = "u1"; break;
+            case ncclInt32: fmt = "i4"; break;
+            case ncclUint32: fmt = "u4"; break;
+            case ncclInt64: fmt = "i8"; break;
+            case ncclUint64: fmt = "u8"; break;
+            case ncclFloat32: fmt = "f4"; break;
+            case ncclFloat64: fmt = "f8"; break;
+            default: throw std::invalid_argument("HostComm: unsupported dtype");
+          }
+          const size_t n = op == -2 ? count * size_t(world) : count;
+          py::capsule view(host, [](void*) {});   // a view: the callback must not keep it
+          py::array arr(py::dtype(fmt), {py::ssize_t(n)}, {py::ssize_t(comm_dtype_size(dt))}, host, view);
+          (*f)(arr, op, root);
+        };
+        return std::shared_ptr<Comm>(std::make_shared<HostComm>(rank, world, cb));
+      },
+      py::arg("rank"), py::arg("world"), py::arg("fn"));
   // In-process loopback group: N engines on threads of one process (tests)
   py::class_<LoopbackHub, std::shared_ptr<LoopbackHub>>(m, "LoopbackGroup")
       .def(py::init<int>(), py::arg("world"))

@@ -1,5 +1,6 @@
 #include "comm.h"
 
+#include <algorithm>
 #include <cstring>
 #include <functional>
 #include <stdexcept>
@@ -59,6 +60,12 @@ void RcclComm::broadcast(void* buf, size_t count, ncclDataType_t dt, int root, h
   TWTML_NCCL_CHECK(ncclBroadcast(buf, buf, count, dt, root, comm_, s));
 }
 
+void RcclComm::allgather(const void* send, void* recv, size_t count, ncclDataType_t dt, hipStream_t s) {
+  if (count == 0) return;
+  TraceRange tr("twtml.rccl.allgather");
+  TWTML_NCCL_CHECK(ncclAllGather(send, recv, count, dt, comm_, s));
+}
+
 void RcclComm::check_async() const {
   ncclResult_t r = ncclSuccess;
   TWTML_NCCL_CHECK(ncclCommGetAsyncError(comm_, &r));
@@ -74,7 +81,7 @@ void RcclComm::abort() {
 }
 
 // ---------------------------------------------------------------------------
-static size_t dt_size(ncclDataType_t dt) {
+size_t comm_dtype_size(ncclDataType_t dt) {
   switch (dt) {
     case ncclInt8: case ncclUint8: return 1;
     case ncclFloat16: case ncclBfloat16: return 2;
@@ -111,7 +118,7 @@ void LoopbackHub::arrive_and_wait(int rank, void* buf, const std::function<void(
 }
 
 void LoopbackHub::allreduce(int rank, void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op) {
-  const size_t bytes = count * dt_size(dt);
+  const size_t bytes = count * comm_dtype_size(dt);
   arrive_and_wait(rank, buf, [&] {
     std::vector<unsigned char> acc(bytes), tmp(bytes);
     TWTML_HIP_CHECK(hipMemcpy(acc.data(), bufs_[0], bytes, hipMemcpyDeviceToHost));
@@ -121,6 +128,8 @@ void LoopbackHub::allreduce(int rank, void* buf, size_t count, ncclDataType_t dt
         case ncclUint8: reduce_into(acc.data(), tmp.data(), count, op); break;
         case ncclInt32: reduce_into(reinterpret_cast<int32_t*>(acc.data()), reinterpret_cast<int32_t*>(tmp.data()), count, op); break;
         case ncclInt64: reduce_into(reinterpret_cast<int64_t*>(acc.data()), reinterpret_cast<int64_t*>(tmp.data()), count, op); break;
+        case ncclUint32: reduce_into(reinterpret_cast<uint32_t*>(acc.data()), reinterpret_cast<uint32_t*>(tmp.data()), count, op); break;
+        case ncclUint64: reduce_into(reinterpret_cast<uint64_t*>(acc.data()), reinterpret_cast<uint64_t*>(tmp.data()), count, op); break;
         case ncclFloat32: reduce_into(reinterpret_cast<float*>(acc.data()), reinterpret_cast<float*>(tmp.data()), count, op); break;
         case ncclFloat64: reduce_into(reinterpret_cast<double*>(acc.data()), reinterpret_cast<double*>(tmp.data()), count, op); break;
         default: throw std::invalid_argument("loopback: unsupported dtype");
@@ -132,12 +141,28 @@ void LoopbackHub::allreduce(int rank, void* buf, size_t count, ncclDataType_t dt
 }
 
 void LoopbackHub::broadcast(int rank, void* buf, size_t count, ncclDataType_t dt, int root) {
-  const size_t bytes = count * dt_size(dt);
+  const size_t bytes = count * comm_dtype_size(dt);
   arrive_and_wait(rank, buf, [&] {
     std::vector<unsigned char> acc(bytes);
     TWTML_HIP_CHECK(hipMemcpy(acc.data(), bufs_[size_t(root)], bytes, hipMemcpyDeviceToHost));
     for (int r = 0; r < world_; ++r)
       TWTML_HIP_CHECK(hipMemcpy(bufs_[size_t(r)], acc.data(), bytes, hipMemcpyHostToDevice));
+  });
+}
+
+void LoopbackHub::allgather(int rank, const void* send, void* recv, size_t count, ncclDataType_t dt) {
+  const size_t bytes = count * comm_dtype_size(dt);
+  {
+    std::lock_guard<std::mutex> lk(m_);
+    if (sends_.size() != size_t(world_)) sends_.assign(size_t(world_), nullptr);
+    sends_[size_t(rank)] = send;
+  }
+  arrive_and_wait(rank, recv, [&] {
+    std::vector<unsigned char> all(bytes * size_t(world_));
+    for (int r = 0; r < world_; ++r)
+      TWTML_HIP_CHECK(hipMemcpy(all.data() + bytes * size_t(r), sends_[size_t(r)], bytes, hipMemcpyDeviceToHost));
+    for (int r = 0; r < world_; ++r)
+      TWTML_HIP_CHECK(hipMemcpy(bufs_[size_t(r)], all.data(), all.size(), hipMemcpyHostToDevice));
   });
 }
 
@@ -156,6 +181,79 @@ void LoopbackComm::broadcast(void* buf, size_t count, ncclDataType_t dt, int roo
   if (world_ == 1 || count == 0) return;
   TWTML_HIP_CHECK(hipStreamSynchronize(s));
   hub_->broadcast(rank_, buf, count, dt, root);
+}
+
+void LoopbackComm::allgather(const void* send, void* recv, size_t count, ncclDataType_t dt, hipStream_t s) {
+  if (count == 0) return;
+  TWTML_HIP_CHECK(hipStreamSynchronize(s));
+  if (world_ == 1) {
+    TWTML_HIP_CHECK(hipMemcpy(recv, send, count * comm_dtype_size(dt), hipMemcpyDeviceToDevice));
+    return;
+  }
+  hub_->allgather(rank_, send, recv, count, dt);
+}
+
+// ---------------------------------------------------------------------------
+HostComm::HostComm(int rank, int world, Fn fn) : fn_(std::move(fn)) {
+  if (world < 1 || rank < 0 || rank >= world) throw std::invalid_argument("bad rank/world");
+  rank_ = rank;
+  world_ = world;
+}
+
+HostComm::~HostComm() {
+  if (host_) (void)hipHostFree(host_);
+}
+
+void* HostComm::stage(size_t bytes) {
+  if (bytes > cap_) {
+    if (host_) TWTML_HIP_CHECK(hipHostFree(host_));
+    cap_ = std::max(bytes, cap_ * 2);
+    TWTML_HIP_CHECK(hipHostMalloc(&host_, cap_, hipHostMallocDefault));
+  }
+  return host_;
+}
+
+static int op_code(ncclRedOp_t op) {
+  switch (op) {
+    case ncclSum: return 0;
+    case ncclMax: return 1;
+    case ncclMin: return 2;
+    default: throw std::invalid_argument("HostComm: unsupported reduction");
+  }
+}
+
+void HostComm::allreduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t s) {
+  if (count == 0) return;
+  TraceRange tr("twtml.hostcomm.allreduce");
+  const size_t bytes = count * comm_dtype_size(dt);
+  void* h = stage(bytes);
+  TWTML_HIP_CHECK(hipMemcpyAsync(h, buf, bytes, hipMemcpyDeviceToHost, s));
+  TWTML_HIP_CHECK(hipStreamSynchronize(s));
+  fn_(h, count, dt, op_code(op), 0);
+  TWTML_HIP_CHECK(hipMemcpyAsync(buf, h, bytes, hipMemcpyHostToDevice, s));
+  TWTML_HIP_CHECK(hipStreamSynchronize(s));   // the staging buffer is reused by the next call
+}
+
+void HostComm::broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t s) {
+  if (count == 0 || world_ == 1) return;
+  const size_t bytes = count * comm_dtype_size(dt);
+  void* h = stage(bytes);
+  TWTML_HIP_CHECK(hipMemcpyAsync(h, buf, bytes, hipMemcpyDeviceToHost, s));
+  TWTML_HIP_CHECK(hipStreamSynchronize(s));
+  fn_(h, count, dt, -1, root);
+  TWTML_HIP_CHECK(hipMemcpyAsync(buf, h, bytes, hipMemcpyHostToDevice, s));
+  TWTML_HIP_CHECK(hipStreamSynchronize(s));
+}
+
+void HostComm::allgather(const void* send, void* recv, size_t count, ncclDataType_t dt, hipStream_t s) {
+  if (count == 0) return;
+  const size_t bytes = count * comm_dtype_size(dt);
+  uint8_t* h = static_cast<uint8_t*>(stage(bytes * size_t(world_)));
+  TWTML_HIP_CHECK(hipMemcpyAsync(h + bytes * size_t(rank_), send, bytes, hipMemcpyDeviceToHost, s));
+  TWTML_HIP_CHECK(hipStreamSynchronize(s));
+  fn_(h, count, dt, -2, 0);
+  TWTML_HIP_CHECK(hipMemcpyAsync(recv, h, bytes * size_t(world_), hipMemcpyHostToDevice, s));
+  TWTML_HIP_CHECK(hipStreamSynchronize(s));
 }
 
 }  // namespace twtml

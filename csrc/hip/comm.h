@@ -29,6 +29,8 @@ class Comm {
   virtual ~Comm() = default;
   virtual void allreduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t s) = 0;
   virtual void broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t s) = 0;
+  // recv[r * count .. (r + 1) * count) = rank r's send[0 .. count)
+  virtual void allgather(const void* send, void* recv, size_t count, ncclDataType_t dt, hipStream_t s) = 0;
   virtual void check_async() const {}
   virtual void abort() {}
   virtual std::string kind() const = 0;
@@ -47,6 +49,7 @@ class RcclComm final : public Comm {
   RcclComm& operator=(const RcclComm&) = delete;
   void allreduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t s) override;
   void broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t s) override;
+  void allgather(const void* send, void* recv, size_t count, ncclDataType_t dt, hipStream_t s) override;
   void check_async() const override;
   void abort() override;
   std::string kind() const override { return "rccl"; }
@@ -61,6 +64,7 @@ class LoopbackHub {
   // Blocking collective: every rank calls it with its device buffer.
   void allreduce(int rank, void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op);
   void broadcast(int rank, void* buf, size_t count, ncclDataType_t dt, int root);
+  void allgather(int rank, const void* send, void* recv, size_t count, ncclDataType_t dt);
   int world() const { return world_; }
 
  private:
@@ -71,6 +75,7 @@ class LoopbackHub {
   int arrived_ = 0;
   unsigned long long generation_ = 0;
   std::vector<void*> bufs_;
+  std::vector<const void*> sends_;
 };
 
 class LoopbackComm final : public Comm {
@@ -78,11 +83,40 @@ class LoopbackComm final : public Comm {
   LoopbackComm(std::shared_ptr<LoopbackHub> hub, int rank);
   void allreduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t s) override;
   void broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t s) override;
+  void allgather(const void* send, void* recv, size_t count, ncclDataType_t dt, hipStream_t s) override;
   std::string kind() const override { return "loopback"; }
 
  private:
   std::shared_ptr<LoopbackHub> hub_;
 };
+
+// Host-staged communicator over a callback -- in practice torch.distributed
+// gloo (parallel/dist.py make_comm(kind="gloo")): the engine's stream is
+// synchronised, the buffer staged through pinned host memory, the callback
+// runs the collective in place on it, and the result goes back to the
+// device.  This is how the multi-PROCESS engine path (torchrun, one engine per
+// process, real process group) runs with several ranks on ONE GPU, which RCCL
+// refuses; slow by design, not a production data plane.
+class HostComm final : public Comm {
+ public:
+  // fn(host, count, dtype, op, root): op 0 sum, 1 max, 2 min, -1 broadcast
+  // from root, -2 all-gather (host holds world * count elements, rank r's at r * count)
+  using Fn = std::function<void(void* host, size_t count, ncclDataType_t dt, int op, int root)>;
+  HostComm(int rank, int world, Fn fn);
+  ~HostComm() override;
+  void allreduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t s) override;
+  void broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t s) override;
+  void allgather(const void* send, void* recv, size_t count, ncclDataType_t dt, hipStream_t s) override;
+  std::string kind() const override { return "host"; }
+
+ private:
+  void* stage(size_t bytes);
+  Fn fn_;
+  void* host_ = nullptr;
+  size_t cap_ = 0;
+};
+
+size_t comm_dtype_size(ncclDataType_t dt);
 
 std::string rccl_unique_id();
 std::string rccl_version();

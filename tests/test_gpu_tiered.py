@@ -59,15 +59,18 @@ def _parity(profile, F, hash, n, batches, seed, expect_tiered, eng=None):
     return out
 
 
-def _check(out, werr_same=2e-4, werr_diff=3e-3):
+def _check(out, werr_same=1e-6, werr_diff=3e-3):
+    """Measured on MI355X (round 2): weight errors 2e-9..2e-8 relative (norm)
+    after 3 x 50 iterations, < 5e-5 of the rounded predictions off by one,
+    MSE within 1e-7 -- the bounds below leave ~50x headroom."""
     for o in out:
         assert abs(o["it_gpu"] - o["it_orc"]) <= 1, o
         # an iteration count differing by one moves the weights by one step
         # below the convergence tolerance (1e-3 |w|)
         assert o["werr"] < (werr_same if o["it_gpu"] == o["it_orc"] else werr_diff), o
-        assert o["pred_mis"] < 0.01, o
+        assert o["pred_mis"] < 1e-3, o
         assert o["pred_maxdiff"] <= 1.0 + 1e-9, o
-        assert o["mse_rel"] < 1e-3, o
+        assert o["mse_rel"] < 1e-5, o
 
 
 def test_tiered_small_matches_oracle(hip_module):

@@ -23,7 +23,7 @@ from typing import Callable, Optional
 
 import numpy as np
 
-__all__ = ["DistInfo", "init_distributed", "dist_info", "make_rccl_comm", "allreduce_fn",
+__all__ = ["DistInfo", "init_distributed", "dist_info", "make_rccl_comm", "make_comm", "allreduce_fn",
            "barrier", "allreduce_max_scalar", "allreduce_sum_scalar", "shutdown",
            "check_replicas", "replica_digest", "ReplicaDivergence", "gather_to_main"]
 
@@ -85,6 +85,42 @@ def make_rccl_comm(device: int):
     obj = [h.rccl_unique_id() if info.rank == 0 else None]
     dist.broadcast_object_list(obj, src=0)
     return h.Comm(obj[0], info.rank, info.world, int(device))
+
+
+def make_comm(device: int, kind: str = "rccl"):
+    """Engine communicator: ``rccl`` (device collectives on the engine stream,
+    one GPU per rank) or ``gloo`` (host-staged through torch.distributed
+    gloo, so N ranks may share one GPU: the real multi-process engine path,
+    testable on a single MI355X).  None when world == 1."""
+    info = dist_info()
+    if info.world <= 1:
+        return None
+    if kind == "rccl":
+        return make_rccl_comm(device)
+    if kind != "gloo":
+        raise ValueError(f"unknown comm {kind!r}")
+    import torch
+    import torch.distributed as dist
+    from ..ops._native import hip
+    group = None if info.backend == "gloo" else dist.new_group(backend="gloo")
+    ops = {0: dist.ReduceOp.SUM, 1: dist.ReduceOp.MAX, 2: dist.ReduceOp.MIN}
+    # unsigned buffers reduce as their signed twins (sums wrap identically);
+    # MAX / MIN only ever see u8 flags, which torch / gloo handle natively
+    as_signed = {np.dtype("u4"): np.dtype("i4"), np.dtype("u8"): np.dtype("i8")}
+
+    def collective(arr: np.ndarray, op: int, root: int) -> None:
+        a = arr.view(as_signed.get(arr.dtype, arr.dtype))
+        t = torch.from_numpy(a)
+        if op == -1:
+            dist.broadcast(t, src=root, group=group)
+        elif op == -2:
+            parts = list(t.chunk(info.world))
+            mine = parts[info.rank].clone()
+            dist.all_gather(parts, mine, group=group)
+        else:
+            dist.all_reduce(t, op=ops[op], group=group)
+
+    return hip().HostComm(info.rank, info.world, collective)
 
 
 def allreduce_fn() -> Optional[Callable[[np.ndarray], np.ndarray]]:
