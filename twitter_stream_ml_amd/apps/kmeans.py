@@ -173,8 +173,8 @@ def main(argv: Optional[List[str]] = None) -> int:
     cap = getattr(engine, "cfg", None)   # device engine: staging capacity per batch
     ssc = StreamingContext(args.seconds, batch_size=args.batchSize, num_batches=remaining,
                            app_name=APP_NAME,
-                           max_batch_rows=int(cap.max_rows) if cap is not None else 0,
-                           max_batch_units=int(cap.max_units) if cap is not None else 0)
+                           max_batch_rows=int(getattr(cap, "max_rows", 0) or 0),
+                           max_batch_units=int(getattr(cap, "max_units", 0) or 0))
     log.info("Initializing Twitter stream...")
     stream = ssc.twitterStream(make_source(args.source, rate=args.sourceRate, seed=args.seed,
                                            shard=info.rank, num_shards=info.world,

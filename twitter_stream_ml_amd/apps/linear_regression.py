@@ -214,8 +214,8 @@ def main(argv: Optional[List[str]] = None) -> int:
     cap = getattr(engine, "cfg", None)   # device engines: staging capacity per batch
     ssc = StreamingContext(conf.seconds, batch_size=conf.batchSize, num_batches=remaining,
                            app_name=conf.appName(),
-                           max_batch_rows=int(cap.max_rows) if cap is not None else 0,
-                           max_batch_units=int(cap.max_units) if cap is not None else 0)
+                           max_batch_rows=int(getattr(cap, "max_rows", 0) or 0),
+                           max_batch_units=int(getattr(cap, "max_units", 0) or 0))
     log.info("Initializing Twitter stream...")
     stream = ssc.twitterStream(make_source(conf.source, rate=conf.sourceRate, seed=conf.seed,
                                            shard=rank, num_shards=world,
