@@ -193,8 +193,8 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
   TWTML_HIP_CHECK(hipMemset(sgd_.red64, 0, 4 * sizeof(double)));
   ensure_compact(4096);
   const int world = comm_ ? comm_->world() : 1;
-  n_global_ = dmalloc<int64_t>(size_t(world) + 2);
-  TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_counters_), 8 * sizeof(int64_t),
+  n_global_ = dmalloc<int64_t>(2 * size_t(world) + 2);
+  TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_counters_), (8 + 2 * size_t(world)) * sizeof(int64_t),
                                 hipHostMallocDefault));
   TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_out_),
                                 (32 + size_t(std::max(1, cfg_.num_iterations))) * sizeof(double),
@@ -351,7 +351,8 @@ LREngine::~LREngine() {
                   prep_.newslot, prep_.slot_fid, prep_.tscan, prep_.tscan_blk, prep_.hist_near, prep_.tparam,
                   sgd_.gfix, sgd_.rbuf,
                   sgd_.w64, sgd_.wc64, sgd_.wc32, sgd_.g64, sgd_.red64, sgd_.stats, sgd_.state,
-                  sgd_.loss_hist, sgd_.pred_out, sgd_.nrm, sgd_.wnorm_next, sgd_.part, sgd_.itrec, iter_tdbg_, lower_page_, lower_blocks_, n_global_};
+                  sgd_.loss_hist, sgd_.pred_out, sgd_.nrm, sgd_.wnorm_next, sgd_.part, sgd_.itrec, iter_tdbg_, lower_page_, lower_blocks_, n_global_,
+                  ugather_};
   for (void* b : bufs) if (b) (void)hipFree(b);
   if (host_counters_) (void)hipHostFree(host_counters_);
   if (host_out_) (void)hipHostFree(host_out_);
@@ -382,7 +383,7 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   auto tr_prep = std::make_unique<TraceRange>("twtml.lr.prep");   // filter .. remap
   FeaturizeParams fp{cfg_.num_text_features, cfg_.hash_kind, cfg_.require_retweet,
                      cfg_.range_filter, cfg_.begin, cfg_.end, now_ms};
-  launch_prep_init(prep_, n_global_, world + 2, s);
+  launch_prep_init(prep_, n_global_, 2 * world + 2, s);
   launch_filter_sort(b, prep_, fp, s);
   launch_chunk_layout(b, prep_, s);
   // lazy ids: only the histogram's sample chunks keep their hashed ids; the
@@ -391,36 +392,59 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   fp.idx_mode = lazy ? 1 : 0;
   launch_featurize(b, prep_, fp, lower_page_, lower_blocks_, s);
   if (!lazy) raw_.release_slot(slot, s);  // raw slot may be overwritten now
-  if (world > 1) comm_->allreduce(prep_.flags, size_t(prep_.flag_len), ncclUint8, ncclMax, s);
-  launch_compact_active(prep_, s);
-  // global kept count (and per-rank counts for sampling offsets)
+  launch_compact_active(prep_, s);        // this rank's active ids (clears the flags)
+  // per-rank kept rows (sampling offsets, global m) and active-set sizes:
+  // n_global_[1 + r] / n_global_[1 + world + r], one small all-reduce
   TWTML_HIP_CHECK(hipMemcpyAsync(n_global_ + 1 + rank, prep_.counters, sizeof(int64_t),
                                  hipMemcpyDeviceToDevice, s));
-  if (world > 1) comm_->allreduce(n_global_ + 1, size_t(world), ncclInt64, ncclSum, s);
+  if (world > 1) {
+    TWTML_HIP_CHECK(hipMemcpyAsync(n_global_ + 1 + world + rank, prep_.counters + 1, sizeof(int64_t),
+                                   hipMemcpyDeviceToDevice, s));
+    comm_->allreduce(n_global_ + 1, size_t(2 * world), ncclInt64, ncclSum, s);
+  }
   TWTML_HIP_CHECK(hipMemcpyAsync(host_counters_, prep_.counters, 4 * sizeof(int64_t),
                                  hipMemcpyDeviceToHost, s));
   TWTML_HIP_CHECK(hipMemcpyAsync(host_norm_, raw_.norm_stats(slot), 2 * sizeof(int64_t),
                                  hipMemcpyDeviceToHost, s));
-  TWTML_HIP_CHECK(hipMemcpyAsync(host_counters_ + 4, n_global_ + 1,
-                                 sizeof(int64_t) * size_t(std::min(world, 4)), hipMemcpyDeviceToHost, s));
-  std::vector<int64_t> per_rank(size_t(world), 0);
+  TWTML_HIP_CHECK(hipMemcpyAsync(host_counters_ + 8, n_global_ + 1, sizeof(int64_t) * size_t(2 * world),
+                                 hipMemcpyDeviceToHost, s));
   TWTML_HIP_CHECK(hipStreamSynchronize(s));
   if (host_counters_[3] != 0) throw std::runtime_error("feature buffer capacity exceeded");
+  const int64_t* per_rank = host_counters_ + 8;
+  if (world > 1) {
+    // Active-set union: every rank numbers the same slots.  Each rank's
+    // sorted id list (padded with -1 to the longest) is all-gathered --
+    // sum_r nU_r ids instead of an all-reduce of F flag bytes (100 MB at
+    // F = 1e8) -- then flagged and compacted again.
+    int64_t maxU = 0;
+    for (int r = 0; r < world; ++r) maxU = std::max(maxU, per_rank[world + r]);
+    if (maxU > 0) {
+      const int64_t mine = host_counters_[1];
+      if (maxU > mine)
+        TWTML_HIP_CHECK(hipMemsetAsync(prep_.uniq + mine, 0xFF, sizeof(int32_t) * size_t(maxU - mine), s));
+      const int64_t need = maxU * int64_t(world);
+      if (need > ugather_cap_) {
+        if (ugather_) (void)hipFree(ugather_);
+        ugather_cap_ = std::max(need, 2 * ugather_cap_);
+        ugather_ = dmalloc<int32_t>(size_t(ugather_cap_));
+      }
+      comm_->allgather(prep_.uniq, ugather_, size_t(maxU), ncclInt32, s);
+      launch_flag_ids(ugather_, need, prep_, s);
+      launch_compact_active(prep_, s);
+      TWTML_HIP_CHECK(hipMemcpyAsync(host_counters_ + 1, prep_.counters + 1, sizeof(int64_t),
+                                     hipMemcpyDeviceToHost, s));
+      TWTML_HIP_CHECK(hipStreamSynchronize(s));
+    }
+  }
   res.n_kept = host_counters_[0];
   res.rows_lowered = host_norm_[0];
   res.rows_narrowed = host_norm_[1];
   res.n_unique = host_counters_[1];
   res.entries = host_counters_[2] * kChunkStride;
   int64_t row_offset = 0, n_glob = 0;
-  if (world <= 4) {
-    for (int r = 0; r < world; ++r) per_rank[size_t(r)] = host_counters_[4 + r];
-  } else {
-    TWTML_HIP_CHECK(hipMemcpy(per_rank.data(), n_global_ + 1, sizeof(int64_t) * size_t(world),
-                              hipMemcpyDeviceToHost));
-  }
   for (int r = 0; r < world; ++r) {
-    if (r < rank) row_offset += per_rank[size_t(r)];
-    n_glob += per_rank[size_t(r)];
+    if (r < rank) row_offset += per_rank[r];
+    n_glob += per_rank[r];
   }
   res.n_kept_global = n_glob;
 

@@ -164,12 +164,14 @@ class LREngine {
   uint64_t* iter_tdbg_ = nullptr;
   uint8_t* lower_page_ = nullptr;
   uint16_t* lower_blocks_ = nullptr;
-  int64_t* host_counters_ = nullptr;  // pinned [8]
+  int64_t* host_counters_ = nullptr;  // pinned [8 + 2 world]: counters | per-rank kept | per-rank active
   double* host_out_ = nullptr;        // pinned [16 + iters]
   double* host_flags_ = nullptr;      // pinned [iters + 1] convergence flag per iteration
   int64_t* host_norm_ = nullptr;      // pinned [2] rows lowered / narrowed on the device
   std::vector<hipEvent_t> iter_events_;
-  int64_t* n_global_ = nullptr;       // device [world + 1]
+  int64_t* n_global_ = nullptr;       // device [2 world + 2]
+  int32_t* ugather_ = nullptr;        // DP active-set union: all-gathered id lists
+  int64_t ugather_cap_ = 0;
   hipEvent_t ev_[4] = {nullptr, nullptr, nullptr, nullptr};
   int num_cu_ = 256;
 };

@@ -839,6 +839,22 @@ void launch_compact_active(const DevPrepared& p, hipStream_t s) {
                      p.slot_of);
 }
 
+// DP active-set union: flag every id of the all-gathered per-rank lists
+// (-1 pads a shorter list); the next compaction numbers the union.
+__global__ __launch_bounds__(kBlock) void k_flag_ids(const int32_t* ids, int64_t n, uint8_t* flags,
+                                                     int64_t flag_len) {
+  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+    const int32_t id = ids[i];
+    if (id >= 0 && id < flag_len) flags[id] = 1;
+  }
+}
+
+void launch_flag_ids(const int32_t* ids, int64_t n, const DevPrepared& p, hipStream_t s) {
+  if (n <= 0) return;
+  const int grid = int(std::min<int64_t>(ceil_div(n, kBlock), 4096));
+  hipLaunchKernelGGL(k_flag_ids, dim3(grid), dim3(kBlock), 0, s, ids, n, p.flags, p.flag_len);
+}
+
 // ---------------------------------------------------------------------------
 // Remap hashed ids to compact slots: slot = 4 + slot_of[id]; pad -> per-lane pad.
 // ---------------------------------------------------------------------------

@@ -195,6 +195,8 @@ void launch_featurize(const DevRawBatch& b, const DevPrepared& p, const Featuriz
 // after a lazy (idx_mode 1) featurize: the ids of every fast chunk (idx_mode 2)
 void launch_featurize_fast_ids(const DevRawBatch& b, const DevPrepared& p, FeaturizeParams fp, hipStream_t s);
 void launch_compact_active(const DevPrepared& p, hipStream_t s);
+// DP: flag the ids of all-gathered active lists (< 0: padding) for a second compaction
+void launch_flag_ids(const int32_t* ids, int64_t n, const DevPrepared& p, hipStream_t s);
 void launch_remap(const DevPrepared& p, int64_t entries, int64_t n_unique, bool u16, hipStream_t s);
 // per-row duplicate merging for u16 slot spaces up to 8192 slots
 bool dedup_supported(int64_t ns);

@@ -1,7 +1,7 @@
 """Data-parallel engine path on one GPU via the in-process loopback communicator.
 
 RCCL refuses two ranks on the same device, so the DP orchestration of the
-engine (flag MAX all-reduce for the active-feature union, per-rank kept counts
+engine (all-gather of the per-rank active id lists, per-rank kept counts
 and sampling offsets, per-iteration gradient all-reduce, stats all-reduce,
 early exit agreement) is exercised with N engines on N threads of one
 process, reducing through host memory.  DP over shards must equal the

@@ -1,0 +1,155 @@
+"""Cross-process data parallelism on one MI355X (SURVEY §2.4 DP, §2.5 CS2).
+
+N ranks are N processes sharing GPU 0; each owns an engine whose collectives
+go through the host-staged torch.distributed gloo communicator
+(``parallel/dist.make_comm(..., "gloo")`` -> ``csrc/hip/comm.cpp`` HostComm).
+This is the engine DP path a one-GPU-per-rank RCCL job runs -- per-rank shards,
+per-rank kept counts / sampling offsets, the active-id all-gather union, the
+tiered slot-count all-reduce, the per-iteration gradient all-reduce, stats and
+early-exit agreement -- across real process boundaries; only the transport
+differs (RCCL refuses two ranks on one device).  DP over shards must equal a
+single engine on the concatenated batch, and the replicas must be
+bit-identical.  The last test drives the real launcher:
+``torch.distributed.run ... bench.py --gpus 2 --comm gloo``.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+NOW = 1_700_000_000_000
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+# (profile, F, hash, rows per batch, batches, expect tiered)
+LR_CASES = [("twitter", 1 << 20, "java", 6000, 3, False),
+            ("wide", 1 << 20, "java", 20000, 2, True),
+            ("wide", 100_000_000, "murmur3", 20000, 2, True)]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _lr_cfg(F, hash, rows):
+    from twitter_stream_ml_amd.ops.lr_engine import LRDeviceConfig
+    return LRDeviceConfig(num_text_features=F, hash=hash, max_rows=rows, max_units=rows * 300,
+                          num_iterations=20)
+
+
+def _km_cfg():
+    from twitter_stream_ml_amd.ops.kmeans_engine import KMDeviceConfig
+    return KMDeviceConfig(k=6, text_dims=4, seed=2, max_rows=8192, max_units=8192 * 300)
+
+
+def _batches(profile, rows, n, seed):
+    from twitter_stream_ml_amd.sources.synthetic import SynthConfig, generate_batch
+    synth = SynthConfig.profile(profile, seed=seed)
+    return [generate_batch(synth, t * rows, rows, batch_time_ms=NOW + t * 5000) for t in range(n)]
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch  # noqa: F401  (binds the HIP runtime before the engine loads)
+    from twitter_stream_ml_amd.ops.kmeans_engine import DeviceKMeans
+    from twitter_stream_ml_amd.ops.lr_engine import DeviceLinearRegression
+    from twitter_stream_ml_amd.parallel import dist as D
+    D.init_distributed(backend="gloo")
+    comm = D.make_comm(0, "gloo")
+    out = {}
+    for ci, (profile, F, hash, rows, nb, _) in enumerate(LR_CASES):
+        eng = DeviceLinearRegression(_lr_cfg(F, hash, rows), device=0, comm=comm)
+        meta = []
+        for full in _batches(profile, rows, nb, seed=40 + ci):
+            r = eng.train_batch(full.shard(rank, world), want_pred=False)
+            meta.append([r["iterations"], r["n_kept_global"], r["n_unique"], int(r["tiered"])]
+                        + list(r["stats"]))
+        out[f"lr{ci}_w"] = eng.get_weights()
+        out[f"lr{ci}_meta"] = np.array(meta, np.float64)
+        del eng
+    km = DeviceKMeans(_km_cfg(), device=0, comm=comm)
+    for t, full in enumerate(_batches("twitter", 4000, 3, seed=8)):
+        r = km.update_raw(full.shard(rank, world))
+        c, w = km.get_state()
+        out[f"km{t}_c"], out[f"km{t}_w"] = c, w
+        out[f"km{t}_n"] = np.array([r["n"], r["n_local"]])
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), **out)
+    D.barrier()
+    D.shutdown()
+
+
+@pytest.fixture(scope="module")
+def dp_runs(tmp_path_factory, hip_module):
+    import torch.multiprocessing as mp
+    out = tmp_path_factory.mktemp("dp_procs")
+    world = 2
+    mp.start_processes(_worker, args=(world, _free_port(), str(out)), nprocs=world, join=True,
+                       start_method="spawn")
+    return world, [dict(np.load(out / f"r{r}.npz")) for r in range(world)]
+
+
+@pytest.mark.parametrize("ci", range(len(LR_CASES)))
+def test_lr_dp_processes_equal_single_engine(dp_runs, ci):
+    from twitter_stream_ml_amd.ops.lr_engine import DeviceLinearRegression
+    world, ranks = dp_runs
+    profile, F, hash, rows, nb, tiered = LR_CASES[ci]
+    single = DeviceLinearRegression(_lr_cfg(F, hash, rows), device=0)
+    for t, full in enumerate(_batches(profile, rows, nb, seed=40 + ci)):
+        r1 = single.train_batch(full, want_pred=False)
+        assert bool(r1["tiered"]) == tiered
+        for d in ranks:
+            it, kept, nu, tr = d[f"lr{ci}_meta"][t][:4]
+            stats = d[f"lr{ci}_meta"][t][4:]
+            assert (int(it), int(kept), int(nu), bool(tr)) == (r1["iterations"], r1["n_kept"],
+                                                                r1["n_unique"], tiered)
+            np.testing.assert_allclose(stats[:3], r1["stats"][:3], rtol=1e-12)
+            np.testing.assert_allclose(stats[3:], r1["stats"][3:], rtol=1e-5)
+    w1 = single.get_weights()
+    scale = max(np.abs(w1).max(), 1e-12)
+    for d in ranks:
+        np.testing.assert_allclose(d[f"lr{ci}_w"], w1, rtol=1e-4, atol=1e-6 * scale)
+    for d in ranks[1:]:   # replicas bit-identical across processes
+        np.testing.assert_array_equal(d[f"lr{ci}_w"], ranks[0][f"lr{ci}_w"])
+
+
+def test_kmeans_dp_processes(dp_runs):
+    from twitter_stream_ml_amd.ops.kmeans_engine import DeviceKMeans
+    world, ranks = dp_runs
+    single = DeviceKMeans(_km_cfg(), device=0)
+    for t, full in enumerate(_batches("twitter", 4000, 3, seed=8)):
+        r1 = single.update_raw(full)
+        assert sum(int(d[f"km{t}_n"][1]) for d in ranks) == r1["n"]
+        c1, w1 = single.get_state()
+        for d in ranks:
+            assert int(d[f"km{t}_n"][0]) == r1["n"]
+            np.testing.assert_allclose(d[f"km{t}_w"].sum(), w1.sum(), rtol=1e-9)
+        for d in ranks[1:]:
+            np.testing.assert_array_equal(d[f"km{t}_c"], ranks[0][f"km{t}_c"])
+        # continue from the DP state: per-batch comparison (ill-conditioned
+        # split ties may flip a point, see test_gpu_kmeans.py)
+        single.set_state(ranks[0][f"km{t}_c"], ranks[0][f"km{t}_w"])
+
+
+def test_torchrun_bench_two_ranks_gloo(hip_module):
+    """The driver's launcher on one GPU: 2 ranks, engine DP through gloo."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--comm", "gloo", "--batch", "100000", "--steps", "3", "--warmup", "1",
+           "--pool", "2"]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-4000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2-gloo"
+    assert d["config"]["global_batch"] == 200000 and d["value"] > 0
