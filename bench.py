@@ -15,24 +15,26 @@ MLlib).  Each rank trains ``--batch`` raw tweets per step (weak scaling).
 
 Two ingest modes:
 
-* default (device pipeline): batches are replayed from a pool that was
+* default (end to end): each timed step also stages a fresh batch on the
+  host from the raw records (the pool stands in for the network receiver): a staging
+  thread runs ahead of the GPU by up to two batches.  ``--ingest utf8``
+  (default) keeps the text as the UTF-8 bytes the network delivers: the
+  host stages row words + packed scalars and the text is DMA'd straight from
+  the receiver's registered buffer (~152 B per tweet on PCIe; the device
+  decodes non-ASCII rows and narrows Latin-1 ones).  ``--ingest utf16`` does
+  the same from Java-style UTF-16 records (~300 B per tweet), ``--ingest
+  wire`` runs the host packer on every batch.  Lower-casing, incl. the
+  special rows, is on the device in every mode.
+* ``--prepacked`` (device pipeline only): batches are replayed from a pool
   packed into the wire format once (Latin-1 / cesu rows, row words, 1-4 byte
   scalar columns, ~166 B per tweet); the H2D of every batch is in the timed
   region, the host packing is not.
-* ``--e2e``: each timed step also stages a fresh batch on the host from the
-  raw UTF-16 records (the pool stands in for the network receiver): a
-  staging thread runs ahead of the GPU by up to two batches.  ``--ingest
-  utf16`` (default) stages row words + packed scalars and DMAs the UTF-16
-  text straight from the receiver's registered buffer (~300 B per tweet on
-  PCIe, the device narrows Latin-1 rows); ``--ingest wire`` runs the host
-  packer on every batch.  Lower-casing, incl. the special rows, is on the
-  device in both modes.
 
 ``--profile wide`` replaces the ~300-word toy vocabulary by a realistic
 50K-word multi-script one (~200K active bigrams per batch: the tiered SGD
 layout).
 
-Usage:  python bench.py [--gpus N --steps K --warmup W] [--e2e] [--profile wide]
+Usage:  python bench.py [--gpus N --steps K --warmup W] [--prepacked] [--profile wide]
         (N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
 """
 from __future__ import annotations
@@ -70,10 +72,12 @@ def parse_args(argv=None):
                     help="synthetic data: bench (toy ~300-word vocabulary, ~1.4K active bigrams) or "
                          "wide (realistic 50K-word multi-script vocabulary, ~200K active bigrams)")
     ap.add_argument("--e2e", action="store_true",
-                    help="stage every batch on the host inside the timed region (see module doc)")
-    ap.add_argument("--ingest", choices=["utf16", "wire"], default="",
-                    help="host staging of --e2e: utf16 (default; text DMA'd from the receiver buffer) "
-                         "or wire (host packer)")
+                    help="stage every batch on the host inside the timed region (the default)")
+    ap.add_argument("--prepacked", action="store_true",
+                    help="device pipeline only: replay a pool packed once, host staging not timed")
+    ap.add_argument("--ingest", choices=["utf8", "utf16", "wire"], default="",
+                    help="host staging of --e2e: utf8 (default) / utf16 (text DMA'd from the receiver "
+                         "buffer) or wire (host packer)")
     ap.add_argument("--sgd-grid", type=int, default=0)
     ap.add_argument("--ablate", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--tol", type=float, default=1e-3, help=argparse.SUPPRESS)
@@ -145,7 +149,7 @@ def run_device_pipeline(r: Runner, pool, warmup: int, steps: int, sync):
     return t0, t1
 
 
-def run_e2e(r: Runner, raws, views, ingest: str, warmup: int, steps: int, sync):
+def run_e2e(r: Runner, raws, u8s, views, ingest: str, warmup: int, steps: int, sync):
     """Host staging inside the loop: a staging thread loads raw batch i into
     the staging buffer of a free raw slot (wire pack or UTF-16 row words +
     scalars) and submits its H2D, up to raw_slots - 1 batches ahead of the
@@ -165,7 +169,9 @@ def run_e2e(r: Runner, raws, views, ingest: str, warmup: int, steps: int, sync):
                 sealed = time.perf_counter()
                 raw = raws[i % len(raws)]
                 hb = views[slot]
-                if ingest == "utf16":
+                if ingest == "utf8":
+                    hb.load_utf8(raw, u8s[i % len(raws)], copy_text=False)
+                elif ingest == "utf16":
                     hb.load_utf16(raw, copy_text=False)
                 else:
                     hb.load(raw, "wire")
@@ -201,10 +207,11 @@ def run_e2e(r: Runner, raws, views, ingest: str, warmup: int, steps: int, sync):
 
 def main(argv=None) -> int:
     args = parse_args(argv)
+    args.e2e = not args.prepacked
     import torch  # noqa: F401  (binds the HIP runtime before the engine loads)
     from twitter_stream_ml_amd.parallel import dist as D
     from twitter_stream_ml_amd.ops.lr_engine import (DeviceLinearRegression, HostBatchView,
-                                                     LRDeviceConfig, register_host)
+                                                     LRDeviceConfig, encode_utf8, register_host)
     from twitter_stream_ml_amd.sources.synthetic import SynthConfig, generate_batch
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
@@ -220,7 +227,7 @@ def main(argv=None) -> int:
     from twitter_stream_ml_amd.parallel.affinity import bind_local_numa
     numa_cpus = bind_local_numa(device)   # before the pinned pool is allocated
     comm = D.make_comm(device, args.comm)
-    ingest = args.ingest or "utf16"
+    ingest = args.ingest or "utf8"
 
     B = args.batch
     synth = SynthConfig.profile(args.profile, seed=args.seed + 7919 * info.rank)
@@ -241,9 +248,14 @@ def main(argv=None) -> int:
                              sgd_grid=args.sgd_grid, ablate=args.ablate, tol=args.tol, dedup=bool(args.dedup),
                              hybrid=bool(args.hybrid), ingest=ingest if args.e2e else "wire")
         eng = DeviceLinearRegression(cfg, device=device, comm=comm)
+    u8s = []
     if args.e2e:
         views = [HostBatchView(B, max_units) for _ in range(eng.raw_slots)]
-        if ingest == "utf16":
+        if ingest == "utf8":   # the receiver's UTF-8 buffers (as the network delivered them)
+            u8s = [encode_utf8(r) for r in pool_raw]
+            for u in u8s:
+                register_host(u.data)
+        elif ingest == "utf16":
             for r in pool_raw:   # the receiver's buffers: DMA source of the text
                 register_host(r.text)
     else:
@@ -265,7 +277,7 @@ def main(argv=None) -> int:
         return t0, t1
 
     if args.e2e:
-        t0, t1 = run_e2e(runner, pool_raw, views, ingest, args.warmup, args.steps, sync)
+        t0, t1 = run_e2e(runner, pool_raw, u8s, views, ingest, args.warmup, args.steps, sync)
     else:
         t0, t1 = run_device_pipeline(runner, pool, args.warmup, args.steps, sync)
     elapsed = D.allreduce_max_scalar(t1 - t0)

@@ -204,7 +204,24 @@ PYBIND11_MODULE(_twtml_hip, m) {
            py::arg("copy_text") = true, py::arg("threads") = 0,
            "Stage a raw UTF-16 batch (row words, offsets, packed scalars; text copied only if "
            "copy_text); returns the text bytes.")
+      .def("load_utf8",
+           [](HostBatch& h, py::array_t<uint8_t, py::array::c_style> text,
+              py::array_t<int64_t, py::array::c_style> offsets, py::array_t<uint8_t, py::array::c_style> is_rt,
+              py::array_t<int64_t, py::array::c_style> scalars, bool copy_text, int threads) {
+             const int64_t n = int64_t(offsets.size()) - 1;
+             if (n < 0 || is_rt.size() < n || scalars.size() < 5 * n)
+               throw std::invalid_argument("load_utf8: offsets / is_rt / scalars mismatch");
+             if (n > 0 && offsets.data()[n] > text.size()) throw std::invalid_argument("offsets exceed text");
+             py::gil_scoped_release nogil;
+             h.load_utf8(text.data(), offsets.data(), is_rt.data(), scalars.data(), n, copy_text, threads);
+             return n > 0 ? offsets.data()[n] : int64_t(0);
+           },
+           py::arg("text"), py::arg("offsets"), py::arg("is_rt"), py::arg("scalars"),
+           py::arg("copy_text") = true, py::arg("threads") = 0,
+           "Stage a raw UTF-8 batch (row words, offsets, packed scalars; text copied only if "
+           "copy_text); returns the text bytes.")
       .def_readonly("utf16", &HostBatch::utf16)
+      .def_readonly("utf8", &HostBatch::utf8)
       .def_readonly("rowpacked_n", &HostBatch::rowpacked_n)
       .def_readonly("wide_rows", &HostBatch::wide_rows)
       .def_property_readonly("scalar_wire", [](const HostBatch& h) {

@@ -101,17 +101,22 @@ bool HostBatch::pack_rows(int64_t n) {
   cesu_rows = cesu;
   wide_rows = wide;
   utf16 = false;
+  utf8 = false;
   rows_scanned_n = n;
   if (fits) rowpacked_n = n;
   return fits;
 }
 
-void HostBatch::load_utf16(const uint16_t* t, const int64_t* uoff, const uint8_t* is_rt, const int64_t* sc,
-                           int64_t n, bool copy_text, int threads) {
-  if (n < 0 || n > max_rows) throw std::invalid_argument("load_utf16: bad row count");
-  const int64_t bytes = n > 0 ? 2 * (uoff[n] - uoff[0]) : 0;
-  if (copy_text && bytes > max_bytes) throw std::invalid_argument("load_utf16: text exceeds staging capacity");
-  if (n > 0 && uoff[0] != 0) throw std::invalid_argument("load_utf16: offsets must start at 0");
+// Raw staging shared by the UTF-16 and UTF-8 ingest modes: row words
+// (byte length | flags), offsets, packed scalars, and optionally the text.
+// `scale` is the bytes per offset unit (2: UTF-16 units, 1: UTF-8 bytes),
+// `row_flags` the wire flags every row carries besides the retweet bit.
+void HostBatch::load_raw(const uint8_t* t, const int64_t* uoff, int64_t scale, uint8_t row_flags,
+                         const uint8_t* is_rt, const int64_t* sc, int64_t n, bool copy_text, int threads) {
+  if (n < 0 || n > max_rows) throw std::invalid_argument("load: bad row count");
+  const int64_t bytes = n > 0 ? scale * (uoff[n] - uoff[0]) : 0;
+  if (copy_text && bytes > max_bytes) throw std::invalid_argument("load: text exceeds staging capacity");
+  if (n > 0 && uoff[0] != 0) throw std::invalid_argument("load: offsets must start at 0");
   rowpacked_n = -1;
   rowpack = reinterpret_cast<uint16_t*>(text - rowpack_prefix(n));
   if (threads <= 0) threads = int(std::min<unsigned>(8, std::max(1u, std::thread::hardware_concurrency())));
@@ -121,17 +126,17 @@ void HostBatch::load_utf16(const uint16_t* t, const int64_t* uoff, const uint8_t
     const int64_t r0 = n * c / T, r1 = n * (c + 1) / T;
     bool ok = true;
     for (int64_t i = r0; i < r1; ++i) {
-      const int64_t len = 2 * (uoff[i + 1] - uoff[i]);
-      const uint8_t f = uint8_t((is_rt[i] ? kRowRetweet : 0) | kRowWide);
-      offsets[i + 1] = 2 * uoff[i + 1];
+      const int64_t len = scale * (uoff[i + 1] - uoff[i]);
+      const uint8_t f = uint8_t((is_rt[i] ? kRowRetweet : 0) | row_flags);
+      offsets[i + 1] = scale * uoff[i + 1];
       flags[i] = f;
       if (len < 0 || len >= (int64_t(1) << kRowLenBits)) ok = false;
       else rowpack[i] = uint16_t(len | (int64_t(f) << kRowLenBits));
     }
     fit[size_t(c)] = ok ? 1 : 0;
     if (copy_text) {   // this thread's share of the text bytes
-      const int64_t b0 = 2 * uoff[r0], b1 = 2 * uoff[r1];
-      if (b1 > b0) std::memcpy(text + b0, reinterpret_cast<const uint8_t*>(t) + b0, size_t(b1 - b0));
+      const int64_t b0 = scale * uoff[r0], b1 = scale * uoff[r1];
+      if (b1 > b0) std::memcpy(text + b0, t + b0, size_t(b1 - b0));
     }
   };
   std::vector<std::thread> th;
@@ -140,13 +145,31 @@ void HostBatch::load_utf16(const uint16_t* t, const int64_t* uoff, const uint8_t
   for (auto& x : th) x.join();
   offsets[0] = 0;
   pack_scalars(n, sc);
-  cesu_rows = 0;
-  wide_rows = n;
-  utf16 = true;
   rows_scanned_n = n;
   bool all = true;
   for (auto f : fit) all = all && f;
   if (all) rowpacked_n = n;
+}
+
+void HostBatch::load_utf16(const uint16_t* t, const int64_t* uoff, const uint8_t* is_rt, const int64_t* sc,
+                           int64_t n, bool copy_text, int threads) {
+  load_raw(reinterpret_cast<const uint8_t*>(t), uoff, 2, kRowWide, is_rt, sc, n, copy_text, threads);
+  cesu_rows = 0;
+  wide_rows = n;
+  utf16 = true;
+  utf8 = false;
+}
+
+// UTF-8 as the network delivers tweet text: every row is flagged cesu (the
+// device decoder handles UTF-8, incl. 4-byte sequences); the device keeps
+// ASCII rows as they are and narrows decoded Latin-1 rows.
+void HostBatch::load_utf8(const uint8_t* t, const int64_t* boff, const uint8_t* is_rt, const int64_t* sc,
+                          int64_t n, bool copy_text, int threads) {
+  load_raw(t, boff, 1, kRowCesu, is_rt, sc, n, copy_text, threads);
+  cesu_rows = n;
+  wide_rows = 0;
+  utf16 = false;
+  utf8 = true;
 }
 
 HostBatch::~HostBatch() {

@@ -71,6 +71,8 @@ struct HostBatch {
                                        // special lower-casing, rows.hip)
   bool utf16 = false;                  // text is plain UTF-16LE (load_utf16): the device narrows
                                        // Latin-1 rows itself
+  bool utf8 = false;                   // text is UTF-8 (load_utf8): the device decodes non-ASCII
+                                       // rows and narrows the Latin-1 ones
   int64_t rows_scanned_n = -1;         // rows of the last pack_rows call (fit or not)
   int64_t max_rows = 0, max_bytes = 0;
   HostBatch(int64_t rows, int64_t text_bytes);
@@ -84,15 +86,26 @@ struct HostBatch {
   // the device narrows Latin-1 rows and lowers special rows (rows.hip).
   void load_utf16(const uint16_t* t, const int64_t* uoff, const uint8_t* is_rt, const int64_t* sc,
                   int64_t n, bool copy_text, int threads);
+  // Raw UTF-8 ingest (the bytes the network delivers): same contract with
+  // byte offsets boff [n+1].  ~1.1 B per unit of tweet text on PCIe and no
+  // per-byte host work: the device decodes (k_cesu_decode) and narrows.
+  void load_utf8(const uint8_t* t, const int64_t* boff, const uint8_t* is_rt, const int64_t* sc,
+                 int64_t n, bool copy_text, int threads);
   // Offsets + flags of rows [0, n) as one u16 per row (the device rebuilds
   // both with a scan): 9 -> 2 bytes per row on PCIe.  False (and the batch
   // ships offsets + flags as before) if a row has >= 8192 wire bytes.
   // Also counts the cesu rows (either way).
   bool pack_rows(int64_t n);
+
+ private:
+  void load_raw(const uint8_t* t, const int64_t* off, int64_t scale, uint8_t row_flags, const uint8_t* is_rt,
+                const int64_t* sc, int64_t n, bool copy_text, int threads);
 };
 
-// bytes of device text buffer for `units` UTF-16 units (all rows wide)
-inline int64_t text_bytes_for_units(int64_t units) { return 2 * units + 64; }
+// bytes of device text buffer for `units` UTF-16 units: all rows wide (2 B
+// per unit) or UTF-8 (<= 3 B per unit: a BMP unit >= U+0800; an astral pair
+// is 4 B for 2 units)
+inline int64_t text_bytes_for_units(int64_t units) { return 3 * units + 64; }
 
 struct BatchResult {
   int64_t n_raw = 0, n_kept = 0, n_kept_global = 0, n_unique = 0, entries = 0;

@@ -236,16 +236,32 @@ void launch_unpack_rows(const uint16_t* rowpack, int64_t n, int64_t* offsets, ui
 }
 
 // ---------------------------------------------------------------------------
-// cesu wire rows (csrc/host/wire.h) -> UTF-16LE rows after the wire bytes.
-// A row of B wire bytes has at most B units, so it expands into
-// [tail + 2 * start, tail + 2 * end): no count or scan pass.  A wave takes
-// 64 rows; lane l owns row l's offsets / flags, and the wave walks the cesu
-// rows among them (ballot) together: 64 bytes per step, a unit starts at
-// every non-continuation byte, its index is the running count plus a
-// popcount of the lead-byte mask below the lane.
+// cesu wire rows (csrc/host/wire.h) and UTF-8 rows (load_utf8) -> UTF-16LE
+// rows after the wire bytes.  A row of B wire bytes has at most B units (a
+// 4-byte UTF-8 sequence is 2 units), so it expands into
+// [tail + 2 * start, tail + 2 * end): no count or scan pass.  A wave takes 64
+// rows; lane l owns row l's offsets / flags, and the wave walks the flagged
+// rows among them (ballot) together.  An all-ASCII row (UTF-8 ingest: most
+// tweets) is only checked -- 4 bytes per lane per step -- and stays a narrow
+// row in place.  Otherwise 64 bytes per step: a unit starts at every
+// non-continuation byte (two at a 4-byte lead: the surrogate pair), its index
+// is the running count plus popcounts of the lead masks below the lane.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t lanes_below() {
   return (uint64_t(1) << lane_id()) - 1u;
+}
+
+__device__ __forceinline__ bool row_is_ascii(const uint8_t* text, int64_t o, int64_t e) {
+  // aligned dwords covering [o, e), bytes outside the row masked off
+  const int64_t a0 = o & ~int64_t(3);
+  uint32_t acc = 0;
+  for (int64_t w = a0 + 4 * lane_id(); w < e; w += 4 * kWave) {
+    uint32_t v = *reinterpret_cast<const uint32_t*>(text + w);
+    if (w < o) v &= 0xFFFFFFFFu << (8 * (o - w));
+    if (w + 4 > e) v &= 0xFFFFFFFFu >> (8 * (w + 4 - e));
+    acc |= v;
+  }
+  return !__any((acc & 0x80808080u) != 0u);
 }
 
 __global__ __launch_bounds__(256) void k_cesu_decode(uint8_t* text, const int64_t* offsets, uint8_t* flags,
@@ -255,7 +271,7 @@ __global__ __launch_bounds__(256) void k_cesu_decode(uint8_t* text, const int64_
   const int64_t nwaves = int64_t(gridDim.x) * 256 / kWave;
   for (int64_t g = wave; g * kWave < n; g += nwaves) {
     const int64_t r = g * kWave + lane;
-    const uint8_t fl = r < n ? flags[r] : 0;
+    uint8_t fl = r < n ? flags[r] : 0;
     const bool mine = r < n && (fl & kRowCesu);
     int64_t s0 = r < n ? offsets[r] : 0, s1 = r < n ? offsets[r + 1] : 0;
     uint64_t m = __ballot(mine);
@@ -264,6 +280,10 @@ __global__ __launch_bounds__(256) void k_cesu_decode(uint8_t* text, const int64_
       m &= m - 1;
       const int64_t rr = g * kWave + l;
       const int64_t o = offsets[rr], e = offsets[rr + 1];
+      if (row_is_ascii(text, o, e)) {   // narrow row as it is
+        if (lane == l) fl = uint8_t(fl & ~kRowCesu);
+        continue;
+      }
       const int64_t d0 = tail + 2 * o;
       uint16_t* dst = reinterpret_cast<uint16_t*>(text + d0);
       int64_t k = 0;
@@ -271,24 +291,35 @@ __global__ __launch_bounds__(256) void k_cesu_decode(uint8_t* text, const int64_
         const int64_t i = i0 + lane;
         const uint32_t b0 = i < e ? text[i] : 0x80u;
         const bool lead = i < e && (b0 & 0xC0u) != 0x80u;
-        const uint64_t lm = __ballot(lead);
+        const bool four = lead && b0 >= 0xF0u;
+        const uint64_t lm = __ballot(lead), fm = __ballot(four);
         if (lead) {
+          const int64_t at = k + __popcll(lm & lanes_below()) + __popcll(fm & lanes_below());
           uint32_t u = b0;
-          if (b0 >= 0xE0u) u = ((b0 & 0x0Fu) << 12) | ((text[i + 1] & 0x3Fu) << 6) | (text[i + 2] & 0x3Fu);
-          else if (b0 >= 0x80u) u = ((b0 & 0x1Fu) << 6) | (text[i + 1] & 0x3Fu);
-          dst[k + __popcll(lm & lanes_below())] = uint16_t(u);
+          if (four) {
+            const uint32_t cp = ((b0 & 0x07u) << 18) | ((text[i + 1] & 0x3Fu) << 12) |
+                                ((text[i + 2] & 0x3Fu) << 6) | (text[i + 3] & 0x3Fu);
+            dst[at] = uint16_t(0xD800u + ((cp - 0x10000u) >> 10));
+            u = 0xDC00u + ((cp - 0x10000u) & 0x3FFu);
+            dst[at + 1] = uint16_t(u);
+          } else {
+            if (b0 >= 0xE0u) u = ((b0 & 0x0Fu) << 12) | ((text[i + 1] & 0x3Fu) << 6) | (text[i + 2] & 0x3Fu);
+            else if (b0 >= 0x80u) u = ((b0 & 0x1Fu) << 6) | (text[i + 1] & 0x3Fu);
+            dst[at] = uint16_t(u);
+          }
         }
-        k += __popcll(lm);
+        k += __popcll(lm) + __popcll(fm);
       }
       if (lane == l) {
         s0 = d0;
         s1 = d0 + 2 * k;
+        fl = uint8_t((fl & ~kRowCesu) | kRowWide);
       }
     }
     if (r < n) {
       rstart[r] = s0;
       rend[r] = s1;
-      if (mine) flags[r] = uint8_t((fl & ~kRowCesu) | kRowWide);
+      if (mine) flags[r] = fl;
     }
   }
 }

@@ -113,6 +113,7 @@ void RawSlots::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, h
   s.cesu_rows = n > 0 ? hb.cesu_rows : 0;
   s.wide_rows = n > 0 ? hb.wide_rows : 0;
   s.utf16 = n > 0 && hb.utf16;
+  s.utf8 = n > 0 && hb.utf8;
   s.n = n;
   s.bytes = bytes;
   s.used = true;
@@ -136,9 +137,11 @@ DevRawBatch RawSlots::acquire(int slot, hipStream_t compute) {
   }
   TWTML_HIP_CHECK(hipMemsetAsync(s.nstats, 0, 2 * sizeof(int64_t), compute));
   if (s.utf16 || s.cesu_rows > 0 || s.wide_rows > 0) {
-    // special rows -> fully lower-cased UTF-16; UTF-16 batches: Latin-1 rows narrowed
+    // special rows -> fully lower-cased UTF-16; UTF-16 / UTF-8 batches: Latin-1
+    // rows narrowed (a decoded UTF-8 row in place: byte i <- unit i, forward)
     launch_row_normalize(s.text, s.offsets, b.offsets, b.oend, s.flags, s.rstart, s.rend, s.n, tail,
-                         tail + 2 * ((s.bytes + 15) / 16 * 16), s.utf16, case_, s.nstats, compute);
+                         tail + 2 * ((s.bytes + 15) / 16 * 16), s.utf16 || s.utf8, case_, s.nstats,
+                         compute);
     b.offsets = s.rstart;
     b.oend = s.rend;
   }

@@ -19,7 +19,7 @@ namespace twtml {
 
 struct HostBatch;
 
-constexpr int kRawSlots = 3;
+constexpr int kRawSlots = 4;
 
 class RawSlots {
  public:
@@ -65,7 +65,7 @@ class RawSlots {
     int64_t* rend = nullptr;
     int64_t cesu_rows = 0, wide_rows = 0;
     int64_t* nstats = nullptr;        // [2] rows lowered / narrowed by row_normalize
-    bool packed = false, utf16 = false;
+    bool packed = false, utf16 = false, utf8 = false;
     int64_t soff[kScalarCols] = {};
     int64_t sbase[kScalarCols] = {};
     uint8_t sw[kScalarCols] = {};

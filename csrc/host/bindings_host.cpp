@@ -121,6 +121,25 @@ PYBIND11_MODULE(_twtml_host, m) {
   });
 
   m.def("wire_bound", &wire_bound, py::arg("units"), py::arg("rows"));
+  m.def("utf8_bound", &utf8_bound, py::arg("units"));
+  m.def("utf8_encode",
+        [](Arr<uint16_t> text, Arr<int64_t> offsets, int threads) {
+          const int64_t n = int64_t(offsets.size()) - 1;
+          if (n < 0) throw std::invalid_argument("offsets must have n + 1 entries");
+          if (n > 0 && offsets.data()[n] > int64_t(text.size())) throw std::invalid_argument("offsets exceed text");
+          const int64_t units = n > 0 ? offsets.data()[n] : 0;
+          py::array_t<uint8_t> out(py::ssize_t(utf8_bound(units)));
+          py::array_t<int64_t> oo(py::ssize_t(n + 1));
+          int64_t total;
+          {
+            py::gil_scoped_release nogil;
+            total = utf8_encode(text.data(), offsets.data(), n, out.mutable_data(), int64_t(out.size()),
+                                oo.mutable_data(), threads);
+          }
+          return py::make_tuple(out[py::slice(0, total, 1)], oo);
+        },
+        py::arg("text"), py::arg("offsets"), py::arg("threads") = 0,
+        "UTF-16 rows -> (UTF-8 bytes, byte offsets [n+1]); astral pairs as 4 bytes, lone surrogates as 3.");
   m.def("wire_pack",
         [](Arr<uint16_t> text, Arr<int64_t> offsets, Arr<uint8_t> is_rt, py::array out,
            py::array out_offsets, py::array flags, int nthreads) {

@@ -156,4 +156,76 @@ void wire_unpack(const uint8_t* wire, const int64_t* woff, const uint8_t* flags,
   }
 }
 
+namespace {
+inline bool hi_sur(uint32_t u) { return u >= 0xD800u && u <= 0xDBFFu; }
+inline bool lo_sur(uint32_t u) { return u >= 0xDC00u && u <= 0xDFFFu; }
+
+// Encodes one row; out == nullptr only counts.
+int64_t utf8_row(const uint16_t* t, int64_t len, uint8_t* out) {
+  int64_t b = 0;
+  for (int64_t i = 0; i < len; ++i) {
+    const uint32_t u = t[i];
+    if (u < 0x80u) {
+      if (out) out[b] = uint8_t(u);
+      b += 1;
+    } else if (u < 0x800u) {
+      if (out) {
+        out[b] = uint8_t(0xC0u | (u >> 6));
+        out[b + 1] = uint8_t(0x80u | (u & 0x3Fu));
+      }
+      b += 2;
+    } else if (hi_sur(u) && i + 1 < len && lo_sur(t[i + 1])) {
+      const uint32_t cp = 0x10000u + ((u - 0xD800u) << 10) + (uint32_t(t[i + 1]) - 0xDC00u);
+      if (out) {
+        out[b] = uint8_t(0xF0u | (cp >> 18));
+        out[b + 1] = uint8_t(0x80u | ((cp >> 12) & 0x3Fu));
+        out[b + 2] = uint8_t(0x80u | ((cp >> 6) & 0x3Fu));
+        out[b + 3] = uint8_t(0x80u | (cp & 0x3Fu));
+      }
+      b += 4;
+      ++i;
+    } else {
+      if (out) {
+        out[b] = uint8_t(0xE0u | (u >> 12));
+        out[b + 1] = uint8_t(0x80u | ((u >> 6) & 0x3Fu));
+        out[b + 2] = uint8_t(0x80u | (u & 0x3Fu));
+      }
+      b += 3;
+    }
+  }
+  return b;
+}
+}  // namespace
+
+int64_t utf8_encode(const uint16_t* text, const int64_t* offsets, int64_t n, uint8_t* out, int64_t out_cap,
+                    int64_t* out_offsets, int threads) {
+  out_offsets[0] = 0;
+  if (n <= 0) return 0;
+  std::vector<int64_t> chunk_bytes(64 + 1, 0);
+  int used = 1;
+  parallel_chunks(n, threads, [&](int c, int T) {
+    used = T;
+    const int64_t r0 = n * c / T, r1 = n * (c + 1) / T;
+    int64_t pos = 0;
+    for (int64_t r = r0; r < r1; ++r) {
+      pos += utf8_row(text + offsets[r], offsets[r + 1] - offsets[r], nullptr);
+      out_offsets[r + 1] = pos;   // chunk-local end
+    }
+    chunk_bytes[size_t(c) + 1] = pos;
+  });
+  for (int c = 0; c < used; ++c) chunk_bytes[size_t(c) + 1] += chunk_bytes[size_t(c)];
+  const int64_t total = chunk_bytes[size_t(used)];
+  if (total > out_cap) throw std::length_error("utf8_encode: output buffer too small");
+  parallel_chunks(n, threads, [&](int c, int T) {
+    const int64_t r0 = n * c / T, r1 = n * (c + 1) / T;
+    const int64_t base = chunk_bytes[size_t(c)];
+    for (int64_t r = r0; r < r1; ++r) out_offsets[r + 1] += base;
+    for (int64_t r = r0; r < r1; ++r) {
+      const int64_t o = r == r0 ? base : out_offsets[r];
+      utf8_row(text + offsets[r], offsets[r + 1] - offsets[r], out + o);
+    }
+  });
+  return total;
+}
+
 }  // namespace twtml

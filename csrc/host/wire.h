@@ -39,4 +39,13 @@ void wire_unpack(const uint8_t* wire, const int64_t* woff, const uint8_t* flags,
 // Total UTF-16 units of a packed batch.
 int64_t wire_units(const uint8_t* wire, const int64_t* woff, const uint8_t* flags, int64_t n);
 
+// UTF-16 -> UTF-8 (what a network receiver holds: tweet JSON is UTF-8).
+// Surrogate pairs become 4-byte sequences; a lone surrogate is encoded as a
+// 3-byte sequence (WTF-8), so every unit sequence round-trips exactly through
+// the device decoder.  Two passes over row chunks (`threads` <= 0: auto);
+// out needs utf8_bound(units) bytes, out_offsets [n+1] byte offsets.
+inline int64_t utf8_bound(int64_t units) { return 3 * units + 64; }
+int64_t utf8_encode(const uint16_t* text, const int64_t* offsets, int64_t n, uint8_t* out, int64_t out_cap,
+                    int64_t* out_offsets, int threads);
+
 }  // namespace twtml

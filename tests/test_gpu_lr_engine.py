@@ -19,7 +19,8 @@ NOW = 1_700_000_000_000
 
 def _engine(F, hash="java", **kw):
     from twitter_stream_ml_amd.ops.lr_engine import DeviceLinearRegression, LRDeviceConfig
-    cfg = LRDeviceConfig(num_text_features=F, hash=hash, max_rows=8192, max_units=8192 * 300, **kw)
+    kw = {"max_rows": 8192, "max_units": 8192 * 300, **kw}
+    cfg = LRDeviceConfig(num_text_features=F, hash=hash, **kw)
     return DeviceLinearRegression(cfg, device=0)
 
 
@@ -57,11 +58,13 @@ def _with_long_row(raw, k=3, n_units=9000):
     (1000, "java", False, False, "wire"), (1 << 20, "java", False, False, "wire"),
     (1 << 20, "murmur3", False, False, "wire"), (1000, "java", True, False, "wire"),
     (1 << 20, "java", False, True, "wire"),
-    (1 << 20, "java", False, False, "utf16"), (1 << 20, "murmur3", True, True, "utf16")])
+    (1 << 20, "java", False, False, "utf16"), (1 << 20, "murmur3", True, True, "utf16"),
+    (1 << 20, "java", False, False, "utf8"), (1 << 20, "murmur3", True, True, "utf8")])
 def test_featurize_matches_oracle(hip_module, F, hash, wide, longrow, ingest):
     """Featurize == oracle; also covers the wire encodings: wide (int64)
     scalar columns and the plain-offsets fallback of a >= 16 KiB row, and
-    raw UTF-16 ingest (Latin-1 rows narrowed on the device).  Special rows
+    raw UTF-16 ingest (Latin-1 rows narrowed on the device) and raw UTF-8
+    ingest (non-ASCII rows decoded, 4-byte sequences included).  Special rows
     (5 %) are fully lower-cased on the device (rows.hip), not on the host."""
     cfg = SynthConfig.profile("twitter", seed=11, special_fraction=0.05, unicode_fraction=0.3)
     raw = generate_batch(cfg, 0, 3000, batch_time_ms=NOW)
@@ -119,7 +122,7 @@ _SPECIAL_TEXTS = [
 ]
 
 
-@pytest.mark.parametrize("ingest", ["wire", "utf16"])
+@pytest.mark.parametrize("ingest", ["wire", "utf16", "utf8"])
 def test_device_special_lowering(hip_module, ingest):
     """Rows whose lower-casing is not one unit per unit (U+0130 -> 2 units,
     Final_Sigma context incl. case-ignorables and astral neighbours, astral
@@ -149,6 +152,30 @@ def test_device_special_lowering(hip_module, ingest):
         s, e = Xt.indptr[k], Xt.indptr[k + 1]
         want = np.repeat(Xt.indices[s:e], Xt.data[s:e].astype(np.int64))
         np.testing.assert_array_equal(rows[k], np.sort(want), err_msg=f"row {k}: {texts[k]!r}")
+
+
+@pytest.mark.parametrize("profile,F,hash", [("twitter", 1 << 20, "java"), ("wide", 1 << 20, "java"),
+                                            ("wide", 100_000_000, "murmur3")])
+def test_utf8_ingest_trains_like_wire(hip_module, profile, F, hash):
+    """UTF-8 ingest (the receiver's bytes, decoded on the device) gives the
+    same featurization and row classes, hence the same training as the
+    host-packed wire format, batch after batch (up to the summation order:
+    rows of equal length are placed by atomics, so even two wire runs differ
+    in the last bits)."""
+    cfg = SynthConfig.profile(profile, seed=19, special_fraction=0.02)
+    engs = {k: _engine(F, hash, ingest=k, max_rows=20000, max_units=20000 * 300) for k in ("wire", "utf8")}
+    for t in range(3):
+        raw = generate_batch(cfg, t * 20000, 20000, batch_time_ms=NOW + t * 5000)
+        res = {k: e.train_batch(raw, want_pred=True) for k, e in engs.items()}
+        a, b = res["wire"], res["utf8"]
+        for key in ("n_kept", "n_unique", "iterations", "tiered", "rows_lowered"):
+            assert a[key] == b[key], (key, a[key], b[key])
+        np.testing.assert_allclose(b["stats"][:3], a["stats"][:3], rtol=1e-12)
+        np.testing.assert_allclose(b["stats"][3:], a["stats"][3:], rtol=1e-5)
+        pa, pb = np.asarray(a["pred"], np.float64), np.asarray(b["pred"], np.float64)
+        assert np.mean(pa != pb) < 1e-3 and np.all(np.abs(pa - pb) <= 1.0)
+    wa, wb = engs["wire"].get_weights(), engs["utf8"].get_weights()
+    np.testing.assert_allclose(wb, wa, rtol=1e-4, atol=1e-6 * max(np.abs(wa).max(), 1e-12))
 
 
 @pytest.mark.parametrize("F,dedup,hybrid", [(1000, False, True), (1 << 20, False, True),

@@ -27,7 +27,7 @@ from ._native import hip, host
 from .ingest import SlotPipeline
 
 __all__ = ["LRDeviceConfig", "DeviceLinearRegression", "prelower", "HostBatchView", "register_host",
-           "unregister_host"]
+           "unregister_host", "Utf8Text", "encode_utf8"]
 
 
 def prelower(raw: RawBatch) -> RawBatch:
@@ -38,6 +38,25 @@ def prelower(raw: RawBatch) -> RawBatch:
         return raw
     text, offsets, _ = h.prelower_special_rows(raw.text, raw.offsets)
     return RawBatch(text, offsets, raw.is_retweet, raw.scalars, raw.batch_time_ms)
+
+
+@dataclass
+class Utf8Text:
+    """A batch's tweet text as UTF-8 bytes + byte offsets [n+1]: the form a
+    network receiver holds (the Twitter stream delivers UTF-8 JSON)."""
+    data: np.ndarray      # uint8 [bytes]
+    offsets: np.ndarray   # int64 [n + 1]
+
+    @property
+    def nbytes(self) -> int:
+        return int(self.offsets[-1]) if self.offsets.shape[0] else 0
+
+
+def encode_utf8(raw: RawBatch, threads: int = 0) -> Utf8Text:
+    """UTF-16 rows -> UTF-8 (astral pairs as 4 bytes, lone surrogates as 3:
+    exact round trip through the device decoder)."""
+    data, off = host().utf8_encode(raw.text, raw.offsets, int(threads))
+    return Utf8Text(np.asarray(data), np.asarray(off))
 
 
 @dataclass
@@ -69,7 +88,9 @@ class LRDeviceConfig:
     lazy_idx: bool = True
     # host staging: "wire" packs rows on the host (Latin-1 / cesu / UTF-16,
     # ~166 B per tweet on PCIe); "utf16" ships plain UTF-16 (~300 B per
-    # tweet) with no per-unit host work -- the device narrows Latin-1 rows
+    # tweet) with no per-unit host work -- the device narrows Latin-1 rows;
+    # "utf8" ships the receiver's UTF-8 bytes (~155 B per tweet) -- the
+    # device decodes non-ASCII rows and narrows the Latin-1 ones
     ingest: str = "wire"
 
     def as_dict(self) -> Dict[str, object]:
@@ -110,7 +131,8 @@ class HostBatchView:
 
     def __init__(self, max_rows: int, max_units: int):
         self.max_units = int(max_units)
-        self._hb = hip().HostBatch(int(max_rows), int(host().wire_bound(self.max_units, int(max_rows))))
+        cap = max(int(host().wire_bound(self.max_units, int(max_rows))), int(host().utf8_bound(self.max_units)))
+        self._hb = hip().HostBatch(int(max_rows), cap)
         self.text = self._hb.text
         self.offsets = self._hb.offsets
         self.flags = self._hb.flags
@@ -139,6 +161,8 @@ class HostBatchView:
     def load(self, raw: RawBatch, ingest: str = "wire") -> "HostBatchView":
         if ingest == "utf16":
             return self.load_utf16(raw, copy_text=True)
+        if ingest == "utf8":
+            return self.load_utf8(raw, encode_utf8(raw), copy_text=True)
         if ingest != "wire":
             raise ValueError(f"unknown ingest mode {ingest!r}")
         self._check(raw)
@@ -166,6 +190,24 @@ class HostBatchView:
         self.rows_packed = int(self._hb.rowpacked_n) == raw.n
         self.ext_text = 0 if copy_text else int(text.ctypes.data)
         self._ext_owner = None if copy_text else text   # keeps the DMA source alive
+        return self
+
+    def load_utf8(self, raw: RawBatch, u8: Utf8Text, copy_text: bool = True) -> "HostBatchView":
+        """Raw UTF-8 staging: row words (byte lengths) + scalars; the text is
+        copied, or (copy_text=False) DMA'd by ``submit`` straight from
+        ``u8.data`` -- register it with :func:`register_host`.  ``raw``
+        supplies the scalar columns, retweet flags and unit count."""
+        self._check(raw)
+        if u8.offsets.shape[0] != raw.n + 1:
+            raise ValueError("UTF-8 offsets do not match the batch")
+        sc = np.ascontiguousarray(raw.scalars, dtype=np.int64)
+        self.bytes = int(self._hb.load_utf8(u8.data, np.ascontiguousarray(u8.offsets, dtype=np.int64),
+                                            np.ascontiguousarray(raw.is_retweet, dtype=np.uint8), sc,
+                                            bool(copy_text)))
+        self.n, self.units, self.batch_time_ms = raw.n, raw.total_units, raw.batch_time_ms
+        self.rows_packed = int(self._hb.rowpacked_n) == raw.n
+        self.ext_text = 0 if copy_text else int(u8.data.ctypes.data)
+        self._ext_owner = None if copy_text else u8.data
         return self
 
     def as_raw(self) -> RawBatch:
