@@ -879,36 +879,45 @@ int sgd_partials(int64_t ns, bool u16, int grid) {
 // ---------------------------------------------------------------------------
 
 // ---------------------------------------------------------------------------
-// SimpleUpdater (fp64 master weights), one wave per column: lane j sums the
-// partial rows j, j + 64, ... (all loads in flight) and a DPP wave sum
-// gives the column (fixed order); 16 columns per 1024-thread workgroup, so
-// a ~1.4K-slot batch spreads over ~90 CUs instead of 23.
+// SimpleUpdater (fp64 master weights).  The partial rows are summed per
+// block of 64 columns: lane l owns column col0 + l, the 16 waves of the
+// workgroup take partial rows w, w + 16, ... (each load one coalesced 512-B
+// row segment, all of a wave's rows in flight), and wave 0 adds the 16 wave
+// sums in a fixed order -- deterministic, like every reduction here.  (The
+// previous one-wave-per-column form read each column with 64 scattered
+// 8-B loads: 20 us per iteration at 12.5K slots x 256 partial rows.)
 // nparts > 0: the column gradients are the sums of the partial rows (single
 // GPU); nparts == 0: g64 holds them (all-reduced, or the generic path).
 // ---------------------------------------------------------------------------
-constexpr int kUpdCols = 1024 / kWave;   // columns (waves) per workgroup
-constexpr int kPartLoads = 512;          // partial rows a lane loads at once
+constexpr int kUpdWaves = 1024 / kWave;   // waves per workgroup (partial-row split)
 
-__device__ __forceinline__ double part_col_wave(const DevSgd& d, int64_t col, int nparts) {
-  const int lane = lane_id();
-  const double* src = d.part + col;
-  const int64_t ps = d.pstride;
-  double a[kPartLoads / kWave];
-#pragma unroll
-  for (int q = 0; q < kPartLoads / kWave; ++q) {
-    const int g = lane + q * kWave;
-    a[q] = g < nparts ? src[int64_t(g) * ps] : 0.0;
+// Sum of partial rows for columns [col0, col0 + 64): returns lane's column
+// sum in wave 0 (other waves: 0).  Contains a block barrier.
+__device__ __forceinline__ double part_block_sum(const DevSgd& d, int64_t col0, int64_t ncols, int nparts,
+                                                 double (*red)[kWave]) {
+  const int lane = lane_id(), w = threadIdx.x / kWave;
+  const int64_t col = col0 + lane;
+  double acc = 0.0;
+  if (col < ncols) {
+    const double* src = d.part + col;
+    const int64_t ps = d.pstride;
+#pragma unroll 8
+    for (int g = w; g < nparts; g += kUpdWaves) acc += src[int64_t(g) * ps];
   }
+  red[w][lane] = acc;
+  __syncthreads();
   double t = 0.0;
-  for (int g0 = kPartLoads; g0 < nparts; g0 += kWave)   // grids beyond 512 (not launched today)
-    if (g0 + lane < nparts) t += src[int64_t(g0 + lane) * ps];
+  if (w == 0) {
 #pragma unroll
-  for (int q = 0; q < kPartLoads / kWave; ++q) t += a[q];
-  return wave_sum(t);
+    for (int k = 0; k < kUpdWaves; ++k) t += red[k][lane];
+  }
+  __syncthreads();   // red is reused by the next column block
+  return t;
 }
 
 __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int nparts) {
-  __shared__ double wsc[kUpdCols][2];
+  __shared__ double wsc[kUpdWaves][2];
+  __shared__ double red[kUpdWaves][kWave];
   __shared__ double m_sh;
   if (d.state[0] != 0.0) return;
   const int tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
@@ -932,10 +941,11 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
   const double m = m_sh;
   const double alpha = sp.step_size / sqrt(double(it));
   double ds = 0.0, ws = 0.0;
-  for (int64_t col = int64_t(blockIdx.x) * kUpdCols + w; col < ncols; col += int64_t(gridDim.x) * kUpdCols) {
-    double g = col <= ns ? d.g64[col] : 0.0;   // wave-uniform load
-    if (nparts > 0) g += part_col_wave(d, col, nparts);
-    if (lane == 0) {
+  for (int64_t col0 = int64_t(blockIdx.x) * kWave; col0 < ncols; col0 += int64_t(gridDim.x) * kWave) {
+    const double gp = nparts > 0 ? part_block_sum(d, col0, ncols, nparts, red) : 0.0;
+    const int64_t col = col0 + lane;
+    if (w == 0 && col < ncols) {
+      const double g = (col <= ns ? d.g64[col] : 0.0) + gp;
       if (col < hi) {
         if (m > 0.0) {
           const double step = alpha * (g / m);
@@ -958,7 +968,6 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
   // the fixed-point far gradient (k_far_grad / all-reduced), re-zeroed here
   const int64_t n_far = kNumNumeric + d.n_unique - d.far_base;
   if (n_far > 0) {
-    double fds = 0.0, fws = 0.0;
     const double inv_m = m > 0.0 ? 1.0 / m : 0.0;
     for (int64_t j = int64_t(blockIdx.x) * 1024 + tid; j < n_far; j += int64_t(gridDim.x) * 1024) {
       const double g = double((long long)d.gfix[j]) * kFarInv;
@@ -969,15 +978,13 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
         const double wn = d.wc64[col] - step;
         d.wc64[col] = wn;
         d.wc32[col] = float(wn);
-        fds += step * step;
-        fws += wn * wn;
+        ds += step * step;
+        ws += wn * wn;
       }
     }
-    fds = wave_sum(fds);
-    fws = wave_sum(fws);
-    ds += fds;   // lane 0 carries the wave's columns (fixed order)
-    ws += fws;
   }
+  ds = wave_sum(ds);   // fixed order within the wave, then across waves
+  ws = wave_sum(ws);
   if (lane == 0) {
     wsc[w][0] = ds;
     wsc[w][1] = ws;
@@ -986,7 +993,7 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
   double* rec = sgd_rec(d, it);
   if (tid < 2) {
     double t = 0.0;
-    for (int k = 0; k < kUpdCols; ++k) t += wsc[k][tid];
+    for (int k = 0; k < kUpdWaves; ++k) t += wsc[k][tid];
     rec[kRecHead + 2 * blockIdx.x + tid] = t;
   }
   if (blockIdx.x == 0 && tid == 0) {
@@ -1001,22 +1008,23 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
 }
 
 void launch_sgd_update(const DevSgd& d, const SgdParams& sp, int nparts, hipStream_t s) {
-  const int64_t tiles = (d.nl + kPartVals - kNumNumeric + kUpdCols - 1) / kUpdCols;
+  const int64_t tiles = (d.nl + kPartVals - kNumNumeric + kWave - 1) / kWave;
   const int64_t far_tiles = (kNumNumeric + d.n_unique - d.far_base + 1023) / 1024;
-  const int grid = int(std::min<int64_t>(std::max(tiles, far_tiles), kMaxUpdGrid));
+  const int grid = int(std::max<int64_t>(1, std::min<int64_t>(std::max(tiles, far_tiles), kMaxUpdGrid)));
   hipLaunchKernelGGL(k_sgd_update, dim3(grid), dim3(1024), 0, s, d, sp, nparts);
 }
 
 // Cross-workgroup reduction of the partial rows (DP: before the all-reduce)
-// into g64 (+ loss, sampled count, batch stats): one wave per column, fixed
-// summation order.
+// into g64 (+ loss, sampled count, batch stats): 64 columns per workgroup,
+// fixed summation order.
 __global__ __launch_bounds__(1024) void k_sgd_reduce(DevSgd d, SgdParams sp) {
+  __shared__ double red[kUpdWaves][kWave];
   if (d.state[0] != 0.0) return;
   const int64_t ncols = d.nl + kPartVals - kNumNumeric;
-  const int64_t col = int64_t(blockIdx.x) * kUpdCols + threadIdx.x / kWave;
-  if (col >= ncols) return;   // wave-uniform
-  const double v = part_col_wave(d, col, d.nparts);
-  if (lane_id() == 0) {
+  const int64_t col0 = int64_t(blockIdx.x) * kWave;
+  const double v = part_block_sum(d, col0, ncols, d.nparts, red);
+  const int64_t col = col0 + lane_id();
+  if (threadIdx.x < kWave && col < ncols) {
     if (col <= d.nl) d.g64[col] = v;                     // slots, then the loss at [nl]
     else if (col == d.nl + 1) *sgd_red_m(d, sp.iteration) = v;   // sampled row count
     else d.stats[col - d.nl - 2] += v;                   // batch stats (iteration 1)
@@ -1025,7 +1033,7 @@ __global__ __launch_bounds__(1024) void k_sgd_reduce(DevSgd d, SgdParams sp) {
 
 void launch_sgd_reduce(const DevSgd& d, const SgdParams& sp, hipStream_t s) {
   if (d.nparts <= 0) return;
-  const int grid = int((d.nl + kPartVals - kNumNumeric + kUpdCols - 1) / kUpdCols);
+  const int grid = int((d.nl + kPartVals - kNumNumeric + kWave - 1) / kWave);
   hipLaunchKernelGGL(k_sgd_reduce, dim3(grid), dim3(1024), 0, s, d, sp);
 }
 
