@@ -33,6 +33,7 @@ static LRConfig lr_config(const py::dict& d) {
   GET(end, int64_t) GET(require_retweet, int32_t) GET(range_filter, int32_t)
   GET(max_rows, int64_t) GET(max_units, int64_t) GET(sgd_grid, int32_t)
   GET(early_exit_depth, int32_t) GET(ablate, int32_t) GET(dedup, int32_t) GET(hybrid, int32_t) GET(lazy_idx, int32_t)
+  GET(overlap, int32_t)
 #undef GET
   return c;
 }
@@ -246,11 +247,13 @@ PYBIND11_MODULE(_twtml_hip, m) {
            }),
            py::arg("device"), py::arg("config"), py::arg("comm") = nullptr)
       .def("submit",
-           [](LREngine& e, const HostBatch& hb, int64_t n, int64_t bytes, int slot, uintptr_t ext_text) {
+           [](LREngine& e, const HostBatch& hb, int64_t n, int64_t bytes, int slot, uintptr_t ext_text,
+              int64_t now_ms) {
              py::gil_scoped_release nogil;
-             e.submit(hb, n, bytes, slot, reinterpret_cast<const uint8_t*>(ext_text));
+             e.submit(hb, n, bytes, slot, reinterpret_cast<const uint8_t*>(ext_text), now_ms);
            },
-           py::arg("host_batch"), py::arg("n"), py::arg("bytes"), py::arg("slot"), py::arg("ext_text") = 0)
+           py::arg("host_batch"), py::arg("n"), py::arg("bytes"), py::arg("slot"), py::arg("ext_text") = 0,
+           py::arg("now_ms") = 0)
       .def("process",
            [](LREngine& e, int slot, int64_t now_ms, bool want_pred) {
              BatchResult r;

@@ -191,16 +191,28 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
   if (cfg_.fraction <= 0.0 || cfg_.fraction > 1.0 + 1e-12)
     throw std::invalid_argument("miniBatchFraction must be in (0, 1]");
   if (const char* v = std::getenv("TWTML_FORCE_TIERED")) force_tiered_ = v[0] == '1';   // tests
+  world_ = comm_ ? comm_->world() : 1;
+  // Prepare-ahead needs the prep-stage collectives off the gradient
+  // communicator, so it runs on one GPU (DP ranks prepare in line).
+  overlap_ = world_ == 1 && cfg_.overlap != 0;
+  if (const char* v = std::getenv("TWTML_OVERLAP")) overlap_ = overlap_ && v[0] != '0';
   TWTML_HIP_CHECK(hipSetDevice(device_));
   hipDeviceProp_t prop;
   TWTML_HIP_CHECK(hipGetDeviceProperties(&prop, device_));
   num_cu_ = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-  TWTML_HIP_CHECK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
+  // the GD loop outranks the prepare-ahead of the next batch for free CUs
+  int lo = 0, hi = 0;
+  TWTML_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  TWTML_HIP_CHECK(hipStreamCreateWithPriority(&compute_, hipStreamNonBlocking, hi));
+  TWTML_HIP_CHECK(hipStreamCreateWithPriority(&pstream_, hipStreamNonBlocking, lo));
   TWTML_HIP_CHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
   raw_.init(cfg_.max_rows, text_bytes_for_units(cfg_.max_units));
   for (auto& e : ev_) TWTML_HIP_CHECK(hipEventCreate(&e));
   upload_lower_tables(compute_, &lower_page_, &lower_blocks_);
-  alloc_prepared();
+  near_cap_ = tier_near_cap();
+  if (const char* v = std::getenv("TWTML_NEAR_CAP"))   // tests / tuning: a smaller LDS tier
+    near_cap_ = std::max<int64_t>(64, std::min<int64_t>(near_cap_, std::atoll(v)));
+  for (int k = 0; k < (overlap_ ? 2 : 1); ++k) alloc_prepared(pb_[k]);
   const int64_t nw = num_weights();
   sgd_.F = cfg_.num_text_features;
   sgd_.w64 = dmalloc<double>(size_t(nw));
@@ -215,10 +227,6 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
   sgd_.wnorm_next = dmalloc<double>(1);
   TWTML_HIP_CHECK(hipMemset(sgd_.red64, 0, 4 * sizeof(double)));
   ensure_compact(4096);
-  const int world = comm_ ? comm_->world() : 1;
-  n_global_ = dmalloc<int64_t>(2 * size_t(world) + 2);
-  TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_counters_), (8 + 2 * size_t(world)) * sizeof(int64_t),
-                                hipHostMallocDefault));
   TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_out_),
                                 (32 + size_t(std::max(1, cfg_.num_iterations))) * sizeof(double),
                                 hipHostMallocDefault));
@@ -226,56 +234,78 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
                                 (2 + size_t(std::max(1, cfg_.num_iterations))) * sizeof(double),
                                 hipHostMallocMapped | hipHostMallocCoherent));
   TWTML_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&sgd_.host_flags), host_flags_, 0));
-  TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_norm_), 2 * sizeof(int64_t), hipHostMallocDefault));
   TWTML_HIP_CHECK(hipDeviceSynchronize());
+  if (overlap_) worker_ = std::thread([this] { prep_worker(); });
 }
 
-void LREngine::alloc_prepared() {
+void LREngine::alloc_prepared(PrepBuf& b) {
+  DevPrepared& p = b.dp;
   const int64_t R = cfg_.max_rows;
   const int64_t C = (R + kRowsPerChunk - 1) / kRowsPerChunk;
   const int64_t R16 = C * kRowsPerChunk;
   int64_t E = 2 * cfg_.max_units + 2 * C * kChunkStride + 65536;
   E = (E + kChunkStride - 1) / kChunkStride * kChunkStride;
-  prep_.cap_rows = R;
-  prep_.cap_rows16 = R16;
-  prep_.cap_chunks = C;
-  prep_.cap_entries = E;
-  prep_.kept = dmalloc<int64_t>(size_t(R));
-  prep_.nnz = dmalloc<int32_t>(size_t(R));
-  prep_.sorted = dmalloc<int32_t>(size_t(R));
-  prep_.blk = dmalloc<int64_t>(size_t(R / kBlock + 2));
-  prep_.hist = dmalloc<int64_t>(kLenBuckets + 1);
-  prep_.clen8 = dmalloc<int32_t>(size_t(C) + 1);
-  prep_.cfast = dmalloc<uint8_t>(size_t(C) + 1);
-  prep_.clen8d = dmalloc<int32_t>(size_t(C) + 1);
-  prep_.cnt = dmalloc<uint16_t>(size_t(E));
-  prep_.cslot = dmalloc<uint16_t>(size_t(E));
-  prep_.hot_dense = dmalloc<uint32_t>(size_t(C) * kWave * 4);
-  prep_.clen8c = dmalloc<int32_t>(size_t(C) + 1);
-  prep_.hot_slot = dmalloc<int32_t>(kHot);
-  prep_.hot_of = dmalloc<uint8_t>(kMaxHybridSlots);
-  prep_.slot_hist = dmalloc<uint32_t>(kMaxHybridSlots);
-  slot_hist_cap_ = kMaxHybridSlots;
-  prep_.code = dmalloc<uint16_t>(8192);
-  prep_.cbase = dmalloc<int64_t>(size_t(C) + 1);
-  prep_.idx = dmalloc<int32_t>(size_t(E));
-  prep_.slot = dmalloc<uint32_t>(size_t(E));
-  prep_.y = dmalloc<float>(size_t(R16));
-  prep_.num = dmalloc<float>(4 * size_t(R16));
-  prep_.perm = dmalloc<int32_t>(size_t(R16));
-  prep_.rtext = dmalloc<int64_t>(size_t(R16));
-  prep_.scan_tmp = dmalloc<int64_t>(size_t(C) / 8192 + 2);
+  p.cap_rows = R;
+  p.cap_rows16 = R16;
+  p.cap_chunks = C;
+  p.cap_entries = E;
+  p.kept = dmalloc<int64_t>(size_t(R));
+  p.nnz = dmalloc<int32_t>(size_t(R));
+  p.sorted = dmalloc<int32_t>(size_t(R));
+  p.blk = dmalloc<int64_t>(size_t(R / kBlock + 2));
+  p.hist = dmalloc<int64_t>(kLenBuckets + 1);
+  p.clen8 = dmalloc<int32_t>(size_t(C) + 1);
+  p.cfast = dmalloc<uint8_t>(size_t(C) + 1);
+  p.clen8d = dmalloc<int32_t>(size_t(C) + 1);
+  p.cnt = dmalloc<uint16_t>(size_t(E));
+  p.cslot = dmalloc<uint16_t>(size_t(E));
+  p.hot_dense = dmalloc<uint32_t>(size_t(C) * kWave * 4);
+  p.clen8c = dmalloc<int32_t>(size_t(C) + 1);
+  p.hot_slot = dmalloc<int32_t>(kHot);
+  p.hot_of = dmalloc<uint8_t>(kMaxHybridSlots);
+  p.slot_hist = dmalloc<uint32_t>(kMaxHybridSlots);
+  b.slot_hist_cap = kMaxHybridSlots;
+  p.code = dmalloc<uint16_t>(8192);
+  p.cbase = dmalloc<int64_t>(size_t(C) + 1);
+  p.idx = dmalloc<int32_t>(size_t(E));
+  p.slot = dmalloc<uint32_t>(size_t(E));
+  p.y = dmalloc<float>(size_t(R16));
+  p.num = dmalloc<float>(4 * size_t(R16));
+  p.perm = dmalloc<int32_t>(size_t(R16));
+  p.rtext = dmalloc<int64_t>(size_t(R16));
+  p.scan_tmp = dmalloc<int64_t>(size_t(C) / 8192 + 2);
   // active-feature flags: Java-hash bigrams are < 2^21 whatever F is
   const int64_t F = cfg_.num_text_features;
   int64_t fl = cfg_.hash_kind == 0 ? std::min<int64_t>(F, int64_t(1) << 21) : F;
   fl = (fl + 4095) / 4096 * 4096;
-  prep_.flag_len = fl;
-  prep_.flags = dmalloc<uint8_t>(size_t(fl));
-  TWTML_HIP_CHECK(hipMemset(prep_.flags, 0, size_t(fl)));
-  prep_.uniq = dmalloc<int32_t>(size_t(fl));
-  prep_.slot_of = dmalloc<int32_t>(size_t(fl));
-  prep_.ublk = dmalloc<int64_t>(size_t(fl / 4096) + 2);
-  prep_.counters = dmalloc<int64_t>(8);
+  p.flag_len = fl;
+  p.flags = dmalloc<uint8_t>(size_t(fl));
+  TWTML_HIP_CHECK(hipMemset(p.flags, 0, size_t(fl)));
+  p.uniq = dmalloc<int32_t>(size_t(fl));
+  p.slot_of = dmalloc<int32_t>(size_t(fl));
+  p.ublk = dmalloc<int64_t>(size_t(fl / 4096) + 2);
+  p.counters = dmalloc<int64_t>(8);
+  b.n_global = dmalloc<int64_t>(2 * size_t(world_) + 2);
+  TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&b.host_counters),
+                                (8 + 2 * size_t(world_)) * sizeof(int64_t), hipHostMallocDefault));
+  TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&b.host_norm), 2 * sizeof(int64_t), hipHostMallocDefault));
+  TWTML_HIP_CHECK(hipEventCreate(&b.ev_start));
+  TWTML_HIP_CHECK(hipEventCreate(&b.ev_done));
+}
+
+void LREngine::free_prepared(PrepBuf& b) {
+  DevPrepared& p = b.dp;
+  void* bufs[] = {p.kept, p.nnz, p.sorted, p.blk, p.hist, p.clen8, p.cfast, p.clen8d, p.cnt, p.cslot,
+                  p.hot_dense, p.clen8c, p.hot_slot, p.hot_of, p.slot_hist, p.code, p.cbase, p.idx, p.slot,
+                  p.y, p.num, p.perm, p.rtext, p.scan_tmp, p.flags, p.uniq, p.slot_of, p.ublk, p.counters,
+                  p.fslot, p.fcount, p.fhist, p.fcur, p.fcsc_pos, p.fcsc_slot, p.newslot, p.slot_fid, p.tscan,
+                  p.tscan_blk, p.hist_near, p.tparam, b.n_global, b.ugather};
+  for (void* x : bufs) if (x) (void)hipFree(x);
+  if (b.host_counters) (void)hipHostFree(b.host_counters);
+  if (b.host_norm) (void)hipHostFree(b.host_norm);
+  if (b.ev_start) (void)hipEventDestroy(b.ev_start);
+  if (b.ev_done) (void)hipEventDestroy(b.ev_done);
+  b = PrepBuf{};
 }
 
 // Host side of the early stop: spin (with back-off) on the zero-copy verdict
@@ -298,36 +328,37 @@ double LREngine::wait_flag(int j) {
   return v;
 }
 
-// Tiered-layout buffers: per-batch arrays of the nU compact slots (grown on
-// demand) and, at the first tiered batch, the entry-sized far lists / CSC.
-void LREngine::ensure_tier(int64_t n_unique) {
-  if (!prep_.fslot) {
-    const size_t E = size_t(prep_.cap_entries);
-    prep_.fslot = dmalloc<uint32_t>(E);
-    prep_.fcsc_pos = dmalloc<uint32_t>(E);
-    prep_.fcsc_slot = dmalloc<uint32_t>(E);
-    prep_.fcount = dmalloc<int32_t>(size_t(prep_.cap_chunks) + 1);
-    prep_.hist_near = dmalloc<uint32_t>(kMaxHybridSlots);
-    prep_.tparam = dmalloc<int64_t>(4);
-    sgd_.rbuf = dmalloc<float>(size_t(prep_.cap_rows16));
+// Tiered-layout buffers of a prepared batch: arrays of the nU compact slots
+// (grown on demand) and, at its first tiered batch, the entry-sized far
+// lists / CSC.  The residual buffer of the far backward is the trainer's.
+void LREngine::ensure_tier(PrepBuf& b, int64_t n_unique, hipStream_t s) {
+  DevPrepared& p = b.dp;
+  if (!p.fslot) {
+    const size_t E = size_t(p.cap_entries);
+    p.fslot = dmalloc<uint32_t>(E);
+    p.fcsc_pos = dmalloc<uint32_t>(E);
+    p.fcsc_slot = dmalloc<uint32_t>(E);
+    p.fcount = dmalloc<int32_t>(size_t(p.cap_chunks) + 1);
+    p.hist_near = dmalloc<uint32_t>(kMaxHybridSlots);
+    p.tparam = dmalloc<int64_t>(4);
   }
-  if (n_unique <= prep_.cap_tier) return;
-  TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
-  void* old[] = {prep_.newslot, prep_.slot_fid, prep_.tscan, prep_.tscan_blk, prep_.fhist, prep_.fcur};
-  for (void* p : old) if (p) (void)hipFree(p);
-  const int64_t cap = std::max<int64_t>(n_unique, prep_.cap_tier * 2);
-  prep_.cap_tier = cap;
-  prep_.newslot = dmalloc<int32_t>(size_t(cap));
-  prep_.slot_fid = dmalloc<int32_t>(size_t(cap) + kNumNumeric + 2 * kPadSlots);
-  prep_.tscan = dmalloc<int64_t>(size_t(cap) + 1 + 2048);   // + 4096 u32 count buckets
-  prep_.tscan_blk = dmalloc<int64_t>(size_t(cap) / 8192 + 4);
-  prep_.fhist = dmalloc<uint64_t>(size_t(cap) + 1);
-  prep_.fcur = dmalloc<uint64_t>(size_t(cap) + 1);
-  if (cap + kNumNumeric + 64 > slot_hist_cap_) {
-    (void)hipFree(prep_.slot_hist);
-    slot_hist_cap_ = cap + kNumNumeric + 64;
-    prep_.slot_hist = dmalloc<uint32_t>(size_t(slot_hist_cap_));
-    TWTML_HIP_CHECK(hipMemset(prep_.slot_hist, 0, sizeof(uint32_t) * size_t(slot_hist_cap_)));
+  if (n_unique <= p.cap_tier) return;
+  TWTML_HIP_CHECK(hipStreamSynchronize(s));
+  void* old[] = {p.newslot, p.slot_fid, p.tscan, p.tscan_blk, p.fhist, p.fcur};
+  for (void* x : old) if (x) (void)hipFree(x);
+  const int64_t cap = std::max<int64_t>(n_unique, p.cap_tier * 2);
+  p.cap_tier = cap;
+  p.newslot = dmalloc<int32_t>(size_t(cap));
+  p.slot_fid = dmalloc<int32_t>(size_t(cap) + kNumNumeric + 2 * kPadSlots);
+  p.tscan = dmalloc<int64_t>(size_t(cap) + 1 + 2048);   // + 4096 u32 count buckets
+  p.tscan_blk = dmalloc<int64_t>(size_t(cap) / 8192 + 4);
+  p.fhist = dmalloc<uint64_t>(size_t(cap) + 1);
+  p.fcur = dmalloc<uint64_t>(size_t(cap) + 1);
+  if (cap + kNumNumeric + 64 > b.slot_hist_cap) {
+    (void)hipFree(p.slot_hist);
+    b.slot_hist_cap = cap + kNumNumeric + 64;
+    p.slot_hist = dmalloc<uint32_t>(size_t(b.slot_hist_cap));
+    TWTML_HIP_CHECK(hipMemset(p.slot_hist, 0, sizeof(uint32_t) * size_t(b.slot_hist_cap)));
   }
 }
 
@@ -361,79 +392,85 @@ void LREngine::ensure_compact(int64_t ns) {
 }
 
 LREngine::~LREngine() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  if (worker_.joinable()) worker_.join();
   (void)hipSetDevice(device_);
   (void)hipDeviceSynchronize();
   raw_.release();
   for (auto& e : ev_) (void)hipEventDestroy(e);
-  void* bufs[] = {prep_.kept, prep_.nnz, prep_.sorted, prep_.blk, prep_.hist, prep_.clen8, prep_.cfast,
-                  prep_.clen8d, prep_.cnt, prep_.cslot, prep_.hot_dense, prep_.clen8c,
-                  prep_.hot_slot, prep_.hot_of, prep_.slot_hist, prep_.code,
-                  prep_.cbase, prep_.idx, prep_.slot, prep_.y, prep_.num, prep_.perm, prep_.rtext, prep_.scan_tmp,
-                  prep_.flags, prep_.uniq, prep_.slot_of, prep_.ublk, prep_.counters,
-                  prep_.fslot, prep_.fcount, prep_.fhist, prep_.fcur, prep_.fcsc_pos, prep_.fcsc_slot,
-                  prep_.newslot, prep_.slot_fid, prep_.tscan, prep_.tscan_blk, prep_.hist_near, prep_.tparam,
-                  sgd_.gfix, sgd_.rbuf,
-                  sgd_.w64, sgd_.wc64, sgd_.wc32, sgd_.g64, sgd_.red64, sgd_.stats, sgd_.state,
-                  sgd_.loss_hist, sgd_.pred_out, sgd_.nrm, sgd_.wnorm_next, sgd_.part, sgd_.itrec, iter_tdbg_, lower_page_, lower_blocks_, n_global_,
-                  ugather_};
+  for (auto& b : pb_) free_prepared(b);
+  void* bufs[] = {sgd_.gfix, sgd_.rbuf, sgd_.w64, sgd_.wc64, sgd_.wc32, sgd_.g64, sgd_.red64, sgd_.stats, sgd_.state,
+                  sgd_.loss_hist, sgd_.pred_out, sgd_.nrm, sgd_.wnorm_next, sgd_.part, sgd_.itrec, iter_tdbg_,
+                  lower_page_, lower_blocks_};
   for (void* b : bufs) if (b) (void)hipFree(b);
-  if (host_counters_) (void)hipHostFree(host_counters_);
   if (host_out_) (void)hipHostFree(host_out_);
   if (host_flags_) (void)hipHostFree(host_flags_);
-  if (host_norm_) (void)hipHostFree(host_norm_);
   for (auto e : iter_events_) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(compute_);
+  (void)hipStreamDestroy(pstream_);
   (void)hipStreamDestroy(copy_);
 }
 
-void LREngine::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, const uint8_t* ext_text) {
+void LREngine::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, const uint8_t* ext_text,
+                      int64_t now_ms) {
   TraceRange tr("twtml.lr.submit_h2d");
   TWTML_HIP_CHECK(hipSetDevice(device_));
+  std::lock_guard<std::mutex> lk(mu_);
   raw_.submit(hb, n, bytes, slot, copy_, kScalarCols, ext_text);
+  submitted_.push_back({slot, now_ms});
+  cv_.notify_all();
 }
 
-BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
-  TraceRange tr_batch("twtml.lr.batch");
+// ---------------------------------------------------------------------------
+// prepare: filter .. layout of one raw slot into a PrepBuf, on stream `s`
+// (the prep stream; host syncs for the batch's counts stay on this thread).
+// ---------------------------------------------------------------------------
+void LREngine::prepare(PrepBuf& pb, int slot, int64_t now_ms, hipStream_t s) {
+  TraceRange tr_prep("twtml.lr.prep");   // filter .. remap
   TWTML_HIP_CHECK(hipSetDevice(device_));
-  hipStream_t s = compute_;
-  const int world = comm_ ? comm_->world() : 1;
+  const int world = world_;
   const int rank = comm_ ? comm_->rank() : 0;
-  BatchResult res;
+  DevPrepared& prep = pb.dp;
+  BatchResult& res = pb.res;
+  res = BatchResult{};
   const DevRawBatch b = raw_.acquire(slot, s);
   res.n_raw = b.n;
-  TWTML_HIP_CHECK(hipEventRecord(ev_[0], s));
+  TWTML_HIP_CHECK(hipEventRecord(pb.ev_start, s));
 
-  auto tr_prep = std::make_unique<TraceRange>("twtml.lr.prep");   // filter .. remap
   FeaturizeParams fp{cfg_.num_text_features, cfg_.hash_kind, cfg_.require_retweet,
                      cfg_.range_filter, cfg_.begin, cfg_.end, now_ms};
-  launch_prep_init(prep_, n_global_, 2 * world + 2, s);
-  launch_filter_sort(b, prep_, fp, s);
-  launch_chunk_layout(b, prep_, s);
+  launch_prep_init(prep, pb.n_global, 2 * world + 2, s);
+  launch_filter_sort(b, prep, fp, s);
+  launch_chunk_layout(b, prep, s);
   // lazy ids: only the histogram's sample chunks keep their hashed ids; the
   // hybrid remap re-reads the (still resident) raw text for the rest
   const bool lazy = cfg_.lazy_idx && cfg_.hybrid && !cfg_.dedup;
   fp.idx_mode = lazy ? 1 : 0;
-  launch_featurize(b, prep_, fp, lower_page_, lower_blocks_, s);
+  launch_featurize(b, prep, fp, lower_page_, lower_blocks_, s);
   if (!lazy) raw_.release_slot(slot, s);  // raw slot may be overwritten now
-  launch_compact_active(prep_, s);        // this rank's active ids (clears the flags)
+  launch_compact_active(prep, s);        // this rank's active ids (clears the flags)
   // per-rank kept rows (sampling offsets, global m) and active-set sizes:
-  // n_global_[1 + r] / n_global_[1 + world + r], one small all-reduce
-  TWTML_HIP_CHECK(hipMemcpyAsync(n_global_ + 1 + rank, prep_.counters, sizeof(int64_t),
+  // n_global[1 + r] / n_global[1 + world + r], one small all-reduce
+  int64_t* hc = pb.host_counters;
+  TWTML_HIP_CHECK(hipMemcpyAsync(pb.n_global + 1 + rank, prep.counters, sizeof(int64_t),
                                  hipMemcpyDeviceToDevice, s));
   if (world > 1) {
-    TWTML_HIP_CHECK(hipMemcpyAsync(n_global_ + 1 + world + rank, prep_.counters + 1, sizeof(int64_t),
+    TWTML_HIP_CHECK(hipMemcpyAsync(pb.n_global + 1 + world + rank, prep.counters + 1, sizeof(int64_t),
                                    hipMemcpyDeviceToDevice, s));
-    comm_->allreduce(n_global_ + 1, size_t(2 * world), ncclInt64, ncclSum, s);
+    comm_->allreduce(pb.n_global + 1, size_t(2 * world), ncclInt64, ncclSum, s);
   }
-  TWTML_HIP_CHECK(hipMemcpyAsync(host_counters_, prep_.counters, 4 * sizeof(int64_t),
+  TWTML_HIP_CHECK(hipMemcpyAsync(hc, prep.counters, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  TWTML_HIP_CHECK(hipMemcpyAsync(pb.host_norm, raw_.norm_stats(slot), 2 * sizeof(int64_t),
                                  hipMemcpyDeviceToHost, s));
-  TWTML_HIP_CHECK(hipMemcpyAsync(host_norm_, raw_.norm_stats(slot), 2 * sizeof(int64_t),
-                                 hipMemcpyDeviceToHost, s));
-  TWTML_HIP_CHECK(hipMemcpyAsync(host_counters_ + 8, n_global_ + 1, sizeof(int64_t) * size_t(2 * world),
+  TWTML_HIP_CHECK(hipMemcpyAsync(hc + 8, pb.n_global + 1, sizeof(int64_t) * size_t(2 * world),
                                  hipMemcpyDeviceToHost, s));
   TWTML_HIP_CHECK(hipStreamSynchronize(s));
-  if (host_counters_[3] != 0) throw std::runtime_error("feature buffer capacity exceeded");
-  const int64_t* per_rank = host_counters_ + 8;
+  if (hc[3] != 0) throw std::runtime_error("feature buffer capacity exceeded");
+  const int64_t* per_rank = hc + 8;
   if (world > 1) {
     // Active-set union: every rank numbers the same slots.  Each rank's
     // sorted id list (padded with -1 to the longest) is all-gathered --
@@ -442,84 +479,105 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
     int64_t maxU = 0;
     for (int r = 0; r < world; ++r) maxU = std::max(maxU, per_rank[world + r]);
     if (maxU > 0) {
-      const int64_t mine = host_counters_[1];
+      const int64_t mine = hc[1];
       if (maxU > mine)
-        TWTML_HIP_CHECK(hipMemsetAsync(prep_.uniq + mine, 0xFF, sizeof(int32_t) * size_t(maxU - mine), s));
+        TWTML_HIP_CHECK(hipMemsetAsync(prep.uniq + mine, 0xFF, sizeof(int32_t) * size_t(maxU - mine), s));
       const int64_t need = maxU * int64_t(world);
-      if (need > ugather_cap_) {
-        if (ugather_) (void)hipFree(ugather_);
-        ugather_cap_ = std::max(need, 2 * ugather_cap_);
-        ugather_ = dmalloc<int32_t>(size_t(ugather_cap_));
+      if (need > pb.ugather_cap) {
+        if (pb.ugather) (void)hipFree(pb.ugather);
+        pb.ugather_cap = std::max(need, 2 * pb.ugather_cap);
+        pb.ugather = dmalloc<int32_t>(size_t(pb.ugather_cap));
       }
-      comm_->allgather(prep_.uniq, ugather_, size_t(maxU), ncclInt32, s);
-      launch_flag_ids(ugather_, need, prep_, s);
-      launch_compact_active(prep_, s);
-      TWTML_HIP_CHECK(hipMemcpyAsync(host_counters_ + 1, prep_.counters + 1, sizeof(int64_t),
-                                     hipMemcpyDeviceToHost, s));
+      comm_->allgather(prep.uniq, pb.ugather, size_t(maxU), ncclInt32, s);
+      launch_flag_ids(pb.ugather, need, prep, s);
+      launch_compact_active(prep, s);
+      TWTML_HIP_CHECK(hipMemcpyAsync(hc + 1, prep.counters + 1, sizeof(int64_t), hipMemcpyDeviceToHost, s));
       TWTML_HIP_CHECK(hipStreamSynchronize(s));
     }
   }
-  res.n_kept = host_counters_[0];
-  res.rows_lowered = host_norm_[0];
-  res.rows_narrowed = host_norm_[1];
-  res.n_unique = host_counters_[1];
-  res.entries = host_counters_[2] * kChunkStride;
+  res.n_kept = hc[0];
+  res.rows_lowered = pb.host_norm[0];
+  res.rows_narrowed = pb.host_norm[1];
+  res.n_unique = hc[1];
+  res.entries = hc[2] * kChunkStride;
   int64_t row_offset = 0, n_glob = 0;
   for (int r = 0; r < world; ++r) {
     if (r < rank) row_offset += per_rank[r];
     n_glob += per_rank[r];
   }
   res.n_kept_global = n_glob;
+  pb.row_offset = row_offset;
 
   // ---- compact space
   const int64_t nU = res.n_unique;
   int64_t ns = kNumNumeric + nU + kPadSlots;
   ns = (ns + 63) / 64 * 64;
-  ensure_compact(ns);
-  sgd_.ns = ns;
-  sgd_.n_unique = nU;
   // Active sets beyond LDS take the tiered layout (hot_split.hip / k_far_grad):
   // decided from the global active set, so every DP rank takes the same path.
   const bool tiered = !(ns <= 65536 && sgd_hybrid_fits(ns)) || force_tiered_;
   const bool u16 = ns <= 65536 || tiered;   // tiered: the near streams are u16
   const bool dedup = cfg_.dedup && !tiered && dedup_supported(ns);
-  prep_.tiered = tiered ? 1 : 0;
-  prep_.hybrid = (tiered || (!dedup && cfg_.hybrid && res.n_kept > 0)) ? 1 : 0;
-  sgd_.nl = ns;
-  sgd_.n_near = nU;
-  sgd_.far_base = kNumNumeric + nU;
-  sgd_.slot_fid = nullptr;
+  prep.tiered = tiered ? 1 : 0;
+  prep.hybrid = (tiered || (!dedup && cfg_.hybrid && res.n_kept > 0)) ? 1 : 0;
+  pb.ns = ns;
+  pb.nl = ns;
+  pb.n_near = nU;
+  pb.far_base = kNumNumeric + nU;
+  pb.u16 = u16;
   if (tiered) {
-    if (near_cap_ <= 0) {
-      near_cap_ = tier_near_cap();
-      if (const char* v = std::getenv("TWTML_NEAR_CAP"))   // tests / tuning: a smaller LDS tier
-        near_cap_ = std::max<int64_t>(64, std::min<int64_t>(near_cap_, std::atoll(v)));
-    }
     const int64_t n_near = std::min(nU, near_cap_);
     const int64_t nl = (kNumNumeric + n_near + kPadSlots + 63) / 64 * 64;
-    ensure_tier(nU);
-    prep_.near_end = kNumNumeric + n_near;
-    TWTML_HIP_CHECK(hipMemsetAsync(prep_.slot_hist + kNumNumeric, 0, sizeof(uint32_t) * size_t(nU), s));
-    launch_tier_hist(prep_, nU, num_cu_, s);
+    ensure_tier(pb, nU, s);
+    prep.near_end = kNumNumeric + n_near;
+    TWTML_HIP_CHECK(hipMemsetAsync(prep.slot_hist + kNumNumeric, 0, sizeof(uint32_t) * size_t(nU), s));
+    launch_tier_hist(prep, nU, num_cu_, s);
     // every rank numbers the slots from the same (summed) sampled counts
-    if (world > 1) comm_->allreduce(prep_.slot_hist + kNumNumeric, size_t(nU), ncclUint32, ncclSum, s);
-    launch_tier_layout(prep_, res.entries, nU, n_near, ns, nl, num_cu_, b, fp, lazy, s);
-    sgd_.nl = nl;
-    sgd_.n_near = n_near;
-    sgd_.far_base = kNumNumeric + n_near;
-    sgd_.slot_fid = prep_.slot_fid;
-    sgd_.fcsc_pos = prep_.fcsc_pos;
-    sgd_.fcsc_slot = prep_.fcsc_slot;
-    sgd_.far_n = prep_.tparam + 2;
+    if (world > 1) comm_->allreduce(prep.slot_hist + kNumNumeric, size_t(nU), ncclUint32, ncclSum, s);
+    launch_tier_layout(prep, res.entries, nU, n_near, ns, nl, num_cu_, b, fp, lazy, s);
+    pb.nl = nl;
+    pb.n_near = n_near;
+    pb.far_base = kNumNumeric + n_near;
     res.tiered = true;
   } else {
-    if (lazy && !prep_.hybrid) launch_featurize_fast_ids(b, prep_, fp, s);   // every id after all
-    if (prep_.hybrid) launch_remap_hybrid(prep_, res.entries, ns, kNumNumeric + nU, num_cu_, b, fp, lazy, s);
-    else launch_remap(prep_, res.entries, nU, u16, s);
+    if (lazy && !prep.hybrid) launch_featurize_fast_ids(b, prep, fp, s);   // every id after all
+    if (prep.hybrid) launch_remap_hybrid(prep, res.entries, ns, kNumNumeric + nU, num_cu_, b, fp, lazy, s);
+    else launch_remap(prep, res.entries, nU, u16, s);
   }
   if (lazy) raw_.release_slot(slot, s);
-  prep_.dedup = dedup ? 1 : 0;
-  if (prep_.dedup) launch_dedup(prep_, ns, kNumNumeric + nU, res.n_kept, s);
+  prep.dedup = dedup ? 1 : 0;
+  if (prep.dedup) launch_dedup(prep, ns, kNumNumeric + nU, res.n_kept, s);
+  res.n_near = pb.n_near;
+  TWTML_HIP_CHECK(hipEventRecord(pb.ev_done, s));
+}
+
+// ---------------------------------------------------------------------------
+// train: GD on a prepared batch, on the compute stream (after its prep).
+// ---------------------------------------------------------------------------
+BatchResult LREngine::train(PrepBuf& pb, bool want_pred) {
+  TWTML_HIP_CHECK(hipSetDevice(device_));
+  hipStream_t s = compute_;
+  const int world = world_;
+  DevPrepared& prep = pb.dp;
+  BatchResult res = pb.res;
+  TWTML_HIP_CHECK(hipStreamWaitEvent(s, pb.ev_done, 0));
+  TWTML_HIP_CHECK(hipEventRecord(ev_[0], s));
+  const int64_t nU = res.n_unique;
+  const int64_t n_glob = res.n_kept_global;
+  const bool tiered = res.tiered;
+  const bool u16 = pb.u16;
+  ensure_compact(pb.ns);
+  sgd_.ns = pb.ns;
+  sgd_.n_unique = nU;
+  sgd_.nl = pb.nl;
+  sgd_.n_near = pb.n_near;
+  sgd_.far_base = pb.far_base;
+  sgd_.slot_fid = tiered ? prep.slot_fid : nullptr;
+  if (tiered) {
+    if (!sgd_.rbuf) sgd_.rbuf = dmalloc<float>(size_t(prep.cap_rows16));
+    sgd_.fcsc_pos = prep.fcsc_pos;
+    sgd_.fcsc_slot = prep.fcsc_slot;
+    sgd_.far_n = prep.tparam + 2;
+  }
   launch_batch_init(sgd_, double(n_glob), cfg_.num_iterations + 2, s);  // state[5] = m (global kept rows)
   if (norm_age_ < 0 || norm_age_ >= kNormRefresh) {
     launch_norm2(sgd_.w64, num_weights(), &sgd_.state[4], sgd_, s);
@@ -528,14 +586,12 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
     launch_norm_carry(sgd_, s);
   }
   ++norm_age_;
-  launch_gather_w(sgd_, prep_, s);
+  launch_gather_w(sgd_, prep, s);
   TWTML_HIP_CHECK(hipEventRecord(ev_[1], s));
-  tr_prep.reset();
   TraceRange tr_train("twtml.lr.train");   // GD iterations (host enqueue + early-stop polling)
 
   const int64_t nl = sgd_.nl;
-  res.n_near = sgd_.n_near;
-  int grid = cfg_.sgd_grid > 0 ? cfg_.sgd_grid : sgd_iter_grid(nl, res.n_kept, num_cu_, prep_.hybrid != 0);
+  int grid = cfg_.sgd_grid > 0 ? cfg_.sgd_grid : sgd_iter_grid(nl, res.n_kept, num_cu_, prep.hybrid != 0);
   sgd_.pstride = sgd_part_stride(nl);
   sgd_.nparts = sgd_partials(nl, u16, grid);
   ensure_part(int64_t(sgd_.nparts) * sgd_.pstride);
@@ -544,7 +600,7 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   sp.fraction = cfg_.fraction;
   sp.tol = cfg_.tol;
   sp.num_iterations = cfg_.num_iterations;
-  sp.row_offset = row_offset;
+  sp.row_offset = pb.row_offset;
   sp.want_pred = want_pred ? 1 : 0;
   sp.sample = cfg_.fraction < 1.0 ? 1 : 0;
   sp.ablate = cfg_.ablate;
@@ -556,20 +612,13 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   if (n_glob > 0) {
     // Host-side early stop: the convergence test of update j runs in the
     // prologue of iteration j+1's gradient kernel, which copies its verdict
-    // to pinned memory (zero copy); an event after that kernel lets the host
-    // keep at most `depth` iterations queued and stop enqueueing once an
-    // earlier verdict is set.  Verdicts derive from all-reduced values in a
-    // fixed summation order, so every rank stops at the same iteration and
-    // the collectives match.
+    // to pinned memory (zero copy); the host keeps at most `depth`
+    // iterations queued and stops enqueueing once an earlier verdict is
+    // set.  Verdicts derive from all-reduced values in a fixed summation
+    // order, so every rank stops at the same iteration and the collectives
+    // match.
     const int depth = std::max(2, cfg_.early_exit_depth);
     const int iters = cfg_.num_iterations;
-    if (int(iter_events_.size()) < iters + 1) {
-      for (int k = int(iter_events_.size()); k < iters + 1; ++k) {
-        hipEvent_t e;
-        TWTML_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        iter_events_.push_back(e);
-      }
-    }
     std::fill(host_flags_, host_flags_ + iters + 2, -1.0);   // -1: verdict not published yet
     // single GPU with partial rows: the update kernel reduces them itself
     const bool fused = world == 1 && sgd_.nparts > 0;
@@ -585,7 +634,7 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
       sp.iteration = i;
       // every rank launches the gradient kernel (an empty shard writes zero
       // partials) so every rank runs the convergence prologue
-      launch_sgd_iter(sgd_, prep_, sp, host_counters_[2], u16, grid, s);
+      launch_sgd_iter(sgd_, prep, sp, pb.host_counters[2], u16, grid, s);
       if (tiered) launch_far_grad(sgd_, sp, num_cu_, s);
       if (world > 1) {
         launch_sgd_reduce(sgd_, sp, s);
@@ -597,34 +646,9 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
       launch_sgd_update(sgd_, sp, fused ? sgd_.nparts : 0, s);
     }
     launch_sgd_finish(sgd_, sp, s);
-    launch_scatter_w(sgd_, prep_, s);
+    launch_scatter_w(sgd_, prep, s);
     launch_norm_next(sgd_, true, s);
-    if (itime) {   // iteration-kernel phases (us): stop-check, lds init, chunks, hot reduce, scalars, slots
-      std::vector<uint64_t> tb(4096 + size_t(iters + 2) * 32);
-      TWTML_HIP_CHECK(hipMemcpyAsync(tb.data(), iter_tdbg_, tb.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-      TWTML_HIP_CHECK(hipStreamSynchronize(s));
-      for (int which = 0; which < 2; ++which) {
-        double acc[6] = {0, 0, 0, 0, 0, 0};
-        int n = 0;
-        for (int i = 2; i <= iters; ++i) {
-          const uint64_t* t = tb.data() + (size_t(i) * 2 + size_t(which)) * 8;
-          if (t[6] == 0) continue;
-          for (int k = 0; k < 6; ++k) acc[k] += double(t[k + 1] - t[k]) * 0.01;
-          ++n;
-        }
-        if (n) std::fprintf(stderr, "iter timing wg %s (us, %d iters): stop %.2f init %.2f chunks %.2f hotred %.2f scalars %.2f slots %.2f\n",
-                            which ? "last" : "0", n, acc[0] / n, acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n);
-      }
-      {   // wave end spread inside WG 0, iteration 10
-        const int i = std::min(10, iters);
-        const uint64_t* t0 = tb.data() + (size_t(i) * 2) * 8;
-        const uint64_t* we = tb.data() + 4096 + size_t(i) * 32;
-        std::fprintf(stderr, "wave ends (us after kernel start) / chunks, WG 0 it %d:", i);
-        for (int w = 0; w < 16; ++w)
-          std::fprintf(stderr, " %.1f/%d", double(we[2 * w] - t0[0]) * 0.01, int(we[2 * w + 1]));
-        std::fprintf(stderr, "\n");
-      }
-    }
+    if (itime) print_iter_timing(iters);
   }
   if (n_glob <= 0) launch_norm_next(sgd_, false, s);   // weights unchanged: carry |w|^2 as is
   TWTML_HIP_CHECK(hipEventRecord(ev_[2], s));
@@ -646,8 +670,147 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   res.overflow = st[7] == 1.0;
   res.iterations = int32_t(st[3]);
   for (int i = 1; i <= res.iterations; ++i) res.loss_history.push_back(host_out_[16 + i]);
-  TWTML_HIP_CHECK(hipEventElapsedTime(&res.prep_ms, ev_[0], ev_[1]));
+  // prep_ms: the batch's prep on its own stream (overlapped with the previous
+  // batch's training when prepared ahead); train_ms: compute stream
+  TWTML_HIP_CHECK(hipEventElapsedTime(&res.prep_ms, pb.ev_start, pb.ev_done));
   TWTML_HIP_CHECK(hipEventElapsedTime(&res.train_ms, ev_[1], ev_[2]));
+  return res;
+}
+
+void LREngine::print_iter_timing(int iters) {
+  // iteration-kernel phases (us): stop-check, lds init, chunks, hot reduce, scalars, slots
+  hipStream_t s = compute_;
+  std::vector<uint64_t> tb(4096 + size_t(iters + 2) * 32);
+  TWTML_HIP_CHECK(hipMemcpyAsync(tb.data(), iter_tdbg_, tb.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  TWTML_HIP_CHECK(hipStreamSynchronize(s));
+  for (int which = 0; which < 2; ++which) {
+    double acc[6] = {0, 0, 0, 0, 0, 0};
+    int n = 0;
+    for (int i = 2; i <= iters; ++i) {
+      const uint64_t* t = tb.data() + (size_t(i) * 2 + size_t(which)) * 8;
+      if (t[6] == 0) continue;
+      for (int k = 0; k < 6; ++k) acc[k] += double(t[k + 1] - t[k]) * 0.01;
+      ++n;
+    }
+    if (n) std::fprintf(stderr, "iter timing wg %s (us, %d iters): stop %.2f init %.2f chunks %.2f hotred %.2f scalars %.2f slots %.2f\n",
+                        which ? "last" : "0", n, acc[0] / n, acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n);
+  }
+  const int i = std::min(10, iters);   // wave end spread inside WG 0, iteration 10
+  const uint64_t* t0 = tb.data() + (size_t(i) * 2) * 8;
+  const uint64_t* we = tb.data() + 4096 + size_t(i) * 32;
+  std::fprintf(stderr, "wave ends (us after kernel start) / chunks, WG 0 it %d:", i);
+  for (int w = 0; w < 16; ++w) std::fprintf(stderr, " %.1f/%d", double(we[2 * w] - t0[0]) * 0.01, int(we[2 * w + 1]));
+  std::fprintf(stderr, "\n");
+}
+
+// ---------------------------------------------------------------------------
+// Prepare-ahead: the prep thread prepares the oldest submitted slot that is
+// not prepared yet into a free PrepBuf while the caller trains.
+// ---------------------------------------------------------------------------
+void LREngine::prep_worker() {
+  (void)hipSetDevice(device_);
+  std::unique_lock<std::mutex> lk(mu_);
+  for (;;) {
+    cv_.wait(lk, [&] { return stop_ || job_ >= 0; });
+    if (stop_) return;
+    PrepBuf& b = pb_[job_];
+    const int slot = b.slot;
+    const int64_t now_ms = b.now_ms;
+    lk.unlock();
+    std::exception_ptr err;
+    try {
+      prepare(b, slot, now_ms, pstream_);
+    } catch (...) {
+      err = std::current_exception();
+    }
+    lk.lock();
+    b.error = err;
+    b.state = 2;
+    job_ = -1;
+    cv_.notify_all();
+  }
+}
+
+// Caller holds mu_: start preparing the next submitted slot if a buffer and
+// the prep thread are free.
+void LREngine::schedule_ahead_locked() {
+  if (!overlap_ || job_ >= 0 || submitted_.empty()) return;
+  int free_buf = -1;
+  for (int k = 0; k < 2; ++k)
+    if (pb_[k].state == 0) free_buf = k;
+  if (free_buf < 0) return;
+  const auto next = submitted_.front();
+  for (auto& b : pb_)
+    if (b.state != 0 && b.slot == next.first) return;   // already there
+  submitted_.pop_front();
+  PrepBuf& b = pb_[free_buf];
+  b.state = 1;
+  b.slot = next.first;
+  b.now_ms = next.second;
+  job_ = free_buf;
+  cv_.notify_all();
+}
+
+BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
+  TraceRange tr_batch("twtml.lr.batch");
+  TWTML_HIP_CHECK(hipSetDevice(device_));
+  int k = -1;
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (int i = 0; i < 2; ++i)
+      if (pb_[i].state != 0 && pb_[i].slot == slot) k = i;
+    if (k >= 0) {
+      cv_.wait(lk, [&] { return pb_[k].state == 2; });
+      if (pb_[k].error || pb_[k].now_ms != now_ms) {   // failed ahead / other batch time: redo in line
+        std::exception_ptr err = pb_[k].error;
+        pb_[k].error = nullptr;
+        if (err && pb_[k].now_ms == now_ms) {
+          pb_[k].state = 0;
+          std::rethrow_exception(err);
+        }
+        pb_[k].state = 1;
+        lk.unlock();
+        prepare(pb_[k], slot, now_ms, pstream_);
+        lk.lock();
+        pb_[k].state = 2;
+      }
+    } else {
+      // not prepared ahead: drop it from the submission queue, prepare in line
+      for (auto it = submitted_.begin(); it != submitted_.end(); ++it)
+        if (it->first == slot) { submitted_.erase(it); break; }
+      for (int i = 0; i < (overlap_ ? 2 : 1); ++i)
+        if (pb_[i].state == 0) k = i;
+      if (k < 0) throw std::logic_error("no free prepared-batch buffer");
+      pb_[k].state = 1;
+      pb_[k].slot = slot;
+      pb_[k].now_ms = now_ms;
+      lk.unlock();
+      try {
+        prepare(pb_[k], slot, now_ms, pstream_);
+      } catch (...) {
+        lk.lock();
+        pb_[k].state = 0;
+        throw;
+      }
+      lk.lock();
+      pb_[k].state = 2;
+    }
+    last_buf_ = k;
+    schedule_ahead_locked();   // batch t+1's prep overlaps batch t's training
+  }
+  BatchResult res;
+  try {
+    res = train(pb_[k], want_pred);
+  } catch (...) {
+    std::lock_guard<std::mutex> lk(mu_);
+    pb_[k].state = 0;
+    throw;
+  }
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    pb_[k].state = 0;
+    schedule_ahead_locked();
+  }
   return res;
 }
 
@@ -676,6 +839,7 @@ void LREngine::set_step(double step, int iters, double fraction) {
 void LREngine::synchronize() {
   TWTML_HIP_CHECK(hipSetDevice(device_));
   TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
+  TWTML_HIP_CHECK(hipStreamSynchronize(pstream_));
   TWTML_HIP_CHECK(hipStreamSynchronize(copy_));
 }
 
@@ -683,19 +847,21 @@ void LREngine::debug_merged(std::vector<int32_t>& slot, std::vector<int32_t>& cn
                             std::vector<int32_t>& clen8d) const {
   TWTML_HIP_CHECK(hipSetDevice(device_));
   TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
+  TWTML_HIP_CHECK(hipStreamSynchronize(pstream_));
+  const DevPrepared& lp = pb_[last_buf_ < 0 ? 0 : last_buf_].dp;
   slot.clear(); cnt.clear(); clen8d.clear();
-  if (!prep_.dedup) return;
+  if (!lp.dedup) return;
   int64_t counters[4];
-  TWTML_HIP_CHECK(hipMemcpy(counters, prep_.counters, sizeof(counters), hipMemcpyDeviceToHost));
+  TWTML_HIP_CHECK(hipMemcpy(counters, lp.counters, sizeof(counters), hipMemcpyDeviceToHost));
   const int64_t C = (counters[0] + kRowsPerChunk - 1) / kRowsPerChunk;
   const int64_t E = counters[2] * kChunkStride;
   std::vector<uint16_t> s16(static_cast<size_t>(E)), c16(static_cast<size_t>(E));
   clen8d.resize(size_t(C));
   if (E) {
-    TWTML_HIP_CHECK(hipMemcpy(s16.data(), prep_.slot, sizeof(uint16_t) * size_t(E), hipMemcpyDeviceToHost));
-    TWTML_HIP_CHECK(hipMemcpy(c16.data(), prep_.cnt, sizeof(uint16_t) * size_t(E), hipMemcpyDeviceToHost));
+    TWTML_HIP_CHECK(hipMemcpy(s16.data(), lp.slot, sizeof(uint16_t) * size_t(E), hipMemcpyDeviceToHost));
+    TWTML_HIP_CHECK(hipMemcpy(c16.data(), lp.cnt, sizeof(uint16_t) * size_t(E), hipMemcpyDeviceToHost));
   }
-  if (C) TWTML_HIP_CHECK(hipMemcpy(clen8d.data(), prep_.clen8d, sizeof(int32_t) * size_t(C), hipMemcpyDeviceToHost));
+  if (C) TWTML_HIP_CHECK(hipMemcpy(clen8d.data(), lp.clen8d, sizeof(int32_t) * size_t(C), hipMemcpyDeviceToHost));
   slot.assign(s16.begin(), s16.end());
   cnt.assign(c16.begin(), c16.end());
 }
@@ -704,23 +870,25 @@ void LREngine::debug_hybrid(std::vector<int32_t>& hot_slot, std::vector<uint32_t
                             std::vector<int32_t>& clen8c, std::vector<int32_t>& cslot) const {
   TWTML_HIP_CHECK(hipSetDevice(device_));
   TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
+  TWTML_HIP_CHECK(hipStreamSynchronize(pstream_));
+  const DevPrepared& lp = pb_[last_buf_ < 0 ? 0 : last_buf_].dp;
   hot_slot.clear(); hot_dense.clear(); clen8c.clear(); cslot.clear();
-  if (!prep_.hybrid) return;
+  if (!lp.hybrid) return;
   int64_t counters[4];
-  TWTML_HIP_CHECK(hipMemcpy(counters, prep_.counters, sizeof(counters), hipMemcpyDeviceToHost));
+  TWTML_HIP_CHECK(hipMemcpy(counters, lp.counters, sizeof(counters), hipMemcpyDeviceToHost));
   const int64_t C = (counters[0] + kRowsPerChunk - 1) / kRowsPerChunk;
   const int64_t E = counters[2] * kChunkStride;
   hot_slot.resize(kHot);
   hot_dense.resize(size_t(C) * kWave * 4);
   clen8c.resize(size_t(C));
   std::vector<uint16_t> c16(static_cast<size_t>(E));
-  TWTML_HIP_CHECK(hipMemcpy(hot_slot.data(), prep_.hot_slot, sizeof(int32_t) * kHot, hipMemcpyDeviceToHost));
+  TWTML_HIP_CHECK(hipMemcpy(hot_slot.data(), lp.hot_slot, sizeof(int32_t) * kHot, hipMemcpyDeviceToHost));
   if (C) {
-    TWTML_HIP_CHECK(hipMemcpy(hot_dense.data(), prep_.hot_dense, sizeof(uint32_t) * hot_dense.size(),
+    TWTML_HIP_CHECK(hipMemcpy(hot_dense.data(), lp.hot_dense, sizeof(uint32_t) * hot_dense.size(),
                               hipMemcpyDeviceToHost));
-    TWTML_HIP_CHECK(hipMemcpy(clen8c.data(), prep_.clen8c, sizeof(int32_t) * size_t(C), hipMemcpyDeviceToHost));
+    TWTML_HIP_CHECK(hipMemcpy(clen8c.data(), lp.clen8c, sizeof(int32_t) * size_t(C), hipMemcpyDeviceToHost));
   }
-  if (E) TWTML_HIP_CHECK(hipMemcpy(c16.data(), prep_.cslot, sizeof(uint16_t) * size_t(E), hipMemcpyDeviceToHost));
+  if (E) TWTML_HIP_CHECK(hipMemcpy(c16.data(), lp.cslot, sizeof(uint16_t) * size_t(E), hipMemcpyDeviceToHost));
   cslot.assign(c16.begin(), c16.end());
 }
 
@@ -730,8 +898,10 @@ void LREngine::debug_prepared(std::vector<int64_t>& counters, std::vector<int32_
                               std::vector<float>& num, std::vector<int32_t>& uniq) {
   TWTML_HIP_CHECK(hipSetDevice(device_));
   TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
+  TWTML_HIP_CHECK(hipStreamSynchronize(pstream_));
+  const DevPrepared& lp = pb_[last_buf_ < 0 ? 0 : last_buf_].dp;
   counters.resize(4);
-  TWTML_HIP_CHECK(hipMemcpy(counters.data(), prep_.counters, 4 * sizeof(int64_t), hipMemcpyDeviceToHost));
+  TWTML_HIP_CHECK(hipMemcpy(counters.data(), lp.counters, 4 * sizeof(int64_t), hipMemcpyDeviceToHost));
   const int64_t nk = counters[0], nu = counters[1], groups = counters[2];
   const int64_t C = (nk + kRowsPerChunk - 1) / kRowsPerChunk;
   const int64_t R = C * kRowsPerChunk;
@@ -743,18 +913,18 @@ void LREngine::debug_prepared(std::vector<int64_t>& counters, std::vector<int32_
   num.resize(size_t(4 * R));
   uniq.resize(size_t(nu));
   if (C) {
-    TWTML_HIP_CHECK(hipMemcpy(clen8.data(), prep_.clen8, sizeof(int32_t) * size_t(C), hipMemcpyDeviceToHost));
-    TWTML_HIP_CHECK(hipMemcpy(cbase.data(), prep_.cbase, sizeof(int64_t) * size_t(C), hipMemcpyDeviceToHost));
-    TWTML_HIP_CHECK(hipMemcpy(perm.data(), prep_.perm, sizeof(int32_t) * size_t(R), hipMemcpyDeviceToHost));
-    TWTML_HIP_CHECK(hipMemcpy(y.data(), prep_.y, sizeof(float) * size_t(R), hipMemcpyDeviceToHost));
+    TWTML_HIP_CHECK(hipMemcpy(clen8.data(), lp.clen8, sizeof(int32_t) * size_t(C), hipMemcpyDeviceToHost));
+    TWTML_HIP_CHECK(hipMemcpy(cbase.data(), lp.cbase, sizeof(int64_t) * size_t(C), hipMemcpyDeviceToHost));
+    TWTML_HIP_CHECK(hipMemcpy(perm.data(), lp.perm, sizeof(int32_t) * size_t(R), hipMemcpyDeviceToHost));
+    TWTML_HIP_CHECK(hipMemcpy(y.data(), lp.y, sizeof(float) * size_t(R), hipMemcpyDeviceToHost));
     for (int k = 0; k < 4; ++k)
-      TWTML_HIP_CHECK(hipMemcpy(num.data() + k * R, prep_.num + k * prep_.cap_rows16,
+      TWTML_HIP_CHECK(hipMemcpy(num.data() + k * R, lp.num + k * lp.cap_rows16,
                                 sizeof(float) * size_t(R), hipMemcpyDeviceToHost));
   }
   if (groups)
-    TWTML_HIP_CHECK(hipMemcpy(idx.data(), prep_.idx, sizeof(int32_t) * idx.size(), hipMemcpyDeviceToHost));
+    TWTML_HIP_CHECK(hipMemcpy(idx.data(), lp.idx, sizeof(int32_t) * idx.size(), hipMemcpyDeviceToHost));
   if (nu)
-    TWTML_HIP_CHECK(hipMemcpy(uniq.data(), prep_.uniq, sizeof(int32_t) * size_t(nu), hipMemcpyDeviceToHost));
+    TWTML_HIP_CHECK(hipMemcpy(uniq.data(), lp.uniq, sizeof(int32_t) * size_t(nu), hipMemcpyDeviceToHost));
 }
 
 }  // namespace twtml

@@ -1,20 +1,28 @@
 // MI355X micro-batch engine for StreamingLinearRegressionWithSGD.
 //
 // One engine per process/GPU.  A micro-batch flows:
-//   pinned host RawBatch --(copy stream, async H2D)--> device slot (x3)
-//   compute stream: filter -> length sort -> featurize -> [RCCL max of the
-//   active-feature flags] -> compact -> remap -> gather w ->
-//   numIterations x ( fused predict/gradient kernel -> [RCCL all-reduce of
-//   the packed gradient] -> fp64 update + convergence ) -> scatter w
-// Three device slots let the H2D of batches t+1 and t+2 overlap batch t's
+//   pinned host RawBatch --(copy stream, async H2D)--> device slot (x4)
+//   prep stream: decode / lower rows -> filter -> length sort -> featurize
+//   -> compact [RCCL all-gather of the active id lists] -> layout (hybrid /
+//   tiered) -- for batch t+1 while batch t trains (prep thread)
+//   compute stream: gather w -> numIterations x ( fused predict/gradient
+//   kernel -> [RCCL all-reduce of the packed gradient] -> fp64 update +
+//   convergence ) -> scatter w
+// Four device slots let the H2D of the next batches overlap batch t's
 // training (SURVEY §2.4 "Ingest || compute pipelining").  Output op #1 (prequential stats)
 // is fused into iteration 1, so it sees the weights before training on the
 // batch (LinearRegression.scala:53-86 ordering).
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <condition_variable>
+#include <deque>
+#include <exception>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
+#include <utility>
 #include <vector>
 
 #include "comm.h"
@@ -41,6 +49,7 @@ struct LRConfig {
   int32_t dedup = 0;             // merge repeated bigrams of a row into counts
   int32_t hybrid = 1;            // dense 4-bit counts for the batch's hottest slots (hot_split.hip)
   int32_t lazy_idx = 1;          // hybrid: fast chunks' ids re-derived from text by the remap
+  int32_t overlap = 1;           // prepare batch t+1 (prep stream, prep thread) while t trains
 };
 
 // Pinned staging buffer of one raw batch in the wire format
@@ -121,14 +130,42 @@ struct BatchResult {
   float prep_ms = 0.f, train_ms = 0.f;
 };
 
+// One prepared micro-batch: filtered, featurized, compacted and laid out for
+// the GD kernels.  Two of them, so batch t+1 is prepared on the prep stream
+// (by the engine's prep thread) while batch t trains on the compute stream.
+struct PrepBuf {
+  DevPrepared dp{};
+  int64_t slot_hist_cap = 0;
+  int64_t* n_global = nullptr;        // device [2 world + 2]: per-rank kept rows | active-set sizes
+  int32_t* ugather = nullptr;         // DP active-set union: all-gathered id lists
+  int64_t ugather_cap = 0;
+  int64_t* host_counters = nullptr;   // pinned [8 + 2 world]: counters | per-rank kept | per-rank active
+  int64_t* host_norm = nullptr;       // pinned [2] rows lowered / narrowed on the device
+  hipEvent_t ev_start = nullptr, ev_done = nullptr;
+  // guarded by LREngine::mu_
+  int state = 0;                      // 0 free, 1 being prepared, 2 prepared
+  int slot = -1;
+  int64_t now_ms = 0;
+  std::exception_ptr error;
+  // prepare() outputs
+  BatchResult res;                    // n_raw .. n_near, rows lowered / narrowed
+  int64_t row_offset = 0;             // global index of this rank's first kept row
+  bool u16 = true;
+  int64_t ns = 0, nl = 0, n_near = 0, far_base = 0;
+};
+
 class LREngine {
  public:
   LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm);
   ~LREngine();
 
   // Async H2D of rows [0, n) of a pinned host batch into device slot `slot`.
-  void submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, const uint8_t* ext_text = nullptr);
-  // Train on the batch in `slot` (blocks until done); stats use w before training.
+  // now_ms: the batch's time (featurizeNumbers), used if it is prepared ahead.
+  void submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, const uint8_t* ext_text = nullptr,
+              int64_t now_ms = 0);
+  // Train on the batch in `slot` (blocks until done); stats use w before
+  // training.  The next submitted slot is then prepared ahead (prep thread,
+  // prep stream) while this one trains.
   BatchResult process(int slot, int64_t now_ms, bool want_pred);
 
   void set_weights(const double* w, int64_t n);
@@ -151,18 +188,34 @@ class LREngine {
                     std::vector<int32_t>& clen8c, std::vector<int32_t>& cslot) const;
 
  private:
-  void alloc_prepared();
+  void alloc_prepared(PrepBuf& b);
+  void free_prepared(PrepBuf& b);
   void ensure_compact(int64_t ns);
   void ensure_part(int64_t n);
-  void ensure_tier(int64_t n_unique);
+  void ensure_tier(PrepBuf& b, int64_t n_unique, hipStream_t s);
+  void prepare(PrepBuf& b, int slot, int64_t now_ms, hipStream_t s);
+  BatchResult train(PrepBuf& b, bool want_pred);
+  void prep_worker();
+  void schedule_ahead_locked();
+  void print_iter_timing(int iters);
   double wait_flag(int j);
 
   int device_;
   LRConfig cfg_;
   std::shared_ptr<Comm> comm_;
-  hipStream_t compute_ = nullptr, copy_ = nullptr;
+  int world_ = 1;
+  hipStream_t compute_ = nullptr, pstream_ = nullptr, copy_ = nullptr;
   RawSlots raw_;
-  DevPrepared prep_{};
+  PrepBuf pb_[2];
+  int last_buf_ = -1;               // buffer of the last trained batch (debug_*)
+  bool overlap_ = true;
+  // prepare-ahead: submitted slots in order, the prep thread's job (a pb_ index)
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::pair<int, int64_t>> submitted_;
+  int job_ = -1;
+  bool stop_ = false;
+  std::thread worker_;
   DevSgd sgd_{};
   int64_t ns_cap_ = 0;
   // |w|^2 is carried from batch to batch (|w_rest|^2 + trained active part)
@@ -173,18 +226,12 @@ class LREngine {
   int64_t part_cap_ = 0;
   int64_t near_cap_ = 0;          // tiered layout: LDS-resident text slots (tier_near_cap)
   bool force_tiered_ = false;     // TWTML_FORCE_TIERED=1: tiered layout for any active set (tests)
-  int64_t slot_hist_cap_ = 0;
   uint64_t* iter_tdbg_ = nullptr;
   uint8_t* lower_page_ = nullptr;
   uint16_t* lower_blocks_ = nullptr;
-  int64_t* host_counters_ = nullptr;  // pinned [8 + 2 world]: counters | per-rank kept | per-rank active
   double* host_out_ = nullptr;        // pinned [16 + iters]
   double* host_flags_ = nullptr;      // pinned [iters + 1] convergence flag per iteration
-  int64_t* host_norm_ = nullptr;      // pinned [2] rows lowered / narrowed on the device
   std::vector<hipEvent_t> iter_events_;
-  int64_t* n_global_ = nullptr;       // device [2 world + 2]
-  int32_t* ugather_ = nullptr;        // DP active-set union: all-gathered id lists
-  int64_t ugather_cap_ = 0;
   hipEvent_t ev_[4] = {nullptr, nullptr, nullptr, nullptr};
   int num_cu_ = 256;
 };

@@ -402,7 +402,9 @@ __global__ __launch_bounds__(kSplitWaves * kWave) void k_remap_hybrid(DevPrepare
 // global atomic each.  Multiple ranges = multiple launches.
 constexpr int kTierHistSpan = 32768;
 
-__global__ __launch_bounds__(kHistBlock) void k_tier_hist(DevPrepared p, int64_t lo, int64_t hi) {
+// step: every step-th sampled chunk (the same subset in every span pass),
+// so the passes over wide active sets cost one sampled pass in total.
+__global__ __launch_bounds__(kHistBlock) void k_tier_hist(DevPrepared p, int64_t lo, int64_t hi, int64_t step) {
   __shared__ uint32_t h[kTierHistSpan];
   const int64_t span = hi - lo;
   for (int64_t i = threadIdx.x; i < span; i += kHistBlock) h[i] = 0u;
@@ -412,7 +414,7 @@ __global__ __launch_bounds__(kHistBlock) void k_tier_hist(DevPrepared p, int64_t
   const int64_t nsamp = ((n_kept + kRowsPerChunk - 1) / kRowsPerChunk + kHistChunks - 1) / kHistChunks;
   const int64_t wave = (int64_t(blockIdx.x) * kHistBlock + threadIdx.x) / kWave;
   const int64_t nwaves = int64_t(gridDim.x) * kHistBlock / kWave;
-  for (int64_t sc = wave; sc < nsamp; sc += nwaves) {
+  for (int64_t sc = wave * step; sc < nsamp; sc += nwaves * step) {
     const int64_t c = sc * kHistChunks;
     const int32_t L8 = p.clen8[c];
     const int32_t* src = p.idx + p.cbase[c] * kChunkStride + lane * kGroup;
@@ -625,11 +627,15 @@ void launch_tier_hist(const DevPrepared& p, int64_t n_unique, int num_cu, hipStr
   // slot_hist[4 .. 4 + nU) zeroed by the caller
   const int64_t cmax = (p.cap_rows + kRowsPerChunk - 1) / kRowsPerChunk;
   const int64_t nsamp = (cmax + kHistChunks - 1) / kHistChunks;
-  int gh = int((nsamp + kHistBlock / kWave - 1) / (kHistBlock / kWave));
+  // one LDS-privatised pass per 32K-slot span; each reads every step-th
+  // sampled chunk, step = number of spans (the near tier only needs the
+  // frequency order of the top slots: ~1/100 of the entries at 200K slots)
+  const int64_t step = std::max<int64_t>(1, (n_unique + kTierHistSpan - 1) / kTierHistSpan);
+  int gh = int((nsamp / step + kHistBlock / kWave - 1) / (kHistBlock / kWave));
   gh = std::max(1, std::min(gh, num_cu / 2));
   for (int64_t lo = 0; lo < n_unique; lo += kTierHistSpan)
     hipLaunchKernelGGL(k_tier_hist, dim3(gh), dim3(kHistBlock), 0, s, p, lo,
-                       std::min<int64_t>(n_unique, lo + kTierHistSpan));
+                       std::min<int64_t>(n_unique, lo + kTierHistSpan), step);
 }
 
 int64_t tier_near_cap() {

@@ -92,6 +92,10 @@ class LRDeviceConfig:
     # "utf8" ships the receiver's UTF-8 bytes (~155 B per tweet) -- the
     # device decodes non-ASCII rows and narrows the Latin-1 ones
     ingest: str = "wire"
+    # prepare batch t+1 (featurize .. layout, on a prep stream and the
+    # engine's prep thread) while batch t trains; one GPU only (DP ranks
+    # prepare in line: the prep collectives would share the communicator)
+    overlap: bool = True
 
     def as_dict(self) -> Dict[str, object]:
         return {
@@ -112,6 +116,7 @@ class LRDeviceConfig:
             "dedup": int(bool(self.dedup)),
             "hybrid": int(bool(self.hybrid)),
             "lazy_idx": int(bool(self.lazy_idx)),
+            "overlap": int(bool(self.overlap)),
         }
 
 
@@ -263,7 +268,7 @@ class DeviceLinearRegression:
         return self._staging[i]
 
     def submit(self, hb: HostBatchView, slot: int) -> None:
-        self._eng.submit(hb._hb, int(hb.n), int(hb.bytes), int(slot), int(hb.ext_text))
+        self._eng.submit(hb._hb, int(hb.n), int(hb.bytes), int(slot), int(hb.ext_text), int(hb.batch_time_ms))
 
     def process(self, slot: int, now_ms: int, want_pred: bool = False) -> Dict[str, object]:
         return self._eng.process(int(slot), int(now_ms), bool(want_pred))
