@@ -226,7 +226,10 @@ def main(argv=None) -> int:
     torch.cuda.set_device(device)
     from twitter_stream_ml_amd.parallel.affinity import bind_local_numa
     numa_cpus = bind_local_numa(device)   # before the pinned pool is allocated
-    comm = D.make_comm(device, args.comm)
+    if args.model == "kmeans":
+        comm, prep_comm = D.make_comm(device, args.comm), None
+    else:   # LR: a second communicator lets batch t+1 be prepared during t's all-reduces
+        comm, prep_comm = D.make_comm_pair(device, args.comm)
     ingest = args.ingest or "utf8"
 
     B = args.batch
@@ -247,7 +250,7 @@ def main(argv=None) -> int:
                              begin=100, end=1000, max_rows=B, max_units=max_units,
                              sgd_grid=args.sgd_grid, ablate=args.ablate, tol=args.tol, dedup=bool(args.dedup),
                              hybrid=bool(args.hybrid), ingest=ingest if args.e2e else "wire")
-        eng = DeviceLinearRegression(cfg, device=device, comm=comm)
+        eng = DeviceLinearRegression(cfg, device=device, comm=comm, prep_comm=prep_comm)
     u8s = []
     if args.e2e:
         views = [HostBatchView(B, max_units) for _ in range(eng.raw_slots)]

@@ -240,12 +240,13 @@ PYBIND11_MODULE(_twtml_hip, m) {
       });
 
   py::class_<LREngine, std::shared_ptr<LREngine>>(m, "LREngine")
-      .def(py::init([](int device, const py::dict& cfg, std::shared_ptr<Comm> comm) {
+      .def(py::init([](int device, const py::dict& cfg, std::shared_ptr<Comm> comm,
+                       std::shared_ptr<Comm> prep_comm) {
              LRConfig c = lr_config(cfg);
              py::gil_scoped_release nogil;
-             return std::make_shared<LREngine>(device, c, comm);
+             return std::make_shared<LREngine>(device, c, comm, prep_comm);
            }),
-           py::arg("device"), py::arg("config"), py::arg("comm") = nullptr)
+           py::arg("device"), py::arg("config"), py::arg("comm") = nullptr, py::arg("prep_comm") = nullptr)
       .def("submit",
            [](LREngine& e, const HostBatch& hb, int64_t n, int64_t bytes, int slot, uintptr_t ext_text,
               int64_t now_ms) {

@@ -183,8 +183,8 @@ static T* dmalloc(size_t n) {
   return static_cast<T*>(p);
 }
 
-LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
-    : device_(device), cfg_(cfg), comm_(std::move(comm)) {
+LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm, std::shared_ptr<Comm> prep_comm)
+    : device_(device), cfg_(cfg), comm_(std::move(comm)), prep_comm_(std::move(prep_comm)) {
   if (cfg_.num_text_features <= 0) throw std::invalid_argument("numTextFeatures must be > 0");
   if (cfg_.max_rows <= 0 || cfg_.max_units < 0) throw std::invalid_argument("bad capacity");
   if (cfg_.max_rows >= (int64_t(1) << 31)) throw std::invalid_argument("max_rows must be < 2^31");
@@ -192,9 +192,12 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
     throw std::invalid_argument("miniBatchFraction must be in (0, 1]");
   if (const char* v = std::getenv("TWTML_FORCE_TIERED")) force_tiered_ = v[0] == '1';   // tests
   world_ = comm_ ? comm_->world() : 1;
-  // Prepare-ahead needs the prep-stage collectives off the gradient
-  // communicator, so it runs on one GPU (DP ranks prepare in line).
-  overlap_ = world_ == 1 && cfg_.overlap != 0;
+  if (prep_comm_ && (prep_comm_->world() != world_ || prep_comm_->rank() != comm_->rank()))
+    throw std::invalid_argument("prep communicator must span the same ranks");
+  // Prepare-ahead runs the prep-stage collectives (kept counts, active-id
+  // union, tier counts) concurrently with the gradient all-reduces, so DP
+  // ranks need a second communicator for them (one GPU: no collectives).
+  overlap_ = cfg_.overlap != 0 && (world_ == 1 || prep_comm_ != nullptr);
   if (const char* v = std::getenv("TWTML_OVERLAP")) overlap_ = overlap_ && v[0] != '0';
   TWTML_HIP_CHECK(hipSetDevice(device_));
   hipDeviceProp_t prop;
@@ -434,6 +437,7 @@ void LREngine::prepare(PrepBuf& pb, int slot, int64_t now_ms, hipStream_t s) {
   TWTML_HIP_CHECK(hipSetDevice(device_));
   const int world = world_;
   const int rank = comm_ ? comm_->rank() : 0;
+  Comm* pc = prep_comm_ ? prep_comm_.get() : comm_.get();   // prep-stage collectives
   DevPrepared& prep = pb.dp;
   BatchResult& res = pb.res;
   res = BatchResult{};
@@ -461,7 +465,7 @@ void LREngine::prepare(PrepBuf& pb, int slot, int64_t now_ms, hipStream_t s) {
   if (world > 1) {
     TWTML_HIP_CHECK(hipMemcpyAsync(pb.n_global + 1 + world + rank, prep.counters + 1, sizeof(int64_t),
                                    hipMemcpyDeviceToDevice, s));
-    comm_->allreduce(pb.n_global + 1, size_t(2 * world), ncclInt64, ncclSum, s);
+    pc->allreduce(pb.n_global + 1, size_t(2 * world), ncclInt64, ncclSum, s);
   }
   TWTML_HIP_CHECK(hipMemcpyAsync(hc, prep.counters, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
   TWTML_HIP_CHECK(hipMemcpyAsync(pb.host_norm, raw_.norm_stats(slot), 2 * sizeof(int64_t),
@@ -488,7 +492,7 @@ void LREngine::prepare(PrepBuf& pb, int slot, int64_t now_ms, hipStream_t s) {
         pb.ugather_cap = std::max(need, 2 * pb.ugather_cap);
         pb.ugather = dmalloc<int32_t>(size_t(pb.ugather_cap));
       }
-      comm_->allgather(prep.uniq, pb.ugather, size_t(maxU), ncclInt32, s);
+      pc->allgather(prep.uniq, pb.ugather, size_t(maxU), ncclInt32, s);
       launch_flag_ids(pb.ugather, need, prep, s);
       launch_compact_active(prep, s);
       TWTML_HIP_CHECK(hipMemcpyAsync(hc + 1, prep.counters + 1, sizeof(int64_t), hipMemcpyDeviceToHost, s));
@@ -532,7 +536,7 @@ void LREngine::prepare(PrepBuf& pb, int slot, int64_t now_ms, hipStream_t s) {
     TWTML_HIP_CHECK(hipMemsetAsync(prep.slot_hist + kNumNumeric, 0, sizeof(uint32_t) * size_t(nU), s));
     launch_tier_hist(prep, nU, num_cu_, s);
     // every rank numbers the slots from the same (summed) sampled counts
-    if (world > 1) comm_->allreduce(prep.slot_hist + kNumNumeric, size_t(nU), ncclUint32, ncclSum, s);
+    if (world > 1) pc->allreduce(prep.slot_hist + kNumNumeric, size_t(nU), ncclUint32, ncclSum, s);
     launch_tier_layout(prep, res.entries, nU, n_near, ns, nl, num_cu_, b, fp, lazy, s);
     pb.nl = nl;
     pb.n_near = n_near;
@@ -761,7 +765,10 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
       if (pb_[i].state != 0 && pb_[i].slot == slot) k = i;
     if (k >= 0) {
       cv_.wait(lk, [&] { return pb_[k].state == 2; });
-      if (pb_[k].error || pb_[k].now_ms != now_ms) {   // failed ahead / other batch time: redo in line
+      // prepared ahead with the batch time given at submit; a different time
+      // here is re-prepared on one GPU (DP ranks keep it: a re-prepare would
+      // repeat the prep collectives on this rank only)
+      if (pb_[k].error || (pb_[k].now_ms != now_ms && world_ == 1)) {   // failed ahead / other time
         std::exception_ptr err = pb_[k].error;
         pb_[k].error = nullptr;
         if (err && pb_[k].now_ms == now_ms) {
@@ -780,7 +787,20 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
         if (it->first == slot) { submitted_.erase(it); break; }
       for (int i = 0; i < (overlap_ ? 2 : 1); ++i)
         if (pb_[i].state == 0) k = i;
-      if (k < 0) throw std::logic_error("no free prepared-batch buffer");
+      if (k < 0) {
+        // every buffer holds a batch prepared ahead that is not this one
+        // (submitted but processed out of order): evict one -- its slot goes
+        // back to the front of the queue and is prepared again when due
+        cv_.wait(lk, [&] { return job_ < 0; });
+        for (int i = 0; i < 2 && k < 0; ++i)
+          if (pb_[i].state == 2) {
+            submitted_.push_front({pb_[i].slot, pb_[i].now_ms});
+            pb_[i].state = 0;
+            pb_[i].error = nullptr;
+            k = i;
+          }
+        if (k < 0) throw std::logic_error("no free prepared-batch buffer");
+      }
       pb_[k].state = 1;
       pb_[k].slot = slot;
       pb_[k].now_ms = now_ms;

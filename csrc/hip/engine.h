@@ -156,7 +156,10 @@ struct PrepBuf {
 
 class LREngine {
  public:
-  LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm);
+  // prep_comm (DP, optional): a second communicator over the same ranks for
+  // the prep-stage collectives, which lets batch t+1 be prepared while t's
+  // gradient all-reduces run on `comm`.
+  LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm, std::shared_ptr<Comm> prep_comm = nullptr);
   ~LREngine();
 
   // Async H2D of rows [0, n) of a pinned host batch into device slot `slot`.
@@ -203,6 +206,7 @@ class LREngine {
   int device_;
   LRConfig cfg_;
   std::shared_ptr<Comm> comm_;
+  std::shared_ptr<Comm> prep_comm_;
   int world_ = 1;
   hipStream_t compute_ = nullptr, pstream_ = nullptr, copy_ = nullptr;
   RawSlots raw_;

@@ -23,18 +23,25 @@ def _cfg(F, **kw):
     return LRDeviceConfig(num_text_features=F, max_rows=8192, max_units=8192 * 300, **kw)
 
 
-def _run_dp(world, batches, cfg):
+def _run_dp(world, batches, cfg, prep_group=False):
     from twitter_stream_ml_amd.ops._native import hip
     from twitter_stream_ml_amd.ops.lr_engine import DeviceLinearRegression
     group = hip().LoopbackGroup(world)
-    engines = [DeviceLinearRegression(cfg, device=0, comm=group.comm(r)) for r in range(world)]
+    pgroup = hip().LoopbackGroup(world) if prep_group else None   # prep communicator: prepare-ahead
+    engines = [DeviceLinearRegression(cfg, device=0, comm=group.comm(r),
+                                      prep_comm=pgroup.comm(r) if pgroup else None) for r in range(world)]
     results = [[None] * len(batches) for _ in range(world)]
     errors = []
 
     def worker(r):
         try:
-            for t, full in enumerate(batches):
-                results[r][t] = engines[r].train_batch(full.shard(r, world), want_pred=False)
+            eng = engines[r]
+            shards = [full.shard(r, world) for full in batches]
+            if prep_group:   # queue the shards first: batch t+1 is prepared while t trains
+                for sh in shards[:eng.raw_slots - 1]:
+                    assert eng.prefetch(sh)
+            for t, sh in enumerate(shards):
+                results[r][t] = eng.train_batch(sh, want_pred=False)
         except Exception as e:  # pragma: no cover - surfaced below
             errors.append(e)
 
@@ -47,14 +54,18 @@ def _run_dp(world, batches, cfg):
     return engines, results
 
 
-@pytest.mark.parametrize("world,fraction", [(2, 1.0), (3, 1.0), (2, 0.5)])
-def test_dp_equals_single_engine(hip_module, world, fraction):
+@pytest.mark.parametrize("world,fraction,prep_group", [(2, 1.0, False), (3, 1.0, False), (2, 0.5, False),
+                                                      (2, 1.0, True), (3, 0.5, True)])
+def test_dp_equals_single_engine(hip_module, world, fraction, prep_group):
+    """prep_group: a second (prep) communicator per rank, so every rank
+    prepares batch t+1 -- incl. its kept-count all-reduce and active-id
+    all-gather -- while batch t's gradient all-reduces run."""
     from twitter_stream_ml_amd.ops.lr_engine import DeviceLinearRegression
     F = 1 << 20
     cfg = _cfg(F, fraction=fraction, num_iterations=20)
     synth = SynthConfig.profile("twitter", seed=33, unicode_fraction=0.2)
     batches = [generate_batch(synth, t * 3000, 3000, batch_time_ms=NOW + t) for t in range(3)]
-    engines, res = _run_dp(world, batches, cfg)
+    engines, res = _run_dp(world, batches, cfg, prep_group)
     single = DeviceLinearRegression(cfg, device=0)
     for t, full in enumerate(batches):
         r1 = single.train_batch(full, want_pred=False)

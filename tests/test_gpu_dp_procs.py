@@ -5,7 +5,8 @@ go through the host-staged torch.distributed gloo communicator
 (``parallel/dist.make_comm(..., "gloo")`` -> ``csrc/hip/comm.cpp`` HostComm).
 This is the engine DP path a one-GPU-per-rank RCCL job runs -- per-rank shards,
 per-rank kept counts / sampling offsets, the active-id all-gather union, the
-tiered slot-count all-reduce, the per-iteration gradient all-reduce, stats and
+tiered slot-count all-reduce (on a second, prep communicator while the
+previous batch's per-iteration gradient all-reduces run), stats and
 early-exit agreement -- across real process boundaries; only the transport
 differs (RCCL refuses two ranks on one device).  DP over shards must equal a
 single engine on the concatenated batch, and the replicas must be
@@ -64,13 +65,16 @@ def _worker(rank, world, port, out_dir):
     from twitter_stream_ml_amd.ops.lr_engine import DeviceLinearRegression
     from twitter_stream_ml_amd.parallel import dist as D
     D.init_distributed(backend="gloo")
-    comm = D.make_comm(0, "gloo")
+    comm, prep_comm = D.make_comm_pair(0, "gloo")   # prep communicator: batch t+1 prepared during t
     out = {}
     for ci, (profile, F, hash, rows, nb, _) in enumerate(LR_CASES):
-        eng = DeviceLinearRegression(_lr_cfg(F, hash, rows), device=0, comm=comm)
+        eng = DeviceLinearRegression(_lr_cfg(F, hash, rows), device=0, comm=comm, prep_comm=prep_comm)
         meta = []
-        for full in _batches(profile, rows, nb, seed=40 + ci):
-            r = eng.train_batch(full.shard(rank, world), want_pred=False)
+        shards = [full.shard(rank, world) for full in _batches(profile, rows, nb, seed=40 + ci)]
+        for sh in shards[:eng.raw_slots - 1]:   # queued ahead: exercises the prepare-ahead path
+            eng.prefetch(sh)
+        for sh in shards:
+            r = eng.train_batch(sh, want_pred=False)
             meta.append([r["iterations"], r["n_kept_global"], r["n_unique"], int(r["tiered"])]
                         + list(r["stats"]))
         out[f"lr{ci}_w"] = eng.get_weights()

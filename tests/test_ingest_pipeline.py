@@ -164,3 +164,45 @@ def test_gpu_prefetched_training_matches_synchronous():
     assert b._pipe.hits == 4
     np.testing.assert_allclose(b.get_weights(), wa, rtol=1e-4, atol=1e-10)
     assert np.count_nonzero(b.get_weights()) == np.count_nonzero(wa)
+
+
+@pytest.mark.gpu
+def test_prepare_ahead_out_of_order_and_toggle(hip_module):
+    """Prepare-ahead (batch t+1 prepared on the prep stream while t trains)
+    against the in-line engine: same model; prefetched batches trained out of
+    submission order (the engine evicts a batch it prepared ahead and
+    prepares it again when it is due) still give the in-order result of that
+    order."""
+    import numpy as np
+    from twitter_stream_ml_amd.ops.lr_engine import DeviceLinearRegression, LRDeviceConfig
+    from twitter_stream_ml_amd.sources.synthetic import SynthConfig, generate_batch
+    cfg = SynthConfig.profile("wide", seed=12)
+    batches = [generate_batch(cfg, i * 4096, 4096, batch_time_ms=1_700_000_000_000 + i) for i in range(5)]
+    mk = lambda ov: DeviceLinearRegression(LRDeviceConfig(num_text_features=1 << 20, max_rows=4096,
+                                                          max_units=4096 * 300, overlap=ov), device=0)
+    ref, ahead, ooo = mk(False), mk(True), mk(True)
+    order = [0, 2, 1, 4, 3]
+    for i in order:
+        ref.train_batch(batches[i])
+    for i in order[:3]:
+        assert ahead.prefetch(batches[i])
+    for t, i in enumerate(order):
+        if t + 3 < len(order):
+            ahead.prefetch(batches[order[t + 3]])
+        ahead.train_batch(batches[i])
+    # equal up to the summation order (rows of equal length are placed by
+    # atomics, so two in-line engines differ in the last bits as well)
+    w = ref.get_weights()
+    tol = dict(rtol=1e-4, atol=1e-6 * np.abs(w).max())
+    np.testing.assert_allclose(ahead.get_weights(), w, **tol)
+    # 0, 1, 2 submitted; 0 trains, 1 and 2 get prepared ahead; then 3 (not
+    # prefetched) must evict one of them
+    order2 = [0, 3, 1, 2, 4]
+    ref2 = mk(False)
+    for i in order2:
+        ref2.train_batch(batches[i])
+    for i in (0, 1, 2):
+        assert ooo.prefetch(batches[i])
+    for i in order2:
+        ooo.train_batch(batches[i])
+    np.testing.assert_allclose(ooo.get_weights(), ref2.get_weights(), **tol)

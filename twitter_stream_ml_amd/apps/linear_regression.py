@@ -62,7 +62,7 @@ def build_engine(conf: ConfArguments, rank: int, world: int, device: Optional[in
     F = conf.effectiveNumTextFeatures
     if spec.is_gpu:
         from ..ops.lr_engine import DeviceLinearRegression, LRDeviceConfig
-        from ..parallel.dist import make_rccl_comm
+        from ..parallel.dist import make_comm_pair
         dev = device if device is not None else (spec.devices[rank] if spec.devices else rank)
         from ..parallel.affinity import bind_local_numa
         bind_local_numa(dev)   # pinned staging buffers on the GPU's NUMA node
@@ -71,7 +71,8 @@ def build_engine(conf: ConfArguments, rank: int, world: int, device: Optional[in
                              num_iterations=conf.numIterations, fraction=conf.miniBatchFraction,
                              begin=conf.numRetweetBegin, end=conf.numRetweetEnd,
                              max_rows=rows, max_units=rows * 290)
-        return DeviceLinearRegression(cfg, device=dev, comm=make_rccl_comm(dev) if world > 1 else None)
+        comm, prep_comm = make_comm_pair(dev, "rccl") if world > 1 else (None, None)
+        return DeviceLinearRegression(cfg, device=dev, comm=comm, prep_comm=prep_comm)
     from ..parallel.dist import allreduce_fn
     cfg = CpuLRConfig(num_text_features=F, hash=conf.hash, step_size=conf.stepSize,
                       num_iterations=conf.numIterations, fraction=conf.miniBatchFraction,

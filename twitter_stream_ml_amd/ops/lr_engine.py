@@ -93,8 +93,9 @@ class LRDeviceConfig:
     # device decodes non-ASCII rows and narrows the Latin-1 ones
     ingest: str = "wire"
     # prepare batch t+1 (featurize .. layout, on a prep stream and the
-    # engine's prep thread) while batch t trains; one GPU only (DP ranks
-    # prepare in line: the prep collectives would share the communicator)
+    # engine's prep thread) while batch t trains; DP ranks need a second
+    # communicator for the prep collectives (``prep_comm``), else they
+    # prepare in line
     overlap: bool = True
 
     def as_dict(self) -> Dict[str, object]:
@@ -237,11 +238,12 @@ def unregister_host(arr: np.ndarray) -> None:
 class DeviceLinearRegression:
     """StreamingLinearRegressionWithSGD state + pipeline on one GPU."""
 
-    def __init__(self, cfg: LRDeviceConfig, device: int = 0, comm=None):
+    def __init__(self, cfg: LRDeviceConfig, device: int = 0, comm=None, prep_comm=None):
         self.cfg = cfg
         self.device = int(device)
         self.comm = comm
-        self._eng = hip().LREngine(self.device, cfg.as_dict(), comm)
+        self.prep_comm = prep_comm
+        self._eng = hip().LREngine(self.device, cfg.as_dict(), comm, prep_comm)
         self._staging: List[HostBatchView] = []
         self.raw_slots = int(hip().RAW_SLOTS)
         self._pipe = SlotPipeline(self.raw_slots, lambda s, raw: self.staging(s).load(raw, cfg.ingest),

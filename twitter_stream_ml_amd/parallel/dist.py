@@ -23,7 +23,8 @@ from typing import Callable, Optional
 
 import numpy as np
 
-__all__ = ["DistInfo", "init_distributed", "dist_info", "make_rccl_comm", "make_comm", "allreduce_fn",
+__all__ = ["DistInfo", "init_distributed", "dist_info", "make_rccl_comm", "make_comm", "make_comm_pair",
+           "allreduce_fn",
            "barrier", "allreduce_max_scalar", "allreduce_sum_scalar", "shutdown",
            "check_replicas", "replica_digest", "ReplicaDivergence", "gather_to_main"]
 
@@ -87,11 +88,14 @@ def make_rccl_comm(device: int):
     return h.Comm(obj[0], info.rank, info.world, int(device))
 
 
-def make_comm(device: int, kind: str = "rccl"):
+def make_comm(device: int, kind: str = "rccl", own_group: bool = False):
     """Engine communicator: ``rccl`` (device collectives on the engine stream,
     one GPU per rank) or ``gloo`` (host-staged through torch.distributed
     gloo, so N ranks may share one GPU: the real multi-process engine path,
-    testable on a single MI355X).  None when world == 1."""
+    testable on a single MI355X).  None when world == 1.  ``own_group``:
+    gloo collectives on a process group of their own (a second communicator
+    used concurrently with the first, e.g. the engine's prep communicator;
+    every RCCL communicator is its own)."""
     info = dist_info()
     if info.world <= 1:
         return None
@@ -102,7 +106,7 @@ def make_comm(device: int, kind: str = "rccl"):
     import torch
     import torch.distributed as dist
     from ..ops._native import hip
-    group = None if info.backend == "gloo" else dist.new_group(backend="gloo")
+    group = None if (info.backend == "gloo" and not own_group) else dist.new_group(backend="gloo")
     ops = {0: dist.ReduceOp.SUM, 1: dist.ReduceOp.MAX, 2: dist.ReduceOp.MIN}
     # unsigned buffers reduce as their signed twins (sums wrap identically);
     # MAX / MIN only ever see u8 flags, which torch / gloo handle natively
@@ -121,6 +125,15 @@ def make_comm(device: int, kind: str = "rccl"):
             dist.all_reduce(t, op=ops[op], group=group)
 
     return hip().HostComm(info.rank, info.world, collective)
+
+
+def make_comm_pair(device: int, kind: str = "rccl"):
+    """(gradient communicator, prep communicator) for a DP engine: the
+    second one carries the prep-stage collectives of batch t+1 while batch
+    t's gradient all-reduces run on the first.  (None, None) at world 1."""
+    if dist_info().world <= 1:
+        return None, None
+    return make_comm(device, kind), make_comm(device, kind, own_group=True)
 
 
 def allreduce_fn() -> Optional[Callable[[np.ndarray], np.ndarray]]:
