@@ -71,7 +71,11 @@ def build_engine(conf: ConfArguments, rank: int, world: int, device: Optional[in
                              num_iterations=conf.numIterations, fraction=conf.miniBatchFraction,
                              begin=conf.numRetweetBegin, end=conf.numRetweetEnd,
                              max_rows=rows, max_units=rows * 290)
+        # TWTML_PREP_COMM=1: a second RCCL communicator, so batch t+1 is
+        # prepared while t's gradient all-reduces run (opt-in)
         comm, prep_comm = make_comm_pair(dev, "rccl") if world > 1 else (None, None)
+        if prep_comm is not None and os.environ.get("TWTML_PREP_COMM", "0") != "1":
+            prep_comm = None
         return DeviceLinearRegression(cfg, device=dev, comm=comm, prep_comm=prep_comm)
     from ..parallel.dist import allreduce_fn
     cfg = CpuLRConfig(num_text_features=F, hash=conf.hash, step_size=conf.stepSize,
