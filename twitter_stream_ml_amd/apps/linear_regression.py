@@ -62,7 +62,7 @@ def build_engine(conf: ConfArguments, rank: int, world: int, device: Optional[in
     F = conf.effectiveNumTextFeatures
     if spec.is_gpu:
         from ..ops.lr_engine import DeviceLinearRegression, LRDeviceConfig
-        from ..parallel.dist import make_comm_pair
+        from ..parallel.dist import make_comm, make_comm_pair
         dev = device if device is not None else (spec.devices[rank] if spec.devices else rank)
         from ..parallel.affinity import bind_local_numa
         bind_local_numa(dev)   # pinned staging buffers on the GPU's NUMA node
@@ -73,9 +73,11 @@ def build_engine(conf: ConfArguments, rank: int, world: int, device: Optional[in
                              max_rows=rows, max_units=rows * 290)
         # TWTML_PREP_COMM=1: a second RCCL communicator, so batch t+1 is
         # prepared while t's gradient all-reduces run (opt-in)
-        comm, prep_comm = make_comm_pair(dev, "rccl") if world > 1 else (None, None)
-        if prep_comm is not None and os.environ.get("TWTML_PREP_COMM", "0") != "1":
-            prep_comm = None
+        comm, prep_comm = None, None
+        if world > 1 and os.environ.get("TWTML_PREP_COMM", "0") == "1":
+            comm, prep_comm = make_comm_pair(dev, "rccl")
+        elif world > 1:
+            comm = make_comm(dev, "rccl")
         return DeviceLinearRegression(cfg, device=dev, comm=comm, prep_comm=prep_comm)
     from ..parallel.dist import allreduce_fn
     cfg = CpuLRConfig(num_text_features=F, hash=conf.hash, step_size=conf.stepSize,
