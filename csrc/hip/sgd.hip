@@ -550,7 +550,7 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
     const RowIn ri = row_in(p, pos);
     // far entries of the chunk: their row sums land in lane t == 0 of the row
     float far = 0.f;
-    if (TIERED && fc > 0) {   // wave-uniform
+    if (TIERED && fc > 0 && abl != 8) {   // wave-uniform (ablate 8: no far forward)
       float* fd = fdot[w];
       if (lane < kRowsPerChunk) fd[lane] = 0.f;
       wave_lds_sync();
