@@ -199,16 +199,17 @@ def test_sgd_matches_oracle_over_batches(hip_module, F, dedup, hybrid):
         assert int(n) == fb.n
         np.testing.assert_allclose(sy, fb.y.sum(), rtol=1e-12)
         np.testing.assert_allclose(se2 / n, np.mean((fb.y - pred_o) ** 2), rtol=2e-3)
-        # training
+        # training: the oracle continues from its own weights (no re-seeding),
+        # so errors would accumulate over the warm-started batches
         r = run_minibatch_sgd(fb.X, fb.y, w, 0.005, 50)
         w = r.weights
         wg = eng.get_weights()
         scale = max(np.abs(w).max(), 1e-12)
         assert abs(res["iterations"] - r.iterations) <= 1, (res["iterations"], r.iterations)
-        if res["iterations"] == r.iterations:
-            np.testing.assert_allclose(wg, w, rtol=2e-3, atol=2e-4 * scale)
-        # continue the oracle from the engine's weights so batches stay comparable
-        w = wg.copy()
+        # one iteration more or less moves w by one step below the tolerance (1e-3 |w|)
+        tol = 1e-6 if res["iterations"] == r.iterations else 3e-3
+        assert np.linalg.norm(wg - w) <= tol * max(np.linalg.norm(w), 1e-30), (t, np.linalg.norm(wg - w))
+        np.testing.assert_allclose(wg, w, rtol=2e-3, atol=2e-4 * scale)
 
 
 def test_fraction_sampling_matches_oracle(hip_module):
