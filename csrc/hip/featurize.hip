@@ -291,7 +291,9 @@ __global__ __launch_bounds__(256) void k_cesu_decode(uint8_t* text, const int64_
         const int64_t i = i0 + lane;
         const uint32_t b0 = i < e ? text[i] : 0x80u;
         const bool lead = i < e && (b0 & 0xC0u) != 0x80u;
-        const bool four = lead && b0 >= 0xF0u;
+        // a 4-byte lead needs its 3 continuation bytes inside the row (malformed
+        // input must not write a second unit past the row's 2 * bytes region)
+        const bool four = lead && b0 >= 0xF0u && i + 3 < e;
         const uint64_t lm = __ballot(lead), fm = __ballot(four);
         if (lead) {
           const int64_t at = k + __popcll(lm & lanes_below()) + __popcll(fm & lanes_below());

@@ -360,3 +360,39 @@ def test_wide_murmur3_hybrid_matches_plain_remap(hip_module):
         np.testing.assert_allclose(ra["loss_history"], rb["loss_history"], rtol=1e-5)
     wb = b.get_weights()
     np.testing.assert_allclose(a.get_weights(), wb, rtol=1e-4, atol=1e-6 * max(np.abs(wb).max(), 1e-12))
+
+
+def test_utf8_truncated_sequences_stay_in_their_row(hip_module):
+    """Malformed UTF-8 from a receiver (a 4-byte lead with its continuation
+    bytes missing at a row end, stray continuation bytes) garbles only its
+    own row: every other row featurizes exactly as the oracle."""
+    from twitter_stream_ml_amd.ops.lr_engine import Utf8Text, encode_utf8
+    cfg = SynthConfig.profile("twitter", seed=23, unicode_fraction=0.3)
+    raw = generate_batch(cfg, 0, 800, batch_time_ms=NOW)
+    raw.is_retweet[:] = 1
+    raw.scalars[0, :] = 500
+    u8 = encode_utf8(raw)
+    bad = set(range(5, raw.n, 37))
+    parts, off = [], [0]
+    for i in range(raw.n):
+        b = bytes(u8.data[u8.offsets[i]:u8.offsets[i + 1]])
+        if i in bad:
+            b = b + (b"\xf0" if i % 2 else b"\x80\xf0\x9f")   # truncated lead / stray continuation
+        parts.append(b)
+        off.append(off[-1] + len(b))
+    bad_u8 = Utf8Text(np.frombuffer(b"".join(parts), np.uint8).copy(), np.asarray(off, np.int64))
+    eng = _engine(1 << 20, lazy_idx=False, ingest="utf8")
+    hb = eng.staging(0).load_utf8(raw, bad_u8, copy_text=True)
+    eng.submit(hb, 0)
+    eng.process(0, NOW)
+    dbg = eng._eng.debug_prepared()
+    fb = featurize_batch(raw, 1 << 20, 100, 1000, now_ms=NOW)
+    assert int(dbg["counters"][0]) == fb.n == raw.n
+    rows = _rows_from_debug(dbg)
+    Xt = fb.X[:, :1 << 20].tocsr()
+    for k in range(fb.n):
+        if k in bad:
+            continue
+        s, e = Xt.indptr[k], Xt.indptr[k + 1]
+        want = np.repeat(Xt.indices[s:e], Xt.data[s:e].astype(np.int64))
+        np.testing.assert_array_equal(rows[k], np.sort(want), err_msg=f"row {k}")
