@@ -169,3 +169,30 @@ def test_kmeans_dp_loopback(hip_module, world):
         exact += n_ill == 0
         single.set_state(*states[0][t])
     assert exact >= 1   # at least one batch compared exactly
+
+
+def test_kmeans_utf8_ingest_equals_wire(hip_module):
+    """The end-to-end bench stages k-means batches as raw UTF-8 (device
+    decode); the engine state must match the host-packed wire ingest."""
+    from twitter_stream_ml_amd.ops.kmeans_engine import DeviceKMeans
+    from twitter_stream_ml_amd.ops.lr_engine import encode_utf8
+    cfg = _cfg(16, 14, seed=6)
+    a, b = DeviceKMeans(cfg, device=0), DeviceKMeans(cfg, device=0)
+    for raw in _batches(n=3, seed=31, unicode_fraction=0.3, special_fraction=0.02):
+        ra = a.update_raw(raw)
+        hb = b.staging(0).load_utf8(raw, encode_utf8(raw), copy_text=True)
+        b.submit(hb, 0)
+        rb = b.process(0)
+        assert ra["n"] == rb["n"]
+        np.testing.assert_allclose(rb["std"], ra["std"], rtol=1e-12)
+    # the two ingest paths order rows differently (fp64 sums in another
+    # order), which may flip a point that is equidistant from the two halves
+    # of a just-split cluster (see test_kmeans_matches_cpu): weights move by
+    # a point, their total is conserved, the other clusters agree
+    ca, wa = a.get_state()
+    cb, wb = b.get_state()
+    np.testing.assert_allclose(wb.sum(), wa.sum(), rtol=1e-12)
+    assert np.abs(wb - wa).sum() <= 4.0, (wa, wb)
+    same = np.abs(wb - wa) <= 1e-9 * np.maximum(np.abs(wa), 1.0)
+    assert same.sum() >= len(wa) - 4
+    np.testing.assert_allclose(cb[same], ca[same], rtol=1e-6, atol=1e-9)
