@@ -194,10 +194,13 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm, 
   world_ = comm_ ? comm_->world() : 1;
   if (prep_comm_ && (prep_comm_->world() != world_ || prep_comm_->rank() != comm_->rank()))
     throw std::invalid_argument("prep communicator must span the same ranks");
-  // Prepare-ahead runs the prep-stage collectives (kept counts, active-id
-  // union, tier counts) concurrently with the gradient all-reduces, so DP
-  // ranks need a second communicator for them (one GPU: no collectives).
-  overlap_ = cfg_.overlap != 0 && (world_ == 1 || prep_comm_ != nullptr);
+  // Prepare-ahead: the local part of batch t+1's prep (decode .. featurize
+  // .. this rank's active set) always; its collective part (kept counts,
+  // active-id union, tier counts) + layout only on one GPU or with a second
+  // communicator, since it would run concurrently with t's gradient
+  // all-reduces.
+  overlap_ = cfg_.overlap != 0;
+  ahead_global_ = world_ == 1 || prep_comm_ != nullptr;
   if (const char* v = std::getenv("TWTML_OVERLAP")) overlap_ = overlap_ && v[0] != '0';
   TWTML_HIP_CHECK(hipSetDevice(device_));
   hipDeviceProp_t prop;
@@ -432,12 +435,17 @@ void LREngine::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, c
 // prepare: filter .. layout of one raw slot into a PrepBuf, on stream `s`
 // (the prep stream; host syncs for the batch's counts stay on this thread).
 // ---------------------------------------------------------------------------
-void LREngine::prepare(PrepBuf& pb, int slot, int64_t now_ms, hipStream_t s) {
+void LREngine::prepare(PrepBuf& pb, int slot, int64_t now_ms, hipStream_t s, bool global) {
+  prepare_local(pb, slot, now_ms, s);
+  if (global) prepare_global(pb, s);
+}
+
+// Local part (no collectives): decode / lower rows, filter, sort, chunk
+// layout, featurize, this rank's active set; ends with its counts on the host.
+void LREngine::prepare_local(PrepBuf& pb, int slot, int64_t now_ms, hipStream_t s) {
   TraceRange tr_prep("twtml.lr.prep");   // filter .. remap
   TWTML_HIP_CHECK(hipSetDevice(device_));
   const int world = world_;
-  const int rank = comm_ ? comm_->rank() : 0;
-  Comm* pc = prep_comm_ ? prep_comm_.get() : comm_.get();   // prep-stage collectives
   DevPrepared& prep = pb.dp;
   BatchResult& res = pb.res;
   res = BatchResult{};
@@ -457,6 +465,34 @@ void LREngine::prepare(PrepBuf& pb, int slot, int64_t now_ms, hipStream_t s) {
   launch_featurize(b, prep, fp, lower_page_, lower_blocks_, s);
   if (!lazy) raw_.release_slot(slot, s);  // raw slot may be overwritten now
   launch_compact_active(prep, s);        // this rank's active ids (clears the flags)
+  TWTML_HIP_CHECK(hipMemcpyAsync(pb.host_counters, prep.counters, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  TWTML_HIP_CHECK(hipMemcpyAsync(pb.host_norm, raw_.norm_stats(slot), 2 * sizeof(int64_t),
+                                 hipMemcpyDeviceToHost, s));
+  TWTML_HIP_CHECK(hipStreamSynchronize(s));
+  if (pb.host_counters[3] != 0) throw std::runtime_error("feature buffer capacity exceeded");
+  pb.raw = b;
+  pb.fp = fp;
+  pb.lazy = lazy;
+  pb.slot = slot;
+  pb.stage = 1;
+}
+
+// Global part: per-rank counts and the active-id union across ranks (the
+// prep collectives), then the hybrid / tiered layout.  On one GPU, or with a
+// prep communicator, it runs ahead with the local part; DP ranks without one
+// run it in line on the compute stream, after the previous batch trained.
+void LREngine::prepare_global(PrepBuf& pb, hipStream_t s) {
+  TraceRange tr_prep("twtml.lr.prep_global");
+  TWTML_HIP_CHECK(hipSetDevice(device_));
+  const int world = world_;
+  const int rank = comm_ ? comm_->rank() : 0;
+  Comm* pc = prep_comm_ ? prep_comm_.get() : comm_.get();   // prep-stage collectives
+  DevPrepared& prep = pb.dp;
+  BatchResult& res = pb.res;
+  const DevRawBatch& b = pb.raw;
+  const FeaturizeParams& fp = pb.fp;
+  const bool lazy = pb.lazy;
+  const int slot = pb.slot;
   // per-rank kept rows (sampling offsets, global m) and active-set sizes:
   // n_global[1 + r] / n_global[1 + world + r], one small all-reduce
   int64_t* hc = pb.host_counters;
@@ -467,13 +503,9 @@ void LREngine::prepare(PrepBuf& pb, int slot, int64_t now_ms, hipStream_t s) {
                                    hipMemcpyDeviceToDevice, s));
     pc->allreduce(pb.n_global + 1, size_t(2 * world), ncclInt64, ncclSum, s);
   }
-  TWTML_HIP_CHECK(hipMemcpyAsync(hc, prep.counters, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  TWTML_HIP_CHECK(hipMemcpyAsync(pb.host_norm, raw_.norm_stats(slot), 2 * sizeof(int64_t),
-                                 hipMemcpyDeviceToHost, s));
   TWTML_HIP_CHECK(hipMemcpyAsync(hc + 8, pb.n_global + 1, sizeof(int64_t) * size_t(2 * world),
                                  hipMemcpyDeviceToHost, s));
   TWTML_HIP_CHECK(hipStreamSynchronize(s));
-  if (hc[3] != 0) throw std::runtime_error("feature buffer capacity exceeded");
   const int64_t* per_rank = hc + 8;
   if (world > 1) {
     // Active-set union: every rank numbers the same slots.  Each rank's
@@ -552,6 +584,7 @@ void LREngine::prepare(PrepBuf& pb, int slot, int64_t now_ms, hipStream_t s) {
   if (prep.dedup) launch_dedup(prep, ns, kNumNumeric + nU, res.n_kept, s);
   res.n_near = pb.n_near;
   TWTML_HIP_CHECK(hipEventRecord(pb.ev_done, s));
+  pb.stage = 2;
 }
 
 // ---------------------------------------------------------------------------
@@ -723,7 +756,7 @@ void LREngine::prep_worker() {
     lk.unlock();
     std::exception_ptr err;
     try {
-      prepare(b, slot, now_ms, pstream_);
+      prepare(b, slot, now_ms, pstream_, ahead_global_);
     } catch (...) {
       err = std::current_exception();
     }
@@ -777,7 +810,7 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
         }
         pb_[k].state = 1;
         lk.unlock();
-        prepare(pb_[k], slot, now_ms, pstream_);
+        prepare(pb_[k], slot, now_ms, pstream_, true);
         lk.lock();
         pb_[k].state = 2;
       }
@@ -806,7 +839,7 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
       pb_[k].now_ms = now_ms;
       lk.unlock();
       try {
-        prepare(pb_[k], slot, now_ms, pstream_);
+        prepare(pb_[k], slot, now_ms, pstream_, true);
       } catch (...) {
         lk.lock();
         pb_[k].state = 0;
@@ -820,6 +853,9 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   }
   BatchResult res;
   try {
+    // DP ranks without a prep communicator prepared only the local part
+    // ahead: the collectives + layout run here, on the compute stream
+    if (pb_[k].stage < 2) prepare_global(pb_[k], compute_);
     res = train(pb_[k], want_pred);
   } catch (...) {
     std::lock_guard<std::mutex> lk(mu_);

@@ -148,6 +148,10 @@ struct PrepBuf {
   int64_t now_ms = 0;
   std::exception_ptr error;
   // prepare() outputs
+  int stage = 0;                      // 1: local part done (prepare_local), 2: ready to train
+  DevRawBatch raw{};                  // the raw slot's device view (global part, lazy remap)
+  FeaturizeParams fp{};
+  bool lazy = false;
   BatchResult res;                    // n_raw .. n_near, rows lowered / narrowed
   int64_t row_offset = 0;             // global index of this rank's first kept row
   bool u16 = true;
@@ -196,7 +200,9 @@ class LREngine {
   void ensure_compact(int64_t ns);
   void ensure_part(int64_t n);
   void ensure_tier(PrepBuf& b, int64_t n_unique, hipStream_t s);
-  void prepare(PrepBuf& b, int slot, int64_t now_ms, hipStream_t s);
+  void prepare(PrepBuf& b, int slot, int64_t now_ms, hipStream_t s, bool global);
+  void prepare_local(PrepBuf& b, int slot, int64_t now_ms, hipStream_t s);
+  void prepare_global(PrepBuf& b, hipStream_t s);
   BatchResult train(PrepBuf& b, bool want_pred);
   void prep_worker();
   void schedule_ahead_locked();
@@ -213,6 +219,7 @@ class LREngine {
   PrepBuf pb_[2];
   int last_buf_ = -1;               // buffer of the last trained batch (debug_*)
   bool overlap_ = true;
+  bool ahead_global_ = true;        // prepare-ahead includes the collective part + layout
   // prepare-ahead: submitted slots in order, the prep thread's job (a pb_ index)
   std::mutex mu_;
   std::condition_variable cv_;

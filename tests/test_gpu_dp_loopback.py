@@ -37,9 +37,11 @@ def _run_dp(world, batches, cfg, prep_group=False):
         try:
             eng = engines[r]
             shards = [full.shard(r, world) for full in batches]
-            if prep_group:   # queue the shards first: batch t+1 is prepared while t trains
-                for sh in shards[:eng.raw_slots - 1]:
-                    assert eng.prefetch(sh)
+            # queue the shards first: batch t+1 is prepared while t trains --
+            # only its local part without a prep communicator (the collective
+            # part then runs in line), all of it with one
+            for sh in shards[:eng.raw_slots - 1]:
+                assert eng.prefetch(sh)
             for t, sh in enumerate(shards):
                 results[r][t] = eng.train_batch(sh, want_pred=False)
         except Exception as e:  # pragma: no cover - surfaced below
