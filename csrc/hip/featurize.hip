@@ -251,24 +251,32 @@ __device__ __forceinline__ uint64_t lanes_below() {
   return (uint64_t(1) << lane_id()) - 1u;
 }
 
-__device__ __forceinline__ bool row_is_ascii(const uint8_t* text, int64_t o, int64_t e) {
-  // aligned dwords covering [o, e), bytes outside the row masked off
+// Row class from its bytes (aligned dword loads, bytes outside [o, e)
+// masked off): 0 ASCII, 1 Latin-1 (valid UTF-8 whose bytes are all < 0xC4,
+// i.e. every code point < U+0100), 2 other.
+__device__ __forceinline__ int row_class(const uint8_t* text, int64_t o, int64_t e) {
   const int64_t a0 = o & ~int64_t(3);
   uint32_t acc = 0;
+  bool big = false;
   for (int64_t w = a0 + 4 * lane_id(); w < e; w += 4 * kWave) {
     uint32_t v = *reinterpret_cast<const uint32_t*>(text + w);
     if (w < o) v &= 0xFFFFFFFFu << (8 * (o - w));
     if (w + 4 > e) v &= 0xFFFFFFFFu >> (8 * (w + 4 - e));
     acc |= v;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) big |= ((v >> (8 * k)) & 0xFFu) >= 0xC4u;
   }
-  return !__any((acc & 0x80808080u) != 0u);
+  if (__any(big)) return 2;
+  return __any((acc & 0x80808080u) != 0u) ? 1 : 0;
 }
 
 __global__ __launch_bounds__(256) void k_cesu_decode(uint8_t* text, const int64_t* offsets, uint8_t* flags,
-                                                     int64_t n, int64_t tail, int64_t* rstart, int64_t* rend) {
+                                                     int64_t n, int64_t tail, int64_t* rstart, int64_t* rend,
+                                                     int64_t* stats) {
   const int lane = lane_id();
   const int64_t wave = (int64_t(blockIdx.x) * 256 + threadIdx.x) / kWave;
   const int64_t nwaves = int64_t(gridDim.x) * 256 / kWave;
+  int n_nar = 0;
   for (int64_t g = wave; g * kWave < n; g += nwaves) {
     const int64_t r = g * kWave + lane;
     uint8_t fl = r < n ? flags[r] : 0;
@@ -280,12 +288,17 @@ __global__ __launch_bounds__(256) void k_cesu_decode(uint8_t* text, const int64_
       m &= m - 1;
       const int64_t rr = g * kWave + l;
       const int64_t o = offsets[rr], e = offsets[rr + 1];
-      if (row_is_ascii(text, o, e)) {   // narrow row as it is
+      const int cls = row_class(text, o, e);
+      if (cls == 0) {   // ASCII: narrow row as it is
         if (lane == l) fl = uint8_t(fl & ~kRowCesu);
         continue;
       }
+      // Latin-1 rows decode straight to narrow bytes (no UTF-16 pass, no
+      // narrowing pass in k_row_normalize); others to UTF-16
+      const bool nar = cls == 1;
       const int64_t d0 = tail + 2 * o;
       uint16_t* dst = reinterpret_cast<uint16_t*>(text + d0);
+      uint8_t* dst8 = text + d0;
       int64_t k = 0;
       for (int64_t i0 = o; i0 < e; i0 += kWave) {
         const int64_t i = i0 + lane;
@@ -307,16 +320,18 @@ __global__ __launch_bounds__(256) void k_cesu_decode(uint8_t* text, const int64_
           } else {
             if (b0 >= 0xE0u) u = ((b0 & 0x0Fu) << 12) | ((text[i + 1] & 0x3Fu) << 6) | (text[i + 2] & 0x3Fu);
             else if (b0 >= 0x80u) u = ((b0 & 0x1Fu) << 6) | (text[i + 1] & 0x3Fu);
-            dst[at] = uint16_t(u);
+            if (nar) dst8[at] = uint8_t(u);
+            else dst[at] = uint16_t(u);
           }
         }
         k += __popcll(lm) + __popcll(fm);
       }
       if (lane == l) {
         s0 = d0;
-        s1 = d0 + 2 * k;
-        fl = uint8_t((fl & ~kRowCesu) | kRowWide);
+        s1 = d0 + (nar ? k : 2 * k);
+        fl = nar ? uint8_t(fl & ~kRowCesu) : uint8_t((fl & ~kRowCesu) | kRowWide);
       }
+      n_nar += nar ? 1 : 0;
     }
     if (r < n) {
       rstart[r] = s0;
@@ -324,14 +339,16 @@ __global__ __launch_bounds__(256) void k_cesu_decode(uint8_t* text, const int64_
       if (mine) flags[r] = fl;
     }
   }
+  if (stats && lane == 0 && n_nar) atomicAdd(reinterpret_cast<unsigned long long*>(&stats[1]), (unsigned long long)n_nar);
 }
 
 void launch_cesu_expand(uint8_t* text, const int64_t* offsets, uint8_t* flags, int64_t n, int64_t tail,
-                        int64_t* rstart, int64_t* rend, hipStream_t s) {
+                        int64_t* rstart, int64_t* rend, int64_t* stats, hipStream_t s) {
   if (n <= 0) return;
   // one wave per 64 rows, ~4 waves per SIMD
   const int grid = int(std::min<int64_t>((n + 255) / 256, 4096));
-  hipLaunchKernelGGL(k_cesu_decode, dim3(grid), dim3(256), 0, s, text, offsets, flags, n, tail, rstart, rend);
+  hipLaunchKernelGGL(k_cesu_decode, dim3(grid), dim3(256), 0, s, text, offsets, flags, n, tail, rstart, rend,
+                     stats);
 }
 
 // nnz[k] carries the row's bigram count in bits 0..29 and the wide (UTF-16

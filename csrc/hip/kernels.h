@@ -62,11 +62,13 @@ constexpr uint8_t kRowCesu = 4;   // wire only (csrc/host/wire.h); expanded by l
 // Packed row words on the wire (HostBatch::pack_rows): byte length in the
 // low kRowLenBits bits, the three flag bits above.
 constexpr int kRowLenBits = 13;
-// cesu rows -> UTF-16LE rows behind the wire bytes (row with wire bytes
-// [o, e) -> from byte tail + 2 * o); writes every row's start / end offset
-// and turns the cesu rows' flags wide.  text needs tail + 2 * bytes + 64.
+// cesu / UTF-8 rows -> rows behind the wire bytes (row with wire bytes
+// [o, e) -> from byte tail + 2 * o): UTF-16LE (flag wide), or narrow bytes
+// for Latin-1 rows; ASCII rows stay in place.  Writes every row's start /
+// end offset; stats[1] (nullable) counts the rows decoded to narrow bytes.
+// text needs tail + 2 * bytes + 64.
 void launch_cesu_expand(uint8_t* text, const int64_t* offsets, uint8_t* flags, int64_t n, int64_t tail,
-                        int64_t* rstart, int64_t* rend, hipStream_t s);
+                        int64_t* rstart, int64_t* rend, int64_t* stats, hipStream_t s);
 // Rebuild offsets [n+1] (exclusive scan of the lengths) and flags [n] from
 // packed row words on `s`; tsum: scratch of ceil(n / 8192) int64.
 void launch_unpack_rows(const uint16_t* rowpack, int64_t n, int64_t* offsets, uint8_t* flags, int64_t* tsum,

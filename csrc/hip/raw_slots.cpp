@@ -130,12 +130,12 @@ DevRawBatch RawSlots::acquire(int slot, hipStream_t compute) {
   b.oend = s.offsets + 1;
   b.flags = s.flags;
   const int64_t tail = (s.bytes + 15) / 16 * 16;
-  if (s.cesu_rows > 0) {   // expand cesu rows behind the wire bytes (16-byte aligned)
-    launch_cesu_expand(s.text, s.offsets, s.flags, s.n, tail, s.rstart, s.rend, compute);
+  TWTML_HIP_CHECK(hipMemsetAsync(s.nstats, 0, 2 * sizeof(int64_t), compute));
+  if (s.cesu_rows > 0) {   // expand cesu / UTF-8 rows behind the wire bytes (16-byte aligned)
+    launch_cesu_expand(s.text, s.offsets, s.flags, s.n, tail, s.rstart, s.rend, s.nstats, compute);
     b.offsets = s.rstart;
     b.oend = s.rend;
   }
-  TWTML_HIP_CHECK(hipMemsetAsync(s.nstats, 0, 2 * sizeof(int64_t), compute));
   if (s.utf16 || s.cesu_rows > 0 || s.wide_rows > 0) {
     // special rows -> fully lower-cased UTF-16; UTF-16 / UTF-8 batches: Latin-1
     // rows narrowed (a decoded UTF-8 row in place: byte i <- unit i, forward)
