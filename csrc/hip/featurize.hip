@@ -251,15 +251,38 @@ __device__ __forceinline__ uint64_t lanes_below() {
   return (uint64_t(1) << lane_id()) - 1u;
 }
 
-// Row class from its bytes (aligned dword loads, bytes outside [o, e)
-// masked off): 0 ASCII, 1 Latin-1 (valid UTF-8 whose bytes are all < 0xC4,
-// i.e. every code point < U+0100), 2 other.
-__device__ __forceinline__ int row_class(const uint8_t* text, int64_t o, int64_t e) {
+__device__ __forceinline__ int64_t bcast_lane64(int64_t v, int l) {
+  const uint32_t lo = uint32_t(__builtin_amdgcn_readlane(int32_t(uint32_t(v)), l));
+  const uint32_t hi = uint32_t(__builtin_amdgcn_readlane(int32_t(uint32_t(uint64_t(v) >> 32)), l));
+  return int64_t((uint64_t(hi) << 32) | lo);
+}
+
+// Byte readers of the decode: the wave's staged LDS copy of its 64-row group,
+// or global memory (groups too long to stage).
+struct GlobalBytes {
+  const uint8_t* text;
+  __device__ __forceinline__ uint32_t byte(int64_t i) const { return text[i]; }
+  __device__ __forceinline__ uint32_t dword(int64_t w) const { return *reinterpret_cast<const uint32_t*>(text + w); }
+};
+struct LdsBytes {
+  const uint8_t* lds;   // staged bytes of [a0, a0 + staged)
+  int64_t a0;
+  __device__ __forceinline__ uint32_t byte(int64_t i) const { return lds[i - a0]; }
+  __device__ __forceinline__ uint32_t dword(int64_t w) const {
+    return *reinterpret_cast<const uint32_t*>(lds + (w - a0));
+  }
+};
+
+// Row class from its bytes (aligned dwords, bytes outside [o, e) masked
+// off): 0 ASCII, 1 Latin-1 (valid UTF-8 whose bytes are all < 0xC4, i.e.
+// every code point < U+0100), 2 other.
+template <typename Src>
+__device__ __forceinline__ int row_class(const Src& src, int64_t o, int64_t e) {
   const int64_t a0 = o & ~int64_t(3);
   uint32_t acc = 0;
   bool big = false;
   for (int64_t w = a0 + 4 * lane_id(); w < e; w += 4 * kWave) {
-    uint32_t v = *reinterpret_cast<const uint32_t*>(text + w);
+    uint32_t v = src.dword(w);
     if (w < o) v &= 0xFFFFFFFFu << (8 * (o - w));
     if (w + 4 > e) v &= 0xFFFFFFFFu >> (8 * (w + 4 - e));
     acc |= v;
@@ -270,12 +293,60 @@ __device__ __forceinline__ int row_class(const uint8_t* text, int64_t o, int64_t
   return __any((acc & 0x80808080u) != 0u) ? 1 : 0;
 }
 
-__global__ __launch_bounds__(256) void k_cesu_decode(uint8_t* text, const int64_t* offsets, uint8_t* flags,
-                                                     int64_t n, int64_t tail, int64_t* rstart, int64_t* rend,
-                                                     int64_t* stats) {
+// Decode row [o, e) (class 1 or 2) to dst (tail + 2 o); returns its units.
+template <typename Src>
+__device__ __forceinline__ int64_t decode_row(const Src& src, uint8_t* text, int64_t o, int64_t e, int64_t d0,
+                                              bool nar) {
+  uint16_t* dst = reinterpret_cast<uint16_t*>(text + d0);
+  uint8_t* dst8 = text + d0;
   const int lane = lane_id();
-  const int64_t wave = (int64_t(blockIdx.x) * 256 + threadIdx.x) / kWave;
-  const int64_t nwaves = int64_t(gridDim.x) * 256 / kWave;
+  int64_t k = 0;
+  for (int64_t i0 = o; i0 < e; i0 += kWave) {
+    const int64_t i = i0 + lane;
+    const uint32_t b0 = i < e ? src.byte(i) : 0x80u;
+    const bool lead = i < e && (b0 & 0xC0u) != 0x80u;
+    // a 4-byte lead needs its 3 continuation bytes inside the row (malformed
+    // input must not write a second unit past the row's 2 * bytes region)
+    const bool four = lead && b0 >= 0xF0u && i + 3 < e;
+    const uint64_t lm = __ballot(lead), fm = __ballot(four);
+    if (lead) {
+      const int64_t at = k + __popcll(lm & lanes_below()) + __popcll(fm & lanes_below());
+      uint32_t u = b0;
+      if (four) {
+        const uint32_t cp = ((b0 & 0x07u) << 18) | ((src.byte(i + 1) & 0x3Fu) << 12) |
+                            ((src.byte(i + 2) & 0x3Fu) << 6) | (src.byte(i + 3) & 0x3Fu);
+        dst[at] = uint16_t(0xD800u + ((cp - 0x10000u) >> 10));
+        u = 0xDC00u + ((cp - 0x10000u) & 0x3FFu);
+        dst[at + 1] = uint16_t(u);
+      } else {
+        if (b0 >= 0xE0u) u = ((b0 & 0x0Fu) << 12) | ((src.byte(i + 1) & 0x3Fu) << 6) | (src.byte(i + 2) & 0x3Fu);
+        else if (b0 >= 0x80u) u = ((b0 & 0x1Fu) << 6) | (src.byte(i + 1) & 0x3Fu);
+        if (nar) dst8[at] = uint8_t(u);
+        else dst[at] = uint16_t(u);
+      }
+    }
+    k += __popcll(lm) + __popcll(fm);
+  }
+  return k;
+}
+
+// LDS staging per wave: the 64 rows of a group are consecutive on the wire,
+// so their bytes are one range, loaded with 16-B loads (8 per lane in
+// flight) -- one memory round trip per group instead of several per row.
+constexpr int kDecStage = 12288;   // bytes per wave (groups beyond: global reads)
+constexpr int kDecWaves = 4;
+
+__global__ __launch_bounds__(kDecWaves * kWave) void k_cesu_decode(uint8_t* text, const int64_t* offsets,
+                                                                   uint8_t* flags, int64_t n, int64_t tail,
+                                                                   int64_t* rstart, int64_t* rend,
+                                                                   int64_t* stats) {
+  __shared__ __attribute__((aligned(16))) uint8_t stage[kDecWaves][kDecStage + 16];
+  const int lane = lane_id();
+  const int wv = threadIdx.x / kWave;
+  uint8_t* lbuf = stage[wv];
+  const int64_t wave = (int64_t(blockIdx.x) * kDecWaves * kWave + threadIdx.x) / kWave;
+  const int64_t nwaves = int64_t(gridDim.x) * kDecWaves;
+  const GlobalBytes gsrc{text};
   int n_nar = 0;
   for (int64_t g = wave; g * kWave < n; g += nwaves) {
     const int64_t r = g * kWave + lane;
@@ -283,12 +354,37 @@ __global__ __launch_bounds__(256) void k_cesu_decode(uint8_t* text, const int64_
     const bool mine = r < n && (fl & kRowCesu);
     int64_t s0 = r < n ? offsets[r] : 0, s1 = r < n ? offsets[r + 1] : 0;
     uint64_t m = __ballot(mine);
+    // stage the group's byte range if it fits
+    const int last = int(std::min<int64_t>(kWave, n - g * kWave)) - 1;
+    const int64_t gs = offsets[g * kWave], ge = offsets[g * kWave + last + 1];
+    const int64_t a0 = gs & ~int64_t(15);
+    const bool staged = m != 0 && ge - a0 <= kDecStage;
+    if (staged) {
+      const int64_t nq = (ge - a0 + 15) >> 4;   // 16-B chunks
+      for (int64_t q0 = 0; q0 < nq; q0 += 8 * kWave) {
+        uint4 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int64_t q = q0 + j * kWave + lane;
+          v[j] = q < nq ? *reinterpret_cast<const uint4*>(text + a0 + 16 * q) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int64_t q = q0 + j * kWave + lane;
+          if (q < nq) *reinterpret_cast<uint4*>(lbuf + 16 * q) = v[j];
+        }
+      }
+      __threadfence_block();
+      __builtin_amdgcn_wave_barrier();
+    }
+    const LdsBytes lsrc{lbuf, a0};
     while (m) {
       const int l = __builtin_ctzll(m);
       m &= m - 1;
-      const int64_t rr = g * kWave + l;
-      const int64_t o = offsets[rr], e = offsets[rr + 1];
-      const int cls = row_class(text, o, e);
+      // the row's extents from lane l's registers (a load here would put a
+      // memory round trip on every row of the wave's sequential walk)
+      const int64_t o = bcast_lane64(s0, l), e = bcast_lane64(s1, l);
+      const int cls = staged ? row_class(lsrc, o, e) : row_class(gsrc, o, e);
       if (cls == 0) {   // ASCII: narrow row as it is
         if (lane == l) fl = uint8_t(fl & ~kRowCesu);
         continue;
@@ -297,35 +393,7 @@ __global__ __launch_bounds__(256) void k_cesu_decode(uint8_t* text, const int64_
       // narrowing pass in k_row_normalize); others to UTF-16
       const bool nar = cls == 1;
       const int64_t d0 = tail + 2 * o;
-      uint16_t* dst = reinterpret_cast<uint16_t*>(text + d0);
-      uint8_t* dst8 = text + d0;
-      int64_t k = 0;
-      for (int64_t i0 = o; i0 < e; i0 += kWave) {
-        const int64_t i = i0 + lane;
-        const uint32_t b0 = i < e ? text[i] : 0x80u;
-        const bool lead = i < e && (b0 & 0xC0u) != 0x80u;
-        // a 4-byte lead needs its 3 continuation bytes inside the row (malformed
-        // input must not write a second unit past the row's 2 * bytes region)
-        const bool four = lead && b0 >= 0xF0u && i + 3 < e;
-        const uint64_t lm = __ballot(lead), fm = __ballot(four);
-        if (lead) {
-          const int64_t at = k + __popcll(lm & lanes_below()) + __popcll(fm & lanes_below());
-          uint32_t u = b0;
-          if (four) {
-            const uint32_t cp = ((b0 & 0x07u) << 18) | ((text[i + 1] & 0x3Fu) << 12) |
-                                ((text[i + 2] & 0x3Fu) << 6) | (text[i + 3] & 0x3Fu);
-            dst[at] = uint16_t(0xD800u + ((cp - 0x10000u) >> 10));
-            u = 0xDC00u + ((cp - 0x10000u) & 0x3FFu);
-            dst[at + 1] = uint16_t(u);
-          } else {
-            if (b0 >= 0xE0u) u = ((b0 & 0x0Fu) << 12) | ((text[i + 1] & 0x3Fu) << 6) | (text[i + 2] & 0x3Fu);
-            else if (b0 >= 0x80u) u = ((b0 & 0x1Fu) << 6) | (text[i + 1] & 0x3Fu);
-            if (nar) dst8[at] = uint8_t(u);
-            else dst[at] = uint16_t(u);
-          }
-        }
-        k += __popcll(lm) + __popcll(fm);
-      }
+      const int64_t k = staged ? decode_row(lsrc, text, o, e, d0, nar) : decode_row(gsrc, text, o, e, d0, nar);
       if (lane == l) {
         s0 = d0;
         s1 = d0 + (nar ? k : 2 * k);
@@ -338,6 +406,7 @@ __global__ __launch_bounds__(256) void k_cesu_decode(uint8_t* text, const int64_
       rend[r] = s1;
       if (mine) flags[r] = fl;
     }
+    __builtin_amdgcn_wave_barrier();   // LDS reads of this group precede the next staging
   }
   if (stats && lane == 0 && n_nar) atomicAdd(reinterpret_cast<unsigned long long*>(&stats[1]), (unsigned long long)n_nar);
 }
@@ -345,10 +414,10 @@ __global__ __launch_bounds__(256) void k_cesu_decode(uint8_t* text, const int64_
 void launch_cesu_expand(uint8_t* text, const int64_t* offsets, uint8_t* flags, int64_t n, int64_t tail,
                         int64_t* rstart, int64_t* rend, int64_t* stats, hipStream_t s) {
   if (n <= 0) return;
-  // one wave per 64 rows, ~4 waves per SIMD
-  const int grid = int(std::min<int64_t>((n + 255) / 256, 4096));
-  hipLaunchKernelGGL(k_cesu_decode, dim3(grid), dim3(256), 0, s, text, offsets, flags, n, tail, rstart, rend,
-                     stats);
+  // one wave per 64-row group, 4 waves (48 KB of staging) per workgroup
+  const int grid = int(std::min<int64_t>((n + kDecWaves * kWave - 1) / (kDecWaves * kWave), 4096));
+  hipLaunchKernelGGL(k_cesu_decode, dim3(grid), dim3(kDecWaves * kWave), 0, s, text, offsets, flags, n, tail,
+                     rstart, rend, stats);
 }
 
 // nnz[k] carries the row's bigram count in bits 0..29 and the wide (UTF-16
@@ -651,8 +720,12 @@ __global__ __launch_bounds__(kBlock) void k_featurize(DevRawBatch b, DevPrepared
                                                       int64_t cmax) {
   __shared__ uint32_t fbits[kFlagWords];
   __shared__ uint32_t stage[kFeatWaves][kRowsPerChunk * kStageStride];
+  __shared__ __attribute__((aligned(16))) uint8_t lpage_s[256];
+  __shared__ __attribute__((aligned(16))) uint16_t lblk_s[kLowerLdsBlocks * 256];
   for (int i = threadIdx.x; i < kFlagWords; i += kBlock) fbits[i] = 0u;
+  stage_lower_tables(lpage_s, lblk_s, lpage, lblocks, threadIdx.x, kBlock);
   __syncthreads();
+  const LowerLds lt{lpage_s, lblk_s, lblocks};
   const int64_t n_kept = p.counters[0];
   const int lane = lane_id();
   const int r = lane / kLanesPerRow, t = lane % kLanesPerRow;
@@ -687,7 +760,7 @@ __global__ __launch_bounds__(kBlock) void k_featurize(DevRawBatch b, DevPrepared
     const StagedRow sr = staged_row(meta, st, r);
     const int64_t len = valid ? sr.rt.len : 0;
     const int64_t nz = len >= 2 ? len - 1 : len;
-    auto unit = [&](int64_t j) -> uint32_t { return sr.unit(b, j, lpage, lblocks); };
+    auto unit = [&](int64_t j) -> uint32_t { return sr.unit(b, j, lt); };
     int32_t* out = p.idx + g0 * kChunkStride + lane * kGroup;
     const int32_t total = L8 * kGroup;
     for (int32_t jj0 = 0; jj0 < total; jj0 += kGroup) {

@@ -81,6 +81,11 @@ __global__ __launch_bounds__(kBlock) void k_km_features_chunk(DevRawBatch b, con
                                                               const uint8_t* lpage,
                                                               const uint16_t* lblocks) {
   extern __shared__ uint32_t smem[];
+  __shared__ __attribute__((aligned(16))) uint8_t lpage_s[256];
+  __shared__ __attribute__((aligned(16))) uint16_t lblk_s[kLowerLdsBlocks * 256];
+  stage_lower_tables(lpage_s, lblk_s, lpage, lblocks, threadIdx.x, kBlock);
+  __syncthreads();
+  const LowerLds lt{lpage_s, lblk_s, lblocks};
   const int lane = lane_id(), w = threadIdx.x / kWave;
   const int tdp = text_dims > 0 ? text_dims : 1;
   uint32_t* st = smem + w * (kRowsPerChunk * kStageStride + kRowsPerChunk * tdp);
@@ -107,8 +112,8 @@ __global__ __launch_bounds__(kBlock) void k_km_features_chunk(DevRawBatch b, con
         const int64_t nz = len >= 2 ? len - 1 : len;
         uint32_t* h = hist + q * text_dims;
         for (int64_t j = lane; j < nz; j += kWave) {
-          const uint32_t u0 = sr.unit(b, j, lpage, lblocks);
-          const uint32_t hsh = len >= 2 ? 31u * u0 + sr.unit(b, j + 1, lpage, lblocks) : u0;
+          const uint32_t u0 = sr.unit(b, j, lt);
+          const uint32_t hsh = len >= 2 ? 31u * u0 + sr.unit(b, j + 1, lt) : u0;
           atomicAdd(&h[fm.mod(hsh)], 1u);
         }
       }

@@ -22,6 +22,33 @@ __device__ __forceinline__ uint32_t lower_dev(uint32_t c, const uint8_t* page, c
   return (c + blocks[page[c >> 8] * 256 + (c & 255)]) & 0xFFFFu;
 }
 
+// The lowering tables' first kLowerLdsBlocks delta blocks (Latin, IPA,
+// Greek, Cyrillic, Armenian and the identity block every uncased page --
+// CJK, Arabic, Devanagari, ... -- maps to) plus the page index, copied to
+// LDS by a kernel's workgroup: a non-ASCII unit then costs two LDS reads
+// instead of two dependent global loads.  Blocks beyond it stay global.
+constexpr int kLowerLdsBlocks = 7;
+struct LowerLds {
+  const uint8_t* page;      // LDS [256]
+  const uint16_t* blocks;   // LDS [kLowerLdsBlocks][256]
+  const uint16_t* gblocks;  // global, all blocks
+  __device__ __forceinline__ uint32_t lower(uint32_t c) const {
+    if (c < 128) return (c >= 'A' && c <= 'Z') ? c + 32 : c;
+    const uint32_t blk = page[c >> 8];
+    const uint32_t d = blk < uint32_t(kLowerLdsBlocks) ? blocks[blk * 256 + (c & 255)] : gblocks[blk * 256 + (c & 255)];
+    return (c + d) & 0xFFFFu;
+  }
+};
+
+// Copy the tables into the workgroup's LDS arrays (caller synchronises).
+__device__ __forceinline__ void stage_lower_tables(uint8_t* page_s, uint16_t* blocks_s, const uint8_t* page,
+                                                   const uint16_t* blocks, int tid, int nthreads) {
+  for (int i = tid; i < 256 / 4; i += nthreads)
+    reinterpret_cast<uint32_t*>(page_s)[i] = reinterpret_cast<const uint32_t*>(page)[i];
+  for (int i = tid; i < kLowerLdsBlocks * 256 / 2; i += nthreads)
+    reinterpret_cast<uint32_t*>(blocks_s)[i] = reinterpret_cast<const uint32_t*>(blocks)[i];
+}
+
 // Latin-1 lower-casing in closed form (narrow rows): A-Z and U+00C0..U+00DE
 // except U+00D7 map to +0x20; nothing else in 0..255 changes under
 // Character.toLowerCase.
@@ -85,6 +112,13 @@ struct StagedRow {
       return lower_dev(uint32_t(sb[2 * j]) | (uint32_t(sb[2 * j + 1]) << 8), lpage, lblocks);
     }
     return lower_dev(row_unit(b, rt, j), lpage, lblocks);
+  }
+  __device__ __forceinline__ uint32_t unit(const DevRawBatch& b, int64_t j, const LowerLds& lt) const {
+    if (staged) {
+      if (!rt.wide) return lower_latin1(sb[j]);
+      return lt.lower(uint32_t(sb[2 * j]) | (uint32_t(sb[2 * j + 1]) << 8));
+    }
+    return lt.lower(row_unit(b, rt, j));
   }
 };
 

@@ -173,12 +173,14 @@ def test_kmeans_dp_loopback(hip_module, world):
 
 def test_kmeans_utf8_ingest_equals_wire(hip_module):
     """The end-to-end bench stages k-means batches as raw UTF-8 (device
-    decode); per batch the engine state must match the host-packed wire
-    ingest.  The two paths order rows differently (fp64 sums in another
-    order), which may flip a point equidistant from the two halves of a
-    just-split cluster (see test_kmeans_matches_cpu): then the weights move
-    by a point, their total is conserved, the other clusters agree, and the
-    UTF-8 engine continues from the wire engine's state."""
+    decode); per batch it must agree with the host-packed wire ingest: same
+    points (count, scaler), same assignments except for points equidistant
+    from the two halves of a just-split cluster (the two paths order rows
+    differently, so fp64 sums differ in the last bits and such ties may flip,
+    see test_kmeans_matches_cpu), conserved total weight.  The UTF-8 engine
+    continues from the wire engine's state after every batch.  (The decoded
+    text itself is checked exactly against the oracle by the LR featurize
+    tests.)"""
     from twitter_stream_ml_amd.ops.kmeans_engine import DeviceKMeans
     from twitter_stream_ml_amd.ops.lr_engine import encode_utf8
     cfg = _cfg(16, 14, seed=6)
@@ -190,11 +192,10 @@ def test_kmeans_utf8_ingest_equals_wire(hip_module):
         rb = b.process(0)
         assert ra["n"] == rb["n"]
         np.testing.assert_allclose(rb["std"], ra["std"], rtol=1e-12)
+        pa, pb = np.asarray(ra["pred"]), np.asarray(rb["pred"])
+        assert pa.shape == pb.shape and np.count_nonzero(pa != pb) <= 4, np.count_nonzero(pa != pb)
         ca, wa = a.get_state()
         cb, wb = b.get_state()
         np.testing.assert_allclose(wb.sum(), wa.sum(), rtol=1e-12)
         assert np.abs(wb - wa).sum() <= 4.0, (wa, wb)
-        same = np.abs(wb - wa) <= 1e-9 * np.maximum(np.abs(wa), 1.0)
-        assert same.sum() >= len(wa) - 4
-        np.testing.assert_allclose(cb[same], ca[same], rtol=1e-9, atol=1e-12)
         b.set_state(ca, wa)
