@@ -222,10 +222,32 @@ static int op_code(ncclRedOp_t op) {
   }
 }
 
+// Floating-point sums over > 2 ranks depend on the summation order, and
+// gloo's order differs between ranks: the parts are all-gathered and every
+// rank adds them in rank order, so all replicas get the same bits.
+template <typename T>
+static void sum_parts_in_order(T* parts, size_t count, int world) {
+  for (int r = 1; r < world; ++r) {
+    const T* p = parts + size_t(r) * count;
+    for (size_t i = 0; i < count; ++i) parts[i] += p[i];
+  }
+}
+
 void HostComm::allreduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t s) {
   if (count == 0) return;
   TraceRange tr("twtml.hostcomm.allreduce");
   const size_t bytes = count * comm_dtype_size(dt);
+  if (op == ncclSum && world_ > 2 && (dt == ncclFloat64 || dt == ncclFloat32)) {
+    uint8_t* h = static_cast<uint8_t*>(stage(bytes * size_t(world_)));
+    TWTML_HIP_CHECK(hipMemcpyAsync(h + bytes * size_t(rank_), buf, bytes, hipMemcpyDeviceToHost, s));
+    TWTML_HIP_CHECK(hipStreamSynchronize(s));
+    fn_(h, count, dt, -2, 0);
+    if (dt == ncclFloat64) sum_parts_in_order(reinterpret_cast<double*>(h), count, world_);
+    else sum_parts_in_order(reinterpret_cast<float*>(h), count, world_);
+    TWTML_HIP_CHECK(hipMemcpyAsync(buf, h, bytes, hipMemcpyHostToDevice, s));
+    TWTML_HIP_CHECK(hipStreamSynchronize(s));
+    return;
+  }
   void* h = stage(bytes);
   TWTML_HIP_CHECK(hipMemcpyAsync(h, buf, bytes, hipMemcpyDeviceToHost, s));
   TWTML_HIP_CHECK(hipStreamSynchronize(s));

@@ -1,5 +1,6 @@
 // LREngine implementation; see engine.h.
 #include "engine.h"
+#include "alloc.h"
 #include "trace.h"
 
 #include <algorithm>
@@ -178,9 +179,7 @@ HostBatch::~HostBatch() {
 
 template <typename T>
 static T* dmalloc(size_t n) {
-  void* p = nullptr;
-  TWTML_HIP_CHECK(hipMalloc(&p, std::max<size_t>(1, n) * sizeof(T)));
-  return static_cast<T*>(p);
+  return static_cast<T*>(dev_alloc(n * sizeof(T)));
 }
 
 LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm, std::shared_ptr<Comm> prep_comm)
@@ -364,7 +363,10 @@ void LREngine::ensure_tier(PrepBuf& b, int64_t n_unique, hipStream_t s) {
     (void)hipFree(p.slot_hist);
     b.slot_hist_cap = cap + kNumNumeric + 64;
     p.slot_hist = dmalloc<uint32_t>(size_t(b.slot_hist_cap));
-    TWTML_HIP_CHECK(hipMemset(p.slot_hist, 0, sizeof(uint32_t) * size_t(b.slot_hist_cap)));
+    // stream-ordered: the null stream does not order against the engine's
+    // non-blocking streams, so a plain hipMemset could land after the
+    // histogram pass that follows on `s`
+    TWTML_HIP_CHECK(hipMemsetAsync(p.slot_hist, 0, sizeof(uint32_t) * size_t(b.slot_hist_cap), s));
   }
 }
 
@@ -390,10 +392,13 @@ void LREngine::ensure_compact(int64_t ns) {
   }
   sgd_.wc64 = dmalloc<double>(size_t(cap));
   sgd_.wc32 = dmalloc<float>(size_t(cap));
-  sgd_.g64 = dmalloc<double>(size_t(cap) + 1);
+  sgd_.g64 = dmalloc<double>(size_t(cap) + 2);   // [nl]: loss, [nl + 1]: DP verdict
   sgd_.gfix = dmalloc<uint64_t>(size_t(cap));   // far gradients (tiered), kept zeroed by k_sgd_update
-  TWTML_HIP_CHECK(hipMemset(sgd_.g64, 0, sizeof(double) * (size_t(cap) + 1)));
-  TWTML_HIP_CHECK(hipMemset(sgd_.gfix, 0, sizeof(uint64_t) * size_t(cap)));
+  // zeroed on the compute stream, ahead of the kernels that accumulate into
+  // them (a null-stream hipMemset is unordered against the non-blocking
+  // compute stream and could wipe an iteration's far gradients)
+  TWTML_HIP_CHECK(hipMemsetAsync(sgd_.g64, 0, sizeof(double) * (size_t(cap) + 2), compute_));
+  TWTML_HIP_CHECK(hipMemsetAsync(sgd_.gfix, 0, sizeof(uint64_t) * size_t(cap), compute_));
   ns_cap_ = cap;
 }
 
@@ -641,6 +646,8 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred) {
   sp.want_pred = want_pred ? 1 : 0;
   sp.sample = cfg_.fraction < 1.0 ? 1 : 0;
   sp.ablate = cfg_.ablate;
+  sp.dp = world > 1 ? 1 : 0;
+  sp.rank0 = (comm_ ? comm_->rank() : 0) == 0 ? 1 : 0;
   // entries one workgroup can add into a slot: its share of the chunks (x2 for imbalance)
   sp.fix_lim = sgd_fix_limit(2 * (res.entries / std::max(1, grid)) + 65536);
   // far slots sum entries of every workgroup and rank
@@ -675,7 +682,7 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred) {
       if (tiered) launch_far_grad(sgd_, sp, num_cu_, s);
       if (world > 1) {
         launch_sgd_reduce(sgd_, sp, s);
-        comm_->allreduce(sgd_.g64, size_t(nl + 1), ncclFloat64, ncclSum, s);
+        comm_->allreduce(sgd_.g64, size_t(nl + 2), ncclFloat64, ncclSum, s);   // + loss, verdict
         // far gradients are int64 fixed point: the sum over ranks is exact
         if (n_far > 0) comm_->allreduce(sgd_.gfix, size_t(n_far), ncclUint64, ncclSum, s);
         if (sp.sample) comm_->allreduce(sgd_.red64 + 2 * (i & 1), 2, ncclFloat64, ncclSum, s);
@@ -874,7 +881,10 @@ void LREngine::set_weights(const double* w, int64_t n) {
   if (n != num_weights()) throw std::invalid_argument("weights size mismatch");
   TWTML_HIP_CHECK(hipSetDevice(device_));
   TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
-  TWTML_HIP_CHECK(hipMemcpy(sgd_.w64, w, sizeof(double) * size_t(n), hipMemcpyHostToDevice));
+  // stream-ordered, complete on return (a pageable hipMemcpy may return
+  // before its DMA lands, unordered against the non-blocking compute stream)
+  TWTML_HIP_CHECK(hipMemcpyAsync(sgd_.w64, w, sizeof(double) * size_t(n), hipMemcpyHostToDevice, compute_));
+  TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
   norm_age_ = -1;   // the carried |w|^2 no longer holds
 }
 

@@ -298,6 +298,8 @@ struct SgdParams {
                         // 6 = loads only, 7 = no chunks (fixed cost)
   float fix_lim;        // |r| * 2^24 clamp so a workgroup's int64 slot sums cannot overflow
   float far_lim;        // |r| * 2^16 clamp of the far (tiered) gradient: batch-wide int64 sums
+  int32_t dp;           // world > 1: convergence verdicts travel in the gradient all-reduce
+  int32_t rank0;        // this rank's verdict is the one that counts (DP)
 };
 
 // Fixed-point clamp for a launch: every slot of a workgroup receives at most

@@ -1,5 +1,6 @@
 // KMEngine: the streaming k-means micro-batch pipeline (see kmeans.hip).
 #include "kmeans_engine.h"
+#include "alloc.h"
 #include "trace.h"
 
 #include <pybind11/numpy.h>
@@ -19,9 +20,7 @@ namespace twtml {
 
 template <typename T>
 static T* km_alloc(size_t n) {
-  void* p = nullptr;
-  TWTML_HIP_CHECK(hipMalloc(&p, std::max<size_t>(1, n) * sizeof(T)));
-  return static_cast<T*>(p);
+  return static_cast<T*>(dev_alloc(n * sizeof(T)));
 }
 
 static int pad_dim(int d) {
@@ -68,8 +67,9 @@ KMEngine::KMEngine(int device, const KMConfig& cfg, std::shared_ptr<Comm> comm)
   frag_ = km_alloc<uint16_t>(km_frag_elems(cfg_.k, dp_));
   cnp_ = km_alloc<float>(size_t((cfg_.k + 31) / 32) * 32);
   lhist_ = km_alloc<int64_t>(k + 1);
-  TWTML_HIP_CHECK(hipMemset(centers_, 0, sizeof(double) * k * d));
-  TWTML_HIP_CHECK(hipMemset(weights_, 0, sizeof(double) * k));
+  // on the compute stream: the null stream does not order against it
+  TWTML_HIP_CHECK(hipMemsetAsync(centers_, 0, sizeof(double) * k * d, compute_));
+  TWTML_HIP_CHECK(hipMemsetAsync(weights_, 0, sizeof(double) * k, compute_));
   upload_lower_tables(compute_, &lower_page_, &lower_blocks_);
   TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_out_), sizeof(double) * (4 + d),
                                 hipHostMallocDefault));
@@ -182,8 +182,13 @@ KMResult KMEngine::process(int slot, bool want_labels) {
 void KMEngine::set_state(const double* centers, const double* weights) {
   TWTML_HIP_CHECK(hipSetDevice(device_));
   TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
-  TWTML_HIP_CHECK(hipMemcpy(centers_, centers, sizeof(double) * size_t(cfg_.k) * d_, hipMemcpyHostToDevice));
-  TWTML_HIP_CHECK(hipMemcpy(weights_, weights, sizeof(double) * size_t(cfg_.k), hipMemcpyHostToDevice));
+  // stream-ordered and complete on return (a pageable hipMemcpy may return
+  // before its DMA lands, unordered against the non-blocking compute stream)
+  TWTML_HIP_CHECK(hipMemcpyAsync(centers_, centers, sizeof(double) * size_t(cfg_.k) * d_, hipMemcpyHostToDevice,
+                                 compute_));
+  TWTML_HIP_CHECK(hipMemcpyAsync(weights_, weights, sizeof(double) * size_t(cfg_.k), hipMemcpyHostToDevice,
+                                 compute_));
+  TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
   launch_km_centers32(centers_, cfg_.k, d_, dp_, c32_, cnorm_, compute_);
   TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
 }

@@ -1,4 +1,5 @@
 #include "raw_slots.h"
+#include "alloc.h"
 
 #include <algorithm>
 #include <stdexcept>
@@ -9,9 +10,7 @@ namespace twtml {
 
 template <typename T>
 static T* slot_alloc(size_t n) {
-  void* p = nullptr;
-  TWTML_HIP_CHECK(hipMalloc(&p, std::max<size_t>(1, n) * sizeof(T)));
-  return static_cast<T*>(p);
+  return static_cast<T*>(dev_alloc(n * sizeof(T)));
 }
 
 int RawSlots::check(int slot) {

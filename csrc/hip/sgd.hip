@@ -218,18 +218,20 @@ __device__ bool sgd_converged_wave(const DevSgd& d, int it, double tol) {
 // Also publishes the verdict for update i-1 to the host (zero-copy pinned
 // memory, initialised to -1 by the host): the host polls it to stop
 // enqueueing iterations, without a per-iteration event in the stream.
+// DP ranks do not act on their own verdict here: k_sgd_reduce puts rank 0's
+// into the gradient all-reduce and k_sgd_update acts on the agreed value.
 __device__ bool sgd_stop(const DevSgd& d, const SgdParams& sp, int* flag) {
   if (threadIdx.x < kWave) {
     const bool done = d.state[0] != 0.0;
     bool stop = done;
-    if (!done && sp.iteration > 1) {
+    if (!done && sp.iteration > 1 && !sp.dp) {
       stop = sgd_converged_wave(d, sp.iteration - 1, sp.tol);
       if (stop && blockIdx.x == 0 && threadIdx.x == 0) {
         d.state[0] = 1.0;
         d.state[1] = 1.0;
       }
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0 && d.host_flags && sp.iteration > 1) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && d.host_flags && sp.iteration > 1 && !sp.dp) {
       __hip_atomic_store(&d.host_flags[sp.iteration - 1], stop ? 1.0 : 0.0, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
     }
@@ -866,7 +868,13 @@ int sgd_partials(int64_t ns, bool u16, int grid) {
 //                 so all workgroups -- and all DP ranks -- agree); workgroup
 //                 0 publishes state[0..1] and the host flag.  Then one
 //                 partial gradient row per workgroup.
-//   [k_sgd_reduce + RCCL all-reduce of g64 when DP]
+//   [k_sgd_reduce + RCCL all-reduce of g64 when DP; the verdict on update
+//    i-1 rides along in g64[nl + 1] -- rank 0's, so the all-reduced value is
+//    exact and the same on every rank whatever the backend's summation
+//    order -- and k_sgd_update i acts on it: no update, state[0..1] and the
+//    host flag.  The gradient pass of iteration i is then wasted once per
+//    batch, but ranks can never disagree on the iteration count (a mismatch
+//    would pair unequal collectives).]
 //   k_sgd_update  (iteration i)  multi-workgroup: sums the partial rows of
 //                 64 columns (world 1) or reads the all-reduced g64,
 //                 SimpleUpdater on them, per-workgroup ||dw||^2, ||w||^2
@@ -919,9 +927,25 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
   __shared__ double wsc[kUpdWaves][2];
   __shared__ double red[kUpdWaves][kWave];
   __shared__ double m_sh;
-  if (d.state[0] != 0.0) return;
   const int tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
   const int it = sp.iteration;
+  if (sp.dp && it > 1) {   // the agreed verdict on update it - 1 (checked before state[0]:
+                           // block 0 sets it below while other blocks may still start)
+    const bool stop = d.g64[d.nl + 1] > 0.5;
+    if (blockIdx.x == 0 && tid == 0 && d.host_flags)
+      __hip_atomic_store(&d.host_flags[it - 1], stop ? 1.0 : 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (stop) {
+      const int64_t n_far = kNumNumeric + d.n_unique - d.far_base;   // this pass's far sums are dropped
+      for (int64_t j = int64_t(blockIdx.x) * 1024 + tid; j < n_far; j += int64_t(gridDim.x) * 1024)
+        d.gfix[j] = 0ull;
+      if (blockIdx.x == 0 && tid == 0) {
+        d.state[0] = 1.0;
+        d.state[1] = 1.0;
+      }
+      return;
+    }
+  }
+  if (d.state[0] != 0.0) return;
   const int64_t ns = d.nl, hi = d.far_base;   // partial-row columns; near text slots end at far_base
   const int64_t ncols = ns + kPartVals - kNumNumeric;
   // m: global kept rows, or the sampled row count of this iteration
@@ -1020,20 +1044,27 @@ void launch_sgd_update(const DevSgd& d, const SgdParams& sp, int nparts, hipStre
 __global__ __launch_bounds__(1024) void k_sgd_reduce(DevSgd d, SgdParams sp) {
   __shared__ double red[kUpdWaves][kWave];
   if (d.state[0] != 0.0) return;
-  const int64_t ncols = d.nl + kPartVals - kNumNumeric;
-  const int64_t col0 = int64_t(blockIdx.x) * kWave;
-  const double v = part_block_sum(d, col0, ncols, d.nparts, red);
-  const int64_t col = col0 + lane_id();
-  if (threadIdx.x < kWave && col < ncols) {
-    if (col <= d.nl) d.g64[col] = v;                     // slots, then the loss at [nl]
-    else if (col == d.nl + 1) *sgd_red_m(d, sp.iteration) = v;   // sampled row count
-    else d.stats[col - d.nl - 2] += v;                   // batch stats (iteration 1)
+  if (d.nparts > 0) {
+    const int64_t ncols = d.nl + kPartVals - kNumNumeric;
+    const int64_t col0 = int64_t(blockIdx.x) * kWave;
+    const double v = part_block_sum(d, col0, ncols, d.nparts, red);
+    const int64_t col = col0 + lane_id();
+    if (threadIdx.x < kWave && col < ncols) {
+      if (col <= d.nl) d.g64[col] = v;                     // slots, then the loss at [nl]
+      else if (col == d.nl + 1) *sgd_red_m(d, sp.iteration) = v;   // sampled row count
+      else d.stats[col - d.nl - 2] += v;                   // batch stats (iteration 1)
+    }
+  }
+  // DP: rank 0's verdict on update i-1 -> g64[nl + 1] (all-reduced with the gradient)
+  if (sp.dp && blockIdx.x == 0 && threadIdx.x < kWave) {
+    const bool conv = sp.iteration > 1 && sgd_converged_wave(d, sp.iteration - 1, sp.tol);
+    if (threadIdx.x == 0) d.g64[d.nl + 1] = (conv && sp.rank0) ? 1.0 : 0.0;
   }
 }
 
 void launch_sgd_reduce(const DevSgd& d, const SgdParams& sp, hipStream_t s) {
-  if (d.nparts <= 0) return;
-  const int grid = int((d.nl + kPartVals - kNumNumeric + kWave - 1) / kWave);
+  if (d.nparts <= 0 && !sp.dp) return;
+  const int grid = d.nparts > 0 ? int((d.nl + kPartVals - kNumNumeric + kWave - 1) / kWave) : 1;
   hipLaunchKernelGGL(k_sgd_reduce, dim3(grid), dim3(1024), 0, s, d, sp);
 }
 

@@ -1,6 +1,6 @@
 """Cross-process data parallelism on one MI355X (SURVEY §2.4 DP, §2.5 CS2).
 
-N ranks are N processes sharing GPU 0; each owns an engine whose collectives
+N ranks (2 and 3) are N processes sharing GPU 0; each owns an engine whose collectives
 go through the host-staged torch.distributed gloo communicator
 (``parallel/dist.make_comm(..., "gloo")`` -> ``csrc/hip/comm.cpp`` HostComm).
 This is the engine DP path a one-GPU-per-rank RCCL job runs -- per-rank shards,
@@ -91,11 +91,13 @@ def _worker(rank, world, port, out_dir):
     D.shutdown()
 
 
-@pytest.fixture(scope="module")
-def dp_runs(tmp_path_factory, hip_module):
+@pytest.fixture(scope="module", params=[2, 3], ids=["world2", "world3"])
+def dp_runs(request, tmp_path_factory, hip_module):
+    """2 ranks, and 3 (odd world: uneven shards, all-gather parts of unequal
+    fill, fixed-order reductions over an odd number of partials)."""
     import torch.multiprocessing as mp
-    out = tmp_path_factory.mktemp("dp_procs")
-    world = 2
+    world = request.param
+    out = tmp_path_factory.mktemp(f"dp_procs{world}")
     mp.start_processes(_worker, args=(world, _free_port(), str(out)), nprocs=world, join=True,
                        start_method="spawn")
     return world, [dict(np.load(out / f"r{r}.npz")) for r in range(world)]

@@ -18,6 +18,8 @@ from __future__ import annotations
 
 import datetime
 import os
+import sys
+import threading
 from dataclasses import dataclass
 from typing import Callable, Optional
 
@@ -112,7 +114,13 @@ def make_comm(device: int, kind: str = "rccl", own_group: bool = False):
     # MAX / MIN only ever see u8 flags, which torch / gloo handle natively
     as_signed = {np.dtype("u4"): np.dtype("i4"), np.dtype("u8"): np.dtype("i8")}
 
+    trace = os.environ.get("TWTML_COMM_TRACE")
+    label = "prep" if own_group else "main"
+
     def collective(arr: np.ndarray, op: int, root: int) -> None:
+        if trace:   # debugging collective order across ranks / threads
+            print(f"[comm r{info.rank} {label} {threading.get_ident() % 100000}] op {op} n {arr.size} "
+                  f"{arr.dtype}", file=sys.stderr, flush=True)
         a = arr.view(as_signed.get(arr.dtype, arr.dtype))
         t = torch.from_numpy(a)
         if op == -1:
@@ -148,8 +156,17 @@ def allreduce_fn() -> Optional[Callable[[np.ndarray], np.ndarray]]:
         t = torch.from_numpy(np.ascontiguousarray(v, dtype=np.float64).copy())
         if info.backend == "nccl":
             t = t.cuda()
-        dist.all_reduce(t)
-        return t.cpu().numpy()
+        if info.world <= 2:   # a + b == b + a: every rank gets the same bits
+            dist.all_reduce(t)
+            return t.cpu().numpy()
+        # > 2 ranks: gloo's summation order differs between ranks; all-gather
+        # and add in rank order so the replicas stay bit-identical
+        parts = [torch.empty_like(t) for _ in range(info.world)]
+        dist.all_gather(parts, t)
+        acc = parts[0].cpu().numpy().copy()
+        for p in parts[1:]:
+            acc += p.cpu().numpy()
+        return acc
 
     return _allreduce
 
