@@ -109,6 +109,9 @@ void LoopbackHub::arrive_and_wait(int rank, void* buf, const std::function<void(
   bufs_[size_t(rank)] = buf;
   if (++arrived_ == world_) {
     leader_work();
+    // the leader's pageable H2D copies may return before their DMA lands and
+    // are unordered against the ranks' non-blocking streams: complete them
+    TWTML_HIP_CHECK(hipDeviceSynchronize());
     arrived_ = 0;
     ++generation_;
     cv_.notify_all();
@@ -187,7 +190,7 @@ void LoopbackComm::allgather(const void* send, void* recv, size_t count, ncclDat
   if (count == 0) return;
   TWTML_HIP_CHECK(hipStreamSynchronize(s));
   if (world_ == 1) {
-    TWTML_HIP_CHECK(hipMemcpy(recv, send, count * comm_dtype_size(dt), hipMemcpyDeviceToDevice));
+    TWTML_HIP_CHECK(hipMemcpyAsync(recv, send, count * comm_dtype_size(dt), hipMemcpyDeviceToDevice, s));
     return;
   }
   hub_->allgather(rank_, send, recv, count, dt);

@@ -226,6 +226,7 @@ void upload_case_tables(DevCaseTables* ct) {
   TWTML_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&cr), sizeof(uni::kCaseRanges)));
   TWTML_HIP_CHECK(hipMemcpy(sl, uni::kSuppLower, sizeof(uni::kSuppLower), hipMemcpyHostToDevice));
   TWTML_HIP_CHECK(hipMemcpy(cr, uni::kCaseRanges, sizeof(uni::kCaseRanges), hipMemcpyHostToDevice));
+  TWTML_HIP_CHECK(hipDeviceSynchronize());   // landed before any engine stream reads them
   ct->supp_lower = sl;
   ct->case_ranges = cr;
   ct->n_supp = uni::kNumSuppLower;
