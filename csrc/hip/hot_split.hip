@@ -404,9 +404,10 @@ constexpr int kTierHistSpan = 32768;
 
 // step: every step-th sampled chunk (the same subset in every span pass),
 // so the passes over wide active sets cost one sampled pass in total.
-__global__ __launch_bounds__(kHistBlock) void k_tier_hist(DevPrepared p, int64_t lo, int64_t hi, int64_t step) {
+__global__ __launch_bounds__(kHistBlock) void k_tier_hist(DevPrepared p, int64_t n_unique, int64_t step) {
   __shared__ uint32_t h[kTierHistSpan];
-  const int64_t span = hi - lo;
+  const int64_t lo = int64_t(blockIdx.y) * kTierHistSpan;   // this workgroup's slot span
+  const int64_t span = std::min<int64_t>(n_unique - lo, kTierHistSpan);
   for (int64_t i = threadIdx.x; i < span; i += kHistBlock) h[i] = 0u;
   __syncthreads();
   const int lane = lane_id();
@@ -631,11 +632,12 @@ void launch_tier_hist(const DevPrepared& p, int64_t n_unique, int num_cu, hipStr
   // sampled chunk, step = number of spans (the near tier only needs the
   // frequency order of the top slots: ~1/100 of the entries at 200K slots)
   const int64_t step = std::max<int64_t>(1, (n_unique + kTierHistSpan - 1) / kTierHistSpan);
+  // every span in one launch (blockIdx.y), the CUs shared out among them:
+  // one workgroup (128 KB of LDS) per CU, no span waiting for another
+  const int64_t spans = step;
   int gh = int((nsamp / step + kHistBlock / kWave - 1) / (kHistBlock / kWave));
-  gh = std::max(1, std::min(gh, num_cu / 2));
-  for (int64_t lo = 0; lo < n_unique; lo += kTierHistSpan)
-    hipLaunchKernelGGL(k_tier_hist, dim3(gh), dim3(kHistBlock), 0, s, p, lo,
-                       std::min<int64_t>(n_unique, lo + kTierHistSpan), step);
+  gh = std::max(1, std::min<int>(gh, int(std::max<int64_t>(1, num_cu / spans))));
+  hipLaunchKernelGGL(k_tier_hist, dim3(gh, unsigned(spans)), dim3(kHistBlock), 0, s, p, n_unique, step);
 }
 
 int64_t tier_near_cap() {
