@@ -224,7 +224,7 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm, 
   TWTML_HIP_CHECK(hipMemset(sgd_.w64, 0, sizeof(double) * size_t(nw)));  // Vectors.zeros
   sgd_.red64 = dmalloc<double>(4);
   sgd_.stats = dmalloc<double>(8);
-  sgd_.state = dmalloc<double>(8);
+  sgd_.state = dmalloc<double>(kStateLen);
   sgd_.loss_hist = dmalloc<double>(size_t(std::max(1, cfg_.num_iterations)) + 2);
   sgd_.itrec = dmalloc<double>((size_t(std::max(1, cfg_.num_iterations)) + 2) * kRecStride);
   sgd_.pred_out = dmalloc<float>(size_t(cfg_.max_rows));

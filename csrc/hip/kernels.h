@@ -284,6 +284,11 @@ constexpr int kRecStride = kRecHead + 2 * kMaxUpdGrid;
 // Partial-row stride for a compact space of ns slots (multiple of 64).
 constexpr int64_t sgd_part_stride(int64_t ns) { return ns + 64; }
 
+// DevSgd::state: [0] done, [1] converged, [2] updates applied, [3] last
+// iteration, [4] |w|^2, [5] rows m, [6] |w_active|^2, [7] clamp flag,
+// [8] DP: iteration whose gradient pass this rank skipped
+constexpr int kStateLen = 10;
+
 struct SgdParams {
   double step_size;
   double fraction;

@@ -218,17 +218,24 @@ __device__ bool sgd_converged_wave(const DevSgd& d, int it, double tol) {
 // Also publishes the verdict for update i-1 to the host (zero-copy pinned
 // memory, initialised to -1 by the host): the host polls it to stop
 // enqueueing iterations, without a per-iteration event in the stream.
-// DP ranks do not act on their own verdict here: k_sgd_reduce puts rank 0's
-// into the gradient all-reduce and k_sgd_update acts on the agreed value.
+// DP ranks only skip the pass on their own verdict (state[8] = iteration):
+// k_sgd_reduce puts rank 0's into the gradient all-reduce and k_sgd_update
+// acts on the agreed value.
 __device__ bool sgd_stop(const DevSgd& d, const SgdParams& sp, int* flag) {
   if (threadIdx.x < kWave) {
     const bool done = d.state[0] != 0.0;
     bool stop = done;
-    if (!done && sp.iteration > 1 && !sp.dp) {
+    if (!done && sp.iteration > 1) {
       stop = sgd_converged_wave(d, sp.iteration - 1, sp.tol);
       if (stop && blockIdx.x == 0 && threadIdx.x == 0) {
-        d.state[0] = 1.0;
-        d.state[1] = 1.0;
+        if (!sp.dp) {
+          d.state[0] = 1.0;
+          d.state[1] = 1.0;
+        } else {
+          // DP: this rank skips the pass (identical weights -> every rank
+          // does); the agreed verdict in k_sgd_update ends the batch
+          d.state[8] = double(sp.iteration);
+        }
       }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0 && d.host_flags && sp.iteration > 1 && !sp.dp) {
@@ -872,9 +879,11 @@ int sgd_partials(int64_t ns, bool u16, int grid) {
 //    i-1 rides along in g64[nl + 1] -- rank 0's, so the all-reduced value is
 //    exact and the same on every rank whatever the backend's summation
 //    order -- and k_sgd_update i acts on it: no update, state[0..1] and the
-//    host flag.  The gradient pass of iteration i is then wasted once per
-//    batch, but ranks can never disagree on the iteration count (a mismatch
-//    would pair unequal collectives).]
+//    host flag.  Each rank skips the gradient pass of iteration i on its own
+//    verdict (state[8]; identical weights -> the same verdict everywhere)
+//    and then contributes zeros, but only the agreed verdict ends the loop,
+//    so ranks can never disagree on the iteration count (a mismatch would
+//    pair unequal collectives).]
 //   k_sgd_update  (iteration i)  multi-workgroup: sums the partial rows of
 //                 64 columns (world 1) or reads the all-reduced g64,
 //                 SimpleUpdater on them, per-workgroup ||dw||^2, ||w||^2
@@ -1044,10 +1053,13 @@ void launch_sgd_update(const DevSgd& d, const SgdParams& sp, int nparts, hipStre
 __global__ __launch_bounds__(1024) void k_sgd_reduce(DevSgd d, SgdParams sp) {
   __shared__ double red[kUpdWaves][kWave];
   if (d.state[0] != 0.0) return;
+  // DP pass skipped on this rank's verdict: its partial rows are stale, it
+  // contributes zeros
+  const bool skipped = d.state[8] == double(sp.iteration);
   if (d.nparts > 0) {
     const int64_t ncols = d.nl + kPartVals - kNumNumeric;
     const int64_t col0 = int64_t(blockIdx.x) * kWave;
-    const double v = part_block_sum(d, col0, ncols, d.nparts, red);
+    const double v = skipped ? 0.0 : part_block_sum(d, col0, ncols, d.nparts, red);
     const int64_t col = col0 + lane_id();
     if (threadIdx.x < kWave && col < ncols) {
       if (col <= d.nl) d.g64[col] = v;                     // slots, then the loss at [nl]
@@ -1095,7 +1107,7 @@ void launch_sgd_finish(const DevSgd& d, const SgdParams& sp, hipStream_t s) {
 // float atomics, deterministic across runs and DP ranks.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_far_grad(DevSgd d, SgdParams sp) {
-  if (d.state[0] != 0.0) return;
+  if (d.state[0] != 0.0 || d.state[8] == double(sp.iteration)) return;   // done / DP pass skipped
   const int64_t n = *d.far_n;
   const int lane = lane_id();
   bool clamped = false;
@@ -1233,10 +1245,8 @@ void launch_norm_carry(const DevSgd& d, hipStream_t s) {
 // batch stats, sampled counts, the loss slot g64[ns] and the loss history.
 __global__ void k_batch_init(DevSgd d, double m_global, int n_loss) {
   const int i = threadIdx.x;
-  if (i < 8) {
-    d.state[i] = i == 5 ? m_global : 0.0;
-    d.stats[i] = 0.0;
-  }
+  if (i < kStateLen) d.state[i] = i == 5 ? m_global : 0.0;
+  if (i < 8) d.stats[i] = 0.0;
   if (i < 4) d.red64[i] = 0.0;
   if (i == 0) d.g64[d.nl] = 0.0;
   for (int k = i; k < n_loss; k += blockDim.x) d.loss_hist[k] = 0.0;
