@@ -61,7 +61,11 @@ def parse_args(argv=None):
     ap.add_argument("--text-dims", type=int, default=62, help="kmeans hashed bigram dims (+2 numeric)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=1_000_000, help="raw tweets per GPU per step")
+    ap.add_argument("--batch", default="1000000",
+                    help="raw tweets per GPU per step, or 'hbm': the largest micro-batch whose engine "
+                         "fits --hbm-fraction of the GPU's free memory (config 5 sizing), capped by --batch-cap")
+    ap.add_argument("--hbm-fraction", type=float, default=0.8, help="--batch hbm: share of free HBM")
+    ap.add_argument("--batch-cap", type=int, default=8_000_000, help="--batch hbm: upper bound (host pool size)")
     ap.add_argument("--features", type=int, default=1_000_000, help="numTextFeatures")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--step-size", type=float, default=0.005)
@@ -209,6 +213,37 @@ def run_e2e(r: Runner, raws, u8s, views, ingest: str, warmup: int, steps: int, s
     return t0, t1
 
 
+def lr_config(args, rows: int, max_units: int, ingest: str):
+    from twitter_stream_ml_amd.ops.lr_engine import LRDeviceConfig
+    return LRDeviceConfig(num_text_features=args.features, hash=args.hash,
+                          step_size=args.step_size, num_iterations=args.iters, fraction=1.0,
+                          begin=100, end=1000, max_rows=rows, max_units=max_units,
+                          sgd_grid=args.sgd_grid, ablate=args.ablate, tol=args.tol, dedup=bool(args.dedup),
+                          hybrid=bool(args.hybrid), ingest=ingest if args.e2e else "wire")
+
+
+def hbm_batch(args, synth, device: int, ingest: str):
+    """--batch hbm: micro-batch rows from the engine's measured footprint and
+    the GPU's free memory (ops/sizing.py); units per row from a sample."""
+    import torch
+    from twitter_stream_ml_amd.ops.lr_engine import DeviceLinearRegression
+    from twitter_stream_ml_amd.ops.sizing import hbm_max_rows
+    from twitter_stream_ml_amd.sources.synthetic import generate_batch
+    if args.model != "lr":
+        raise SystemExit("--batch hbm sizes the LR engine (config 5)")
+    sample = generate_batch(synth, 0, 65536, batch_time_ms=synth.now_ms)
+    upr = 1.1 * sample.total_units / max(1, sample.n)   # units per row, 10 % margin
+
+    def make(rows: int):
+        return DeviceLinearRegression(lr_config(args, rows, int(rows * upr) + 1024, ingest), device=device)
+
+    free, total = torch.cuda.mem_get_info(device)
+    rows = hbm_max_rows(make, free, args.hbm_fraction)
+    B = min(rows, args.batch_cap)
+    return B, {"rule": f"hbm: {args.hbm_fraction:.2f} x {free / 2**30:.0f} GiB free of {total / 2**30:.0f} GiB",
+               "hbm_max_rows": rows, "batch_cap": args.batch_cap}
+
+
 def main(argv=None) -> int:
     args = parse_args(argv)
     args.e2e = not args.prepacked
@@ -237,9 +272,14 @@ def main(argv=None) -> int:
         comm, prep_comm = D.make_comm_pair(device, args.comm)
     ingest = args.ingest or "utf8"
 
-    B = args.batch
     synth = SynthConfig.profile(args.profile, seed=args.seed + 7919 * info.rank)
     now_ms = synth.now_ms
+    sizing = None
+    if str(args.batch).lower() == "hbm":
+        B, sizing = hbm_batch(args, synth, device, ingest)
+        B = int(D.allreduce_max_scalar(-float(B)) * -1)   # the smallest over ranks
+    else:
+        B = int(args.batch)
     t_gen = time.time()
     pool_raw = [generate_batch(synth, i * B, B, batch_time_ms=now_ms) for i in range(args.pool)]
     max_units = max(r.total_units for r in pool_raw) + 1024
@@ -250,12 +290,8 @@ def main(argv=None) -> int:
                               max_units=max_units, seed=args.seed)
         eng = DeviceKMeans(kcfg, device=device, comm=comm)
     else:
-        cfg = LRDeviceConfig(num_text_features=args.features, hash=args.hash,
-                             step_size=args.step_size, num_iterations=args.iters, fraction=1.0,
-                             begin=100, end=1000, max_rows=B, max_units=max_units,
-                             sgd_grid=args.sgd_grid, ablate=args.ablate, tol=args.tol, dedup=bool(args.dedup),
-                             hybrid=bool(args.hybrid), ingest=ingest if args.e2e else "wire")
-        eng = DeviceLinearRegression(cfg, device=device, comm=comm, prep_comm=prep_comm)
+        eng = DeviceLinearRegression(lr_config(args, B, max_units, ingest), device=device, comm=comm,
+                                     prep_comm=prep_comm)
     u8s = []
     if args.e2e:
         views = [HostBatchView(B, max_units) for _ in range(eng.raw_slots)]
@@ -327,6 +363,8 @@ def main(argv=None) -> int:
             "numIterations": args.iters, "stepSize": args.step_size, "miniBatchFraction": 1.0,
             "hash": args.hash, "profile": args.profile,
         }
+        if sizing:
+            out["config"]["batch_sizing"] = sizing
         out["gd_iterations_mean"] = float(np.mean(runner.iters)) if runner.iters else 0.0
         out["prep_ms_mean"] = float(np.mean([s[0] for s in stage])) if stage else 0.0
         out["train_ms_mean"] = float(np.mean([s[1] for s in stage])) if stage else 0.0

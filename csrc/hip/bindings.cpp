@@ -6,6 +6,7 @@
 
 #include <memory>
 
+#include "alloc.h"
 #include "comm.h"
 #include "common.h"
 #include "engine.h"
@@ -97,6 +98,8 @@ PYBIND11_MODULE(_twtml_hip, m) {
     TWTML_HIP_CHECK(hipHostUnregister(reinterpret_cast<void*>(ptr)));
   }, py::arg("ptr"));
   m.def("rccl_version", &rccl_version);
+  // device bytes allocated by the engines so far (monotonic; HBM batch sizing)
+  m.def("device_bytes_allocated", [] { return uint64_t(dev_alloc_bytes().load()); });
 
   py::class_<Comm, std::shared_ptr<Comm>>(m, "CommBase")
       .def_property_readonly("rank", &Comm::rank)
