@@ -1106,6 +1106,20 @@ void launch_sgd_finish(const DevSgd& d, const SgdParams& sp, hipStream_t s) {
 // order of entries inside a slot or on which wave adds first: no per-entry
 // float atomics, deterministic across runs and DP ranks.
 // ---------------------------------------------------------------------------
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t old, uint32_t v) {
+  return uint32_t(__builtin_amdgcn_update_dpp(int(old), int(v), CTRL, ROWS, 0xf, false));
+}
+// One Hillis-Steele step of a segmented 64-bit sum: lanes without a DPP
+// source (or outside ROWS) see slot ~0 and add nothing.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void seg_scan_step(long long& q, uint32_t sl) {
+  const uint32_t lo = dpp_u32<CTRL, ROWS>(0u, uint32_t(uint64_t(q)));
+  const uint32_t hi = dpp_u32<CTRL, ROWS>(0u, uint32_t(uint64_t(q) >> 32));
+  const uint32_t su = dpp_u32<CTRL, ROWS>(0xFFFFFFFFu, sl);
+  if (su == sl) q += (long long)((uint64_t(hi) << 32) | lo);
+}
+
 __global__ __launch_bounds__(256) void k_far_grad(DevSgd d, SgdParams sp) {
   if (d.state[0] != 0.0 || d.state[8] == double(sp.iteration)) return;   // done / DP pass skipped
   const int64_t n = *d.far_n;
@@ -1125,12 +1139,16 @@ __global__ __launch_bounds__(256) void k_far_grad(DevSgd d, SgdParams sp) {
       }
       q = __float2ll_rn(v);
     }
-#pragma unroll
-    for (int off = 1; off < kWave; off <<= 1) {
-      const long long qu = __shfl_up(q, off, kWave);
-      const uint32_t su = uint32_t(__shfl_up(int(sl), off, kWave));
-      if (lane >= off && su == sl) q += qu;
-    }
+    // segmented inclusive scan on the VALU (DPP row shifts, then the row
+    // broadcasts across the four 16-lane rows) instead of 18 LDS permutes:
+    // the CSC is slot-sorted, so a lane k places back is in this lane's
+    // segment iff it holds the same slot
+    seg_scan_step<0x111, 0xf>(q, sl);   // row_shr:1
+    seg_scan_step<0x112, 0xf>(q, sl);   // row_shr:2
+    seg_scan_step<0x114, 0xf>(q, sl);   // row_shr:4
+    seg_scan_step<0x118, 0xf>(q, sl);   // row_shr:8
+    seg_scan_step<0x142, 0xa>(q, sl);   // row_bcast:15 -> rows 1, 3
+    seg_scan_step<0x143, 0xc>(q, sl);   // row_bcast:31 -> rows 2, 3
     const uint32_t sn = uint32_t(__shfl_down(int(sl), 1, kWave));
     const bool tail = valid && (lane == kWave - 1 || e + 1 >= n || sn != sl);
     if (tail && q != 0)
