@@ -90,10 +90,12 @@ def parse_args(argv=None):
     ap.add_argument("--comm", choices=["rccl", "gloo"], default="rccl",
                     help="DP gradient collectives: RCCL over xGMI, or host-staged torch.distributed "
                          "gloo (lets N ranks share one GPU for testing)")
-    ap.add_argument("--prep-comm", choices=["auto", "on", "off"], default="auto",
-                    help="DP: a second communicator for the prep collectives so batch t+1 is prepared "
-                         "while t's gradient all-reduces run (auto: on for gloo; RCCL opt-in -- the "
-                         "toy config is H2D bound, where it gains nothing)")
+    ap.add_argument("--prep-comm", choices=["auto", "gloo", "on", "off"], default="auto",
+                    help="DP: a second communicator for the prep collectives (kept counts, active-id "
+                         "union, tier counts) so batch t+1 is prepared entirely on the side stream while "
+                         "t's gradient all-reduces run.  auto/gloo: a host-staged gloo group (small "
+                         "messages; no second RCCL communicator competing for the process's hardware "
+                         "queues); on: the same kind as --comm; off: the collective part runs in line")
     ap.add_argument("--json-out", default="")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args(argv)
@@ -265,11 +267,11 @@ def main(argv=None) -> int:
     torch.cuda.set_device(device)
     from twitter_stream_ml_amd.parallel.affinity import bind_local_numa
     numa_cpus = bind_local_numa(device)   # before the pinned pool is allocated
-    want_prep = args.prep_comm == "on" or (args.prep_comm == "auto" and args.comm == "gloo")
-    if args.model == "kmeans" or not want_prep:
+    if args.model == "kmeans" or args.prep_comm == "off":
         comm, prep_comm = D.make_comm(device, args.comm), None
     else:   # LR: a second communicator lets batch t+1 be prepared during t's all-reduces
-        comm, prep_comm = D.make_comm_pair(device, args.comm)
+        prep_kind = args.comm if args.prep_comm == "on" else "gloo"
+        comm, prep_comm = D.make_comm_pair(device, args.comm, prep_kind)
     ingest = args.ingest or "utf8"
 
     synth = SynthConfig.profile(args.profile, seed=args.seed + 7919 * info.rank)

@@ -135,13 +135,16 @@ def make_comm(device: int, kind: str = "rccl", own_group: bool = False):
     return hip().HostComm(info.rank, info.world, collective)
 
 
-def make_comm_pair(device: int, kind: str = "rccl"):
+def make_comm_pair(device: int, kind: str = "rccl", prep_kind: Optional[str] = None):
     """(gradient communicator, prep communicator) for a DP engine: the
     second one carries the prep-stage collectives of batch t+1 while batch
-    t's gradient all-reduces run on the first.  (None, None) at world 1."""
+    t's gradient all-reduces run on the first.  ``prep_kind`` (default
+    ``kind``): e.g. RCCL gradients with a host-staged gloo prep group -- the
+    prep messages are small and a second RCCL communicator would compete for
+    the process's hardware queues.  (None, None) at world 1."""
     if dist_info().world <= 1:
         return None, None
-    return make_comm(device, kind), make_comm(device, kind, own_group=True)
+    return make_comm(device, kind), make_comm(device, prep_kind or kind, own_group=True)
 
 
 def allreduce_fn() -> Optional[Callable[[np.ndarray], np.ndarray]]:
