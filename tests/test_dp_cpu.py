@@ -74,3 +74,33 @@ def test_cpu_dp_equals_single_process(tmp_path, world, fraction):
         np.testing.assert_allclose(d["w"], lr.get_weights(), rtol=1e-9, atol=1e-15)
         np.testing.assert_allclose(d["c"], km.state.centers, rtol=1e-9, atol=1e-12)
         np.testing.assert_allclose(d["cw"], km.state.weights, rtol=1e-12)
+
+
+def _sum_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from twitter_stream_ml_amd.parallel import dist as D
+    D.init_distributed(backend="gloo")
+    red = D.allreduce_fn()
+    rng = np.random.default_rng(100 + rank)
+    # magnitudes spread over 30 decades: the fp64 sum depends on the order
+    v = rng.standard_normal(4096) * 10.0 ** rng.integers(-15, 15, 4096)
+    np.save(os.path.join(out_dir, f"in{rank}.npy"), v)
+    np.save(os.path.join(out_dir, f"out{rank}.npy"), red(v))
+    D.barrier()
+    D.shutdown()
+
+
+@pytest.mark.parametrize("world", [3, 4])
+def test_allreduce_fn_bit_identical_in_rank_order(tmp_path, world):
+    """> 2 ranks: every rank gets the same bits -- the parts added in rank
+    order -- so replicas (and their convergence verdicts) cannot diverge."""
+    mp.start_processes(_sum_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    ins = [np.load(tmp_path / f"in{r}.npy") for r in range(world)]
+    outs = [np.load(tmp_path / f"out{r}.npy") for r in range(world)]
+    ref = ins[0].copy()
+    for x in ins[1:]:
+        ref += x
+    for o in outs:
+        np.testing.assert_array_equal(o, ref)
