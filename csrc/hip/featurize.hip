@@ -330,6 +330,20 @@ __device__ __forceinline__ int64_t decode_row(const Src& src, uint8_t* text, int
   return k;
 }
 
+// One lane's row class from the staged bytes [lo, le) (as row_class).
+__device__ __forceinline__ int lane_row_class(const uint8_t* lbuf, int lo, int le) {
+  uint32_t acc = 0, big = 0;
+  for (int w = lo & ~3; w < le; w += 4) {
+    uint32_t v = *reinterpret_cast<const uint32_t*>(lbuf + w);
+    if (w < lo) v &= 0xFFFFFFFFu << (8 * (lo - w));
+    if (w + 4 > le) v &= 0xFFFFFFFFu >> (8 * (w + 4 - le));
+    acc |= v;
+    big |= v & ((v & 0x7F7F7F7Fu) + 0x3C3C3C3Cu);   // a byte >= 0xC4 sets its bit 7
+  }
+  if (big & 0x80808080u) return 2;
+  return (acc & 0x80808080u) ? 1 : 0;
+}
+
 // LDS staging per wave: the 64 rows of a group are consecutive on the wire,
 // so their bytes are one range, loaded with 16-B loads (8 per lane in
 // flight) -- one memory round trip per group instead of several per row.
@@ -378,13 +392,21 @@ __global__ __launch_bounds__(kDecWaves * kWave) void k_cesu_decode(uint8_t* text
       __builtin_amdgcn_wave_barrier();
     }
     const LdsBytes lsrc{lbuf, a0};
+    // staged: every lane classifies its own row from LDS (aligned dwords),
+    // so ASCII rows -- most tweets -- leave the wave's per-row walk entirely
+    int my_cls = -1;
+    if (staged) {
+      if (mine) my_cls = lane_row_class(lbuf, int(s0 - a0), int(s1 - a0));
+      if (my_cls == 0) fl = uint8_t(fl & ~kRowCesu);
+      m = __ballot(my_cls > 0);
+    }
     while (m) {
       const int l = __builtin_ctzll(m);
       m &= m - 1;
       // the row's extents from lane l's registers (a load here would put a
       // memory round trip on every row of the wave's sequential walk)
       const int64_t o = bcast_lane64(s0, l), e = bcast_lane64(s1, l);
-      const int cls = staged ? row_class(lsrc, o, e) : row_class(gsrc, o, e);
+      const int cls = staged ? __builtin_amdgcn_readlane(my_cls, l) : row_class(gsrc, o, e);
       if (cls == 0) {   // ASCII: narrow row as it is
         if (lane == l) fl = uint8_t(fl & ~kRowCesu);
         continue;
