@@ -93,9 +93,10 @@ def parse_args(argv=None):
     ap.add_argument("--prep-comm", choices=["auto", "gloo", "on", "off"], default="auto",
                     help="DP: a second communicator for the prep collectives (kept counts, active-id "
                          "union, tier counts) so batch t+1 is prepared entirely on the side stream while "
-                         "t's gradient all-reduces run.  auto/gloo: a host-staged gloo group (small "
-                         "messages; no second RCCL communicator competing for the process's hardware "
-                         "queues); on: the same kind as --comm; off: the collective part runs in line")
+                         "t's gradient all-reduces run.  gloo: a host-staged gloo group next to any --comm; "
+                         "on: the same kind as --comm (two RCCL communicators: opt-in); off: the collective "
+                         "part runs in line on the compute stream (RCCL: a few tens of us per collective, "
+                         "no host TCP hops); auto: gloo when --comm gloo, else off")
     ap.add_argument("--json-out", default="")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args(argv)
@@ -267,10 +268,13 @@ def main(argv=None) -> int:
     torch.cuda.set_device(device)
     from twitter_stream_ml_amd.parallel.affinity import bind_local_numa
     numa_cpus = bind_local_numa(device)   # before the pinned pool is allocated
-    if args.model == "kmeans" or args.prep_comm == "off":
+    prep_mode = args.prep_comm
+    if prep_mode == "auto":
+        prep_mode = "gloo" if args.comm == "gloo" else "off"
+    if args.model == "kmeans" or prep_mode == "off":
         comm, prep_comm = D.make_comm(device, args.comm), None
     else:   # LR: a second communicator lets batch t+1 be prepared during t's all-reduces
-        prep_kind = args.comm if args.prep_comm == "on" else "gloo"
+        prep_kind = args.comm if prep_mode == "on" else "gloo"
         comm, prep_comm = D.make_comm_pair(device, args.comm, prep_kind)
     ingest = args.ingest or "utf8"
 
