@@ -1,6 +1,6 @@
 """Cross-process data parallelism on one MI355X (SURVEY §2.4 DP, §2.5 CS2).
 
-N ranks (2 and 3) are N processes sharing GPU 0; each owns an engine whose collectives
+N ranks (2, 3 and 4) are N processes sharing GPU 0; each owns an engine whose collectives
 go through the host-staged torch.distributed gloo communicator
 (``parallel/dist.make_comm(..., "gloo")`` -> ``csrc/hip/comm.cpp`` HostComm).
 This is the engine DP path a one-GPU-per-rank RCCL job runs -- per-rank shards,
@@ -91,7 +91,7 @@ def _worker(rank, world, port, out_dir):
     D.shutdown()
 
 
-@pytest.fixture(scope="module", params=[2, 3], ids=["world2", "world3"])
+@pytest.fixture(scope="module", params=[2, 3, 4], ids=["world2", "world3", "world4"])
 def dp_runs(request, tmp_path_factory, hip_module):
     """2 ranks, and 3 (odd world: uneven shards, all-gather parts of unequal
     fill, fixed-order reductions over an odd number of partials)."""
