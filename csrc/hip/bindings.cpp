@@ -236,7 +236,7 @@ PYBIND11_MODULE(_twtml_hip, m) {
         std::vector<int> w(h.sw, h.sw + kScalarCols);
         d["widths"] = w;
         int mask = 0;
-        for (int c = 0; c < kScalarCols; ++c) mask |= (h.sw[c] == 8 ? 1 : 0) << c;
+        for (int c = 0; c < kScalarCols; ++c) mask |= (h.sw[c] == 64 ? 1 : 0) << c;
         d["wide_mask"] = mask;
         d["rows"] = h.spacked_n;
         return d;

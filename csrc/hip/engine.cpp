@@ -55,33 +55,43 @@ void HostBatch::pack_scalars(int64_t n, const int64_t* src) {
   th.clear();
   soff[0] = 0;
   for (int c = 0; c < kScalarCols; ++c) {
-    // range in unsigned arithmetic (hi - lo may overflow int64)
+    // range in unsigned arithmetic (hi - lo may overflow int64); a column
+    // ships as a bit stream of `bits`-bit offsets from its base, or raw int64
     const uint64_t span = uint64_t(hi[c]) - uint64_t(lo[c]);
-    const int w = span < (1ull << 8) ? 1 : span < (1ull << 16) ? 2 : span < (1ull << 24) ? 3
-                : span <= uint64_t(UINT32_MAX) ? 4 : 8;
-    sw[c] = uint8_t(w);
-    sbase[c] = w == 8 ? 0 : lo[c];
-    soff[c + 1] = soff[c] + int64_t(w) * n;
+    const int bits = span > uint64_t(UINT32_MAX) ? 64 : span == 0 ? 1 : 64 - __builtin_clzll(span);
+    sw[c] = uint8_t(bits);
+    sbase[c] = bits == 64 ? 0 : lo[c];
+    // + one u32 of slack: the device reads two consecutive words per value
+    const int64_t cb = bits == 64 ? 8 * n : ((n * bits + 31) / 32 + 1) * 4;
+    soff[c + 1] = soff[c] + ((cb + 7) & ~int64_t(7));   // columns 8-B aligned
   }
-  auto put = [&](int c) {
+  // rows [i0, i1) of column c; chunk boundaries are multiples of 32 rows, so
+  // chunks own whole 32-bit words of the stream
+  auto put = [&](int c, int64_t i0, int64_t i1) {
     const int64_t* v = src + int64_t(c) * n;
     uint8_t* o = spack + soff[c];
+    const int bits = sw[c];
+    if (bits == 64) {
+      std::memcpy(o + 8 * i0, v + i0, sizeof(int64_t) * size_t(i1 - i0));
+      return;
+    }
+    uint32_t* o32 = reinterpret_cast<uint32_t*>(o);
     const uint64_t b = uint64_t(sbase[c]);
-    switch (sw[c]) {
-      case 8: std::memcpy(o, v, sizeof(int64_t) * size_t(n)); break;
-      case 4: for (int64_t i = 0; i < n; ++i) reinterpret_cast<uint32_t*>(o)[i] = uint32_t(uint64_t(v[i]) - b); break;
-      case 2: for (int64_t i = 0; i < n; ++i) reinterpret_cast<uint16_t*>(o)[i] = uint16_t(uint64_t(v[i]) - b); break;
-      case 1: for (int64_t i = 0; i < n; ++i) o[i] = uint8_t(uint64_t(v[i]) - b); break;
-      default:
-        for (int64_t i = 0; i < n; ++i) {
-          const uint32_t x = uint32_t(uint64_t(v[i]) - b);
-          o[3 * i] = uint8_t(x);
-          o[3 * i + 1] = uint8_t(x >> 8);
-          o[3 * i + 2] = uint8_t(x >> 16);
-        }
+    const int64_t w0 = (i0 * bits) >> 5;
+    const int64_t w1 = i1 == n ? (soff[c + 1] - soff[c]) / 4 : (i1 * bits) >> 5;
+    std::memset(o32 + w0, 0, sizeof(uint32_t) * size_t(w1 - w0));
+    for (int64_t i = i0; i < i1; ++i) {
+      const uint64_t off = uint64_t(i) * uint64_t(bits);
+      const uint64_t t = (uint64_t(v[i]) - b) << (off & 31);
+      o32[off >> 5] |= uint32_t(t);
+      if ((off & 31) + uint64_t(bits) > 32) o32[(off >> 5) + 1] |= uint32_t(t >> 32);
     }
   };
-  for (int c = 0; c < kScalarCols; ++c) th.emplace_back(put, c);
+  const int64_t half = (n / 2 + 31) / 32 * 32;   // two chunks per column
+  for (int c = 0; c < kScalarCols; ++c) {
+    th.emplace_back(put, c, int64_t(0), std::min(half, n));
+    if (half < n) th.emplace_back(put, c, half, n);
+  }
   for (auto& x : th) x.join();
   spacked_n = n;
 }

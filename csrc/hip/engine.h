@@ -68,9 +68,9 @@ struct HostBatch {
   uint8_t* flags = nullptr;
   int64_t* scalars = nullptr;
   uint8_t* spack = nullptr;            // packed columns, column c at soff[c]
-  int64_t soff[kScalarCols + 1] = {};  // byte offsets; soff[c+1]-soff[c] = sw[c] * n
+  int64_t soff[kScalarCols + 1] = {};  // byte offsets of the columns (8-B aligned)
   int64_t sbase[kScalarCols] = {};
-  uint8_t sw[kScalarCols] = {};        // wire bytes per value (DevRawBatch::sw)
+  uint8_t sw[kScalarCols] = {};        // wire bits per value (DevRawBatch::sw)
   int64_t spacked_n = -1;              // rows of the last pack_scalars (-1: none)
   uint16_t* rowpack = nullptr;         // per row: byte length | wire flags << kRowLenBits;
                                        // ends rowpack_prefix(n) bytes before `text`

@@ -21,12 +21,12 @@ namespace twtml {
 // Raw batch in the wire format (csrc/host/wire.h).
 //
 // Scalar columns (retweetCount, followers, favourites, friends, createdAt) are
-// int64 in the record; on the wire column c is the offset from a per-batch
-// base in the fewest bytes that hold the batch's range (1, 2, 3 or 4 bytes,
-// little endian), or the raw int64 if the range needs more than 32 bits
-// (HostBatch::pack_scalars).  Counts are small and createdAt spans far less
-// than 49 days within a batch, so a tweet's five scalars take ~14 B instead
-// of 40.  Exact either way.
+// int64 in the record; on the wire column c is a bit stream of offsets from a
+// per-batch base in the fewest bits that hold the batch's range (1..32), or
+// the raw int64 if the range needs more than 32 bits (HostBatch::pack_scalars).
+// Counts are small and createdAt spans far less than 49 days within a batch,
+// so a tweet's five scalars take ~12 B instead of 40 (14 B with whole-byte
+// widths).  Exact either way.
 constexpr int kScalarCols = 5;
 
 struct DevRawBatch {
@@ -34,26 +34,22 @@ struct DevRawBatch {
   const int64_t* offsets;   // [n] byte offset where row r starts
   const int64_t* oend;      // [n] byte offset where it ends (offsets + 1 unless rows were relocated)
   const uint8_t* flags;     // [n] bit0 isRetweet, bit1 wide (cesu rows are expanded to wide)
-  const uint8_t* scol[kScalarCols];   // column c: n values of sw[c] bytes (+ sbase[c])
+  const uint8_t* scol[kScalarCols];   // column c: n values of sw[c] bits (+ sbase[c]), 8-B aligned
   int64_t sbase[kScalarCols];
-  uint8_t sw[kScalarCols];  // bytes per value: 1..4 (offset from sbase) or 8 (raw int64)
+  uint8_t sw[kScalarCols];  // bits per value: 1..32 (offset from sbase, bit stream) or 64 (raw int64)
   int64_t n;                // rows in this batch (host-known)
   int64_t bytes;
 };
 
 // Scalar column c of raw row r (the width test is wave-uniform).
 __device__ __forceinline__ int64_t raw_scalar(const DevRawBatch& b, int c, int64_t r) {
-  const uint8_t* p = b.scol[c];
-  switch (b.sw[c]) {
-    case 8: return reinterpret_cast<const int64_t*>(p)[r];
-    case 4: return b.sbase[c] + int64_t(reinterpret_cast<const uint32_t*>(p)[r]);
-    case 2: return b.sbase[c] + int64_t(reinterpret_cast<const uint16_t*>(p)[r]);
-    case 1: return b.sbase[c] + int64_t(p[r]);
-    default: {   // 3 bytes
-      const uint8_t* q = p + 3 * r;
-      return b.sbase[c] + int64_t(uint32_t(q[0]) | (uint32_t(q[1]) << 8) | (uint32_t(q[2]) << 16));
-    }
-  }
+  const int bits = b.sw[c];
+  if (bits == 64) return reinterpret_cast<const int64_t*>(b.scol[c])[r];
+  // bit stream: value r at bit r * bits, read from two aligned words
+  const uint32_t* p = reinterpret_cast<const uint32_t*>(b.scol[c]);
+  const uint64_t off = uint64_t(r) * uint64_t(bits);
+  const uint64_t w = uint64_t(p[off >> 5]) | (uint64_t(p[(off >> 5) + 1]) << 32);
+  return b.sbase[c] + int64_t((w >> (off & 31)) & ((uint64_t(1) << bits) - 1u));
 }
 
 constexpr uint8_t kRowRetweet = 1;

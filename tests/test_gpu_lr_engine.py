@@ -84,7 +84,11 @@ def test_featurize_matches_oracle(hip_module, F, hash, wide, longrow, ingest):
     sw = hb._hb.scalar_wire
     assert sw["rows"] == raw.n
     assert sw["wide_mask"] == (0b10010 if wide else 0), sw
-    assert all(w in (1, 2, 3, 4, 8) for w in sw["widths"]) and max(sw["widths"]) <= (8 if wide else 4)
+    # bits per value: the column's range (bit-packed), or 64 (raw int64)
+    sc = raw.scalars.astype(np.int64)
+    for c, w in enumerate(sw["widths"]):
+        span = int(sc[c].max()) - int(sc[c].min())
+        assert w == (64 if span >= 1 << 32 else max(1, span.bit_length())), (c, w, span)
     assert hb.rows_packed == (not longrow)
     dbg = eng._eng.debug_prepared()
     fb = featurize_batch(raw, F, 100, 1000, now_ms=NOW, hash=hash)

@@ -127,7 +127,7 @@ class HostBatchView:
     ``load`` packs the UTF-16 batch into narrow (Latin-1, 1 byte/unit) /
     cesu / wide rows with the native multi-threaded packer
     (``csrc/host/wire.cpp``): typical tweet text crosses PCIe at half the
-    UTF-16 size.  The five int64 scalar columns ship as 1-4 byte offsets
+    UTF-16 size.  The five int64 scalar columns ship as bit-packed offsets
     from a per-batch base when their range fits (exact), and a row's byte
     length + flags as one u16 that the device scans back into offsets.
     ``load_utf16`` stages only the row words and scalars and leaves the
@@ -176,7 +176,7 @@ class HostBatchView:
         self.bytes = int(host().wire_pack(raw.text, raw.offsets, raw.is_retweet, self.text,
                                           self.offsets, self.flags))
         self.scalars_flat[:5 * n] = raw.scalars.reshape(-1)
-        self._hb.pack_scalars(n)   # u32 + per-batch base where a column's range fits
+        self._hb.pack_scalars(n)   # bit-packed offsets from a per-batch base where a column's range fits
         self.rows_packed = bool(self._hb.pack_rows(n))   # offsets + flags as 2 B per row
         self.n, self.units, self.batch_time_ms = n, u, raw.batch_time_ms
         self.ext_text, self._ext_owner = 0, None
