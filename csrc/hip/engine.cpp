@@ -75,23 +75,30 @@ void HostBatch::pack_scalars(int64_t n, const int64_t* src) {
       std::memcpy(o + 8 * i0, v + i0, sizeof(int64_t) * size_t(i1 - i0));
       return;
     }
-    uint32_t* o32 = reinterpret_cast<uint32_t*>(o);
+    // word-at-a-time writer: the chunk starts on a word boundary
+    uint32_t* out = reinterpret_cast<uint32_t*>(o) + ((i0 * bits) >> 5);
     const uint64_t b = uint64_t(sbase[c]);
-    const int64_t w0 = (i0 * bits) >> 5;
-    const int64_t w1 = i1 == n ? (soff[c + 1] - soff[c]) / 4 : (i1 * bits) >> 5;
-    std::memset(o32 + w0, 0, sizeof(uint32_t) * size_t(w1 - w0));
+    uint64_t acc = 0;
+    int nb = 0;
     for (int64_t i = i0; i < i1; ++i) {
-      const uint64_t off = uint64_t(i) * uint64_t(bits);
-      const uint64_t t = (uint64_t(v[i]) - b) << (off & 31);
-      o32[off >> 5] |= uint32_t(t);
-      if ((off & 31) + uint64_t(bits) > 32) o32[(off >> 5) + 1] |= uint32_t(t >> 32);
+      acc |= (uint64_t(v[i]) - b) << nb;
+      nb += bits;
+      if (nb >= 32) {
+        *out++ = uint32_t(acc);
+        acc >>= 32;
+        nb -= 32;
+      }
     }
+    if (nb > 0) *out++ = uint32_t(acc);
+    if (i1 == n)   // the column's slack words
+      for (uint32_t* end = reinterpret_cast<uint32_t*>(o + (soff[c + 1] - soff[c])); out < end;) *out++ = 0u;
   };
-  const int64_t half = (n / 2 + 31) / 32 * 32;   // two chunks per column
-  for (int c = 0; c < kScalarCols; ++c) {
-    th.emplace_back(put, c, int64_t(0), std::min(half, n));
-    if (half < n) th.emplace_back(put, c, half, n);
-  }
+  const int64_t part = (n / 4 + 31) / 32 * 32;   // up to four chunks per column
+  for (int c = 0; c < kScalarCols; ++c)
+    for (int64_t i0 = 0; i0 < n || (i0 == 0 && n == 0); i0 += std::max<int64_t>(part, 32)) {
+      th.emplace_back(put, c, i0, std::min(i0 + std::max<int64_t>(part, 32), n));
+      if (n == 0) break;
+    }
   for (auto& x : th) x.join();
   spacked_n = n;
 }
