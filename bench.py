@@ -301,7 +301,10 @@ def main(argv=None) -> int:
     u8s = []
     if args.e2e:
         views = [HostBatchView(B, max_units) for _ in range(eng.raw_slots)]
-        if ingest == "utf8":   # the receiver's UTF-8 buffers (as the network delivered them)
+        if ingest == "utf8" and is_km and args.text_dims == 0:   # 2 scalar features: no text needed
+            from twitter_stream_ml_amd.ops.kmeans_engine import no_text
+            u8s = [no_text(r) for r in pool_raw]
+        elif ingest == "utf8":   # the receiver's UTF-8 buffers (as the network delivered them)
             u8s = [encode_utf8(r) for r in pool_raw]
             for u in u8s:
                 register_host(u.data)

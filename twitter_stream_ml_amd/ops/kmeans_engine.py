@@ -27,7 +27,14 @@ from ..oracle.mllib import KMeansState, decay_factor_from_half_life
 from ..records.batch import RawBatch
 from ._native import hip
 from .ingest import SlotPipeline
-from .lr_engine import HostBatchView
+from .lr_engine import HostBatchView, Utf8Text
+
+
+def no_text(raw: RawBatch) -> Utf8Text:
+    """Zero-length rows: what a 2-feature k-means (text_dims 0, the
+    reference's [retweetCount, followers]) needs of a batch's text -- only
+    the row words (retweet flags) and the two scalar columns cross PCIe."""
+    return Utf8Text(np.empty(0, np.uint8), np.zeros(raw.n + 1, np.int64))
 
 __all__ = ["KMDeviceConfig", "DeviceKMeans"]
 
@@ -76,8 +83,13 @@ class DeviceKMeans:
         self.set_state(st.centers, st.weights)
         self._staging: List[HostBatchView] = []
         self.raw_slots = int(hip().RAW_SLOTS)
-        self._pipe = SlotPipeline(self.raw_slots, lambda s, raw: self.staging(s).load(raw),
-                                  self.submit, self.synchronize)
+        self._pipe = SlotPipeline(self.raw_slots, self._stage, self.submit, self.synchronize)
+
+    def _stage(self, slot: int, raw: RawBatch) -> HostBatchView:
+        hb = self.staging(slot)
+        if self.cfg.text_dims == 0:
+            return hb.load_utf8(raw, no_text(raw), copy_text=True)
+        return hb.load(raw)
 
     # ---- model state (latestModel.clusterCenters / clusterWeights) -------
     def get_state(self):
