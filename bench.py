@@ -301,6 +301,9 @@ def main(argv=None) -> int:
     u8s = []
     if args.e2e:
         views = [HostBatchView(B, max_units) for _ in range(eng.raw_slots)]
+        if is_km:
+            for v in views:
+                v._hb.scalar_cols = 2   # k-means reads retweetCount and followersCount only
         if ingest == "utf8" and is_km and args.text_dims == 0:   # 2 scalar features: no text needed
             from twitter_stream_ml_amd.ops.kmeans_engine import no_text
             u8s = [no_text(r) for r in pool_raw]
@@ -312,7 +315,12 @@ def main(argv=None) -> int:
             for r in pool_raw:   # the receiver's buffers: DMA source of the text
                 register_host(r.text)
     else:
-        pool = [HostBatchView(B, max_units).load(r) for r in pool_raw]
+        pool = []
+        for r in pool_raw:
+            v = HostBatchView(B, max_units)
+            if is_km:
+                v._hb.scalar_cols = 2
+            pool.append(v.load(r))
         del pool_raw
     t_gen = time.time() - t_gen
     runner = Runner(eng, is_km, now_ms)

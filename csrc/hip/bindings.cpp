@@ -188,6 +188,7 @@ PYBIND11_MODULE(_twtml_hip, m) {
         py::gil_scoped_release nogil;
         return h.pack_rows(n);
       }, py::arg("n"))
+      .def_readwrite("scalar_cols", &HostBatch::scalar_cols)
       .def("pack_scalars", [](HostBatch& h, int64_t n) {
         py::gil_scoped_release nogil;
         h.pack_scalars(n);

@@ -49,10 +49,12 @@ void HostBatch::pack_scalars(int64_t n, const int64_t* src) {
     lo[c] = a;
     hi[c] = b;
   };
+  const int ncols = std::max(1, std::min(scalar_cols, kScalarCols));
   std::vector<std::thread> th;
-  for (int c = 0; c < kScalarCols; ++c) th.emplace_back(range, c);
+  for (int c = 0; c < ncols; ++c) th.emplace_back(range, c);
   for (auto& x : th) x.join();
   th.clear();
+  for (int c = ncols; c < kScalarCols; ++c) lo[c] = hi[c] = 0;   // not shipped
   soff[0] = 0;
   for (int c = 0; c < kScalarCols; ++c) {
     // range in unsigned arithmetic (hi - lo may overflow int64); a column
@@ -62,7 +64,7 @@ void HostBatch::pack_scalars(int64_t n, const int64_t* src) {
     sw[c] = uint8_t(bits);
     sbase[c] = bits == 64 ? 0 : lo[c];
     // + one u32 of slack: the device reads two consecutive words per value
-    const int64_t cb = bits == 64 ? 8 * n : ((n * bits + 31) / 32 + 1) * 4;
+    const int64_t cb = c >= ncols ? 0 : bits == 64 ? 8 * n : ((n * bits + 31) / 32 + 1) * 4;
     soff[c + 1] = soff[c] + ((cb + 7) & ~int64_t(7));   // columns 8-B aligned
   }
   // rows [i0, i1) of column c; chunk boundaries are multiples of 32 rows, so
@@ -94,13 +96,14 @@ void HostBatch::pack_scalars(int64_t n, const int64_t* src) {
       for (uint32_t* end = reinterpret_cast<uint32_t*>(o + (soff[c + 1] - soff[c])); out < end;) *out++ = 0u;
   };
   const int64_t part = (n / 4 + 31) / 32 * 32;   // up to four chunks per column
-  for (int c = 0; c < kScalarCols; ++c)
+  for (int c = 0; c < ncols; ++c)
     for (int64_t i0 = 0; i0 < n || (i0 == 0 && n == 0); i0 += std::max<int64_t>(part, 32)) {
       th.emplace_back(put, c, i0, std::min(i0 + std::max<int64_t>(part, 32), n));
       if (n == 0) break;
     }
   for (auto& x : th) x.join();
   spacked_n = n;
+  spacked_cols = ncols;
 }
 
 bool HostBatch::pack_rows(int64_t n) {

@@ -72,6 +72,8 @@ struct HostBatch {
   int64_t sbase[kScalarCols] = {};
   uint8_t sw[kScalarCols] = {};        // wire bits per value (DevRawBatch::sw)
   int64_t spacked_n = -1;              // rows of the last pack_scalars (-1: none)
+  int scalar_cols = kScalarCols;       // leading columns pack_scalars encodes (k-means reads 2)
+  int spacked_cols = 0;                // ... and the last call did
   uint16_t* rowpack = nullptr;         // per row: byte length | wire flags << kRowLenBits;
                                        // ends rowpack_prefix(n) bytes before `text`
   int64_t rowpacked_n = -1;            // rows of the last successful pack_rows (-1: none)

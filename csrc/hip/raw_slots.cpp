@@ -68,6 +68,8 @@ void RawSlots::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, h
     throw std::invalid_argument("text bytes exceed capacity");
   if (hb.offsets[0] != 0 || hb.offsets[n] != bytes) throw std::invalid_argument("offsets[n] != bytes");
   if (n > 0 && hb.spacked_n != n) throw std::logic_error("HostBatch scalars not packed for this row count");
+  if (n > 0 && hb.spacked_cols < scalar_cols)
+    throw std::logic_error("HostBatch packed fewer scalar columns than this engine reads");
   if (n > 0 && hb.rows_scanned_n != n) throw std::logic_error("HostBatch rows not packed (pack_rows) for this row count");
   // wait until the compute stream has finished reading this slot
   if (s.used) TWTML_HIP_CHECK(hipStreamWaitEvent(copy, s.consumed, 0));

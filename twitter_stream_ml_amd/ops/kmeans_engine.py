@@ -112,7 +112,9 @@ class DeviceKMeans:
     # ---- pipeline ---------------------------------------------------------
     def staging(self, i: int = 0) -> HostBatchView:
         while len(self._staging) <= i:
-            self._staging.append(HostBatchView(self.cfg.max_rows, self.cfg.max_units))
+            hb = HostBatchView(self.cfg.max_rows, self.cfg.max_units)
+            hb._hb.scalar_cols = 2   # the features read retweetCount and followersCount only
+            self._staging.append(hb)
         return self._staging[i]
 
     def submit(self, hb: HostBatchView, slot: int) -> None:
