@@ -66,11 +66,22 @@ def build_engine(conf: ConfArguments, rank: int, world: int, device: Optional[in
         dev = device if device is not None else (spec.devices[rank] if spec.devices else rank)
         from ..parallel.affinity import bind_local_numa
         bind_local_numa(dev)   # pinned staging buffers on the GPU's NUMA node
+        def lr_cfg(rows: int) -> LRDeviceConfig:
+            return LRDeviceConfig(num_text_features=F, hash=conf.hash, step_size=conf.stepSize,
+                                  num_iterations=conf.numIterations, fraction=conf.miniBatchFraction,
+                                  begin=conf.numRetweetBegin, end=conf.numRetweetEnd,
+                                  max_rows=rows, max_units=rows * 290)
+
         rows = max_rows or max(65536, int(conf.batchSize or 0))
-        cfg = LRDeviceConfig(num_text_features=F, hash=conf.hash, step_size=conf.stepSize,
-                             num_iterations=conf.numIterations, fraction=conf.miniBatchFraction,
-                             begin=conf.numRetweetBegin, end=conf.numRetweetEnd,
-                             max_rows=rows, max_units=rows * 290)
+        cap = os.environ.get("TWTML_BATCH_ROWS", "")
+        if cap.lower() == "hbm":   # the largest micro-batch 80 % of this GPU's free HBM holds
+            import torch
+            from ..ops.sizing import hbm_max_rows
+            rows = max(rows, hbm_max_rows(lambda r: DeviceLinearRegression(lr_cfg(r), device=dev),
+                                          torch.cuda.mem_get_info(dev)[0]))
+        elif cap:
+            rows = max(rows, int(cap))
+        cfg = lr_cfg(rows)
         # TWTML_PREP_COMM=1: a second RCCL communicator, so batch t+1 is
         # prepared while t's gradient all-reduces run (opt-in)
         comm, prep_comm = None, None
