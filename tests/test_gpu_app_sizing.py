@@ -19,3 +19,20 @@ def test_app_batch_rows_override(hip_module, monkeypatch, cap):
     del eng
     import gc
     gc.collect()   # the engine wrapper holds reference cycles: free its HBM now
+
+
+def test_engine_frees_device_memory_on_del(hip_module):
+    """No reference cycle in the engine wrappers: dropping the last reference
+    releases the engine's HBM at once (no wait for the cyclic GC)."""
+    import torch
+    from twitter_stream_ml_amd.ops.kmeans_engine import DeviceKMeans, KMDeviceConfig
+    from twitter_stream_ml_amd.ops.lr_engine import DeviceLinearRegression, LRDeviceConfig
+    free0 = torch.cuda.mem_get_info(0)[0]
+    lr = DeviceLinearRegression(LRDeviceConfig(num_text_features=100_000_000, hash="murmur3",
+                                               max_rows=200_000, max_units=200_000 * 300), device=0)
+    km = DeviceKMeans(KMDeviceConfig(k=64, text_dims=14, max_rows=200_000, max_units=200_000 * 300), device=0)
+    free1 = torch.cuda.mem_get_info(0)[0]
+    assert free0 - free1 > 1 << 30            # the F = 1e8 weights and maps alone are > 1 GB
+    del lr, km
+    free2 = torch.cuda.mem_get_info(0)[0]
+    assert free0 - free2 < 256 << 20, (free0, free1, free2)

@@ -21,6 +21,8 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
+import weakref
+
 import numpy as np
 
 from ..oracle.mllib import KMeansState, decay_factor_from_half_life
@@ -83,7 +85,9 @@ class DeviceKMeans:
         self.set_state(st.centers, st.weights)
         self._staging: List[HostBatchView] = []
         self.raw_slots = int(hip().RAW_SLOTS)
-        self._pipe = SlotPipeline(self.raw_slots, self._stage, self.submit, self.synchronize)
+        me = weakref.proxy(self)   # no reference cycle (see DeviceLinearRegression)
+        self._pipe = SlotPipeline(self.raw_slots, lambda s, raw: me._stage(s, raw),
+                                  lambda hb, slot: me.submit(hb, slot), lambda: me.synchronize())
 
     def _stage(self, slot: int, raw: RawBatch) -> HostBatchView:
         hb = self.staging(slot)

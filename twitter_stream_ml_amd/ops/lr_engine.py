@@ -20,6 +20,8 @@ from __future__ import annotations
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
+import weakref
+
 import numpy as np
 
 from ..records.batch import RETWEET_COUNT, RawBatch
@@ -246,8 +248,11 @@ class DeviceLinearRegression:
         self._eng = hip().LREngine(self.device, cfg.as_dict(), comm, prep_comm)
         self._staging: List[HostBatchView] = []
         self.raw_slots = int(hip().RAW_SLOTS)
-        self._pipe = SlotPipeline(self.raw_slots, lambda s, raw: self.staging(s).load(raw, cfg.ingest),
-                                  self.submit, self.synchronize)
+        # callbacks through a weak proxy: no reference cycle, so dropping the
+        # last reference frees the engine's device memory at once
+        me = weakref.proxy(self)
+        self._pipe = SlotPipeline(self.raw_slots, lambda s, raw: me.staging(s).load(raw, cfg.ingest),
+                                  lambda hb, slot: me.submit(hb, slot), lambda: me.synchronize())
 
     # ---- weights (MLlib setInitialWeights / latestModel.weights) ---------
     @property
