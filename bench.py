@@ -169,7 +169,8 @@ def run_e2e(r: Runner, raws, u8s, views, ingest: str, warmup: int, steps: int, s
     total = warmup + steps
     free: "queue.Queue[int]" = queue.Queue()
     ready: "queue.Queue" = queue.Queue()
-    for s in range(eng.raw_slots - 1):
+    ahead = max(1, min(int(os.environ.get("TWTML_E2E_DEPTH", eng.raw_slots - 1)), eng.raw_slots - 1))
+    for s in range(ahead):   # batches staged ahead of the one training
         free.put(s)
     err = []
 
