@@ -293,39 +293,73 @@ __device__ __forceinline__ int row_class(const Src& src, int64_t o, int64_t e) {
   return __any((acc & 0x80808080u) != 0u) ? 1 : 0;
 }
 
+// Byte flags of a dword -> a 4-bit mask: `x` holds 0/1 in bits 0, 8, 16, 24.
+__device__ __forceinline__ uint32_t byte_bits(uint32_t x) {
+  return (x * 0x10204080u) >> 28;   // the four products land on bits 28..31, no carries
+}
+
 // Decode row [o, e) (class 1 or 2) to dst (tail + 2 o); returns its units.
+// A lane takes an aligned dword of the row per step (256 bytes per wave
+// step: a tweet is one or two steps) plus the next dword for the
+// continuation bytes of its leads.  A unit starts at every non-continuation
+// byte (two at a 4-byte lead: the surrogate pair); a lane's units (0..8) are
+// ranked across the wave from four ballots of their bit planes.
 template <typename Src>
 __device__ __forceinline__ int64_t decode_row(const Src& src, uint8_t* text, int64_t o, int64_t e, int64_t d0,
                                               bool nar) {
   uint16_t* dst = reinterpret_cast<uint16_t*>(text + d0);
   uint8_t* dst8 = text + d0;
   const int lane = lane_id();
-  int64_t k = 0;
-  for (int64_t i0 = o; i0 < e; i0 += kWave) {
-    const int64_t i = i0 + lane;
-    const uint32_t b0 = i < e ? src.byte(i) : 0x80u;
-    const bool lead = i < e && (b0 & 0xC0u) != 0x80u;
-    // a 4-byte lead needs its 3 continuation bytes inside the row (malformed
-    // input must not write a second unit past the row's 2 * bytes region)
-    const bool four = lead && b0 >= 0xF0u && i + 3 < e;
-    const uint64_t lm = __ballot(lead), fm = __ballot(four);
-    if (lead) {
-      const int64_t at = k + __popcll(lm & lanes_below()) + __popcll(fm & lanes_below());
-      uint32_t u = b0;
-      if (four) {
-        const uint32_t cp = ((b0 & 0x07u) << 18) | ((src.byte(i + 1) & 0x3Fu) << 12) |
-                            ((src.byte(i + 2) & 0x3Fu) << 6) | (src.byte(i + 3) & 0x3Fu);
+  const uint64_t below = lanes_below();
+  const int32_t ie = int32_t(e - o);   // row bytes (< 2^13)
+  int32_t k = 0;
+  for (int64_t w0 = o & ~int64_t(3); w0 < e; w0 += 4 * kWave) {
+    const int32_t iw = int32_t(w0 - o) + 4 * lane;   // the lane's dword, relative to o (>= -3)
+    uint32_t v = 0, v2 = 0;
+    if (iw < ie) {
+      v = src.dword(w0 + 4 * lane);
+      v2 = src.dword(w0 + 4 * lane + 4);
+    }
+    // bytes j of the dword inside the row: 0 <= iw + j < ie
+    const int32_t lo = iw < 0 ? -iw : 0;
+    const int32_t hi = ie - iw >= 4 ? 4 : (ie - iw < 0 ? 0 : ie - iw);
+    const uint32_t rng = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+    // a 4-byte lead also needs iw + j + 3 < ie
+    const int32_t h3 = ie - iw - 3;
+    const uint32_t rng3 = h3 >= 4 ? 0xFu : (h3 <= 0 ? 0u : (1u << h3) - 1u);
+    // lead: top two bits != 10; 4-byte lead: top nibble 1111 (SWAR over the dword)
+    const uint32_t t = ((v >> 6) & 0x03030303u) ^ 0x02020202u;
+    const uint32_t lead = byte_bits(((t + 0x7F7F7F7Fu) >> 7) & 0x01010101u) & rng;
+    const uint32_t f = ((v >> 4) & 0x0F0F0F0Fu) + 0x01010101u;
+    const uint32_t four = byte_bits((f >> 4) & 0x01010101u) & lead & rng3;
+    const uint32_t cnt = uint32_t(__popc(lead) + __popc(four));
+    const uint64_t p0 = __ballot(cnt & 1u), p1 = __ballot(cnt & 2u), p2 = __ballot(cnt & 4u),
+                   p3 = __ballot(cnt & 8u);
+    int32_t at = k + __popcll(p0 & below) + 2 * __popcll(p1 & below) + 4 * __popcll(p2 & below) +
+                 8 * __popcll(p3 & below);
+    const uint64_t q = uint64_t(v) | (uint64_t(v2) << 32);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!((lead >> j) & 1u)) continue;
+      const uint32_t c0 = uint32_t(q >> (8 * j)) & 0xFFu;
+      const uint32_t c1 = uint32_t(q >> (8 * j + 8)) & 0x3Fu;
+      const uint32_t c2 = uint32_t(q >> (8 * j + 16)) & 0x3Fu;
+      if ((four >> j) & 1u) {
+        const uint32_t c3 = uint32_t(q >> (8 * j + 24)) & 0x3Fu;
+        const uint32_t cp = ((c0 & 0x07u) << 18) | (c1 << 12) | (c2 << 6) | c3;
         dst[at] = uint16_t(0xD800u + ((cp - 0x10000u) >> 10));
-        u = 0xDC00u + ((cp - 0x10000u) & 0x3FFu);
-        dst[at + 1] = uint16_t(u);
+        dst[at + 1] = uint16_t(0xDC00u + ((cp - 0x10000u) & 0x3FFu));
+        at += 2;
       } else {
-        if (b0 >= 0xE0u) u = ((b0 & 0x0Fu) << 12) | ((src.byte(i + 1) & 0x3Fu) << 6) | (src.byte(i + 2) & 0x3Fu);
-        else if (b0 >= 0x80u) u = ((b0 & 0x1Fu) << 6) | (src.byte(i + 1) & 0x3Fu);
+        uint32_t u = c0;
+        if (c0 >= 0xE0u) u = ((c0 & 0x0Fu) << 12) | (c1 << 6) | c2;
+        else if (c0 >= 0x80u) u = ((c0 & 0x1Fu) << 6) | c1;
         if (nar) dst8[at] = uint8_t(u);
         else dst[at] = uint16_t(u);
+        at += 1;
       }
     }
-    k += __popcll(lm) + __popcll(fm);
+    k += __popcll(p0) + 2 * __popcll(p1) + 4 * __popcll(p2) + 8 * __popcll(p3);
   }
   return k;
 }
@@ -367,68 +401,82 @@ __global__ __launch_bounds__(kDecWaves * kWave) void k_cesu_decode(uint8_t* text
     uint8_t fl = r < n ? flags[r] : 0;
     const bool mine = r < n && (fl & kRowCesu);
     int64_t s0 = r < n ? offsets[r] : 0, s1 = r < n ? offsets[r + 1] : 0;
-    uint64_t m = __ballot(mine);
-    // stage the group's byte range if it fits
-    const int last = int(std::min<int64_t>(kWave, n - g * kWave)) - 1;
-    const int64_t gs = offsets[g * kWave], ge = offsets[g * kWave + last + 1];
-    const int64_t a0 = gs & ~int64_t(15);
-    const bool staged = m != 0 && ge - a0 <= kDecStage;
-    if (staged) {
-      const int64_t nq = (ge - a0 + 15) >> 4;   // 16-B chunks
-      for (int64_t q0 = 0; q0 < nq; q0 += 8 * kWave) {
-        uint4 v[8];
+    // windows of consecutive rows whose bytes fit the wave's staging buffer
+    // (a whole 64-row group when it fits; long multi-byte groups take two):
+    // a group walked from global memory pays a memory round trip per row
+    // step and became the kernel's tail
+    uint64_t todo = __ballot(mine);
+    while (todo) {
+      const int lf = __builtin_ctzll(todo);
+      const int64_t a0 = bcast_lane64(s0, lf) & ~int64_t(15);
+      const uint64_t fit = __ballot(r < n && lane >= lf && s1 - a0 <= kDecStage);
+      uint64_t win, m;
+      bool staged = (fit >> lf) & 1u;
+      if (staged) {   // offsets grow with the lane: the fitting rows are lanes lf..lk
+        const int lk = 63 - __builtin_clzll(fit);
+        win = (lk == 63 ? ~uint64_t(0) : ((uint64_t(1) << (lk + 1)) - 1u)) & ~((uint64_t(1) << lf) - 1u);
+        const int64_t ge = bcast_lane64(s1, lk);
+        const int64_t nq = (ge - a0 + 15) >> 4;   // 16-B chunks
+        for (int64_t q0 = 0; q0 < nq; q0 += 8 * kWave) {
+          uint4 v[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int64_t q = q0 + j * kWave + lane;
-          v[j] = q < nq ? *reinterpret_cast<const uint4*>(text + a0 + 16 * q) : make_uint4(0, 0, 0, 0);
-        }
+          for (int j = 0; j < 8; ++j) {
+            const int64_t q = q0 + j * kWave + lane;
+            v[j] = q < nq ? *reinterpret_cast<const uint4*>(text + a0 + 16 * q) : make_uint4(0, 0, 0, 0);
+          }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int64_t q = q0 + j * kWave + lane;
-          if (q < nq) *reinterpret_cast<uint4*>(lbuf + 16 * q) = v[j];
+          for (int j = 0; j < 8; ++j) {
+            const int64_t q = q0 + j * kWave + lane;
+            if (q < nq) *reinterpret_cast<uint4*>(lbuf + 16 * q) = v[j];
+          }
         }
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+      } else {   // a single row longer than the buffer: from global memory
+        win = uint64_t(1) << lf;
       }
-      __threadfence_block();
-      __builtin_amdgcn_wave_barrier();
-    }
-    const LdsBytes lsrc{lbuf, a0};
-    // staged: every lane classifies its own row from LDS (aligned dwords),
-    // so ASCII rows -- most tweets -- leave the wave's per-row walk entirely
-    int my_cls = -1;
-    if (staged) {
-      if (mine) my_cls = lane_row_class(lbuf, int(s0 - a0), int(s1 - a0));
-      if (my_cls == 0) fl = uint8_t(fl & ~kRowCesu);
-      m = __ballot(my_cls > 0);
-    }
-    while (m) {
-      const int l = __builtin_ctzll(m);
-      m &= m - 1;
-      // the row's extents from lane l's registers (a load here would put a
-      // memory round trip on every row of the wave's sequential walk)
-      const int64_t o = bcast_lane64(s0, l), e = bcast_lane64(s1, l);
-      const int cls = staged ? __builtin_amdgcn_readlane(my_cls, l) : row_class(gsrc, o, e);
-      if (cls == 0) {   // ASCII: narrow row as it is
-        if (lane == l) fl = uint8_t(fl & ~kRowCesu);
-        continue;
+      m = todo & win;
+      todo &= ~win;
+      const LdsBytes lsrc{lbuf, a0};
+      // staged: every lane classifies its own row from LDS (aligned dwords),
+      // so ASCII rows -- most tweets -- leave the wave's per-row walk entirely
+      int my_cls = -1;
+      if (staged) {
+        const bool in_win = (m >> lane) & 1u;
+        if (in_win) my_cls = lane_row_class(lbuf, int(s0 - a0), int(s1 - a0));
+        if (my_cls == 0) fl = uint8_t(fl & ~kRowCesu);
+        m = __ballot(my_cls > 0);
       }
-      // Latin-1 rows decode straight to narrow bytes (no UTF-16 pass, no
-      // narrowing pass in k_row_normalize); others to UTF-16
-      const bool nar = cls == 1;
-      const int64_t d0 = tail + 2 * o;
-      const int64_t k = staged ? decode_row(lsrc, text, o, e, d0, nar) : decode_row(gsrc, text, o, e, d0, nar);
-      if (lane == l) {
-        s0 = d0;
-        s1 = d0 + (nar ? k : 2 * k);
-        fl = nar ? uint8_t(fl & ~kRowCesu) : uint8_t((fl & ~kRowCesu) | kRowWide);
+      while (m) {
+        const int l = __builtin_ctzll(m);
+        m &= m - 1;
+        // the row's extents from lane l's registers (a load here would put a
+        // memory round trip on every row of the wave's sequential walk)
+        const int64_t o = bcast_lane64(s0, l), e = bcast_lane64(s1, l);
+        const int cls = staged ? __builtin_amdgcn_readlane(my_cls, l) : row_class(gsrc, o, e);
+        if (cls == 0) {   // ASCII: narrow row as it is
+          if (lane == l) fl = uint8_t(fl & ~kRowCesu);
+          continue;
+        }
+        // Latin-1 rows decode straight to narrow bytes (no UTF-16 pass, no
+        // narrowing pass in k_row_normalize); others to UTF-16
+        const bool nar = cls == 1;
+        const int64_t d0 = tail + 2 * o;
+        const int64_t k = staged ? decode_row(lsrc, text, o, e, d0, nar) : decode_row(gsrc, text, o, e, d0, nar);
+        if (lane == l) {
+          s0 = d0;
+          s1 = d0 + (nar ? k : 2 * k);
+          fl = nar ? uint8_t(fl & ~kRowCesu) : uint8_t((fl & ~kRowCesu) | kRowWide);
+        }
+        n_nar += nar ? 1 : 0;
       }
-      n_nar += nar ? 1 : 0;
+      __builtin_amdgcn_wave_barrier();   // LDS reads of this window precede the next staging
     }
     if (r < n) {
       rstart[r] = s0;
       rend[r] = s1;
       if (mine) flags[r] = fl;
     }
-    __builtin_amdgcn_wave_barrier();   // LDS reads of this group precede the next staging
   }
   if (stats && lane == 0 && n_nar) atomicAdd(reinterpret_cast<unsigned long long*>(&stats[1]), (unsigned long long)n_nar);
 }
