@@ -1,5 +1,6 @@
 // LREngine implementation; see engine.h.
 #include "engine.h"
+#include "../common/task_pool.h"
 #include "alloc.h"
 #include "trace.h"
 
@@ -42,18 +43,33 @@ void HostBatch::pack_scalars(int64_t n, const int64_t* src) {
   if (n < 0 || n > max_rows) throw std::invalid_argument("pack_scalars: bad row count");
   if (!src) src = scalars;
   int64_t lo[kScalarCols], hi[kScalarCols];
-  auto range = [&](int c) {
-    const int64_t* v = src + int64_t(c) * n;
-    int64_t a = n ? v[0] : 0, b = a;
-    for (int64_t i = 1; i < n; ++i) { a = std::min(a, v[i]); b = std::max(b, v[i]); }
-    lo[c] = a;
-    hi[c] = b;
-  };
   const int ncols = std::max(1, std::min(scalar_cols, kScalarCols));
-  std::vector<std::thread> th;
-  for (int c = 0; c < ncols; ++c) th.emplace_back(range, c);
-  for (auto& x : th) x.join();
-  th.clear();
+  TaskPool& pool = TaskPool::get();
+  // chunks of whole 32-row words: a column's chunks own disjoint words of its stream
+  const int per_col = int(std::max<int64_t>(1, std::min<int64_t>((pool.width() + ncols - 1) / ncols,
+                                                                   (n + 65535) / 65536)));
+  const int64_t part = std::max<int64_t>(32, (n / per_col + 31) / 32 * 32);
+  const int nparts = int(std::max<int64_t>(1, (n + part - 1) / part));
+  std::vector<int64_t> plo(size_t(ncols) * nparts), phi(size_t(ncols) * nparts);
+  pool.run(ncols * nparts, [&](int task) {
+    const int c = task / nparts;
+    const int64_t i0 = int64_t(task % nparts) * part, i1 = std::min(n, i0 + part);
+    const int64_t* v = src + int64_t(c) * n;
+    int64_t a = i0 < i1 ? v[i0] : INT64_MAX, b = i0 < i1 ? v[i0] : INT64_MIN;
+    for (int64_t i = i0 + 1; i < i1; ++i) { a = std::min(a, v[i]); b = std::max(b, v[i]); }
+    plo[size_t(task)] = a;
+    phi[size_t(task)] = b;
+  });
+  for (int c = 0; c < ncols; ++c) {
+    lo[c] = hi[c] = 0;
+    if (n == 0) continue;
+    lo[c] = INT64_MAX;
+    hi[c] = INT64_MIN;
+    for (int k = 0; k < nparts; ++k) {
+      lo[c] = std::min(lo[c], plo[size_t(c) * nparts + k]);
+      hi[c] = std::max(hi[c], phi[size_t(c) * nparts + k]);
+    }
+  }
   for (int c = ncols; c < kScalarCols; ++c) lo[c] = hi[c] = 0;   // not shipped
   soff[0] = 0;
   for (int c = 0; c < kScalarCols; ++c) {
@@ -95,13 +111,11 @@ void HostBatch::pack_scalars(int64_t n, const int64_t* src) {
     if (i1 == n)   // the column's slack words
       for (uint32_t* end = reinterpret_cast<uint32_t*>(o + (soff[c + 1] - soff[c])); out < end;) *out++ = 0u;
   };
-  const int64_t part = (n / 4 + 31) / 32 * 32;   // up to four chunks per column
-  for (int c = 0; c < ncols; ++c)
-    for (int64_t i0 = 0; i0 < n || (i0 == 0 && n == 0); i0 += std::max<int64_t>(part, 32)) {
-      th.emplace_back(put, c, i0, std::min(i0 + std::max<int64_t>(part, 32), n));
-      if (n == 0) break;
-    }
-  for (auto& x : th) x.join();
+  pool.run(ncols * nparts, [&](int task) {
+    const int c = task / nparts;
+    const int64_t i0 = int64_t(task % nparts) * part;
+    put(c, i0, std::min(n, i0 + part));
+  });
   spacked_n = n;
   spacked_cols = ncols;
 }
@@ -140,7 +154,8 @@ void HostBatch::load_raw(const uint8_t* t, const int64_t* uoff, int64_t scale, u
   if (n > 0 && uoff[0] != 0) throw std::invalid_argument("load: offsets must start at 0");
   rowpacked_n = -1;
   rowpack = reinterpret_cast<uint16_t*>(text - rowpack_prefix(n));
-  if (threads <= 0) threads = int(std::min<unsigned>(8, std::max(1u, std::thread::hardware_concurrency())));
+  TaskPool& pool = TaskPool::get();
+  if (threads <= 0) threads = pool.width();
   const int T = int(std::max<int64_t>(1, std::min<int64_t>(threads, (n + 65535) / 65536)));
   std::vector<uint8_t> fit(size_t(T), 1);
   auto rows = [&](int c) {
@@ -160,10 +175,7 @@ void HostBatch::load_raw(const uint8_t* t, const int64_t* uoff, int64_t scale, u
       if (b1 > b0) std::memcpy(text + b0, t + b0, size_t(b1 - b0));
     }
   };
-  std::vector<std::thread> th;
-  for (int c = 1; c < T; ++c) th.emplace_back(rows, c);
-  rows(0);
-  for (auto& x : th) x.join();
+  pool.run(T, rows);
   offsets[0] = 0;
   pack_scalars(n, sc);
   rows_scanned_n = n;

@@ -33,14 +33,14 @@ def _build(tmp_path, name, flags):
 
 def _run(exe, env_extra):
     env = dict(os.environ, **env_extra)
-    env.pop("LD_PRELOAD", None)   # the sanitizer runtime must come first in the process
     r = subprocess.run([exe, "12000", "4"], capture_output=True, text=True, timeout=240, env=env)
     return r
 
 
 def test_host_runtime_asan_ubsan(tmp_path):
     exe = _build(tmp_path, "selftest_asan", ["-fsanitize=address,undefined",
-                                             "-fno-sanitize-recover=undefined"])
+                                             "-fno-sanitize-recover=undefined",
+                                             "-static-libasan"])
     r = _run(exe, {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0",
                    "UBSAN_OPTIONS": "print_stacktrace=1"})
     assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
@@ -49,7 +49,7 @@ def test_host_runtime_asan_ubsan(tmp_path):
 
 
 def test_host_runtime_tsan(tmp_path):
-    exe = _build(tmp_path, "selftest_tsan", ["-fsanitize=thread"])
+    exe = _build(tmp_path, "selftest_tsan", ["-fsanitize=thread", "-static-libtsan"])
     r = _run(exe, {"TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1"})
     if r.returncode != 0 and "unexpected memory mapping" in r.stderr:
         pytest.skip("ThreadSanitizer cannot map its shadow memory on this kernel")

@@ -1,7 +1,8 @@
 // Host-runtime self test for sanitizer builds (SURVEY §5 "Race detection /
 // sanitizers"): the multi-threaded synthetic generator, the multi-threaded
 // wire packer and its inverse, the special-row pre-lowering and the CPU
-// featurizer, run end to end on a batch with Unicode / special rows.
+// featurizer, run end to end on a batch with Unicode / special rows, and the
+// staging task pool (back-to-back and concurrent runs).
 // tests/test_host_sanitizers.py compiles it with -fsanitize=address,undefined
 // and with -fsanitize=thread (the GPU code is never built with sanitizers
 // on this pool).  Exit status 0 = every check passed.
@@ -11,6 +12,10 @@
 #include <cstring>
 #include <vector>
 
+#include <atomic>
+#include <thread>
+
+#include "common/task_pool.h"
 #include "host/featurize_cpu.h"
 #include "host/synth.h"
 #include "host/unicode_lower.h"
@@ -95,6 +100,30 @@ int main(int argc, char** argv) {
   }
   const uint8_t abc[3] = {'a', 'b', 'c'};
   CHECK(murmur3_spark(abc, 3, 42) == murmur3_spark(abc, 3, 42));
+
+  // staging task pool: every task exactly once, runs back to back (a worker
+  // waking late for a finished run must not take the next run's tasks) and
+  // from two callers at once
+  {
+    TaskPool& pool = TaskPool::get();
+    bool once = true;
+    for (int r = 0; r < 2000; ++r) {
+      const int nt = 1 + r % 37;
+      std::vector<std::atomic<int>> hits(static_cast<size_t>(nt));
+      for (auto& h : hits) h.store(0);
+      pool.run(nt, [&](int i) { hits[size_t(i)].fetch_add(1); });
+      for (auto& h : hits) once &= h.load() == 1;
+    }
+    CHECK(once);
+    std::atomic<long> sum{0};
+    auto caller = [&](int base) {
+      for (int r = 0; r < 300; ++r) pool.run(16, [&](int i) { sum.fetch_add(base + i); });
+    };
+    std::thread a(caller, 0), b(caller, 1000);
+    a.join();
+    b.join();
+    CHECK(sum.load() == 300L * (120 + 16 * 1000 + 120));
+  }
 
   if (fails) {
     std::fprintf(stderr, "%d check(s) failed\n", fails);
