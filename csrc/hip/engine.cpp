@@ -158,29 +158,39 @@ void HostBatch::load_raw(const uint8_t* t, const int64_t* uoff, int64_t scale, u
   if (threads <= 0) threads = pool.width();
   const int T = int(std::max<int64_t>(1, std::min<int64_t>(threads, (n + 65535) / 65536)));
   std::vector<uint8_t> fit(size_t(T), 1);
+  // offsets / flags: the device rebuilds both from the row words of a packed
+  // batch, so the DMA path (text not copied) writes them only when a row does
+  // not fit a row word; a copied batch keeps them for as_raw()
+  auto host_rows = [&](int64_t r0, int64_t r1) {
+    for (int64_t i = r0; i < r1; ++i) {
+      offsets[i + 1] = scale * uoff[i + 1];
+      flags[i] = uint8_t((is_rt[i] ? kRowRetweet : 0) | row_flags);
+    }
+  };
   auto rows = [&](int c) {
     const int64_t r0 = n * c / T, r1 = n * (c + 1) / T;
     bool ok = true;
     for (int64_t i = r0; i < r1; ++i) {
       const int64_t len = scale * (uoff[i + 1] - uoff[i]);
-      const uint8_t f = uint8_t((is_rt[i] ? kRowRetweet : 0) | row_flags);
-      offsets[i + 1] = scale * uoff[i + 1];
-      flags[i] = f;
+      const uint32_t f = (is_rt[i] ? kRowRetweet : 0) | row_flags;
       if (len < 0 || len >= (int64_t(1) << kRowLenBits)) ok = false;
       else rowpack[i] = uint16_t(len | (int64_t(f) << kRowLenBits));
     }
     fit[size_t(c)] = ok ? 1 : 0;
     if (copy_text) {   // this thread's share of the text bytes
+      host_rows(r0, r1);
       const int64_t b0 = scale * uoff[r0], b1 = scale * uoff[r1];
       if (b1 > b0) std::memcpy(text + b0, t + b0, size_t(b1 - b0));
     }
   };
   pool.run(T, rows);
-  offsets[0] = 0;
-  pack_scalars(n, sc);
-  rows_scanned_n = n;
   bool all = true;
   for (auto f : fit) all = all && f;
+  if (!copy_text && !all) pool.run(T, [&](int c) { host_rows(n * c / T, n * (c + 1) / T); });
+  offsets[0] = 0;
+  offsets[n] = scale * uoff[n];
+  pack_scalars(n, sc);
+  rows_scanned_n = n;
   if (all) rowpacked_n = n;
 }
 
