@@ -251,7 +251,18 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm, 
   int lo = 0, hi = 0;
   TWTML_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
   TWTML_HIP_CHECK(hipStreamCreateWithPriority(&compute_, hipStreamNonBlocking, hi));
-  TWTML_HIP_CHECK(hipStreamCreateWithPriority(&pstream_, hipStreamNonBlocking, lo));
+  // TWTML_PREP_CU=k:n[:s] (tuning, off by default): the prep stream may only
+  // use CUs i with (i / s) % n < k (measured: no gain, profiles/README.md)
+  if (const char* v = std::getenv("TWTML_PREP_CU")) {
+    int k = 0, n = 0, st = 1;
+    if (std::sscanf(v, "%d:%d:%d", &k, &n, &st) >= 2 && n > 0 && k > 0 && k < n && st > 0) {
+      std::vector<uint32_t> mask(size_t((num_cu_ + 31) / 32), 0u);
+      for (int i = 0; i < num_cu_; ++i)
+        if ((i / st) % n < k) mask[size_t(i / 32)] |= 1u << (i % 32);
+      TWTML_HIP_CHECK(hipExtStreamCreateWithCUMask(&pstream_, uint32_t(mask.size()), mask.data()));
+    }
+  }
+  if (!pstream_) TWTML_HIP_CHECK(hipStreamCreateWithPriority(&pstream_, hipStreamNonBlocking, lo));
   TWTML_HIP_CHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
   raw_.init(cfg_.max_rows, text_bytes_for_units(cfg_.max_units));
   for (auto& e : ev_) TWTML_HIP_CHECK(hipEventCreate(&e));

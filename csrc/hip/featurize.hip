@@ -808,7 +808,7 @@ __global__ __launch_bounds__(kBlock) void k_featurize(DevRawBatch b, DevPrepared
   const int64_t lds_lim = p.flag_len < kFlagLds ? p.flag_len : kFlagLds;
   const int64_t cap_groups = p.cap_entries / kChunkStride;
   const int64_t nch = (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;
-  for (int64_t c = wave; c < nch && c < cmax; c += nwaves) {
+  for (int64_t c = fp.c_lo + wave; c < nch && c < cmax && c < fp.c_hi; c += nwaves) {
     if (p.cfast[c]) continue;            // k_featurize_narrow's chunk
     const int32_t L8 = p.clen8[c];
     const int64_t g0 = p.cbase[c];
@@ -901,7 +901,7 @@ __global__ __launch_bounds__(kBlock) void k_featurize_narrow(DevRawBatch b, DevP
   const int64_t lds_lim = p.flag_len < kFlagLds ? p.flag_len : kFlagLds;
   const int64_t cap_groups = p.cap_entries / kChunkStride;
   const int64_t nch = (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;
-  for (int64_t c = wave; c < nch && c < cmax; c += nwaves) {
+  for (int64_t c = fp.c_lo + wave; c < nch && c < cmax && c < fp.c_hi; c += nwaves) {
     if (!p.cfast[c]) continue;
     const int32_t L8 = p.clen8[c];
     const int64_t g0 = p.cbase[c];
@@ -947,15 +947,22 @@ void launch_featurize(const DevRawBatch& b, const DevPrepared& p, const Featuriz
   if (cmax == 0) return;
   // ~8 blocks per CU, each sweeping many chunks, so the LDS flag bitmap is
   // flushed rarely (XCD-agnostic: chunk order is length-sorted anyway)
-  int grid = ceil_div(cmax, kBlock / kWave);
-  if (grid > 2048) grid = 2048;
-  // ids of a Java-hashed Latin-1 bigram are < 8161, always in the LDS bitmap;
-  // murmur3 ids above it get the flag cache
-  if (fp.hash_kind == 1 && p.flag_len > kFlagLds)
-    hipLaunchKernelGGL(k_featurize_narrow<true>, dim3(grid), dim3(kBlock), 0, s, b, p, fp, cmax);
-  else
-    hipLaunchKernelGGL(k_featurize_narrow<false>, dim3(grid), dim3(kBlock), 0, s, b, p, fp, cmax);
-  hipLaunchKernelGGL(k_featurize, dim3(grid), dim3(kBlock), 0, s, b, p, fp, lpage, lblocks, cmax);
+  const int ns = prep_slices();
+  for (int k = 0; k < ns; ++k) {   // chunk slices (prep_slices)
+    FeaturizeParams f = fp;
+    f.c_lo = cmax * k / ns;
+    f.c_hi = cmax * (k + 1) / ns;
+    if (f.c_hi <= f.c_lo) continue;
+    int grid = ceil_div(f.c_hi - f.c_lo, kBlock / kWave);
+    if (grid > 2048 * prep_grid_mult()) grid = 2048 * prep_grid_mult();
+    // ids of a Java-hashed Latin-1 bigram are < 8161, always in the LDS bitmap;
+    // murmur3 ids above it get the flag cache
+    if (f.hash_kind == 1 && p.flag_len > kFlagLds)
+      hipLaunchKernelGGL(k_featurize_narrow<true>, dim3(grid), dim3(kBlock), 0, s, b, p, f, cmax);
+    else
+      hipLaunchKernelGGL(k_featurize_narrow<false>, dim3(grid), dim3(kBlock), 0, s, b, p, f, cmax);
+    hipLaunchKernelGGL(k_featurize, dim3(grid), dim3(kBlock), 0, s, b, p, f, lpage, lblocks, cmax);
+  }
 }
 
 void launch_featurize_fast_ids(const DevRawBatch& b, const DevPrepared& p, FeaturizeParams fp, hipStream_t s) {

@@ -235,10 +235,12 @@ __global__ __launch_bounds__(kSplitWaves * kWave) void k_remap_hybrid(DevPrepare
   const uint32_t near_end = uint32_t(p.near_end);
 
   // the next chunk's packed row-text words are loaded one chunk ahead
-  int64_t rt_next = (from_text && wave < nch) ? p.rtext[wave * kRowsPerChunk + lane / kLanesPerRow] : 0;
-  for (int64_t c = wave; c < nch; c += nwaves) {
+  const int64_t c_end = nch < fp.c_hi ? nch : fp.c_hi;   // this launch's chunk slice
+  const int64_t c_first = fp.c_lo + wave;
+  int64_t rt_next = (from_text && c_first < c_end) ? p.rtext[c_first * kRowsPerChunk + lane / kLanesPerRow] : 0;
+  for (int64_t c = c_first; c < c_end; c += nwaves) {
     const int64_t rt = rt_next;
-    if (from_text && c + nwaves < nch) rt_next = p.rtext[(c + nwaves) * kRowsPerChunk + lane / kLanesPerRow];
+    if (from_text && c + nwaves < c_end) rt_next = p.rtext[(c + nwaves) * kRowsPerChunk + lane / kLanesPerRow];
     const int32_t L8 = p.clen8[c];
     const int64_t off = p.cbase[c] * kChunkStride + lane * kGroup;
     const int32_t* src = p.idx + off;
@@ -578,14 +580,14 @@ __global__ __launch_bounds__(1024) void k_code_tag_tiered(DevPrepared p, int64_t
 }
 
 // Far CSC: every far entry of every chunk list -> its slot's segment.
-__global__ __launch_bounds__(256) void k_far_csc(DevPrepared p) {
+__global__ __launch_bounds__(256) void k_far_csc(DevPrepared p, int64_t c_lo, int64_t c_hi) {
   const int lane = lane_id();
   const int64_t n_kept = p.counters[0];
   const int64_t nch = (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;
   const int64_t wave = (int64_t(blockIdx.x) * 256 + threadIdx.x) / kWave;
   const int64_t nwaves = int64_t(gridDim.x) * 256 / kWave;
   const uint32_t near_end = uint32_t(p.near_end);
-  for (int64_t c = wave; c < nch; c += nwaves) {
+  for (int64_t c = c_lo + wave; c < nch && c < c_hi; c += nwaves) {
     const int32_t fc = p.fcount[c];
     const uint32_t* fl = p.fslot + p.cbase[c] * kChunkStride;
     for (int32_t k = lane; k < fc; k += kWave) {
@@ -595,6 +597,26 @@ __global__ __launch_bounds__(256) void k_far_csc(DevPrepared p) {
       p.fcsc_pos[at] = uint32_t(c * kRowsPerChunk + (e >> 28));
       p.fcsc_slot[at] = sl;
     }
+  }
+}
+
+// k_remap_hybrid over the chunk range in prep_slices() launches; a
+// persistent-style grid per launch (each workgroup loads the 16 KB code
+// table once)
+template <bool TIERED>
+void launch_remap_slices(const DevPrepared& p, int64_t ns, int64_t pad_base, int64_t cmax, int num_cu,
+                         const DevRawBatch& b, const FeaturizeParams& fp, bool from_text, hipStream_t s) {
+  const int nsl = prep_slices();
+  for (int k = 0; k < nsl; ++k) {
+    FeaturizeParams f = fp;
+    f.c_lo = cmax * k / nsl;
+    f.c_hi = cmax * (k + 1) / nsl;
+    if (f.c_hi <= f.c_lo) continue;
+    int grid = int(std::min<int64_t>(int64_t(num_cu) * 4 * prep_grid_mult(),
+                                     (f.c_hi - f.c_lo + kSplitWaves - 1) / kSplitWaves));
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL(k_remap_hybrid<TIERED>, dim3(grid), dim3(kSplitWaves * kWave), 0, s, p, ns, pad_base,
+                       p.code, b, f, from_text ? 1 : 0);
   }
 }
 
@@ -616,11 +638,7 @@ void launch_remap_hybrid(const DevPrepared& p, int64_t entries, int64_t ns, int6
   hipLaunchKernelGGL(k_code_table, dim3(kCodeIds / 1024), dim3(1024), 0, s, p, p.code);
   const int64_t nU = pad_base - kNumNumeric;
   if (nU > 0) hipLaunchKernelGGL(k_code_tag, dim3(int((nU + 1023) / 1024)), dim3(1024), 0, s, p, nU);
-  // persistent-style grid (each workgroup loads the 16 KB code table once)
-  int grid = int(std::min<int64_t>(int64_t(num_cu) * 4, (cmax + kSplitWaves - 1) / kSplitWaves));
-  if (grid < 1) grid = 1;
-  hipLaunchKernelGGL(k_remap_hybrid<false>, dim3(grid), dim3(kSplitWaves * kWave), 0, s, p, ns, pad_base, p.code,
-                     b, fp, from_text ? 1 : 0);
+  launch_remap_slices<false>(p, ns, pad_base, cmax, num_cu, b, fp, from_text, s);
 }
 
 
@@ -677,10 +695,7 @@ void launch_tier_layout(const DevPrepared& p, int64_t entries, int64_t n_unique,
   TWTML_HIP_CHECK(hipMemsetAsync(p.fhist, 0, sizeof(uint64_t) * size_t(n_far + 1), s));
   if (entries > 0) {
     const int64_t cmax = (p.cap_rows + kRowsPerChunk - 1) / kRowsPerChunk;
-    int grid = int(std::min<int64_t>(int64_t(num_cu) * 4, (cmax + kSplitWaves - 1) / kSplitWaves));
-    if (grid < 1) grid = 1;
-    hipLaunchKernelGGL(k_remap_hybrid<true>, dim3(grid), dim3(kSplitWaves * kWave), 0, s, p, ns, p.near_end,
-                       p.code, b, fp, from_text ? 1 : 0);
+    launch_remap_slices<true>(p, ns, p.near_end, cmax, num_cu, b, fp, from_text, s);
   }
   // CSC offsets (exclusive scan of the far counts, in place), cursors, scatter
   launch_scan_excl(reinterpret_cast<const int64_t*>(p.fhist), reinterpret_cast<int64_t*>(p.fhist), n_far,
@@ -688,8 +703,13 @@ void launch_tier_layout(const DevPrepared& p, int64_t entries, int64_t n_unique,
   TWTML_HIP_CHECK(hipMemcpyAsync(p.fcur, p.fhist, sizeof(uint64_t) * size_t(n_far), hipMemcpyDeviceToDevice, s));
   if (entries > 0) {
     const int64_t cmax = (p.cap_rows + kRowsPerChunk - 1) / kRowsPerChunk;
-    const int grid = int(std::max<int64_t>(1, std::min<int64_t>((cmax + 3) / 4, int64_t(num_cu) * 8)));
-    hipLaunchKernelGGL(k_far_csc, dim3(grid), dim3(256), 0, s, p);
+    const int nsl = prep_slices();
+    for (int k = 0; k < nsl; ++k) {   // chunk slices (prep_slices)
+      const int64_t lo = cmax * k / nsl, hi = cmax * (k + 1) / nsl;
+      if (hi <= lo) continue;
+      const int grid = int(std::max<int64_t>(1, std::min<int64_t>((hi - lo + 3) / 4, int64_t(num_cu) * 8 * prep_grid_mult())));
+      hipLaunchKernelGGL(k_far_csc, dim3(grid), dim3(256), 0, s, p, lo, hi);
+    }
   }
 }
 

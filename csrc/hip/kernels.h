@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 namespace twtml {
 
@@ -178,6 +179,9 @@ struct FeaturizeParams {
   int64_t begin, end;
   int64_t now_ms;
   int32_t idx_mode = 0;       // narrow featurizer ids: 0 all, 1 lazy (sampled chunks), 2 all, no flags
+  // chunk slice [c_lo, c_hi) of one launch (prep kernels split into slices,
+  // see prep_slices())
+  int64_t c_lo = 0, c_hi = INT64_MAX;
 };
 
 void upload_lower_tables(hipStream_t s, uint8_t** d_page, uint16_t** d_blocks);
@@ -337,5 +341,29 @@ bool sgd_hybrid_fits(int64_t ns);
 int sgd_iter_grid(int64_t ns, int64_t n_kept, int num_cu, bool hybrid);
 
 // (k-means launchers: kmeans_kernels.h)
+
+// Grid-cap multiplier of the grid-stride prep kernels (TWTML_PREP_WG_MULT,
+// default 1): prep workgroups that live for the whole kernel hold their CUs
+// against the GD loop's next launch on the compute stream.
+// Launches per long prep kernel (TWTML_PREP_SLICES, default 1): the chunk
+// range is split so a launch on the prep stream ends before the GD loop's
+// next kernel has waited long behind it.
+inline int prep_slices() {
+  static const int m = [] {
+    const char* e = std::getenv("TWTML_PREP_SLICES");
+    const int v = e ? std::atoi(e) : 1;
+    return v >= 1 && v <= 64 ? v : 1;
+  }();
+  return m;
+}
+
+inline int prep_grid_mult() {
+  static const int m = [] {
+    const char* e = std::getenv("TWTML_PREP_WG_MULT");
+    const int v = e ? std::atoi(e) : 1;
+    return v >= 1 && v <= 64 ? v : 1;
+  }();
+  return m;
+}
 
 }  // namespace twtml
