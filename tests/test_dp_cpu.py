@@ -1,4 +1,4 @@
-"""Multi-process data parallelism on CPU (gloo, world_size 2 and 3).
+"""Multi-process data parallelism on CPU (gloo, world_size 2, 3 and 8 -- the driver's node size).
 
 Mirrors what one process per GPU does on an MI355X node (SURVEY §2.4 DP row):
 every rank owns a shard of each micro-batch, the per-iteration gradient (and
@@ -49,7 +49,7 @@ def _worker(rank, world, port, out_dir, fraction):
     D.shutdown()
 
 
-@pytest.mark.parametrize("world,fraction", [(2, 1.0), (3, 0.7)])
+@pytest.mark.parametrize("world,fraction", [(2, 1.0), (3, 0.7), (8, 1.0)])
 def test_cpu_dp_equals_single_process(tmp_path, world, fraction):
     port = _free_port()
     mp.start_processes(_worker, args=(world, port, str(tmp_path), fraction), nprocs=world,
