@@ -612,7 +612,7 @@ void launch_remap_slices(const DevPrepared& p, int64_t ns, int64_t pad_base, int
     f.c_lo = cmax * k / nsl;
     f.c_hi = cmax * (k + 1) / nsl;
     if (f.c_hi <= f.c_lo) continue;
-    int grid = int(std::min<int64_t>(int64_t(num_cu) * 4 * prep_grid_mult(),
+    int grid = int(std::min<int64_t>(int64_t(num_cu) * 4 * prep_grid_mult(TIERED ? 4 : 1),
                                      (f.c_hi - f.c_lo + kSplitWaves - 1) / kSplitWaves));
     if (grid < 1) grid = 1;
     hipLaunchKernelGGL(k_remap_hybrid<TIERED>, dim3(grid), dim3(kSplitWaves * kWave), 0, s, p, ns, pad_base,
@@ -707,7 +707,7 @@ void launch_tier_layout(const DevPrepared& p, int64_t entries, int64_t n_unique,
     for (int k = 0; k < nsl; ++k) {   // chunk slices (prep_slices)
       const int64_t lo = cmax * k / nsl, hi = cmax * (k + 1) / nsl;
       if (hi <= lo) continue;
-      const int grid = int(std::max<int64_t>(1, std::min<int64_t>((hi - lo + 3) / 4, int64_t(num_cu) * 8 * prep_grid_mult())));
+      const int grid = int(std::max<int64_t>(1, std::min<int64_t>((hi - lo + 3) / 4, int64_t(num_cu) * 8 * prep_grid_mult(4))));
       hipLaunchKernelGGL(k_far_csc, dim3(grid), dim3(256), 0, s, p, lo, hi);
     }
   }

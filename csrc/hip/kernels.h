@@ -357,13 +357,16 @@ inline int prep_slices() {
   return m;
 }
 
-inline int prep_grid_mult() {
+// def: the default when the variable is unset (4 for the tiered layout's
+// remap / far CSC: +0.5-1 % on wide and 1e8 murmur3; 1 for featurize, where
+// 4x the grid costs the toy bench ~0.5 %).
+inline int prep_grid_mult(int def = 1) {
   static const int m = [] {
     const char* e = std::getenv("TWTML_PREP_WG_MULT");
-    const int v = e ? std::atoi(e) : 1;
-    return v >= 1 && v <= 64 ? v : 1;
+    const int v = e ? std::atoi(e) : 0;
+    return v >= 1 && v <= 64 ? v : 0;
   }();
-  return m;
+  return m ? m : def;
 }
 
 }  // namespace twtml
