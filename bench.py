@@ -69,12 +69,15 @@ def parse_args(argv=None):
     ap.add_argument("--features", type=int, default=1_000_000, help="numTextFeatures")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--step-size", type=float, default=0.005)
-    ap.add_argument("--pool", type=int, default=4, help="pre-generated batches per rank")
+    ap.add_argument("--pool", type=int, default=0,
+                    help="pre-generated batches per rank (0: warmup + steps, i.e. every step trains a batch "
+                         "it has never seen; a smaller pool replays batches)")
     ap.add_argument("--hash", default="java")
     ap.add_argument("--seed", type=int, default=1234)
-    ap.add_argument("--profile", default="bench", choices=["bench", "wide"],
-                    help="synthetic data: bench (toy ~300-word vocabulary, ~1.4K active bigrams) or "
-                         "wide (realistic 50K-word multi-script vocabulary, ~200K active bigrams)")
+    ap.add_argument("--profile", default="wide", choices=["bench", "wide"],
+                    help="synthetic data: wide (default: realistic 50K-word multi-script vocabulary, "
+                         "~200K active bigrams per batch) or bench (toy ~300-word vocabulary, ~1.4K active "
+                         "bigrams)")
     ap.add_argument("--e2e", action="store_true",
                     help="stage every batch on the host inside the timed region (the default)")
     ap.add_argument("--prepacked", action="store_true",
@@ -255,6 +258,7 @@ def main(argv=None) -> int:
     from twitter_stream_ml_amd.parallel import dist as D
     from twitter_stream_ml_amd.ops.lr_engine import (DeviceLinearRegression, HostBatchView,
                                                      LRDeviceConfig, encode_utf8, register_host)
+    from twitter_stream_ml_amd.records.batch import RawBatch
     from twitter_stream_ml_amd.sources.synthetic import SynthConfig, generate_batch
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
@@ -288,7 +292,10 @@ def main(argv=None) -> int:
     else:
         B = int(args.batch)
     t_gen = time.time()
-    pool_raw = [generate_batch(synth, i * B, B, batch_time_ms=now_ms) for i in range(args.pool)]
+    n_pool = args.pool if args.pool > 0 else args.warmup + args.steps
+    if args.pool <= 0:   # fresh batches for every step, within a host-memory budget of pooled tweets
+        n_pool = max(1, min(n_pool, int(os.environ.get("TWTML_BENCH_POOL_TWEETS", "64000000")) // max(1, B)))
+    pool_raw = [generate_batch(synth, i * B, B, batch_time_ms=now_ms) for i in range(n_pool)]
     max_units = max(r.total_units for r in pool_raw) + 1024
     is_km = args.model == "kmeans"
     if is_km:
@@ -312,6 +319,9 @@ def main(argv=None) -> int:
             u8s = [encode_utf8(r) for r in pool_raw]
             for u in u8s:
                 register_host(u.data)
+            # the UTF-16 copy is not staged in this mode: keep only its length
+            pool_raw = [RawBatch(np.broadcast_to(np.uint16(0), r.text.shape), r.offsets, r.is_retweet,
+                                 r.scalars, r.batch_time_ms) for r in pool_raw]
         elif ingest == "utf16":
             for r in pool_raw:   # the receiver's buffers: DMA source of the text
                 register_host(r.text)
@@ -350,7 +360,9 @@ def main(argv=None) -> int:
     stage = runner.stage
     par = f"dp{info.world}" + ("-gloo" if args.comm == "gloo" else "")
     data = ("synthetic tweet-shaped records (seeded C++ generator, "
-            f"{'realistic 50K-word multi-script' if args.profile == 'wide' else 'toy ~300-word'} vocabulary)")
+            f"{'realistic 50K-word multi-script' if args.profile == 'wide' else 'toy ~300-word'} vocabulary, "
+            + (f"{n_pool} distinct batches per rank: no batch is trained twice)"
+               if n_pool >= args.warmup + args.steps else f"{n_pool} batches per rank, replayed)"))
     out = {
         "metric": "tweets/sec trained (whole node)",
         "value": round(value, 1),
@@ -397,6 +409,7 @@ def main(argv=None) -> int:
     if args.e2e:
         out["host_stage_ms_p50"] = round(getattr(runner, "host_stage_ms", 0.0), 3)
     out["pool_gen_s"] = round(t_gen, 2)
+    out["pool_batches"] = n_pool
     out["numa_bound_cpus"] = len(numa_cpus) if numa_cpus else None
     if info.is_main:
         line = json.dumps(out)
