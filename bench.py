@@ -93,13 +93,6 @@ def parse_args(argv=None):
     ap.add_argument("--comm", choices=["rccl", "gloo"], default="rccl",
                     help="DP gradient collectives: RCCL over xGMI, or host-staged torch.distributed "
                          "gloo (lets N ranks share one GPU for testing)")
-    ap.add_argument("--prep-comm", choices=["auto", "gloo", "on", "off"], default="auto",
-                    help="DP: a second communicator for the prep collectives (kept counts, active-id "
-                         "union, tier counts) so batch t+1 is prepared entirely on the side stream while "
-                         "t's gradient all-reduces run.  gloo: a host-staged gloo group next to any --comm; "
-                         "on: the same kind as --comm (two RCCL communicators: opt-in); off: the collective "
-                         "part runs in line on the compute stream (RCCL: a few tens of us per collective, "
-                         "no host TCP hops); auto: gloo when --comm gloo, else off")
     ap.add_argument("--json-out", default="")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args(argv)
@@ -273,14 +266,9 @@ def main(argv=None) -> int:
     torch.cuda.set_device(device)
     from twitter_stream_ml_amd.parallel.affinity import bind_local_numa
     numa_cpus = bind_local_numa(device)   # before the pinned pool is allocated
-    prep_mode = args.prep_comm
-    if prep_mode == "auto":
-        prep_mode = "gloo" if args.comm == "gloo" else "off"
-    if args.model == "kmeans" or prep_mode == "off":
-        comm, prep_comm = D.make_comm(device, args.comm), None
-    else:   # LR: a second communicator lets batch t+1 be prepared during t's all-reduces
-        prep_kind = args.comm if prep_mode == "on" else "gloo"
-        comm, prep_comm = D.make_comm_pair(device, args.comm, prep_kind)
+    # one communicator: LR DP issues one int64 all-reduce per GD iteration and
+    # one all-gather of the next batch's prep packets per batch
+    comm = D.make_comm(device, args.comm)
     ingest = args.ingest or "utf8"
 
     synth = SynthConfig.profile(args.profile, seed=args.seed + 7919 * info.rank)
@@ -304,8 +292,7 @@ def main(argv=None) -> int:
                               max_units=max_units, seed=args.seed)
         eng = DeviceKMeans(kcfg, device=device, comm=comm)
     else:
-        eng = DeviceLinearRegression(lr_config(args, B, max_units, ingest), device=device, comm=comm,
-                                     prep_comm=prep_comm)
+        eng = DeviceLinearRegression(lr_config(args, B, max_units, ingest), device=device, comm=comm)
     u8s = []
     if args.e2e:
         views = [HostBatchView(B, max_units) for _ in range(eng.raw_slots)]

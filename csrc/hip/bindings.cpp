@@ -48,7 +48,7 @@ static py::dict result_dict(BatchResult& r) {
   d["entries"] = r.entries;
   d["iterations"] = r.iterations;
   d["converged"] = r.converged;
-  d["overflow"] = r.overflow;
+  d["diverged"] = r.diverged;
   d["stats"] = std::vector<double>(r.stats, r.stats + 6);
   d["loss_history"] = r.loss_history;
   d["prep_ms"] = r.prep_ms;
@@ -244,13 +244,12 @@ PYBIND11_MODULE(_twtml_hip, m) {
       });
 
   py::class_<LREngine, std::shared_ptr<LREngine>>(m, "LREngine")
-      .def(py::init([](int device, const py::dict& cfg, std::shared_ptr<Comm> comm,
-                       std::shared_ptr<Comm> prep_comm) {
+      .def(py::init([](int device, const py::dict& cfg, std::shared_ptr<Comm> comm) {
              LRConfig c = lr_config(cfg);
              py::gil_scoped_release nogil;
-             return std::make_shared<LREngine>(device, c, comm, prep_comm);
+             return std::make_shared<LREngine>(device, c, comm);
            }),
-           py::arg("device"), py::arg("config"), py::arg("comm") = nullptr, py::arg("prep_comm") = nullptr)
+           py::arg("device"), py::arg("config"), py::arg("comm") = nullptr)
       .def("submit",
            [](LREngine& e, const HostBatch& hb, int64_t n, int64_t bytes, int slot, uintptr_t ext_text,
               int64_t now_ms) {

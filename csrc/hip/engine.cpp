@@ -224,8 +224,8 @@ static T* dmalloc(size_t n) {
   return static_cast<T*>(dev_alloc(n * sizeof(T)));
 }
 
-LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm, std::shared_ptr<Comm> prep_comm)
-    : device_(device), cfg_(cfg), comm_(std::move(comm)), prep_comm_(std::move(prep_comm)) {
+LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
+    : device_(device), cfg_(cfg), comm_(std::move(comm)) {
   if (cfg_.num_text_features <= 0) throw std::invalid_argument("numTextFeatures must be > 0");
   if (cfg_.max_rows <= 0 || cfg_.max_units < 0) throw std::invalid_argument("bad capacity");
   if (cfg_.max_rows >= (int64_t(1) << 31)) throw std::invalid_argument("max_rows must be < 2^31");
@@ -233,15 +233,10 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm, 
     throw std::invalid_argument("miniBatchFraction must be in (0, 1]");
   if (const char* v = std::getenv("TWTML_FORCE_TIERED")) force_tiered_ = v[0] == '1';   // tests
   world_ = comm_ ? comm_->world() : 1;
-  if (prep_comm_ && (prep_comm_->world() != world_ || prep_comm_->rank() != comm_->rank()))
-    throw std::invalid_argument("prep communicator must span the same ranks");
-  // Prepare-ahead: the local part of batch t+1's prep (decode .. featurize
-  // .. this rank's active set) always; its collective part (kept counts,
-  // active-id union, tier counts) + layout only on one GPU or with a second
-  // communicator, since it would run concurrently with t's gradient
-  // all-reduces.
+  // Prepare-ahead of batch t+1 while t trains: all of it on one GPU; on DP
+  // ranks the local part, then (after the training thread all-gathered the
+  // ranks' packets between two of t's GD iterations) the rest.
   overlap_ = cfg_.overlap != 0;
-  ahead_global_ = world_ == 1 || prep_comm_ != nullptr;
   if (const char* v = std::getenv("TWTML_OVERLAP")) overlap_ = overlap_ && v[0] != '0';
   TWTML_HIP_CHECK(hipSetDevice(device_));
   hipDeviceProp_t prop;
@@ -275,15 +270,16 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm, 
   sgd_.F = cfg_.num_text_features;
   sgd_.w64 = dmalloc<double>(size_t(nw));
   TWTML_HIP_CHECK(hipMemset(sgd_.w64, 0, sizeof(double) * size_t(nw)));  // Vectors.zeros
-  sgd_.red64 = dmalloc<double>(4);
   sgd_.stats = dmalloc<double>(8);
   sgd_.state = dmalloc<double>(kStateLen);
   sgd_.loss_hist = dmalloc<double>(size_t(std::max(1, cfg_.num_iterations)) + 2);
   sgd_.itrec = dmalloc<double>((size_t(std::max(1, cfg_.num_iterations)) + 2) * kRecStride);
   sgd_.pred_out = dmalloc<float>(size_t(cfg_.max_rows));
-  sgd_.nrm = dmalloc<double>(kNormParts);
+  sgd_.nrm = dmalloc<double>(2 * kNormParts);
   sgd_.wnorm_next = dmalloc<double>(1);
-  TWTML_HIP_CHECK(hipMemset(sgd_.red64, 0, 4 * sizeof(double)));
+  sgd_.world = world_;
+  sgd_.rank = comm_ ? comm_->rank() : 0;
+  sgd_.tail_len = sgd_tail_len(world_);
   ensure_compact(4096);
   TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_out_),
                                 (32 + size_t(std::max(1, cfg_.num_iterations))) * sizeof(double),
@@ -292,6 +288,16 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm, 
                                 (2 + size_t(std::max(1, cfg_.num_iterations))) * sizeof(double),
                                 hipHostMallocMapped | hipHostMallocCoherent));
   TWTML_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&sgd_.host_flags), host_flags_, 0));
+  if (world_ > 1) {
+    TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&ready_host_), 64, hipHostMallocMapped | hipHostMallocCoherent));
+    *ready_host_ = 0;
+    int64_t* dev_ready = nullptr;
+    TWTML_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&dev_ready), ready_host_, 0));
+    sgd_.ready_word = dev_ready;
+    dnu_ = dmalloc<int64_t>(size_t(world_));
+    TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&hnu_), sizeof(int64_t) * size_t(world_),
+                                  hipHostMallocDefault));
+  }
   TWTML_HIP_CHECK(hipDeviceSynchronize());
   if (overlap_) worker_ = std::thread([this] { prep_worker(); });
 }
@@ -344,11 +350,19 @@ void LREngine::alloc_prepared(PrepBuf& b) {
   p.ublk = dmalloc<int64_t>(size_t(fl / 4096) + 2);
   p.counters = dmalloc<int64_t>(8);
   b.n_global = dmalloc<int64_t>(2 * size_t(world_) + 2);
+  b.bounds = dmalloc<double>(kBoundsLen);
   TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&b.host_counters),
                                 (8 + 2 * size_t(world_)) * sizeof(int64_t), hipHostMallocDefault));
   TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&b.host_norm), 2 * sizeof(int64_t), hipHostMallocDefault));
   TWTML_HIP_CHECK(hipEventCreate(&b.ev_start));
   TWTML_HIP_CHECK(hipEventCreate(&b.ev_done));
+  if (world_ > 1) {
+    TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&b.host_hdr),
+                                  sizeof(int64_t) * size_t(world_) * (kC1HeaderWords / 2), hipHostMallocDefault));
+    TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&b.host_bounds), sizeof(double) * kBoundsLen,
+                                  hipHostMallocDefault));
+    TWTML_HIP_CHECK(hipEventCreateWithFlags(&b.ev_c1, hipEventDisableTiming));
+  }
 }
 
 void LREngine::free_prepared(PrepBuf& b) {
@@ -357,10 +371,13 @@ void LREngine::free_prepared(PrepBuf& b) {
                   p.hot_dense, p.clen8c, p.hot_slot, p.hot_of, p.slot_hist, p.code, p.cbase, p.idx, p.slot,
                   p.y, p.num, p.perm, p.rtext, p.scan_tmp, p.flags, p.uniq, p.slot_of, p.ublk, p.counters,
                   p.fslot, p.fcount, p.fhist, p.fcur, p.fcsc_pos, p.fcsc_slot, p.newslot, p.slot_fid, p.tscan,
-                  p.tscan_blk, p.hist_near, p.tparam, b.n_global, b.ugather};
+                  p.tscan_blk, p.hist_near, p.tparam, b.n_global, b.ugather, b.bounds, b.packet, b.gathered};
   for (void* x : bufs) if (x) (void)hipFree(x);
   if (b.host_counters) (void)hipHostFree(b.host_counters);
   if (b.host_norm) (void)hipHostFree(b.host_norm);
+  if (b.host_hdr) (void)hipHostFree(b.host_hdr);
+  if (b.host_bounds) (void)hipHostFree(b.host_bounds);
+  if (b.ev_c1) (void)hipEventDestroy(b.ev_c1);
   if (b.ev_start) (void)hipEventDestroy(b.ev_start);
   if (b.ev_done) (void)hipEventDestroy(b.ev_done);
   b = PrepBuf{};
@@ -430,7 +447,7 @@ void LREngine::ensure_part(int64_t n) {
     (void)hipFree(sgd_.part);
   }
   part_cap_ = std::max<int64_t>(n, part_cap_ * 2);
-  sgd_.part = dmalloc<double>(size_t(part_cap_));
+  sgd_.part = dmalloc<int64_t>(size_t(part_cap_));
 }
 
 void LREngine::ensure_compact(int64_t ns) {
@@ -440,18 +457,17 @@ void LREngine::ensure_compact(int64_t ns) {
     TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
     (void)hipFree(sgd_.wc64);
     (void)hipFree(sgd_.wc32);
-    (void)hipFree(sgd_.g64);
-    (void)hipFree(sgd_.gfix);
+    (void)hipFree(sgd_.gacc);
   }
   sgd_.wc64 = dmalloc<double>(size_t(cap));
   sgd_.wc32 = dmalloc<float>(size_t(cap));
-  sgd_.g64 = dmalloc<double>(size_t(cap) + 2);   // [nl]: loss, [nl + 1]: DP verdict
-  sgd_.gfix = dmalloc<uint64_t>(size_t(cap));   // far gradients (tiered), kept zeroed by k_sgd_update
+  // packed int64 buffer: near columns (<= cap) | tail | far slots (<= cap)
+  const size_t gl = 2 * size_t(cap) + size_t(sgd_tail_len(world_)) + 64;
+  sgd_.gacc = dmalloc<int64_t>(gl);
   // zeroed on the compute stream, ahead of the kernels that accumulate into
-  // them (a null-stream hipMemset is unordered against the non-blocking
+  // it (a null-stream hipMemset is unordered against the non-blocking
   // compute stream and could wipe an iteration's far gradients)
-  TWTML_HIP_CHECK(hipMemsetAsync(sgd_.g64, 0, sizeof(double) * (size_t(cap) + 2), compute_));
-  TWTML_HIP_CHECK(hipMemsetAsync(sgd_.gfix, 0, sizeof(uint64_t) * size_t(cap), compute_));
+  TWTML_HIP_CHECK(hipMemsetAsync(sgd_.gacc, 0, sizeof(int64_t) * gl, compute_));
   ns_cap_ = cap;
 }
 
@@ -467,12 +483,15 @@ LREngine::~LREngine() {
   raw_.release();
   for (auto& e : ev_) (void)hipEventDestroy(e);
   for (auto& b : pb_) free_prepared(b);
-  void* bufs[] = {sgd_.gfix, sgd_.rbuf, sgd_.w64, sgd_.wc64, sgd_.wc32, sgd_.g64, sgd_.red64, sgd_.stats, sgd_.state,
+  void* bufs[] = {sgd_.gacc, sgd_.rbuf, sgd_.w64, sgd_.wc64, sgd_.wc32, sgd_.stats, sgd_.state,
                   sgd_.loss_hist, sgd_.pred_out, sgd_.nrm, sgd_.wnorm_next, sgd_.part, sgd_.itrec, iter_tdbg_,
                   lower_page_, lower_blocks_};
   for (void* b : bufs) if (b) (void)hipFree(b);
   if (host_out_) (void)hipHostFree(host_out_);
   if (host_flags_) (void)hipHostFree(host_flags_);
+  if (ready_host_) (void)hipHostFree(ready_host_);
+  if (hnu_) (void)hipHostFree(hnu_);
+  if (dnu_) (void)hipFree(dnu_);
   for (auto e : iter_events_) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(compute_);
   (void)hipStreamDestroy(pstream_);
@@ -492,14 +511,14 @@ void LREngine::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, c
 // ---------------------------------------------------------------------------
 // prepare: filter .. layout of one raw slot into a PrepBuf, on stream `s`
 // (the prep stream; host syncs for the batch's counts stay on this thread).
+// One GPU: prepare_local + prepare_global.  DP: prepare_local (ends with the
+// rank's packet), the all-gather by the training thread (issue_c1), then
+// prepare_global_dp.
 // ---------------------------------------------------------------------------
-void LREngine::prepare(PrepBuf& pb, int slot, int64_t now_ms, hipStream_t s, bool global) {
-  prepare_local(pb, slot, now_ms, s);
-  if (global) prepare_global(pb, s);
-}
 
 // Local part (no collectives): decode / lower rows, filter, sort, chunk
-// layout, featurize, this rank's active set; ends with its counts on the host.
+// layout, featurize, this rank's active set; ends with its counts on the
+// host.  DP: + the sampled counts of the local active ids and the packet.
 void LREngine::prepare_local(PrepBuf& pb, int slot, int64_t now_ms, hipStream_t s) {
   TraceRange tr_prep("twtml.lr.prep");   // filter .. remap
   TWTML_HIP_CHECK(hipSetDevice(device_));
@@ -521,6 +540,7 @@ void LREngine::prepare_local(PrepBuf& pb, int slot, int64_t now_ms, hipStream_t 
   const bool lazy = cfg_.lazy_idx && cfg_.hybrid && !cfg_.dedup;
   fp.idx_mode = lazy ? 1 : 0;
   launch_featurize(b, prep, fp, lower_page_, lower_blocks_, s);
+  launch_batch_bounds(prep, pb.bounds, s);   // fixed-point scale bounds of this rank's rows
   if (!lazy) raw_.release_slot(slot, s);  // raw slot may be overwritten now
   launch_compact_active(prep, s);        // this rank's active ids (clears the flags)
   TWTML_HIP_CHECK(hipMemcpyAsync(pb.host_counters, prep.counters, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
@@ -528,6 +548,27 @@ void LREngine::prepare_local(PrepBuf& pb, int slot, int64_t now_ms, hipStream_t 
                                  hipMemcpyDeviceToHost, s));
   TWTML_HIP_CHECK(hipStreamSynchronize(s));
   if (pb.host_counters[3] != 0) throw std::runtime_error("feature buffer capacity exceeded");
+  if (world > 1) {
+    // the packet: sampled counts of the local active ids (the same sampled
+    // chunks as the tiered near-tier choice), then header + (id, count) pairs
+    const int64_t nU = pb.host_counters[1];
+    ensure_tier(pb, nU, s);
+    if (nU > 0) {
+      TWTML_HIP_CHECK(hipMemsetAsync(prep.slot_hist + kNumNumeric, 0, sizeof(uint32_t) * size_t(nU), s));
+      launch_tier_hist(prep, nU, num_cu_, s);
+    }
+    if (nU > pb.pkt_cap || !pb.packet) {
+      if (pb.packet) (void)hipFree(pb.packet);
+      pb.pkt_cap = std::max<int64_t>(std::max<int64_t>(2 * nU, 4096), pb.pkt_cap);
+      pb.packet = dmalloc<int32_t>(size_t(c1_packet_words(pb.pkt_cap)));
+    }
+    launch_pack_c1(prep, pb.bounds, pb.packet, nU, s);
+    // back to zero for the hybrid remap's own histogram (k_prep_init zeroed the rest)
+    TWTML_HIP_CHECK(hipMemsetAsync(prep.slot_hist, 0,
+                                   sizeof(uint32_t) * size_t(std::min<int64_t>(kNumNumeric + nU, pb.slot_hist_cap)), s));
+    TWTML_HIP_CHECK(hipStreamSynchronize(s));
+    pb.nu_local = nU;
+  }
   pb.raw = b;
   pb.fp = fp;
   pb.lazy = lazy;
@@ -535,74 +576,126 @@ void LREngine::prepare_local(PrepBuf& pb, int slot, int64_t now_ms, hipStream_t 
   pb.stage = 1;
 }
 
-// Global part: per-rank counts and the active-id union across ranks (the
-// prep collectives), then the hybrid / tiered layout.  On one GPU, or with a
-// prep communicator, it runs ahead with the local part; DP ranks without one
-// run it in line on the compute stream, after the previous batch trained.
+// One GPU: counts from the device, then the layout.
 void LREngine::prepare_global(PrepBuf& pb, hipStream_t s) {
   TraceRange tr_prep("twtml.lr.prep_global");
   TWTML_HIP_CHECK(hipSetDevice(device_));
-  const int world = world_;
-  const int rank = comm_ ? comm_->rank() : 0;
-  Comm* pc = prep_comm_ ? prep_comm_.get() : comm_.get();   // prep-stage collectives
+  const int64_t* hc = pb.host_counters;
+  BatchResult& res = pb.res;
+  res.n_kept = hc[0];
+  res.n_kept_global = hc[0];
+  res.rows_lowered = pb.host_norm[0];
+  res.rows_narrowed = pb.host_norm[1];
+  res.n_unique = hc[1];
+  res.entries = hc[2] * kChunkStride;
+  pb.row_offset = 0;
+  finish_layout(pb, s, false);
+}
+
+// DP: the all-gather of the ranks' packets, on the compute stream, between
+// two GD iterations of the previous batch (or in line, issue_c1_inline).
+// Every rank issues it at the same point of its collective sequence.
+void LREngine::issue_c1(PrepBuf& pb, int64_t max_u) {
+  TraceRange tr("twtml.lr.prep_allgather");
+  hipStream_t s = compute_;
+  const int64_t pw = c1_packet_words(max_u);
+  if (max_u > pb.pkt_cap) {   // another rank's active set is larger than this packet holds (rare)
+    int32_t* np = dmalloc<int32_t>(size_t(pw));
+    TWTML_HIP_CHECK(hipMemcpyAsync(np, pb.packet, sizeof(int32_t) * size_t(c1_packet_words(pb.nu_local)),
+                                   hipMemcpyDeviceToDevice, s));
+    TWTML_HIP_CHECK(hipStreamSynchronize(s));
+    (void)hipFree(pb.packet);
+    pb.packet = np;
+    pb.pkt_cap = max_u;
+  }
+  if (max_u > pb.gath_cap || !pb.gathered) {
+    if (pb.gathered) {
+      TWTML_HIP_CHECK(hipStreamSynchronize(s));
+      (void)hipFree(pb.gathered);
+    }
+    pb.gath_cap = std::max<int64_t>(max_u + max_u / 4 + 1024, pb.gath_cap);
+    pb.gathered = dmalloc<int32_t>(size_t(world_) * size_t(c1_packet_words(pb.gath_cap)));
+  }
+  if (max_u > pb.nu_local)   // pad this rank's pairs to the largest rank's: id -1
+    TWTML_HIP_CHECK(hipMemsetAsync(pb.packet + c1_packet_words(pb.nu_local), 0xFF,
+                                   sizeof(int32_t) * 2 * size_t(max_u - pb.nu_local), s));
+  comm_->allgather(pb.packet, pb.gathered, size_t(pw), ncclInt32, s);
+  TWTML_HIP_CHECK(hipEventRecord(pb.ev_c1, s));
+  std::lock_guard<std::mutex> lk(mu_);
+  pb.c1_maxu = max_u;
+  pb.c1 = 2;
+  __atomic_store_n(ready_host_, int64_t(0), __ATOMIC_RELEASE);
+  cv_.notify_all();
+}
+
+// DP, the packets were not gathered during the previous batch (first batch,
+// or the ranks' local parts finished after its GD loop): size the all-gather
+// with an all-reduce of one active-set size per rank, then gather.
+void LREngine::issue_c1_inline(PrepBuf& pb) {
+  hipStream_t s = compute_;
+  const int rank = comm_->rank();
+  for (int r = 0; r < world_; ++r) hnu_[r] = r == rank ? pb.nu_local : 0;
+  TWTML_HIP_CHECK(hipMemcpyAsync(dnu_, hnu_, sizeof(int64_t) * size_t(world_), hipMemcpyHostToDevice, s));
+  comm_->allreduce(dnu_, size_t(world_), ncclInt64, ncclSum, s);
+  TWTML_HIP_CHECK(hipMemcpyAsync(hnu_, dnu_, sizeof(int64_t) * size_t(world_), hipMemcpyDeviceToHost, s));
+  TWTML_HIP_CHECK(hipStreamSynchronize(s));
+  int64_t mx = 0;
+  for (int r = 0; r < world_; ++r) mx = std::max(mx, hnu_[r]);
+  issue_c1(pb, mx);
+}
+
+// DP global part, no collectives: per-rank kept rows (global m, sampling
+// offsets) and bounds from the gathered headers, the active-id union
+// (flags + compaction: every rank numbers the same slots), the union's
+// summed sampled counts (tiered near tier), then the layout.
+void LREngine::prepare_global_dp(PrepBuf& pb, hipStream_t s) {
+  TraceRange tr_prep("twtml.lr.prep_global");
+  TWTML_HIP_CHECK(hipSetDevice(device_));
+  const int world = world_, rank = comm_->rank();
+  DevPrepared& prep = pb.dp;
+  BatchResult& res = pb.res;
+  const int64_t max_u = pb.c1_maxu;
+  const int64_t pw = c1_packet_words(max_u);
+  constexpr int kH = kC1HeaderWords / 2;   // int64 header words per rank
+  TWTML_HIP_CHECK(hipStreamWaitEvent(s, pb.ev_c1, 0));
+  for (int r = 0; r < world; ++r)
+    TWTML_HIP_CHECK(hipMemcpyAsync(pb.host_hdr + r * kH, pb.gathered + int64_t(r) * pw, sizeof(int64_t) * kH,
+                                   hipMemcpyDeviceToHost, s));
+  TWTML_HIP_CHECK(hipStreamSynchronize(s));
+  int64_t row_offset = 0, n_glob = 0;
+  for (int k = 0; k < kBoundsLen; ++k) pb.host_bounds[k] = 0.0;
+  for (int r = 0; r < world; ++r) {
+    const int64_t* h = pb.host_hdr + r * kH;
+    if (r < rank) row_offset += h[0];
+    n_glob += h[0];
+    for (int k = 0; k < kBoundsLen; ++k)
+      pb.host_bounds[k] = std::max(pb.host_bounds[k], __builtin_bit_cast(double, h[2 + k]));
+  }
+  TWTML_HIP_CHECK(hipMemcpyAsync(pb.bounds, pb.host_bounds, sizeof(double) * kBoundsLen, hipMemcpyHostToDevice, s));
+  launch_union_flag(pb.gathered, world, max_u, prep, s);
+  launch_compact_active(prep, s);
+  int64_t* hc = pb.host_counters;
+  TWTML_HIP_CHECK(hipMemcpyAsync(hc + 1, prep.counters + 1, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  TWTML_HIP_CHECK(hipStreamSynchronize(s));
+  res.n_kept = hc[0];
+  res.n_kept_global = n_glob;
+  res.rows_lowered = pb.host_norm[0];
+  res.rows_narrowed = pb.host_norm[1];
+  res.n_unique = hc[1];
+  res.entries = hc[2] * kChunkStride;
+  pb.row_offset = row_offset;
+  finish_layout(pb, s, true);
+}
+
+// Compact space of the (global) active set and the hybrid / tiered layout.
+// dp_hist: slot counts for the tiered near tier from the gathered packets
+// (every rank numbers the slots from the same counts), else sampled here.
+void LREngine::finish_layout(PrepBuf& pb, hipStream_t s, bool dp_hist) {
   DevPrepared& prep = pb.dp;
   BatchResult& res = pb.res;
   const DevRawBatch& b = pb.raw;
   const FeaturizeParams& fp = pb.fp;
   const bool lazy = pb.lazy;
-  const int slot = pb.slot;
-  // per-rank kept rows (sampling offsets, global m) and active-set sizes:
-  // n_global[1 + r] / n_global[1 + world + r], one small all-reduce
-  int64_t* hc = pb.host_counters;
-  TWTML_HIP_CHECK(hipMemcpyAsync(pb.n_global + 1 + rank, prep.counters, sizeof(int64_t),
-                                 hipMemcpyDeviceToDevice, s));
-  if (world > 1) {
-    TWTML_HIP_CHECK(hipMemcpyAsync(pb.n_global + 1 + world + rank, prep.counters + 1, sizeof(int64_t),
-                                   hipMemcpyDeviceToDevice, s));
-    pc->allreduce(pb.n_global + 1, size_t(2 * world), ncclInt64, ncclSum, s);
-  }
-  TWTML_HIP_CHECK(hipMemcpyAsync(hc + 8, pb.n_global + 1, sizeof(int64_t) * size_t(2 * world),
-                                 hipMemcpyDeviceToHost, s));
-  TWTML_HIP_CHECK(hipStreamSynchronize(s));
-  const int64_t* per_rank = hc + 8;
-  if (world > 1) {
-    // Active-set union: every rank numbers the same slots.  Each rank's
-    // sorted id list (padded with -1 to the longest) is all-gathered --
-    // sum_r nU_r ids instead of an all-reduce of F flag bytes (100 MB at
-    // F = 1e8) -- then flagged and compacted again.
-    int64_t maxU = 0;
-    for (int r = 0; r < world; ++r) maxU = std::max(maxU, per_rank[world + r]);
-    if (maxU > 0) {
-      const int64_t mine = hc[1];
-      if (maxU > mine)
-        TWTML_HIP_CHECK(hipMemsetAsync(prep.uniq + mine, 0xFF, sizeof(int32_t) * size_t(maxU - mine), s));
-      const int64_t need = maxU * int64_t(world);
-      if (need > pb.ugather_cap) {
-        if (pb.ugather) (void)hipFree(pb.ugather);
-        pb.ugather_cap = std::max(need, 2 * pb.ugather_cap);
-        pb.ugather = dmalloc<int32_t>(size_t(pb.ugather_cap));
-      }
-      pc->allgather(prep.uniq, pb.ugather, size_t(maxU), ncclInt32, s);
-      launch_flag_ids(pb.ugather, need, prep, s);
-      launch_compact_active(prep, s);
-      TWTML_HIP_CHECK(hipMemcpyAsync(hc + 1, prep.counters + 1, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-      TWTML_HIP_CHECK(hipStreamSynchronize(s));
-    }
-  }
-  res.n_kept = hc[0];
-  res.rows_lowered = pb.host_norm[0];
-  res.rows_narrowed = pb.host_norm[1];
-  res.n_unique = hc[1];
-  res.entries = hc[2] * kChunkStride;
-  int64_t row_offset = 0, n_glob = 0;
-  for (int r = 0; r < world; ++r) {
-    if (r < rank) row_offset += per_rank[r];
-    n_glob += per_rank[r];
-  }
-  res.n_kept_global = n_glob;
-  pb.row_offset = row_offset;
-
-  // ---- compact space
   const int64_t nU = res.n_unique;
   int64_t ns = kNumNumeric + nU + kPadSlots;
   ns = (ns + 63) / 64 * 64;
@@ -624,9 +717,8 @@ void LREngine::prepare_global(PrepBuf& pb, hipStream_t s) {
     ensure_tier(pb, nU, s);
     prep.near_end = kNumNumeric + n_near;
     TWTML_HIP_CHECK(hipMemsetAsync(prep.slot_hist + kNumNumeric, 0, sizeof(uint32_t) * size_t(nU), s));
-    launch_tier_hist(prep, nU, num_cu_, s);
-    // every rank numbers the slots from the same (summed) sampled counts
-    if (world > 1) pc->allreduce(prep.slot_hist + kNumNumeric, size_t(nU), ncclUint32, ncclSum, s);
+    if (dp_hist) launch_union_hist(pb.gathered, world_, pb.c1_maxu, prep, s);
+    else launch_tier_hist(prep, nU, num_cu_, s);
     launch_tier_layout(prep, res.entries, nU, n_near, ns, nl, num_cu_, b, fp, lazy, s);
     pb.nl = nl;
     pb.n_near = n_near;
@@ -637,7 +729,7 @@ void LREngine::prepare_global(PrepBuf& pb, hipStream_t s) {
     if (prep.hybrid) launch_remap_hybrid(prep, res.entries, ns, kNumNumeric + nU, num_cu_, b, fp, lazy, s);
     else launch_remap(prep, res.entries, nU, u16, s);
   }
-  if (lazy) raw_.release_slot(slot, s);
+  if (lazy) raw_.release_slot(pb.slot, s);
   prep.dedup = dedup ? 1 : 0;
   if (prep.dedup) launch_dedup(prep, ns, kNumNumeric + nU, res.n_kept, s);
   res.n_near = pb.n_near;
@@ -667,6 +759,8 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred) {
   sgd_.n_near = pb.n_near;
   sgd_.far_base = pb.far_base;
   sgd_.slot_fid = tiered ? prep.slot_fid : nullptr;
+  sgd_.bounds = pb.bounds;
+  sgd_.far_off = pb.nl + sgd_.tail_len;
   if (tiered) {
     if (!sgd_.rbuf) sgd_.rbuf = dmalloc<float>(size_t(prep.cap_rows16));
     sgd_.fcsc_pos = prep.fcsc_pos;
@@ -701,12 +795,9 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred) {
   sp.ablate = cfg_.ablate;
   sp.dp = world > 1 ? 1 : 0;
   sp.rank0 = (comm_ ? comm_->rank() : 0) == 0 ? 1 : 0;
-  // entries one workgroup can add into a slot: its share of the chunks (x2 for imbalance)
-  sp.fix_lim = sgd_fix_limit(2 * (res.entries / std::max(1, grid)) + 65536);
-  // far slots sum entries of every workgroup and rank
-  sp.far_lim = sgd_far_limit((res.entries + 65536) * int64_t(world));
   const int64_t n_far = kNumNumeric + nU - sgd_.far_base;
-  if (n_glob > 0) {
+  res.diverged = diverged_;
+  if (n_glob > 0 && !diverged_) {
     // Host-side early stop: the convergence test of update j runs in the
     // prologue of iteration j+1's gradient kernel, which copies its verdict
     // to pinned memory (zero copy); the host keeps at most `depth`
@@ -726,7 +817,21 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred) {
     for (int i = 1; i <= iters; ++i) {
       if (i > depth) {
         const int j = i - depth;                       // verdict after update j
-        if (wait_flag(j) != 0.0) break;
+        const int64_t v = int64_t(wait_flag(j));       // bit 0 stop; DP: bit 1 every rank's next
+                                                       // packet ready, >> 2 the largest one
+        if (world > 1 && (v & 2)) {
+          // the next batch's packets are ready on every rank: all-gather them
+          // here, between iterations j + depth - 1 and j + depth -- every rank
+          // sees the same all-reduced flag at the same point
+          PrepBuf* nb = nullptr;
+          {
+            std::lock_guard<std::mutex> lk(mu_);
+            for (auto& b : pb_)
+              if (&b != &pb && b.c1 == 1) nb = &b;
+          }
+          if (nb) issue_c1(*nb, v >> 2);
+        }
+        if (v & 1) break;
       }
       sp.iteration = i;
       // every rank launches the gradient kernel (an empty shard writes zero
@@ -734,11 +839,11 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred) {
       launch_sgd_iter(sgd_, prep, sp, pb.host_counters[2], u16, grid, s);
       if (tiered) launch_far_grad(sgd_, sp, num_cu_, s);
       if (world > 1) {
+        // ONE collective per iteration: the packed int64 buffer (near
+        // columns, loss, sampled m, verdict, ready words, far slots); integer
+        // sums are exact in any order, so every rank gets the same bits
         launch_sgd_reduce(sgd_, sp, s);
-        comm_->allreduce(sgd_.g64, size_t(nl + 2), ncclFloat64, ncclSum, s);   // + loss, verdict
-        // far gradients are int64 fixed point: the sum over ranks is exact
-        if (n_far > 0) comm_->allreduce(sgd_.gfix, size_t(n_far), ncclUint64, ncclSum, s);
-        if (sp.sample) comm_->allreduce(sgd_.red64 + 2 * (i & 1), 2, ncclFloat64, ncclSum, s);
+        comm_->allreduce(sgd_.gacc, size_t(sgd_.far_off + n_far), ncclInt64, ncclSum, s);
       }
       launch_sgd_update(sgd_, sp, fused ? sgd_.nparts : 0, s);
     }
@@ -747,7 +852,7 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred) {
     launch_norm_next(sgd_, true, s);
     if (itime) print_iter_timing(iters);
   }
-  if (n_glob <= 0) launch_norm_next(sgd_, false, s);   // weights unchanged: carry |w|^2 as is
+  if (n_glob <= 0 || diverged_) launch_norm_next(sgd_, false, s);   // weights unchanged: carry |w|^2 as is
   TWTML_HIP_CHECK(hipEventRecord(ev_[2], s));
   if (world > 1) comm_->allreduce(sgd_.stats, 6, ncclFloat64, ncclSum, s);
   TWTML_HIP_CHECK(hipMemcpyAsync(host_out_, sgd_.stats, 8 * sizeof(double), hipMemcpyDeviceToHost, s));
@@ -764,7 +869,8 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred) {
   for (int k = 0; k < 6; ++k) res.stats[k] = host_out_[k];
   const double* st = host_out_ + 8;
   res.converged = st[1] != 0.0;
-  res.overflow = st[7] == 1.0;
+  res.diverged = diverged_ || st[7] == 1.0;
+  diverged_ = res.diverged;
   res.iterations = int32_t(st[3]);
   for (int i = 1; i <= res.iterations; ++i) res.loss_history.push_back(host_out_[16 + i]);
   // prep_ms: the batch's prep on its own stream (overlapped with the previous
@@ -816,12 +922,27 @@ void LREngine::prep_worker() {
     lk.unlock();
     std::exception_ptr err;
     try {
-      prepare(b, slot, now_ms, pstream_, ahead_global_);
+      prepare_local(b, slot, now_ms, pstream_);
+      if (world_ > 1) {
+        // packet ready: announce it (the ready word travels in the gradient
+        // all-reduce) and wait for the training thread's all-gather
+        lk.lock();
+        b.c1 = 1;
+        __atomic_store_n(ready_host_, b.nu_local + 1, __ATOMIC_RELEASE);
+        cv_.notify_all();
+        cv_.wait(lk, [&] { return stop_ || b.c1 == 2; });
+        if (stop_) return;
+        lk.unlock();
+        prepare_global_dp(b, pstream_);
+      } else {
+        prepare_global(b, pstream_);
+      }
     } catch (...) {
       err = std::current_exception();
     }
-    lk.lock();
+    if (!lk.owns_lock()) lk.lock();
     b.error = err;
+    if (err && b.c1 == 1) b.c1 = -1;
     b.state = 2;
     job_ = -1;
     cv_.notify_all();
@@ -856,12 +977,29 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
     std::unique_lock<std::mutex> lk(mu_);
     for (int i = 0; i < 2; ++i)
       if (pb_[i].state != 0 && pb_[i].slot == slot) k = i;
-    if (k >= 0) {
+    if (k >= 0 && world_ > 1) {
+      // DP: the packets were all-gathered during the previous batch, or are
+      // now, in line -- the same choice on every rank (it follows the
+      // all-reduced ready words); then the prep thread finishes the layout
+      cv_.wait(lk, [&] { return pb_[k].c1 != 0 || pb_[k].state == 2; });
+      if (pb_[k].c1 == 1) {
+        lk.unlock();
+        issue_c1_inline(pb_[k]);
+        lk.lock();
+      }
+      cv_.wait(lk, [&] { return pb_[k].state == 2; });
+      if (pb_[k].error) {
+        std::exception_ptr err = pb_[k].error;
+        pb_[k].error = nullptr;
+        pb_[k].state = 0;
+        pb_[k].c1 = 0;
+        std::rethrow_exception(err);
+      }
+    } else if (k >= 0) {
       cv_.wait(lk, [&] { return pb_[k].state == 2; });
       // prepared ahead with the batch time given at submit; a different time
-      // here is re-prepared on one GPU (DP ranks keep it: a re-prepare would
-      // repeat the prep collectives on this rank only)
-      if (pb_[k].error || (pb_[k].now_ms != now_ms && world_ == 1)) {   // failed ahead / other time
+      // here is re-prepared
+      if (pb_[k].error || pb_[k].now_ms != now_ms) {   // failed ahead / other time
         std::exception_ptr err = pb_[k].error;
         pb_[k].error = nullptr;
         if (err && pb_[k].now_ms == now_ms) {
@@ -870,7 +1008,8 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
         }
         pb_[k].state = 1;
         lk.unlock();
-        prepare(pb_[k], slot, now_ms, pstream_, true);
+        prepare_local(pb_[k], slot, now_ms, pstream_);
+        prepare_global(pb_[k], pstream_);
         lk.lock();
         pb_[k].state = 2;
       }
@@ -878,12 +1017,19 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
       // not prepared ahead: drop it from the submission queue, prepare in line
       for (auto it = submitted_.begin(); it != submitted_.end(); ++it)
         if (it->first == slot) { submitted_.erase(it); break; }
+      if (world_ > 1) {
+        // every rank must issue the same collectives in the same order: a
+        // batch prepared (and possibly all-gathered) ahead may not be skipped
+        for (int i = 0; i < 2; ++i)
+          if (pb_[i].state != 0)
+            throw std::logic_error("DP: batches must be processed in submission order");
+      }
       for (int i = 0; i < (overlap_ ? 2 : 1); ++i)
         if (pb_[i].state == 0) k = i;
       if (k < 0) {
-        // every buffer holds a batch prepared ahead that is not this one
-        // (submitted but processed out of order): evict one -- its slot goes
-        // back to the front of the queue and is prepared again when due
+        // one GPU: every buffer holds a batch prepared ahead that is not this
+        // one (submitted but processed out of order): evict one -- its slot
+        // goes back to the front of the queue and is prepared again when due
         cv_.wait(lk, [&] { return job_ < 0; });
         for (int i = 0; i < 2 && k < 0; ++i)
           if (pb_[i].state == 2) {
@@ -899,10 +1045,17 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
       pb_[k].now_ms = now_ms;
       lk.unlock();
       try {
-        prepare(pb_[k], slot, now_ms, pstream_, true);
+        prepare_local(pb_[k], slot, now_ms, pstream_);
+        if (world_ > 1) {
+          issue_c1_inline(pb_[k]);
+          prepare_global_dp(pb_[k], pstream_);
+        } else {
+          prepare_global(pb_[k], pstream_);
+        }
       } catch (...) {
         lk.lock();
         pb_[k].state = 0;
+        pb_[k].c1 = 0;
         throw;
       }
       lk.lock();
@@ -913,18 +1066,17 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   }
   BatchResult res;
   try {
-    // DP ranks without a prep communicator prepared only the local part
-    // ahead: the collectives + layout run here, on the compute stream
-    if (pb_[k].stage < 2) prepare_global(pb_[k], compute_);
     res = train(pb_[k], want_pred);
   } catch (...) {
     std::lock_guard<std::mutex> lk(mu_);
     pb_[k].state = 0;
+    pb_[k].c1 = 0;
     throw;
   }
   {
     std::lock_guard<std::mutex> lk(mu_);
     pb_[k].state = 0;
+    pb_[k].c1 = 0;
     schedule_ahead_locked();
   }
   return res;
@@ -939,6 +1091,7 @@ void LREngine::set_weights(const double* w, int64_t n) {
   TWTML_HIP_CHECK(hipMemcpyAsync(sgd_.w64, w, sizeof(double) * size_t(n), hipMemcpyHostToDevice, compute_));
   TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
   norm_age_ = -1;   // the carried |w|^2 no longer holds
+  diverged_ = false;
 }
 
 void LREngine::get_weights(double* w, int64_t n) const {

@@ -3,8 +3,11 @@
 // One engine per process/GPU.  A micro-batch flows:
 //   pinned host RawBatch --(copy stream, async H2D)--> device slot (x4)
 //   prep stream: decode / lower rows -> filter -> length sort -> featurize
-//   -> compact [RCCL all-gather of the active id lists] -> layout (hybrid /
-//   tiered) -- for batch t+1 while batch t trains (prep thread)
+//   -> compact -> layout (hybrid / tiered) -- for batch t+1 while batch t
+//   trains (prep thread).  DP: the local part ends in one packet per rank
+//   (kept rows, active ids + sampled counts, bounds) that the training
+//   thread all-gathers between two of batch t's GD iterations (the ONE prep
+//   collective); the prep thread finishes t+1 from it on the prep stream.
 //   compute stream: gather w -> numIterations x ( fused predict/gradient
 //   kernel -> [RCCL all-reduce of the packed gradient] -> fp64 update +
 //   convergence ) -> scatter w
@@ -122,7 +125,8 @@ struct BatchResult {
   int64_t n_raw = 0, n_kept = 0, n_kept_global = 0, n_unique = 0, entries = 0;
   int32_t iterations = 0;
   bool converged = false;
-  bool overflow = false;  // a residual hit the fixed-point clamp (diverging model)
+  bool diverged = false;  // the model left any usable range (|r| bound >= 1e30 or non-finite
+                          // weights): training stopped at that iteration (sgd.hip sgd_scales)
   int64_t rows_lowered = 0, rows_narrowed = 0;   // device row normalisation (rows.hip)
   bool tiered = false;    // active set beyond LDS: tiered layout (near slots in LDS, far via CSC)
   int64_t n_near = 0;     // text slots in the LDS tier
@@ -142,7 +146,20 @@ struct PrepBuf {
   int32_t* ugather = nullptr;         // DP active-set union: all-gathered id lists
   int64_t ugather_cap = 0;
   int64_t* host_counters = nullptr;   // pinned [8 + 2 world]: counters | per-rank kept | per-rank active
+  // DP prep packet (dp_prep.hip) and the all-gathered packets of every rank
+  int32_t* packet = nullptr;          // device [c1_packet_words(pkt_cap)]
+  int64_t pkt_cap = 0;
+  int32_t* gathered = nullptr;        // device [world * c1_packet_words(gath_cap)]
+  int64_t gath_cap = 0;
+  int64_t* host_hdr = nullptr;        // pinned [world * kC1HeaderWords / 2] gathered headers
+  double* host_bounds = nullptr;      // pinned [kBoundsLen]
+  hipEvent_t ev_c1 = nullptr;         // compute stream, after the all-gather
+  int64_t nu_local = 0;               // this rank's active ids (packet pairs)
+  int64_t c1_maxu = 0;                // pairs per rank in the all-gather
+  int c1 = 0;                         // guarded by mu_: 0 -, 1 packet ready, 2 all-gather issued, -1 failed
   int64_t* host_norm = nullptr;       // pinned [2] rows lowered / narrowed on the device
+  double* bounds = nullptr;           // device [kBoundsLen] batch bounds of the fixed-point scales
+                                      // (DP: the max over ranks)
   hipEvent_t ev_start = nullptr, ev_done = nullptr;
   // guarded by LREngine::mu_
   int state = 0;                      // 0 free, 1 being prepared, 2 prepared
@@ -162,10 +179,12 @@ struct PrepBuf {
 
 class LREngine {
  public:
-  // prep_comm (DP, optional): a second communicator over the same ranks for
-  // the prep-stage collectives, which lets batch t+1 be prepared while t's
-  // gradient all-reduces run on `comm`.
-  LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm, std::shared_ptr<Comm> prep_comm = nullptr);
+  // comm: the DP communicator (one per rank; null on one GPU).  Per GD
+  // iteration one int64 all-reduce; per batch one all-gather of the prep
+  // packets (issued between two GD iterations of the previous batch) and one
+  // all-reduce of the 6 batch statistics.  DP batches must be processed in
+  // submission order (every rank trains the same sequence).
+  LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm);
   ~LREngine();
 
   // Async H2D of rows [0, n) of a pinned host batch into device slot `slot`.
@@ -202,9 +221,16 @@ class LREngine {
   void ensure_compact(int64_t ns);
   void ensure_part(int64_t n);
   void ensure_tier(PrepBuf& b, int64_t n_unique, hipStream_t s);
-  void prepare(PrepBuf& b, int slot, int64_t now_ms, hipStream_t s, bool global);
   void prepare_local(PrepBuf& b, int slot, int64_t now_ms, hipStream_t s);
   void prepare_global(PrepBuf& b, hipStream_t s);
+  // DP: the all-gather of b's packet, on the compute stream (max_u pairs per rank)
+  void issue_c1(PrepBuf& b, int64_t max_u);
+  // DP, not issued during the previous batch: size it with an all-reduce first
+  void issue_c1_inline(PrepBuf& b);
+  // DP: union, global counts / bounds and layout from the gathered packets
+  void prepare_global_dp(PrepBuf& b, hipStream_t s);
+  // shared tail of prepare_global / prepare_global_dp: compact space + layout
+  void finish_layout(PrepBuf& b, hipStream_t s, bool dp_hist);
   BatchResult train(PrepBuf& b, bool want_pred);
   void prep_worker();
   void schedule_ahead_locked();
@@ -214,14 +240,15 @@ class LREngine {
   int device_;
   LRConfig cfg_;
   std::shared_ptr<Comm> comm_;
-  std::shared_ptr<Comm> prep_comm_;
   int world_ = 1;
   hipStream_t compute_ = nullptr, pstream_ = nullptr, copy_ = nullptr;
   RawSlots raw_;
   PrepBuf pb_[2];
   int last_buf_ = -1;               // buffer of the last trained batch (debug_*)
   bool overlap_ = true;
-  bool ahead_global_ = true;        // prepare-ahead includes the collective part + layout
+  int64_t* ready_host_ = nullptr;   // DP: pinned mapped ready word (next packet's pairs + 1; 0: none)
+  int64_t* dnu_ = nullptr;          // DP: device [world] active-set sizes (in-line all-gather sizing)
+  int64_t* hnu_ = nullptr;          // pinned [world]
   // prepare-ahead: submitted slots in order, the prep thread's job (a pb_ index)
   std::mutex mu_;
   std::condition_variable cv_;
@@ -237,6 +264,12 @@ class LREngine {
   static constexpr int kNormRefresh = 256;
   int norm_age_ = -1;   // batches since the last full pass (-1: carried value invalid)
   int64_t part_cap_ = 0;
+  // The model diverged (a batch stopped on invalid fixed-point scales):
+  // later batches are not trained -- like MLlib's NaN weights, which never
+  // recover -- until set_weights() installs a new model.  Identical on every
+  // DP rank (decided from all-reduced values), so no collective is skipped
+  // on one rank only.
+  bool diverged_ = false;
   int64_t near_cap_ = 0;          // tiered layout: LDS-resident text slots (tier_near_cap)
   bool force_tiered_ = false;     // TWTML_FORCE_TIERED=1: tiered layout for any active set (tests)
   uint64_t* iter_tdbg_ = nullptr;

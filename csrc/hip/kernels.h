@@ -238,27 +238,42 @@ int64_t tier_near_cap();
 
 // ---------------------------------------------------------------------------
 // SGD on the compact active set.
+//
+// Exact, partition-independent GD arithmetic (sgd.hip): every weight enters
+// the forward dot as an int32 fixed-point value (scale 2^K from max |w|),
+// every row residual enters the gradient as q = rint(r * 2^S) (S from a
+// rigorous bound on |r|), and every gradient / loss / numeric-feature sum is
+// an int64 fixed-point sum.  Integer sums do not depend on the order rows are
+// added in, so a row's contribution is the same whichever layout (hot dense,
+// LDS cold stream, far tier), workgroup or DP rank it goes through: DP over
+// any sharding is bit-identical to one GPU on the concatenated batch.
 struct DevSgd {
   double* w64;          // [F+4] master weights (fp64)
   double* wc64;         // [NS]  compact master weights
   float* wc32;          // [NS]  compact fp32 copy read by the gradient kernel
-  double* g64;          // [NS+1] gradient accumulator (+ loss at [NS])
-  double* red64;        // [4] {loss, m, pad, pad} for sampled iterations
+  // Packed int64 gradient buffer (one all-reduce per GD iteration in DP):
+  //   [0, nl)              numeric (2^N_k) and near text (2^S) columns, pads
+  //   [nl, nl + tail_len)  loss (2^L), sampled m, DP verdict, per-rank ready words
+  //   [far_off, +n_far)    far text slots (2^S), slot - far_base (tiered)
+  int64_t* gacc;
+  int64_t far_off;      // = nl + tail_len
+  int32_t tail_len;
   double* stats;        // [8] n, sum_y, sum_y2, sum_p, sum_p2, sum_e2, -, -
-  double* state;        // [8] 0 done 1 converged 2 n_updates 3 iters 4 |w|^2 (all F+4) 5 m_global
-                        //     6 |w_active|^2 at gather (|w_rest|^2 = [4] - [6])
+  double* state;        // [kStateLen] see below
   double* loss_hist;    // [max_iters+1]
   float* pred_out;      // [R] rounded predictions in kept order (optional)
   double* host_flags;   // [max_iters+1] pinned host memory: done flag after each update
-  double* part;         // [nparts][pstride] per-workgroup partial gradients (LDS paths)
-  double* itrec;        // [max_iters+2][kRecStride] per-iteration update records
+  int64_t* part;        // [nparts][pstride] per-workgroup int64 partial rows
+  double* itrec;        // [max_iters+2][kRecStride] per-iteration scale / update records
   uint64_t* tdbg;       // optional phase stamps (TWTML_ITER_TIMING): [iter][wg 0 / last][8]
+  const double* bounds; // [8] batch bounds: max row bigram count, max |y|, max |n_k| (k = 0..3)
+  const volatile int64_t* ready_word;   // DP: host-mapped, this rank's next-batch ready word
+  int32_t rank, world;
   // LDS / partial-row slot space: nl slots (= ns unless tiered), text slots
   // [4, 4 + n_near) in LDS; tiered: far slots [far_base, 4 + n_unique)
   int64_t nl;
   int64_t n_near;
   int64_t far_base;
-  uint64_t* gfix;       // [ns] far gradients, 2^-24 fixed point, by slot - far_base (tiered)
   float* rbuf;          // [R16] residual per sorted position (tiered backward)
   const int32_t* slot_fid;   // slot -> feature id (tiered); null: uniq[slot - 4]
   const uint32_t* fcsc_pos;
@@ -267,27 +282,40 @@ struct DevSgd {
   int64_t F;
   int64_t ns;           // 4 + n_unique + pads (rounded)
   int64_t n_unique;
-  int64_t pstride;      // ns + 64: slots, then loss, m, 6 batch stats (see sgd_part_stride)
-  int32_t nparts;       // partial rows written by the last iteration launch (0 = global path)
-  double* nrm;          // [kNormParts] per-block partial squared norms (fixed-order sums)
+  int64_t pstride;      // nl + 64: slots, then loss, m, 6 batch stats (see sgd_part_stride)
+  int32_t nparts;       // partial rows written by the last iteration launch
+  double* nrm;          // [2 kNormParts] per-block partial squared norms | max |w| (fixed-order)
   double* wnorm_next;   // [1] |w|^2 after the last batch (state[4] of the next batch)
 };
 
 constexpr int kNormParts = 1024;   // grid cap of the norm / gather / scatter kernels
 
-// Iteration record: [0] updates so far, [1] m, [2] update workgroups,
-// [kRecHead + 2w] ||dw||^2 and ||w||^2 partials of update workgroup w.
+// Iteration record i: [0] updates so far, [1] m, [2] update workgroups,
+// [3] K, [4] S, [5] L, [6..9] N_0..N_3 (fixed-point exponents of iteration
+// i, written by its gradient kernel), [10] |r| bound B, [11] scales invalid
+// (diverged); [kRecHead + 3w] ||dw||^2, ||w||^2 and max |w_text| partials of
+// update workgroup w.
 constexpr int kMaxUpdGrid = 256;
-constexpr int kRecHead = 8;
-constexpr int kRecStride = kRecHead + 2 * kMaxUpdGrid;
+constexpr int kRecHead = 16;
+constexpr int kRecStride = kRecHead + 3 * kMaxUpdGrid;
+constexpr int kRecK = 3, kRecS = 4, kRecL = 5, kRecN = 6, kRecB = 10, kRecBad = 11;
+
+// Packed-buffer tail (DevSgd::gacc + nl): loss, sampled m, DP verdict, then
+// one ready word per rank (next batch's local prep done: its active-set size + 1).
+constexpr int kTailLoss = 0, kTailM = 1, kTailVerdict = 2, kTailReady = 3;
+inline int32_t sgd_tail_len(int world) { return (kTailReady + world + 7) / 8 * 8; }
 
 // Partial-row stride for a compact space of ns slots (multiple of 64).
 constexpr int64_t sgd_part_stride(int64_t ns) { return ns + 64; }
 
 // DevSgd::state: [0] done, [1] converged, [2] updates applied, [3] last
-// iteration, [4] |w|^2, [5] rows m, [6] |w_active|^2, [7] clamp flag,
-// [8] DP: iteration whose gradient pass this rank skipped
-constexpr int kStateLen = 10;
+// iteration, [4] |w|^2, [5] rows m, [6] |w_active|^2, [7] diverged (the
+// |r| bound or the weights left the fixed-point range: training stopped),
+// [8] DP: iteration whose gradient pass this rank skipped, [9] max |w_text|
+// at gather (iteration 1's weight scale)
+constexpr int kStateLen = 12;
+// bounds: [0] max bigram count of a row, [1] max |y|, [2..5] max |n_k|
+constexpr int kBoundsLen = 8;
 
 struct SgdParams {
   double step_size;
@@ -298,34 +326,23 @@ struct SgdParams {
   int64_t row_offset;   // global row id of this rank's kept row 0 (sampling)
   int32_t want_pred;
   int32_t sample;       // fraction < 1
-  int32_t ablate;       // perf diagnostics: 1 = skip scatter, 2 = skip gather+scatter,
-                        // hybrid only: 3 = skip hot grad, 4 = skip hot dot, 5 = skip cold scatter,
-                        // 6 = loads only, 7 = no chunks (fixed cost)
-  float fix_lim;        // |r| * 2^24 clamp so a workgroup's int64 slot sums cannot overflow
-  float far_lim;        // |r| * 2^16 clamp of the far (tiered) gradient: batch-wide int64 sums
+  int32_t ablate;       // perf diagnostics (hybrid): 7 = no chunks (fixed cost), 8 = no far forward
   int32_t dp;           // world > 1: convergence verdicts travel in the gradient all-reduce
   int32_t rank0;        // this rank's verdict is the one that counts (DP)
 };
-
-// Fixed-point clamp for a launch: every slot of a workgroup receives at most
-// `entries_per_wg` contributions, each |q| <= lim, so lim * entries < 2^62.
-float sgd_fix_limit(int64_t entries_per_wg);
-// Far-gradient clamp: `entries_total` entries (all ranks) may add into one slot.
-float sgd_far_limit(int64_t entries_total);
 
 void launch_gather_w(const DevSgd& d, const DevPrepared& p, hipStream_t s);
 void launch_norm2(const double* v, int64_t n, double* out, const DevSgd& d, hipStream_t s);
 void launch_sgd_iter(const DevSgd& d, const DevPrepared& p, const SgdParams& sp, int64_t groups,
                      bool u16, int grid, hipStream_t s);
-// Partial rows an iteration launch of `grid` workgroups writes (0: the
-// generic path accumulates straight into g64).
+// Partial rows an iteration launch of `grid` workgroups writes.
 int sgd_partials(int64_t ns, bool u16, int grid);
-// g64 (+ loss, m, stats) += sum of the d.nparts partial rows
+// DP: gacc[0, nl + 2) = sums of the d.nparts partial rows (+ stats), verdict and ready words
 void launch_sgd_reduce(const DevSgd& d, const SgdParams& sp, hipStream_t s);
 // nparts > 0: sums the partial rows itself (single GPU, no separate reduce)
 void launch_sgd_update(const DevSgd& d, const SgdParams& sp, int nparts, hipStream_t s);
-// Far backward of one iteration: gfix[slot - far_base] += sum of the fixed-
-// point residuals of the slot's entries (CSC segmented sums).
+// Far backward of one iteration: gacc[far_off + slot - far_base] += sum of the
+// fixed-point residuals of the slot's entries (CSC segmented sums).
 void launch_far_grad(const DevSgd& d, const SgdParams& sp, int num_cu, hipStream_t s);
 // after the GD loop: convergence of the last update -> state
 void launch_sgd_finish(const DevSgd& d, const SgdParams& sp, hipStream_t s);
@@ -335,10 +352,26 @@ void launch_scatter_w(const DevSgd& d, const DevPrepared& p, hipStream_t s);
 void launch_norm_next(const DevSgd& d, bool trained, hipStream_t s);
 // state[4] = wnorm_next (instead of a full |w|^2 pass over all F+4 weights)
 void launch_norm_carry(const DevSgd& d, hipStream_t s);
+// batch bounds of the scale choice (max row bigram count, max |y|, max |n_k|)
+// of this rank's kept rows -> out[kBoundsLen] (zeroed here)
+void launch_batch_bounds(const DevPrepared& p, double* out, hipStream_t s);
 int sgd_lds_rep(int64_t ns);
 // the hybrid iteration kernel's LDS (gradient replicas + hot partials) fits
 bool sgd_hybrid_fits(int64_t ns);
 int sgd_iter_grid(int64_t ns, int64_t n_kept, int num_cu, bool hybrid);
+
+// ---------------------------------------------------------------------------
+// DP batch preparation (dp_prep.hip): one packet per rank, all-gathered once.
+// Packet (int32 words): header kC1HeaderWords (16 int64: kept rows, active
+// ids, kBoundsLen fp64 bounds, 0) then max_u (id, sampled count) pairs.
+constexpr int kC1HeaderWords = 32;
+__host__ __device__ constexpr int64_t c1_packet_words(int64_t max_u) { return kC1HeaderWords + 2 * max_u; }
+// this rank's packet from its local active set (slot_hist[4 + u] = sampled counts)
+void launch_pack_c1(const DevPrepared& p, const double* bounds, int32_t* packet, int64_t n_unique, hipStream_t s);
+// flag the ids of all gathered packets (the next compaction numbers the union)
+void launch_union_flag(const int32_t* gathered, int world, int64_t max_u, const DevPrepared& p, hipStream_t s);
+// slot_hist[4 + slot_of[id]] += gathered sampled counts (union slots numbered)
+void launch_union_hist(const int32_t* gathered, int world, int64_t max_u, const DevPrepared& p, hipStream_t s);
 
 // (k-means launchers: kmeans_kernels.h)
 

@@ -12,19 +12,34 @@
 // features have exactly zero gradient, so the compact iteration is exactly
 // the full-width one; ||w|| adds the constant norm of the untouched part.
 //
-// k_sgd_iter_lds (the hot kernel): a 1024-thread workgroup stages the compact
-// fp32 weights in LDS, streams its SELL-16x4 chunks (4 lanes per row, the
-// row's slots kept in VGPRs between the forward gather and the backward
-// scatter), and accumulates the gradient in LDS as 64-bit FIXED POINT with
-// ds_add_u64.  Measured on gfx950 (tools/ubench_lds_atomics.hip): ds_add_f32
-// costs ~170 LDS cycles per wave-instruction, ds_add_u64 ~12 and ds_read_b32
-// ~8, so integer accumulation is ~14x faster -- and exact, so a workgroup's
-// partial gradient is independent of the order rows are added in.  Each
-// workgroup flushes its non-zero slots once (fp64 global atomics).  At
+// Exact, partition-independent arithmetic.  Per iteration i three kinds of
+// fixed point are chosen from values every workgroup and every DP rank holds
+// bit for bit (sgd_scales):
+//   * weights: w_fix = rint(w32 * 2^K) with K from max |w_text| and the
+//     longest row, so a row's whole text dot fits int32 (< 2^30 + 2^13);
+//     a row's text dot is the int32 sum of count * w_fix -- hot counts
+//     against base-128 weight digits (v_dot4_i32_i8), cold slots from LDS,
+//     far slots from global memory -- so it does not depend on which of
+//     those paths (layout, hot set, LDS tier) an entry took;
+//   * gradients: q = rint(r * 2^S) with S from a rigorous bound B >= |r|
+//     (max row bigram count * max |w| + sum max |n_k| |w_k| + max |y|), so
+//     |q| <= 2^22 and 32 rows x count 15 of it fit an int32 hot accumulator;
+//     cold entries add q into int64 LDS slots (ds_add_u64), far entries go
+//     through the slot-sorted CSC (k_far_grad), the numeric features and the
+//     loss are int64 sums at their own scales (2^N_k, 2^L);
+//   * every cross-lane / workgroup / rank sum is an int64 sum.
+// Integer sums are independent of the order rows are added in, so the
+// gradient of a batch is the same whether one workgroup or 256, one GPU or
+// eight DP ranks (any sharding) computed it: DP is bit-identical to one GPU.
+//
+// k_sgd_iter_hyb (the hot kernel): a 1024-thread workgroup stages the int32
+// weights in LDS, streams its SELL-16x4 chunks (4 lanes per row, the row's
+// slots kept in VGPRs between the forward gather and the backward scatter)
+// and writes one int64 partial row (plain stores, no contended atomics).  At
 // iteration 1 the same pass yields the prequential predictions and batch
 // statistics (K4 + K7 fused: output op #1 uses the weights before training).
-// k_sgd_update (one workgroup): fp64 master update + norms + convergence
-// flag; every later kernel of the batch early-exits once the flag is set.
+// k_sgd_update: fp64 master update + norms + max |w| + convergence record;
+// every later kernel of the batch early-exits once the flag is set.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -36,25 +51,8 @@
 
 namespace twtml {
 
-// Fixed-point scale of the LDS gradient: residuals are added as
-// round(r * 2^24) (resolution 6e-8, finer than fp32 for |r| > 1).  |r| is
-// clamped (at most 2^26, tighter when a workgroup sees more entries, see
-// sgd_fix_limit) so a workgroup's int64 slot sums cannot overflow; a clamp
-// raises the overflow flag (state[7]) and the host reports it.
-constexpr float kFixScale = 16777216.0f;        // 2^24
-constexpr double kFixInv = 1.0 / 16777216.0;
-constexpr float kFixClamp = 67108864.0f;        // 2^26
-// Far gradients (tiered layout) sum over all of a slot's entries in the
-// batch (all ranks): a coarser 2^-16 scale and a clamp from the batch's
-// entry count keep those int64 sums from overflowing (SgdParams::far_lim).
-constexpr float kFarScale = 65536.0f;           // 2^16
-constexpr double kFarInv = 1.0 / 65536.0;
-
-// Iteration record i (k_sgd_update -> convergence test) and the sampled row
-// count of iteration i (double-buffered by parity: iteration i+1's count is
-// zeroed while iteration i's is still being read).
+// Iteration record i and its per-update-workgroup partials.
 __device__ __forceinline__ double* sgd_rec(const DevSgd& d, int it) { return d.itrec + int64_t(it) * kRecStride; }
-__device__ __forceinline__ double* sgd_red_m(const DevSgd& d, int it) { return d.red64 + 2 * (it & 1) + 1; }
 
 __device__ __forceinline__ void unpack4(const uint2 v, uint32_t (&s)[4]) {
   s[0] = v.x & 0xFFFF; s[1] = v.x >> 16; s[2] = v.y & 0xFFFF; s[3] = v.y >> 16;
@@ -65,147 +63,155 @@ __device__ __forceinline__ void unpack8(const uint4 v, uint32_t (&s)[8]) {
   s[4] = v.z & 0xFFFF; s[5] = v.z >> 16; s[6] = v.w & 0xFFFF; s[7] = v.w >> 16;
 }
 
-// Per-row epilogue shared by both iteration kernels: residual, stats, preds.
-struct RowAcc {
-  float gn0 = 0.f, gn1 = 0.f, gn2 = 0.f, gn3 = 0.f, loss = 0.f;
-  double msum = 0.0;
-  double st[6] = {0, 0, 0, 0, 0, 0};
-};
-
-// Row-level inputs (numeric features + label), loadable ahead of the dot.
-struct RowIn {
-  float n0, n1, n2, n3, y;
-};
-
-__device__ __forceinline__ RowIn row_in(const DevPrepared& p, int64_t pos) {
-  const int64_t cap = p.cap_rows16;
-  return RowIn{p.num[0 * cap + pos], p.num[1 * cap + pos], p.num[2 * cap + pos],
-               p.num[3 * cap + pos], p.y[pos]};
+// ---------------------------------------------------------------------------
+// 64-bit lane exchanges.  DPP moves on the two halves stay on the VALU;
+// shuffles go through ds_bpermute (used only in epilogues).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int64_t shfl_xor_i64(int64_t v, int m) {
+  const int lo = __shfl_xor(int(uint32_t(uint64_t(v))), m, kWave);
+  const int hi = __shfl_xor(int(uint32_t(uint64_t(v) >> 32)), m, kWave);
+  return int64_t((uint64_t(uint32_t(hi)) << 32) | uint32_t(lo));
 }
 
-template <bool STATS, bool SAMPLE>
-__device__ __forceinline__ float row_residual(float dot, const RowIn& ri, int64_t pos, int t,
-                                              const DevSgd& d, const DevPrepared& p,
-                                              const SgdParams& sp, int64_t n_kept, float w0, float w1,
-                                              float w2, float w3, RowAcc& acc) {
-  const bool valid = pos < n_kept;
-  const float n0 = ri.n0, n1 = ri.n1, n2 = ri.n2, n3 = ri.n3;
-  dot += n0 * w0 + n1 * w1 + n2 * w2 + n3 * w3;
-  const float y = ri.y;
-  bool in = valid;
-  if (SAMPLE && valid)
-    in = sample_uniform(uint64_t(42 + sp.iteration), uint64_t(sp.row_offset + p.perm[pos])) <
-         sp.fraction;
-  const float r = in ? dot - y : 0.f;
-  if (t == 0) {  // one lane per row owns the row-level accumulators
-    if (STATS && valid) {
-      const double pr = round_half_away(double(dot));
-      if (sp.want_pred) d.pred_out[p.perm[pos]] = float(pr);
-      const double yd = double(y), e = yd - pr;
-      acc.st[0] += 1.0; acc.st[1] += yd; acc.st[2] += yd * yd;
-      acc.st[3] += pr; acc.st[4] += pr * pr; acc.st[5] += e * e;
-    }
-    acc.gn0 += r * n0; acc.gn1 += r * n1; acc.gn2 += r * n2; acc.gn3 += r * n3;
-    acc.loss += r * r;
-    acc.msum += in ? 1.0 : 0.0;
-  }
-  return r;
+template <int CTRL>
+__device__ __forceinline__ int64_t dpp_i64(int64_t v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, int(uint32_t(uint64_t(v))), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, int(uint32_t(uint64_t(v) >> 32)), CTRL, 0xf, 0xf, false);
+  return int64_t((uint64_t(uint32_t(hi)) << 32) | uint32_t(lo));
 }
 
-template <bool STATS, bool SAMPLE>
-__device__ __forceinline__ float row_residual(float dot, int64_t pos, int t, const DevSgd& d,
-                                              const DevPrepared& p, const SgdParams& sp,
-                                              int64_t n_kept, float w0, float w1, float w2,
-                                              float w3, RowAcc& acc) {
-  return row_residual<STATS, SAMPLE>(dot, row_in(p, pos), pos, t, d, p, sp, n_kept, w0, w1, w2, w3, acc);
+// every lane: the sum over the 4 lanes j, j+4, j+8, j+12 of its 16-lane row
+__device__ __forceinline__ int64_t row_sum_mod4_i64(int64_t v) {
+  v += dpp_i64<0x124>(v);   // row_ror:4
+  v += dpp_i64<0x128>(v);   // row_ror:8
+  return v;
 }
 
-// Workgroup epilogue without contended atomics.  Every workgroup writes one
-// partial row (plain stores) that k_sgd_reduce sums in a fixed order:
-//   cols 0..3 numeric gradients, 4..hi-1 text slots, hi..ns-1 pads (0),
-//   ns loss, ns+1 sampled row count, ns+2..ns+7 batch stats (STATS).
-// (256 workgroups adding into the same fp64 addresses serialise at the
-// memory-side atomic units: ~10-20 us per launch on MI355X, measured.)
-constexpr int kPartVals = 12;
-
-template <bool STATS, bool SAMPLE>
-__device__ __forceinline__ void part_scalars(const DevSgd& d, const RowAcc& acc,
-                                             double (*wsc)[kPartVals], double* prow) {
-  double v[kPartVals] = {0.0, 0.0, 0.0, 0.0, 0.0, acc.msum, acc.st[0], acc.st[1], acc.st[2],
-                         acc.st[3], acc.st[4], acc.st[5]};
-  constexpr int nv = STATS ? kPartVals : (SAMPLE ? 6 : 5);
-  const int w = threadIdx.x / kWave;
-  // the per-lane fp32 partials reduce on the VALU (DPP); fp64 from here on
-  v[0] = double(wave_sum_f32(acc.gn0));
-  v[1] = double(wave_sum_f32(acc.gn1));
-  v[2] = double(wave_sum_f32(acc.gn2));
-  v[3] = double(wave_sum_f32(acc.gn3));
-  v[4] = 0.5 * double(wave_sum_f32(acc.loss));
+__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
 #pragma unroll
-  for (int k = 5; k < nv; ++k) v[k] = wave_sum(v[k]);
-  if (lane_id() == 0) {
-#pragma unroll
-    for (int k = 0; k < nv; ++k) wsc[w][k] = v[k];
-  }
-  __syncthreads();
-  const int tid = threadIdx.x;
-  if (tid < kPartVals) {
-    double t = 0.0;
-    if (tid < nv)
-      for (int k = 0; k < int(blockDim.x) / kWave; ++k) t += wsc[k][tid];
-    prow[tid < kNumNumeric ? int64_t(tid) : d.nl + (tid - kNumNumeric)] = t;
-  }
-}
-
-// Text-slot columns of a partial row: the REP fixed-point replicas summed
-// (+ the hot total of a hot slot).
-template <int REP>
-__device__ __forceinline__ double part_slot(const unsigned long long* gl, int64_t s) {
-  long long v = 0;
-#pragma unroll
-  for (int k = 0; k < REP; ++k) v += (long long)gl[s * REP + k];
-  return double(v) * kFixInv;
-}
-
-float sgd_far_limit(int64_t entries_total) {
-  const double e = double(entries_total < 1 ? 1 : entries_total);
-  return float(std::min(double(kFixClamp) * double(kFarScale), 4.611686018427388e18 / e) * 0.999);
-}
-
-float sgd_fix_limit(int64_t entries_per_wg) {
-  const double e = double(entries_per_wg < 1 ? 1 : entries_per_wg);
-  const double lim = std::min(double(kFixClamp) * double(kFixScale), 4.611686018427388e18 / e);
-  return float(lim * 0.999);
-}
-
-__device__ __forceinline__ unsigned long long to_fix(float r, bool& clamped, float lim) {
-  float v = r * kFixScale;
-  if (fabsf(v) > lim) {
-    clamped = true;
-    v = v > 0.f ? lim : -lim;
-  }
-  return (unsigned long long)(long long)__float2ll_rn(v);
+  for (int off = 32; off > 0; off >>= 1) v += shfl_xor_i64(v, off);
+  return v;
 }
 
 // ---------------------------------------------------------------------------
-// Fast path: u16 slots, LDS weights + REP replicated fixed-point gradients.
+// Per-iteration fixed-point scales.
 // ---------------------------------------------------------------------------
-constexpr int kIterBlock = 1024;
+__device__ __forceinline__ int floor_log2(double x) {   // x > 0, finite
+  int e;
+  (void)frexp(x, &e);
+  return e - 1;
+}
+__device__ __forceinline__ int ceil_log2(double x) {    // x >= 1
+  const int e = floor_log2(x);
+  return ldexp(1.0, e) < x ? e + 1 : e;
+}
 
-// CNT: entries carry HashingTF term counts (p.cnt, merged duplicates, chunk
-// lengths p.clen8d); otherwise every entry counts once.
+struct IterScale {
+  float wscale, wunscale;   // 2^K, 2^-K
+  float qscale;             // 2^S
+  float lhalf;              // 2^(L/2)
+  float nscale[kNumNumeric];    // 2^N_k
+  int K, S, L, N[kNumNumeric];
+  double B;
+  int bad;
+};
+
+// Deterministic in (max |w_text|, numeric weights, batch bounds, m): every
+// workgroup, every iteration kernel and every DP rank derives the same.
+__device__ IterScale sgd_scales(const DevSgd& d, double maxw, const float* wn) {
+  IterScale s{};
+  const double* bd = d.bounds;
+  double B = bd[0] * maxw + bd[1];
+#pragma unroll
+  for (int k = 0; k < kNumNumeric; ++k) B += bd[2 + k] * fabs(double(wn[k]));
+  B = B * (1.0 + 1.0 / 1024.0) + 1.0;   // fp32 rounding of the dot, rint of the weights
+  s.B = B;
+  // diverged: the residual bound (or the weights) left any usable range
+  s.bad = !(B < 1e30) || !(maxw < 1e30) || !(B == B);
+  if (s.bad) {
+    s.wscale = s.wunscale = s.qscale = s.lhalf = 1.f;
+    for (int k = 0; k < kNumNumeric; ++k) s.nscale[k] = 1.f;
+    return s;
+  }
+  // maxw 2^K < 2^25 (4 base-128 digits) and rowmax maxw 2^K < 2^30: a row's
+  // fixed-point dot, rint errors included (<= rowmax / 2), fits int32
+  int K = 0;
+  if (maxw > 0.0) {
+    K = 24 - floor_log2(maxw);
+    const double T = bd[0] * maxw;
+    if (T > 0.0) K = min(K, 29 - floor_log2(T));
+  }
+  K = K < -120 ? -120 : (K > 120 ? 120 : K);
+  const int eb = floor_log2(B) + 1;                     // B < 2^eb
+  // Per row |q|, |r n_k| 2^N_k and r^2 2^L stay <= 2^22: kHotFlush rows of
+  // them (x count 15 for q) fit the kernels' int32 accumulators, and m rows
+  // (m < 2^31) the int64 sums.
+  s.K = K;
+  s.S = 22 - eb;                                        // |q| <= B 2^S + 1/2 <= 2^22
+  s.L = 2 * (11 - eb);                                  // (r 2^(L/2))^2 <= 2^22
+  s.wscale = ldexpf(1.f, K);
+  s.wunscale = ldexpf(1.f, -K);
+  s.qscale = ldexpf(1.f, s.S);
+  s.lhalf = ldexpf(1.f, 11 - eb);
+#pragma unroll
+  for (int k = 0; k < kNumNumeric; ++k) {
+    const double nm = bd[2 + k];
+    int n = nm > 0.0 ? 22 - eb - (floor_log2(nm) + 1) : 0;   // B max|n_k| 2^N < 2^22
+    n = n < -120 ? -120 : (n > 120 ? 120 : n);
+    s.N[k] = n;
+    s.nscale[k] = ldexpf(1.f, n);
+  }
+  return s;
+}
+
+__device__ __forceinline__ float sgpr_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+}
+__device__ __forceinline__ double sgpr_d(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(u))));
+  const uint32_t hi = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(u >> 32))));
+  return __builtin_bit_cast(double, (uint64_t(hi) << 32) | lo);
+}
+
+// What a lane of the iteration kernels keeps of the scales: wave-uniform
+// factors in SGPRs, its numeric feature's weight and scale.
+struct LaneScale {
+  float wscale, wunscale, qscale, lhalf;
+  float nsc_t;   // 2^N_t of this lane's numeric feature
+  float wn_t;
+};
+
+__device__ __forceinline__ LaneScale lane_scale(const IterScale& sc, const DevSgd& d, int t) {
+  LaneScale l;
+  l.wscale = sgpr_f(sc.wscale);
+  l.wunscale = sgpr_f(sc.wunscale);
+  l.qscale = sgpr_f(sc.qscale);
+  l.lhalf = sgpr_f(sc.lhalf);
+  l.nsc_t = sc.nscale[t];
+  l.wn_t = d.wc32[t];
+  return l;
+}
+
+
+// ---------------------------------------------------------------------------
 // Convergence after update `it`, evaluated by one wave (lane-parallel loads,
-// fixed-order DPP reduction): identical in every caller.
-__device__ bool sgd_converged_wave(const DevSgd& d, int it, double tol) {
+// fixed-order DPP reduction): identical in every caller.  Also returns the
+// max |w_text| after that update (the next iteration's weight scale).
+// ---------------------------------------------------------------------------
+__device__ bool sgd_converged_wave(const DevSgd& d, int it, double tol, double* maxw_out = nullptr) {
   const double* rec = sgd_rec(d, it);
   const int nw = int(rec[2]);
-  double ds = 0.0, ws = 0.0;
+  double ds = 0.0, ws = 0.0, mx = 0.0;
   for (int k = lane_id(); k < nw; k += kWave) {
-    ds += rec[kRecHead + 2 * k];
-    ws += rec[kRecHead + 2 * k + 1];
+    ds += rec[kRecHead + 3 * k];
+    ws += rec[kRecHead + 3 * k + 1];
+    mx = fmax(mx, rec[kRecHead + 3 * k + 2]);
   }
   ds = wave_sum(ds);
   ws = wave_sum(ws);
+  mx = wave_max(mx);
+  if (maxw_out) *maxw_out = mx;
   if (!(rec[1] > 0.0) || rec[0] < 2.0) return false;   // no update this iteration / first update
   double rest = d.state[4] - d.state[6];
   if (rest < 0.0) rest = 0.0;
@@ -213,30 +219,46 @@ __device__ bool sgd_converged_wave(const DevSgd& d, int it, double tol) {
   return sqrt(ds) < tol * (wnorm > 1.0 ? wnorm : 1.0);
 }
 
-// Iteration-kernel prologue: true when the batch is finished (the caller
-// returns).  Called by every thread; `flag` is a workgroup-shared int.
-// Also publishes the verdict for update i-1 to the host (zero-copy pinned
-// memory, initialised to -1 by the host): the host polls it to stop
-// enqueueing iterations, without a per-iteration event in the stream.
-// DP ranks only skip the pass on their own verdict (state[8] = iteration):
-// k_sgd_reduce puts rank 0's into the gradient all-reduce and k_sgd_update
-// acts on the agreed value.
-__device__ bool sgd_stop(const DevSgd& d, const SgdParams& sp, int* flag) {
+// Iteration-kernel prologue (every thread calls it; `flag` / `sc` are
+// workgroup-shared): true when the batch is finished (the caller returns).
+// Wave 0 checks convergence after update i-1, derives iteration i's scales
+// (workgroup 0 records them for the far backward / reduce / update kernels)
+// and publishes the verdict on update i-1 to the host (zero-copy pinned
+// memory, initialised to -1 by the host) which polls it to stop enqueueing.
+// A diverged model (scales invalid) stops like a converged one, with
+// state[7] set instead of state[1].  DP ranks only skip the pass on their
+// own verdict (state[8] = iteration): k_sgd_reduce puts rank 0's into the
+// gradient all-reduce and k_sgd_update acts on the agreed value.
+__device__ bool sgd_prologue(const DevSgd& d, const SgdParams& sp, int* flag, IterScale* sc) {
   if (threadIdx.x < kWave) {
+    const int it = sp.iteration;
     const bool done = d.state[0] != 0.0;
     bool stop = done;
-    if (!done && sp.iteration > 1) {
-      stop = sgd_converged_wave(d, sp.iteration - 1, sp.tol);
-      if (stop && blockIdx.x == 0 && threadIdx.x == 0) {
-        if (!sp.dp) {
-          d.state[0] = 1.0;
-          d.state[1] = 1.0;
-        } else {
-          // DP: this rank skips the pass (identical weights -> every rank
-          // does); the agreed verdict in k_sgd_update ends the batch
-          d.state[8] = double(sp.iteration);
+    if (!done) {
+      double maxw = d.state[9];
+      const bool conv = it > 1 && sgd_converged_wave(d, it - 1, sp.tol, &maxw);
+      const float wn[kNumNumeric] = {d.wc32[0], d.wc32[1], d.wc32[2], d.wc32[3]};
+      const IterScale s = sgd_scales(d, maxw, wn);
+      stop = conv || s.bad;
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        double* rec = sgd_rec(d, it);
+        rec[kRecK] = s.K;
+        rec[kRecS] = s.S;
+        rec[kRecL] = s.L;
+        for (int k = 0; k < kNumNumeric; ++k) rec[kRecN + k] = s.N[k];
+        rec[kRecB] = s.B;
+        rec[kRecBad] = s.bad ? 1.0 : 0.0;
+        if (s.bad) d.state[7] = 1.0;
+        if (stop) {
+          if (!sp.dp) {
+            d.state[0] = 1.0;
+            if (conv && !s.bad) d.state[1] = 1.0;
+          } else {
+            d.state[8] = double(it);   // DP: skip this pass; the agreed verdict ends the batch
+          }
         }
       }
+      if (threadIdx.x == 0) *sc = s;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0 && d.host_flags && sp.iteration > 1 && !sp.dp) {
       __hip_atomic_store(&d.host_flags[sp.iteration - 1], stop ? 1.0 : 0.0, __ATOMIC_RELAXED,
@@ -248,20 +270,152 @@ __device__ bool sgd_stop(const DevSgd& d, const SgdParams& sp, int* flag) {
   return *flag != 0;
 }
 
+// ---------------------------------------------------------------------------
+// Row epilogue shared by the iteration kernels.
+// ---------------------------------------------------------------------------
+// Per-lane accumulators.  Lane t of a row owns numeric feature t; lane 0 the
+// loss, sampled count and batch statistics.  qn / ql hold at most kHotFlush
+// rows (int32, <= 2^22 per row) before the kernel folds them into int64.
+struct RowAcc {
+  int32_t qn = 0;     // sum rint(r n_t 2^N_t)
+  int32_t ql = 0;     // sum rint((r 2^(L/2))^2) (t == 0)
+  int32_t msum = 0;   // rows in the sampled gradient (t == 0, SAMPLE)
+  double st[6] = {0, 0, 0, 0, 0, 0};
+};
+
+struct RowIn {
+  float nt, y;   // this lane's numeric feature, the label
+};
+
+__device__ __forceinline__ RowIn row_in(const DevPrepared& p, int64_t pos, int t) {
+  return RowIn{p.num[int64_t(t) * p.cap_rows16 + pos], p.y[pos]};
+}
+
+// sum of a row's 4 lane values (every lane of the row gets the same bits)
+__device__ __forceinline__ int32_t row_total(int32_t v) {
+  v += __shfl_xor(v, 1, kWave);
+  v += __shfl_xor(v, 2, kWave);
+  return v;
+}
+
+// Residual of the row at sorted position pos from its fixed-point text dot
+// (already summed over the row's 4 lanes); accumulates stats (iteration 1),
+// numeric-feature gradients, loss and the sampled count.  Returns r (0 for
+// rows outside the batch / the sample).
+template <bool STATS, bool SAMPLE>
+__device__ __forceinline__ float row_residual(int32_t dot_fix, const RowIn& ri, int64_t pos, int t,
+                                              const DevSgd& d, const DevPrepared& p, const SgdParams& sp,
+                                              int64_t n_kept, const LaneScale& sc, RowAcc& acc) {
+  const bool valid = pos < n_kept;
+  // numeric part: (n0 w0 + n1 w1) + (n2 w2 + n3 w3), the same bits on the row's 4 lanes
+  float vn = ri.nt * sc.wn_t;
+  vn += __shfl_xor(vn, 1, kWave);
+  vn += __shfl_xor(vn, 2, kWave);
+  const float dot = float(dot_fix) * sc.wunscale + vn;
+  bool in = valid;
+  if (SAMPLE && valid)
+    in = sample_uniform(uint64_t(42 + sp.iteration), uint64_t(sp.row_offset + p.perm[pos])) < sp.fraction;
+  const float r = in ? dot - ri.y : 0.f;
+  if (t == 0) {
+    if (STATS && valid) {
+      const double pr = round_half_away(double(dot));
+      if (sp.want_pred) d.pred_out[p.perm[pos]] = float(pr);
+      const double yd = double(ri.y), e = yd - pr;
+      acc.st[0] += 1.0; acc.st[1] += yd; acc.st[2] += yd * yd;
+      acc.st[3] += pr; acc.st[4] += pr * pr; acc.st[5] += e * e;
+    }
+    if (SAMPLE && in) ++acc.msum;
+    const float u = r * sc.lhalf;
+    acc.ql += __float2int_rn(u * u);
+  }
+  acc.qn += __float2int_rn((r * ri.nt) * sc.nsc_t);
+  return r;
+}
+
+// Workgroup epilogue: every workgroup writes one int64 partial row (plain
+// stores) that k_sgd_update / k_sgd_reduce sum (exact in any order):
+//   cols 0..3 numeric gradients (2^N_k), 4..far_base-1 text slots (2^S),
+//   far_base..nl-1 zero, nl loss (2^L), nl+1 sampled row count, nl+2..nl+7
+//   batch stats (fp64 bits, STATS: integer-valued, so their fp64 sums are
+//   exact too).
+constexpr int kPartVals = 12;
+
+template <bool STATS>
+__device__ __forceinline__ void part_scalars(const DevSgd& d, int64_t qn, int64_t ql, const RowAcc& acc,
+                                             const unsigned long long* wg_tot, int64_t (*wsc)[kPartVals],
+                                             int64_t* prow) {
+  const int w = threadIdx.x / kWave, lane = lane_id();
+  // numeric: lanes with t == k hold feature k -> sum per quad column, then the 4 rows
+  qn = row_sum_mod4_i64(qn);
+  qn += shfl_xor_i64(qn, 16);
+  qn += shfl_xor_i64(qn, 32);
+  ql = wave_sum_i64(ql);
+  const int ms = wave_sum(acc.msum);
+  double st[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) st[k] = STATS ? wave_sum(acc.st[k]) : 0.0;
+  if (lane < kNumNumeric) wsc[w][lane] = qn;
+  if (lane == 0) {
+    wsc[w][4] = ql;
+    wsc[w][5] = ms;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) wsc[w][6 + k] = __builtin_bit_cast(int64_t, st[k]);
+  }
+  __syncthreads();
+  const int tid = threadIdx.x;
+  if (tid < kPartVals) {
+    const int nw = int(blockDim.x) / kWave;
+    int64_t v;
+    if (tid < 6) {
+      v = (wg_tot && tid < 5) ? (long long)wg_tot[tid] : 0;
+      for (int k = 0; k < nw; ++k) v += wsc[k][tid];
+    } else {
+      double t = 0.0;
+      for (int k = 0; k < nw; ++k) t += __builtin_bit_cast(double, wsc[k][tid]);
+      v = __builtin_bit_cast(int64_t, t);
+    }
+    const int64_t col = tid < kNumNumeric ? int64_t(tid) : d.nl + (tid - kNumNumeric);
+    prow[col] = v;
+  }
+}
+
+template <int REP>
+__device__ __forceinline__ int64_t part_slot(const unsigned long long* gl, int64_t s) {
+  long long v = 0;
+#pragma unroll
+  for (int k = 0; k < REP; ++k) v += (long long)gl[s * REP + k];
+  return v;
+}
+
+__device__ __forceinline__ int32_t w_to_fix(float w, float wscale) {
+  return __float2int_rn(w * wscale);
+}
+
+// ---------------------------------------------------------------------------
+// Plain path (u16 slots, no hot split): LDS int32 weights + REP replicated
+// int64 gradients.  CNT: entries carry HashingTF term counts (p.cnt, merged
+// duplicates, chunk lengths p.clen8d); otherwise every entry counts once.
+// ---------------------------------------------------------------------------
+constexpr int kIterBlock = 1024;
+
 template <bool STATS, bool SAMPLE, int REP, bool CNT>
 __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_lds(DevSgd d, DevPrepared p, SgdParams sp) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  __shared__ double wsc[kIterBlock / kWave][kPartVals];
+  extern __shared__ __attribute__((aligned(16))) int32_t lds[];
+  __shared__ int64_t wsc[kIterBlock / kWave][kPartVals];
   __shared__ int stop_flag;
-  if (sgd_stop(d, sp, &stop_flag)) return;  // converged / finished: the rest of the batch is a no-op
-  const int64_t ns = d.nl;        // multiple of 64 (== d.ns: the plain path is never tiered)
-  float* wl = lds;
-  unsigned long long* gl = reinterpret_cast<unsigned long long*>(lds + ns);
-  for (int64_t s = threadIdx.x; s < ns; s += kIterBlock) wl[s] = d.wc32[s];
-  for (int64_t s = threadIdx.x; s < ns * REP; s += kIterBlock) gl[s] = 0ull;
-  __syncthreads();
+  __shared__ IterScale scs;
+  if (sgd_prologue(d, sp, &stop_flag, &scs)) return;   // converged / finished: the rest of the batch is a no-op
   const int lane = lane_id();
   const int r = lane / kLanesPerRow, t = lane % kLanesPerRow;
+  const LaneScale sc = lane_scale(scs, d, t);
+  const int64_t ns = d.nl;        // multiple of 64 (== d.ns: the plain path is never tiered)
+  int32_t* wl = lds;
+  unsigned long long* gl = reinterpret_cast<unsigned long long*>(lds + ns);
+  const int64_t hi_slot = kNumNumeric + d.n_unique;
+  for (int64_t s = threadIdx.x; s < ns; s += kIterBlock)
+    wl[s] = (s >= kNumNumeric && s < hi_slot) ? w_to_fix(d.wc32[s], sc.wscale) : 0;
+  for (int64_t s = threadIdx.x; s < ns * REP; s += kIterBlock) gl[s] = 0ull;
+  __syncthreads();
   const int rep = lane % REP;
   const int64_t n_kept = p.counters[0];
   const int64_t nch = (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;
@@ -269,11 +423,10 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_lds(DevSgd d, DevPrepar
                        __builtin_amdgcn_readfirstlane(int(threadIdx.x) / kWave);   // wave-uniform
   const int64_t nwaves = int64_t(gridDim.x) * (kIterBlock / kWave);
   const uint16_t* slot = static_cast<const uint16_t*>(p.slot);
-  const float w0 = wl[0], w1 = wl[1], w2 = wl[2], w3 = wl[3];
   RowAcc acc;
-  bool clamped = false;
+  int64_t qn64 = 0, ql64 = 0;   // acc.qn / acc.ql folded every chunk
 
-  // chunk metadata for 64 chunks at a time in lanes (see k_sgd_iter_hyb)
+  // chunk metadata for 64 chunks at a time in lanes
   const int32_t* __restrict__ clen = CNT ? p.clen8d : p.clen8;
   int32_t md_l8 = 0;
   int64_t md_cb = 0;
@@ -291,7 +444,10 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_lds(DevSgd d, DevPrepar
     const int64_t off = cb * kChunkStride + lane * kGroup;
     const uint16_t* sl = slot + off;
     const int64_t pos = c * kRowsPerChunk + r;
-    const RowIn ri = row_in(p, pos);
+    const RowIn ri = row_in(p, pos, t);
+    qn64 += acc.qn;   // the previous chunk's row
+    ql64 += acc.ql;
+    acc.qn = acc.ql = 0;
     if (L8 <= kMaxRegGroups) {
       uint4 v[kMaxRegGroups];
       uint4 cv[CNT ? kMaxRegGroups : 1];
@@ -301,46 +457,39 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_lds(DevSgd d, DevPrepar
           v[g] = *reinterpret_cast<const uint4*>(sl + int64_t(g) * kChunkStride);
           if (CNT) cv[g] = *reinterpret_cast<const uint4*>(p.cnt + off + int64_t(g) * kChunkStride);
         }
-      float d0 = 0.f, d1 = 0.f;
+      int32_t d0 = 0, d1 = 0;   // partial sums of the row's int32 dot (sgd_scales)
 #pragma unroll
       for (int g = 0; g < kMaxRegGroups; ++g) {
-        if (g < L8 && sp.ablate < 2) {
+        if (g < L8) {
           uint32_t s[8];
           unpack8(v[g], s);
           if (CNT) {
-            uint32_t k[8];
-            unpack8(cv[g], k);
-            d0 += wl[s[0]] * float(k[0]) + wl[s[2]] * float(k[2]) + wl[s[4]] * float(k[4]) +
-                  wl[s[6]] * float(k[6]);
-            d1 += wl[s[1]] * float(k[1]) + wl[s[3]] * float(k[3]) + wl[s[5]] * float(k[5]) +
-                  wl[s[7]] * float(k[7]);
+            uint32_t kk[8];
+            unpack8(cv[g], kk);
+            d0 += wl[s[0]] * int32_t(kk[0]) + wl[s[2]] * int32_t(kk[2]) + wl[s[4]] * int32_t(kk[4]) +
+                  wl[s[6]] * int32_t(kk[6]);
+            d1 += wl[s[1]] * int32_t(kk[1]) + wl[s[3]] * int32_t(kk[3]) + wl[s[5]] * int32_t(kk[5]) +
+                  wl[s[7]] * int32_t(kk[7]);
           } else {
             d0 += wl[s[0]] + wl[s[2]] + wl[s[4]] + wl[s[6]];
             d1 += wl[s[1]] + wl[s[3]] + wl[s[5]] + wl[s[7]];
           }
         }
       }
-      float dot = d0 + d1;
-      if (sp.ablate >= 2) {
-        uint32_t s[8];
-        unpack8(v[0], s);
-        dot += float(s[0] + s[7]) * 1e-30f;  // keep the loads live
-      }
-      dot += __shfl_xor(dot, 1, kWave);
-      dot += __shfl_xor(dot, 2, kWave);
-      const float res = row_residual<STATS, SAMPLE>(dot, ri, pos, t, d, p, sp, n_kept, w0, w1, w2, w3, acc);
+      const int32_t dot = row_total(d0 + d1);
+      const float res = row_residual<STATS, SAMPLE>(dot, ri, pos, t, d, p, sp, n_kept, sc, acc);
       if (res != 0.f && sp.ablate == 0) {
-        const unsigned long long q = to_fix(res, clamped, sp.fix_lim);
+        const unsigned long long q = (unsigned long long)(long long)__float2int_rn(res * sc.qscale);
 #pragma unroll
         for (int g = 0; g < kMaxRegGroups; ++g) {
           if (g < L8) {
             uint32_t s[8];
             unpack8(v[g], s);
             if (CNT) {
-              uint32_t k[8];
-              unpack8(cv[g], k);
+              uint32_t kk[8];
+              unpack8(cv[g], kk);
 #pragma unroll
-              for (int e = 0; e < 8; ++e) atomicAdd(&gl[s[e] * REP + rep], q * (unsigned long long)k[e]);
+              for (int e = 0; e < 8; ++e) atomicAdd(&gl[s[e] * REP + rep], q * (unsigned long long)kk[e]);
             } else {
 #pragma unroll
               for (int e = 0; e < 8; ++e) atomicAdd(&gl[s[e] * REP + rep], q);
@@ -349,67 +498,64 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_lds(DevSgd d, DevPrepar
         }
       }
     } else {  // very long rows: stream the slots twice (never merged: count 1)
-      float dot = 0.f;
+      int32_t dot = 0;
       for (int32_t g = 0; g < L8; ++g) {
         uint32_t s[8];
         unpack8(*reinterpret_cast<const uint4*>(sl + int64_t(g) * kChunkStride), s);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) dot += wl[s[k]];
+        for (int e = 0; e < 8; ++e) dot += wl[s[e]];
       }
-      dot += __shfl_xor(dot, 1, kWave);
-      dot += __shfl_xor(dot, 2, kWave);
-      const float res = row_residual<STATS, SAMPLE>(dot, ri, pos, t, d, p, sp, n_kept, w0, w1, w2, w3, acc);
+      dot = row_total(dot);
+      const float res = row_residual<STATS, SAMPLE>(dot, ri, pos, t, d, p, sp, n_kept, sc, acc);
       if (res != 0.f) {
-        const unsigned long long q = to_fix(res, clamped, sp.fix_lim);
+        const unsigned long long q = (unsigned long long)(long long)__float2int_rn(res * sc.qscale);
         for (int32_t g = 0; g < L8; ++g) {
           uint32_t s[8];
           unpack8(*reinterpret_cast<const uint4*>(sl + int64_t(g) * kChunkStride), s);
 #pragma unroll
-          for (int k = 0; k < 8; ++k) atomicAdd(&gl[s[k] * REP + rep], q);
+          for (int e = 0; e < 8; ++e) atomicAdd(&gl[s[e] * REP + rep], q);
         }
       }
     }
   }
 
-  if (__any(clamped) && lane == 0) d.state[7] = 1.0;
-  double* prow = d.part + int64_t(blockIdx.x) * d.pstride;
-  part_scalars<STATS, SAMPLE>(d, acc, wsc, prow);   // includes the block barrier
-  const int64_t hi = kNumNumeric + d.n_unique;      // pads are never flushed
+  int64_t* prow = d.part + int64_t(blockIdx.x) * d.pstride;
+  part_scalars<STATS>(d, qn64 + acc.qn, ql64 + acc.ql, acc, nullptr, wsc, prow);   // includes the block barrier
   for (int64_t s = kNumNumeric + threadIdx.x; s < ns; s += kIterBlock)
-    prow[s] = s < hi ? part_slot<REP>(gl, s) : 0.0;
+    prow[s] = s < hi_slot ? part_slot<REP>(gl, s) : 0;   // pads are never flushed
 }
 
 // ---------------------------------------------------------------------------
 // Hybrid dense-hot path (layout: hot_split.hip).  Per chunk a lane reads its
 // row's 32 hot counts (16 B: 4-bit counts of hot ids 32t..32t+31) and the
-// row-balanced cold groups.  Hot weights are read from LDS with b128 loads
-// (broadcast across the 16 lanes of a quarter), the hot gradient accumulates
-// in VGPRs (fp32 per lane, fp64 across waves); only cold entries use the LDS
-// fixed-point gradient.  Chunks left
-// in the plain layout (clen8c < 0) take the plain route.
+// row-balanced cold groups.  Hot weights are read from LDS as base-128
+// digit planes (b128 loads, broadcast across the 16 lanes of a quarter), the
+// hot gradient accumulates as int32 count * q per lane (flushed to an int64
+// LDS row every kHotFlush chunks); cold entries use the LDS int64 gradient.
+// Chunks left in the plain layout (clen8c < 0) take the plain route.
 // ---------------------------------------------------------------------------
 constexpr int kMaxColdGroups = 8;   // cold 4-entry groups kept in VGPRs (32 cold entries per lane)
 constexpr int kHotPerLane = kHot / kLanesPerRow;   // 32
+// rows a lane adds into its int32 hot accumulators between flushes:
+// kHotFlush * 15 * 2^22 < 2^31
+constexpr int kHotFlush = 32;
 
-// wq: this lane's 32 hot weights in LDS (quarter t, 16-B aligned, stride 36
-// floats so the four quarters' b128 reads hit different banks)
+// wq: this lane's 32 hot weight digits in LDS (quarter t, 16-B aligned,
+// stride 36 dwords so the four quarters' b128 reads hit different banks)
 constexpr int kHotLdsStride = kHotPerLane + 4;
 
-// Hot weights as 4 signed base-128 digits of a 28-bit fixed-point value
-// (w ~= S * 2^-27 * (d0 2^21 + d1 2^14 + d2 2^7 + d3), S = max |w_hot| of
-// the pass): the forward dot of a lane's 32 hot counts is 32
-// v_dot4_i32_iu8 (4 counts x 4 digits each, exact int32), not 96 VALU ops
-// of extract / convert / fma.  Quantisation error <= S * 2^-28 per weight.
+// Hot weights w_fix (|w_fix| < 2^25) as 4 signed base-128 digits
+// (w_fix = d0 2^21 + d1 2^14 + d2 2^7 + d3): the forward dot of a lane's 32
+// hot counts is 32 v_dot4_i32_i8 (4 counts x 4 digits each, exact int32).
 // LDS per lane quarter t (kHotLdsStride dwords): dword (d*4 + q)*2 + half
 // packs digit d of the 4 hot ids held in the even (half 0) / odd (half 1)
-// nibbles of the lane's count dword q; dwords 32..35 hold the 4 digit scales.
-// (Counts 0..15 are valid signed bytes, so the signed v_dot4_i32_i8 serves.)
+// nibbles of the lane's count dword q.
 __device__ __forceinline__ void nib_split(uint32_t x, uint32_t& lo, uint32_t& hi) {
   lo = x & 0x0F0F0F0Fu;           // nibbles 0,2,4,6 -> bytes 0..3
   hi = (x >> 4) & 0x0F0F0F0Fu;    // nibbles 1,3,5,7 -> bytes 0..3
 }
 
-__device__ __forceinline__ float hot_dot(const uint4 hv, const uint32_t* wq) {
+__device__ __forceinline__ int32_t hot_dot(const uint4 hv, const uint32_t* wq) {
   const uint32_t hw[4] = {hv.x, hv.y, hv.z, hv.w};
   int acc[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -425,44 +571,55 @@ __device__ __forceinline__ float hot_dot(const uint4 hv, const uint32_t* wq) {
       acc[d] = __builtin_amdgcn_sdot4(int(hi), int(dg[2 * q + 1]), acc[d], false);
     }
   }
-  const float4 sc = reinterpret_cast<const float4*>(wq)[8];
-  return float(acc[0]) * sc.x + float(acc[1]) * sc.y + float(acc[2]) * sc.z + float(acc[3]) * sc.w;
+  // the lane's exact hot dot, a partial sum of the row's int32 dot (sgd_scales)
+  return (((acc[0] << 7) + acc[1]) << 14) + (acc[2] << 7) + acc[3];
 }
 
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
-// gh[j] accumulates hot ids (2j, 2j+1) of the lane's quarter: counts convert
-// straight from bytes (v_cvt_f32_ubyteN) and pairs update with v_pk_fma_f32.
-__device__ __forceinline__ void hot_grad(const uint4 hv, float res, f32x2 (&gh)[kHotPerLane / 2]) {
+// gh[i] += count of hot id 32t + i times q (v_bfe + v_mad_i32_i24)
+__device__ __forceinline__ void hot_grad(const uint4 hv, int32_t q, int32_t (&gh)[kHotPerLane]) {
   const uint32_t hw[4] = {hv.x, hv.y, hv.z, hv.w};
-  const f32x2 r2 = {res, res};
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    uint32_t lo, hi;
-    nib_split(hw[q], lo, hi);
+  for (int qq = 0; qq < 4; ++qq) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const f32x2 c = {float((lo >> (8 * i)) & 0xFFu), float((hi >> (8 * i)) & 0xFFu)};
-      gh[4 * q + i] = __builtin_elementwise_fma(c, r2, gh[4 * q + i]);
+    for (int k = 0; k < 8; ++k) {
+      const int32_t c = int32_t((hw[qq] >> (4 * k)) & 15u);
+      // in place (tied operand): the accumulators keep their registers
+      // across the loop instead of being renamed and copied back
+      asm volatile("v_mad_i32_i24 %0, %1, %2, %0" : "+v"(gh[8 * qq + k]) : "v"(c), "v"(q));
     }
   }
 }
 
-// Build the digit table of the pass from the LDS weights (one wave; the
+// int32 hot / numeric / loss accumulators -> the workgroup's int64 row
+// hsum[0, kHot + 5): per quad column over the 16-lane row (DPP), then lanes
+// 0..3 of each row add (4 rows per address; once per kHotFlush chunks).
+__device__ __forceinline__ void hot_flush(int32_t (&gh)[kHotPerLane], RowAcc& acc, unsigned long long* hsum) {
+  const int lane = lane_id();
+  const bool head = (lane & 15) < kLanesPerRow;
+#pragma unroll
+  for (int i = 0; i < kHotPerLane; ++i) {
+    const int64_t v = row_sum_mod4_i64(int64_t(gh[i]));
+    if (head && v != 0) atomicAdd(&hsum[kHotPerLane * (lane & 3) + i], (unsigned long long)v);
+    asm volatile("v_mov_b32 %0, 0" : "+v"(gh[i]));   // zeroed in place (no second register set)
+  }
+  const int64_t qn = row_sum_mod4_i64(int64_t(acc.qn));
+  const int64_t ql = row_sum_mod4_i64(int64_t(acc.ql));
+  if (head && qn != 0) atomicAdd(&hsum[kHot + (lane & 3)], (unsigned long long)qn);
+  if ((lane & 15) == 0 && ql != 0) atomicAdd(&hsum[kHot + kNumNumeric], (unsigned long long)ql);
+  acc.qn = 0;
+  acc.ql = 0;
+}
+
+// Build the digit table of the pass from the LDS int32 weights (one wave; the
 // caller synchronises).  Hot id h: quarter t = h / 32, count dword
 // q = (h % 32) / 8, nibble k = h % 8 -> half = k & 1, byte i = k >> 1.
-__device__ __forceinline__ void hot_digits(const DevPrepared& p, const float* wl, uint32_t* whl) {
+__device__ __forceinline__ void hot_digits(const DevPrepared& p, const int32_t* wl, uint32_t* whl) {
   const int lane = lane_id();
-  const float wa = wl[p.hot_slot[lane]], wb = wl[p.hot_slot[lane + kWave]];
-  float S = fmaxf(fabsf(wa), fabsf(wb));
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) S = fmaxf(S, __shfl_xor(S, off, kWave));
-  const float inv = S > 0.f ? 134217728.0f / S : 0.f;   // 2^27 / S
   uint8_t* bytes = reinterpret_cast<uint8_t*>(whl);
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int h = lane + u * kWave;
-    int32_t W = int32_t(rintf((u ? wb : wa) * inv));
+    int32_t W = wl[p.hot_slot[h]];
     int32_t dg[4];
 #pragma unroll
     for (int d = 3; d > 0; --d) {   // balanced base-128 digits, least significant first
@@ -470,55 +627,40 @@ __device__ __forceinline__ void hot_digits(const DevPrepared& p, const float* wl
       dg[d] = x;
       W = (W - x) >> 7;
     }
-    dg[0] = W;                       // |W| <= 2^27 -> |d0| <= 64
+    dg[0] = W;                       // |W| <= 2^25 -> |d0| <= 16
     const int t = h / 32, q = (h % 32) / 8, k = h % 8;
 #pragma unroll
     for (int d = 0; d < 4; ++d)
       bytes[(t * kHotLdsStride + (d * 4 + q) * 2 + (k & 1)) * 4 + (k >> 1)] = uint8_t(int8_t(dg[d]));
   }
-  if (lane < kLanesPerRow) {
-    float* sc = reinterpret_cast<float*>(whl + lane * kHotLdsStride + 32);
-    const float s0 = S * (1.0f / 64.0f);   // S * 2^-27 * 2^21
-    sc[0] = s0;
-    sc[1] = s0 * (1.0f / 128.0f);
-    sc[2] = s0 * (1.0f / 16384.0f);
-    sc[3] = s0 * (1.0f / 2097152.0f);
-  }
-}
-
-__device__ __forceinline__ float sgpr_f(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
 }
 
 // wctr: the workgroup's LDS chunk counter, zeroed by hyb_lds_init.
 // TIERED: the chunk's far entries (p.fslot list, weights from global memory)
-// join the row dots through the per-wave LDS row sums fdot, and every row's
-// residual goes to d.rbuf for the far backward (k_far_grad).
+// join the row dots through the per-wave LDS row sums fdot (int32), and every
+// row's residual goes to d.rbuf for the far backward (k_far_grad).
 template <bool STATS, bool SAMPLE, int REP, bool TIERED>
 __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, const SgdParams& sp,
-                                         const float* wl, unsigned long long* gl, const uint32_t* whl,
-                                         float (*hsum)[kHot], double (*wsc)[kPartVals], double* prow,
-                                         uint32_t* wctr, float (*fdot)[kRowsPerChunk], uint64_t* tst = nullptr) {
+                                         const LaneScale& sc, const int32_t* wl, unsigned long long* gl,
+                                         const uint32_t* whl, unsigned long long* hsum,
+                                         int64_t (*wsc)[kPartVals], int64_t* prow, uint32_t* wctr,
+                                         int32_t (*fdot)[kRowsPerChunk], uint64_t* tst = nullptr) {
   const int64_t ns = d.nl;
   const int lane = lane_id();
   const int w = __builtin_amdgcn_readfirstlane(int(threadIdx.x) / kWave);   // wave-uniform
   const int r = lane / kLanesPerRow, t = lane % kLanesPerRow;
   const int rep = lane % REP;
   const int64_t n_kept = p.counters[0];
-  const int64_t nch = sp.ablate % 10 == 7 ? 0 : (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;  // 7: fixed cost
+  const int64_t nch = sp.ablate == 7 ? 0 : (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;  // 7: fixed cost
   const uint16_t* slot = static_cast<const uint16_t*>(p.slot);
   const uint4* hdense = reinterpret_cast<const uint4*>(p.hot_dense);
   const int32_t* __restrict__ clen8c = p.clen8c;
   const int64_t* __restrict__ cbase = p.cbase;
-  // the 4 numeric-feature weights are wave-uniform: SGPRs, not 4 VGPRs (the
-  // chunk loop sits at the 128-VGPR limit of 1024-thread workgroups)
-  const float w0 = sgpr_f(wl[0]), w1 = sgpr_f(wl[1]), w2 = sgpr_f(wl[2]), w3 = sgpr_f(wl[3]);
   const uint32_t* wq = whl + t * kHotLdsStride;
-  f32x2 gh[kHotPerLane / 2];
+  int32_t gh[kHotPerLane];
 #pragma unroll
-  for (int i = 0; i < kHotPerLane / 2; ++i) gh[i] = f32x2{0.f, 0.f};
+  for (int i = 0; i < kHotPerLane; ++i) gh[i] = 0;
   RowAcc acc;
-  bool clamped = false;
 
   // Dynamic chunk assignment inside the workgroup: workgroup b owns chunks
   // b, b + G, b + 2G, ... and its waves take the next one from an LDS
@@ -534,7 +676,7 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
     if (lane == 0) j = atomicAdd(wctr, 1u);
     return int64_t(__builtin_amdgcn_readfirstlane(__shfl(int(j), 0, kWave)));
   };
-  int k = 0;   // chunks this wave took
+  int k = 0;          // chunks this wave took
   int64_t j = grab();
   int32_t L8n = 0, fcn = 0;
   int64_t cbn = 0;
@@ -543,7 +685,10 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
     cbn = cbase[b + j * G];
     if (TIERED) fcn = p.fcount[b + j * G];
   }
+  // epochs of at most kHotFlush chunks: each lane adds <= kHotFlush rows
+  // into its int32 accumulators before they are folded into the int64 row
   while (j < nj) {
+  for (int e = 0; e < kHotFlush && j < nj; ++e) {
     const int64_t c = b + j * G;
     const int32_t L8c = L8n, fc = fcn;
     const int64_t cb = cbn;
@@ -556,18 +701,18 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
     }
     const int64_t pos = c * kRowsPerChunk + r;
     const int64_t off = cb * kChunkStride + lane * kGroup;
-    const RowIn ri = row_in(p, pos);
+    const RowIn ri = row_in(p, pos, t);
     // far entries of the chunk: their row sums land in lane t == 0 of the row
-    float far = 0.f;
+    int32_t far = 0;
     if (TIERED && fc > 0 && abl != 8) {   // wave-uniform (ablate 8: no far forward)
-      float* fd = fdot[w];
-      if (lane < kRowsPerChunk) fd[lane] = 0.f;
+      int32_t* fd = fdot[w];
+      if (lane < kRowsPerChunk) fd[lane] = 0;
       wave_lds_sync();
       const uint32_t* fl = p.fslot + cb * kChunkStride;
       for (int32_t k0 = 0; k0 < fc; k0 += kWave)
         if (k0 + lane < fc) {
           const uint32_t e = fl[k0 + lane];
-          atomicAdd(&fd[e >> 28], d.wc32[e & 0x0FFFFFFFu]);
+          atomicAdd(&fd[e >> 28], w_to_fix(d.wc32[e & 0x0FFFFFFFu], sc.wscale));   // ds_add_u32: exact
         }
       wave_lds_sync();
       if (t == 0) far = fd[r];
@@ -583,18 +728,7 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
         for (int g = 0; g < kMaxColdGroups; ++g)
           if (g < L8c) v[g] = *reinterpret_cast<const uint2*>(sl + int64_t(g) * kColdStride);
       }
-      if (abl == 6) {  // loads only: memory floor of the chunk stream
-        uint32_t x = hv.x ^ hv.y ^ hv.z ^ hv.w ^ __float_as_uint(ri.y + ri.n0 + ri.n1 + ri.n2 + ri.n3);
-        if (reg) {
-#pragma unroll
-          for (int g = 0; g < kMaxColdGroups; ++g)
-            if (g < L8c) x ^= v[g].x ^ v[g].y;
-        }
-        acc.loss += float(x & 1u);
-        continue;
-      }
-      // ablate 4: no hot dot (counts still loaded)
-      float d0 = abl == 4 ? __uint_as_float(hv.x & 1u) : hot_dot(hv, wq), d1 = far;
+      int32_t d0 = hot_dot(hv, wq), d1 = far;   // partial sums of the row's int32 dot
       if (reg) {
 #pragma unroll
         for (int g = 0; g < kMaxColdGroups; ++g)
@@ -612,19 +746,15 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
           d1 += wl[s[1]] + wl[s[3]];
         }
       }
-      float dot = d0 + d1;
-      dot += __shfl_xor(dot, 1, kWave);
-      dot += __shfl_xor(dot, 2, kWave);
-      const float res = row_residual<STATS, SAMPLE>(dot, ri, pos, t, d, p, sp, n_kept, w0, w1, w2, w3, acc);
+      const int32_t dot = row_total(d0 + d1);
+      const float res = row_residual<STATS, SAMPLE>(dot, ri, pos, t, d, p, sp, n_kept, sc, acc);
       if (TIERED && t == 0) d.rbuf[pos] = res;
+      const int32_t q = __float2int_rn(res * sc.qscale);
+      // unconditional (q = 0 adds nothing): the accumulators then need no
+      // second register set for a skipped update
+      hot_grad(hv, q, gh);
       if (res != 0.f) {
-        // opaque copy: re-extract the counts instead of keeping 32 converted
-        // floats live across the residual (register pressure)
-        uint4 hg = hv;
-        asm volatile("" : "+v"(hg.x), "+v"(hg.y), "+v"(hg.z), "+v"(hg.w));
-        if (abl != 1 && abl != 3) hot_grad(hg, res, gh);   // ablate 3: no hot grad
-        if (abl == 1 || abl == 5) continue;                 // 1/5: no cold scatter
-        const unsigned long long q = to_fix(res, clamped, sp.fix_lim);
+        const unsigned long long qq = (unsigned long long)(long long)q;
         if (reg) {
 #pragma unroll
           for (int g = 0; g < kMaxColdGroups; ++g)
@@ -632,41 +762,42 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
               uint32_t s[4];
               unpack4(v[g], s);
 #pragma unroll
-              for (int e = 0; e < 4; ++e) atomicAdd(&gl[s[e] * REP + rep], q);
+              for (int e = 0; e < 4; ++e) atomicAdd(&gl[s[e] * REP + rep], qq);
             }
         } else {
           for (int32_t g = 0; g < L8c; ++g) {
             uint32_t s[4];
             unpack4(*reinterpret_cast<const uint2*>(sl + int64_t(g) * kColdStride), s);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) atomicAdd(&gl[s[e] * REP + rep], q);
+            for (int e = 0; e < 4; ++e) atomicAdd(&gl[s[e] * REP + rep], qq);
           }
         }
       }
     } else {  // plain layout: every entry (hot ones too) through the LDS gradient
       const int32_t L8 = p.clen8[c];
       const uint16_t* sl = slot + off;
-      float dot = far;
+      int32_t dot = far;
       for (int32_t g = 0; g < L8; ++g) {
         uint32_t s[8];
         unpack8(*reinterpret_cast<const uint4*>(sl + int64_t(g) * kChunkStride), s);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) dot += wl[s[k]];
+        for (int e = 0; e < 8; ++e) dot += wl[s[e]];
       }
-      dot += __shfl_xor(dot, 1, kWave);
-      dot += __shfl_xor(dot, 2, kWave);
-      const float res = row_residual<STATS, SAMPLE>(dot, ri, pos, t, d, p, sp, n_kept, w0, w1, w2, w3, acc);
+      dot = row_total(dot);
+      const float res = row_residual<STATS, SAMPLE>(dot, ri, pos, t, d, p, sp, n_kept, sc, acc);
       if (TIERED && t == 0) d.rbuf[pos] = res;
       if (res != 0.f) {
-        const unsigned long long q = to_fix(res, clamped, sp.fix_lim);
+        const unsigned long long q = (unsigned long long)(long long)__float2int_rn(res * sc.qscale);
         for (int32_t g = 0; g < L8; ++g) {
           uint32_t s[8];
           unpack8(*reinterpret_cast<const uint4*>(sl + int64_t(g) * kChunkStride), s);
 #pragma unroll
-          for (int k = 0; k < 8; ++k) atomicAdd(&gl[s[k] * REP + rep], q);
+          for (int e = 0; e < 8; ++e) atomicAdd(&gl[s[e] * REP + rep], q);
         }
       }
     }
+  }
+  hot_flush(gh, acc, hsum);
   }
 
   if (tst) tst[3] = __builtin_amdgcn_s_memrealtime();
@@ -675,49 +806,34 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
     we[0] = __builtin_amdgcn_s_memrealtime();
     we[1] = uint64_t(k);
   }
-  if (__any(clamped) && lane == 0) d.state[7] = 1.0;
-  // hot gradient: sum the 16 lanes of each quarter t (per wave), into LDS
-  // per 16-lane row (DPP), the four row partials of each hot id go to LDS
-  // and the slot loop adds the 4 x 16 of them
-  float* hrow = hsum[w];
-#pragma unroll
-  for (int i = 0; i < kHotPerLane; ++i) {
-    float v = row_sum_mod4((i & 1) ? gh[i >> 1].y : gh[i >> 1].x);
-    v += __shfl_xor(v, 16, kWave);   // the wave's four 16-lane rows
-    v += __shfl_xor(v, 32, kWave);
-    if (lane < kLanesPerRow) hrow[kHotPerLane * lane + i] = v;
-  }
   if (tst) tst[4] = __builtin_amdgcn_s_memrealtime();
-  part_scalars<STATS, SAMPLE>(d, acc, wsc, prow);   // includes the block barrier
+  __syncthreads();   // every wave's hsum adds
+  part_scalars<STATS>(d, 0, 0, acc, hsum + kHot, wsc, prow);   // includes the block barrier
   if (tst) tst[5] = __builtin_amdgcn_s_memrealtime();
-  const int64_t hi = d.far_base;                    // pads (and far slots) are never flushed
+  const int64_t hi = d.far_base;            // pads (and far slots) are never flushed
   for (int64_t s = kNumNumeric + threadIdx.x; s < ns; s += kIterBlock) {
-    double v = 0.0;
+    int64_t v = 0;
     if (s < hi) {
       v = part_slot<REP>(gl, s);
       const uint32_t h = p.hot_of[s];
-      if (h != 0xFFu) {
-        double hv = 0.0;
-        for (int k = 0; k < kIterBlock / kWave; ++k) hv += double(hsum[k][h]);
-        v += hv;
-      }
+      if (h != 0xFFu) v += (long long)hsum[h];
     }
     prow[s] = v;
   }
 }
 
-
-// Weights -> LDS (fp32 compact weights, hot weights in hot order) and a
-// zeroed fixed-point gradient; ends with a block barrier.
-
-// Slots >= hi (pads) get weight 0 whatever wsrc holds there.
+// Weights -> LDS (int32 fixed point; slots >= hi, the pads, get 0), a
+// zeroed int64 gradient and hot row, the hot digit table; ends with a block
+// barrier.
 template <int REP>
-__device__ __forceinline__ void hyb_lds_init(const DevPrepared& p, const float* wsrc, int64_t ns,
-                                             int64_t hi, float* wl, unsigned long long* gl, uint32_t* whl,
-                                             uint32_t* wctr) {
+__device__ __forceinline__ void hyb_lds_init(const DevPrepared& p, const float* wsrc, int64_t ns, int64_t hi,
+                                             float wscale, int32_t* wl, unsigned long long* gl,
+                                             uint32_t* whl, unsigned long long* hsum, uint32_t* wctr) {
   if (threadIdx.x == 0) *wctr = 0u;
-  for (int64_t s = threadIdx.x; s < ns; s += kIterBlock) wl[s] = s < hi ? wsrc[s] : 0.f;
+  for (int64_t s = threadIdx.x; s < ns; s += kIterBlock)
+    wl[s] = (s >= kNumNumeric && s < hi) ? w_to_fix(wsrc[s], wscale) : 0;
   for (int64_t s = threadIdx.x; s < ns * REP; s += kIterBlock) gl[s] = 0ull;
+  for (int s = threadIdx.x; s < kHot + 8; s += kIterBlock) hsum[s] = 0ull;
   __syncthreads();
   if (threadIdx.x < kWave) hot_digits(p, wl, whl);
   __syncthreads();
@@ -725,31 +841,33 @@ __device__ __forceinline__ void hyb_lds_init(const DevPrepared& p, const float* 
 
 template <bool STATS, bool SAMPLE, int REP, bool TIERED>
 __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_hyb(DevSgd d, DevPrepared p, SgdParams sp) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  __shared__ double wsc[kIterBlock / kWave][kPartVals];
-  __shared__ float hsum[kIterBlock / kWave][kHot];
-  __shared__ float fdot[TIERED ? kIterBlock / kWave : 1][kRowsPerChunk];
+  extern __shared__ __attribute__((aligned(16))) int32_t lds[];
+  __shared__ int64_t wsc[kIterBlock / kWave][kPartVals];
+  __shared__ unsigned long long hsum[kHot + 8];
+  __shared__ int32_t fdot[TIERED ? kIterBlock / kWave : 1][kRowsPerChunk];
   __shared__ __attribute__((aligned(16))) uint32_t whl[kLanesPerRow * kHotLdsStride];
   __shared__ int stop_flag;
   __shared__ uint32_t wctr;
+  __shared__ IterScale scs;
   uint64_t* tst = nullptr;
   if (d.tdbg && threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1))
     tst = d.tdbg + (int64_t(sp.iteration) * 2 + (blockIdx.x == 0 ? 0 : 1)) * 8;
   if (tst) tst[0] = __builtin_amdgcn_s_memrealtime();
-  if (sgd_stop(d, sp, &stop_flag)) return;
+  if (sgd_prologue(d, sp, &stop_flag, &scs)) return;
+  const LaneScale sc = lane_scale(scs, d, lane_id() % kLanesPerRow);
   if (tst) tst[1] = __builtin_amdgcn_s_memrealtime();
-  float* wl = lds;
+  int32_t* wl = lds;
   unsigned long long* gl = reinterpret_cast<unsigned long long*>(lds + d.nl);
-  hyb_lds_init<REP>(p, d.wc32, d.nl, d.far_base, wl, gl, whl, &wctr);
+  hyb_lds_init<REP>(p, d.wc32, d.nl, d.far_base, sc.wscale, wl, gl, whl, hsum, &wctr);
   if (tst) tst[2] = __builtin_amdgcn_s_memrealtime();
-  hyb_pass<STATS, SAMPLE, REP, TIERED>(d, p, sp, wl, gl, whl, hsum, wsc, d.part + int64_t(blockIdx.x) * d.pstride,
-                                       &wctr, fdot, tst);
+  hyb_pass<STATS, SAMPLE, REP, TIERED>(d, p, sp, sc, wl, gl, whl, hsum, wsc,
+                                       d.part + int64_t(blockIdx.x) * d.pstride, &wctr, fdot, tst);
   if (tst) tst[6] = __builtin_amdgcn_s_memrealtime();
 }
 
 // LDS bytes of the fast path for a given replication factor.
 static int64_t lds_bytes(int64_t ns, int rep) {
-  return ns * int64_t(sizeof(float)) + ns * rep * int64_t(sizeof(unsigned long long));
+  return ns * int64_t(sizeof(int32_t)) + ns * rep * int64_t(sizeof(unsigned long long));
 }
 
 // Replication factor for the LDS gradient (0 = does not fit -> global path).
@@ -778,11 +896,11 @@ int sgd_lds_rep(int64_t ns) {
 
 bool sgd_hybrid_fits(int64_t ns) {
   const int rep = sgd_lds_rep(ns);
-  // static LDS of k_sgd_iter_hyb<.., TIERED>: wsc, hsum, fdot per wave + whl, flags
+  // static LDS of k_sgd_iter_hyb<.., TIERED>: wsc, fdot per wave + hot row, whl, scales, flags
   const int64_t statics = int64_t(kIterBlock / kWave) *
-                              (kPartVals * int64_t(sizeof(double)) + kHot * int64_t(sizeof(float)) +
-                               kRowsPerChunk * int64_t(sizeof(float))) +
-                          kLanesPerRow * kHotLdsStride * int64_t(sizeof(uint32_t)) + 64;
+                              (kPartVals * int64_t(sizeof(int64_t)) + kRowsPerChunk * int64_t(sizeof(int32_t))) +
+                          (kHot + 8) * int64_t(sizeof(int64_t)) +
+                          kLanesPerRow * kHotLdsStride * int64_t(sizeof(uint32_t)) + int64_t(sizeof(IterScale)) + 64;
   return ns <= kMaxHybridSlots && rep > 0 && lds_bytes(ns, rep) + statics <= 160 * 1024 - 1024;
 }
 
@@ -872,22 +990,26 @@ int sgd_partials(int64_t ns, bool u16, int grid) {
 //
 //   k_sgd_iter_*  (iteration i)  prologue: converged after update i-1?  ->
 //                 every workgroup decides from record i-1 (fixed-order sums,
-//                 so all workgroups -- and all DP ranks -- agree); workgroup
-//                 0 publishes state[0..1] and the host flag.  Then one
-//                 partial gradient row per workgroup.
-//   [k_sgd_reduce + RCCL all-reduce of g64 when DP; the verdict on update
-//    i-1 rides along in g64[nl + 1] -- rank 0's, so the all-reduced value is
-//    exact and the same on every rank whatever the backend's summation
-//    order -- and k_sgd_update i acts on it: no update, state[0..1] and the
-//    host flag.  Each rank skips the gradient pass of iteration i on its own
-//    verdict (state[8]; identical weights -> the same verdict everywhere)
-//    and then contributes zeros, but only the agreed verdict ends the loop,
-//    so ranks can never disagree on the iteration count (a mismatch would
-//    pair unequal collectives).]
+//                 so all workgroups -- and all DP ranks -- agree) and derives
+//                 iteration i's fixed-point scales; workgroup 0 records them
+//                 and publishes state[0..1] and the host flag.  Then one int64
+//                 partial row per workgroup.
+//   k_far_grad    (tiered) far slots' int64 sums into gacc[far_off ..].
+//   [DP: k_sgd_reduce sums the partial rows into gacc[0, nl + 2), adds rank
+//    0's verdict on update i-1 and this rank's ready word to the tail, and
+//    ONE int64 all-reduce covers the whole packed buffer (near columns, loss,
+//    sampled m, verdict, ready words, far slots): integer sums, so the
+//    result is exact and the same on every rank whatever the backend's
+//    summation order.  k_sgd_update i acts on the agreed verdict.  Each rank
+//    skips the gradient pass of iteration i on its own verdict (state[8];
+//    identical weights -> the same verdict everywhere) and then contributes
+//    zeros, but only the agreed verdict ends the loop, so ranks can never
+//    disagree on the iteration count (a mismatch would pair unequal
+//    collectives).]
 //   k_sgd_update  (iteration i)  multi-workgroup: sums the partial rows of
-//                 64 columns (world 1) or reads the all-reduced g64,
-//                 SimpleUpdater on them, per-workgroup ||dw||^2, ||w||^2
-//                 into record i.
+//                 64 columns (world 1) or reads the all-reduced gacc,
+//                 SimpleUpdater on them, per-workgroup ||dw||^2, ||w||^2,
+//                 max |w_text| into record i.
 //   k_sgd_finish  after the loop: convergence of the last update.
 //
 // MLlib semantics: the update of iteration i is applied, then
@@ -900,134 +1022,175 @@ int sgd_partials(int64_t ns, bool u16, int grid) {
 // block of 64 columns: lane l owns column col0 + l, the 16 waves of the
 // workgroup take partial rows w, w + 16, ... (each load one coalesced 512-B
 // row segment, all of a wave's rows in flight), and wave 0 adds the 16 wave
-// sums in a fixed order -- deterministic, like every reduction here.  (The
-// previous one-wave-per-column form read each column with 64 scattered
-// 8-B loads: 20 us per iteration at 12.5K slots x 256 partial rows.)
-// nparts > 0: the column gradients are the sums of the partial rows (single
-// GPU); nparts == 0: g64 holds them (all-reduced, or the generic path).
+// sums -- int64 (exact) for the fixed-point columns, fp64 in a fixed order
+// for the batch-stat columns.
+// nparts > 0: the column sums come from the partial rows (single GPU);
+// nparts == 0: gacc holds them (all-reduced).
 // ---------------------------------------------------------------------------
 constexpr int kUpdWaves = 1024 / kWave;   // waves per workgroup (partial-row split)
 
 // Sum of partial rows for columns [col0, col0 + 64): returns lane's column
-// sum in wave 0 (other waves: 0).  Contains a block barrier.
-__device__ __forceinline__ double part_block_sum(const DevSgd& d, int64_t col0, int64_t ncols, int nparts,
-                                                 double (*red)[kWave]) {
+// sum in wave 0 (other waves: 0); columns >= dcol0 are fp64 (bits returned).
+// Contains a block barrier.
+__device__ __forceinline__ int64_t part_block_sum(const DevSgd& d, int64_t col0, int64_t ncols, int64_t dcol0,
+                                                  int nparts, int64_t (*red)[kWave]) {
   const int lane = lane_id(), w = threadIdx.x / kWave;
   const int64_t col = col0 + lane;
-  double acc = 0.0;
+  const bool dbl = col >= dcol0;
+  int64_t acc = 0;
+  double accd = 0.0;
   if (col < ncols) {
-    const double* src = d.part + col;
+    const int64_t* src = d.part + col;
     const int64_t ps = d.pstride;
+    if (!dbl) {
 #pragma unroll 8
-    for (int g = w; g < nparts; g += kUpdWaves) acc += src[int64_t(g) * ps];
+      for (int g = w; g < nparts; g += kUpdWaves) acc += src[int64_t(g) * ps];
+    } else {
+      for (int g = w; g < nparts; g += kUpdWaves) accd += __builtin_bit_cast(double, src[int64_t(g) * ps]);
+      acc = __builtin_bit_cast(int64_t, accd);
+    }
   }
   red[w][lane] = acc;
   __syncthreads();
-  double t = 0.0;
+  int64_t t = 0;
   if (w == 0) {
+    if (!dbl) {
 #pragma unroll
-    for (int k = 0; k < kUpdWaves; ++k) t += red[k][lane];
+      for (int k = 0; k < kUpdWaves; ++k) t += red[k][lane];
+    } else {
+      double td = 0.0;
+      for (int k = 0; k < kUpdWaves; ++k) td += __builtin_bit_cast(double, red[k][lane]);
+      t = __builtin_bit_cast(int64_t, td);
+    }
   }
   __syncthreads();   // red is reused by the next column block
   return t;
 }
 
+// Host flag of update it-1 (zero-copy): stop bit, DP "every rank's next
+// batch is locally prepared" bit, and the largest ready active-set size.
+__device__ __forceinline__ double flag_word(bool stop, bool all_ready, int64_t max_u) {
+  return double(stop ? 1 : 0) + 2.0 * double(all_ready ? 1 : 0) + 4.0 * double(max_u);
+}
+
 __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int nparts) {
-  __shared__ double wsc[kUpdWaves][2];
-  __shared__ double red[kUpdWaves][kWave];
+  __shared__ double wsc[kUpdWaves][3];
+  __shared__ int64_t red[kUpdWaves][kWave];
   __shared__ double m_sh;
   const int tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
   const int it = sp.iteration;
-  if (sp.dp && it > 1) {   // the agreed verdict on update it - 1 (checked before state[0]:
-                           // block 0 sets it below while other blocks may still start)
-    const bool stop = d.g64[d.nl + 1] > 0.5;
-    if (blockIdx.x == 0 && tid == 0 && d.host_flags)
-      __hip_atomic_store(&d.host_flags[it - 1], stop ? 1.0 : 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const int64_t ns = d.nl, hi = d.far_base;   // partial-row columns; near text slots end at far_base
+  int64_t* tail = d.gacc + ns;
+  const int64_t n_far = kNumNumeric + d.n_unique - d.far_base;
+  int64_t* gfar = d.gacc + d.far_off;
+  if (sp.dp) {
+    // the agreed verdict on update it - 1 (checked before state[0]: block 0
+    // sets it below while other blocks may still start), and the ready words
+    const bool stop = it > 1 && tail[kTailVerdict] != 0;
+    if (blockIdx.x == 0 && tid == 0 && d.host_flags) {
+      bool all = true;
+      int64_t mx = 0;
+      for (int r = 0; r < d.world; ++r) {
+        const int64_t v = tail[kTailReady + r];
+        all = all && v > 0;
+        mx = v - 1 > mx ? v - 1 : mx;
+      }
+      __hip_atomic_store(&d.host_flags[it - 1], flag_word(stop, all, mx), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     if (stop) {
-      const int64_t n_far = kNumNumeric + d.n_unique - d.far_base;   // this pass's far sums are dropped
       for (int64_t j = int64_t(blockIdx.x) * 1024 + tid; j < n_far; j += int64_t(gridDim.x) * 1024)
-        d.gfix[j] = 0ull;
+        gfar[j] = 0;   // this pass's far sums are dropped
       if (blockIdx.x == 0 && tid == 0) {
         d.state[0] = 1.0;
-        d.state[1] = 1.0;
+        if (d.state[7] == 0.0) d.state[1] = 1.0;
       }
       return;
     }
   }
   if (d.state[0] != 0.0) return;
-  const int64_t ns = d.nl, hi = d.far_base;   // partial-row columns; near text slots end at far_base
+  const double* rec_it = sgd_rec(d, it);
+  const int sS = int(rec_it[kRecS]), sL = int(rec_it[kRecL]);
   const int64_t ncols = ns + kPartVals - kNumNumeric;
   // m: global kept rows, or the sampled row count of this iteration
   if (tid < kWave) {
     double m = d.state[5];
     if (sp.sample) {
-      m = *sgd_red_m(d, it);
+      int64_t t = 0;
       if (nparts > 0) {
-        double t = 0.0;
-        for (int g = tid; g < nparts; g += kWave) t += d.part[int64_t(g) * d.pstride + ns + 1];   // ns = nl
-        m += wave_sum(t);
+        for (int g = tid; g < nparts; g += kWave) t += d.part[int64_t(g) * d.pstride + ns + 1];
+        t = wave_sum_i64(t);
+      } else {
+        t = tail[kTailM];
       }
+      m = double(t);
     }
     if (tid == 0) m_sh = m;
   }
   __syncthreads();
   const double m = m_sh;
   const double alpha = sp.step_size / sqrt(double(it));
-  double ds = 0.0, ws = 0.0;
+  const double gsc = ldexp(1.0, -sS);
+  double ds = 0.0, ws = 0.0, mx = 0.0;
   for (int64_t col0 = int64_t(blockIdx.x) * kWave; col0 < ncols; col0 += int64_t(gridDim.x) * kWave) {
-    const double gp = nparts > 0 ? part_block_sum(d, col0, ncols, nparts, red) : 0.0;
+    const int64_t gp = nparts > 0 ? part_block_sum(d, col0, ncols, ns + 2, nparts, red) : 0;
     const int64_t col = col0 + lane;
     if (w == 0 && col < ncols) {
-      const double g = (col <= ns ? d.g64[col] : 0.0) + gp;
+      const int64_t gi = (nparts > 0 ? gp : (col <= ns + 1 ? d.gacc[col] : 0));
       if (col < hi) {
+        double wn = d.wc64[col];
         if (m > 0.0) {
+          const double g = double(gi) * (col < kNumNumeric ? ldexp(1.0, -int(rec_it[kRecN + col])) : gsc);
           const double step = alpha * (g / m);
-          const double wn = d.wc64[col] - step;
+          wn -= step;
           d.wc64[col] = wn;
           d.wc32[col] = float(wn);
           ds += step * step;
           ws += wn * wn;
         }
-        d.g64[col] = 0.0;
+        if (col >= kNumNumeric) mx = fmax(mx, fabs(double(float(wn))));   // the next iteration's weight scale
       } else if (col == ns) {
-        if (m > 0.0) d.loss_hist[it] = g / m;
-        d.g64[ns] = 0.0;
+        if (m > 0.0) d.loss_hist[it] = 0.5 * double(gi) * ldexp(1.0, -sL) / m;
       } else if (col >= ns + 2 && nparts > 0) {
-        d.stats[col - ns - 2] += g;     // batch stats (iteration 1, single GPU)
+        d.stats[col - ns - 2] += __builtin_bit_cast(double, gp);   // batch stats (iteration 1, single GPU)
       }
     }
   }
   // tiered: far slots [far_base, 4 + n_unique), one thread per slot, from
   // the fixed-point far gradient (k_far_grad / all-reduced), re-zeroed here
-  const int64_t n_far = kNumNumeric + d.n_unique - d.far_base;
   if (n_far > 0) {
-    const double inv_m = m > 0.0 ? 1.0 / m : 0.0;
     for (int64_t j = int64_t(blockIdx.x) * 1024 + tid; j < n_far; j += int64_t(gridDim.x) * 1024) {
-      const double g = double((long long)d.gfix[j]) * kFarInv;
-      d.gfix[j] = 0ull;
+      const double g = double(gfar[j]) * gsc;
+      gfar[j] = 0;
+      const int64_t col = d.far_base + j;
+      double wn = d.wc64[col];
       if (m > 0.0) {
-        const int64_t col = d.far_base + j;
-        const double step = alpha * (g * inv_m);
-        const double wn = d.wc64[col] - step;
+        // the near columns' formula bit for bit: which tier a slot lands in
+        // depends on sampled counts (row placement), its update must not
+        const double step = alpha * (g / m);
+        wn -= step;
         d.wc64[col] = wn;
         d.wc32[col] = float(wn);
         ds += step * step;
         ws += wn * wn;
       }
+      mx = fmax(mx, fabs(double(float(wn))));
     }
   }
   ds = wave_sum(ds);   // fixed order within the wave, then across waves
   ws = wave_sum(ws);
+  mx = wave_max(mx);
   if (lane == 0) {
     wsc[w][0] = ds;
     wsc[w][1] = ws;
+    wsc[w][2] = mx;
   }
   __syncthreads();
-  double* rec = sgd_rec(d, it);
-  if (tid < 2) {
+  double* rec = sgd_rec(d, it);   // (= rec_it)
+  if (tid < 3) {
     double t = 0.0;
-    for (int k = 0; k < kUpdWaves; ++k) t += wsc[k][tid];
-    rec[kRecHead + 2 * blockIdx.x + tid] = t;
+    for (int k = 0; k < kUpdWaves; ++k) t = tid < 2 ? t + wsc[k][tid] : fmax(t, wsc[k][tid]);
+    rec[kRecHead + 3 * blockIdx.x + tid] = t;
   }
   if (blockIdx.x == 0 && tid == 0) {
     const double nupd = (it > 1 ? sgd_rec(d, it - 1)[0] : 0.0) + (m > 0.0 ? 1.0 : 0.0);
@@ -1036,7 +1199,6 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
     rec[2] = double(gridDim.x);
     d.state[2] = nupd;
     d.state[3] = double(it);
-    *sgd_red_m(d, it + 1) = 0.0;      // the next iteration's sampled count accumulates from 0
   }
 }
 
@@ -1047,35 +1209,41 @@ void launch_sgd_update(const DevSgd& d, const SgdParams& sp, int nparts, hipStre
   hipLaunchKernelGGL(k_sgd_update, dim3(grid), dim3(1024), 0, s, d, sp, nparts);
 }
 
-// Cross-workgroup reduction of the partial rows (DP: before the all-reduce)
-// into g64 (+ loss, sampled count, batch stats): 64 columns per workgroup,
-// fixed summation order.
+// DP: cross-workgroup reduction of the partial rows into the packed buffer
+// gacc[0, nl + 2) (slots, loss, sampled count; the batch stats add into
+// d.stats), rank 0's verdict on update i-1 and this rank's ready word into
+// the tail -- all of it int64, ahead of the one all-reduce per iteration.
 __global__ __launch_bounds__(1024) void k_sgd_reduce(DevSgd d, SgdParams sp) {
-  __shared__ double red[kUpdWaves][kWave];
+  __shared__ int64_t red[kUpdWaves][kWave];
   if (d.state[0] != 0.0) return;
-  // DP pass skipped on this rank's verdict: its partial rows are stale, it
-  // contributes zeros
+  // pass skipped on this rank's verdict: its partial rows are stale, it contributes zeros
   const bool skipped = d.state[8] == double(sp.iteration);
+  const int64_t nl = d.nl;
   if (d.nparts > 0) {
-    const int64_t ncols = d.nl + kPartVals - kNumNumeric;
+    const int64_t ncols = nl + kPartVals - kNumNumeric;
     const int64_t col0 = int64_t(blockIdx.x) * kWave;
-    const double v = skipped ? 0.0 : part_block_sum(d, col0, ncols, d.nparts, red);
+    const int64_t v = skipped ? 0 : part_block_sum(d, col0, ncols, nl + 2, d.nparts, red);
     const int64_t col = col0 + lane_id();
     if (threadIdx.x < kWave && col < ncols) {
-      if (col <= d.nl) d.g64[col] = v;                     // slots, then the loss at [nl]
-      else if (col == d.nl + 1) *sgd_red_m(d, sp.iteration) = v;   // sampled row count
-      else d.stats[col - d.nl - 2] += v;                   // batch stats (iteration 1)
+      if (col <= nl + 1) d.gacc[col] = v;                                  // slots, loss, sampled count
+      else if (!skipped) d.stats[col - nl - 2] += __builtin_bit_cast(double, v);   // batch stats (iteration 1)
     }
   }
-  // DP: rank 0's verdict on update i-1 -> g64[nl + 1] (all-reduced with the gradient)
-  if (sp.dp && blockIdx.x == 0 && threadIdx.x < kWave) {
+  if (blockIdx.x == 0 && threadIdx.x < kWave) {
+    // rank 0's verdict on update i-1 (converged, or this iteration's scales invalid)
     const bool conv = sp.iteration > 1 && sgd_converged_wave(d, sp.iteration - 1, sp.tol);
-    if (threadIdx.x == 0) d.g64[d.nl + 1] = (conv && sp.rank0) ? 1.0 : 0.0;
+    const bool bad = sgd_rec(d, sp.iteration)[kRecBad] != 0.0;
+    int64_t* tail = d.gacc + nl;
+    if (threadIdx.x == 0) tail[kTailVerdict] = ((conv || bad) && sp.rank0) ? 1 : 0;
+    for (int r = threadIdx.x; r < d.tail_len - kTailReady; r += kWave)
+      tail[kTailReady + r] = (r == d.rank && d.ready_word)
+                                 ? int64_t(__hip_atomic_load(const_cast<int64_t*>(d.ready_word), __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_SYSTEM))
+                                 : 0;
   }
 }
 
 void launch_sgd_reduce(const DevSgd& d, const SgdParams& sp, hipStream_t s) {
-  if (d.nparts <= 0 && !sp.dp) return;
   const int grid = d.nparts > 0 ? int((d.nl + kPartVals - kNumNumeric + kWave - 1) / kWave) : 1;
   hipLaunchKernelGGL(k_sgd_reduce, dim3(grid), dim3(1024), 0, s, d, sp);
 }
@@ -1098,13 +1266,13 @@ void launch_sgd_finish(const DevSgd& d, const SgdParams& sp, hipStream_t s) {
 
 // ---------------------------------------------------------------------------
 // Far backward (tiered layout): the CSC lists every far entry grouped by
-// slot; lane e of the grid takes entry e, converts its row's residual to the
-// 2^-16 fixed point (kFarScale), and a segmented inclusive scan over
-// the wave (segments = runs of equal slot) leaves each run's sum in its last
-// lane, which adds it to gfix[slot - far_base] with one 64-bit integer
-// atomic.  Integer sums are exact, so the result does not depend on the
-// order of entries inside a slot or on which wave adds first: no per-entry
-// float atomics, deterministic across runs and DP ranks.
+// slot; lane e of the grid takes entry e, converts its row's residual to
+// the iteration's 2^S fixed point (the same q as the LDS tier), and a
+// segmented inclusive scan over the wave (segments = runs of equal slot)
+// leaves each run's sum in its last lane, which adds it to the packed
+// buffer's far part with one 64-bit integer atomic.  Integer sums are exact,
+// so the result does not depend on the order of entries inside a slot or on
+// which wave adds first: deterministic across runs and DP ranks.
 // ---------------------------------------------------------------------------
 template <int CTRL, int ROWS>
 __device__ __forceinline__ uint32_t dpp_u32(uint32_t old, uint32_t v) {
@@ -1124,21 +1292,14 @@ __global__ __launch_bounds__(256) void k_far_grad(DevSgd d, SgdParams sp) {
   if (d.state[0] != 0.0 || d.state[8] == double(sp.iteration)) return;   // done / DP pass skipped
   const int64_t n = *d.far_n;
   const int lane = lane_id();
-  bool clamped = false;
+  const float qscale = ldexpf(1.f, int(sgd_rec(d, sp.iteration)[kRecS]));
+  unsigned long long* gfar = reinterpret_cast<unsigned long long*>(d.gacc + d.far_off);
   const int64_t stride = int64_t(gridDim.x) * 256;
   for (int64_t e0 = int64_t(blockIdx.x) * 256 + (threadIdx.x & ~(kWave - 1)); e0 < n; e0 += stride) {
     const int64_t e = e0 + lane;
     const bool valid = e < n;
     uint32_t sl = valid ? d.fcsc_slot[e] : 0xFFFFFFFFu;
-    long long q = 0;
-    if (valid) {
-      float v = d.rbuf[d.fcsc_pos[e]] * kFarScale;
-      if (fabsf(v) > sp.far_lim) {
-        clamped = true;
-        v = v > 0.f ? sp.far_lim : -sp.far_lim;
-      }
-      q = __float2ll_rn(v);
-    }
+    long long q = valid ? (long long)__float2int_rn(d.rbuf[d.fcsc_pos[e]] * qscale) : 0;
     // segmented inclusive scan on the VALU (DPP row shifts, then the row
     // broadcasts across the four 16-lane rows) instead of 18 LDS permutes:
     // the CSC is slot-sorted, so a lane k places back is in this lane's
@@ -1151,10 +1312,8 @@ __global__ __launch_bounds__(256) void k_far_grad(DevSgd d, SgdParams sp) {
     seg_scan_step<0x143, 0xc>(q, sl);   // row_bcast:31 -> rows 2, 3
     const uint32_t sn = uint32_t(__shfl_down(int(sl), 1, kWave));
     const bool tail = valid && (lane == kWave - 1 || e + 1 >= n || sn != sl);
-    if (tail && q != 0)
-      atomicAdd(reinterpret_cast<unsigned long long*>(&d.gfix[sl - d.far_base]), (unsigned long long)q);
+    if (tail && q != 0) atomicAdd(&gfar[sl - d.far_base], (unsigned long long)q);
   }
-  if (__any(clamped) && lane == 0) d.state[7] = 1.0;
 }
 
 void launch_far_grad(const DevSgd& d, const SgdParams& sp, int num_cu, hipStream_t s) {
@@ -1168,11 +1327,16 @@ void launch_far_grad(const DevSgd& d, const SgdParams& sp, int num_cu, hipStream
 // to d.nrm[blockIdx], one wave adds the partials in a fixed order (DP ranks
 // hold identical weights, so their convergence verdicts must match bit for
 // bit; float atomics would add in arrival order).
-// mode 0: out = sum; 1: out = |w_rest|^2 (state[4] - state[6]) + sum; 2: out = state[4]
-__global__ void k_norm_sum(const double* parts, int n, double* out, const double* state, int mode) {
-  double acc = 0.0;
-  for (int k = lane_id(); k < n; k += kWave) acc += parts[k];
+// mode 0: out = sum (+ mx_out = max of the max partials); 1: out = |w_rest|^2
+// (state[4] - state[6]) + sum; 2: out = state[4]
+__global__ void k_norm_sum(const double* parts, int n, double* out, const double* state, int mode, double* mx_out) {
+  double acc = 0.0, mx = 0.0;
+  for (int k = lane_id(); k < n; k += kWave) {
+    acc += parts[k];
+    if (mx_out) mx = fmax(mx, parts[kNormParts + k]);
+  }
   acc = wave_sum(acc);
+  mx = wave_max(mx);
   if (threadIdx.x == 0) {
     double base = 0.0;
     if (mode == 1) {             // rest of the previous batch + active part
@@ -1180,24 +1344,40 @@ __global__ void k_norm_sum(const double* parts, int n, double* out, const double
       if (base < 0.0) base = 0.0;
     }
     *out = mode == 2 ? state[4] : base + acc;
+    if (mx_out) *mx_out = mx;
   }
 }
 
 __global__ __launch_bounds__(kBlock) void k_gather_w(DevSgd d, const int32_t* uniq) {
   __shared__ double scratch[kBlock / kWave];
-  double acc = 0.0;
+  __shared__ double mscratch[kBlock / kWave];
+  double acc = 0.0, mx = 0.0;
+  const int64_t text_end = kNumNumeric + d.n_unique;
   for (int64_t s = int64_t(blockIdx.x) * kBlock + threadIdx.x; s < d.ns;
        s += int64_t(gridDim.x) * kBlock) {
     double v = 0.0;
     if (s < kNumNumeric) v = d.w64[d.F + s];
-    else if (s < kNumNumeric + d.n_unique) v = d.w64[d.slot_fid ? d.slot_fid[s] : uniq[s - kNumNumeric]];
+    else if (s < text_end) v = d.w64[d.slot_fid ? d.slot_fid[s] : uniq[s - kNumNumeric]];
     d.wc64[s] = v;
     d.wc32[s] = float(v);
-    d.g64[s] = 0.0;
     acc += v * v;
+    if (s >= kNumNumeric && s < text_end) mx = fmax(mx, fabs(double(float(v))));
+    if (s >= d.far_base && s < text_end) d.gacc[d.far_off + s - d.far_base] = 0;   // far sums start at 0
   }
+  // packed near columns + tail start at 0 (single GPU never writes them; DP rewrites them)
+  for (int64_t s = int64_t(blockIdx.x) * kBlock + threadIdx.x; s < d.nl + d.tail_len;
+       s += int64_t(gridDim.x) * kBlock)
+    d.gacc[s] = 0;
   acc = block_sum(acc, scratch);
-  if (threadIdx.x == 0) d.nrm[blockIdx.x] = acc;
+  mx = wave_max(mx);
+  if (lane_id() == 0) mscratch[threadIdx.x / kWave] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double m2 = 0.0;
+    for (int k = 0; k < kBlock / kWave; ++k) m2 = fmax(m2, mscratch[k]);
+    d.nrm[blockIdx.x] = acc;
+    d.nrm[kNormParts + blockIdx.x] = m2;
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void k_norm2(const double* v, int64_t n, double* parts) {
@@ -1223,7 +1403,9 @@ __global__ __launch_bounds__(kBlock) void k_scatter_w(DevSgd d, const int32_t* u
   if (threadIdx.x == 0) d.nrm[blockIdx.x] = acc;
 }
 
-static int gather_grid(const DevSgd& d) { return std::max(1, std::min(ceil_div(d.ns, kBlock), kNormParts)); }
+static int gather_grid(const DevSgd& d) {
+  return std::max(1, std::min(ceil_div(std::max<int64_t>(d.ns, d.nl + d.tail_len), kBlock), kNormParts));
+}
 static int scatter_grid(const DevSgd& d) {
   return std::max(1, std::min(ceil_div(kNumNumeric + d.n_unique, kBlock), kNormParts));
 }
@@ -1231,7 +1413,7 @@ static int scatter_grid(const DevSgd& d) {
 void launch_gather_w(const DevSgd& d, const DevPrepared& p, hipStream_t s) {
   const int grid = gather_grid(d);
   hipLaunchKernelGGL(k_gather_w, dim3(grid), dim3(kBlock), 0, s, d, p.uniq);
-  hipLaunchKernelGGL(k_norm_sum, dim3(1), dim3(kWave), 0, s, d.nrm, grid, &d.state[6], d.state, 0);
+  hipLaunchKernelGGL(k_norm_sum, dim3(1), dim3(kWave), 0, s, d.nrm, grid, &d.state[6], d.state, 0, &d.state[9]);
 }
 
 void launch_norm2(const double* v, int64_t n, double* out, const DevSgd& d, hipStream_t s) {
@@ -1239,7 +1421,7 @@ void launch_norm2(const double* v, int64_t n, double* out, const DevSgd& d, hipS
   if (grid > kNormParts) grid = kNormParts;
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(k_norm2, dim3(grid), dim3(kBlock), 0, s, v, n, d.nrm);
-  hipLaunchKernelGGL(k_norm_sum, dim3(1), dim3(kWave), 0, s, d.nrm, grid, out, d.state, 0);
+  hipLaunchKernelGGL(k_norm_sum, dim3(1), dim3(kWave), 0, s, d.nrm, grid, out, d.state, 0, (double*)nullptr);
 }
 
 void launch_scatter_w(const DevSgd& d, const DevPrepared& p, hipStream_t s) {
@@ -1248,7 +1430,7 @@ void launch_scatter_w(const DevSgd& d, const DevPrepared& p, hipStream_t s) {
 
 void launch_norm_next(const DevSgd& d, bool trained, hipStream_t s) {
   hipLaunchKernelGGL(k_norm_sum, dim3(1), dim3(kWave), 0, s, d.nrm, trained ? scatter_grid(d) : 0,
-                     d.wnorm_next, d.state, trained ? 1 : 2);
+                     d.wnorm_next, d.state, trained ? 1 : 2, (double*)nullptr);
 }
 
 __global__ void k_norm_carry(DevSgd d) {
@@ -1260,18 +1442,46 @@ void launch_norm_carry(const DevSgd& d, hipStream_t s) {
 }
 
 // Per-batch SGD state in one launch: state (m = global kept rows at [5]),
-// batch stats, sampled counts, the loss slot g64[ns] and the loss history.
+// batch stats and the loss history.
 __global__ void k_batch_init(DevSgd d, double m_global, int n_loss) {
   const int i = threadIdx.x;
   if (i < kStateLen) d.state[i] = i == 5 ? m_global : 0.0;
   if (i < 8) d.stats[i] = 0.0;
-  if (i < 4) d.red64[i] = 0.0;
-  if (i == 0) d.g64[d.nl] = 0.0;
   for (int k = i; k < n_loss; k += blockDim.x) d.loss_hist[k] = 0.0;
 }
 
 void launch_batch_init(const DevSgd& d, double m_global, int n_loss, hipStream_t s) {
   hipLaunchKernelGGL(k_batch_init, dim3(1), dim3(256), 0, s, d, m_global, n_loss);
+}
+
+// ---------------------------------------------------------------------------
+// Batch bounds of the scale choice: max bigram count of a kept row, max |y|,
+// max |n_k| (non-negative doubles order like their bit patterns: u64 max).
+// ---------------------------------------------------------------------------
+constexpr int32_t kNnzCountMask = (1 << 30) - 1;   // featurize.hip: nnz bits 0..29 = bigram count
+
+__global__ __launch_bounds__(kBlock) void k_batch_bounds(DevPrepared p, double* out) {
+  const int64_t n_kept = p.counters[0];
+  const int64_t cap = p.cap_rows16;
+  double b[2 + kNumNumeric] = {0, 0, 0, 0, 0, 0};
+  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n_kept; i += int64_t(gridDim.x) * kBlock) {
+    b[0] = fmax(b[0], double(p.nnz[i] & kNnzCountMask));
+    b[1] = fmax(b[1], fabs(double(p.y[i])));
+#pragma unroll
+    for (int k = 0; k < kNumNumeric; ++k) b[2 + k] = fmax(b[2 + k], fabs(double(p.num[int64_t(k) * cap + i])));
+  }
+#pragma unroll
+  for (int k = 0; k < 2 + kNumNumeric; ++k) {
+    const double v = wave_max(b[k]);
+    if (lane_id() == 0 && v > 0.0)
+      atomicMax(reinterpret_cast<unsigned long long*>(&out[k]), __builtin_bit_cast(unsigned long long, v));
+  }
+}
+
+void launch_batch_bounds(const DevPrepared& p, double* out, hipStream_t s) {
+  TWTML_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(double) * kBoundsLen, s));
+  const int grid = int(std::max<int64_t>(1, std::min<int64_t>((p.cap_rows + kBlock - 1) / kBlock, 512)));
+  hipLaunchKernelGGL(k_batch_bounds, dim3(grid), dim3(kBlock), 0, s, p, out);
 }
 
 }  // namespace twtml

@@ -39,7 +39,7 @@ def _parity(profile, F, hash, n, batches, seed, expect_tiered, eng=None):
         pred_o = round_half_up_array(fb.X @ w)
         res = eng.train_batch(raw, want_pred=True)
         assert res["tiered"] == expect_tiered, res["n_unique"]
-        assert not res["overflow"]
+        assert not res["diverged"]
         assert res["n_kept"] == fb.n
         r = run_minibatch_sgd_active(fb.X, fb.y, w, 0.005, 50)
         w = r.weights                     # the oracle continues from its own weights

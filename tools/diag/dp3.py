@@ -25,14 +25,11 @@ def worker(rank, world, port, out_dir, mode):
     from twitter_stream_ml_amd.ops.lr_engine import DeviceLinearRegression
     from twitter_stream_ml_amd.parallel import dist as D
     D.init_distributed(backend="gloo")
-    if mode == "noprep":
-        comm, prep_comm = D.make_comm(0, "gloo"), None
-    else:
-        comm, prep_comm = D.make_comm_pair(0, "gloo")
+    comm = D.make_comm(0, "gloo")
     keep = []
     for ci in (range(CASE + 1) if os.environ.get("DIAG_ALL") else [CASE]):   # DIAG_ALL: like the test
         profile, F, hash, rows, nb, _ = T.LR_CASES[ci]
-        eng = DeviceLinearRegression(T._lr_cfg(F, hash, rows), device=0, comm=comm, prep_comm=prep_comm)
+        eng = DeviceLinearRegression(T._lr_cfg(F, hash, rows), device=0, comm=comm)
         shards = [full.shard(rank, world) for full in T._batches(profile, rows, nb, seed=40 + ci)]
         if mode == "prefetch":
             for sh in shards[:eng.raw_slots - 1]:

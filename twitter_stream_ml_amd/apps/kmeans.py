@@ -178,7 +178,7 @@ def main(argv: Optional[List[str]] = None) -> int:
     log.info("Initializing Twitter stream...")
     stream = ssc.twitterStream(make_source(args.source, rate=args.sourceRate, seed=args.seed,
                                            shard=info.rank, num_shards=info.world,
-                                           start=resume.records))
+                                           start=resume.records, batch_size=args.batchSize))
     session = None
     if info.rank == 0:
         log.info("Initializing Lightning graph session...")

@@ -30,6 +30,7 @@ import logging
 import math
 import os
 import sys
+import time
 from typing import List, Optional
 
 import numpy as np
@@ -38,7 +39,7 @@ from ..config.arguments import ConfArguments
 from ..config.hocon import load_java_opts
 from ..models.linear_regression import CpuLinearRegression, CpuLRConfig, LinearRegressionModel
 from ..models.mllib_helper import MllibHelper
-from ..parallel.dist import barrier, check_replicas, gather_to_main
+from ..parallel.dist import barrier, broadcast_flag, check_replicas, gather_to_main
 from ..utils.faults import maybe_inject
 from ._common import ResumeState, StreamCheckpointer, load_resume_state, make_watchdog
 from ..oracle.mllib import round_half_up
@@ -62,15 +63,18 @@ def build_engine(conf: ConfArguments, rank: int, world: int, device: Optional[in
     F = conf.effectiveNumTextFeatures
     if spec.is_gpu:
         from ..ops.lr_engine import DeviceLinearRegression, LRDeviceConfig
-        from ..parallel.dist import make_comm, make_comm_pair
+        from ..parallel.dist import make_comm
         dev = device if device is not None else (spec.devices[rank] if spec.devices else rank)
         from ..parallel.affinity import bind_local_numa
         bind_local_numa(dev)   # pinned staging buffers on the GPU's NUMA node
         def lr_cfg(rows: int) -> LRDeviceConfig:
+            # ingest "utf8": the receiver's UTF-8 bytes cross PCIe as they are
+            # (DMA'd from its page-locked buffer when the source pins them) and
+            # the device decodes / lower-cases / narrows -- the path bench.py times
             return LRDeviceConfig(num_text_features=F, hash=conf.hash, step_size=conf.stepSize,
                                   num_iterations=conf.numIterations, fraction=conf.miniBatchFraction,
                                   begin=conf.numRetweetBegin, end=conf.numRetweetEnd,
-                                  max_rows=rows, max_units=rows * 290)
+                                  max_rows=rows, max_units=rows * 290, ingest="utf8")
 
         rows = max_rows or max(65536, int(conf.batchSize or 0))
         cap = os.environ.get("TWTML_BATCH_ROWS", "")
@@ -82,14 +86,11 @@ def build_engine(conf: ConfArguments, rank: int, world: int, device: Optional[in
         elif cap:
             rows = max(rows, int(cap))
         cfg = lr_cfg(rows)
-        # TWTML_PREP_COMM=1: a second RCCL communicator, so batch t+1 is
-        # prepared while t's gradient all-reduces run (opt-in)
-        comm, prep_comm = None, None
-        if world > 1 and os.environ.get("TWTML_PREP_COMM", "0") == "1":
-            comm, prep_comm = make_comm_pair(dev, "rccl")
-        elif world > 1:
-            comm = make_comm(dev, "rccl")
-        return DeviceLinearRegression(cfg, device=dev, comm=comm, prep_comm=prep_comm)
+        # one RCCL communicator: per GD iteration one int64 all-reduce, per
+        # batch one all-gather of the prep packets (overlapped with the
+        # previous batch's GD loop) and the stats all-reduce
+        comm = make_comm(dev, "rccl") if world > 1 else None
+        return DeviceLinearRegression(cfg, device=dev, comm=comm)
     from ..parallel.dist import allreduce_fn
     cfg = CpuLRConfig(num_text_features=F, hash=conf.hash, step_size=conf.stepSize,
                       num_iterations=conf.numIterations, fraction=conf.miniBatchFraction,
@@ -102,19 +103,25 @@ class LinearRegressionJob:
 
     def __init__(self, conf: ConfArguments, engine, session: Optional[SessionStats] = None,
                  rank: int = 0, metrics: Optional[MetricsLogger] = None,
-                 resume: Optional[ResumeState] = None, world: int = 1):
+                 resume: Optional[ResumeState] = None, world: int = 1, plot: Optional[bool] = None):
         self.conf = conf
         self.engine = engine
         self.session = session
         self.rank = rank
         self.world = world
+        # plot: rank 0 appends real/pred to a live Lightning plot, so every
+        # rank collects its predictions (D2H) and ships a sample; otherwise
+        # a batch's report needs only the six fused statistics
+        self.plot = (session is not None and getattr(session, "viz", None) is not None) if plot is None else plot
+        self.tweets = 0                # trained tweets (all ranks), for the throughput summary
+        self.t_first = self.t_last = None
         resume = resume or ResumeState()
         self.count = resume.count      # the "count" accumulator
         self.batches = resume.batches  # stream batches trained into the model
         self.records = resume.records  # source records this rank consumed
         self.metrics = metrics or MetricsLogger(None)
         self.last = None
-        self.overflows = 0   # batches whose gradient hit the fixed-point clamp
+        self.diverged = 0    # batches on which the model was found diverged (training stopped)
         self.checkpointer = StreamCheckpointer(
             conf.checkpoint, conf.checkpointInterval, rank,
             lambda path, prog: LinearRegressionModel(self.engine.get_weights(), 0.0).save(path, prog),
@@ -126,14 +133,21 @@ class LinearRegressionJob:
         maybe_inject(self.rank, self.batches + 1)
         if self.watchdog is not None:
             self.watchdog.arm()
-        res = self.engine.train_batch(raw, want_pred=True)     # op #1 then op #2
+        t0 = time.perf_counter()
+        res = self.engine.train_batch(raw, want_pred=self.plot)     # op #1 then op #2
+        t1 = time.perf_counter()
+        if self.t_first is None:
+            self.t_first = t0
+        self.t_last = t1
+        self.tweets += int(res.get("n_kept_global", 0))
         self.last = res
-        if res.get("overflow"):
-            # a residual hit the fixed-point gradient clamp (sgd.hip sgd_fix_limit):
-            # the update no longer follows MLlib exactly -- the model is diverging
-            log.error("batch %d: gradient fixed-point clamp hit (|residual| too large); "
-                      "the model is diverging (stepSize %s too large?)", self.batches + 1, self.conf.stepSize)
-            self.overflows += 1
+        if res.get("diverged"):
+            # the residual bound / weights left any usable range (sgd.hip
+            # sgd_scales): MLlib's fp64 model would go to Inf/NaN here and
+            # Utils.round throw; the engine stops training the batch instead
+            log.error("batch %d: the model diverged (|residual| bound >= 1e30 or non-finite weights); "
+                      "training stopped (stepSize %s too large?)", self.batches + 1, self.conf.stepSize)
+            self.diverged += 1
         self.batches += 1
         self.records += raw.n
         try:
@@ -153,6 +167,10 @@ class LinearRegressionJob:
             return
         self.count += batch
         n, sy, sy2, sp, sp2, se2 = res["stats"]
+        if n <= 0:   # no prequential pass: the model had diverged before this batch
+            log.error("batch %d: model diverged; skipping report", self.batches)
+            self.metrics.log(batch_time_ms=time_ms, raw=raw.n, batch=batch, diverged=True)
+            return
         my, mp = sy / n, sp / n
         try:
             real_sd = round_half_up(math.sqrt(max(sy2 / n - my * my, 0.0)))
@@ -160,15 +178,23 @@ class LinearRegressionJob:
             mse = round_half_up(se2 / n)
         except ValueError as e:  # Utils.round on NaN/Inf: the model diverged
             log.error("batch %d: model diverged (%s); skipping report", self.batches, e)
-            self.metrics.log(batch_time_ms=time_ms, raw=raw.n, batch=batch, diverged=True,
-                             overflow=bool(res.get("overflow", False)))
+            self.metrics.log(batch_time_ms=time_ms, raw=raw.n, batch=batch, diverged=True)
             return
-        mask = self._kept_mask(raw)
-        real = raw.scalars[RETWEET_COUNT][mask].astype(np.float64)
-        pred = np.asarray(res["pred"], np.float64) if res.get("pred") is not None else np.zeros(0)
-        real_all, pred_all = real, pred
-        if self.world > 1:   # CS7: real.toArray / pred.toArray are collected to the driver
-            real_all, pred_all = gather_to_main(real), gather_to_main(pred)
+        real = pred = real_all = pred_all = np.zeros(0)
+        if self.plot:
+            mask = self._kept_mask(raw)
+            real = raw.scalars[RETWEET_COUNT][mask].astype(np.float64)
+            pred = np.asarray(res["pred"], np.float64) if res.get("pred") is not None else np.zeros(0)
+            real_all, pred_all = real, pred
+            if self.world > 1:
+                # CS7: real.toArray / pred.toArray are collected to the driver;
+                # with --plotPoints each rank ships only its share of the sample
+                if self.conf.plotPoints > 0:
+                    k = max(1, self.conf.plotPoints // self.world)
+                    if real.shape[0] > k:
+                        idx = np.linspace(0, real.shape[0] - 1, k).astype(np.int64)
+                        real, pred = real[idx], pred[idx]
+                real_all, pred_all = gather_to_main(real), gather_to_main(pred)
         if log.isEnabledFor(logging.DEBUG):
             log.debug("count: %d", self.count)
             log.debug("batch: %d,  mse: %d", batch, int(mse))
@@ -178,10 +204,21 @@ class LinearRegressionJob:
         self.metrics.log(batch_time_ms=time_ms, raw=raw.n, batch=batch, count=self.count,
                          mse=mse, realStdev=real_sd, predStdev=pred_sd,
                          iterations=res["iterations"], converged=bool(res["converged"]),
-                         overflow=bool(res.get("overflow", False)),
+                         diverged=bool(res.get("diverged", False)),
                          prep_ms=res.get("prep_ms", 0.0), train_ms=res.get("train_ms", 0.0))
         if self.session is not None and self.rank == 0:
             self.session.update(self.count, batch, mse, real_sd, pred_sd, real_all, pred_all)
+
+    def summary(self) -> dict:
+        """Throughput of the run: trained tweets (all ranks) over the wall
+        time from the first batch's start to the last one's end."""
+        secs = (self.t_last - self.t_first) if self.t_first is not None else 0.0
+        rec = dict(summary=True, batches=self.batches, tweets=self.tweets, seconds=round(secs, 6),
+                   tweets_per_s=(self.tweets / secs) if secs > 0 else 0.0, diverged_batches=self.diverged)
+        self.metrics.log(**rec)
+        log.info("trained %d tweets in %d batches, %.3f s: %.1f tweets/s", self.tweets, self.batches, secs,
+                 rec["tweets_per_s"])
+        return rec
 
     def _kept_mask(self, raw):
         rc = raw.scalars[RETWEET_COUNT]
@@ -237,9 +274,10 @@ def main(argv: Optional[List[str]] = None) -> int:
     log.info("Initializing Twitter stream...")
     stream = ssc.twitterStream(make_source(conf.source, rate=conf.sourceRate, seed=conf.seed,
                                            shard=rank, num_shards=world,
-                                           start=resume.records)).cache()
+                                           start=resume.records, batch_size=conf.batchSize)).cache()
+    plot = broadcast_flag(session is not None and session.viz is not None)   # the same on every rank
     job = LinearRegressionJob(conf, engine, session, rank,
-                              MetricsLogger(os.environ.get("TWTML_METRICS")), resume, world)
+                              MetricsLogger(os.environ.get("TWTML_METRICS")), resume, world, plot=plot)
     log.info("Initializing prediction model...")
     stream.foreachRDD(job.on_batch)   # op #1 (stats) + op #2 (trainOn), prequential order
     if hasattr(engine, "prefetch"):   # device engine: H2D of queued batches overlaps training
@@ -258,6 +296,8 @@ def main(argv: Optional[List[str]] = None) -> int:
         ssc.stop()
         if not failed:
             job.final_checkpoint()
+            if rank == 0:
+                job.summary()
         job.close()
         if session is not None:
             session.close()

@@ -159,7 +159,7 @@ class CpuLinearRegression:
                                   "loss_history": [], "stats": stats.tolist(),
                                   "pred": pred.astype(np.float32) if want_pred else None,
                                   "n_unique": int(np.unique(X.indices).shape[0]) if X.nnz else 0,
-                                  "prep_ms": 0.0, "train_ms": 0.0, "overflow": False}
+                                  "prep_ms": 0.0, "train_ms": 0.0, "diverged": False}
         if n_glob == 0:
             return res
         r = run_minibatch_sgd(X, y, self.w, c.step_size, c.num_iterations, c.fraction, c.tol,

@@ -56,6 +56,10 @@ class KMDeviceConfig:
     max_rows: int = 1 << 16
     max_units: int = (1 << 16) * 281
     seed: int = 42
+    # host staging of the text (text_dims > 0): "utf8" ships the receiver's
+    # UTF-8 bytes (DMA'd in place when page-locked; the device decodes),
+    # "wire" runs the host packer
+    ingest: str = "utf8"
 
     def as_dict(self) -> Dict[str, object]:
         if self.time_unit not in ("batches", "points"):
@@ -93,7 +97,7 @@ class DeviceKMeans:
         hb = self.staging(slot)
         if self.cfg.text_dims == 0:
             return hb.load_utf8(raw, no_text(raw), copy_text=True)
-        return hb.load(raw)
+        return hb.load(raw, self.cfg.ingest)
 
     # ---- model state (latestModel.clusterCenters / clusterWeights) -------
     def get_state(self):

@@ -24,7 +24,7 @@ import weakref
 
 import numpy as np
 
-from ..records.batch import RETWEET_COUNT, RawBatch
+from ..records.batch import RETWEET_COUNT, RawBatch, Utf8Text
 from ._native import hip, host
 from .ingest import SlotPipeline
 
@@ -40,18 +40,6 @@ def prelower(raw: RawBatch) -> RawBatch:
         return raw
     text, offsets, _ = h.prelower_special_rows(raw.text, raw.offsets)
     return RawBatch(text, offsets, raw.is_retweet, raw.scalars, raw.batch_time_ms)
-
-
-@dataclass
-class Utf8Text:
-    """A batch's tweet text as UTF-8 bytes + byte offsets [n+1]: the form a
-    network receiver holds (the Twitter stream delivers UTF-8 JSON)."""
-    data: np.ndarray      # uint8 [bytes]
-    offsets: np.ndarray   # int64 [n + 1]
-
-    @property
-    def nbytes(self) -> int:
-        return int(self.offsets[-1]) if self.offsets.shape[0] else 0
 
 
 def encode_utf8(raw: RawBatch, threads: int = 0) -> Utf8Text:
@@ -95,9 +83,8 @@ class LRDeviceConfig:
     # device decodes non-ASCII rows and narrows the Latin-1 ones
     ingest: str = "wire"
     # prepare batch t+1 (featurize .. layout, on a prep stream and the
-    # engine's prep thread) while batch t trains; DP ranks need a second
-    # communicator for the prep collectives (``prep_comm``), else they
-    # prepare in line
+    # engine's prep thread) while batch t trains; DP ranks all-gather their
+    # prep packets between two of t's GD iterations (engine.cpp issue_c1)
     overlap: bool = True
 
     def as_dict(self) -> Dict[str, object]:
@@ -167,6 +154,11 @@ class HostBatchView:
                              f"({self.max_rows}, {self.max_units})")
 
     def load(self, raw: RawBatch, ingest: str = "wire") -> "HostBatchView":
+        if ingest == "utf8" and raw.utf8 is not None:
+            # the receiver's own UTF-8 bytes: DMA'd from its page-locked
+            # buffer (no host copy), or copied into the staging buffer
+            return self.load_utf8(raw, raw.utf8, copy_text=not raw.utf8.pinned)
+        raw.ensure_text()
         if ingest == "utf16":
             return self.load_utf16(raw, copy_text=True)
         if ingest == "utf8":
@@ -226,8 +218,13 @@ class HostBatchView:
         return RawBatch(text, offsets, is_rt, self.scalars().copy(), self.batch_time_ms)
 
 
-def register_host(arr: np.ndarray) -> None:
-    """Page-lock a host array so ``submit`` can DMA from it asynchronously."""
+def register_host(arr) -> None:
+    """Page-lock a host array (or a :class:`Utf8Text`'s bytes) so ``submit``
+    can DMA from it asynchronously."""
+    if isinstance(arr, Utf8Text):
+        register_host(arr.data)
+        arr.pinned = True
+        return
     if arr.nbytes:
         hip().host_register(int(arr.ctypes.data), int(arr.nbytes))
 
@@ -240,12 +237,11 @@ def unregister_host(arr: np.ndarray) -> None:
 class DeviceLinearRegression:
     """StreamingLinearRegressionWithSGD state + pipeline on one GPU."""
 
-    def __init__(self, cfg: LRDeviceConfig, device: int = 0, comm=None, prep_comm=None):
+    def __init__(self, cfg: LRDeviceConfig, device: int = 0, comm=None):
         self.cfg = cfg
         self.device = int(device)
         self.comm = comm
-        self.prep_comm = prep_comm
-        self._eng = hip().LREngine(self.device, cfg.as_dict(), comm, prep_comm)
+        self._eng = hip().LREngine(self.device, cfg.as_dict(), comm)
         self._staging: List[HostBatchView] = []
         self.raw_slots = int(hip().RAW_SLOTS)
         # callbacks through a weak proxy: no reference cycle, so dropping the

@@ -25,7 +25,7 @@ from typing import Callable, Optional
 
 import numpy as np
 
-__all__ = ["DistInfo", "init_distributed", "dist_info", "make_rccl_comm", "make_comm", "make_comm_pair",
+__all__ = ["DistInfo", "init_distributed", "dist_info", "make_rccl_comm", "make_comm", "broadcast_flag",
            "allreduce_fn",
            "barrier", "allreduce_max_scalar", "allreduce_sum_scalar", "shutdown",
            "check_replicas", "replica_digest", "ReplicaDivergence", "gather_to_main"]
@@ -135,18 +135,6 @@ def make_comm(device: int, kind: str = "rccl", own_group: bool = False):
     return hip().HostComm(info.rank, info.world, collective)
 
 
-def make_comm_pair(device: int, kind: str = "rccl", prep_kind: Optional[str] = None):
-    """(gradient communicator, prep communicator) for a DP engine: the
-    second one carries the prep-stage collectives of batch t+1 while batch
-    t's gradient all-reduces run on the first.  ``prep_kind`` (default
-    ``kind``): e.g. RCCL gradients with a host-staged gloo prep group -- the
-    prep messages are small and a second RCCL communicator would compete for
-    the process's hardware queues.  (None, None) at world 1."""
-    if dist_info().world <= 1:
-        return None, None
-    return make_comm(device, kind), make_comm(device, prep_kind or kind, own_group=True)
-
-
 def allreduce_fn() -> Optional[Callable[[np.ndarray], np.ndarray]]:
     """float64 sum across ranks (gloo/nccl via torch), or None for 1 rank."""
     info = dist_info()
@@ -231,6 +219,15 @@ def check_replicas(arr: np.ndarray, what: str = "model") -> None:
     if int(lo.item()) != int(hi.item()):
         raise ReplicaDivergence(f"{what} replicas diverged across ranks (digest on rank "
                                 f"{info.rank}: {d:#x})")
+
+
+def broadcast_flag(flag: bool) -> bool:
+    """Rank 0's boolean on every rank (True/False as the max of 0/1 with the
+    other ranks contributing 0)."""
+    if dist_info().world <= 1:
+        return bool(flag)
+    v = 1.0 if (flag and dist_info().rank == 0) else 0.0
+    return _reduce_scalar(v, "max") > 0.5
 
 
 def gather_to_main(arr: np.ndarray) -> Optional[np.ndarray]:

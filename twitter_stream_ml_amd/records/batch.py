@@ -23,17 +23,23 @@ row   name                    source
 
 ``is_retweet`` is separate (uint8).  For non-retweets the scalar/text columns
 hold the tweet's own fields; every consumer filters on ``is_retweet`` first.
+
+A receiver may also hand over the text as it holds it -- UTF-8 bytes
+(:class:`Utf8Text`, the form the network delivers) -- in ``utf8``; the device
+engines then DMA those bytes and decode on the GPU.  Such a batch may leave
+``text`` empty (``offsets`` still count UTF-16 units); :meth:`ensure_text`
+decodes it on demand for host consumers.
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
+from dataclasses import dataclass, replace
 from typing import Iterable, List, Optional, Sequence
 
 import numpy as np
 
 from .schema import Status, User
 
-__all__ = ["RawBatch", "SCALAR_FIELDS", "RETWEET_COUNT", "FOLLOWERS", "FAVOURITES",
+__all__ = ["RawBatch", "Utf8Text", "SCALAR_FIELDS", "RETWEET_COUNT", "FOLLOWERS", "FAVOURITES",
            "FRIENDS", "CREATED_AT", "utf16_units", "units_to_str"]
 
 RETWEET_COUNT, FOLLOWERS, FAVOURITES, FRIENDS, CREATED_AT = range(5)
@@ -50,12 +56,28 @@ def units_to_str(units: np.ndarray) -> str:
 
 
 @dataclass
+class Utf8Text:
+    """A batch's tweet text as UTF-8 bytes + byte offsets [n+1]: the form a
+    network receiver holds (the Twitter stream delivers UTF-8 JSON).
+    ``pinned``: the bytes are page-locked (``register_host``), so the engines
+    DMA them without a staging copy."""
+    data: np.ndarray      # uint8 [bytes]
+    offsets: np.ndarray   # int64 [n + 1]
+    pinned: bool = False
+
+    @property
+    def nbytes(self) -> int:
+        return int(self.offsets[-1]) if self.offsets.shape[0] else 0
+
+
+@dataclass
 class RawBatch:
-    text: np.ndarray          # uint16 [total_units]
-    offsets: np.ndarray       # int64  [n+1]
+    text: np.ndarray          # uint16 [total_units] (may be empty when utf8 holds the text)
+    offsets: np.ndarray       # int64  [n+1], UTF-16 units
     is_retweet: np.ndarray    # uint8  [n]
     scalars: np.ndarray       # int64  [5, n]
     batch_time_ms: int = 0    # seal time ("now" for featurizeNumbers)
+    utf8: Optional[Utf8Text] = None   # the receiver's UTF-8 bytes of the same text
 
     def __post_init__(self) -> None:
         self.text = np.ascontiguousarray(self.text, dtype=np.uint16)
@@ -66,7 +88,10 @@ class RawBatch:
         if self.offsets.shape != (n + 1,) or self.scalars.shape != (5, n):
             raise ValueError(f"inconsistent RawBatch shapes: n={n} offsets={self.offsets.shape} "
                              f"scalars={self.scalars.shape}")
-        if n and (self.offsets[0] != 0 or self.offsets[-1] != self.text.shape[0]):
+        if self.utf8 is not None and self.utf8.offsets.shape != (n + 1,):
+            raise ValueError("UTF-8 offsets do not match the batch")
+        text_dropped = self.utf8 is not None and self.text.shape[0] == 0
+        if n and (self.offsets[0] != 0 or (self.offsets[-1] != self.text.shape[0] and not text_dropped)):
             raise ValueError("offsets must start at 0 and end at len(text)")
 
     # ------------------------------------------------------------------
@@ -79,7 +104,18 @@ class RawBatch:
 
     @property
     def total_units(self) -> int:
-        return int(self.text.shape[0])
+        return int(self.offsets[-1]) if self.offsets.shape[0] else 0
+
+    def ensure_text(self) -> "RawBatch":
+        """Decode the UTF-16 text from ``utf8`` if the receiver dropped it."""
+        if self.text.shape[0] != self.total_units and self.utf8 is not None:
+            raw = bytes(self.utf8.data[:self.utf8.nbytes])
+            self.text = utf16_units(raw.decode("utf-8", "surrogatepass"))
+        return self
+
+    def with_time(self, batch_time_ms: int) -> "RawBatch":
+        """Shallow copy (arrays shared) with another seal time."""
+        return replace(self, batch_time_ms=int(batch_time_ms))
 
     @property
     def nbytes(self) -> int:
@@ -90,6 +126,7 @@ class RawBatch:
         return self.scalars[k]
 
     def text_of(self, i: int) -> str:
+        self.ensure_text()
         return units_to_str(self.text[self.offsets[i]:self.offsets[i + 1]])
 
     # ------------------------------------------------------------------
@@ -137,6 +174,7 @@ class RawBatch:
         return out
 
     def take(self, rows: Iterable[int]) -> "RawBatch":
+        self.ensure_text()
         rows = np.asarray(list(rows), dtype=np.int64)
         lens = self.offsets[rows + 1] - self.offsets[rows]
         offsets = np.zeros(rows.shape[0] + 1, np.int64)
@@ -147,6 +185,7 @@ class RawBatch:
                         self.batch_time_ms)
 
     def slice(self, start: int, stop: int) -> "RawBatch":
+        self.ensure_text()
         start = max(0, start)
         stop = min(self.n, stop)
         t0, t1 = int(self.offsets[start]), int(self.offsets[stop])
@@ -163,7 +202,10 @@ class RawBatch:
     def concat(batches: Sequence["RawBatch"], batch_time_ms: Optional[int] = None) -> "RawBatch":
         if not batches:
             return RawBatch.empty(batch_time_ms or 0)
-        text = np.concatenate([b.text for b in batches])
+        if len(batches) == 1:   # a receiver that delivers whole batches: no copy
+            b = batches[0]
+            return b.with_time(b.batch_time_ms if batch_time_ms is None else batch_time_ms)
+        text = np.concatenate([b.ensure_text().text for b in batches])
         lens = np.concatenate([np.diff(b.offsets) for b in batches])
         offsets = np.zeros(lens.shape[0] + 1, np.int64)
         np.cumsum(lens, out=offsets[1:])

@@ -272,7 +272,9 @@ class StreamingContext:
             if self.max_pending > 0 and self._jobs.qsize() >= self.max_pending:
                 self._stop.wait(0.005)          # backpressure: executor is behind
                 continue
-            want = self.poll_chunk
+            # a source that delivers whole batches (chunk_rows, e.g. a replay
+            # pool) is polled for them: one part per batch, no concatenation
+            want = max(self.poll_chunk, int(getattr(src, "chunk_rows", 0) or 0))
             if self.batch_size > 0:             # never overfill: exact-size batches
                 with self._lock:
                     want = min(want, self.batch_size - self._buffered)
