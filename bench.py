@@ -306,9 +306,10 @@ def main(argv=None) -> int:
             u8s = [encode_utf8(r) for r in pool_raw]
             for u in u8s:
                 register_host(u.data)
-            # the UTF-16 copy is not staged in this mode: keep only its length
-            pool_raw = [RawBatch(np.broadcast_to(np.uint16(0), r.text.shape), r.offsets, r.is_retweet,
-                                 r.scalars, r.batch_time_ms) for r in pool_raw]
+            # the UTF-16 copy is not staged in this mode: drop it (the batch
+            # carries the receiver's UTF-8 buffer instead)
+            pool_raw = [RawBatch(np.zeros(0, np.uint16), r.offsets, r.is_retweet, r.scalars, r.batch_time_ms,
+                                 utf8=u) for r, u in zip(pool_raw, u8s)]
         elif ingest == "utf16":
             for r in pool_raw:   # the receiver's buffers: DMA source of the text
                 register_host(r.text)

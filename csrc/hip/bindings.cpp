@@ -247,7 +247,17 @@ PYBIND11_MODULE(_twtml_hip, m) {
       .def(py::init([](int device, const py::dict& cfg, std::shared_ptr<Comm> comm) {
              LRConfig c = lr_config(cfg);
              py::gil_scoped_release nogil;
-             return std::make_shared<LREngine>(device, c, comm);
+             // The destructor stops and joins the prep thread and drains the
+             // device: never do that holding the GIL (a training-thread
+             // collective on a host communicator takes it in a callback).
+             return std::shared_ptr<LREngine>(new LREngine(device, c, comm), [](LREngine* e) {
+               if (PyGILState_Check()) {
+                 py::gil_scoped_release nogil2;
+                 delete e;
+               } else {
+                 delete e;
+               }
+             });
            }),
            py::arg("device"), py::arg("config"), py::arg("comm") = nullptr)
       .def("submit",
@@ -268,6 +278,8 @@ PYBIND11_MODULE(_twtml_hip, m) {
              return result_dict(r);
            },
            py::arg("slot"), py::arg("now_ms"), py::arg("want_pred") = false)
+      .def_property_readonly("lazy_bytes", &LREngine::lazy_bytes,
+                             "device bytes the engine allocates on its first tiered batch (sizing)")
       .def("get_weights", [](const LREngine& e) {
         py::array_t<double> out(e.num_weights());
         e.get_weights(out.mutable_data(), e.num_weights());

@@ -199,6 +199,14 @@ class LREngine {
   void set_weights(const double* w, int64_t n);
   void get_weights(double* w, int64_t n) const;
   int64_t num_weights() const { return cfg_.num_text_features + kNumNumeric; }
+  // Device bytes allocated on demand by the first tiered batch (per prepared
+  // buffer: the entry-sized far lists and CSC; the trainer's residual row
+  // buffer): ops/sizing.py adds them to the measured construction footprint.
+  int64_t lazy_bytes() const {
+    const int nbuf = overlap_ ? 2 : 1;
+    return int64_t(nbuf) * 3 * int64_t(sizeof(uint32_t)) * pb_[0].dp.cap_entries +
+           int64_t(sizeof(float)) * pb_[0].dp.cap_rows16;
+  }
   const LRConfig& config() const { return cfg_; }
   void set_step(double step, int iters, double fraction);
   void synchronize();

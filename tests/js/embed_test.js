@@ -15,7 +15,8 @@ function fakeWindow(name, search) {
     dispatch(t, ev) { (listeners[t] || []).slice().forEach((f) => f(ev)); },
     setInterval() {},
   };
-  w.postMessage = (data) => { w.sent.push(data); w.dispatch("message", { data, origin: "http://dash.local" }); };
+  // a real postMessage reports the sending window as ev.source: w.peer
+  w.postMessage = (data) => { w.sent.push(data); w.dispatch("message", { data, origin: "http://dash.local", source: w.peer }); };
   return w;
 }
 
@@ -66,6 +67,7 @@ const cw = fakeWindow("child", "?initialWidth=640&childId=viz1&parentUrl=x");
 makeDocument(cw, 321);
 cw.parent = pw;                       // child -> parent messages
 parent.iframe.contentWindow = cw;     // parent -> child messages
+pw.peer = cw; cw.peer = pw;
 const C = load(cw);
 let rendered = [];
 const child = new C.Child({ renderCallback: (w) => rendered.push(w) });
@@ -87,6 +89,20 @@ check(cw.sent.some((m) => m === "pymxPYMxviz1xPYMxwidthxPYMx300"), "wire format"
 // navigateTo; messages for another id or non-strings are ignored
 child.navigateParentTo("http://elsewhere/");
 check(pw.document.location.href === "http://elsewhere/", "navigateTo");
+child.scrollParentTo("sec2");
+check(pw.document.location.href === "#sec2", "navigateTo fragment");
+// script / data URLs (even disguised) never reach location.href
+for (const bad of ["javascript:alert(1)", " javascript:alert(1)", "java\tscript:alert(1)", "JAVASCRIPT:x",
+                   "data:text/html,<script>1</script>", "vbscript:x", "//evil.example/", "http:/x"]) {
+  child.navigateParentTo(bad);
+  check(pw.document.location.href === "#sec2", "navigateTo blocked: " + JSON.stringify(bad));
+}
+// a message from some other window (not our iframe) is ignored even if well formed
+pw.dispatch("message", { data: "pymxPYMxviz1xPYMxnavigateToxPYMxhttp://phish.example/", origin: "http://dash.local",
+                         source: { other: true } });
+check(pw.document.location.href === "#sec2", "foreign source ignored");
+pw.dispatch("message", { data: "pymxPYMxviz1xPYMxheightxPYMx9", origin: "http://dash.local", source: undefined });
+check(parent.iframe.attrs.height !== "9px", "sourceless message ignored");
 const h0 = parent.iframe.attrs.height;
 pw.dispatch("message", { data: "pymxPYMxotherxPYMxheightxPYMx1", origin: "x" });
 pw.dispatch("message", { data: { obj: 1 }, origin: "x" });
@@ -95,9 +111,10 @@ check(P._parse("viz1", "pymxPYMxviz1xPYMxbad typexPYMx1") === null, "type withou
 
 // xdomain filter
 const strict = new P.Parent("viz1", "http://lgn.local/v", { xdomain: "lgn\\.local" });
-pw.dispatch("message", { data: "pymxPYMxviz1xPYMxheightxPYMx99", origin: "http://evil.example" });
+strict.iframe.contentWindow = cw;
+pw.dispatch("message", { data: "pymxPYMxviz1xPYMxheightxPYMx99", origin: "http://evil.example", source: cw });
 check(strict.iframe.attrs.height !== "99px", "xdomain blocks");
-pw.dispatch("message", { data: "pymxPYMxviz1xPYMxheightxPYMx77", origin: "http://lgn.local:3000" });
+pw.dispatch("message", { data: "pymxPYMxviz1xPYMxheightxPYMx77", origin: "http://lgn.local:3000", source: cw });
 check(strict.iframe.attrs.height === "77px", "xdomain allows");
 strict.remove();
 

@@ -40,7 +40,12 @@ def test_linear_regression_driver_cpu(sinks, tmp_path, monkeypatch):
                       "-f", "1000", "--checkpoint", str(ck), "--checkpointInterval", "2"])
     assert rc == 0
     recs = [json.loads(l) for l in open(metrics)]
+    summ = [r for r in recs if r.get("summary")]
+    recs = [r for r in recs if not r.get("summary")]
     assert len(recs) == 3 and all(r["batch"] > 0 for r in recs)
+    # the end-of-run throughput summary (rank 0)
+    assert len(summ) == 1 and summ[0]["batches"] == 3 and summ[0]["tweets"] == sum(r["batch"] for r in recs)
+    assert summ[0]["tweets_per_s"] > 0
     assert recs[-1]["count"] == sum(r["batch"] for r in recs)
     # twtml-web got Config (viz from Lightning) and the last batch's Stats
     cfg = WebClient(web.url).config()

@@ -115,6 +115,7 @@ class LinearRegressionJob:
         self.plot = (session is not None and getattr(session, "viz", None) is not None) if plot is None else plot
         self.tweets = 0                # trained tweets (all ranks), for the throughput summary
         self.t_first = self.t_last = None
+        self.timeline = []             # (end time, trained tweets) per batch
         resume = resume or ResumeState()
         self.count = resume.count      # the "count" accumulator
         self.batches = resume.batches  # stream batches trained into the model
@@ -140,6 +141,7 @@ class LinearRegressionJob:
             self.t_first = t0
         self.t_last = t1
         self.tweets += int(res.get("n_kept_global", 0))
+        self.timeline.append((t1, int(res.get("n_kept_global", 0))))
         self.last = res
         if res.get("diverged"):
             # the residual bound / weights left any usable range (sgd.hip
@@ -211,10 +213,19 @@ class LinearRegressionJob:
 
     def summary(self) -> dict:
         """Throughput of the run: trained tweets (all ranks) over the wall
-        time from the first batch's start to the last one's end."""
+        time from the first batch's start to the last one's end, and the
+        steady state after the first quarter of the batches (at most 5, the
+        warm-up bench.py does not time either)."""
         secs = (self.t_last - self.t_first) if self.t_first is not None else 0.0
         rec = dict(summary=True, batches=self.batches, tweets=self.tweets, seconds=round(secs, 6),
                    tweets_per_s=(self.tweets / secs) if secs > 0 else 0.0, diverged_batches=self.diverged)
+        skip = min(5, len(self.timeline) // 4)
+        if len(self.timeline) - skip >= 2:
+            t_a = self.timeline[skip - 1][0] if skip else self.t_first
+            n = sum(k for _, k in self.timeline[skip:])
+            dt = self.timeline[-1][0] - t_a
+            rec.update(steady_batches=len(self.timeline) - skip, steady_tweets=n,
+                       steady_seconds=round(dt, 6), steady_tweets_per_s=n / dt if dt > 0 else 0.0)
         self.metrics.log(**rec)
         log.info("trained %d tweets in %d batches, %.3f s: %.1f tweets/s", self.tweets, self.batches, secs,
                  rec["tweets_per_s"])

@@ -6,10 +6,13 @@ LDS-tier and partial-row buffers) plus per-row staging (raw text slots with
 their decode tails, the prepared-batch entry streams, tier lists).  Rather
 than restating every allocation here, :func:`engine_footprint` builds two
 probe engines and reads the bytes they allocate
-(``_twtml_hip.device_bytes_allocated``), and :func:`hbm_max_rows` solves for
-the largest capacity that fits a fraction of the GPU's free memory.  The
-remaining headroom covers the buffers that grow with a batch's active set
-(compact weights, tier arrays: ~100 B per active feature).
+(``_twtml_hip.device_bytes_allocated``) plus what an LR engine allocates on
+its first tiered batch (``lazy_bytes``: the entry-sized far lists and CSC of
+both prepared buffers, ~48 B per text unit of capacity), and
+:func:`hbm_max_rows` solves for the largest capacity that fits a fraction of
+the GPU's free memory.  The remaining headroom covers the buffers that grow
+with a batch's active set (compact weights, slot-sized tier arrays: ~100 B
+per active feature).
 """
 from __future__ import annotations
 
@@ -29,6 +32,8 @@ def engine_footprint(make_engine: Callable[[int], object], rows: int) -> int:
     before = _allocated()
     eng = make_engine(int(rows))
     used = _allocated() - before
+    inner = getattr(eng, "_eng", eng)
+    used += int(getattr(inner, "lazy_bytes", 0) or 0)   # allocated by the first tiered batch
     del eng
     gc.collect()   # engine wrappers hold reference cycles: free the probe now
     return used

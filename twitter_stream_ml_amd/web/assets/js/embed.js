@@ -9,7 +9,12 @@
  * on every resize; the child sends "height" (its document height) on load, on
  * resize and after every width message, and "navigateTo" to move the parent
  * page.  Messages whose origin does not match the xdomain setting (a regex
- * source, default any) are ignored.  Exposed as window.embed and window.pym.
+ * source, default any) are ignored, and so are messages not sent by the
+ * iframe's own window (parent side) or by the parent window (child side).
+ * Unlike pym.js 0.4.5 (pym.js:254-256, which assigns any string to
+ * location.href -- a "javascript:" URL runs in the dashboard's origin),
+ * "navigateTo" only accepts a "#fragment" or an absolute http(s) URL.
+ * Exposed as window.embed and window.pym.
  */
 (function (global) {
   "use strict";
@@ -36,6 +41,12 @@
   function originOk(ev, xdomain) {
     if (!xdomain || xdomain === "*") return true;
     return new RegExp("^https?://" + xdomain + "(:\\d+)?$").test(ev.origin);
+  }
+
+  function safeNavTarget(m) {
+    // no whitespace / control characters (browsers strip them out of schemes)
+    if (/[\u0000-\u0020\u007f]/.test(m)) return false;
+    return /^#/.test(m) || /^https?:\/\/[^\/]/i.test(m);
   }
 
   function Handlers() { this.map = {}; }
@@ -70,10 +81,11 @@
     this.onMessage("height", function (m) {
       self.iframe.setAttribute("height", parseInt(m, 10) + "px");
     });
-    this.onMessage("navigateTo", function (m) { global.document.location.href = m; });
+    this.onMessage("navigateTo", function (m) { if (safeNavTarget(m)) global.document.location.href = m; });
 
     this._onMessage = function (ev) {
       if (!originOk(ev, self.settings.xdomain)) return;
+      if (ev.source !== self.iframe.contentWindow) return;   // only our own iframe
       var m = parse(self.id, ev.data);
       if (m) self.handlers.fire(self, m[0], m[1]);
     };
@@ -117,6 +129,7 @@
     });
     this._onMessage = function (ev) {
       if (!originOk(ev, self.settings.xdomain)) return;
+      if (ev.source !== global.parent) return;                // only the embedding page
       var m = parse(self.id, ev.data);
       if (m) self.handlers.fire(self, m[0], m[1]);
     };
@@ -149,7 +162,8 @@
     }
   }
 
-  var api = { Parent: Parent, Child: Child, autoInit: autoInit, _frame: frame, _parse: parse };
+  var api = { Parent: Parent, Child: Child, autoInit: autoInit, _frame: frame, _parse: parse,
+              _safeNavTarget: safeNavTarget };
   global.embed = api;
   if (!global.pym) global.pym = api;
   if (global.document && global.document.readyState !== "loading") autoInit();
