@@ -327,6 +327,30 @@ PYBIND11_MODULE(_twtml_hip, m) {
       .def("set_step", &LREngine::set_step)
       .def("synchronize", &LREngine::synchronize)
       .def_property_readonly("num_weights", &LREngine::num_weights)
+      .def("snapshot_begin",
+           [](LREngine& e) {
+             py::gil_scoped_release nogil;
+             e.snapshot_begin();
+           },
+           "compact the non-zero weights on the device behind the last batch (non-blocking)")
+      .def("snapshot_fetch",
+           [](LREngine& e) {
+             int64_t nnz;
+             {
+               py::gil_scoped_release nogil;
+               nnz = e.snapshot_wait();
+             }
+             py::array_t<int32_t> idx(nnz);
+             py::array_t<double> val(nnz);
+             int32_t* pi = idx.mutable_data();
+             double* pv = val.mutable_data();
+             {
+               py::gil_scoped_release nogil;
+               e.snapshot_copy(pi, pv);
+             }
+             return py::make_tuple(idx, val);
+           },
+           "(indices int32, values fp64) of the begun snapshot's non-zero weights, in index order")
       .def_property_readonly("device", &LREngine::device);
 
   bind_kmeans(m);

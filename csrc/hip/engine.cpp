@@ -483,6 +483,17 @@ LREngine::~LREngine() {
   raw_.release();
   for (auto& e : ev_) (void)hipEventDestroy(e);
   for (auto& b : pb_) free_prepared(b);
+  if (snap_stream_) {
+    (void)hipStreamSynchronize(snap_stream_);
+    (void)hipStreamDestroy(snap_stream_);
+  }
+  if (snap_ev_) (void)hipEventDestroy(snap_ev_);
+  if (snap_src_ev_) (void)hipEventDestroy(snap_src_ev_);
+  for (void* b : {static_cast<void*>(snap_cnt_), static_cast<void*>(snap_off_), static_cast<void*>(snap_idx_),
+                  static_cast<void*>(snap_val_)})
+    if (b) (void)hipFree(b);
+  if (snap_total_) (void)hipHostFree(snap_total_);
+  if (snap_stage_) (void)hipHostFree(snap_stage_);
   void* bufs[] = {sgd_.gacc, sgd_.rbuf, sgd_.w64, sgd_.wc64, sgd_.wc32, sgd_.stats, sgd_.state,
                   sgd_.loss_hist, sgd_.pred_out, sgd_.nrm, sgd_.wnorm_next, sgd_.part, sgd_.itrec, iter_tdbg_,
                   lower_page_, lower_blocks_};
@@ -848,6 +859,10 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred) {
       launch_sgd_update(sgd_, sp, fused ? sgd_.nparts : 0, s);
     }
     launch_sgd_finish(sgd_, sp, s);
+    if (snap_guard_) {   // a checkpoint snapshot still reading the master weights
+      TWTML_HIP_CHECK(hipStreamWaitEvent(s, snap_ev_, 0));
+      snap_guard_ = false;
+    }
     launch_scatter_w(sgd_, prep, s);
     launch_norm_next(sgd_, true, s);
     if (itime) print_iter_timing(iters);
@@ -1086,6 +1101,10 @@ void LREngine::set_weights(const double* w, int64_t n) {
   if (n != num_weights()) throw std::invalid_argument("weights size mismatch");
   TWTML_HIP_CHECK(hipSetDevice(device_));
   TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
+  if (snap_guard_) {
+    TWTML_HIP_CHECK(hipEventSynchronize(snap_ev_));
+    snap_guard_ = false;
+  }
   // stream-ordered, complete on return (a pageable hipMemcpy may return
   // before its DMA lands, unordered against the non-blocking compute stream)
   TWTML_HIP_CHECK(hipMemcpyAsync(sgd_.w64, w, sizeof(double) * size_t(n), hipMemcpyHostToDevice, compute_));
@@ -1099,6 +1118,74 @@ void LREngine::get_weights(double* w, int64_t n) const {
   TWTML_HIP_CHECK(hipSetDevice(device_));
   TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
   TWTML_HIP_CHECK(hipMemcpy(w, sgd_.w64, sizeof(double) * size_t(n), hipMemcpyDeviceToHost));
+}
+
+void LREngine::snapshot_begin() {
+  TWTML_HIP_CHECK(hipSetDevice(device_));
+  std::lock_guard<std::mutex> lk(snap_mu_);
+  if (snap_pending_) throw std::runtime_error("snapshot_begin: the previous snapshot was not copied yet");
+  const int64_t n = num_weights();
+  if (n >= (int64_t(1) << 31)) throw std::runtime_error("snapshot: more than 2^31 weights");
+  if (!snap_idx_) {   // once: F+4 pairs worst case (1.2 GB at F = 1e8, of 288 GB)
+    const int64_t nb = snapshot_chunks(n);
+    snap_cnt_ = static_cast<uint32_t*>(dev_alloc(sizeof(uint32_t) * size_t(nb)));
+    snap_off_ = static_cast<int64_t*>(dev_alloc(sizeof(int64_t) * size_t(nb + 1)));
+    snap_idx_ = static_cast<int32_t*>(dev_alloc(sizeof(int32_t) * size_t(n)));
+    snap_val_ = static_cast<double*>(dev_alloc(sizeof(double) * size_t(n)));
+    TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&snap_total_), sizeof(int64_t), hipHostMallocMapped));
+    TWTML_HIP_CHECK(hipHostMalloc(&snap_stage_, size_t(kSnapStage), hipHostMallocDefault));
+    int lo = 0, hi = 0;
+    TWTML_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    TWTML_HIP_CHECK(hipStreamCreateWithPriority(&snap_stream_, hipStreamNonBlocking, lo));
+    TWTML_HIP_CHECK(hipEventCreateWithFlags(&snap_ev_, hipEventDisableTiming));
+    TWTML_HIP_CHECK(hipEventCreateWithFlags(&snap_src_ev_, hipEventDisableTiming));
+  }
+  *snap_total_ = -1;
+  int64_t* dtot = nullptr;
+  TWTML_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&dtot), snap_total_, 0));
+  // The master weights change only in k_scatter_w at the end of a batch, so
+  // the compaction runs on its own low-priority stream behind the last
+  // batch and overlaps the next batch's prep and GD loop; that batch's
+  // scatter waits for it (train: snap_guard_).
+  TWTML_HIP_CHECK(hipEventRecord(snap_src_ev_, compute_));
+  TWTML_HIP_CHECK(hipStreamWaitEvent(snap_stream_, snap_src_ev_, 0));
+  launch_snapshot(sgd_.w64, n, snap_cnt_, snap_off_, snap_idx_, snap_val_, dtot, snap_stream_);
+  TWTML_HIP_CHECK(hipGetLastError());
+  TWTML_HIP_CHECK(hipEventRecord(snap_ev_, snap_stream_));
+  snap_guard_ = true;
+  snap_pending_ = true;
+}
+
+int64_t LREngine::snapshot_wait() {
+  TWTML_HIP_CHECK(hipSetDevice(device_));
+  {
+    std::lock_guard<std::mutex> lk(snap_mu_);
+    if (!snap_pending_) throw std::runtime_error("snapshot_wait: no snapshot was begun");
+  }
+  TWTML_HIP_CHECK(hipEventSynchronize(snap_ev_));
+  const int64_t nnz = __atomic_load_n(snap_total_, __ATOMIC_ACQUIRE);
+  if (nnz < 0 || nnz > num_weights()) throw std::runtime_error("snapshot: bad non-zero count");
+  return nnz;
+}
+
+void LREngine::snapshot_copy(int32_t* idx, double* val) {
+  const int64_t nnz = snapshot_wait();
+  // chunks through the page-locked stage: the DMA never waits on pageable memory
+  const int64_t per = kSnapStage / int64_t(sizeof(double));
+  for (int part = 0; part < 2; ++part) {
+    const int64_t esz = part == 0 ? int64_t(sizeof(int32_t)) : int64_t(sizeof(double));
+    const char* src = part == 0 ? reinterpret_cast<const char*>(snap_idx_) : reinterpret_cast<const char*>(snap_val_);
+    char* dst = part == 0 ? reinterpret_cast<char*>(idx) : reinterpret_cast<char*>(val);
+    for (int64_t o = 0; o < nnz; o += per) {
+      const int64_t c = std::min(per, nnz - o);
+      TWTML_HIP_CHECK(hipMemcpyAsync(snap_stage_, src + o * esz, size_t(c * esz), hipMemcpyDeviceToHost,
+                                     snap_stream_));
+      TWTML_HIP_CHECK(hipStreamSynchronize(snap_stream_));
+      std::memcpy(dst + o * esz, snap_stage_, size_t(c * esz));
+    }
+  }
+  std::lock_guard<std::mutex> lk(snap_mu_);
+  snap_pending_ = false;
 }
 
 void LREngine::set_step(double step, int iters, double fraction) {

@@ -199,14 +199,25 @@ class LREngine {
   void set_weights(const double* w, int64_t n);
   void get_weights(double* w, int64_t n) const;
   int64_t num_weights() const { return cfg_.num_text_features + kNumNumeric; }
-  // Device bytes allocated on demand by the first tiered batch (per prepared
+  // Device bytes allocated on demand: by the first tiered batch (per prepared
   // buffer: the entry-sized far lists and CSC; the trainer's residual row
-  // buffer): ops/sizing.py adds them to the measured construction footprint.
+  // buffer) and by the first checkpoint snapshot ((index, value) pairs for
+  // every weight): ops/sizing.py adds them to the construction footprint.
   int64_t lazy_bytes() const {
     const int nbuf = overlap_ ? 2 : 1;
     return int64_t(nbuf) * 3 * int64_t(sizeof(uint32_t)) * pb_[0].dp.cap_entries +
-           int64_t(sizeof(float)) * pb_[0].dp.cap_rows16;
+           int64_t(sizeof(float)) * pb_[0].dp.cap_rows16 +
+           (snap_idx_ ? 0 : num_weights() * int64_t(sizeof(int32_t) + sizeof(double)));
   }
+  // Non-blocking checkpoints: snapshot_begin() (training thread, between
+  // batches) compacts the non-zero master weights on the device behind the
+  // last batch; snapshot_wait() (any thread) returns their count once the
+  // compaction is done and snapshot_copy() copies the (index, value) pairs to
+  // host memory on the snapshot stream in page-locked chunks, then releases
+  // the snapshot.  One snapshot at a time (begin throws if one is pending).
+  void snapshot_begin();
+  int64_t snapshot_wait();
+  void snapshot_copy(int32_t* idx, double* val);
   const LRConfig& config() const { return cfg_; }
   void set_step(double step, int iters, double fraction);
   void synchronize();
@@ -288,6 +299,20 @@ class LREngine {
   std::vector<hipEvent_t> iter_events_;
   hipEvent_t ev_[4] = {nullptr, nullptr, nullptr, nullptr};
   int num_cu_ = 256;
+  // weight snapshot (snapshot.hip); allocated on the first snapshot_begin
+  std::mutex snap_mu_;
+  bool snap_pending_ = false;
+  uint32_t* snap_cnt_ = nullptr;
+  int64_t* snap_off_ = nullptr;
+  int32_t* snap_idx_ = nullptr;
+  double* snap_val_ = nullptr;
+  int64_t* snap_total_ = nullptr;     // pinned mapped
+  void* snap_stage_ = nullptr;        // pinned staging, kSnapStage bytes
+  hipStream_t snap_stream_ = nullptr;
+  hipEvent_t snap_ev_ = nullptr;      // snapshot kernels done (snap_stream_)
+  hipEvent_t snap_src_ev_ = nullptr;  // the batch the snapshot is taken after (compute_)
+  bool snap_guard_ = false;           // the next scatter into w64 must wait for snap_ev_
+  static constexpr int64_t kSnapStage = 32ll << 20;
 };
 
 }  // namespace twtml

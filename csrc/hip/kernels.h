@@ -373,6 +373,13 @@ void launch_union_flag(const int32_t* gathered, int world, int64_t max_u, const 
 // slot_hist[4 + slot_of[id]] += gathered sampled counts (union slots numbered)
 void launch_union_hist(const int32_t* gathered, int world, int64_t max_u, const DevPrepared& p, hipStream_t s);
 
+// ---- sparse weight snapshot (snapshot.hip): non-zero (index, value) pairs
+// of the master weights, in index order, for non-blocking checkpoints --------
+constexpr int64_t kSnapChunk = 16384;   // weights per counting / writing workgroup
+int64_t snapshot_chunks(int64_t n);
+void launch_snapshot(const double* w, int64_t n, uint32_t* cnt, int64_t* off, int32_t* idx, double* val,
+                     volatile int64_t* host_total, hipStream_t s);
+
 // (k-means launchers: kmeans_kernels.h)
 
 // Grid-cap multiplier of the grid-stride prep kernels (TWTML_PREP_WG_MULT,

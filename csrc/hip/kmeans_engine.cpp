@@ -193,6 +193,16 @@ void KMEngine::set_state(const double* centers, const double* weights) {
   TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
 }
 
+std::vector<int32_t> KMEngine::debug_labels() const {
+  TWTML_HIP_CHECK(hipSetDevice(device_));
+  TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
+  int64_t n = 0;
+  TWTML_HIP_CHECK(hipMemcpy(&n, prep_.counters, sizeof(int64_t), hipMemcpyDeviceToHost));
+  std::vector<int32_t> out(size_t(std::max<int64_t>(n, 0)));
+  if (n > 0) TWTML_HIP_CHECK(hipMemcpy(out.data(), labels_, sizeof(int32_t) * size_t(n), hipMemcpyDeviceToHost));
+  return out;
+}
+
 void KMEngine::get_state(double* centers, double* weights) const {
   TWTML_HIP_CHECK(hipSetDevice(device_));
   TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
@@ -254,6 +264,14 @@ void bind_kmeans(py::module_& m) {
         return py::make_tuple(c, w);
       })
       .def("synchronize", &KMEngine::synchronize)
+      .def("debug_labels", [](const KMEngine& e) {
+        std::vector<int32_t> v;
+        {
+          py::gil_scoped_release nogil;
+          v = e.debug_labels();
+        }
+        return py::array_t<int32_t>(py::ssize_t(v.size()), v.data());
+      })
       .def_property_readonly("k", &KMEngine::k)
       .def_property_readonly("d", &KMEngine::d);
 }

@@ -41,6 +41,9 @@ class KMEngine {
   KMResult process(int slot, bool want_labels);
   void set_state(const double* centers, const double* weights);
   void get_state(double* centers, double* weights) const;
+  // Debug/test: the labels left by the last process() (the update's
+  // assignment with the old centres when want_labels was false).
+  std::vector<int32_t> debug_labels() const;
   int k() const { return cfg_.k; }
   int d() const { return d_; }
   void synchronize();

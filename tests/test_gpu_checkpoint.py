@@ -1,0 +1,111 @@
+"""Non-blocking checkpoints on the device engine (csrc/hip/snapshot.hip,
+apps/_common.py StreamCheckpointer).
+
+* the device snapshot is exactly the non-zero master weights, in index order;
+* at the wide config (F = 1e8, murmur3) a run with ``--checkpointInterval 1``
+  keeps the per-batch p99 latency within 10 % of a run without checkpoints
+  (VERDICT r2 item 6), and the model on disk loads back bit-exactly.
+
+SURVEY §5 checkpoint row; the reference keeps no checkpoint at all.
+"""
+import json
+import os
+import time
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+
+from twitter_stream_ml_amd.sources.synthetic import SynthConfig, generate_batch
+
+pytestmark = pytest.mark.gpu
+NOW = 1_700_000_000_000
+
+
+def test_snapshot_is_the_nonzero_weights(hip_module):
+    from twitter_stream_ml_amd.ops.lr_engine import DeviceLinearRegression, LRDeviceConfig
+    eng = DeviceLinearRegression(LRDeviceConfig(num_text_features=100_000_000, hash="murmur3", max_rows=60_000,
+                                                max_units=60_000 * 300), device=0)
+    synth = SynthConfig.profile("wide", seed=21)
+    for t in range(2):
+        eng.train_batch(generate_batch(synth, t * 60_000, 60_000, batch_time_ms=NOW + t * 5000), want_pred=False)
+    eng.snapshot_begin()
+    with pytest.raises(RuntimeError):
+        eng.snapshot_begin()                     # one snapshot at a time
+    # training goes on while the snapshot is pending: it holds batch 2's model
+    eng.train_batch(generate_batch(synth, 2 * 60_000, 60_000, batch_time_ms=NOW + 10_000), want_pred=False)
+    size, idx, val = eng.snapshot_fetch()
+    w3 = eng.get_weights()
+    eng.snapshot_begin()
+    size3, idx3, val3 = eng.snapshot_fetch()
+    nz = np.flatnonzero(w3)
+    assert size3 == w3.shape[0] and np.array_equal(idx3, nz) and np.array_equal(val3, w3[nz])
+    assert idx.shape[0] > 1000 and np.all(np.diff(idx) > 0)
+    assert not np.array_equal(val, w3[idx]) or idx.shape != idx3.shape   # batch 3 moved the weights
+    # a dense model (every weight non-zero) and an all-zero one
+    eng.set_weights(np.arange(1, w3.shape[0] + 1, dtype=np.float64))
+    eng.snapshot_begin()
+    _, di, dv = eng.snapshot_fetch()
+    assert di.shape[0] == w3.shape[0] and di[-1] == w3.shape[0] - 1 and dv[-1] == w3.shape[0]
+    eng.set_weights(np.zeros(w3.shape[0]))
+    eng.snapshot_begin()
+    _, zi, zv = eng.snapshot_fetch()
+    assert zi.shape[0] == 0 and zv.shape[0] == 0
+
+
+def _run(tmp_path, interval, pool, n_batches, F=100_000_000):
+    from twitter_stream_ml_amd.apps.linear_regression import LinearRegressionJob, build_engine
+    from twitter_stream_ml_amd.config.arguments import ConfArguments
+    ck = str(tmp_path / f"ck{interval}")
+    conf = ConfArguments().parse(["--master", "rocm[1]", "-f", str(F), "--hash", "murmur3",
+                                  "--checkpoint", ck, "--checkpointInterval", str(interval),
+                                  "--batchSize", str(pool[0].n)])
+    eng = build_engine(conf, rank=0, world=1, max_rows=pool[0].n)
+    eng.set_weights(np.zeros(eng.num_weights))
+    job = LinearRegressionJob(conf, eng, None, 0, plot=False)
+    lat = []
+    for t in range(n_batches):
+        raw = pool[t % len(pool)].with_time(NOW + t * 5000)
+        nxt = pool[(t + 1) % len(pool)].with_time(NOW + (t + 1) * 5000)
+        t0 = time.perf_counter()
+        job.on_batch(SimpleNamespace(raw=raw), raw.batch_time_ms)
+        lat.append(time.perf_counter() - t0)
+        eng.prefetch(nxt)                       # the receiver's next batch, as the app's scheduler does
+    job.final_checkpoint()
+    ckp = job.checkpointer
+    w = eng.get_weights()
+    job.close()
+    del job, eng
+    import gc
+    gc.collect()
+    return np.asarray(lat), w, ck, ckp
+
+
+def test_async_checkpoint_p99_wide_1e8(hip_module, tmp_path):
+    from twitter_stream_ml_amd.checkpoint import load_linear_regression, load_progress
+    from twitter_stream_ml_amd.sources.synthetic import SyntheticReplaySource
+    rows, n = 500_000, 60
+    src = SyntheticReplaySource(SynthConfig.profile("wide", seed=22), batches=6, batch_rows=rows)
+    pool = list(src.pool)
+    warm = 8
+    lat0, w0, _, _ = _run(tmp_path, 0, pool, n)
+    lat1, w1, ck1, cp1 = _run(tmp_path, 1, pool, n)
+    np.testing.assert_array_equal(w0, w1)            # checkpoints never change the model
+    p99_0 = float(np.percentile(lat0[warm:], 99))
+    p99_1 = float(np.percentile(lat1[warm:], 99))
+    res = dict(p99_ms_no_ckpt=p99_0 * 1e3, p99_ms_ckpt1=p99_1 * 1e3,
+               p50_ms_no_ckpt=float(np.median(lat0[warm:])) * 1e3,
+               p50_ms_ckpt1=float(np.median(lat1[warm:])) * 1e3,
+               written=cp1.written, skipped=cp1.skipped, batches=n, rows=rows)
+    out = os.environ.get("TWTML_TEST_OUT")
+    if out:
+        os.makedirs(out, exist_ok=True)
+        with open(os.path.join(out, "ckpt_p99.json"), "w") as fh:
+            json.dump(res, fh)
+    print(res)
+    assert cp1.written >= 3, res
+    assert p99_1 <= 1.10 * p99_0, res
+    # the final (synchronous) checkpoint is the trained model, bit for bit
+    w_disk, _ = load_linear_regression(ck1)
+    np.testing.assert_array_equal(w_disk, w1)
+    assert load_progress(ck1)["batches"] == n

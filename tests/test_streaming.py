@@ -3,6 +3,7 @@ import threading
 import time
 
 import numpy as np
+import pytest
 
 from twitter_stream_ml_amd.records.batch import RawBatch
 from twitter_stream_ml_amd.runtime.streaming import StreamingContext
@@ -105,3 +106,31 @@ def test_time_sealed_batches_respect_engine_capacity():
     assert len(sizes) == 4 and _t.time() - t0 < 30   # sealed by capacity, not the 30 s timer
     assert all(0 < n <= 5000 and u <= 5000 * 120 for n, u in sizes), sizes
     assert ssc.capacity_seals >= 4
+
+
+def test_manual_clock_batch_times():
+    """spark.streaming.clock=ManualClock analogue: batch k has time
+    start + k * step whatever the wall clock does, and every poll inside it
+    reads that time (the age feature's reference point)."""
+    from twitter_stream_ml_amd.runtime.clock import ManualClock, SystemClock, streaming_clock
+    seen = []
+
+    class Src:
+        def poll(self, n, now_ms=None):
+            seen.append(now_ms)
+            return generate_batch(SynthConfig(seed=1), 0, n, batch_time_ms=now_ms)
+
+    ssc = StreamingContext(0, batch_size=500, num_batches=3, poll_chunk=200, clock=ManualClock(1000, 5000))
+    times = []
+    ssc.twitterStream(Src()).foreachRDD(lambda rdd, t: times.append(t))
+    ssc.start()
+    ssc.awaitTermination()
+    ssc.stop()
+    assert times == [1000, 6000, 11000]
+    assert seen[:3] == [1000, 1000, 1000] and seen[3] == 6000   # 200 + 200 + 100 rows, then the next batch
+    assert isinstance(streaming_clock(""), SystemClock)
+    c = streaming_clock("manual:7:3")
+    c.advance()
+    assert c.now_ms() == 10
+    with pytest.raises(ValueError):
+        streaming_clock("manual:1")

@@ -3,6 +3,7 @@ from __future__ import annotations
 
 import logging
 import os
+import threading
 from dataclasses import dataclass
 from typing import Callable, Optional
 
@@ -44,18 +45,43 @@ def load_resume_state(resume: str, checkpoint: str, rank: int) -> ResumeState:
 
 class StreamCheckpointer:
     """Every ``interval`` batches: each rank records its stream position, a
-    barrier, then rank 0 atomically replaces the model directory (with
-    ``streaming/progress.json``).  A crash at any point leaves a model whose
-    batch count every rank can resume from."""
+    barrier, then rank 0 takes a snapshot of the model and replaces the model
+    directory (with ``streaming/progress.json``) atomically.  A crash at any
+    point leaves a model whose batch count every rank can resume from
+    (positions keep a history, ``checkpoint/stream_state.py``).
+
+    ``snapshot()`` runs on the training thread between two batches and
+    returns ``save(path, progress)``.  With ``asynchronous`` (the default)
+    ``save`` runs on a writer thread while the next batches train: for the
+    device LR engine the snapshot is a device-side compaction of the non-zero
+    weights and ``save`` copies just those pairs to the host (its own stream)
+    and writes the parquet file -- nothing of size F touches the training
+    thread (an F = 1e8 checkpoint used to copy 800 MB and scan it
+    on the host inside the batch).  One write is in flight at most: a
+    checkpoint that comes due while the previous one is still being written
+    is skipped (positions are still recorded; the next due batch snapshots
+    the newest model), so training never waits on the disk -- with
+    ``--checkpointInterval 1`` the model on disk is as fresh as the writer
+    can keep it.  The final checkpoint (``force``) waits and is synchronous.
+    Errors of a background write are raised at the next checkpoint or at
+    :meth:`flush`."""
 
     def __init__(self, path: str, interval: int, rank: int,
-                 save_model: Callable[[str, dict], None], barrier: Callable[[], None]):
+                 snapshot: Callable[[], Callable[[str, dict], None]], barrier: Callable[[], None],
+                 asynchronous: Optional[bool] = None):
         self.path = path
         self.interval = int(interval)
         self.rank = rank
-        self.save_model = save_model
+        self.snapshot = snapshot
         self.barrier = barrier
+        if asynchronous is None:
+            asynchronous = os.environ.get("TWTML_CHECKPOINT_ASYNC", "1") != "0"
+        self.asynchronous = bool(asynchronous)
         self.positions = StreamPositions(path, rank) if path else None
+        self._thread: Optional[threading.Thread] = None
+        self._error: Optional[BaseException] = None
+        self.written = 0          # checkpoints completed (rank 0)
+        self.skipped = 0          # due while the previous write was in flight (rank 0)
 
     def after_batch(self, batches: int, records: int, count: int, force: bool = False) -> bool:
         if not self.path:
@@ -65,9 +91,47 @@ class StreamCheckpointer:
         self.positions.record(batches, records)
         self.barrier()
         if self.rank == 0:
-            self.save_model(self.path, {"batches": int(batches), "count": int(count)})
-            log.info("checkpoint written to %s after %d batches", self.path, batches)
+            progress = {"batches": int(batches), "count": int(count)}
+            if self.asynchronous and not force:
+                if self._thread is not None and self._thread.is_alive():
+                    self.skipped += 1
+                    log.debug("checkpoint after batch %d skipped: the previous write is in flight", batches)
+                    return False
+                self._wait_writer()
+                save = self.snapshot()
+                t = threading.Thread(target=self._write, args=(save, progress, batches),
+                                     name="twtml-checkpoint", daemon=True)
+                self._thread = t
+                t.start()
+            else:
+                self._wait_writer()
+                self._write(self.snapshot(), progress, batches)
+                self._raise_error()
         return True
+
+    def flush(self) -> None:
+        """Wait for a background write (end of run) and raise its error."""
+        self._wait_writer()
+
+    def _write(self, save, progress: dict, batches: int) -> None:
+        try:
+            save(self.path, progress)
+            self.written += 1
+            log.info("checkpoint written to %s after %d batches", self.path, batches)
+        except BaseException as e:   # surfaced on the training thread
+            self._error = e
+
+    def _wait_writer(self) -> None:
+        t = self._thread
+        if t is not None:
+            t.join()
+            self._thread = None
+        self._raise_error()
+
+    def _raise_error(self) -> None:
+        if self._error is not None:
+            e, self._error = self._error, None
+            raise RuntimeError(f"checkpoint write to {self.path} failed: {e}") from e
 
 
 def make_watchdog(timeout_s: float, comm=None) -> Optional[Watchdog]:

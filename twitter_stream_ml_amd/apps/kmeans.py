@@ -96,8 +96,7 @@ class KMeansJob:
         self.check_every = getattr(args, "checkReplicas", 0) if args is not None else 0
         self.checkpointer = StreamCheckpointer(
             ckpt, interval, rank,
-            lambda path, prog: StreamingKMeansModel(*self.engine.get_state()).save(path, prog),
-            barrier)
+            self._snapshot, barrier)
         self.watchdog = make_watchdog(getattr(args, "batchTimeout", 0.0) if args is not None else 0.0,
                                       getattr(engine, "comm", None))
 
@@ -118,10 +117,21 @@ class KMeansJob:
             if self.watchdog is not None:
                 self.watchdog.disarm()
 
+    def _snapshot(self):
+        """k x d centres + k weights (small): copied on the training thread,
+        written on the checkpoint writer thread."""
+        model = StreamingKMeansModel(*[np.array(a, copy=True) for a in self.engine.get_state()])
+        return model.save
+
     def final_checkpoint(self) -> None:
+        self.checkpointer.flush()
         self.checkpointer.after_batch(self.batches, self.records, self.count, force=True)
 
     def close(self) -> None:
+        try:
+            self.checkpointer.flush()   # never leave a checkpoint half-written behind
+        except Exception as e:
+            log.error("%s", e)
         if self.watchdog is not None:
             self.watchdog.close()
 
@@ -149,6 +159,7 @@ class KMeansJob:
 
 def main(argv: Optional[List[str]] = None) -> int:
     setup_logging()
+    from ..runtime.clock import streaming_clock
     rest = load_java_opts(list(sys.argv[1:] if argv is None else argv))
     args = parse_args(rest)
     log.info("Loading application config...")
@@ -174,7 +185,8 @@ def main(argv: Optional[List[str]] = None) -> int:
     ssc = StreamingContext(args.seconds, batch_size=args.batchSize, num_batches=remaining,
                            app_name=APP_NAME,
                            max_batch_rows=int(getattr(cap, "max_rows", 0) or 0),
-                           max_batch_units=int(getattr(cap, "max_units", 0) or 0))
+                           max_batch_units=int(getattr(cap, "max_units", 0) or 0),
+                           clock=streaming_clock())
     log.info("Initializing Twitter stream...")
     stream = ssc.twitterStream(make_source(args.source, rate=args.sourceRate, seed=args.seed,
                                            shard=info.rank, num_shards=info.world,

@@ -41,6 +41,7 @@ from ..models.linear_regression import CpuLinearRegression, CpuLRConfig, LinearR
 from ..models.mllib_helper import MllibHelper
 from ..parallel.dist import barrier, broadcast_flag, check_replicas, gather_to_main
 from ..utils.faults import maybe_inject
+from ..checkpoint.saveable import SparseWeights
 from ._common import ResumeState, StreamCheckpointer, load_resume_state, make_watchdog
 from ..oracle.mllib import round_half_up
 from ..records.batch import RETWEET_COUNT
@@ -123,10 +124,8 @@ class LinearRegressionJob:
         self.metrics = metrics or MetricsLogger(None)
         self.last = None
         self.diverged = 0    # batches on which the model was found diverged (training stopped)
-        self.checkpointer = StreamCheckpointer(
-            conf.checkpoint, conf.checkpointInterval, rank,
-            lambda path, prog: LinearRegressionModel(self.engine.get_weights(), 0.0).save(path, prog),
-            barrier)
+        self.checkpointer = StreamCheckpointer(conf.checkpoint, conf.checkpointInterval, rank,
+                                               self._snapshot, barrier)
         self.watchdog = make_watchdog(conf.batchTimeout, getattr(engine, "comm", None))
 
     def on_batch(self, rdd, time_ms: int) -> None:
@@ -231,20 +230,42 @@ class LinearRegressionJob:
                  rec["tweets_per_s"])
         return rec
 
+    def _snapshot(self):
+        """Checkpoint snapshot on the training thread; the returned save runs
+        on the checkpoint writer thread.  Device engine: the non-zero weights
+        are compacted on the GPU behind the last batch and only they are
+        copied (csrc/hip/snapshot.hip); CPU engine: a copy of the weights."""
+        eng = self.engine
+        if hasattr(eng, "snapshot_begin"):
+            eng.snapshot_begin()
+
+            def save(path, prog):
+                size, idx, val = eng.snapshot_fetch()
+                LinearRegressionModel.save_sparse(path, SparseWeights(size, idx, val), 0.0, prog)
+            return save
+        w = np.array(eng.get_weights(), dtype=np.float64, copy=True)
+        return lambda path, prog: LinearRegressionModel(w, 0.0).save(path, prog)
+
     def _kept_mask(self, raw):
         rc = raw.scalars[RETWEET_COUNT]
         return (raw.is_retweet != 0) & (rc >= self.conf.numRetweetBegin) & (rc <= self.conf.numRetweetEnd)
 
     def final_checkpoint(self) -> None:
+        self.checkpointer.flush()
         self.checkpointer.after_batch(self.batches, self.records, self.count, force=True)
 
     def close(self) -> None:
+        try:
+            self.checkpointer.flush()   # never leave a checkpoint half-written behind
+        except Exception as e:
+            log.error("%s", e)
         if self.watchdog is not None:
             self.watchdog.close()
 
 
 def main(argv: Optional[List[str]] = None) -> int:
     setup_logging()
+    from ..runtime.clock import streaming_clock
     args = load_java_opts(list(sys.argv[1:] if argv is None else argv))
     log.info("Parsing applications arguments")
     conf = ConfArguments().setAppName(APP_NAME).parse(args)
@@ -281,7 +302,8 @@ def main(argv: Optional[List[str]] = None) -> int:
     ssc = StreamingContext(conf.seconds, batch_size=conf.batchSize, num_batches=remaining,
                            app_name=conf.appName(),
                            max_batch_rows=int(getattr(cap, "max_rows", 0) or 0),
-                           max_batch_units=int(getattr(cap, "max_units", 0) or 0))
+                           max_batch_units=int(getattr(cap, "max_units", 0) or 0),
+                           clock=streaming_clock())
     log.info("Initializing Twitter stream...")
     stream = ssc.twitterStream(make_source(conf.source, rate=conf.sourceRate, seed=conf.seed,
                                            shard=rank, num_shards=world,

@@ -42,7 +42,7 @@ import numpy as np
 import pyarrow as pa
 import pyarrow.parquet as pq
 
-__all__ = ["save_linear_regression", "load_linear_regression", "save_kmeans", "load_kmeans",
+__all__ = ["SparseWeights", "save_linear_regression", "load_linear_regression", "save_kmeans", "load_kmeans",
            "LR_CLASS", "KMEANS_CLASS", "vector_udt_type"]
 
 LR_CLASS = "org.apache.spark.mllib.regression.LinearRegressionModel"
@@ -81,12 +81,42 @@ def _spark_row_metadata(fields) -> dict:
     return {b"org.apache.spark.sql.parquet.row.metadata": json.dumps(js, separators=(",", ":")).encode()}
 
 
+class SparseWeights:
+    """A weight vector held as its non-zeros: ``size``, int32 ``indices``
+    (ascending) and fp64 ``values`` -- what the device snapshot delivers
+    (``DeviceLinearRegression.snapshot_fetch``), saved without densifying."""
+
+    def __init__(self, size: int, indices: np.ndarray, values: np.ndarray):
+        self.size = int(size)
+        self.indices = np.asarray(indices, np.int32)
+        self.values = np.asarray(values, np.float64)
+        if self.indices.shape != self.values.shape:
+            raise ValueError("indices / values length mismatch")
+
+    def dense(self) -> np.ndarray:
+        d = np.zeros(self.size, np.float64)
+        d[self.indices] = self.values
+        return d
+
+
 def _udt_array(vecs, sparse_density: float = SPARSE_DENSITY) -> pa.StructArray:
     """VectorUDT column of ``vecs`` from numpy buffers (no Python floats)."""
     types, sizes, size_null = [], [], []
     iv, io, inull = [], [0], []
     vv, vo = [], [0]
     for v in vecs:
+        if isinstance(v, SparseWeights):
+            if v.size > 0 and v.indices.shape[0] < sparse_density * v.size:
+                types.append(0)
+                sizes.append(v.size)
+                size_null.append(False)
+                iv.append(v.indices)
+                vv.append(v.values)
+                inull.append(False)
+                io.append(io[-1] + v.indices.shape[0])
+                vo.append(vo[-1] + v.values.shape[0])
+                continue
+            v = v.dense()
         v = np.asarray(v, dtype=np.float64)
         nz = np.flatnonzero(v)
         sparse = v.shape[0] > 0 and nz.shape[0] < sparse_density * v.shape[0]
@@ -185,13 +215,15 @@ def _read_data(path: str) -> pa.Table:
     return pa.concat_tables([pq.read_table(os.path.join(d, f)) for f in files])
 
 
-def save_linear_regression(path: str, weights: np.ndarray, intercept: float = 0.0,
+def save_linear_regression(path: str, weights, intercept: float = 0.0,
                            progress: Optional[dict] = None) -> None:
-    w = np.asarray(weights, dtype=np.float64)
+    """``weights``: a dense vector or :class:`SparseWeights`."""
+    w = weights if isinstance(weights, SparseWeights) else np.asarray(weights, dtype=np.float64)
+    size = w.size if isinstance(w, SparseWeights) else int(w.shape[0])
     schema = pa.schema([pa.field("weights", vector_udt_type()), pa.field("intercept", pa.float64(), nullable=False)],
                        metadata=_spark_row_metadata([("weights", "vector", True), ("intercept", "double", False)]))
     table = pa.Table.from_arrays([_udt_array([w]), pa.array([float(intercept)], pa.float64())], schema=schema)
-    _write_dir(path, {"class": LR_CLASS, "version": "1.0", "numFeatures": int(w.shape[0])}, table,
+    _write_dir(path, {"class": LR_CLASS, "version": "1.0", "numFeatures": size}, table,
                {"progress.json": progress} if progress else None)
 
 

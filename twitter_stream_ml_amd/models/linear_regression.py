@@ -61,6 +61,12 @@ class LinearRegressionModel:
         from ..checkpoint.saveable import save_linear_regression
         save_linear_regression(path, self.weights, self.intercept, progress)
 
+    @staticmethod
+    def save_sparse(path: str, weights, intercept: float = 0.0, progress: Optional[dict] = None) -> None:
+        """Save weights given as ``checkpoint.SparseWeights`` (non-zeros only)."""
+        from ..checkpoint.saveable import save_linear_regression
+        save_linear_regression(path, weights, intercept, progress)
+
     @classmethod
     def load(cls, path: str) -> "LinearRegressionModel":
         from ..checkpoint.saveable import load_linear_regression

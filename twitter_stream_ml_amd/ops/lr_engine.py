@@ -258,6 +258,19 @@ class DeviceLinearRegression:
     def get_weights(self) -> np.ndarray:
         return np.asarray(self._eng.get_weights())
 
+    def snapshot_begin(self) -> None:
+        """Non-blocking checkpoint, part 1 (training thread, between batches):
+        the device compacts the non-zero weights behind the last batch
+        (``csrc/hip/snapshot.hip``); nothing is copied yet."""
+        self._eng.snapshot_begin()
+
+    def snapshot_fetch(self):
+        """Part 2 (any thread, e.g. a checkpoint writer): ``(size, indices,
+        values)`` of the begun snapshot -- only the non-zero weights cross
+        PCIe, on the engine's snapshot stream, while training goes on."""
+        idx, val = self._eng.snapshot_fetch()
+        return self.num_weights, np.asarray(idx), np.asarray(val)
+
     def set_weights(self, w: np.ndarray) -> None:
         w = np.ascontiguousarray(w, dtype=np.float64)
         if w.shape != (self.num_weights,):

@@ -39,6 +39,7 @@ from dataclasses import dataclass, field
 from typing import Any, Callable, List, Optional
 
 from ..records.batch import RawBatch
+from .clock import SystemClock
 from .rdd import RDD
 
 __all__ = ["StreamingContext", "DStream", "ReceiverDStream", "Accumulator", "BatchInfo",
@@ -172,7 +173,7 @@ class StreamingContext:
 
     def __init__(self, batch_seconds: float = 5.0, batch_size: int = 0, num_batches: int = 0,
                  app_name: str = "", poll_chunk: int = 4096, max_pending: int = 8,
-                 max_batch_rows: int = 0, max_batch_units: int = 0):
+                 max_batch_rows: int = 0, max_batch_units: int = 0, clock=None):
         if batch_seconds <= 0 and batch_size <= 0:
             raise ValueError("need batch_seconds > 0 or batch_size > 0")
         self.batch_seconds = float(batch_seconds)
@@ -183,6 +184,7 @@ class StreamingContext:
         self.max_pending = int(max_pending)
         self.max_batch_rows = int(max_batch_rows)
         self.max_batch_units = int(max_batch_units)
+        self.clock = clock or SystemClock()   # batch times (runtime/clock.py)
         if self.batch_size > 0 and self.max_batch_rows > 0 and self.batch_size > self.max_batch_rows:
             raise ValueError(f"batch_size {self.batch_size} exceeds the engine capacity {self.max_batch_rows}")
         self._buffered_units = 0
@@ -256,10 +258,12 @@ class StreamingContext:
         src = self._inputs[0].source
         out = []
         for _ in range(n):
-            t_ms = now_ms() if now_ms else int(time.time() * 1000)
+            t_ms = now_ms() if now_ms else self.clock.now_ms()
             size = self.batch_size if self.batch_size > 0 else self.poll_chunk
             batch = src.poll(size, now_ms=t_ms)
             batch.batch_time_ms = t_ms
+            if not now_ms:
+                self.clock.advance()
             out.append(self.run_batch(batch))
         return out
 
@@ -288,7 +292,7 @@ class StreamingContext:
                     self._capacity_seal()
                     continue
             try:
-                chunk = src.poll(want, now_ms=int(time.time() * 1000))
+                chunk = src.poll(want, now_ms=self.clock.now_ms())
             except Exception as e:  # receiver restart semantics: log and retry
                 log.warning("receiver error, restarting: %s", e)
                 time.sleep(0.5)
@@ -320,7 +324,8 @@ class StreamingContext:
             parts, self._buffer, self._buffered = self._buffer, [], 0
             self._buffered_units = 0
             self._sealed += 1
-        t_ms = int(time.time() * 1000)
+            t_ms = self.clock.now_ms()
+            self.clock.advance()
         batch = RawBatch.concat(parts, t_ms) if parts else RawBatch.empty(t_ms)
         batch.batch_time_ms = t_ms
         self._jobs.put((batch, BatchInfo(t_ms, batch.n, time.monotonic())))
