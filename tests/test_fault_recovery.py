@@ -25,9 +25,9 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, argv, fault):
+def _rank_main(rank, world, port, argv, fault, ck_async="1"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), TWTML_CHECKPOINT_ASYNC=ck_async)
     if fault:
         os.environ["TWTML_FAULT"] = fault
     else:
@@ -40,8 +40,8 @@ def _rank_main(rank, world, port, argv, fault):
         raise SystemExit(rc)
 
 
-def _run(world, argv, fault=None):
-    mp.start_processes(_rank_main, args=(world, _free_port(), argv, fault), nprocs=world,
+def _run(world, argv, fault=None, ck_async="1"):
+    mp.start_processes(_rank_main, args=(world, _free_port(), argv, fault, ck_async), nprocs=world,
                        join=True, start_method="spawn")
 
 
@@ -52,22 +52,30 @@ def _argv(ck, batches=6):
             "--checkpoint", str(ck), "--checkpointInterval", "1", "--checkReplicas", "1"]
 
 
-def test_kill_rank_then_resume_equals_uninterrupted(tmp_path):
+@pytest.mark.parametrize("ck_async", ["0", "1"], ids=["sync", "async"])
+def test_kill_rank_then_resume_equals_uninterrupted(tmp_path, ck_async):
+    """Synchronous checkpoints leave batch 3 (the last batch every rank
+    finished) on disk.  Asynchronous ones skip a checkpoint that comes due
+    while the previous write is in flight, so the model on disk is from some
+    batch 1..3 -- resume must continue exactly from whichever it is."""
     world = 2
     ref = tmp_path / "ref"
-    _run(world, _argv(ref))
+    _run(world, _argv(ref), ck_async=ck_async)
     w_ref, _ = load_linear_regression(str(ref))
     assert load_progress(str(ref))["batches"] == 6
 
     ck = tmp_path / "ck"
     with pytest.raises(Exception):
-        _run(world, _argv(ck), fault="rank=1,batch=4,kind=exit")
+        _run(world, _argv(ck), fault="rank=1,batch=4,kind=exit", ck_async=ck_async)
     prog = load_progress(str(ck))
-    assert prog["batches"] == 3                     # last batch every rank finished
+    if ck_async == "0":
+        assert prog["batches"] == 3                 # last batch every rank finished
+    else:
+        assert 1 <= prog["batches"] <= 3
     w3, _ = load_linear_regression(str(ck))
     assert not np.array_equal(w3, w_ref)
 
-    _run(world, _argv(ck) + ["--resume", "auto"])   # restart: continue at batch 4
+    _run(world, _argv(ck) + ["--resume", "auto"], ck_async=ck_async)   # restart: continue
     w, _ = load_linear_regression(str(ck))
     assert load_progress(str(ck)) == load_progress(str(ref))
     np.testing.assert_array_equal(w[:-1], w_ref[:-1])        # text + 3 count features

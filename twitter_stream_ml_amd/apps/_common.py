@@ -10,7 +10,8 @@ from typing import Callable, Optional
 from ..checkpoint import StreamPositions, load_progress, resolve_resume
 from ..utils.faults import EXIT_HUNG, Watchdog
 
-__all__ = ["ResumeState", "load_resume_state", "StreamCheckpointer", "make_watchdog"]
+__all__ = ["ResumeState", "load_resume_state", "StreamCheckpointer", "make_watchdog",
+           "exit_on_sigterm"]
 
 log = logging.getLogger("twtml.apps")
 
@@ -132,6 +133,24 @@ class StreamCheckpointer:
         if self._error is not None:
             e, self._error = self._error, None
             raise RuntimeError(f"checkpoint write to {self.path} failed: {e}") from e
+
+
+def exit_on_sigterm() -> None:
+    """Turn SIGTERM into ``SystemExit`` on the main thread, so the drivers'
+    ``finally`` blocks run: a launcher that tears the job down after a peer
+    rank failed (torchrun, ``torch.multiprocessing``) sends SIGTERM first,
+    and an asynchronous checkpoint write still in flight must complete
+    (:meth:`StreamCheckpointer.flush`) rather than die with the process --
+    otherwise the newest checkpoint on disk can be far older than the last
+    batch every rank finished."""
+    import signal
+    if threading.current_thread() is not threading.main_thread():
+        return
+
+    def _term(signum, frame):
+        raise SystemExit(128 + signum)
+
+    signal.signal(signal.SIGTERM, _term)
 
 
 def make_watchdog(timeout_s: float, comm=None) -> Optional[Watchdog]:

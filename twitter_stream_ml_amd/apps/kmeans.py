@@ -33,7 +33,8 @@ from ..runtime.streaming import StreamingContext
 from ..sources import make_source
 from ..utils.faults import maybe_inject
 from ..utils.logging import setup_logging
-from ._common import ResumeState, StreamCheckpointer, load_resume_state, make_watchdog
+from ._common import (ResumeState, StreamCheckpointer, exit_on_sigterm, load_resume_state,
+                      make_watchdog)
 
 __all__ = ["main", "KMeansJob", "build_kmeans_engine"]
 
@@ -159,6 +160,7 @@ class KMeansJob:
 
 def main(argv: Optional[List[str]] = None) -> int:
     setup_logging()
+    exit_on_sigterm()
     from ..runtime.clock import streaming_clock
     rest = load_java_opts(list(sys.argv[1:] if argv is None else argv))
     args = parse_args(rest)

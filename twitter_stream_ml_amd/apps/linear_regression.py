@@ -42,7 +42,8 @@ from ..models.mllib_helper import MllibHelper
 from ..parallel.dist import barrier, broadcast_flag, check_replicas, gather_to_main
 from ..utils.faults import maybe_inject
 from ..checkpoint.saveable import SparseWeights
-from ._common import ResumeState, StreamCheckpointer, load_resume_state, make_watchdog
+from ._common import (ResumeState, StreamCheckpointer, exit_on_sigterm, load_resume_state,
+                      make_watchdog)
 from ..oracle.mllib import round_half_up
 from ..records.batch import RETWEET_COUNT
 from ..report.session_stats import SessionStats
@@ -265,6 +266,7 @@ class LinearRegressionJob:
 
 def main(argv: Optional[List[str]] = None) -> int:
     setup_logging()
+    exit_on_sigterm()
     from ..runtime.clock import streaming_clock
     args = load_java_opts(list(sys.argv[1:] if argv is None else argv))
     log.info("Parsing applications arguments")
