@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
+#include <cstdlib>
+#include <cstring>
 
 #include "common.h"
 #include "kernels.h"
@@ -138,9 +140,129 @@ __global__ __launch_bounds__(kBlock) void k_km_features_chunk(DevRawBatch b, con
   }
 }
 
+// Lane-private variant (0 < text_dims <= kKmLaneDims, config 4's 62 dims):
+// the chunk's 16 rows are staged as above, but each row is split into 4
+// contiguous segments, one per lane (lanes 4q..4q+3 own row q), and every
+// lane counts into its OWN histogram copy: u16 bins packed two per dword,
+// copies kKmLaneStride(td) dwords apart (odd: lanes hitting the same bin
+// land in different banks).  The increments are fire-and-forget ds_add_u32
+// on distinct addresses -- no same-address serialisation, which is what the
+// shared per-row histogram paid when 64 lanes hashed one row's bigrams into
+// 62 bins (787 us, 463 GB/s).  The 4 copies of a row are summed
+// when the chunk's 16 feature rows are written (coalesced).  A lane's count
+// is <= its segment length (< 2^16), the sum <= the row length.
+constexpr int kKmLaneDims = 64;
+__host__ __device__ constexpr int km_lane_stride(int td) { return ((td + 1) / 2) | 1; }
+
+__global__ __launch_bounds__(kBlock) void k_km_features_lanes(DevRawBatch b, const int64_t* kept,
+                                                              const int64_t* counters, float* X,
+                                                              int dp, int text_dims,
+                                                              const uint8_t* lpage,
+                                                              const uint16_t* lblocks) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem_l[];
+  __shared__ __attribute__((aligned(16))) uint8_t lpage_s[256];
+  __shared__ __attribute__((aligned(16))) uint16_t lblk_s[kLowerLdsBlocks * 256];
+  stage_lower_tables(lpage_s, lblk_s, lpage, lblocks, threadIdx.x, kBlock);
+  __syncthreads();
+  const LowerLds lt{lpage_s, lblk_s, lblocks};
+  const int lane = lane_id(), w = threadIdx.x / kWave;
+  const int hs = km_lane_stride(text_dims);
+  const int hwords = (kWave * hs + 3) & ~3;                 // per wave, uint4-aligned
+  const int wbase = w * (kRowsPerChunk * kStageStride + 3 + hwords);
+  uint32_t* st = smem_l + wbase;
+  // index arithmetic on the LDS array itself (an integer round trip of the
+  // pointer would lose the address space: flat atomics instead of ds_add)
+  uint32_t* hist = smem_l + ((wbase + kRowsPerChunk * kStageStride + 3) & ~3);
+  uint32_t* mine = hist + lane * hs;
+  const int64_t n_kept = counters[0];
+  const int64_t nch = (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;
+  const FastMod32 fm{static_cast<uint32_t>(text_dims)};
+  const int q = lane >> 2, sub = lane & 3;
+  for (int64_t c = int64_t(blockIdx.x) * kKmFeatWaves + w; c < nch;
+       c += int64_t(gridDim.x) * kKmFeatWaves) {
+    const int64_t mk = c * kRowsPerChunk + (lane & 15);
+    const bool mvalid = mk < n_kept;
+    const int64_t mrow = mvalid ? kept[mk] : 0;
+    const float mx0 = mvalid ? float(raw_scalar(b, 0, mrow)) : 0.f;   // retweetCount
+    const float mx1 = mvalid ? float(raw_scalar(b, 1, mrow)) : 0.f;   // followersCount
+    const StageMeta meta = stage_meta(b, mvalid, mrow);
+    for (int i = lane; i < hwords / 4; i += kWave) reinterpret_cast<uint4*>(hist)[i] = make_uint4(0, 0, 0, 0);
+    stage_rows(b, meta, st, lane);                // includes the fence + wave barrier
+    {
+      const StagedRow sr = staged_row(meta, st, q);
+      const bool valid = c * kRowsPerChunk + q < n_kept;
+      const int len = valid ? int(sr.rt.len) : 0;
+      const int nz = len >= 2 ? len - 1 : len;
+      const int j0 = (nz * sub) >> 2, j1 = (nz * (sub + 1)) >> 2;
+      if (len == 1 && sub == 0) {
+        const uint32_t bin = fm.mod(sr.unit(b, 0, lt));
+        __hip_atomic_fetch_add(mine + (bin >> 1), 1u << ((bin & 1) * 16), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+      } else if (len >= 2 && j1 > j0) {
+        uint32_t u0 = sr.unit(b, j0, lt);
+        int j = j0;
+        for (; j + 4 <= j1; j += 4) {            // 4 independent reads, then 4 adds
+          uint32_t u[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) u[t] = sr.unit(b, j + 1 + t, lt);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const uint32_t bin = fm.mod(31u * (t == 0 ? u0 : u[t - 1]) + u[t]);
+            __hip_atomic_fetch_add(mine + (bin >> 1), 1u << ((bin & 1) * 16), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+          u0 = u[3];
+        }
+        for (; j < j1; ++j) {
+          const uint32_t u1 = sr.unit(b, j + 1, lt);
+          const uint32_t bin = fm.mod(31u * u0 + u1);
+          __hip_atomic_fetch_add(mine + (bin >> 1), 1u << ((bin & 1) * 16), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+          u0 = u1;
+        }
+      }
+    }
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+    // 16 consecutive rows x dp floats, contiguous in X: bin = the 4 copies' sum
+    const int64_t k0 = c * kRowsPerChunk;
+    const int nrows = int(n_kept - k0 < kRowsPerChunk ? n_kept - k0 : kRowsPerChunk);
+    float* xc = X + k0 * dp;
+    for (int i = lane; i < nrows * dp; i += kWave) {
+      const int r = i / dp, col = i - r * dp;
+      if (col < 2) continue;                      // scalar columns below
+      float v = 0.f;
+      if (col < 2 + text_dims) {
+        const int bin = col - 2, sh = (bin & 1) * 16;
+        const uint32_t* h4 = hist + (4 * r) * hs + (bin >> 1);
+        v = float(((h4[0] >> sh) & 0xFFFFu) + ((h4[hs] >> sh) & 0xFFFFu) +
+                  ((h4[2 * hs] >> sh) & 0xFFFFu) + ((h4[3 * hs] >> sh) & 0xFFFFu));
+      }
+      xc[i] = v;
+    }
+    if (lane < nrows) {
+      xc[int64_t(lane) * dp + 0] = mx0;
+      xc[int64_t(lane) * dp + 1] = mx1;
+    }
+    __builtin_amdgcn_wave_barrier();   // LDS reuse by the next chunk
+  }
+}
+
 void launch_km_features(const DevRawBatch& b, const int64_t* kept, const int64_t* counters,
                         float* X, int dp, int text_dims, const uint8_t* lpage,
                         const uint16_t* lblocks, int64_t max_rows, hipStream_t s) {
+  if (text_dims > 0 && text_dims <= kKmLaneDims) {
+    const int64_t nch = (max_rows + kRowsPerChunk - 1) / kRowsPerChunk;
+    int grid = int((nch + kKmFeatWaves - 1) / kKmFeatWaves);
+    if (grid < 1) grid = 1;
+    if (grid > 2048) grid = 2048;
+    const int hwords = (kWave * km_lane_stride(text_dims) + 3) & ~3;
+    const size_t lds = size_t(kKmFeatWaves) * size_t(kRowsPerChunk * kStageStride + 3 + hwords) *
+                       sizeof(uint32_t);
+    hipLaunchKernelGGL(k_km_features_lanes, dim3(grid), dim3(kBlock), lds, s, b, kept, counters, X,
+                       dp, text_dims, lpage, lblocks);
+    return;
+  }
   if (text_dims <= kKmChunkDims) {
     const int64_t nch = (max_rows + kRowsPerChunk - 1) / kRowsPerChunk;
     int grid = int((nch + kKmFeatWaves - 1) / kKmFeatWaves);
@@ -516,6 +638,148 @@ __global__ __launch_bounds__(kBlock) void k_km_assign_bf16x3(const float* X, con
   }
 }
 
+// The same bf16x3 assignment with the centre fragments shared through LDS
+// (the default for 16 <= dp <= 128).  k_km_assign_bf16x3 has every wave
+// fetch every tile's fragments from L2 (8 KB per tile per wave at d = 64:
+// ~4 GB of L2 reads per 1M points x 1024 centres) and wait on them right
+// before its MFMAs -- 545 us at 1.8 waves/SIMD.  Here the
+// workgroup's 4 waves load a tile once, cooperatively, one tile AHEAD into
+// registers (2 x 16 B per thread), park it in a double-buffered LDS slot
+// (one barrier per tile), and each wave reads its A operands with
+// conflict-free ds_read_b128 just before the MFMAs that use them.  The
+// epilogue and the near-tie routing are k_km_assign_bf16x3's: a top-4, so
+// the twin / triplet centres that repeated dying-cluster splits leave behind
+// go to the 2-3 candidate refine (a top-3 sent the triplets to the full
+// refine: +620 us per batch on the wide profile).
+template <int DP, int NB>
+__global__ __launch_bounds__(kBlock) void k_km_assign_bf16x3_lds(const float* X, const float* fac,
+                                                                 const int64_t* counters,
+                                                                 const uint16_t* frag,
+                                                                 const float* cnp, int ntiles,
+                                                                 int lbits, int32_t* labels,
+                                                                 int32_t* refine,
+                                                                 unsigned long long* refine_cnt,
+                                                                 int64_t R) {
+  static_assert(DP % 16 == 0, "bf16x3 path needs DP % 16 == 0");
+  constexpr int KB = DP / 16;
+  constexpr int TILE_V = KB * 2 * kWave;                 // bf16x8 vectors per tile
+  constexpr int PER_T = (TILE_V + kBlock - 1) / kBlock;  // per thread per tile
+  __shared__ bf16x8 fs[2][TILE_V];
+  __shared__ float cs[2][32];
+  const int lane = lane_id(), h = lane >> 5;
+  const int64_t n = counters[0];
+  const int64_t pb = int64_t(blockIdx.x) * (kBlock / kWave) * (32 * NB);
+  if (pb >= n) return;                                   // block-uniform
+  const int64_t p0 = pb + int64_t(threadIdx.x / kWave) * (32 * NB);
+  const bf16x8* F = reinterpret_cast<const bf16x8*>(frag);
+  bf16x8 pre[PER_T];
+  float pc = 0.f;
+  auto fetch = [&](int tile) {
+#pragma unroll
+    for (int j = 0; j < PER_T; ++j) {
+      const int v = threadIdx.x + j * kBlock;
+      if (v < TILE_V) pre[j] = F[int64_t(tile) * TILE_V + v];
+    }
+    if (threadIdx.x < 32) pc = cnp[tile * 32 + threadIdx.x];
+  };
+  auto park = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < PER_T; ++j) {
+      const int v = threadIdx.x + j * kBlock;
+      if (v < TILE_V) fs[buf][v] = pre[j];
+    }
+    if (threadIdx.x < 32) cs[buf][threadIdx.x] = pc;
+  };
+  fetch(0);
+  bf16x8 xh[NB][KB], xl[NB][KB];
+  float xn[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const int64_t p = p0 + 32 * b + (lane & 31);
+    xn[b] = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+      const int col = 16 * kb + 8 * h;
+      float v[8];
+      if (p < n) {
+        const float4 a = *reinterpret_cast<const float4*>(X + p * DP + col);
+        const float4 c = *reinterpret_cast<const float4*>(X + p * DP + col + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = c.x; v[5] = c.y; v[6] = c.z; v[7] = c.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float x = v[j] * fac[col + j];
+        xn[b] += x * x;
+        const uint16_t hi = km_f2bf(x);
+        xh[b][kb][j] = short(hi);
+        xl[b][kb][j] = short(km_f2bf(x - km_bf2f(hi)));
+      }
+    }
+    xn[b] += __shfl_xor(xn[b], 32, kWave);
+  }
+  park(0);
+  __syncthreads();
+  const uint32_t imask = (1u << lbits) - 1u;
+  KmKeys4 t[NB];
+  for (int tile = 0; tile < ntiles; ++tile) {
+    const int buf = tile & 1;
+    if (tile + 1 < ntiles) fetch(tile + 1);              // in flight during this tile
+    f32x16 acc[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[b] = f32x16{};
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+      const bf16x8 ah = fs[buf][(kb * 2) * kWave + lane];
+      const bf16x8 al = fs[buf][(kb * 2 + 1) * kWave + lane];
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, xh[b][kb], acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, xl[b][kb], acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, xh[b][kb], acc[b], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int cl = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const float dist = fmaf(-2.f, acc[b][r], cs[buf][cl]);
+        t[b].add(__uint_as_float((__float_as_uint(dist) & ~imask) | uint32_t(tile * 32 + cl)));
+      }
+    }
+    if (tile + 1 < ntiles) park(buf ^ 1);   // its readers finished at the last barrier
+    __syncthreads();
+  }
+  const float q = ldexpf(1.f, lbits - 21);   // 4 key quanta, relative
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    float o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = __shfl_xor(t[b].b[j], 32, kWave);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) t[b].add(o[j]);
+    const int64_t p = p0 + 32 * b + (lane & 31);
+    if (h != 0 || p >= n) continue;
+    const float* k4 = t[b].b;
+    const int i1 = int(__float_as_uint(k4[0]) & imask);
+    labels[p] = i1;
+    const float m = 1e-4f * (3.f * xn[b] + fabsf(k4[0]) + cnp[i1]) + q * fabsf(k4[0]) + 1e-30f;
+    if (k4[1] - k4[0] > m) continue;
+    if (k4[3] - k4[0] <= m) {
+      refine[atomicAdd(&refine_cnt[0], 1ull)] = int32_t(p);
+    } else {
+      const int64_t qn = int64_t(atomicAdd(&refine_cnt[1], 1ull));
+      refine[R + qn] = int32_t(p);
+      reinterpret_cast<int4*>(refine + 2 * R)[qn] =
+          make_int4(i1, int(__float_as_uint(k4[1]) & imask),
+                    k4[2] - k4[0] <= m ? int(__float_as_uint(k4[2]) & imask) : -1, -1);
+    }
+  }
+}
+
 // Generic fallback (any width): one thread per point, scalar fp32.
 __global__ __launch_bounds__(kBlock) void k_km_assign_scalar(const float* X, const float* fac,
                                                              const int64_t* counters,
@@ -616,6 +880,15 @@ void launch_km_assign(const float* X, const float* f32, const double* f64, const
     int gs = int((int64_t(ntiles) * (dp / 16) * kWave + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(k_km_split_bf16, dim3(gs < 1024 ? gs : 1024), dim3(kBlock), 0, s, C, cnorm, k,
                        dp, ntiles, frag, cnp);
+#define KM_BF16L(DPV, NBV)                                                                         \
+  case DPV: {                                                                                      \
+    const int64_t waves = (max_rows + 32 * NBV - 1) / (32 * NBV);                                  \
+    hipLaunchKernelGGL((k_km_assign_bf16x3_lds<DPV, NBV>), dim3(int((waves + 3) / 4)), dim3(kBlock), \
+                       0, s, X, f32, counters, frag, cnp, ntiles, lbits, labels, refine, refine_cnt, \
+                       R);                                                                         \
+    done = true;                                                                                   \
+    break;                                                                                         \
+  }
 #define KM_BF16(DPV, NBV)                                                                          \
   case DPV: {                                                                                      \
     const int64_t waves = (max_rows + 32 * NBV - 1) / (32 * NBV);                                  \
@@ -624,8 +897,23 @@ void launch_km_assign(const float* X, const float* f32, const double* f64, const
     done = true;                                                                                   \
     break;                                                                                         \
   }
-    switch (dp) { KM_BF16(16, 2) KM_BF16(32, 2) KM_BF16(64, 2) KM_BF16(128, 1) default: break; }
+    // TWTML_KM_ASSIGN: lds (default), lds1 (one 32-point block per wave), reg
+    // (per-wave L2 fragment loads, the round-2 kernel) -- for A/B runs
+    static const int variant = [] {
+      const char* e = std::getenv("TWTML_KM_ASSIGN");
+      if (e && std::strcmp(e, "reg") == 0) return 0;
+      if (e && std::strcmp(e, "lds1") == 0) return 2;
+      return 1;
+    }();
+    if (variant == 0) {
+      switch (dp) { KM_BF16(16, 2) KM_BF16(32, 2) KM_BF16(64, 2) KM_BF16(128, 1) default: break; }
+    } else if (variant == 2) {
+      switch (dp) { KM_BF16L(16, 1) KM_BF16L(32, 1) KM_BF16L(64, 1) KM_BF16L(128, 1) default: break; }
+    } else {
+      switch (dp) { KM_BF16L(16, 2) KM_BF16L(32, 2) KM_BF16L(64, 2) KM_BF16L(128, 1) default: break; }
+    }
 #undef KM_BF16
+#undef KM_BF16L
   }
   if (mfma && !done) {
 #define KM_MFMA(DPV)                                                                                \

@@ -203,6 +203,16 @@ std::vector<int32_t> KMEngine::debug_labels() const {
   return out;
 }
 
+std::vector<float> KMEngine::debug_features() const {
+  TWTML_HIP_CHECK(hipSetDevice(device_));
+  TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
+  int64_t n = 0;
+  TWTML_HIP_CHECK(hipMemcpy(&n, prep_.counters, sizeof(int64_t), hipMemcpyDeviceToHost));
+  std::vector<float> out(size_t(std::max<int64_t>(n, 0)) * size_t(dp_));
+  if (n > 0) TWTML_HIP_CHECK(hipMemcpy(out.data(), X_, sizeof(float) * out.size(), hipMemcpyDeviceToHost));
+  return out;
+}
+
 void KMEngine::get_state(double* centers, double* weights) const {
   TWTML_HIP_CHECK(hipSetDevice(device_));
   TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
@@ -271,6 +281,17 @@ void bind_kmeans(py::module_& m) {
           v = e.debug_labels();
         }
         return py::array_t<int32_t>(py::ssize_t(v.size()), v.data());
+      })
+      .def("debug_features", [](const KMEngine& e) {
+        std::vector<float> v;
+        {
+          py::gil_scoped_release nogil;
+          v = e.debug_features();
+        }
+        const py::ssize_t dp = py::ssize_t(e.dp());
+        py::array_t<float> a({py::ssize_t(v.size()) / dp, dp});
+        std::copy(v.begin(), v.end(), a.mutable_data());
+        return a;
       })
       .def_property_readonly("k", &KMEngine::k)
       .def_property_readonly("d", &KMEngine::d);

@@ -44,8 +44,11 @@ class KMEngine {
   // Debug/test: the labels left by the last process() (the update's
   // assignment with the old centres when want_labels was false).
   std::vector<int32_t> debug_labels() const;
+  // Debug/test: the unscaled fp32 feature rows [n_local][dp] of the last batch.
+  std::vector<float> debug_features() const;
   int k() const { return cfg_.k; }
   int d() const { return d_; }
+  int dp() const { return dp_; }
   void synchronize();
 
  private:

@@ -201,6 +201,20 @@ def test_kmeans_utf8_ingest_equals_wire(hip_module):
         b.set_state(ca, wa)
 
 
+def _split_twins(C, w):
+    """Cluster pairs made by a dying-cluster split in the last update: equal
+    weights and centres 2e-14 (relative) apart (``kmeans_update``)."""
+    order = np.argsort(w, kind="stable")
+    ws = w[order]
+    out = []
+    for i in np.flatnonzero(ws[1:] == ws[:-1]):
+        a, b = int(order[i]), int(order[i + 1])
+        tol = 1e-12 * max(1.0, float(np.abs(C[a]).max()))
+        if ws[i] > 0 and np.abs(C[a] - C[b]).max() <= tol:
+            out.append((a, b))
+    return out
+
+
 def _gap_check(X, C, rel=1e-9, chunk=16384):
     """Per point: the two nearest centres (fp64, |x|^2 - 2 x.c + |c|^2 in
     chunks) and whether the best / second gap is resolvable."""
@@ -252,8 +266,14 @@ def test_kmeans_config4_bench_scale_matches_oracle(hip_module):
         bad = ~ok_c | ~ok_g | (top_c[:, 0] != top_g[:, 0])
         tainted[top_c[bad].ravel()] = True
         tainted[top_g[bad].ravel()] = True
-        clean = ~tainted
         c, w = dev.get_state()
+        # a dying-cluster split gives the dying cluster half of the largest
+        # one's weight: a tainted largest taints its (point-less) partner
+        for cc, ww in ((c, w), (cpu.state.centers, cpu.state.weights)):
+            for a, b in _split_twins(cc, ww):
+                if tainted[a] or tainted[b]:
+                    tainted[a] = tainted[b] = True
+        clean = ~tainted
         print(f"batch {t}: ill/disagreeing points {int(bad.sum())}, tainted clusters {int(tainted.sum())}")
         assert tainted.mean() < 0.05, int(tainted.sum())
         np.testing.assert_allclose(w.sum(), cpu.state.weights.sum(), rtol=1e-12)
@@ -266,3 +286,19 @@ def test_kmeans_config4_bench_scale_matches_oracle(hip_module):
         pred = np.asarray(r["pred"])
         sel = ok_n & clean[top_n[:, 0]]
         assert np.count_nonzero(pred[sel] != top_n[sel, 0]) == 0
+
+
+@pytest.mark.parametrize("text_dims", [1, 8, 14, 62, 64, 65, 126])
+def test_kmeans_features_exact(hip_module, text_dims):
+    """The device feature rows (before scaling) equal the host featurizer's
+    exactly: the lane-private histogram kernel (text_dims <= 64, config 4's
+    62) and the shared-histogram kernel above it; padding columns are 0."""
+    from twitter_stream_ml_amd.ops.kmeans_engine import DeviceKMeans
+    dev = DeviceKMeans(_cfg(16, text_dims, seed=3), device=0)
+    for raw in _batches(n=2, rows=6000, seed=33, unicode_fraction=0.4):
+        dev.update_raw(raw, want_pred=False)
+        got = np.asarray(dev._eng.debug_features())
+        want, _ = kmeans_features(raw, text_dims)
+        assert got.shape[0] == want.shape[0]
+        np.testing.assert_array_equal(got[:, :2 + text_dims], want.astype(np.float32))
+        assert not got[:, 2 + text_dims:].any()
