@@ -7,7 +7,7 @@ import sys
 
 src = sys.argv[1]
 flt = sys.argv[2] if len(sys.argv) > 2 else ""
-cmd = ["hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-munsafe-fp-atomics", "-ffp-contract=fast",
+cmd = ["hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-munsafe-fp-atomics", "-ffp-contract=fast", *(["-mllvm", "-amdgpu-mfma-vgpr-form"] if src.endswith("kmeans.hip") else []),
        "-Wno-unused-result", "-fvisibility=hidden", "-I/opt/rocm/include", "-Icsrc", "-x", "hip", "-c", src,
        "-o", "/tmp/resusage.o", "-Rpass-analysis=kernel-resource-usage"]
 out = subprocess.run(cmd, capture_output=True, text=True).stderr
