@@ -33,9 +33,21 @@ struct LowerLds {
   const uint16_t* blocks;   // LDS [kLowerLdsBlocks][256]
   const uint16_t* gblocks;  // global, all blocks
   __device__ __forceinline__ uint32_t lower(uint32_t c) const {
-    if (c < 128) return (c >= 'A' && c <= 'Z') ? c + 32 : c;
+    return lower_any(c);
+  }
+  // Any unit (ASCII included: page 0's block lower-cases A-Z) without a
+  // branch in the common case.  The LDS read is unconditional (clamped
+  // block) and only the rare block beyond LDS reads global memory: written
+  // as `blk < N ? lds[..] : global[..]` the compiler merges the two into ONE
+  // flat load of a selected address -- a vector-memory round trip, waited
+  // on, for every unit (measured: the k-means featurizer at 630 us).
+  __device__ __forceinline__ uint32_t lower_any(uint32_t c) const {
     const uint32_t blk = page[c >> 8];
-    const uint32_t d = blk < uint32_t(kLowerLdsBlocks) ? blocks[blk * 256 + (c & 255)] : gblocks[blk * 256 + (c & 255)];
+    const uint32_t i = (blk < uint32_t(kLowerLdsBlocks) ? blk : 0u) * 256u + (c & 255u);
+    uint32_t d = blocks[i];
+    // (a relaxed atomic load: not mergeable with the LDS load above)
+    if (blk >= uint32_t(kLowerLdsBlocks))
+      d = __hip_atomic_load(gblocks + (blk * 256 + (c & 255)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return (c + d) & 0xFFFFu;
   }
 };

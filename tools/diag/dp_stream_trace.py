@@ -25,11 +25,11 @@ out = [[] for _ in range(WORLD)]
 def worker(r):
     eng = engines[r]
     shards = [b.shard(r, WORLD) for b in batches]
-    for sh in shards[:eng.raw_slots - 1]:
-        eng.prefetch(sh)
+    nxt = 0   # next shard to prefetch: strictly in order, stop at the first refusal
     for t, sh in enumerate(shards):
-        if t + eng.raw_slots - 1 < NB:
-            eng.prefetch(shards[t + eng.raw_slots - 1])
+        nxt = max(nxt, t + 1)
+        while nxt < NB and nxt <= t + eng.raw_slots - 1 and eng.prefetch(shards[nxt]):
+            nxt += 1
         res = eng.train_batch(sh, want_pred=False)
         out[r].append((res["iterations"], round(res["prep_ms"], 3), round(res["train_ms"], 3)))
 

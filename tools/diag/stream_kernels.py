@@ -8,8 +8,8 @@ import sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 by = collections.defaultdict(collections.Counter)
 for r in rows:
-    name = re.sub(r"\(.*$", "", r["Kernel_Name"]).replace("void ", "").replace("twtml::", "")
-    name = re.sub(r"\(anonymous namespace\)::", "", name)
+    name = re.sub(r"\(anonymous namespace\)::", "", r["Kernel_Name"])
+    name = re.sub(r"\(.*$", "", name).replace("void ", "").replace("twtml::", "")
     by[(r["Agent_Id"], r["Queue_Id"], r["Stream_Id"])][name] += 1
 PREP = re.compile(r"k_cesu|k_featurize|k_remap|k_tier|k_far_csc|k_code_table|k_hot_select|k_row_normalize|"
                   r"k_filter|k_sort|k_union|k_compact|k_pack_c1|k_batch_bounds")

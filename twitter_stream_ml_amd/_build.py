@@ -110,6 +110,10 @@ def hipcc() -> str:
 
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
              "-ffp-contract=fast", "-Wno-unused-result"]
+# Per-source extras.  kmeans.hip: MFMA accumulators in VGPRs (the k-means
+# assignment reads every accumulator on the VALU after each tile; AGPR
+# accumulators cost a v_accvgpr_read per value -- 16 of ~128 VALU per tile).
+HIP_FILE_FLAGS = {"kmeans.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
 
 
 def build_hip(force: bool = False, verbose: bool = False) -> str:
@@ -135,7 +139,8 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
                 cmd = [cc, "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", *inc, *extra,
                        "-c", src, "-o", obj]
             else:
-                cmd = [cc, *HIP_FLAGS, "-fvisibility=hidden", *inc, *extra, "-c", src, "-o", obj]
+                cmd = [cc, *HIP_FLAGS, *HIP_FILE_FLAGS.get(os.path.basename(src), []), "-fvisibility=hidden",
+                       *inc, *extra, "-c", src, "-o", obj]
             _run(cmd, verbose)
         return obj
 
