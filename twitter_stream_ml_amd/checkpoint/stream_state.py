@@ -25,8 +25,11 @@ class StreamPositions:
         self.dir = os.path.abspath(checkpoint) + ".stream"
         self.path = os.path.join(self.dir, f"rank-{int(rank)}.json")
         self.keep = int(keep)
+        self._h: Optional[Dict[int, int]] = None   # this rank's history (it is the only writer)
 
     def history(self) -> Dict[int, int]:
+        if self._h is not None:
+            return dict(self._h)
         try:
             with open(self.path) as fh:
                 return {int(k): int(v) for k, v in json.load(fh).items()}
@@ -34,6 +37,8 @@ class StreamPositions:
             return {}
 
     def record(self, batches: int, records: int) -> None:
+        # kept in memory after the first read: with --checkpointInterval 1 this
+        # runs on the training thread every batch (one small atomic write, no read)
         h = self.history()
         h[int(batches)] = int(records)
         for k in sorted(h)[:-self.keep]:
@@ -43,6 +48,7 @@ class StreamPositions:
         with os.fdopen(fd, "w") as fh:
             json.dump({str(k): v for k, v in sorted(h.items())}, fh)
         os.replace(tmp, self.path)
+        self._h = h
 
     def records_at(self, batches: int) -> Optional[int]:
         return self.history().get(int(batches))
