@@ -702,32 +702,46 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
     const int64_t pos = c * kRowsPerChunk + r;
     const int64_t off = cb * kChunkStride + lane * kGroup;
     const RowIn ri = row_in(p, pos, t);
-    // far entries of the chunk: their row sums land in lane t == 0 of the row
+    // The chunk's hot block and cold slots are loaded first: their latency
+    // then overlaps the far forward's two dependent round trips below.
+    uint4 hv = make_uint4(0, 0, 0, 0);
+    uint2 v[kMaxColdGroups];
+    // cold stream: L8c groups of kColdGroup slots per lane (hot_split.hip)
+    const uint16_t* csl = p.cslot + cb * kChunkStride + lane * kColdGroup;
+    const bool reg = L8c >= 0 && L8c <= kMaxColdGroups;
+    if (L8c >= 0) {
+      hv = hdense[c * kWave + lane];
+      if (reg) {
+#pragma unroll
+        for (int g = 0; g < kMaxColdGroups; ++g)
+          if (g < L8c) v[g] = *reinterpret_cast<const uint2*>(csl + int64_t(g) * kColdStride);
+      }
+    }
+    // far entries of the chunk: their row sums land in lane t == 0 of the row;
+    // up to 4 list entries per lane in flight, then their weight gathers
     int32_t far = 0;
     if (TIERED && fc > 0 && abl != 8) {   // wave-uniform (ablate 8: no far forward)
       int32_t* fd = fdot[w];
       if (lane < kRowsPerChunk) fd[lane] = 0;
       wave_lds_sync();
       const uint32_t* fl = p.fslot + cb * kChunkStride;
-      for (int32_t k0 = 0; k0 < fc; k0 += kWave)
-        if (k0 + lane < fc) {
-          const uint32_t e = fl[k0 + lane];
-          atomicAdd(&fd[e >> 28], w_to_fix(d.wc32[e & 0x0FFFFFFFu], sc.wscale));   // ds_add_u32: exact
-        }
+      constexpr int kFarU = 4;
+      for (int32_t k0 = 0; k0 < fc; k0 += kFarU * kWave) {
+        uint32_t e[kFarU];
+        float fw[kFarU];
+#pragma unroll
+        for (int u = 0; u < kFarU; ++u) e[u] = k0 + u * kWave + lane < fc ? fl[k0 + u * kWave + lane] : 0xFFFFFFFFu;
+#pragma unroll
+        for (int u = 0; u < kFarU; ++u) fw[u] = e[u] != 0xFFFFFFFFu ? d.wc32[e[u] & 0x0FFFFFFFu] : 0.f;
+#pragma unroll
+        for (int u = 0; u < kFarU; ++u)
+          if (e[u] != 0xFFFFFFFFu) atomicAdd(&fd[e[u] >> 28], w_to_fix(fw[u], sc.wscale));   // ds_add_u32: exact
+      }
       wave_lds_sync();
       if (t == 0) far = fd[r];
     }
     if (L8c >= 0) {
-      const uint4 hv = hdense[c * kWave + lane];
-      // cold stream: L8c groups of kColdGroup slots per lane (hot_split.hip)
-      const uint16_t* sl = p.cslot + cb * kChunkStride + lane * kColdGroup;
-      const bool reg = L8c <= kMaxColdGroups;
-      uint2 v[kMaxColdGroups];
-      if (reg) {
-#pragma unroll
-        for (int g = 0; g < kMaxColdGroups; ++g)
-          if (g < L8c) v[g] = *reinterpret_cast<const uint2*>(sl + int64_t(g) * kColdStride);
-      }
+      const uint16_t* sl = csl;
       int32_t d0 = hot_dot(hv, wq), d1 = far;   // partial sums of the row's int32 dot
       if (reg) {
 #pragma unroll
