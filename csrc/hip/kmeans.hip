@@ -160,10 +160,16 @@ __global__ __launch_bounds__(kBlock) void k_km_features_chunk(DevRawBatch b, con
 // SIMD).  Rejected: one row per lane reading global memory (TA-bound, 64
 // rows' byte loads per instruction: 832 us) or LDS (64 rows' staging halves
 // the occupancy: 1225 us).
-constexpr int kKmStageDw = 1536;   // staged dwords per wave (6 KB; a chunk needs ~700)
+// LDS per wave: the staged rows, the 16 rows' histograms as u16 count pairs
+// (a row has < 2^13 bytes), row metadata: 7.1 KB at td = 62, so with the
+// lower-case tables a workgroup is exactly 32 KB and 5 fit a CU (round 3's
+// first cut, a 6 KB stage + u32 bins, fitted 3).
+constexpr int kKmStageDw = 1216;   // staged dwords per wave (4.75 KB; wide chunks: p50 3.5 KB, p99 4.8 KB)
+
+__host__ __device__ constexpr int km_hist_words(int td) { return (td + 1) / 2; }
 
 __host__ __device__ constexpr int km_bal_wave_dwords(int td) {
-  return kKmStageDw + kRowsPerChunk * td + kRowsPerChunk * 4 + kRowsPerChunk * 2;
+  return kKmStageDw + kRowsPerChunk * km_hist_words(td) + kRowsPerChunk * 4 + kRowsPerChunk * 2;
 }
 
 __global__ __launch_bounds__(kBlock) void k_km_features_bal(DevRawBatch b, const int64_t* kept,
@@ -179,8 +185,9 @@ __global__ __launch_bounds__(kBlock) void k_km_features_bal(DevRawBatch b, const
   const int lane = lane_id(), w = threadIdx.x / kWave;
   const int td = text_dims;
   uint32_t* st = smem_b + w * km_bal_wave_dwords(td);      // staged bytes (4-B aligned rows)
-  uint32_t* hist = st + kKmStageDw;                          // [16][td]
-  int32_t* meta = reinterpret_cast<int32_t*>(hist + kRowsPerChunk * td);   // [16][4]
+  const int hw = km_hist_words(td);
+  uint32_t* hist = st + kKmStageDw;                          // [16][hw]: bin b in the half b & 1 of word b >> 1
+  int32_t* meta = reinterpret_cast<int32_t*>(hist + kRowsPerChunk * hw);   // [16][4]
   int64_t* mo = reinterpret_cast<int64_t*>(meta + kRowsPerChunk * 4);       // [16] row byte offsets
   const uint8_t* stb = reinterpret_cast<const uint8_t*>(st);
   const int64_t n_kept = counters[0];
@@ -228,29 +235,34 @@ __global__ __launch_bounds__(kBlock) void k_km_features_bal(DevRawBatch b, const
       mo[lane] = o;
     }
     const int T = __shfl(snz, kRowsPerChunk - 1, kWave);
-    for (int i = lane; i < kRowsPerChunk * td; i += kWave) hist[i] = 0u;
-    // stage: up to 3 dwords per lane per row, all 48 loads in flight first
-    {
-      uint32_t tmp[kRowsPerChunk][3];
+    for (int i = lane; i < kRowsPerChunk * hw; i += kWave) hist[i] = 0u;
+    // stage: up to 3 dwords per lane per row, 8 rows' 24 loads in flight at a
+    // time (all 16 rows' took 48 VGPRs: occupancy was VGPR-bound)
+    constexpr int kHalf = kRowsPerChunk / 2;
+#pragma unroll 1
+    for (int h0 = 0; h0 < kRowsPerChunk; h0 += kHalf) {
+      uint32_t tmp[kHalf][3];
 #pragma unroll
-      for (int q = 0; q < kRowsPerChunk; ++q) {
+      for (int qq = 0; qq < kHalf; ++qq) {
+        const int q = h0 + qq;
         const int64_t qa = __shfl(al, q, kWave);
         const int qn = __shfl(staged ? ndw : 0, q, kWave);
         const uint32_t* src = reinterpret_cast<const uint32_t*>(b.text + qa);
 #pragma unroll
-        for (int k = 0; k < 3; ++k) tmp[q][k] = (lane + kWave * k < qn) ? src[lane + kWave * k] : 0u;
+        for (int k = 0; k < 3; ++k) tmp[qq][k] = (lane + kWave * k < qn) ? src[lane + kWave * k] : 0u;
       }
       // lower-cased on the way into LDS (every dword of a row is independent
       // work here: no dependent table reads left in the bigram walk below)
 #pragma unroll
-      for (int q = 0; q < kRowsPerChunk; ++q) {
+      for (int qq = 0; qq < kHalf; ++qq) {
+        const int q = h0 + qq;
         const int qn = __shfl(staged ? ndw : 0, q, kWave);
         const int qd = __shfl(dw0, q, kWave);
         const int qw = __shfl(wide, q, kWave);
 #pragma unroll
         for (int k = 0; k < 3; ++k)
           if (lane + kWave * k < qn) {
-            const uint32_t v = tmp[q][k];
+            const uint32_t v = tmp[qq][k];
             uint32_t lv;
             if (qw) {
               lv = lt.lower_any(v & 0xFFFFu) | (lt.lower_any(v >> 16) << 16);
@@ -292,11 +304,12 @@ __global__ __launch_bounds__(kBlock) void k_km_features_bal(DevRawBatch b, const
       j = g - meta[4 * q + 0];
       uint32_t u0 = unit(j);
       while (true) {
-        const int rq = q * td;
+        const int rq = q * hw;
         const uint32_t u1 = (rk & 2) ? 0u : unit(j + 1);
         const uint32_t h = (rk & 2) ? u0 : 31u * u0 + u1;
         const uint32_t bin = one ? 0u : h - __umulhi(h, mg) * tdu;
-        __hip_atomic_fetch_add(hist + rq + int(bin), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(hist + rq + int(bin >> 1), 1u << ((bin & 1u) * 16), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
         if (++g >= g1) break;
         if (++j < rnz) {
           u0 = u1;                               // (a 1-unit row has rnz = 1: never here)
@@ -307,7 +320,69 @@ __global__ __launch_bounds__(kBlock) void k_km_features_bal(DevRawBatch b, const
         }
       }
     };
-    if (all_staged) walk(std::true_type{});
+    // Staged chunks: the lane's range is walked by kCur independent cursors in
+    // lock step, so kCur LDS unit reads and kCur histogram adds are in flight
+    // per step (the single walk was one dependent read -> hash -> ds_add
+    // chain per bigram, at ~2.5 waves per SIMD).
+    auto walk_multi = [&]() {
+      constexpr int kCur = 4;
+      int cg[kCur], ce[kCur], cq[kCur], cj[kCur], cn[kCur], cb[kCur], ck[kCur];
+      uint32_t cu[kCur];
+#pragma unroll
+      for (int i = 0; i < kCur; ++i) {
+        cg[i] = g0 + int((int64_t(g1 - g0) * i) / kCur);
+        ce[i] = g0 + int((int64_t(g1 - g0) * (i + 1)) / kCur);
+        int qq = 0;
+#pragma unroll
+        for (int k = 0; k < kRowsPerChunk; ++k) qq += (cg[i] >= __builtin_amdgcn_readlane(snz, k)) ? 1 : 0;
+        qq = qq < kRowsPerChunk ? qq : kRowsPerChunk - 1;
+        cq[i] = qq;
+        cn[i] = meta[4 * qq + 1];
+        cb[i] = max(meta[4 * qq + 2], 0);   // (-1: an invalid row, only under an empty cursor)
+        ck[i] = meta[4 * qq + 3];
+        cj[i] = cg[i] - meta[4 * qq + 0];
+        const int wd = ck[i] & 1;
+        const int jj = cg[i] < ce[i] ? cj[i] : 0;
+        cu[i] = wd ? uint32_t(*reinterpret_cast<const uint16_t*>(stb + cb[i] + 2 * jj)) : uint32_t(stb[cb[i] + jj]);
+      }
+      while (true) {
+        bool live = false;
+#pragma unroll
+        for (int i = 0; i < kCur; ++i) live |= cg[i] < ce[i];
+        if (!live) break;
+        uint32_t u1[kCur];
+#pragma unroll
+        for (int i = 0; i < kCur; ++i) {   // unconditional reads (clamped): all in flight together
+          const int wd = ck[i] & 1;
+          const int jj = (cg[i] < ce[i] && !(ck[i] & 2)) ? cj[i] + 1 : 0;
+          u1[i] = wd ? uint32_t(*reinterpret_cast<const uint16_t*>(stb + cb[i] + 2 * jj)) : uint32_t(stb[cb[i] + jj]);
+        }
+#pragma unroll
+        for (int i = 0; i < kCur; ++i) {
+          if (cg[i] >= ce[i]) continue;
+          const uint32_t v1 = (ck[i] & 2) ? 0u : u1[i];
+          const uint32_t h = (ck[i] & 2) ? cu[i] : 31u * cu[i] + v1;
+          const uint32_t bin = one ? 0u : h - __umulhi(h, mg) * tdu;
+          __hip_atomic_fetch_add(hist + cq[i] * hw + int(bin >> 1), 1u << ((bin & 1u) * 16), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (++cg[i] >= ce[i]) continue;
+          if (++cj[i] < cn[i]) {
+            cu[i] = v1;
+          } else {                                 // next row with bigrams
+            do {
+              ++cq[i];
+              cn[i] = meta[4 * cq[i] + 1];
+            } while (cn[i] == 0);
+            cb[i] = meta[4 * cq[i] + 2];
+            ck[i] = meta[4 * cq[i] + 3];
+            cj[i] = 0;
+            const int wd = ck[i] & 1;
+            cu[i] = wd ? uint32_t(*reinterpret_cast<const uint16_t*>(stb + cb[i])) : uint32_t(stb[cb[i]]);
+          }
+        }
+      }
+    };
+    if (all_staged) walk_multi();
     else walk(std::false_type{});
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
@@ -318,7 +393,10 @@ __global__ __launch_bounds__(kBlock) void k_km_features_bal(DevRawBatch b, const
     int r = 0, col = lane;                        // i = r * dp + col, advanced without divisions
     while (col >= dp) { col -= dp; ++r; }
     for (int i = lane; i < nrows * dp; i += kWave) {
-      if (col >= 2) xc[i] = col < 2 + td ? float(hist[r * td + col - 2]) : 0.f;   // scalars below
+      if (col >= 2) {   // scalars below
+        const int b = col - 2;
+        xc[i] = b < td ? float((hist[r * hw + (b >> 1)] >> ((b & 1) * 16)) & 0xFFFFu) : 0.f;
+      }
       col += kWave;
       while (col >= dp) { col -= dp; ++r; }
     }

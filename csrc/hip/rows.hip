@@ -64,8 +64,11 @@ struct RowNorm {
 
 __device__ __forceinline__ uint32_t unit_at(const uint8_t* text, int64_t o, int64_t i) {
   const uint8_t* p = text + o + 2 * i;   // wide rows may start at any byte
+  if ((o & 1) == 0) return *reinterpret_cast<const uint16_t*>(p);   // one load when aligned
   return uint32_t(p[0]) | (uint32_t(p[1]) << 8);
 }
+
+constexpr int kScanRows = 8;   // wide rows whose pass-1 loads are in flight together
 
 // 0 = neither, 1 = case-ignorable, 2 = cased (unicode_tables.h kCaseRanges)
 __device__ int case_class(const DevCaseTables& ct, uint32_t cp) {
@@ -140,24 +143,56 @@ __global__ __launch_bounds__(256) void k_row_normalize(RowNorm a) {
     uint64_t m = __ballot(in && (fl & kRowWide));
     int n_low = 0, n_nar = 0;
     while (m) {
-      const int l = __builtin_ctzll(m);
-      m &= m - 1;
-      const int64_t o = readlane64(s0, l), e = readlane64(s1, l), w0 = readlane64(wo, l);
-      const int64_t len = (e - o) >> 1;
-      // pass 1: max unit (narrowing) and special units
-      uint32_t orv = 0;
-      bool sp = false;
-      for (int64_t i0 = 0; i0 < len; i0 += kWave) {
-        const int64_t i = i0 + lane;
-        if (i < len) {
-          const uint32_t u = unit_at(a.text, o, i);
-          orv |= u;
-          sp |= u == 0x130u || u == 0x3A3u;
-          if (is_high(u) && i + 1 < len && supp_high_mapped(u)) sp |= is_low(unit_at(a.text, o, i + 1));
+      // pass 1 over up to kScanRows wide rows at once (their unit loads all
+      // in flight together: one row at a time left this kernel latency-bound,
+      // a memory round trip per row): max unit (narrowing) and special units
+      int nr = 0;
+      int ls[kScanRows];
+      int64_t os[kScanRows], lens[kScanRows];
+      int64_t lmax = 0;
+#pragma unroll
+      for (int q = 0; q < kScanRows; ++q) {
+        ls[q] = -1;
+        os[q] = 0;
+        lens[q] = 0;
+        if (m) {
+          const int l = __builtin_ctzll(m);
+          m &= m - 1;
+          ls[q] = l;
+          os[q] = readlane64(s0, l);
+          lens[q] = (readlane64(s1, l) - os[q]) >> 1;
+          lmax = std::max(lmax, lens[q]);
+          ++nr;
         }
       }
-      orv = wave_or(orv);
-      const bool special = __any(sp);
+      uint32_t orq[kScanRows];
+      bool spq[kScanRows];
+#pragma unroll
+      for (int q = 0; q < kScanRows; ++q) {
+        orq[q] = 0;
+        spq[q] = false;
+      }
+      for (int64_t i0 = 0; i0 < lmax; i0 += kWave) {
+        const int64_t i = i0 + lane;
+        uint32_t u[kScanRows];
+#pragma unroll
+        for (int q = 0; q < kScanRows; ++q) u[q] = i < lens[q] ? unit_at(a.text, os[q], i) : 0u;
+#pragma unroll
+        for (int q = 0; q < kScanRows; ++q) {
+          orq[q] |= u[q];
+          spq[q] |= u[q] == 0x130u || u[q] == 0x3A3u;
+          if (is_high(u[q]) && i + 1 < lens[q] && supp_high_mapped(u[q]))
+            spq[q] |= is_low(unit_at(a.text, os[q], i + 1));
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < kScanRows; ++q) {
+      if (q >= nr) break;   // wave-uniform; q is a constant after unrolling (no scratch arrays)
+      const int l = ls[q];
+      const int64_t o = os[q], len = lens[q];
+      const int64_t e = o + 2 * len, w0 = readlane64(wo, l);
+      const uint32_t orv = wave_or(orq[q]);
+      const bool special = __any(spq[q]);
       int64_t ns0 = o, ns1 = e;
       bool narrowed = false;
       if (a.narrow && orv < 256u) {
@@ -203,6 +238,7 @@ __global__ __launch_bounds__(256) void k_row_normalize(RowNorm a) {
         s0 = ns0;
         s1 = ns1;
         if (narrowed) fl = uint8_t(fl & ~kRowWide);
+      }
       }
     }
     if (in) {
