@@ -298,70 +298,112 @@ __device__ __forceinline__ uint32_t byte_bits(uint32_t x) {
   return (x * 0x10204080u) >> 28;   // the four products land on bits 28..31, no carries
 }
 
-// Decode row [o, e) (class 1 or 2) to dst (tail + 2 o); returns its units.
+// One decode step of row [o, e) (class 1 or 2, output at text + d0): the
+// lane's aligned dword v of the row at w0 + 4 lane (and the next one, v2,
+// for the continuation bytes of its leads); k = the row's units so far.
 // A lane takes an aligned dword of the row per step (256 bytes per wave
-// step: a tweet is one or two steps) plus the next dword for the
-// continuation bytes of its leads.  A unit starts at every non-continuation
-// byte (two at a 4-byte lead: the surrogate pair); a lane's units (0..8) are
-// ranked across the wave from four ballots of their bit planes.
-template <typename Src>
-__device__ __forceinline__ int64_t decode_row(const Src& src, uint8_t* text, int64_t o, int64_t e, int64_t d0,
-                                              bool nar) {
+// step: a tweet is one or two steps).  A unit starts at every
+// non-continuation byte (two at a 4-byte lead: the surrogate pair); a lane's
+// units (0..8) are ranked across the wave from four ballots of their bit
+// planes.
+__device__ __forceinline__ void decode_step(uint8_t* text, int64_t o, int32_t ie, int64_t d0, bool nar,
+                                            int64_t w0, uint32_t v, uint32_t v2, int32_t& k) {
   uint16_t* dst = reinterpret_cast<uint16_t*>(text + d0);
   uint8_t* dst8 = text + d0;
   const int lane = lane_id();
   const uint64_t below = lanes_below();
+  const int32_t iw = int32_t(w0 - o) + 4 * lane;   // the lane's dword, relative to o (>= -3)
+  // bytes j of the dword inside the row: 0 <= iw + j < ie
+  const int32_t lo = iw < 0 ? -iw : 0;
+  const int32_t hi = ie - iw >= 4 ? 4 : (ie - iw < 0 ? 0 : ie - iw);
+  const uint32_t rng = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+  // a 4-byte lead also needs iw + j + 3 < ie
+  const int32_t h3 = ie - iw - 3;
+  const uint32_t rng3 = h3 >= 4 ? 0xFu : (h3 <= 0 ? 0u : (1u << h3) - 1u);
+  // lead: top two bits != 10; 4-byte lead: top nibble 1111 (SWAR over the dword)
+  const uint32_t t = ((v >> 6) & 0x03030303u) ^ 0x02020202u;
+  const uint32_t lead = byte_bits(((t + 0x7F7F7F7Fu) >> 7) & 0x01010101u) & rng;
+  const uint32_t f = ((v >> 4) & 0x0F0F0F0Fu) + 0x01010101u;
+  const uint32_t four = byte_bits((f >> 4) & 0x01010101u) & lead & rng3;
+  const uint32_t cnt = uint32_t(__popc(lead) + __popc(four));
+  const uint64_t p0 = __ballot(cnt & 1u), p1 = __ballot(cnt & 2u), p2 = __ballot(cnt & 4u),
+                 p3 = __ballot(cnt & 8u);
+  int32_t at = k + __popcll(p0 & below) + 2 * __popcll(p1 & below) + 4 * __popcll(p2 & below) +
+               8 * __popcll(p3 & below);
+  const uint64_t q = uint64_t(v) | (uint64_t(v2) << 32);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (!((lead >> j) & 1u)) continue;
+    const uint32_t c0 = uint32_t(q >> (8 * j)) & 0xFFu;
+    const uint32_t c1 = uint32_t(q >> (8 * j + 8)) & 0x3Fu;
+    const uint32_t c2 = uint32_t(q >> (8 * j + 16)) & 0x3Fu;
+    if ((four >> j) & 1u) {
+      const uint32_t c3 = uint32_t(q >> (8 * j + 24)) & 0x3Fu;
+      const uint32_t cp = ((c0 & 0x07u) << 18) | (c1 << 12) | (c2 << 6) | c3;
+      dst[at] = uint16_t(0xD800u + ((cp - 0x10000u) >> 10));
+      dst[at + 1] = uint16_t(0xDC00u + ((cp - 0x10000u) & 0x3FFu));
+      at += 2;
+    } else {
+      uint32_t u = c0;
+      if (c0 >= 0xE0u) u = ((c0 & 0x0Fu) << 12) | (c1 << 6) | c2;
+      else if (c0 >= 0x80u) u = ((c0 & 0x1Fu) << 6) | c1;
+      if (nar) dst8[at] = uint8_t(u);
+      else dst[at] = uint16_t(u);
+      at += 1;
+    }
+  }
+  k += __popcll(p0) + 2 * __popcll(p1) + 4 * __popcll(p2) + 8 * __popcll(p3);
+}
+
+// Decode row [o, e) (class 1 or 2) to dst (tail + 2 o); returns its units.
+template <typename Src>
+__device__ __forceinline__ int64_t decode_row(const Src& src, uint8_t* text, int64_t o, int64_t e, int64_t d0,
+                                              bool nar) {
   const int32_t ie = int32_t(e - o);   // row bytes (< 2^13)
   int32_t k = 0;
   for (int64_t w0 = o & ~int64_t(3); w0 < e; w0 += 4 * kWave) {
-    const int32_t iw = int32_t(w0 - o) + 4 * lane;   // the lane's dword, relative to o (>= -3)
+    const int32_t iw = int32_t(w0 - o) + 4 * lane_id();
     uint32_t v = 0, v2 = 0;
     if (iw < ie) {
-      v = src.dword(w0 + 4 * lane);
-      v2 = src.dword(w0 + 4 * lane + 4);
+      v = src.dword(w0 + 4 * lane_id());
+      v2 = src.dword(w0 + 4 * lane_id() + 4);
     }
-    // bytes j of the dword inside the row: 0 <= iw + j < ie
-    const int32_t lo = iw < 0 ? -iw : 0;
-    const int32_t hi = ie - iw >= 4 ? 4 : (ie - iw < 0 ? 0 : ie - iw);
-    const uint32_t rng = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
-    // a 4-byte lead also needs iw + j + 3 < ie
-    const int32_t h3 = ie - iw - 3;
-    const uint32_t rng3 = h3 >= 4 ? 0xFu : (h3 <= 0 ? 0u : (1u << h3) - 1u);
-    // lead: top two bits != 10; 4-byte lead: top nibble 1111 (SWAR over the dword)
-    const uint32_t t = ((v >> 6) & 0x03030303u) ^ 0x02020202u;
-    const uint32_t lead = byte_bits(((t + 0x7F7F7F7Fu) >> 7) & 0x01010101u) & rng;
-    const uint32_t f = ((v >> 4) & 0x0F0F0F0Fu) + 0x01010101u;
-    const uint32_t four = byte_bits((f >> 4) & 0x01010101u) & lead & rng3;
-    const uint32_t cnt = uint32_t(__popc(lead) + __popc(four));
-    const uint64_t p0 = __ballot(cnt & 1u), p1 = __ballot(cnt & 2u), p2 = __ballot(cnt & 4u),
-                   p3 = __ballot(cnt & 8u);
-    int32_t at = k + __popcll(p0 & below) + 2 * __popcll(p1 & below) + 4 * __popcll(p2 & below) +
-                 8 * __popcll(p3 & below);
-    const uint64_t q = uint64_t(v) | (uint64_t(v2) << 32);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (!((lead >> j) & 1u)) continue;
-      const uint32_t c0 = uint32_t(q >> (8 * j)) & 0xFFu;
-      const uint32_t c1 = uint32_t(q >> (8 * j + 8)) & 0x3Fu;
-      const uint32_t c2 = uint32_t(q >> (8 * j + 16)) & 0x3Fu;
-      if ((four >> j) & 1u) {
-        const uint32_t c3 = uint32_t(q >> (8 * j + 24)) & 0x3Fu;
-        const uint32_t cp = ((c0 & 0x07u) << 18) | (c1 << 12) | (c2 << 6) | c3;
-        dst[at] = uint16_t(0xD800u + ((cp - 0x10000u) >> 10));
-        dst[at + 1] = uint16_t(0xDC00u + ((cp - 0x10000u) & 0x3FFu));
-        at += 2;
-      } else {
-        uint32_t u = c0;
-        if (c0 >= 0xE0u) u = ((c0 & 0x0Fu) << 12) | (c1 << 6) | c2;
-        else if (c0 >= 0x80u) u = ((c0 & 0x1Fu) << 6) | c1;
-        if (nar) dst8[at] = uint8_t(u);
-        else dst[at] = uint16_t(u);
-        at += 1;
-      }
-    }
-    k += __popcll(p0) + 2 * __popcll(p1) + 4 * __popcll(p2) + 8 * __popcll(p3);
+    decode_step(text, o, ie, d0, nar, w0, v, v2, k);
   }
   return k;
+}
+
+// Two staged rows decoded in lock step: their LDS reads are issued together
+// and their two ballot / store chains interleave.  (One row at a time the
+// per-row chain -- LDS read, SWAR, four ballots, stores -- left the decode
+// latency-bound at ~0.1 instructions per cycle per SIMD.)
+__device__ __forceinline__ void decode_rows2(const LdsBytes& src, uint8_t* text, int64_t oA, int64_t eA,
+                                             int64_t d0A, bool narA, int32_t& kA, int64_t oB, int64_t eB,
+                                             int64_t d0B, bool narB, int32_t& kB) {
+  const int32_t ieA = int32_t(eA - oA), ieB = int32_t(eB - oB);
+  const int lane = lane_id();
+  kA = 0;
+  kB = 0;
+  int64_t wA = oA & ~int64_t(3), wB = oB & ~int64_t(3);
+  while (wA < eA || wB < eB) {
+    const bool actA = wA < eA, actB = wB < eB;   // wave-uniform
+    const bool okA = actA && int32_t(wA - oA) + 4 * lane < ieA;
+    const bool okB = actB && int32_t(wB - oB) + 4 * lane < ieB;
+    // unconditional reads of a valid staged address, selected after
+    const int64_t aA = okA ? wA + 4 * lane : src.a0, aB = okB ? wB + 4 * lane : src.a0;
+    uint32_t vA = src.dword(aA), v2A = src.dword(aA + 4);
+    uint32_t vB = src.dword(aB), v2B = src.dword(aB + 4);
+    if (!okA) vA = v2A = 0u;
+    if (!okB) vB = v2B = 0u;
+    if (actA) {
+      decode_step(text, oA, ieA, d0A, narA, wA, vA, v2A, kA);
+      wA += 4 * kWave;
+    }
+    if (actB) {
+      decode_step(text, oB, ieB, d0B, narB, wB, vB, v2B, kB);
+      wB += 4 * kWave;
+    }
+  }
 }
 
 // One lane's row class from the staged bytes [lo, le) (as row_class).
@@ -446,6 +488,35 @@ __global__ __launch_bounds__(kDecWaves * kWave) void k_cesu_decode(uint8_t* text
         if (in_win) my_cls = lane_row_class(lbuf, int(s0 - a0), int(s1 - a0));
         if (my_cls == 0) fl = uint8_t(fl & ~kRowCesu);
         m = __ballot(my_cls > 0);
+      }
+      if (staged) {   // m holds class 1 / 2 rows only: two at a time
+        while (m) {
+          const int lA = __builtin_ctzll(m);
+          m &= m - 1;
+          const bool two = m != 0;
+          const int lB = two ? __builtin_ctzll(m) : lA;
+          if (two) m &= m - 1;
+          const int64_t oA = bcast_lane64(s0, lA), eA = bcast_lane64(s1, lA);
+          // a lone last row runs as row B with an empty extent
+          const int64_t oB = two ? bcast_lane64(s0, lB) : (eA & ~int64_t(3));
+          const int64_t eB = two ? bcast_lane64(s1, lB) : oB;
+          const bool narA = __builtin_amdgcn_readlane(my_cls, lA) == 1;
+          const bool narB = two && __builtin_amdgcn_readlane(my_cls, lB) == 1;
+          const int64_t d0A = tail + 2 * oA, d0B = tail + 2 * oB;
+          int32_t kA = 0, kB = 0;
+          decode_rows2(lsrc, text, oA, eA, d0A, narA, kA, oB, eB, d0B, narB, kB);
+          if (lane == lA) {
+            s0 = d0A;
+            s1 = d0A + (narA ? kA : 2 * kA);
+            fl = narA ? uint8_t(fl & ~kRowCesu) : uint8_t((fl & ~kRowCesu) | kRowWide);
+          }
+          if (two && lane == lB) {
+            s0 = d0B;
+            s1 = d0B + (narB ? kB : 2 * kB);
+            fl = narB ? uint8_t(fl & ~kRowCesu) : uint8_t((fl & ~kRowCesu) | kRowWide);
+          }
+          n_nar += (narA ? 1 : 0) + (narB ? 1 : 0);
+        }
       }
       while (m) {
         const int l = __builtin_ctzll(m);

@@ -1126,18 +1126,6 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
   const double* rec_it = sgd_rec(d, it);
   const int sS = int(rec_it[kRecS]), sL = int(rec_it[kRecL]);
   const int64_t ncols = ns + kPartVals - kNumNumeric;
-  // loads of this thread's first far slot and first near weight issued now:
-  // their latency overlaps the partial-row reduction below instead of adding
-  // two more round trips after it
-  const int64_t jf0 = int64_t(blockIdx.x) * 1024 + tid;
-  int64_t gf0 = 0;
-  double wf0 = 0.0, wn0 = 0.0;
-  if (jf0 < n_far) {
-    gf0 = gfar[jf0];
-    wf0 = d.wc64[d.far_base + jf0];
-  }
-  const int64_t cn0 = int64_t(blockIdx.x) * kWave + lane;
-  if (w == 0 && cn0 < hi) wn0 = d.wc64[cn0];
   // m: global kept rows, or the sampled row count of this iteration
   if (tid < kWave) {
     double m = d.state[5];
@@ -1164,7 +1152,7 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
     if (w == 0 && col < ncols) {
       const int64_t gi = (nparts > 0 ? gp : (col <= ns + 1 ? d.gacc[col] : 0));
       if (col < hi) {
-        double wn = col == cn0 ? wn0 : d.wc64[col];
+        double wn = d.wc64[col];
         if (m > 0.0) {
           const double g = double(gi) * (col < kNumNumeric ? ldexp(1.0, -int(rec_it[kRecN + col])) : gsc);
           const double step = alpha * (g / m);
@@ -1185,11 +1173,11 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
   // tiered: far slots [far_base, 4 + n_unique), one thread per slot, from
   // the fixed-point far gradient (k_far_grad / all-reduced), re-zeroed here
   if (n_far > 0) {
-    for (int64_t j = jf0; j < n_far; j += int64_t(gridDim.x) * 1024) {
-      const double g = double(j == jf0 ? gf0 : gfar[j]) * gsc;
+    for (int64_t j = int64_t(blockIdx.x) * 1024 + tid; j < n_far; j += int64_t(gridDim.x) * 1024) {
+      const double g = double(gfar[j]) * gsc;
       gfar[j] = 0;
       const int64_t col = d.far_base + j;
-      double wn = j == jf0 ? wf0 : d.wc64[col];
+      double wn = d.wc64[col];
       if (m > 0.0) {
         // the near columns' formula bit for bit: which tier a slot lands in
         // depends on sampled counts (row placement), its update must not
