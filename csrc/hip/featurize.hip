@@ -904,17 +904,36 @@ __global__ __launch_bounds__(kBlock) void k_featurize(DevRawBatch b, DevPrepared
     auto unit = [&](int64_t j) -> uint32_t { return sr.unit(b, j, lt); };
     int32_t* out = p.idx + g0 * kChunkStride + lane * kGroup;
     const int32_t total = L8 * kGroup;
+    // Each unit is read and lower-cased once: entry j's second unit j + 1 is
+    // the first unit of lane t + 1 (same step) or, for t = 3, of lane t - 3
+    // (next step) -- a quad DPP rotate within the row's 4 lanes.  (Each
+    // entry lower-casing both of its units read 2 x 4 LDS bytes / table
+    // entries per bigram of a wide row.)
+    auto ua_at = [&](int32_t jj) -> uint32_t {
+      const int64_t j = int64_t(jj) * kLanesPerRow + t;
+      return j < len ? unit(j) : 0u;
+    };
+    auto quad_next = [](uint32_t x) -> uint32_t {   // lane 4r + t <- lane 4r + (t + 1) % 4
+      return uint32_t(__builtin_amdgcn_mov_dpp(int(x), 0x39, 0xf, 0xf, true));
+    };
+    uint32_t ua0 = ua_at(0);
     for (int32_t jj0 = 0; jj0 < total; jj0 += kGroup) {
+      uint32_t ua[kGroup + 1];
+      ua[0] = ua0;
+#pragma unroll
+      for (int k = 1; k <= kGroup; ++k) ua[k] = ua_at(jj0 + k);
+      ua0 = ua[kGroup];
       int32_t v[kGroup];
 #pragma unroll
       for (int k = 0; k < kGroup; ++k) {
         const int64_t j = int64_t(jj0 + k) * kLanesPerRow + t;
+        const uint32_t nA = quad_next(ua[k]), nB = quad_next(ua[k + 1]);
         v[k] = -1;
         if (j < nz) {
-          const uint32_t u0 = unit(j);
+          const uint32_t u0 = ua[k];
           int64_t h;
           if (len >= 2) {
-            const uint32_t u1 = unit(j + 1);
+            const uint32_t u1 = t < kLanesPerRow - 1 ? nA : nB;
             h = fp.hash_kind == 0 ? int64_t(31u * u0 + u1) : int64_t(murmur_term(u0, u1, 2));
           } else {
             h = fp.hash_kind == 0 ? int64_t(u0) : int64_t(murmur_term(u0, 0, 1));
