@@ -93,6 +93,10 @@ def parse_args(argv=None):
     ap.add_argument("--comm", choices=["rccl", "gloo"], default="rccl",
                     help="DP gradient collectives: RCCL over xGMI, or host-staged torch.distributed "
                          "gloo (lets N ranks share one GPU for testing)")
+    ap.add_argument("--force-dp", action="store_true",
+                    help="take the engine's DP path at world 1 through a world-1 RCCL communicator (every "
+                         "collective issued on the compute stream) and report the per-iteration all-reduce "
+                         "time")
     ap.add_argument("--json-out", default="")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args(argv)
@@ -104,6 +108,8 @@ class Runner:
     def __init__(self, eng, is_km: bool, now_ms: int):
         self.eng, self.is_km, self.now_ms = eng, is_km, now_ms
         self.lat, self.kept, self.iters, self.stage, self.extra = [], [], [], [], []
+        self.comm = []            # (gradient all-reduces, their ms) per timed batch
+        self.prestaged_at_t0 = 0  # batches of the timed window staged / submitted before t0
 
     def process(self, slot: int):
         if self.is_km:
@@ -120,6 +126,7 @@ class Runner:
             self.iters.append(res["iterations"])
             self.stage.append((res["prep_ms"], res["train_ms"]))
             self.extra.append((res.get("tiered", False), res.get("n_unique", 0), res.get("n_near", 0)))
+            self.comm.append((res.get("comm_iters", 0), res.get("comm_ms", 0.0)))
 
 
 def run_device_pipeline(r: Runner, pool, warmup: int, steps: int, sync):
@@ -131,16 +138,20 @@ def run_device_pipeline(r: Runner, pool, warmup: int, steps: int, sync):
     state = {"next": 0, "cur": 0}
     sealed_at = {}
 
-    def submit_one():
+    def submit_one(limit):
         i = state["next"]
+        if i >= limit:   # the timed window's batches are submitted inside it
+            return
         sealed_at[i] = time.perf_counter()
         eng.submit(pool[i % len(pool)], i % eng.raw_slots)
         state["next"] = i + 1
 
-    def run(n, record):
+    def run(n, record, limit):
         for _ in range(n):
             t = state["cur"]
-            submit_one()
+            submit_one(limit)
+            if state["next"] <= t:   # pipeline drained at the window edge: submit this one now
+                submit_one(t + 1)
             res = r.process(t % eng.raw_slots)
             done = time.perf_counter()
             state["cur"] = t + 1
@@ -149,10 +160,16 @@ def run_device_pipeline(r: Runner, pool, warmup: int, steps: int, sync):
             else:
                 sealed_at.pop(t)
 
+    def timed():
+        r.prestaged_at_t0 = max(0, state["next"] - warmup)
+        for _ in range(depth - 1):   # prime inside the window
+            submit_one(warmup + steps)
+        run(steps, True, warmup + steps)
+
     for _ in range(depth - 1):   # prime: batches 0..depth-2 in flight before step 0
-        submit_one()
-    run(warmup, False)
-    t0, t1 = sync(lambda: run(steps, True))
+        submit_one(warmup)
+    run(warmup, False, warmup)
+    t0, t1 = sync(timed)
     return t0, t1
 
 
@@ -169,10 +186,16 @@ def run_e2e(r: Runner, raws, u8s, views, ingest: str, warmup: int, steps: int, s
     for s in range(ahead):   # batches staged ahead of the one training
         free.put(s)
     err = []
+    # The timed window starts with an empty pipeline: batch `warmup` (the
+    # first timed one) is not staged, H2D-submitted or prepared before t0.
+    go = threading.Event()
+    staged = [0]
 
     def stager():
         try:
             for i in range(total):
+                if i == warmup:
+                    go.wait()
                 slot = free.get()
                 sealed = time.perf_counter()
                 raw = raws[i % len(raws)]
@@ -184,6 +207,7 @@ def run_e2e(r: Runner, raws, u8s, views, ingest: str, warmup: int, steps: int, s
                 else:
                     hb.load(raw, "wire")
                 eng.submit(hb, slot)
+                staged[0] = i + 1
                 ready.put((slot, sealed, time.perf_counter() - sealed))
         except BaseException as e:   # surfaced by the main thread
             err.append(e)
@@ -206,8 +230,13 @@ def run_e2e(r: Runner, raws, u8s, views, ingest: str, warmup: int, steps: int, s
                 r.record(res, sealed, done)
                 host_ms.append(stage_s * 1e3)
 
+    def timed():
+        r.prestaged_at_t0 = max(0, staged[0] - warmup)
+        go.set()
+        run(steps, True)
+
     run(warmup, False)
-    t0, t1 = sync(lambda: run(steps, True))
+    t0, t1 = sync(timed)
     th.join(timeout=60)
     r.host_stage_ms = float(np.median(host_ms)) if host_ms else 0.0
     return t0, t1
@@ -219,7 +248,9 @@ def lr_config(args, rows: int, max_units: int, ingest: str):
                           step_size=args.step_size, num_iterations=args.iters, fraction=1.0,
                           begin=100, end=1000, max_rows=rows, max_units=max_units,
                           sgd_grid=args.sgd_grid, ablate=args.ablate, tol=args.tol, dedup=bool(args.dedup),
-                          hybrid=bool(args.hybrid), ingest=ingest if args.e2e else "wire")
+                          hybrid=bool(args.hybrid), ingest=ingest if args.e2e else "wire",
+                          force_dp=bool(getattr(args, "force_dp", False)),
+                          comm_timing=bool(getattr(args, "force_dp", False)))
 
 
 def hbm_batch(args, synth, device: int, ingest: str):
@@ -268,7 +299,10 @@ def main(argv=None) -> int:
     numa_cpus = bind_local_numa(device)   # before the pinned pool is allocated
     # one communicator: LR DP issues one int64 all-reduce per GD iteration and
     # one all-gather of the next batch's prep packets per batch
-    comm = D.make_comm(device, args.comm)
+    if args.force_dp and (info.world > 1 or args.comm != "rccl"):
+        print("--force-dp is a world-1 RCCL mode", file=sys.stderr)
+        return 2
+    comm = D.make_comm(device, args.comm, force=args.force_dp)
     ingest = args.ingest or "utf8"
 
     synth = SynthConfig.profile(args.profile, seed=args.seed + 7919 * info.rank)
@@ -289,7 +323,7 @@ def main(argv=None) -> int:
     if is_km:
         from twitter_stream_ml_amd.ops.kmeans_engine import DeviceKMeans, KMDeviceConfig
         kcfg = KMDeviceConfig(k=args.k, text_dims=args.text_dims, half_life=5.0, max_rows=B,
-                              max_units=max_units, seed=args.seed)
+                              max_units=max_units, seed=args.seed, force_dp=args.force_dp)
         eng = DeviceKMeans(kcfg, device=device, comm=comm)
     else:
         eng = DeviceLinearRegression(lr_config(args, B, max_units, ingest), device=device, comm=comm)
@@ -345,8 +379,11 @@ def main(argv=None) -> int:
     p50 = D.allreduce_max_scalar(float(np.median(runner.lat)))
     value = tweets / elapsed
     ms = elapsed / args.steps * 1e3
+    mine = float(sum(runner.kept)) / max(t1 - t0, 1e-12)   # this rank's own tweets/s over its window
+    per_rank = D.gather_to_main(np.array([mine]))
+    prestaged = int(D.allreduce_max_scalar(float(runner.prestaged_at_t0)))
     stage = runner.stage
-    par = f"dp{info.world}" + ("-gloo" if args.comm == "gloo" else "")
+    par = f"dp{info.world}" + ("-gloo" if args.comm == "gloo" else "") + ("-forced" if args.force_dp else "")
     data = ("synthetic tweet-shaped records (seeded C++ generator, "
             f"{'realistic 50K-word multi-script' if args.profile == 'wide' else 'toy ~300-word'} vocabulary, "
             + (f"{n_pool} distinct batches per rank: no batch is trained twice)"
@@ -396,6 +433,20 @@ def main(argv=None) -> int:
                      if args.e2e else "device pipeline: pre-packed wire pool, H2D in the timed region")
     if args.e2e:
         out["host_stage_ms_p50"] = round(getattr(runner, "host_stage_ms", 0.0), 3)
+    # the engine communicator's own view: the world it spans and the
+    # collectives it carried (so a scaling run shows RCCL saw N ranks)
+    out["comm_world"] = int(comm.world) if comm is not None else 1
+    out["comm_kind"] = str(comm.kind) if comm is not None else "none"
+    if comm is not None:
+        out["comm_counters"] = {k: int(v) for k, v in comm.counters().items()}
+    if per_rank is not None:
+        out["per_rank_value"] = [round(float(v), 1) for v in per_rank]
+    out["prestaged_at_t0"] = prestaged
+    if runner.comm and sum(c[0] for c in runner.comm) > 0:
+        n_ar = sum(c[0] for c in runner.comm)
+        out["grad_allreduce_per_step"] = round(n_ar / len(runner.comm), 2)
+        if args.force_dp:
+            out["grad_allreduce_us_per_iter"] = round(1e3 * sum(c[1] for c in runner.comm) / n_ar, 2)
     out["pool_gen_s"] = round(t_gen, 2)
     out["pool_batches"] = n_pool
     out["numa_bound_cpus"] = len(numa_cpus) if numa_cpus else None

@@ -34,7 +34,7 @@ static LRConfig lr_config(const py::dict& d) {
   GET(end, int64_t) GET(require_retweet, int32_t) GET(range_filter, int32_t)
   GET(max_rows, int64_t) GET(max_units, int64_t) GET(sgd_grid, int32_t)
   GET(early_exit_depth, int32_t) GET(ablate, int32_t) GET(dedup, int32_t) GET(hybrid, int32_t) GET(lazy_idx, int32_t)
-  GET(overlap, int32_t)
+  GET(overlap, int32_t) GET(force_dp, int32_t) GET(comm_timing, int32_t)
 #undef GET
   return c;
 }
@@ -57,6 +57,8 @@ static py::dict result_dict(BatchResult& r) {
   d["tiered"] = r.tiered;
   d["n_near"] = r.n_near;
   d["train_ms"] = r.train_ms;
+  d["comm_iters"] = r.comm_iters;
+  d["comm_ms"] = r.comm_ms;
   if (!r.pred.empty()) {
     auto* v = new std::vector<float>(std::move(r.pred));
     py::capsule own(v, [](void* p) { delete static_cast<std::vector<float>*>(p); });
@@ -107,6 +109,17 @@ PYBIND11_MODULE(_twtml_hip, m) {
       .def_property_readonly("kind", &Comm::kind)
       .def("abort", &Comm::abort)
       .def("check", &Comm::check_async)
+      .def("counters", [](const Comm& c) {
+        const auto v = c.counters();
+        py::dict d;
+        d["allreduce_calls"] = v[0];
+        d["allreduce_bytes"] = v[1];
+        d["allgather_calls"] = v[2];
+        d["allgather_bytes"] = v[3];
+        d["broadcast_calls"] = v[4];
+        d["broadcast_bytes"] = v[5];
+        return d;
+      })
       // In-place fp64 sum over a device buffer on a private stream, then
       // synchronise: exercises the communicator outside an engine (tests,
       // link checks).  The engines issue their collectives on their own streams.

@@ -52,17 +52,20 @@ void RcclComm::allreduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t
   // world 1; the direct binding uses this to check a communicator on one GPU)
   if (count == 0) return;
   TraceRange tr("twtml.rccl.allreduce");
+  tally(0, count * comm_dtype_size(dt));
   TWTML_NCCL_CHECK(ncclAllReduce(buf, buf, count, dt, op, comm_, s));
 }
 
 void RcclComm::broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t s) {
   if (world_ == 1 || count == 0) return;
+  tally(2, count * comm_dtype_size(dt));
   TWTML_NCCL_CHECK(ncclBroadcast(buf, buf, count, dt, root, comm_, s));
 }
 
 void RcclComm::allgather(const void* send, void* recv, size_t count, ncclDataType_t dt, hipStream_t s) {
   if (count == 0) return;
   TraceRange tr("twtml.rccl.allgather");
+  tally(1, count * comm_dtype_size(dt) * size_t(world_));
   TWTML_NCCL_CHECK(ncclAllGather(send, recv, count, dt, comm_, s));
 }
 
@@ -176,6 +179,7 @@ LoopbackComm::LoopbackComm(std::shared_ptr<LoopbackHub> hub, int rank) : hub_(st
 
 void LoopbackComm::allreduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t s) {
   if (world_ == 1 || count == 0) return;
+  tally(0, count * comm_dtype_size(dt));
   TWTML_HIP_CHECK(hipStreamSynchronize(s));
   hub_->allreduce(rank_, buf, count, dt, op);
 }
@@ -188,6 +192,7 @@ void LoopbackComm::broadcast(void* buf, size_t count, ncclDataType_t dt, int roo
 
 void LoopbackComm::allgather(const void* send, void* recv, size_t count, ncclDataType_t dt, hipStream_t s) {
   if (count == 0) return;
+  tally(1, count * comm_dtype_size(dt) * size_t(world_));
   TWTML_HIP_CHECK(hipStreamSynchronize(s));
   if (world_ == 1) {
     TWTML_HIP_CHECK(hipMemcpyAsync(recv, send, count * comm_dtype_size(dt), hipMemcpyDeviceToDevice, s));
@@ -238,6 +243,7 @@ static void sum_parts_in_order(T* parts, size_t count, int world) {
 
 void HostComm::allreduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t s) {
   if (count == 0) return;
+  tally(0, count * comm_dtype_size(dt));
   TraceRange tr("twtml.hostcomm.allreduce");
   const size_t bytes = count * comm_dtype_size(dt);
   if (op == ncclSum && world_ > 2 && (dt == ncclFloat64 || dt == ncclFloat32)) {
@@ -272,6 +278,7 @@ void HostComm::broadcast(void* buf, size_t count, ncclDataType_t dt, int root, h
 
 void HostComm::allgather(const void* send, void* recv, size_t count, ncclDataType_t dt, hipStream_t s) {
   if (count == 0) return;
+  tally(1, count * comm_dtype_size(dt) * size_t(world_));
   const size_t bytes = count * comm_dtype_size(dt);
   uint8_t* h = static_cast<uint8_t*>(stage(bytes * size_t(world_)));
   TWTML_HIP_CHECK(hipMemcpyAsync(h + bytes * size_t(rank_), send, bytes, hipMemcpyDeviceToHost, s));

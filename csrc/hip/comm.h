@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <functional>
 #include <memory>
@@ -36,9 +37,22 @@ class Comm {
   virtual std::string kind() const = 0;
   int rank() const { return rank_; }
   int world() const { return world_; }
+  // collectives issued through this communicator: {all-reduce, all-gather,
+  // broadcast} x {calls, bytes} (tests and the bench check that the engine's
+  // DP traffic really went through it)
+  std::vector<uint64_t> counters() const {
+    std::vector<uint64_t> v(6);
+    for (int i = 0; i < 6; ++i) v[size_t(i)] = ctr_[i].load(std::memory_order_relaxed);
+    return v;
+  }
 
  protected:
+  void tally(int kind, size_t bytes) {
+    ctr_[2 * kind].fetch_add(1, std::memory_order_relaxed);
+    ctr_[2 * kind + 1].fetch_add(bytes, std::memory_order_relaxed);
+  }
   int rank_ = 0, world_ = 1;
+  std::atomic<uint64_t> ctr_[6] = {};
 };
 
 class RcclComm final : public Comm {

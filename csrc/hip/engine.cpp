@@ -234,6 +234,11 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
     throw std::invalid_argument("miniBatchFraction must be in (0, 1]");
   if (const char* v = std::getenv("TWTML_FORCE_TIERED")) force_tiered_ = v[0] == '1';   // tests
   world_ = comm_ ? comm_->world() : 1;
+  // forced DP (tests / bench --force-dp): a world-1 communicator carries every
+  // DP collective (packet all-gather, packed int64 all-reduce, stats)
+  const char* fdp = std::getenv("TWTML_FORCE_DP");
+  dp_ = world_ > 1 || (comm_ && (cfg_.force_dp != 0 || (fdp && fdp[0] == '1')));
+  comm_timing_ = dp_ && cfg_.comm_timing != 0;
   // Prepare-ahead of batch t+1 while t trains: all of it on one GPU; on DP
   // ranks the local part, then (after the training thread all-gathered the
   // ranks' packets between two of t's GD iterations) the rest.
@@ -289,7 +294,7 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
                                 (2 + size_t(std::max(1, cfg_.num_iterations))) * sizeof(double),
                                 hipHostMallocMapped | hipHostMallocCoherent));
   TWTML_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&sgd_.host_flags), host_flags_, 0));
-  if (world_ > 1) {
+  if (dp_) {
     TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&ready_host_), 64, hipHostMallocMapped | hipHostMallocCoherent));
     *ready_host_ = 0;
     int64_t* dev_ready = nullptr;
@@ -357,7 +362,7 @@ void LREngine::alloc_prepared(PrepBuf& b) {
   TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&b.host_norm), 2 * sizeof(int64_t), hipHostMallocDefault));
   TWTML_HIP_CHECK(hipEventCreate(&b.ev_start));
   TWTML_HIP_CHECK(hipEventCreate(&b.ev_done));
-  if (world_ > 1) {
+  if (dp_) {
     TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&b.host_hdr),
                                   sizeof(int64_t) * size_t(world_) * (kC1HeaderWords / 2), hipHostMallocDefault));
     TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&b.host_bounds), sizeof(double) * kBoundsLen,
@@ -505,6 +510,7 @@ LREngine::~LREngine() {
   if (hnu_) (void)hipHostFree(hnu_);
   if (dnu_) (void)hipFree(dnu_);
   for (auto e : iter_events_) (void)hipEventDestroy(e);
+  for (auto e : comm_ev_) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(compute_);
   (void)hipStreamDestroy(pstream_);
   (void)hipStreamDestroy(copy_);
@@ -560,7 +566,7 @@ void LREngine::prepare_local(PrepBuf& pb, int slot, int64_t now_ms, hipStream_t 
                                  hipMemcpyDeviceToHost, s));
   TWTML_HIP_CHECK(hipStreamSynchronize(s));
   if (pb.host_counters[3] != 0) throw std::runtime_error("feature buffer capacity exceeded");
-  if (world > 1) {
+  if (dp_) {
     // the packet: sampled counts of the local active ids (the same sampled
     // chunks as the tiered near-tier choice), then header + (id, count) pairs
     const int64_t nU = pb.host_counters[1];
@@ -805,10 +811,11 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred) {
   sp.want_pred = want_pred ? 1 : 0;
   sp.sample = cfg_.fraction < 1.0 ? 1 : 0;
   sp.ablate = cfg_.ablate;
-  sp.dp = world > 1 ? 1 : 0;
+  sp.dp = dp_ ? 1 : 0;
   sp.rank0 = (comm_ ? comm_->rank() : 0) == 0 ? 1 : 0;
   const int64_t n_far = kNumNumeric + nU - sgd_.far_base;
   res.diverged = diverged_;
+  int comm_iters = 0;   // DP: gradient all-reduces issued for this batch
   if (n_glob > 0 && !diverged_) {
     // Host-side early stop: the convergence test of update j runs in the
     // prologue of iteration j+1's gradient kernel, which copies its verdict
@@ -821,17 +828,24 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred) {
     const int iters = cfg_.num_iterations;
     std::fill(host_flags_, host_flags_ + iters + 2, -1.0);   // -1: verdict not published yet
     // single GPU with partial rows: the update kernel reduces them itself
-    const bool fused = world == 1 && sgd_.nparts > 0;
+    const bool fused = !dp_ && sgd_.nparts > 0;
     const bool itime = std::getenv("TWTML_ITER_TIMING") != nullptr;
     if (itime && !iter_tdbg_) iter_tdbg_ = dmalloc<uint64_t>(4096 + size_t(iters + 2) * 32);
     sgd_.tdbg = itime ? iter_tdbg_ : nullptr;
     if (itime) TWTML_HIP_CHECK(hipMemsetAsync(iter_tdbg_, 0, sizeof(uint64_t) * (4096 + size_t(iters + 2) * 32), s));
+    if (comm_timing_ && comm_ev_.size() < size_t(2 * iters)) {
+      for (size_t q = comm_ev_.size(); q < size_t(2 * iters); ++q) {
+        hipEvent_t e;
+        TWTML_HIP_CHECK(hipEventCreate(&e));
+        comm_ev_.push_back(e);
+      }
+    }
     for (int i = 1; i <= iters; ++i) {
       if (i > depth) {
         const int j = i - depth;                       // verdict after update j
         const int64_t v = int64_t(wait_flag(j));       // bit 0 stop; DP: bit 1 every rank's next
                                                        // packet ready, >> 2 the largest one
-        if (world > 1 && (v & 2)) {
+        if (dp_ && (v & 2)) {
           // the next batch's packets are ready on every rank: all-gather them
           // here, between iterations j + depth - 1 and j + depth -- every rank
           // sees the same all-reduced flag at the same point
@@ -850,12 +864,15 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred) {
       // partials) so every rank runs the convergence prologue
       launch_sgd_iter(sgd_, prep, sp, pb.host_counters[2], u16, grid, s);
       if (tiered) launch_far_grad(sgd_, sp, num_cu_, s);
-      if (world > 1) {
+      if (dp_) {
         // ONE collective per iteration: the packed int64 buffer (near
         // columns, loss, sampled m, verdict, ready words, far slots); integer
         // sums are exact in any order, so every rank gets the same bits
         launch_sgd_reduce(sgd_, sp, s);
+        if (comm_timing_) TWTML_HIP_CHECK(hipEventRecord(comm_ev_[size_t(2 * (i - 1))], s));
         comm_->allreduce(sgd_.gacc, size_t(sgd_.far_off + n_far), ncclInt64, ncclSum, s);
+        if (comm_timing_) TWTML_HIP_CHECK(hipEventRecord(comm_ev_[size_t(2 * (i - 1) + 1)], s));
+        ++comm_iters;
       }
       launch_sgd_update(sgd_, sp, fused ? sgd_.nparts : 0, s);
     }
@@ -870,7 +887,7 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred) {
   }
   if (n_glob <= 0 || diverged_) launch_norm_next(sgd_, false, s);   // weights unchanged: carry |w|^2 as is
   TWTML_HIP_CHECK(hipEventRecord(ev_[2], s));
-  if (world > 1) comm_->allreduce(sgd_.stats, 6, ncclFloat64, ncclSum, s);
+  if (dp_) comm_->allreduce(sgd_.stats, 6, ncclFloat64, ncclSum, s);
   TWTML_HIP_CHECK(hipMemcpyAsync(host_out_, sgd_.stats, 8 * sizeof(double), hipMemcpyDeviceToHost, s));
   TWTML_HIP_CHECK(hipMemcpyAsync(host_out_ + 8, sgd_.state, 8 * sizeof(double), hipMemcpyDeviceToHost, s));
   TWTML_HIP_CHECK(hipMemcpyAsync(host_out_ + 16, sgd_.loss_hist,
@@ -893,6 +910,14 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred) {
   // batch's training when prepared ahead); train_ms: compute stream
   TWTML_HIP_CHECK(hipEventElapsedTime(&res.prep_ms, pb.ev_start, pb.ev_done));
   TWTML_HIP_CHECK(hipEventElapsedTime(&res.train_ms, ev_[1], ev_[2]));
+  res.comm_iters = comm_iters;
+  if (comm_timing_) {   // the per-iteration gradient all-reduces on the compute stream
+    for (int q = 0; q < comm_iters; ++q) {
+      float ms = 0.f;
+      TWTML_HIP_CHECK(hipEventElapsedTime(&ms, comm_ev_[size_t(2 * q)], comm_ev_[size_t(2 * q + 1)]));
+      res.comm_ms += ms;
+    }
+  }
   return res;
 }
 
@@ -939,7 +964,7 @@ void LREngine::prep_worker() {
     std::exception_ptr err;
     try {
       prepare_local(b, slot, now_ms, pstream_);
-      if (world_ > 1) {
+      if (dp_) {
         // packet ready: announce it (the ready word travels in the gradient
         // all-reduce) and wait for the training thread's all-gather
         lk.lock();
@@ -993,7 +1018,7 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
     std::unique_lock<std::mutex> lk(mu_);
     for (int i = 0; i < 2; ++i)
       if (pb_[i].state != 0 && pb_[i].slot == slot) k = i;
-    if (k >= 0 && world_ > 1) {
+    if (k >= 0 && dp_) {
       // DP: the packets were all-gathered during the previous batch, or are
       // now, in line -- the same choice on every rank (it follows the
       // all-reduced ready words); then the prep thread finishes the layout
@@ -1033,7 +1058,7 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
       // not prepared ahead: drop it from the submission queue, prepare in line
       for (auto it = submitted_.begin(); it != submitted_.end(); ++it)
         if (it->first == slot) { submitted_.erase(it); break; }
-      if (world_ > 1) {
+      if (dp_) {
         // every rank must issue the same collectives in the same order: a
         // batch prepared (and possibly all-gathered) ahead may not be skipped
         for (int i = 0; i < 2; ++i)
@@ -1062,7 +1087,7 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
       lk.unlock();
       try {
         prepare_local(pb_[k], slot, now_ms, pstream_);
-        if (world_ > 1) {
+        if (dp_) {
           issue_c1_inline(pb_[k]);
           prepare_global_dp(pb_[k], pstream_);
         } else {

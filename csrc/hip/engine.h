@@ -53,6 +53,9 @@ struct LRConfig {
   int32_t hybrid = 1;            // dense 4-bit counts for the batch's hottest slots (hot_split.hip)
   int32_t lazy_idx = 1;          // hybrid: fast chunks' ids re-derived from text by the remap
   int32_t overlap = 1;           // prepare batch t+1 (prep stream, prep thread) while t trains
+  int32_t force_dp = 0;          // take the DP path (packet all-gather, packed all-reduce, stats
+                                 // all-reduce) even with a world-1 communicator (also TWTML_FORCE_DP=1)
+  int32_t comm_timing = 0;       // DP: time the per-iteration gradient all-reduce (events)
 };
 
 // Pinned staging buffer of one raw batch in the wire format
@@ -134,6 +137,8 @@ struct BatchResult {
   std::vector<double> loss_history;
   std::vector<float> pred;
   float prep_ms = 0.f, train_ms = 0.f;
+  int32_t comm_iters = 0;   // DP: gradient all-reduces issued (one per GD iteration)
+  float comm_ms = 0.f;      // DP + comm_timing: their summed time on the compute stream
 };
 
 // One prepared micro-batch: filtered, featurized, compacted and laid out for
@@ -219,6 +224,7 @@ class LREngine {
   int64_t snapshot_wait();
   void snapshot_copy(int32_t* idx, double* val);
   const LRConfig& config() const { return cfg_; }
+  bool dp() const { return dp_; }
   void set_step(double step, int iters, double fraction);
   void synchronize();
   int device() const { return device_; }
@@ -260,6 +266,9 @@ class LREngine {
   LRConfig cfg_;
   std::shared_ptr<Comm> comm_;
   int world_ = 1;
+  bool dp_ = false;                 // DP path: world > 1, or forced with a world-1 communicator
+  bool comm_timing_ = false;
+  std::vector<hipEvent_t> comm_ev_; // comm_timing: [2 iters] around each gradient all-reduce
   hipStream_t compute_ = nullptr, pstream_ = nullptr, copy_ = nullptr;
   RawSlots raw_;
   PrepBuf pb_[2];

@@ -3,14 +3,14 @@
 // Per micro-batch:
 //   K3'  filter isRetweet, K1' features x = [retweetCount, followers, hashed
 //        bigram counts (text_dims)] as dense fp32 rows (width padded to DP)
-//   K11  StandardScaler(withMean=false, withStd=true): two-pass column
-//        moments in fp64 (mean, then centred M2 -> sample std), scale in place
+//   K11  StandardScaler(withMean=false, withStd=true): exact integer column
+//        moments (max, then sum / sum of squares) -> sample std on the host
 //   K8   assignment: distances to all k centres on the MATRIX cores --
 //        v_mfma_f32_32x32x2_f32 (exact fp32 products) computes C.X^T for 32
 //        centres x 32 points per wave, ||c||^2 - 2 c.x is reduced to a running
 //        argmin per point (first index wins ties, as KMeans.findClosest)
 //   K9   per-cluster sums: counting-sort points by label, then a segmented
-//        sum that flushes one fp64 atomic per (label run, column)
+//        int64 sum that flushes one atomic per (label run, column): exact
 //   K10  update (one workgroup): decay, weighted centroid move, dying-
 //        cluster split -- StreamingKMeansModel.update [upstream]
 #include <hip/hip_runtime.h>
@@ -441,80 +441,121 @@ void launch_km_features(const DevRawBatch& b, const int64_t* kept, const int64_t
 }
 
 // ---------------------------------------------------------------------------
-// K11: column moments (fp64).  mode 0: sums -> out[1+j] (+ n in out[0]);
-// mode 1: centred squares -> out[j] using mean = sum_n[1+j] / sum_n[0].
+// K11: StandardScaler moments, exact in integers.
+//
+// Every feature is an integer-valued float (retweet / follower counts and
+// bigram counts), so the column sums are exact int64 sums -- equal in any
+// summation order, on any number of DP ranks, bit for bit (the
+// fp64 moment / cluster sums made DP k-means order dependent).  A column
+// whose magnitudes exceed 2^30 is first scaled by 2^-s (s from the
+// all-reduced column max, identical on every rank) and rounded: then
+// |q| <= 2^30 and
+//   sum q, and q^2 as three limbs a^2 2^32 + 2ab 2^16 + b^2 (q = a 2^16 + b)
+// stay below 2^63 for any batch (< 2^31 rows).  The host combines the limbs
+// in 128-bit integers: var = 2^2s (n sum q^2 - (sum q)^2) / (n (n - 1)).
 // ---------------------------------------------------------------------------
-// thread -> (row lane rr, column j): consecutive threads read consecutive
-// columns of a row (coalesced); row lanes are reduced in LDS, one fp64
-// atomic per (block, column).
 static int km_cols_pow2(int d) {
   int cp = 1;
   while (cp < d && cp < kBlock) cp <<= 1;
   return cp;
 }
 
-__global__ __launch_bounds__(kBlock) void k_km_moments(const float* X, const int64_t* counters,
-                                                       int d, int dp, int cp, int mode,
-                                                       const double* sum_n, double* out) {
-  __shared__ double red[kBlock];
+__device__ __forceinline__ int km_shift(int64_t mx) {
+  const int L = mx > 0 ? 64 - __clzll(static_cast<unsigned long long>(mx)) : 0;
+  return L > kKmQBits ? L - kKmQBits : 0;
+}
+
+// q = rint(x 2^-s): exact for s == 0 (x is integer valued), deterministic else
+__device__ __forceinline__ int64_t km_q(float x, int s) {
+  return static_cast<int64_t>(rint(ldexp(static_cast<double>(x), -s)));
+}
+
+// thread -> (row lane rr, column j): consecutive threads read consecutive
+// columns of a row (coalesced); row lanes are reduced in LDS, one 64-bit
+// atomic per (block, column).
+__global__ __launch_bounds__(kBlock) void k_km_colmax(const float* X, const int64_t* counters, int d, int dp,
+                                                      int cp, int64_t* mx) {
+  __shared__ unsigned long long red[kBlock];
   const int64_t n = counters[0];
   const int rp = kBlock / cp, rr = threadIdx.x / cp;
   for (int jb = 0; jb < d; jb += cp) {
     const int j = jb + int(threadIdx.x) % cp;
-    double acc = 0.0;
-    if (j < d) {
-      const double mean = mode == 1 && sum_n[0] > 0 ? sum_n[1 + j] / sum_n[0] : 0.0;
+    unsigned long long m = 0ull;
+    if (j < d)
       for (int64_t r = int64_t(blockIdx.x) * rp + rr; r < n; r += int64_t(gridDim.x) * rp) {
-        const double v = double(X[r * dp + j]) - mean;
-        acc += mode == 0 ? v : v * v;
+        const float a = fminf(fabsf(X[r * dp + j]), 9.2e18f);
+        const unsigned long long v = static_cast<unsigned long long>(rint(static_cast<double>(a)));
+        m = v > m ? v : m;
       }
-    }
-    red[threadIdx.x] = acc;
+    red[threadIdx.x] = m;
     __syncthreads();
     if (rr == 0 && j < d) {
-      for (int q = 1; q < rp; ++q) acc += red[q * cp + threadIdx.x];
-      atomicAdd(&out[(mode == 0 ? 1 : 0) + j], acc);
+      for (int q = 1; q < rp; ++q) m = red[q * cp + threadIdx.x] > m ? red[q * cp + threadIdx.x] : m;
+      if (m) atomicMax(reinterpret_cast<unsigned long long*>(&mx[j]), m);
     }
     __syncthreads();
   }
-  if (mode == 0 && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&out[0], double(n));
 }
 
-void launch_km_moments(const float* X, const int64_t* counters, int d, int dp, int mode,
-                       const double* sum_n, double* out, int64_t max_rows, hipStream_t s) {
-  int grid = int(max_rows / 256 + 1);
-  if (grid > 1024) grid = 1024;
-  hipLaunchKernelGGL(k_km_moments, dim3(grid), dim3(kBlock), 0, s, X, counters, d, dp,
-                     km_cols_pow2(d), mode, sum_n, out);
-}
-
-// std_j = sqrt(M2_j / (n-1)) (n < 2 -> 0); factor_j = std_j != 0 ? 1/std_j : 0
-// (StandardScalerModel.transform).  The features stay unscaled in X; every
-// consumer multiplies by the factor on load (fp32 copy for the matrix-core
-// distances, fp64 for sums and the tie refine).  scale == 0 -> factor 1.
-__global__ void k_km_factor(int d, int dp, int scale, const double* sum_n, const double* m2,
-                            double* std_out, double* f64, float* f32) {
-  const double cnt = sum_n[0];
-  for (int j = threadIdx.x; j < dp; j += blockDim.x) {
-    double f = 0.0;
+// out[0] = n, out[1 + 4j + {0,1,2,3}] = sum q, sum a^2, sum 2ab, sum b^2
+__global__ __launch_bounds__(kBlock) void k_km_moments_q(const float* X, const int64_t* counters, int d, int dp,
+                                                         int cp, const int64_t* mx, int64_t* out) {
+  __shared__ long long red[4][kBlock];
+  const int64_t n = counters[0];
+  const int rp = kBlock / cp, rr = threadIdx.x / cp;
+  for (int jb = 0; jb < d; jb += cp) {
+    const int j = jb + int(threadIdx.x) % cp;
+    long long acc[4] = {0, 0, 0, 0};
     if (j < d) {
-      if (scale) {
-        const double sd = sqrt(cnt > 1.0 ? m2[j] / (cnt - 1.0) : 0.0);
-        std_out[j] = sd;
-        f = sd != 0.0 ? 1.0 / sd : 0.0;
-      } else {
-        f = 1.0;
+      const int sh = km_shift(mx[j]);
+      for (int64_t r = int64_t(blockIdx.x) * rp + rr; r < n; r += int64_t(gridDim.x) * rp) {
+        const int64_t q = km_q(X[r * dp + j], sh);
+        const uint64_t u = static_cast<uint64_t>(q < 0 ? -q : q);
+        const uint64_t a = u >> 16, b = u & 0xFFFFu;
+        acc[0] += q;
+        acc[1] += static_cast<long long>(a * a);
+        acc[2] += static_cast<long long>(2u * a * b);
+        acc[3] += static_cast<long long>(b * b);
       }
     }
-    f64[j] = f;
-    f32[j] = float(f);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) red[t][threadIdx.x] = acc[t];
+    __syncthreads();
+    if (rr == 0 && j < d) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        long long v = acc[t];
+        for (int q = 1; q < rp; ++q) v += red[t][q * cp + threadIdx.x];
+        if (v) atomicAdd(reinterpret_cast<unsigned long long*>(&out[1 + 4 * j + t]),
+                         static_cast<unsigned long long>(v));
+      }
+    }
+    __syncthreads();
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(reinterpret_cast<unsigned long long*>(&out[0]),
+                                                     static_cast<unsigned long long>(n));
 }
 
-void launch_km_factor(int d, int dp, bool scale, const double* sum_n, const double* m2,
-                      double* std_out, double* f64, float* f32, hipStream_t s) {
-  hipLaunchKernelGGL(k_km_factor, dim3(1), dim3(kBlock), 0, s, d, dp, scale ? 1 : 0, sum_n, m2,
-                     std_out, f64, f32);
+static int km_moment_grid(int64_t max_rows) {
+  int grid = int(max_rows / 256 + 1);
+  return grid > 1024 ? 1024 : grid;
+}
+
+void launch_km_colmax(const float* X, const int64_t* counters, int d, int dp, int64_t* mx, int64_t max_rows,
+                      hipStream_t s) {
+  hipLaunchKernelGGL(k_km_colmax, dim3(km_moment_grid(max_rows)), dim3(kBlock), 0, s, X, counters, d, dp,
+                     km_cols_pow2(d), mx);
+}
+
+void launch_km_moments_q(const float* X, const int64_t* counters, int d, int dp, const int64_t* mx,
+                         int64_t* out, int64_t max_rows, hipStream_t s) {
+  hipLaunchKernelGGL(k_km_moments_q, dim3(km_moment_grid(max_rows)), dim3(kBlock), 0, s, X, counters, d, dp,
+                     km_cols_pow2(d), mx, out);
+}
+
+int km_quant_shift(int64_t mx) {
+  const int L = mx > 0 ? 64 - __builtin_clzll(static_cast<unsigned long long>(mx)) : 0;
+  return L > kKmQBits ? L - kKmQBits : 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -1194,70 +1235,67 @@ __global__ __launch_bounds__(kBlock) void k_km_label_scatter_g(const int32_t* la
 }
 
 constexpr int kSegRows = 1024;
-// k * d + k sums up to this many fp64 go through an LDS copy per workgroup
+// k * d + k sums up to this many go through an LDS copy per workgroup
 constexpr int kSegLdsSums = 4096;
 
-// thread = (row lane rr, column j); walks rows rr, rr+RP, ... of its chunk in
-// label order; flushes its running sum whenever the label changes.  LDS:
-// flushes go to the workgroup's LDS copy of the sums, which is added to the
-// global sums once at the end -- with few clusters (the reference's k = 3)
-// every workgroup's flushes otherwise hit the same handful of fp64 global
-// atomics (2.9 ms per 1M points at k = 3, d = 2).
+// Per-cluster sums of the quantized features (km_q) and counts, int64:
+// exact, so every rank / grid / order gives the same bits.  thread = (row
+// lane rr, column j); walks rows rr, rr+RP, ... of its chunk in label order
+// and flushes its running sum whenever the label changes.  LDS: flushes go to
+// the workgroup's LDS copy (ds_add_u64), added to the global sums once at the
+// end -- with few clusters (the reference's k = 3) every workgroup's flushes
+// would otherwise hit the same handful of global atomics.
 template <bool LDS>
-__global__ __launch_bounds__(kBlock) void k_km_segsum(const float* X, const double* fac,
+__global__ __launch_bounds__(kBlock) void k_km_segsum(const float* X, const int64_t* mx,
                                                       const int32_t* labels,
                                                       const int32_t* order, const int64_t* counters,
-                                                      int k, int d, int dp, int cols_pow2, double* sums,
-                                                      double* counts) {
-  extern __shared__ double lsum[];   // LDS: [k * d] sums, then [k] counts
+                                                      int k, int d, int dp, int cols_pow2, int64_t* sums) {
+  extern __shared__ unsigned long long lsum[];   // LDS: [k * d] sums, then [k] counts
   const int64_t n = counters[0];
   const int nsum = k * d + k;
+  auto* gsum = reinterpret_cast<unsigned long long*>(sums);
   if (LDS) {
-    for (int i = threadIdx.x; i < nsum; i += kBlock) lsum[i] = 0.0;
+    for (int i = threadIdx.x; i < nsum; i += kBlock) lsum[i] = 0ull;
     __syncthreads();
   }
-  auto flush = [&](int cur, int j, double acc, double cnt) {
-    if (LDS) {
-      if (j < d) atomicAdd(&lsum[cur * d + j], acc);
-      if (j == 0) atomicAdd(&lsum[k * d + cur], cnt);
-    } else {
-      if (j < d) atomicAdd(&sums[int64_t(cur) * d + j], acc);
-      if (j == 0) atomicAdd(&counts[cur], cnt);
-    }
+  auto flush = [&](int cur, int j, long long acc, long long cnt) {
+    unsigned long long* dst = LDS ? lsum : gsum;
+    if (j < d && acc) atomicAdd(&dst[cur * d + j], static_cast<unsigned long long>(acc));
+    if (j == 0) atomicAdd(&dst[k * d + cur], static_cast<unsigned long long>(cnt));
   };
   const int rp = kBlock / cols_pow2;               // rows per pass
   const int rr = threadIdx.x / cols_pow2;
   for (int64_t base = int64_t(blockIdx.x) * kSegRows; base < n; base += int64_t(gridDim.x) * kSegRows)
   for (int j = threadIdx.x % cols_pow2; j < d; j += cols_pow2) {   // column passes (d > 256)
     const int64_t end = base + kSegRows < n ? base + kSegRows : n;
-    const double fj = fac[j];
+    const int sh = km_shift(mx[j]);
     int cur = -1;
-    double acc = 0.0, cnt = 0.0;
+    long long acc = 0, cnt = 0;
     for (int64_t q = base + rr; q < end; q += rp) {
       const int32_t p = order[q];
       const int lab = labels[p];
       if (lab != cur) {
         if (cur >= 0) flush(cur, j, acc, cnt);
-        cur = lab; acc = 0.0; cnt = 0.0;
+        cur = lab; acc = 0; cnt = 0;
       }
-      acc += double(X[int64_t(p) * dp + j]) * fj;
-      cnt += 1.0;
+      acc += km_q(X[int64_t(p) * dp + j], sh);
+      cnt += 1;
     }
     if (cur >= 0) flush(cur, j, acc, cnt);
   }
   if (LDS) {
     __syncthreads();
     for (int i = threadIdx.x; i < nsum; i += kBlock) {
-      const double v = lsum[i];
-      if (v != 0.0) atomicAdd(i < k * d ? &sums[i] : &counts[i - k * d], v);
+      const unsigned long long v = lsum[i];
+      if (v) atomicAdd(&gsum[i], v);
     }
   }
 }
 
-void launch_km_cluster_sums(const float* X, const double* f64, const int32_t* labels,
+void launch_km_cluster_sums(const float* X, const int64_t* mx, const int32_t* labels,
                             const int64_t* counters, int k,
-                            int d, int dp, int64_t* hist, int32_t* order, double* sums,
-                            double* counts, int64_t max_rows, hipStream_t s,
+                            int d, int dp, int64_t* hist, int32_t* order, int64_t* sums,
+                            int64_t max_rows, hipStream_t s,
                             void (*scan)(const int64_t*, int64_t*, int64_t, int64_t*, hipStream_t)) {
   TWTML_HIP_CHECK(hipMemsetAsync(hist, 0, sizeof(int64_t) * size_t(k + 1), s));
   if (k <= kKmLdsBins) {
@@ -1278,11 +1316,34 @@ void launch_km_cluster_sums(const float* X, const double* f64, const int32_t* la
   int g2 = int(max_rows / kSegRows + 1);
   if (g2 > 4096) g2 = 4096;
   if (k * d + k <= kSegLdsSums)
-    hipLaunchKernelGGL(k_km_segsum<true>, dim3(g2), dim3(kBlock), sizeof(double) * size_t(k * d + k), s, X, f64,
-                       labels, order, counters, k, d, dp, km_cols_pow2(d), sums, counts);
+    hipLaunchKernelGGL(k_km_segsum<true>, dim3(g2), dim3(kBlock), sizeof(int64_t) * size_t(k * d + k), s, X, mx,
+                       labels, order, counters, k, d, dp, km_cols_pow2(d), sums);
   else
-    hipLaunchKernelGGL(k_km_segsum<false>, dim3(g2), dim3(kBlock), 0, s, X, f64, labels, order, counters, k, d,
-                       dp, km_cols_pow2(d), sums, counts);
+    hipLaunchKernelGGL(k_km_segsum<false>, dim3(g2), dim3(kBlock), 0, s, X, mx, labels, order, counters, k, d,
+                       dp, km_cols_pow2(d), sums);
+}
+
+// the all-reduced integer sums -> the fp64 sums of the SCALED features
+// (factor_j 2^s_j sum q) and the counts the update reads
+__global__ void k_km_sums_f64(const int64_t* si, const int64_t* mx, const double* fac, int k, int d,
+                              double* sums, double* counts) {
+  const int64_t total = int64_t(k) * d + k;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += int64_t(gridDim.x) * blockDim.x) {
+    if (i < int64_t(k) * d) {
+      const int j = int(i % d);
+      sums[i] = ldexp(static_cast<double>(si[i]), km_shift(mx[j])) * fac[j];
+    } else {
+      counts[i - int64_t(k) * d] = static_cast<double>(si[i]);
+    }
+  }
+}
+
+void launch_km_sums_f64(const int64_t* si, const int64_t* mx, const double* fac, int k, int d, double* sums,
+                        double* counts, hipStream_t s) {
+  int grid = int((int64_t(k) * d + k + kBlock - 1) / kBlock);
+  if (grid > 8192) grid = 8192;
+  hipLaunchKernelGGL(k_km_sums_f64, dim3(grid), dim3(kBlock), 0, s, si, mx, fac, k, d, sums, counts);
 }
 
 // ---------------------------------------------------------------------------

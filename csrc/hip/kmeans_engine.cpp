@@ -7,6 +7,7 @@
 #include <pybind11/stl.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -37,6 +38,8 @@ KMEngine::KMEngine(int device, const KMConfig& cfg, std::shared_ptr<Comm> comm)
     throw std::invalid_argument("text_dims must be in [0, 4000]");
   if (cfg_.max_rows <= 0 || cfg_.max_rows >= (int64_t(1) << 31)) throw std::invalid_argument("bad max_rows");
   d_ = 2 + cfg_.text_dims;
+  const char* fdp = std::getenv("TWTML_FORCE_DP");
+  dist_ = comm_ && (comm_->world() > 1 || cfg_.force_dp != 0 || (fdp && fdp[0] == '1'));
   dp_ = pad_dim(d_);
   TWTML_HIP_CHECK(hipSetDevice(device_));
   TWTML_HIP_CHECK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
@@ -54,8 +57,8 @@ KMEngine::KMEngine(int device, const KMConfig& cfg, std::shared_ptr<Comm> comm)
   centers_ = km_alloc<double>(k * d);
   weights_ = km_alloc<double>(k);
   sums_ = km_alloc<double>(k * d + k);
-  mom_ = km_alloc<double>(2 * d + 2);
-  stdv_ = km_alloc<double>(d);
+  sums_i_ = km_alloc<int64_t>(k * d + k);
+  qmom_ = km_alloc<int64_t>(d + 1 + 4 * d);   // [d] column max | n | [d][4] sums of q and limbs
   fac64_ = km_alloc<double>(size_t(dp_));
   fac32_ = km_alloc<float>(size_t(dp_));
   blend_ = km_alloc<double>(2 * k);
@@ -73,6 +76,10 @@ KMEngine::KMEngine(int device, const KMConfig& cfg, std::shared_ptr<Comm> comm)
   upload_lower_tables(compute_, &lower_page_, &lower_blocks_);
   TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_out_), sizeof(double) * (4 + d),
                                 hipHostMallocDefault));
+  TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_q_), sizeof(int64_t) * (d + 1 + 4 * d),
+                                hipHostMallocDefault));
+  TWTML_HIP_CHECK(hipHostMalloc(&host_fac_, sizeof(double) * size_t(dp_) + sizeof(float) * size_t(dp_),
+                                hipHostMallocDefault));
   TWTML_HIP_CHECK(hipEventCreate(&ev0_));
   TWTML_HIP_CHECK(hipEventCreate(&ev1_));
   launch_km_centers32(centers_, cfg_.k, d_, dp_, c32_, cnorm_, compute_);
@@ -84,10 +91,12 @@ KMEngine::~KMEngine() {
   (void)hipDeviceSynchronize();
   raw_.release();
   void* bufs[] = {prep_.kept, prep_.nnz, prep_.blk, prep_.hist, prep_.counters, X_, centers_,
-                  weights_, sums_, mom_, stdv_, c32_, cnorm_, labels_, order_, refine_, frag_, cnp_, lhist_, fac64_, fac32_, blend_,
+                  weights_, sums_, sums_i_, qmom_, c32_, cnorm_, labels_, order_, refine_, frag_, cnp_, lhist_, fac64_, fac32_, blend_,
                   lower_page_, lower_blocks_};
   for (void* b : bufs) if (b) (void)hipFree(b);
   if (host_out_) (void)hipHostFree(host_out_);
+  if (host_q_) (void)hipHostFree(host_q_);
+  if (host_fac_) (void)hipHostFree(host_fac_);
   (void)hipEventDestroy(ev0_);
   (void)hipEventDestroy(ev1_);
   (void)hipStreamDestroy(compute_);
@@ -105,7 +114,6 @@ KMResult KMEngine::process(int slot, bool want_labels) {
   TraceRange tr("twtml.km.batch");
   TWTML_HIP_CHECK(hipSetDevice(device_));
   hipStream_t s = compute_;
-  const int world = comm_ ? comm_->world() : 1;
   const int k = cfg_.k, d = d_;
   KMResult res;
   const DevRawBatch b = raw_.acquire(slot, s);
@@ -117,14 +125,20 @@ KMResult KMEngine::process(int slot, bool want_labels) {
   launch_km_features(b, prep_.kept, prep_.counters, X_, dp_, cfg_.text_dims, lower_page_,
                      lower_blocks_, cfg_.max_rows, s);
   raw_.release_slot(slot, s);
-  // scaler pass 1: n and column sums (global)
-  TWTML_HIP_CHECK(hipMemsetAsync(mom_, 0, sizeof(double) * size_t(2 * d + 2), s));
-  launch_km_moments(X_, prep_.counters, d, dp_, 0, mom_, mom_, cfg_.max_rows, s);
-  if (world > 1) comm_->allreduce(mom_, size_t(d + 1), ncclFloat64, ncclSum, s);
-  TWTML_HIP_CHECK(hipMemcpyAsync(host_out_, mom_, sizeof(double), hipMemcpyDeviceToHost, s));
+  // K11 scaler, exact: the column max (all-reduced MAX) fixes every column's
+  // quantization shift, then n and the integer column sums (all-reduced SUM);
+  // both are the same bits on every rank and in any summation order
+  int64_t* mx = qmom_;
+  int64_t* mq = qmom_ + d;
+  TWTML_HIP_CHECK(hipMemsetAsync(qmom_, 0, sizeof(int64_t) * size_t(d + 1 + 4 * d), s));
+  launch_km_colmax(X_, prep_.counters, d, dp_, mx, cfg_.max_rows, s);
+  if (dist_) comm_->allreduce(mx, size_t(d), ncclInt64, ncclMax, s);
+  launch_km_moments_q(X_, prep_.counters, d, dp_, mx, mq, cfg_.max_rows, s);
+  if (dist_) comm_->allreduce(mq, size_t(1 + 4 * d), ncclInt64, ncclSum, s);
+  TWTML_HIP_CHECK(hipMemcpyAsync(host_q_, qmom_, sizeof(int64_t) * size_t(d + 1 + 4 * d), hipMemcpyDeviceToHost, s));
   TWTML_HIP_CHECK(hipMemcpyAsync(host_out_ + 1, prep_.counters, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   TWTML_HIP_CHECK(hipStreamSynchronize(s));
-  res.n_global = int64_t(host_out_[0] + 0.5);
+  res.n_global = host_q_[d];
   int64_t nl;
   std::memcpy(&nl, host_out_ + 1, sizeof(int64_t));
   res.n_local = nl;
@@ -133,11 +147,37 @@ KMResult KMEngine::process(int slot, bool want_labels) {
     TWTML_HIP_CHECK(hipStreamSynchronize(s));
     return res;
   }
-  if (cfg_.scale) {
-    launch_km_moments(X_, prep_.counters, d, dp_, 1, mom_, mom_ + d + 1, cfg_.max_rows, s);
-    if (world > 1) comm_->allreduce(mom_ + d + 1, size_t(d), ncclFloat64, ncclSum, s);
+  // std_j = sqrt(M2_j / (n - 1)) (n < 2 -> 0); factor_j = std_j != 0 ? 1 / std_j : 0
+  // (StandardScalerModel.transform), M2 = (n sum q^2 - (sum q)^2) / n in
+  // 128-bit integers; scale == 0 -> factor 1
+  double* f64 = static_cast<double*>(host_fac_);
+  float* f32 = reinterpret_cast<float*>(f64 + dp_);
+  if (cfg_.scale) res.std.assign(size_t(d), 0.0);
+  for (int j = 0; j < dp_; ++j) {
+    double f = 0.0;
+    if (j < d) {
+      if (cfg_.scale) {
+        const int64_t n = res.n_global;
+        const int64_t* m = host_q_ + d + 1 + 4 * j;
+        const __int128 s2 = (__int128(m[1]) << 32) + (__int128(m[2]) << 16) + __int128(m[3]);
+        const __int128 num = __int128(n) * s2 - __int128(m[0]) * __int128(m[0]);
+        double sd = 0.0;
+        if (n > 1 && num > 0) {
+          const long double var = std::ldexp(static_cast<long double>(num), 2 * km_quant_shift(host_q_[j])) /
+                                  (static_cast<long double>(n) * static_cast<long double>(n - 1));
+          sd = std::sqrt(static_cast<double>(var));
+        }
+        res.std[size_t(j)] = sd;
+        f = sd != 0.0 ? 1.0 / sd : 0.0;
+      } else {
+        f = 1.0;
+      }
+    }
+    f64[j] = f;
+    f32[j] = float(f);
   }
-  launch_km_factor(d, dp_, cfg_.scale != 0, mom_, mom_ + d + 1, stdv_, fac64_, fac32_, s);
+  TWTML_HIP_CHECK(hipMemcpyAsync(fac64_, f64, sizeof(double) * size_t(dp_), hipMemcpyHostToDevice, s));
+  TWTML_HIP_CHECK(hipMemcpyAsync(fac32_, f32, sizeof(float) * size_t(dp_), hipMemcpyHostToDevice, s));
   // K8 assignment with the current centres, K9 sums, K10 update.  The
   // near-tie lists in refine_, their counts in counters[5..6].
   auto* refine_cnt = reinterpret_cast<unsigned long long*>(prep_.counters + 5);
@@ -154,10 +194,11 @@ KMResult KMEngine::process(int slot, bool want_labels) {
                  static_cast<long long>(res.n_local), c[0], c[1]);
   };
   debug_refine("update");
-  TWTML_HIP_CHECK(hipMemsetAsync(sums_, 0, sizeof(double) * (size_t(k) * d + k), s));
-  launch_km_cluster_sums(X_, fac64_, labels_, prep_.counters, k, d, dp_, lhist_, order_, sums_,
-                         sums_ + size_t(k) * d, cfg_.max_rows, s, &scan_excl_launch);
-  if (world > 1) comm_->allreduce(sums_, size_t(k) * d + k, ncclFloat64, ncclSum, s);
+  TWTML_HIP_CHECK(hipMemsetAsync(sums_i_, 0, sizeof(int64_t) * (size_t(k) * d + k), s));
+  launch_km_cluster_sums(X_, mx, labels_, prep_.counters, k, d, dp_, lhist_, order_, sums_i_, cfg_.max_rows, s,
+                         &scan_excl_launch);
+  if (dist_) comm_->allreduce(sums_i_, size_t(k) * d + k, ncclInt64, ncclSum, s);
+  launch_km_sums_f64(sums_i_, mx, fac64_, k, d, sums_, sums_ + size_t(k) * d, s);
   launch_km_update(centers_, weights_, sums_, sums_ + size_t(k) * d, k, d, cfg_.decay,
                    cfg_.points_unit != 0, blend_, c32_, cnorm_, dp_, s);
   if (want_labels)   // KMeans.scala:113 predicts with the updated model
@@ -165,8 +206,6 @@ KMResult KMEngine::process(int slot, bool want_labels) {
                      refine_, refine_cnt, frag_, cnp_, cfg_.max_rows, cfg_.mfma != 0, cfg_.mfma == 1, s);
   if (want_labels) debug_refine("predict");
   TWTML_HIP_CHECK(hipEventRecord(ev1_, s));
-  if (cfg_.scale)
-    TWTML_HIP_CHECK(hipMemcpyAsync(host_out_ + 4, stdv_, sizeof(double) * size_t(d), hipMemcpyDeviceToHost, s));
   if (want_labels && res.n_local > 0) {
     res.labels.resize(size_t(res.n_local));
     TWTML_HIP_CHECK(hipMemcpyAsync(res.labels.data(), labels_, sizeof(int32_t) * size_t(res.n_local),
@@ -174,7 +213,6 @@ KMResult KMEngine::process(int slot, bool want_labels) {
   }
   TWTML_HIP_CHECK(hipStreamSynchronize(s));
   if (comm_) comm_->check_async();
-  if (cfg_.scale) res.std.assign(host_out_ + 4, host_out_ + 4 + d);
   TWTML_HIP_CHECK(hipEventElapsedTime(&res.ms, ev0_, ev1_));
   return res;
 }
@@ -234,6 +272,7 @@ void bind_kmeans(py::module_& m) {
 #define GET(name, type) if (d.contains(#name)) c.name = d[#name].cast<type>();
              GET(k, int32_t) GET(text_dims, int32_t) GET(decay, double) GET(points_unit, int32_t)
              GET(scale, int32_t) GET(mfma, int32_t) GET(max_rows, int64_t) GET(max_units, int64_t)
+             GET(force_dp, int32_t)
 #undef GET
              py::gil_scoped_release nogil;
              return std::make_shared<KMEngine>(device, c, comm);

@@ -24,6 +24,7 @@ struct KMConfig {
   int32_t mfma = 1;
   int64_t max_rows = 1 << 16;
   int64_t max_units = (1 << 16) * 281;
+  int32_t force_dp = 0;        // DP collectives even with a world-1 communicator (also TWTML_FORCE_DP=1)
 };
 
 struct KMResult {
@@ -55,12 +56,17 @@ class KMEngine {
   int device_;
   KMConfig cfg_;
   int d_, dp_;
+  bool dist_ = false;   // DP collectives: world > 1, or forced with a world-1 communicator
   std::shared_ptr<Comm> comm_;
   hipStream_t compute_ = nullptr, copy_ = nullptr;
   RawSlots raw_;
   DevPrepared prep_{};
   float* X_ = nullptr;
-  double *centers_ = nullptr, *weights_ = nullptr, *sums_ = nullptr, *mom_ = nullptr, *stdv_ = nullptr;
+  double *centers_ = nullptr, *weights_ = nullptr, *sums_ = nullptr;
+  int64_t* sums_i_ = nullptr;          // [k d + k] per-cluster integer sums of q, counts (all-reduced)
+  int64_t* qmom_ = nullptr;            // [d] column max | n | [d][4] integer moments (all-reduced)
+  int64_t* host_q_ = nullptr;          // pinned copy of qmom_
+  void* host_fac_ = nullptr;           // pinned [dp] fp64 + [dp] fp32 factors (H2D staging)
   float *c32_ = nullptr, *cnorm_ = nullptr, *fac32_ = nullptr;
   double *fac64_ = nullptr, *blend_ = nullptr;
   int32_t *labels_ = nullptr, *order_ = nullptr, *refine_ = nullptr;

@@ -103,6 +103,15 @@ PYBIND11_MODULE(_twtml_host, m) {
           if (kind < 0) throw std::invalid_argument("hash must be 'java' or 'murmur3'");
           if (F <= 0) throw std::invalid_argument("F must be positive");
           const int64_t nr = offsets.size() - 1;
+          if (nr < 0) throw std::invalid_argument("offsets must have n + 1 entries");
+          // every row's units must lie in the text (a batch whose UTF-16 copy
+          // was dropped for its UTF-8 bytes has an empty text: RawBatch.ensure_text)
+          if (nr > 0 && (offsets.data()[0] < 0 || offsets.data()[nr] > int64_t(text.size())))
+            throw std::invalid_argument("featurize_rows: offsets exceed the text (" +
+                                        std::to_string(offsets.data()[nr]) + " > " +
+                                        std::to_string(text.size()) + " units)");
+          for (int64_t i = 0; i < nr; ++i)
+            if (offsets.data()[i + 1] < offsets.data()[i]) throw std::invalid_argument("offsets not ascending");
           for (py::ssize_t i = 0; i < rows.size(); ++i)
             if (rows.data()[i] < 0 || rows.data()[i] >= nr) throw std::out_of_range("row id");
           std::vector<int64_t> indptr, indices;

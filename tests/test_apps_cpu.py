@@ -87,3 +87,27 @@ def test_kmeans_driver_cpu(sinks, tmp_path, monkeypatch):
     assert c.shape == (3, 2) and w is not None and w.sum() > 0
     assert any(p == "/sessions/" for (_, p, _) in lgn.calls)
     assert WebClient(web.url).stats().count > 0
+
+
+def test_cpu_drivers_on_replayed_utf8_batches(tmp_path, monkeypatch):
+    """``replay:synthetic`` batches carry only their UTF-8
+    bytes (empty UTF-16 text); the CPU engines must decode them, not read
+    past a zero-length text array."""
+    metrics = tmp_path / "m.jsonl"
+    monkeypatch.setenv("TWTML_METRICS", str(metrics))
+    args = ["--master", "local[1]", "--lightning", "http://127.0.0.1:9", "--twtweb", "http://127.0.0.1:9",
+            "--source", "replay:synthetic:bench:2", "--batchSize", "600", "--seconds", "0",
+            "--sourceRate", "0", "--numBatches", "2", "-f", "1000"]
+    assert lr_app.main(args) == 0
+    recs = [json.loads(l) for l in open(metrics) if '"summary"' not in l]
+    assert len(recs) == 2 and all(r["batch"] > 0 for r in recs)
+    monkeypatch.setenv("TWTML_METRICS", str(tmp_path / "k.jsonl"))
+    assert km_app.main(["--master", "local[1]", "--source", "replay:synthetic:bench:2", "--batchSize", "600",
+                        "--seconds", "0", "--sourceRate", "0", "--numBatches", "2", "--textDims", "6"]) == 0
+
+
+def test_featurize_rows_rejects_offsets_beyond_text():
+    from twitter_stream_ml_amd.ops._native import host
+    with pytest.raises(ValueError, match="exceed"):
+        host().featurize_rows(np.zeros(0, np.uint16), np.array([0, 5, 9], np.int64),
+                              np.array([0, 1], np.int64), 1000, "java", 0)

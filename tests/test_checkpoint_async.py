@@ -113,3 +113,45 @@ def test_checkpoint_positions_recorded_before_model(tmp_path):
     pos = StreamPositions(str(tmp_path / "ck"), 0).history()
     assert pos == {2: 200, 4: 400, 6: 600}
     assert load_progress(str(tmp_path / "ck"))["batches"] == 6
+
+
+def test_positions_survive_a_slow_writer(tmp_path):
+    """with --checkpointInterval 1 an asynchronous write
+    spans many batches; every position a resume could need -- the model on
+    disk (and a .old copy) and the write in flight -- must survive pruning
+    at every point of a long run."""
+    from twitter_stream_ml_amd.apps._common import load_resume_state
+    from twitter_stream_ml_amd.checkpoint import StreamPositions
+    log = []
+    m = _SlowModel(30.0, log)
+    path = str(tmp_path / "ck")
+    ck = StreamCheckpointer(path, 1, 0, m.snapshot, lambda: None, asynchronous=True)
+    other = StreamPositions(path, 1)   # a second rank records its own positions
+    inflight = None
+    for t in range(1, 61):
+        started = ck.after_batch(t, 10 * t, 10 * t)
+        other.record(t, 7 * t)
+        if started:
+            inflight = t
+        if t % 25 == 0:   # let the write in flight land now and then
+            m.gate.set()
+            ck._thread.join()
+            m.gate.clear()
+        prog = load_progress(path)
+        if prog is not None:
+            b = prog["batches"]
+            assert StreamPositions(path, 0).records_at(b) == 10 * b
+            assert StreamPositions(path, 1).records_at(b) == 7 * b
+            st = load_resume_state("auto", path, 1)
+            assert (st.batches, st.records) == (b, 7 * b)
+        # the batch of the write in flight stays recorded on every rank
+        th = ck._thread
+        if th is not None and th.is_alive():
+            assert StreamPositions(path, 0).records_at(inflight) == 10 * inflight
+            assert StreamPositions(path, 1).records_at(inflight) == 7 * inflight
+    m.gate.set()
+    ck.flush()
+    # bounded history: once the newest model landed, old positions go
+    ck.after_batch(61, 610, 610, force=True)
+    other.record(61, 427)
+    assert len(StreamPositions(path, 0).history()) <= 16 + 1

@@ -127,33 +127,19 @@ def test_lr_dp_processes_equal_single_engine(dp_runs, ci):
 
 
 def test_kmeans_dp_processes(dp_runs):
+    """Exact integer scaler moments and cluster sums: DP k-means over 2-4
+    processes equals the single engine on every cluster, bit for bit."""
     from twitter_stream_ml_amd.ops.kmeans_engine import DeviceKMeans
     world, ranks = dp_runs
     single = DeviceKMeans(_km_cfg(), device=0)
     for t, full in enumerate(_batches("twitter", 4000, 3, seed=8)):
-        c_prev = single.get_state()[0]
         r1 = single.update_raw(full)
         assert sum(int(d[f"km{t}_n"][1]) for d in ranks) == r1["n"]
         c1, w1 = single.get_state()
-        # centres too, not only weight sums: equal up to the fp64 summation
-        # order of the per-cluster sums unless an assignment against the old
-        # centres was ill-conditioned (a point may then sit in either twin)
-        from twitter_stream_ml_amd.models.kmeans import kmeans_features
-        from twitter_stream_ml_amd.oracle.mllib import standard_scaler_transform
-        from test_gpu_kmeans import _gap_check
-        Xs = standard_scaler_transform(kmeans_features(full, 4)[0], np.asarray(r1["std"]))
-        ok, _ = _gap_check(Xs, c_prev)
         for d in ranks:
             assert int(d[f"km{t}_n"][0]) == r1["n"]
-            np.testing.assert_allclose(d[f"km{t}_w"].sum(), w1.sum(), rtol=1e-9)
-            if ok.all():
-                np.testing.assert_allclose(d[f"km{t}_w"], w1, rtol=1e-9, atol=1e-12)
-                np.testing.assert_allclose(d[f"km{t}_c"], c1, rtol=1e-9, atol=1e-9)
-        for d in ranks[1:]:
-            np.testing.assert_array_equal(d[f"km{t}_c"], ranks[0][f"km{t}_c"])
-        # continue from the DP state: per-batch comparison (ill-conditioned
-        # split ties may flip a point, see test_gpu_kmeans.py)
-        single.set_state(ranks[0][f"km{t}_c"], ranks[0][f"km{t}_w"])
+            np.testing.assert_array_equal(d[f"km{t}_c"], c1)
+            np.testing.assert_array_equal(d[f"km{t}_w"], w1)
 
 
 def test_torchrun_bench_two_ranks_gloo(hip_module):

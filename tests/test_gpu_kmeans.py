@@ -117,11 +117,11 @@ def test_kmeans_empty_batch_is_noop(hip_module):
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_kmeans_dp_loopback(hip_module, world):
-    """DP k-means equals the single engine batch by batch: exactly (fp64
-    summation-order noise only) whenever every point's assignment against the
-    old centres is well conditioned; otherwise the only allowed difference is
-    the ill-conditioned points moving between clusters, and the single
-    engine continues from the DP state."""
+    """DP k-means equals the single engine bit for bit, batch after batch:
+    a point's label depends only on the point and the (replicated) centres,
+    and the scaler moments and per-cluster sums are exact int64 sums
+    (``csrc/hip/kmeans.hip`` K11 / K9), equal in any order over any sharding
+    (VERDICT r3 #5: the fp64 sums needed conditioning checks here)."""
     from twitter_stream_ml_amd.ops.kmeans_engine import DeviceKMeans
     cfg = _cfg(6, 4, seed=2)
     group = hip_module.LoopbackGroup(world)
@@ -145,42 +145,26 @@ def test_kmeans_dp_loopback(hip_module, world):
         x.join(timeout=300)
     assert not errors, errors
     single = DeviceKMeans(cfg, device=0)
-    exact = 0
     for t, full in enumerate(batches):
-        c_old = single.get_state()[0]
         r1 = single.update_raw(full)
         c1, w1 = single.get_state()
         assert sum(out[r][t]["n_local"] for r in range(world)) == r1["n"]
-        X, _ = kmeans_features(full, 4)
-        std = np.asarray(r1["std"])
-        Xs = X * np.where(std != 0, 1.0 / np.where(std != 0, std, 1.0), 0.0)
-        n_ill = np.count_nonzero(~_well_conditioned(Xs, c_old))
+        # contiguous shards: the ranks' labels concatenate to the single engine's
+        pred = np.concatenate([np.asarray(out[r][t]["pred"]) for r in range(world)])
+        np.testing.assert_array_equal(pred, np.asarray(r1["pred"]))
         for r in range(world):
             assert out[r][t]["n"] == r1["n"]
-            np.testing.assert_allclose(out[r][t]["std"], r1["std"], rtol=1e-12)
+            np.testing.assert_array_equal(out[r][t]["std"], r1["std"])
             c, w = states[r][t]
-            np.testing.assert_array_equal(c, states[0][t][0])   # replicas bit-identical
-            np.testing.assert_allclose(w.sum(), w1.sum(), rtol=1e-12)
-            if n_ill == 0:
-                np.testing.assert_allclose(w, w1, rtol=1e-12, atol=1e-12)
-                np.testing.assert_allclose(c, c1, rtol=1e-9, atol=1e-12 * max(1.0, np.abs(c1).max()))
-            else:
-                assert np.abs(w - w1).sum() <= 2 * n_ill + 1e-9, (w, w1, n_ill)
-        exact += n_ill == 0
-        single.set_state(*states[0][t])
-    assert exact >= 1   # at least one batch compared exactly
+            np.testing.assert_array_equal(c, c1)
+            np.testing.assert_array_equal(w, w1)
 
 
 def test_kmeans_utf8_ingest_equals_wire(hip_module):
     """The end-to-end bench stages k-means batches as raw UTF-8 (device
-    decode); per batch it must agree with the host-packed wire ingest: same
-    points (count, scaler), same assignments except for points equidistant
-    from the two halves of a just-split cluster (the two paths order rows
-    differently, so fp64 sums differ in the last bits and such ties may flip,
-    see test_kmeans_matches_cpu), conserved total weight.  The UTF-8 engine
-    continues from the wire engine's state after every batch.  (The decoded
-    text itself is checked exactly against the oracle by the LR featurize
-    tests.)"""
+    decode); per batch it must equal the host-packed wire ingest bit for bit:
+    same points, scaler, labels and model (the two paths order rows
+    differently, which the exact integer sums do not see)."""
     from twitter_stream_ml_amd.ops.kmeans_engine import DeviceKMeans
     from twitter_stream_ml_amd.ops.lr_engine import encode_utf8
     cfg = _cfg(16, 14, seed=6)
@@ -191,14 +175,12 @@ def test_kmeans_utf8_ingest_equals_wire(hip_module):
         b.submit(hb, 0)
         rb = b.process(0)
         assert ra["n"] == rb["n"]
-        np.testing.assert_allclose(rb["std"], ra["std"], rtol=1e-12)
-        pa, pb = np.asarray(ra["pred"]), np.asarray(rb["pred"])
-        assert pa.shape == pb.shape and np.count_nonzero(pa != pb) <= 4, np.count_nonzero(pa != pb)
+        np.testing.assert_array_equal(rb["std"], ra["std"])
+        np.testing.assert_array_equal(np.asarray(ra["pred"]), np.asarray(rb["pred"]))
         ca, wa = a.get_state()
         cb, wb = b.get_state()
-        np.testing.assert_allclose(wb.sum(), wa.sum(), rtol=1e-12)
-        assert np.abs(wb - wa).sum() <= 4.0, (wa, wb)
-        b.set_state(ca, wa)
+        np.testing.assert_array_equal(cb, ca)
+        np.testing.assert_array_equal(wb, wa)
 
 
 def _split_twins(C, w):

@@ -1,11 +1,19 @@
-"""The real RCCL communicator (``RcclComm``) on one MI355X.
+"""The engines' DP path over a real RCCL communicator on one MI355X.
 
-The multi-GPU path (``parallel/dist.py:make_rccl_comm`` -> ``csrc/hip/comm.cpp``)
-only runs with several GPUs, and RCCL refuses two ranks on one device, so the
-DP orchestration itself is covered by ``test_gpu_dp_loopback.py``.  Here a
-world-1 communicator goes through the same ``ncclGetUniqueId`` ->
-``ncclCommInitRank`` -> ``ncclAllReduce`` calls on a real stream, and engines
-built with it train exactly like engines without one.
+RCCL refuses two ranks on one device, so the multi-rank DP orchestration runs
+through gloo / loopback elsewhere (``test_gpu_dp_procs.py``,
+``test_gpu_dp_loopback.py``).  Here the *transport* is the real one: engines
+built with ``force_dp`` and a world-1 ``RcclComm`` take every DP branch of
+``csrc/hip/engine.cpp`` -- the prep packet and its ``ncclAllGather`` (issued
+between two GD iterations of the previous batch when prepared ahead, else in
+line after an ``ncclAllReduce`` of the active-set sizes), ``k_sgd_reduce`` and
+the packed ``ncclInt64`` gradient all-reduce every GD iteration, the
+all-reduced verdict / ready words, and the fp64 stats all-reduce -- with RCCL
+kernels on the engine's compute stream.  The fixed-point GD is exact, so the
+forced-DP engine must equal the plain one-GPU engine bit for bit (weights,
+stats, loss history, iteration counts), and the communicator's counters must
+show the traffic (reference: ``LinearRegression.scala:86`` trainOn ->
+per-iteration treeAggregate).
 """
 import numpy as np
 import pytest
@@ -15,9 +23,19 @@ from twitter_stream_ml_amd.sources.synthetic import SynthConfig, generate_batch
 pytestmark = pytest.mark.gpu
 NOW = 1_700_000_000_000
 
+# (profile, F, hash, rows per batch, batches, expect tiered)
+LR_CASES = [("twitter", 1 << 20, "java", 6000, 3, False),
+            ("wide", 1 << 20, "java", 20000, 3, True),
+            ("wide", 100_000_000, "murmur3", 20000, 2, True)]
+
 
 def _comm(h):
     return h.Comm(h.rccl_unique_id(), 0, 1, 0)
+
+
+def _batches(profile, rows, n, seed):
+    synth = SynthConfig.profile(profile, seed=seed)
+    return [generate_batch(synth, t * rows, rows, batch_time_ms=NOW + t * 5000) for t in range(n)]
 
 
 def test_rccl_world1_allreduce_identity(hip_module):
@@ -26,41 +44,77 @@ def test_rccl_world1_allreduce_identity(hip_module):
     assert len(h.rccl_unique_id()) == 128
     assert int(h.rccl_version()) > 0
     comm = _comm(h)
-    assert (comm.rank, comm.world) == (0, 1)
+    assert (comm.rank, comm.world, comm.kind) == (0, 1, "rccl")
     x = torch.arange(1, 4097, dtype=torch.float64, device="cuda:0") * 0.25
     ref = x.clone()
     torch.cuda.synchronize()
     comm.allreduce_f64(x.data_ptr(), x.numel())
     torch.testing.assert_close(x, ref, rtol=0, atol=0)
     comm.check()
+    c = comm.counters()
+    assert c["allreduce_calls"] == 1 and c["allreduce_bytes"] == 8 * 4096
 
 
-def test_engines_with_rccl_comm_match_no_comm(hip_module):
-    from twitter_stream_ml_amd.ops.kmeans_engine import DeviceKMeans, KMDeviceConfig
+def _train(eng, batches, ahead):
+    out = []
+    if ahead:   # queued: batch t+1 is prepared while t trains (mid-loop all-gather)
+        for b in batches[:eng.raw_slots - 1]:
+            assert eng.prefetch(b)
+    for b in batches:
+        out.append(eng.train_batch(b, want_pred=True))
+    return out
+
+
+@pytest.mark.parametrize("ci", range(len(LR_CASES)), ids=["toy", "wide-tiered", "1e8-murmur3"])
+@pytest.mark.parametrize("ahead", [True, False], ids=["ahead", "inline"])
+def test_forced_dp_rccl_equals_plain_engine(hip_module, ci, ahead):
     from twitter_stream_ml_amd.ops.lr_engine import DeviceLinearRegression, LRDeviceConfig
-    h = hip_module
-    synth = SynthConfig.profile("twitter", seed=5, unicode_fraction=0.1)
-    batches = [generate_batch(synth, t * 2000, 2000, batch_time_ms=NOW + t) for t in range(2)]
+    profile, F, hsh, rows, nb, tiered = LR_CASES[ci]
+    if F >= 100_000_000 and not ahead:
+        pytest.skip("the 1e8 case runs prepared ahead only (time)")
+    batches = _batches(profile, rows, nb, seed=70 + ci)
+    base = dict(num_text_features=F, hash=hsh, max_rows=rows, max_units=rows * 300, num_iterations=20)
+    comm = _comm(hip_module)
+    dp = DeviceLinearRegression(LRDeviceConfig(force_dp=True, comm_timing=True, **base), device=0, comm=comm)
+    plain = DeviceLinearRegression(LRDeviceConfig(**base), device=0)
+    rd = _train(dp, batches, ahead)
+    rp = _train(plain, batches, ahead)
+    total_iters = 0
+    for a, b in zip(rd, rp):
+        assert bool(b["tiered"]) == tiered
+        assert (a["iterations"], a["n_kept"], a["n_kept_global"], a["n_unique"], bool(a["tiered"])) == \
+               (b["iterations"], b["n_kept"], b["n_kept"], b["n_unique"], tiered)
+        assert list(a["stats"]) == list(b["stats"])
+        assert list(a["loss_history"]) == list(b["loss_history"])
+        np.testing.assert_array_equal(np.asarray(a["pred"]), np.asarray(b["pred"]))
+        # one packed int64 gradient all-reduce per GD iteration, timed on the stream
+        assert a["comm_iters"] == a["iterations"] and b["comm_iters"] == 0
+        assert a["comm_ms"] > 0.0
+        total_iters += a["iterations"]
+    np.testing.assert_array_equal(dp.get_weights(), plain.get_weights())
+    c = comm.counters()
+    # gradient all-reduces + one stats all-reduce per batch (+ the in-line
+    # active-set size all-reduce of a batch not gathered ahead)
+    assert total_iters + nb <= c["allreduce_calls"] <= total_iters + 2 * nb
+    assert c["allgather_calls"] == nb          # one prep-packet all-gather per batch
+    assert c["allreduce_bytes"] > 8 * total_iters
 
-    cfg = LRDeviceConfig(num_text_features=1 << 20, max_rows=4096, max_units=4096 * 300,
-                         num_iterations=10)
-    a = DeviceLinearRegression(cfg, device=0, comm=_comm(h))
-    b = DeviceLinearRegression(cfg, device=0)
-    for bt in batches:
-        ra, rb = a.train_batch(bt, want_pred=False), b.train_batch(bt, want_pred=False)
-        assert ra["iterations"] == rb["iterations"]
-    # the cold-tail gradient flush uses fp64 atomics, so two runs agree to
-    # rounding, not bitwise (same tolerance as test_gpu_dp_loopback.py)
-    wb = b.get_weights()
-    np.testing.assert_allclose(a.get_weights(), wb, rtol=1e-4, atol=1e-6 * max(np.abs(wb).max(), 1e-12))
 
-    kcfg = KMDeviceConfig(k=64, text_dims=14, half_life=5.0, max_rows=4096,
-                          max_units=4096 * 300, seed=3)
-    ka = DeviceKMeans(kcfg, device=0, comm=_comm(h))
-    kb = DeviceKMeans(kcfg, device=0)
+def test_forced_dp_kmeans_rccl(hip_module):
+    from twitter_stream_ml_amd.ops.kmeans_engine import DeviceKMeans, KMDeviceConfig
+    batches = _batches("twitter", 4000, 3, seed=8)
+    kcfg = dict(k=64, text_dims=14, half_life=5.0, max_rows=4096, max_units=4096 * 300, seed=3)
+    comm = _comm(hip_module)
+    ka = DeviceKMeans(KMDeviceConfig(force_dp=True, **kcfg), device=0, comm=comm)
+    kb = DeviceKMeans(KMDeviceConfig(**kcfg), device=0)
     for bt in batches:
-        ka.update_raw(bt, want_pred=False)
-        kb.update_raw(bt, want_pred=False)
+        ra = ka.update_raw(bt, want_pred=True)
+        rb = kb.update_raw(bt, want_pred=True)
+        assert ra["n"] == rb["n"]
+        np.testing.assert_array_equal(ra["pred"], rb["pred"])
     (ca, wa), (cb, wb) = ka.get_state(), kb.get_state()
-    np.testing.assert_allclose(ca, cb, rtol=1e-9, atol=1e-12)
-    np.testing.assert_allclose(wa, wb, rtol=1e-12)
+    # exact integer moments and cluster sums (csrc/hip/kmeans.hip): bit for bit
+    np.testing.assert_array_equal(ca, cb)
+    np.testing.assert_array_equal(wa, wb)
+    c = comm.counters()
+    assert c["allreduce_calls"] >= 3 * len(batches)   # scaler moments x2 + cluster sums per batch

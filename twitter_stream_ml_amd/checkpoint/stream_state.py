@@ -21,11 +21,52 @@ __all__ = ["StreamPositions", "resolve_resume"]
 
 
 class StreamPositions:
+    """This rank's ``{batches: records consumed}`` history.
+
+    Pruning never drops a position a resume can still ask for: every entry at
+    or above the oldest batch count of a model on disk (``<checkpoint>`` and a
+    ``<checkpoint>.old`` left by an interrupted replacement) is kept, plus the
+    newest ``keep`` entries.  A write still in flight is newer than the models
+    on disk, so its position survives too, however many batches the write
+    spans (with ``--checkpointInterval 1`` one asynchronous write
+    covers dozens of batches)."""
+
     def __init__(self, checkpoint: str, rank: int, keep: int = 16):
-        self.dir = os.path.abspath(checkpoint) + ".stream"
+        self.checkpoint = os.path.abspath(checkpoint)
+        self.dir = self.checkpoint + ".stream"
         self.path = os.path.join(self.dir, f"rank-{int(rank)}.json")
         self.keep = int(keep)
         self._h: Optional[Dict[int, int]] = None   # this rank's history (it is the only writer)
+        self._floor_key = None
+        self._floor = 0
+
+    def disk_floor(self) -> int:
+        """Oldest batch count of a model on disk (0 if none): positions at or
+        above it must be kept.  Cached on the progress files' mtimes, so the
+        per-batch cost is two ``stat`` calls."""
+        keys, found = [], []
+        for d in (self.checkpoint, self.checkpoint + ".old"):
+            p = os.path.join(d, "streaming", "progress.json")
+            try:
+                st = os.stat(p)
+            except OSError:
+                keys.append(None)
+                continue
+            keys.append((st.st_mtime_ns, st.st_ino))
+            found.append(p)
+        key = tuple(keys)
+        if key == self._floor_key:
+            return self._floor
+        vals = []
+        for p in found:
+            try:
+                with open(p) as fh:
+                    vals.append(int(json.load(fh).get("batches", 0)))
+            except (OSError, ValueError):
+                # replaced between the stat and the open: keep everything this time
+                return 0
+        self._floor_key, self._floor = key, (min(vals) if vals else 0)
+        return self._floor
 
     def history(self) -> Dict[int, int]:
         if self._h is not None:
@@ -36,13 +77,18 @@ class StreamPositions:
         except (OSError, ValueError):
             return {}
 
-    def record(self, batches: int, records: int) -> None:
+    def record(self, batches: int, records: int, floor: Optional[int] = None) -> None:
+        """Record this rank's position after ``batches``.  ``floor``: the
+        oldest batch count a resume may still need (default: from the models
+        on disk, :meth:`disk_floor`)."""
         # kept in memory after the first read: with --checkpointInterval 1 this
         # runs on the training thread every batch (one small atomic write, no read)
         h = self.history()
         h[int(batches)] = int(records)
+        lo = self.disk_floor() if floor is None else int(floor)
         for k in sorted(h)[:-self.keep]:
-            del h[k]
+            if k < lo:
+                del h[k]
         os.makedirs(self.dir, exist_ok=True)
         fd, tmp = tempfile.mkstemp(prefix=".pos-", dir=self.dir)
         with os.fdopen(fd, "w") as fh:

@@ -44,6 +44,7 @@ def kmeans_features(raw: RawBatch, text_dims: int = 0, hash: str = "java"):
     X[:, 1] = raw.scalars[FOLLOWERS, rows]
     if text_dims > 0 and n:
         from ..ops._native import host
+        raw.ensure_text()   # a replayed batch may carry only its UTF-8 bytes
         indptr, idx = host().featurize_rows(raw.text, raw.offsets, rows, text_dims, hash, 0)
         r = np.repeat(np.arange(n), np.diff(indptr))
         np.add.at(X, (r, 2 + idx), 1.0)

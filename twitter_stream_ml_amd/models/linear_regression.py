@@ -87,6 +87,7 @@ def featurize_columnar(raw: RawBatch, num_text_features: int, begin: int, end: i
     n = rows.shape[0]
     if n == 0:
         return sp.csr_matrix((0, F + 4)), np.zeros(0), rows
+    raw.ensure_text()   # a replayed batch may carry only its UTF-8 bytes
     indptr, idx = host().featurize_rows(raw.text, raw.offsets, rows, F, hash, 0)
     lens = np.diff(indptr)
     row_of = np.repeat(np.arange(n, dtype=np.int64), lens)

@@ -60,6 +60,9 @@ class KMDeviceConfig:
     # UTF-8 bytes (DMA'd in place when page-locked; the device decodes),
     # "wire" runs the host packer
     ingest: str = "utf8"
+    # take the DP path (scaler / cluster-sum all-reduces) even with a
+    # world-1 communicator: RCCL carries the collectives on one GPU
+    force_dp: bool = False
 
     def as_dict(self) -> Dict[str, object]:
         if self.time_unit not in ("batches", "points"):
@@ -73,6 +76,7 @@ class KMDeviceConfig:
             "mfma": 0 if not self.mfma else (1 if self.precision == "bf16x3" else 2),
             "max_rows": int(self.max_rows),
             "max_units": int(self.max_units),
+            "force_dp": int(bool(self.force_dp)),
         }
 
 

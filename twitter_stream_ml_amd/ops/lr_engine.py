@@ -86,6 +86,13 @@ class LRDeviceConfig:
     # engine's prep thread) while batch t trains; DP ranks all-gather their
     # prep packets between two of t's GD iterations (engine.cpp issue_c1)
     overlap: bool = True
+    # take the DP path with a world-1 communicator (the packet all-gather,
+    # the packed int64 gradient all-reduce per GD iteration and the stats
+    # all-reduce all go through it): RCCL carries the DP traffic on one GPU
+    force_dp: bool = False
+    # DP: time each gradient all-reduce on the compute stream (result
+    # "comm_ms"; events around the collective)
+    comm_timing: bool = False
 
     def as_dict(self) -> Dict[str, object]:
         return {
@@ -107,6 +114,8 @@ class LRDeviceConfig:
             "hybrid": int(bool(self.hybrid)),
             "lazy_idx": int(bool(self.lazy_idx)),
             "overlap": int(bool(self.overlap)),
+            "force_dp": int(bool(self.force_dp)),
+            "comm_timing": int(bool(self.comm_timing)),
         }
 
 

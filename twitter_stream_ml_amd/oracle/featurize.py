@@ -40,6 +40,7 @@ def filter_mask(raw: RawBatch, begin: int, end: int) -> np.ndarray:
 
 
 def lowered_units(raw: RawBatch, i: int) -> np.ndarray:
+    raw.ensure_text()
     return text_units(java_lower(units_to_str(raw.text[raw.offsets[i]:raw.offsets[i + 1]])))
 
 
@@ -84,6 +85,7 @@ def featurize_batch_native(raw: RawBatch, num_text_features: int, begin: int, en
     now = raw.batch_time_ms if now_ms is None else int(now_ms)
     mask = filter_mask(raw, begin, end) if apply_filter else np.ones(raw.n, bool)
     rows = np.nonzero(mask)[0].astype(np.int64)
+    raw.ensure_text()   # a replayed batch may carry only its UTF-8 bytes
     indptr, indices = host().featurize_rows(raw.text, raw.offsets, rows, F, hash)
     n = rows.shape[0]
     T = sp.csr_matrix((np.ones(indices.shape[0]), indices, indptr), shape=(n, F))

@@ -77,11 +77,18 @@ def init_distributed(backend: Optional[str] = None, device: Optional[int] = None
     return _INFO
 
 
-def make_rccl_comm(device: int):
-    """Engine-owned RCCL communicator for this process (None when world == 1)."""
+def make_rccl_comm(device: int, force: bool = False):
+    """Engine-owned RCCL communicator for this process (None when world == 1,
+    unless ``force``: a world-1 communicator, so an engine built with
+    ``force_dp`` runs its whole DP path -- every collective -- through RCCL
+    on one GPU)."""
     info = dist_info()
     if info.world <= 1:
-        return None
+        if not force:
+            return None
+        from ..ops._native import hip
+        h = hip()
+        return h.Comm(h.rccl_unique_id(), 0, 1, int(device))
     import torch.distributed as dist
     from ..ops._native import hip
     h = hip()
@@ -90,19 +97,20 @@ def make_rccl_comm(device: int):
     return h.Comm(obj[0], info.rank, info.world, int(device))
 
 
-def make_comm(device: int, kind: str = "rccl", own_group: bool = False):
+def make_comm(device: int, kind: str = "rccl", own_group: bool = False, force: bool = False):
     """Engine communicator: ``rccl`` (device collectives on the engine stream,
     one GPU per rank) or ``gloo`` (host-staged through torch.distributed
     gloo, so N ranks may share one GPU: the real multi-process engine path,
-    testable on a single MI355X).  None when world == 1.  ``own_group``:
+    testable on a single MI355X).  None when world == 1 unless ``force``
+    (a world-1 RCCL communicator for forced-DP engines).  ``own_group``:
     gloo collectives on a process group of their own (a second communicator
     used concurrently with the first, e.g. the engine's prep communicator;
     every RCCL communicator is its own)."""
     info = dist_info()
-    if info.world <= 1:
+    if info.world <= 1 and not (force and kind == "rccl"):
         return None
     if kind == "rccl":
-        return make_rccl_comm(device)
+        return make_rccl_comm(device, force=force)
     if kind != "gloo":
         raise ValueError(f"unknown comm {kind!r}")
     import torch
