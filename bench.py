@@ -297,6 +297,9 @@ def main(argv=None) -> int:
     torch.cuda.set_device(device)
     from twitter_stream_ml_amd.parallel.affinity import bind_local_numa
     numa_cpus = bind_local_numa(device)   # before the pinned pool is allocated
+    from twitter_stream_ml_amd.parallel.affinity import share_host_threads
+    host_threads = share_host_threads(device, info.local_rank,
+                                      int(os.environ.get("LOCAL_WORLD_SIZE", info.world)), n_dev)
     # one communicator: LR DP issues one int64 all-reduce per GD iteration and
     # one all-gather of the next batch's prep packets per batch
     if args.force_dp and (info.world > 1 or args.comm != "rccl"):
@@ -450,6 +453,7 @@ def main(argv=None) -> int:
     out["pool_gen_s"] = round(t_gen, 2)
     out["pool_batches"] = n_pool
     out["numa_bound_cpus"] = len(numa_cpus) if numa_cpus else None
+    out["host_threads"] = host_threads
     if info.is_main:
         line = json.dumps(out)
         print(line, flush=True)

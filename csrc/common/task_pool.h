@@ -3,8 +3,8 @@
 // tens of microseconds per thread on every batch -- visible once the device
 // work per batch is small (the 2-feature k-means stages a 1M-tweet batch in
 // under a millisecond).  Workers are created once, sized to the CPUs this
-// process may run on (sched_getaffinity: the engine binds to the GPU's NUMA
-// node), capped at kMaxWorkers.  run() blocks until every task is done; the
+// process may use (host_threads.h: its share of the GPU's NUMA node), capped
+// at kMaxWorkers.  run() blocks until every task is done; the
 // caller takes tasks too.  Each run is its own Job (task counter, done
 // count), so a worker waking late for a finished run cannot take a task of
 // the next one.
@@ -21,6 +21,8 @@
 #include <mutex>
 #include <thread>
 #include <vector>
+
+#include "host_threads.h"
 
 namespace twtml {
 
@@ -89,11 +91,7 @@ class TaskPool {
   };
 
   TaskPool() {
-    int cpus = 1;
-    cpu_set_t set;
-    CPU_ZERO(&set);
-    if (sched_getaffinity(0, sizeof(set), &set) == 0) cpus = CPU_COUNT(&set);
-    else cpus = int(std::max(1u, std::thread::hardware_concurrency()));
+    const int cpus = host_threads();
     const int n = std::max(0, std::min(kMaxWorkers, cpus) - 1);
     for (int i = 0; i < n; ++i) workers_.emplace_back([this] { loop(); });
   }

@@ -59,6 +59,13 @@ static py::dict result_dict(BatchResult& r) {
   d["train_ms"] = r.train_ms;
   d["comm_iters"] = r.comm_iters;
   d["comm_ms"] = r.comm_ms;
+  if (!r.real.empty()) {
+    auto* v = new std::vector<float>(std::move(r.real));
+    py::capsule own(v, [](void* p) { delete static_cast<std::vector<float>*>(p); });
+    d["real"] = py::array_t<float>({py::ssize_t(v->size())}, {py::ssize_t(sizeof(float))}, v->data(), own);
+  } else {
+    d["real"] = py::none();
+  }
   if (!r.pred.empty()) {
     auto* v = new std::vector<float>(std::move(r.pred));
     py::capsule own(v, [](void* p) { delete static_cast<std::vector<float>*>(p); });
@@ -282,15 +289,15 @@ PYBIND11_MODULE(_twtml_hip, m) {
            py::arg("host_batch"), py::arg("n"), py::arg("bytes"), py::arg("slot"), py::arg("ext_text") = 0,
            py::arg("now_ms") = 0)
       .def("process",
-           [](LREngine& e, int slot, int64_t now_ms, bool want_pred) {
+           [](LREngine& e, int slot, int64_t now_ms, bool want_pred, int64_t plot_points) {
              BatchResult r;
              {
                py::gil_scoped_release nogil;
-               r = e.process(slot, now_ms, want_pred);
+               r = e.process(slot, now_ms, want_pred, plot_points);
              }
              return result_dict(r);
            },
-           py::arg("slot"), py::arg("now_ms"), py::arg("want_pred") = false)
+           py::arg("slot"), py::arg("now_ms"), py::arg("want_pred") = false, py::arg("plot_points") = 0)
       .def_property_readonly("lazy_bytes", &LREngine::lazy_bytes,
                              "device bytes the engine allocates on its first tiered batch (sizing)")
       .def("get_weights", [](const LREngine& e) {

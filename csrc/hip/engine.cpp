@@ -16,6 +16,7 @@
 namespace twtml {
 
 void launch_batch_init(const DevSgd& d, double m_global, int n_loss, hipStream_t s);
+void launch_plot_sample(const float* pred, const float* real, int64_t n, int64_t P, float* out, hipStream_t s);
 
 HostBatch::HostBatch(int64_t rows, int64_t text_bytes) : max_rows(rows), max_bytes(text_bytes) {
   if (rows < 0 || text_bytes < 0) throw std::invalid_argument("HostBatch: negative capacity");
@@ -281,6 +282,8 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
   sgd_.loss_hist = dmalloc<double>(size_t(std::max(1, cfg_.num_iterations)) + 2);
   sgd_.itrec = dmalloc<double>((size_t(std::max(1, cfg_.num_iterations)) + 2) * kRecStride);
   sgd_.pred_out = dmalloc<float>(size_t(cfg_.max_rows));
+  sgd_.real_out = dmalloc<float>(size_t(cfg_.max_rows));
+  plot_buf_ = dmalloc<float>(2 * size_t(cfg_.max_rows));
   sgd_.nrm = dmalloc<double>(2 * kNormParts);
   sgd_.wnorm_next = dmalloc<double>(1);
   sgd_.world = world_;
@@ -501,7 +504,7 @@ LREngine::~LREngine() {
   if (snap_total_) (void)hipHostFree(snap_total_);
   if (snap_stage_) (void)hipHostFree(snap_stage_);
   void* bufs[] = {sgd_.gacc, sgd_.rbuf, sgd_.w64, sgd_.wc64, sgd_.wc32, sgd_.stats, sgd_.state,
-                  sgd_.loss_hist, sgd_.pred_out, sgd_.nrm, sgd_.wnorm_next, sgd_.part, sgd_.itrec, iter_tdbg_,
+                  sgd_.loss_hist, sgd_.pred_out, sgd_.real_out, plot_buf_, sgd_.nrm, sgd_.wnorm_next, sgd_.part, sgd_.itrec, iter_tdbg_,
                   lower_page_, lower_blocks_};
   for (void* b : bufs) if (b) (void)hipFree(b);
   if (host_out_) (void)hipHostFree(host_out_);
@@ -547,6 +550,13 @@ void LREngine::prepare_local(PrepBuf& pb, int slot, int64_t now_ms, hipStream_t 
   const DevRawBatch b = raw_.acquire(slot, s);
   res.n_raw = b.n;
   TWTML_HIP_CHECK(hipEventRecord(pb.ev_start, s));
+  // fault injection (tests): TWTML_INJECT_PREP_FAIL=<rank>:<n> fails this
+  // rank's n-th local prep (1-based)
+  if (const char* f = std::getenv("TWTML_INJECT_PREP_FAIL")) {
+    int fr = -1, fn = 1;
+    if (std::sscanf(f, "%d:%d", &fr, &fn) >= 1 && comm_ && fr == comm_->rank() && ++prep_calls_ == fn)
+      throw std::runtime_error("injected prep failure");
+  }
 
   FeaturizeParams fp{cfg_.num_text_features, cfg_.hash_kind, cfg_.require_retweet,
                      cfg_.range_filter, cfg_.begin, cfg_.end, now_ms};
@@ -649,17 +659,24 @@ void LREngine::issue_c1(PrepBuf& pb, int64_t max_u) {
 // DP, the packets were not gathered during the previous batch (first batch,
 // or the ranks' local parts finished after its GD loop): size the all-gather
 // with an all-reduce of one active-set size per rank, then gather.
-void LREngine::issue_c1_inline(PrepBuf& pb) {
+bool LREngine::issue_c1_inline(PrepBuf* pb) {
   hipStream_t s = compute_;
   const int rank = comm_->rank();
-  for (int r = 0; r < world_; ++r) hnu_[r] = r == rank ? pb.nu_local : 0;
+  // a rank whose local prep failed contributes -1: every rank then skips the
+  // all-gather and raises, instead of the others blocking in it
+  for (int r = 0; r < world_; ++r) hnu_[r] = r == rank ? (pb ? pb->nu_local : int64_t(-1)) : 0;
   TWTML_HIP_CHECK(hipMemcpyAsync(dnu_, hnu_, sizeof(int64_t) * size_t(world_), hipMemcpyHostToDevice, s));
   comm_->allreduce(dnu_, size_t(world_), ncclInt64, ncclSum, s);
   TWTML_HIP_CHECK(hipMemcpyAsync(hnu_, dnu_, sizeof(int64_t) * size_t(world_), hipMemcpyDeviceToHost, s));
   TWTML_HIP_CHECK(hipStreamSynchronize(s));
   int64_t mx = 0;
-  for (int r = 0; r < world_; ++r) mx = std::max(mx, hnu_[r]);
-  issue_c1(pb, mx);
+  bool ok = true;
+  for (int r = 0; r < world_; ++r) {
+    mx = std::max(mx, hnu_[r]);
+    ok = ok && hnu_[r] >= 0;
+  }
+  if (ok && pb) issue_c1(*pb, mx);
+  return ok;
 }
 
 // DP global part, no collectives: per-rank kept rows (global m, sampling
@@ -758,7 +775,7 @@ void LREngine::finish_layout(PrepBuf& pb, hipStream_t s, bool dp_hist) {
 // ---------------------------------------------------------------------------
 // train: GD on a prepared batch, on the compute stream (after its prep).
 // ---------------------------------------------------------------------------
-BatchResult LREngine::train(PrepBuf& pb, bool want_pred) {
+BatchResult LREngine::train(PrepBuf& pb, bool want_pred, int64_t plot_points) {
   TWTML_HIP_CHECK(hipSetDevice(device_));
   hipStream_t s = compute_;
   const int world = world_;
@@ -893,12 +910,26 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred) {
   TWTML_HIP_CHECK(hipMemcpyAsync(host_out_ + 16, sgd_.loss_hist,
                                  sizeof(double) * size_t(cfg_.num_iterations + 1),
                                  hipMemcpyDeviceToHost, s));
-  if (want_pred && res.n_kept > 0) res.pred.resize(size_t(res.n_kept));
-  if (want_pred && res.n_kept > 0)
-    TWTML_HIP_CHECK(hipMemcpyAsync(res.pred.data(), sgd_.pred_out, sizeof(float) * size_t(res.n_kept),
-                                   hipMemcpyDeviceToHost, s));
+  // the plot's (pred, real) pairs of this rank's kept rows: all of them, or
+  // plot_points evenly spaced ones sampled on the device
+  std::vector<float> pairs;
+  if (want_pred && res.n_kept > 0) {
+    const int64_t P = plot_points > 0 ? std::min<int64_t>(plot_points, res.n_kept) : res.n_kept;
+    launch_plot_sample(sgd_.pred_out, sgd_.real_out, res.n_kept, P, plot_buf_, s);
+    pairs.resize(2 * size_t(P));
+    TWTML_HIP_CHECK(hipMemcpyAsync(pairs.data(), plot_buf_, sizeof(float) * pairs.size(), hipMemcpyDeviceToHost, s));
+  }
   TWTML_HIP_CHECK(hipStreamSynchronize(s));
   if (comm_) comm_->check_async();
+  if (!pairs.empty()) {
+    const size_t P = pairs.size() / 2;
+    res.pred.resize(P);
+    res.real.resize(P);
+    for (size_t i = 0; i < P; ++i) {
+      res.pred[i] = pairs[2 * i];
+      res.real[i] = pairs[2 * i + 1];
+    }
+  }
   for (int k = 0; k < 6; ++k) res.stats[k] = host_out_[k];
   const double* st = host_out_ + 8;
   res.converged = st[1] != 0.0;
@@ -971,8 +1002,9 @@ void LREngine::prep_worker() {
         b.c1 = 1;
         __atomic_store_n(ready_host_, b.nu_local + 1, __ATOMIC_RELEASE);
         cv_.notify_all();
-        cv_.wait(lk, [&] { return stop_ || b.c1 == 2; });
+        cv_.wait(lk, [&] { return stop_ || b.c1 == 2 || b.c1 == -2; });
         if (stop_) return;
+        if (b.c1 == -2) throw std::runtime_error("DP: a peer rank failed to prepare this batch");
         lk.unlock();
         prepare_global_dp(b, pstream_);
       } else {
@@ -1010,7 +1042,7 @@ void LREngine::schedule_ahead_locked() {
   cv_.notify_all();
 }
 
-BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
+BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred, int64_t plot_points) {
   TraceRange tr_batch("twtml.lr.batch");
   TWTML_HIP_CHECK(hipSetDevice(device_));
   int k = -1;
@@ -1025,7 +1057,16 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
       cv_.wait(lk, [&] { return pb_[k].c1 != 0 || pb_[k].state == 2; });
       if (pb_[k].c1 == 1) {
         lk.unlock();
-        issue_c1_inline(pb_[k]);
+        const bool ok = issue_c1_inline(&pb_[k]);
+        lk.lock();
+        if (!ok) {   // a peer's prep failed: release the prep thread, raise on every rank
+          pb_[k].c1 = -2;
+          cv_.notify_all();
+        }
+      } else if (pb_[k].c1 == 0 && pb_[k].state == 2 && pb_[k].error) {
+        // this rank's local prep failed before its packet: tell the peers
+        lk.unlock();
+        (void)issue_c1_inline(nullptr);
         lk.lock();
       }
       cv_.wait(lk, [&] { return pb_[k].state == 2; });
@@ -1086,9 +1127,17 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
       pb_[k].now_ms = now_ms;
       lk.unlock();
       try {
-        prepare_local(pb_[k], slot, now_ms, pstream_);
+        bool local_ok = false;
+        try {
+          prepare_local(pb_[k], slot, now_ms, pstream_);
+          local_ok = true;
+        } catch (...) {
+          if (dp_) (void)issue_c1_inline(nullptr);   // the peers raise too instead of waiting
+          throw;
+        }
         if (dp_) {
-          issue_c1_inline(pb_[k]);
+          if (local_ok && !issue_c1_inline(&pb_[k]))
+            throw std::runtime_error("DP: a peer rank failed to prepare this batch");
           prepare_global_dp(pb_[k], pstream_);
         } else {
           prepare_global(pb_[k], pstream_);
@@ -1107,7 +1156,7 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred) {
   }
   BatchResult res;
   try {
-    res = train(pb_[k], want_pred);
+    res = train(pb_[k], want_pred, plot_points);
   } catch (...) {
     std::lock_guard<std::mutex> lk(mu_);
     pb_[k].state = 0;

@@ -135,7 +135,8 @@ struct BatchResult {
   int64_t n_near = 0;     // text slots in the LDS tier
   double stats[6] = {0, 0, 0, 0, 0, 0};  // n, sum y, sum y^2, sum p, sum p^2, sum (y-p)^2
   std::vector<double> loss_history;
-  std::vector<float> pred;
+  std::vector<float> pred;   // want_pred: rounded predictions of this rank's kept rows (or a sample)
+  std::vector<float> real;   // ... and their labels
   float prep_ms = 0.f, train_ms = 0.f;
   int32_t comm_iters = 0;   // DP: gradient all-reduces issued (one per GD iteration)
   float comm_ms = 0.f;      // DP + comm_timing: their summed time on the compute stream
@@ -161,7 +162,8 @@ struct PrepBuf {
   hipEvent_t ev_c1 = nullptr;         // compute stream, after the all-gather
   int64_t nu_local = 0;               // this rank's active ids (packet pairs)
   int64_t c1_maxu = 0;                // pairs per rank in the all-gather
-  int c1 = 0;                         // guarded by mu_: 0 -, 1 packet ready, 2 all-gather issued, -1 failed
+  int c1 = 0;                         // guarded by mu_: 0 -, 1 packet ready, 2 all-gather issued, -1 failed,
+                                      // -2 a peer failed (no all-gather)
   int64_t* host_norm = nullptr;       // pinned [2] rows lowered / narrowed on the device
   double* bounds = nullptr;           // device [kBoundsLen] batch bounds of the fixed-point scales
                                       // (DP: the max over ranks)
@@ -199,7 +201,9 @@ class LREngine {
   // Train on the batch in `slot` (blocks until done); stats use w before
   // training.  The next submitted slot is then prepared ahead (prep thread,
   // prep stream) while this one trains.
-  BatchResult process(int slot, int64_t now_ms, bool want_pred);
+  // plot_points > 0: pred / real hold that many evenly spaced kept rows
+  // (sampled on the device), else all of them.
+  BatchResult process(int slot, int64_t now_ms, bool want_pred, int64_t plot_points = 0);
 
   void set_weights(const double* w, int64_t n);
   void get_weights(double* w, int64_t n) const;
@@ -250,13 +254,15 @@ class LREngine {
   void prepare_global(PrepBuf& b, hipStream_t s);
   // DP: the all-gather of b's packet, on the compute stream (max_u pairs per rank)
   void issue_c1(PrepBuf& b, int64_t max_u);
-  // DP, not issued during the previous batch: size it with an all-reduce first
-  void issue_c1_inline(PrepBuf& b);
+  // DP, not issued during the previous batch: size it with an all-reduce
+  // first, which also carries every rank's prep status (b == null: this
+  // rank's prep failed).  False (no all-gather issued) if any rank failed.
+  bool issue_c1_inline(PrepBuf* b);
   // DP: union, global counts / bounds and layout from the gathered packets
   void prepare_global_dp(PrepBuf& b, hipStream_t s);
   // shared tail of prepare_global / prepare_global_dp: compact space + layout
   void finish_layout(PrepBuf& b, hipStream_t s, bool dp_hist);
-  BatchResult train(PrepBuf& b, bool want_pred);
+  BatchResult train(PrepBuf& b, bool want_pred, int64_t plot_points);
   void prep_worker();
   void schedule_ahead_locked();
   void print_iter_timing(int iters);
@@ -266,6 +272,7 @@ class LREngine {
   LRConfig cfg_;
   std::shared_ptr<Comm> comm_;
   int world_ = 1;
+  float* plot_buf_ = nullptr;       // [2 max_rows] sampled (pred, real) pairs
   bool dp_ = false;                 // DP path: world > 1, or forced with a world-1 communicator
   bool comm_timing_ = false;
   std::vector<hipEvent_t> comm_ev_; // comm_timing: [2 iters] around each gradient all-reduce
@@ -300,6 +307,7 @@ class LREngine {
   bool diverged_ = false;
   int64_t near_cap_ = 0;          // tiered layout: LDS-resident text slots (tier_near_cap)
   bool force_tiered_ = false;     // TWTML_FORCE_TIERED=1: tiered layout for any active set (tests)
+  int prep_calls_ = 0;            // local preps so far (TWTML_INJECT_PREP_FAIL, tests)
   uint64_t* iter_tdbg_ = nullptr;
   uint8_t* lower_page_ = nullptr;
   uint16_t* lower_blocks_ = nullptr;

@@ -262,6 +262,7 @@ struct DevSgd {
   double* state;        // [kStateLen] see below
   double* loss_hist;    // [max_iters+1]
   float* pred_out;      // [R] rounded predictions in kept order (optional)
+  float* real_out;      // [R] labels in kept order, written with pred_out (the plot's real series)
   double* host_flags;   // [max_iters+1] pinned host memory: done flag after each update
   int64_t* part;        // [nparts][pstride] per-workgroup int64 partial rows
   double* itrec;        // [max_iters+2][kRecStride] per-iteration scale / update records

@@ -319,7 +319,10 @@ __device__ __forceinline__ float row_residual(int32_t dot_fix, const RowIn& ri, 
   if (t == 0) {
     if (STATS && valid) {
       const double pr = round_half_away(double(dot));
-      if (sp.want_pred) d.pred_out[p.perm[pos]] = float(pr);
+      if (sp.want_pred) {
+        d.pred_out[p.perm[pos]] = float(pr);
+        d.real_out[p.perm[pos]] = ri.y;
+      }
       const double yd = double(ri.y), e = yd - pr;
       acc.st[0] += 1.0; acc.st[1] += yd; acc.st[2] += yd * yd;
       acc.st[3] += pr; acc.st[4] += pr * pr; acc.st[5] += e * e;
@@ -1520,6 +1523,25 @@ void launch_batch_bounds(const DevPrepared& p, double* out, hipStream_t s) {
   TWTML_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(double) * kBoundsLen, s));
   const int grid = int(std::max<int64_t>(1, std::min<int64_t>((p.cap_rows + kBlock - 1) / kBlock, 256)));
   hipLaunchKernelGGL(k_batch_bounds, dim3(grid), dim3(kBlock), 0, s, p, out);
+}
+
+// ---------------------------------------------------------------------------
+// Plot sample (output op #1's real / pred collect, LinearRegression.scala:77):
+// P evenly spaced kept rows, out[2i] = pred, out[2i + 1] = real, so only P
+// pairs cross PCIe when the Lightning plot is on.
+// ---------------------------------------------------------------------------
+__global__ void k_plot_sample(const float* pred, const float* real, int64_t n, int64_t P, float* out) {
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < P; i += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t r = P > 1 ? (i * (n - 1)) / (P - 1) : 0;
+    out[2 * i] = pred[r];
+    out[2 * i + 1] = real[r];
+  }
+}
+
+void launch_plot_sample(const float* pred, const float* real, int64_t n, int64_t P, float* out, hipStream_t s) {
+  if (P <= 0 || n <= 0) return;
+  const int grid = int(std::min<int64_t>(64, (P + 255) / 256));
+  hipLaunchKernelGGL(k_plot_sample, dim3(grid), dim3(256), 0, s, pred, real, n, P, out);
 }
 
 }  // namespace twtml

@@ -4,6 +4,7 @@
 // kept row, lower-case (unicode_lower), take text.sliding(2) over UTF-16
 // units and hash each term (Java String.hashCode or Spark-2 murmur3), mod F.
 // Duplicates are kept; the Python side sums them into CSR counts.
+#include "../common/host_threads.h"
 #include "featurize_cpu.h"
 
 #include <algorithm>
@@ -84,7 +85,7 @@ void featurize_rows_cpu(const uint16_t* text, const int64_t* offsets, const int6
                         size_t nrows, int64_t F, int hash_kind, std::vector<int64_t>& indptr,
                         std::vector<int64_t>& indices, int nthreads) {
   indptr.assign(nrows + 1, 0);
-  int T = nthreads > 0 ? nthreads : int(std::thread::hardware_concurrency());
+  int T = nthreads > 0 ? nthreads : host_threads();
   T = std::max(1, std::min<int>(T, int((nrows + 1023) / 1024)));
   std::vector<std::vector<int64_t>> part(T);
   std::vector<size_t> r0(T + 1);

@@ -1,4 +1,5 @@
 // Deterministic synthetic tweet stream; see synth.h.
+#include "../common/host_threads.h"
 #include "synth.h"
 
 #include <algorithm>
@@ -482,7 +483,7 @@ int64_t synth_generate(const SynthParams& p, uint64_t start, size_t n, uint16_t*
   (void)vocab();  // initialise statics before threads start
   if (p.vocab == 1) (void)wide_vocab(p.vocab_size);
   if (n == 0) { offsets[0] = 0; return 0; }
-  int T = nthreads > 0 ? nthreads : int(std::thread::hardware_concurrency());
+  int T = nthreads > 0 ? nthreads : host_threads();
   T = std::max(1, std::min<int>(T, int((n + 4095) / 4096)));
   std::vector<std::vector<uint16_t>> bufs(T);
   std::vector<size_t> row0(T + 1);

@@ -1,3 +1,4 @@
+#include "../common/host_threads.h"
 #include "wire.h"
 
 #include <algorithm>
@@ -30,7 +31,7 @@ uint8_t row_kind(const uint16_t* t, int64_t len, int64_t* bytes) {
 
 template <typename F>
 void parallel_chunks(int64_t n, int threads, F&& fn) {
-  if (threads <= 0) threads = int(std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency())));
+  if (threads <= 0) threads = std::min(16, host_threads());
   const int64_t min_rows = 16384;
   int T = int(std::min<int64_t>(std::min(threads, 64), (n + min_rows - 1) / min_rows));
   if (T < 1) T = 1;

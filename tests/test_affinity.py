@@ -1,6 +1,8 @@
 """NUMA-local binding of a GPU rank (parallel/affinity.py) against a fake sysfs."""
 import os
 
+import numpy as np
+
 from twitter_stream_ml_amd.parallel.affinity import bind_local_numa, gpu_numa_node, parse_cpulist
 
 
@@ -55,3 +57,32 @@ def test_real_process_affinity_untouched_without_gpu():
     before = os.sched_getaffinity(0)
     bind_local_numa(0, pci_bus_id=lambda d: "ffff:ff:ff.f")   # nonexistent device path
     assert os.sched_getaffinity(0) == before
+
+
+def test_share_host_threads_divides_the_node(monkeypatch):
+    """8 ranks on 2 NUMA nodes (4 GPUs each): a rank gets its node's CPUs / 4."""
+    from twitter_stream_ml_amd.parallel.affinity import share_host_threads
+    monkeypatch.delenv("TWTML_HOST_THREADS", raising=False)
+    nodes = {d: 0 if d < 4 else 1 for d in range(8)}
+    monkeypatch.setattr("twitter_stream_ml_amd.parallel.affinity.gpu_numa_node",
+                        lambda bdf, sysfs: nodes[int(bdf)])
+    n = share_host_threads(5, 5, 8, 8, pci_bus_id=str, getaffinity=lambda pid: set(range(64)))
+    assert n == 16 and os.environ["TWTML_HOST_THREADS"] == "16"
+    # every rank on one GPU (the gloo rehearsal): the 8 ranks share the node
+    monkeypatch.delenv("TWTML_HOST_THREADS")
+    assert share_host_threads(0, 3, 8, 1, pci_bus_id=str, getaffinity=lambda pid: set(range(64))) == 8
+    # an explicit setting wins
+    assert share_host_threads(0, 3, 8, 1, pci_bus_id=str, getaffinity=lambda pid: set(range(64))) == 8
+    monkeypatch.setenv("TWTML_HOST_THREADS", "3")
+    assert share_host_threads(0, 0, 8, 8, pci_bus_id=str, getaffinity=lambda pid: set(range(64))) == 3
+
+
+def test_native_generator_uses_host_threads(monkeypatch):
+    """The synthetic generator honours TWTML_HOST_THREADS (sized from the
+    affinity mask otherwise, never the machine's CPU count)."""
+    from twitter_stream_ml_amd.sources.synthetic import SynthConfig, generate_batch
+    monkeypatch.setenv("TWTML_HOST_THREADS", "1")
+    a = generate_batch(SynthConfig.profile("bench", seed=3), 0, 20000, batch_time_ms=0)
+    monkeypatch.setenv("TWTML_HOST_THREADS", "5")
+    b = generate_batch(SynthConfig.profile("bench", seed=3), 0, 20000, batch_time_ms=0)
+    np.testing.assert_array_equal(a.text, b.text)   # thread count never changes the data

@@ -104,3 +104,37 @@ def test_allreduce_fn_bit_identical_in_rank_order(tmp_path, world):
         ref += x
     for o in outs:
         np.testing.assert_array_equal(o, ref)
+
+
+def _plot_worker(rank, world, port, lgn_url, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      TWTML_METRICS=os.path.join(out_dir, f"m{rank}.jsonl"))
+    from twitter_stream_ml_amd.apps import linear_regression as app
+    rc = app.main(["--master", "local[1]", "--lightning", lgn_url, "--twtweb", "http://127.0.0.1:9",
+                   "--seconds", "0", "--batchSize", "1200", "--sourceRate", "0", "--numBatches", "3",
+                   "-f", "1000", "--plotPoints", "50"])
+    assert rc == 0
+
+
+def test_dp_driver_plot_samples_reach_rank0(tmp_path):
+    """2 gloo ranks run the LR driver with a (fake) Lightning plot: each rank
+    samples plotPoints / world (pred, real) pairs, the plot shipper threads
+    gather them to rank 0 over their own gloo group, and rank 0's session
+    appends one 4-series update per batch with every rank's points."""
+    import json
+    from fakes import FakeLightning
+    lgn = FakeLightning().start()
+    try:
+        mp.start_processes(_plot_worker, args=(2, _free_port(), lgn.url, str(tmp_path)), nprocs=2,
+                           join=True, start_method="spawn")
+        appends = lgn.appends()
+    finally:
+        lgn.stop()
+    assert len(appends) == 3
+    for a in appends:
+        series = a["data"]["series"]
+        assert len(series) == 4 and len(series[0]) == len(series[1]) == 50   # 25 per rank
+        assert all(100 <= v <= 1000 for v in series[0])                      # real: kept retweet counts
+    recs = [json.loads(l) for l in open(tmp_path / "m0.jsonl") if '"summary"' not in l]
+    assert len(recs) == 3 and all("step_ms" in r for r in recs)

@@ -103,3 +103,35 @@ def test_lr_driver_divergence_reported(hip_module, tmp_path, monkeypatch, caplog
     assert all("mse" not in r for r in batches[1:]), batches
     assert summ and summ[0]["diverged_batches"] == 4
     assert any("diverged" in m for m in caplog.messages), caplog.messages
+
+
+def test_lr_driver_plot_does_not_stall_training(hip_module, tmp_path, monkeypatch):
+    """with a live Lightning plot at 1M tweets per batch the
+    training thread only enqueues a device-sampled series (plotPoints pairs,
+    ``k_plot_sample``); the gather and the HTTP run on the plot shipper /
+    session threads.  Per-batch p99 (train + report on the training thread)
+    stays within 5 % of the plot-off run on the same data."""
+    import json
+    from fakes import FakeLightning
+    from twitter_stream_ml_amd.apps import linear_regression as app
+    base = ["--master", "rocm[1]", "--twtweb", "http://127.0.0.1:9", "--source", "replay:synthetic:wide:4",
+            "--seconds", "0", "--batchSize", "1000000", "--sourceRate", "0", "--numBatches", "40",
+            "-f", "1000000"]
+
+    def p99(path, lightning):
+        monkeypatch.setenv("TWTML_METRICS", str(path))
+        assert app.main(base + ["--lightning", lightning]) == 0
+        steps = [r["step_ms"] for r in (json.loads(l) for l in open(path)) if "step_ms" in r]
+        assert len(steps) == 40
+        return float(np.percentile(steps[8:], 99))   # after warm-up
+
+    off = p99(tmp_path / "off.jsonl", "http://127.0.0.1:9")   # unreachable: plotting disabled
+    lgn = FakeLightning().start()
+    try:
+        on = p99(tmp_path / "on.jsonl", lgn.url)
+        appends = lgn.appends()
+    finally:
+        lgn.stop()
+    assert len(appends) >= 30 and len(appends[-1]["data"]["series"][0]) == 10000
+    print(f"step p99: plot off {off:.3f} ms, plot on {on:.3f} ms")
+    assert on <= 1.05 * off + 0.05, (on, off)

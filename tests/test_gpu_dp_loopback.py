@@ -99,3 +99,44 @@ def test_dp_rank_with_no_rows(hip_module):
     r1 = single.train_batch(full)
     assert res[0][0]["iterations"] == r1["iterations"]
     np.testing.assert_array_equal(engines[1].get_weights(), single.get_weights())
+
+
+@pytest.mark.parametrize("ahead", [True, False], ids=["ahead", "inline"])
+def test_dp_prep_failure_raises_on_every_rank(hip_module, monkeypatch, ahead):
+    """a rank whose local prep fails must not leave its peers
+    blocked in the packet all-gather -- the in-line all-reduce carries every
+    rank's prep status, so all ranks raise for that batch."""
+    from twitter_stream_ml_amd.ops._native import hip
+    from twitter_stream_ml_amd.ops.lr_engine import DeviceLinearRegression
+    # rank 1's second local prep fails: prepared ahead by its prep thread
+    # while batch 0 trains, or in line
+    monkeypatch.setenv("TWTML_INJECT_PREP_FAIL", "1:2")
+    cfg = _cfg(1000, num_iterations=5)
+    group = hip().LoopbackGroup(2)
+    engines = [DeviceLinearRegression(cfg, device=0, comm=group.comm(r)) for r in range(2)]
+    synth = SynthConfig.profile("twitter", seed=4)
+    batches = [generate_batch(synth, t * 2000, 2000, batch_time_ms=NOW + t) for t in range(2)]
+    errors = [None, None]
+    done = [0, 0]
+
+    def worker(r):
+        shards = [b.shard(r, 2) for b in batches]
+        try:
+            if ahead:
+                for sh in shards:
+                    engines[r].prefetch(sh)
+            for sh in shards:
+                engines[r].train_batch(sh, want_pred=False)
+                done[r] += 1
+        except Exception as e:  # noqa: BLE001 -- checked below
+            errors[r] = e
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(2)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=120)
+    assert not any(x.is_alive() for x in th), "a rank is still blocked in a collective"
+    assert done == [1, 1], done
+    assert "injected" in str(errors[1]), errors
+    assert errors[0] is not None and "peer" in str(errors[0]), errors

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import argparse
 import logging
+import os
 import sys
 from typing import List, Optional
 
@@ -71,6 +72,10 @@ def build_kmeans_engine(args, dim: int, rank: int, world: int):
         dev = spec.devices[rank] if spec.devices else rank
         from ..parallel.affinity import bind_local_numa
         bind_local_numa(dev)   # pinned staging buffers on the GPU's NUMA node
+        from ..parallel.affinity import share_host_threads
+        import torch
+        share_host_threads(dev, rank, int(os.environ.get("LOCAL_WORLD_SIZE", world)),
+                           max(1, torch.cuda.device_count()))
         rows = max(65536, args.batchSize)
         cfg = KMDeviceConfig(k=args.k, text_dims=args.textDims, half_life=args.halfLife,
                              max_rows=rows, max_units=rows * 290, seed=args.seed)

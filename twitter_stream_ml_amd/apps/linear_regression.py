@@ -39,13 +39,12 @@ from ..config.arguments import ConfArguments
 from ..config.hocon import load_java_opts
 from ..models.linear_regression import CpuLinearRegression, CpuLRConfig, LinearRegressionModel
 from ..models.mllib_helper import MllibHelper
-from ..parallel.dist import barrier, broadcast_flag, check_replicas, gather_to_main
+from ..parallel.dist import barrier, broadcast_flag, check_replicas
 from ..utils.faults import maybe_inject
 from ..checkpoint.saveable import SparseWeights
 from ._common import (ResumeState, StreamCheckpointer, exit_on_sigterm, load_resume_state,
                       make_watchdog)
 from ..oracle.mllib import round_half_up
-from ..records.batch import RETWEET_COUNT
 from ..report.session_stats import SessionStats
 from ..runtime.streaming import StreamingContext
 from ..sources import make_source
@@ -69,6 +68,10 @@ def build_engine(conf: ConfArguments, rank: int, world: int, device: Optional[in
         dev = device if device is not None else (spec.devices[rank] if spec.devices else rank)
         from ..parallel.affinity import bind_local_numa
         bind_local_numa(dev)   # pinned staging buffers on the GPU's NUMA node
+        from ..parallel.affinity import share_host_threads
+        import torch
+        share_host_threads(dev, rank, int(os.environ.get("LOCAL_WORLD_SIZE", world)),
+                           max(1, torch.cuda.device_count()))
         def lr_cfg(rows: int) -> LRDeviceConfig:
             # ingest "utf8": the receiver's UTF-8 bytes cross PCIe as they are
             # (DMA'd from its page-locked buffer when the source pins them) and
@@ -124,9 +127,19 @@ class LinearRegressionJob:
         self.records = resume.records  # source records this rank consumed
         self.metrics = metrics or MetricsLogger(None)
         self.last = None
+        self._t0 = 0.0
         self.diverged = 0    # batches on which the model was found diverged (training stopped)
         self.checkpointer = StreamCheckpointer(conf.checkpoint, conf.checkpointInterval, rank,
                                                self._snapshot, barrier)
+        # plot samples per rank: the device samples them (0 = every kept row),
+        # the shipper thread gathers them to rank 0 and hands them to the
+        # session worker -- nothing of the plot runs on the training thread
+        pp = int(getattr(conf, "plotPoints", 0) or 0)
+        self.plot_points = 0 if pp <= 0 else max(1, -(-pp // max(1, world)))
+        self.shipper = None
+        if self.plot:
+            from ..report.plot_shipper import PlotShipper
+            self.shipper = PlotShipper(session if rank == 0 else None, rank, world)
         self.watchdog = make_watchdog(conf.batchTimeout, getattr(engine, "comm", None))
 
     def on_batch(self, rdd, time_ms: int) -> None:
@@ -134,8 +147,8 @@ class LinearRegressionJob:
         maybe_inject(self.rank, self.batches + 1)
         if self.watchdog is not None:
             self.watchdog.arm()
-        t0 = time.perf_counter()
-        res = self.engine.train_batch(raw, want_pred=self.plot)     # op #1 then op #2
+        t0 = self._t0 = time.perf_counter()
+        res = self.engine.train_batch(raw, want_pred=self.plot, plot_points=self.plot_points)  # op #1, op #2
         t1 = time.perf_counter()
         if self.t_first is None:
             self.t_first = t0
@@ -182,34 +195,31 @@ class LinearRegressionJob:
             log.error("batch %d: model diverged (%s); skipping report", self.batches, e)
             self.metrics.log(batch_time_ms=time_ms, raw=raw.n, batch=batch, diverged=True)
             return
-        real = pred = real_all = pred_all = np.zeros(0)
+        real = pred = np.zeros(0)
         if self.plot:
-            mask = self._kept_mask(raw)
-            real = raw.scalars[RETWEET_COUNT][mask].astype(np.float64)
-            pred = np.asarray(res["pred"], np.float64) if res.get("pred") is not None else np.zeros(0)
-            real_all, pred_all = real, pred
-            if self.world > 1:
-                # CS7: real.toArray / pred.toArray are collected to the driver;
-                # with --plotPoints each rank ships only its share of the sample
-                if self.conf.plotPoints > 0:
-                    k = max(1, self.conf.plotPoints // self.world)
-                    if real.shape[0] > k:
-                        idx = np.linspace(0, real.shape[0] - 1, k).astype(np.int64)
-                        real, pred = real[idx], pred[idx]
-                real_all, pred_all = gather_to_main(real), gather_to_main(pred)
+            # CS7 real.toArray / pred.toArray: this rank's sampled kept rows,
+            # labels and predictions straight from the engine (no host mask)
+            if res.get("real") is not None:
+                real = np.asarray(res["real"], np.float64)
+                pred = np.asarray(res["pred"], np.float64)
         if log.isEnabledFor(logging.DEBUG):
             log.debug("count: %d", self.count)
             log.debug("batch: %d,  mse: %d", batch, int(mse))
             log.debug("stdev (real, pred): (%d, %d)", int(real_sd), int(pred_sd))
             log.debug("value (real, pred): %s ...",
                       [(float(a), float(b)) for a, b in zip(real[:10], pred[:10])])
+        stats = (self.count, batch, mse, real_sd, pred_sd)
+        if self.shipper is not None:   # every rank: its sample goes to rank 0 off this thread
+            self.shipper.submit(stats, real, pred)
+        elif self.session is not None and self.rank == 0:
+            self.session.update(*stats, real, pred)
+        # step_ms: the batch on the training thread, train + report (the plot included)
         self.metrics.log(batch_time_ms=time_ms, raw=raw.n, batch=batch, count=self.count,
                          mse=mse, realStdev=real_sd, predStdev=pred_sd,
                          iterations=res["iterations"], converged=bool(res["converged"]),
                          diverged=bool(res.get("diverged", False)),
-                         prep_ms=res.get("prep_ms", 0.0), train_ms=res.get("train_ms", 0.0))
-        if self.session is not None and self.rank == 0:
-            self.session.update(self.count, batch, mse, real_sd, pred_sd, real_all, pred_all)
+                         prep_ms=res.get("prep_ms", 0.0), train_ms=res.get("train_ms", 0.0),
+                         step_ms=round((time.perf_counter() - self._t0) * 1e3, 3))
 
     def summary(self) -> dict:
         """Throughput of the run: trained tweets (all ranks) over the wall
@@ -247,15 +257,13 @@ class LinearRegressionJob:
         w = np.array(eng.get_weights(), dtype=np.float64, copy=True)
         return lambda path, prog: LinearRegressionModel(w, 0.0).save(path, prog)
 
-    def _kept_mask(self, raw):
-        rc = raw.scalars[RETWEET_COUNT]
-        return (raw.is_retweet != 0) & (rc >= self.conf.numRetweetBegin) & (rc <= self.conf.numRetweetEnd)
-
     def final_checkpoint(self) -> None:
         self.checkpointer.flush()
         self.checkpointer.after_batch(self.batches, self.records, self.count, force=True)
 
     def close(self) -> None:
+        if self.shipper is not None:
+            self.shipper.close()
         try:
             self.checkpointer.flush()   # never leave a checkpoint half-written behind
         except Exception as e:

@@ -146,7 +146,8 @@ class CpuLinearRegression:
             raise ValueError(f"expected {self.w.shape[0]} weights, got {w.shape}")
         self.w = w.copy()
 
-    def train_batch(self, raw: RawBatch, want_pred: bool = True, slot: int = 0) -> Dict[str, object]:
+    def train_batch(self, raw: RawBatch, want_pred: bool = True, plot_points: int = 0,
+                    slot: int = 0) -> Dict[str, object]:
         c = self.cfg
         X, y, rows = featurize_columnar(raw, c.num_text_features, c.begin, c.end, hash=c.hash)
         red = self.allreduce
@@ -164,9 +165,13 @@ class CpuLinearRegression:
         res: Dict[str, object] = {"n_raw": raw.n, "n_kept": int(y.shape[0]),
                                   "n_kept_global": n_glob, "iterations": 0, "converged": False,
                                   "loss_history": [], "stats": stats.tolist(),
-                                  "pred": pred.astype(np.float32) if want_pred else None,
+                                  "pred": None, "real": None,
                                   "n_unique": int(np.unique(X.indices).shape[0]) if X.nnz else 0,
                                   "prep_ms": 0.0, "train_ms": 0.0, "diverged": False}
+        if want_pred:   # the plot's series: all kept rows, or plot_points evenly spaced ones
+            P = y.shape[0] if plot_points <= 0 else min(int(plot_points), y.shape[0])
+            idx = (np.arange(P, dtype=np.int64) * max(y.shape[0] - 1, 0)) // max(P - 1, 1)
+            res["pred"], res["real"] = pred[idx].astype(np.float32), y[idx].astype(np.float32)
         if n_glob == 0:
             return res
         r = run_minibatch_sgd(X, y, self.w, c.step_size, c.num_iterations, c.fraction, c.tol,

@@ -295,16 +295,19 @@ class DeviceLinearRegression:
     def submit(self, hb: HostBatchView, slot: int) -> None:
         self._eng.submit(hb._hb, int(hb.n), int(hb.bytes), int(slot), int(hb.ext_text), int(hb.batch_time_ms))
 
-    def process(self, slot: int, now_ms: int, want_pred: bool = False) -> Dict[str, object]:
-        return self._eng.process(int(slot), int(now_ms), bool(want_pred))
+    def process(self, slot: int, now_ms: int, want_pred: bool = False, plot_points: int = 0) -> Dict[str, object]:
+        """``want_pred``: ``pred`` / ``real`` hold this rank's kept rows'
+        rounded predictions and labels (kept order) -- all of them, or
+        ``plot_points`` evenly spaced ones sampled on the device."""
+        return self._eng.process(int(slot), int(now_ms), bool(want_pred), int(plot_points))
 
     def prefetch(self, raw: RawBatch) -> bool:
         """Stage + async H2D of a queued future batch (overlaps the current one)."""
         return self._pipe.prefetch(raw)
 
-    def train_batch(self, raw: RawBatch, want_pred: bool = True) -> Dict[str, object]:
+    def train_batch(self, raw: RawBatch, want_pred: bool = True, plot_points: int = 0) -> Dict[str, object]:
         """Train on one micro-batch: uses its prefetched slot, else stages + H2D now."""
-        return self.process(self._pipe.take(raw), raw.batch_time_ms, want_pred)
+        return self.process(self._pipe.take(raw), raw.batch_time_ms, want_pred, plot_points)
 
     def synchronize(self) -> None:
         self._eng.synchronize()

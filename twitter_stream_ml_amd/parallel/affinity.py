@@ -18,7 +18,7 @@ from __future__ import annotations
 import os
 from typing import Callable, Optional, Set
 
-__all__ = ["parse_cpulist", "gpu_numa_node", "bind_local_numa"]
+__all__ = ["parse_cpulist", "gpu_numa_node", "bind_local_numa", "share_host_threads"]
 
 SYSFS = "/sys"
 
@@ -84,3 +84,40 @@ def bind_local_numa(device: int, pci_bus_id: Optional[Callable[[int], str]] = No
         return None
     setaffinity(0, cpus)
     return cpus
+
+
+def share_host_threads(device: int, local_rank: int, local_world: int, n_devices: int,
+                       pci_bus_id: Optional[Callable[[int], str]] = None, sysfs: str = SYSFS,
+                       getaffinity: Callable[[int], Set[int]] = os.sched_getaffinity) -> int:
+    """Host worker threads for this rank: the CPUs it may run on divided by
+    the local ranks that share them, exported as ``TWTML_HOST_THREADS`` for
+    the native runtime (``csrc/common/host_threads.h``: the synthetic
+    generator, the CPU featurizer, the wire packer and the staging pool).
+    Local rank r drives device ``r % n_devices``; ranks whose devices sit on
+    the same NUMA node as ours share its CPUs (all local ranks share them when
+    the node is unknown).  An explicit ``TWTML_HOST_THREADS`` wins."""
+    if os.environ.get("TWTML_HOST_THREADS"):
+        return int(os.environ["TWTML_HOST_THREADS"])
+    cpus = len(getaffinity(0))
+    n_dev = max(1, int(n_devices))
+    sharing = max(1, int(local_world))
+    if pci_bus_id is None:
+        try:
+            from ..ops._native import hip
+            pci_bus_id = hip().pci_bus_id
+        except Exception:   # noqa: BLE001 -- no runtime: every local rank shares
+            pci_bus_id = None
+    if pci_bus_id is not None and local_world > 1:
+        def node(d: int):
+            try:
+                return gpu_numa_node(pci_bus_id(d), sysfs)
+            except Exception:   # noqa: BLE001
+                return None
+        mine = node(int(device))
+        if mine is not None:
+            nodes = [node(r % n_dev) for r in range(int(local_world))]
+            if all(x is not None for x in nodes):
+                sharing = max(1, sum(1 for x in nodes if x == mine))
+    n = max(1, cpus // sharing)
+    os.environ["TWTML_HOST_THREADS"] = str(n)
+    return n

@@ -238,28 +238,29 @@ def broadcast_flag(flag: bool) -> bool:
     return _reduce_scalar(v, "max") > 0.5
 
 
-def gather_to_main(arr: np.ndarray) -> Optional[np.ndarray]:
+def gather_to_main(arr: np.ndarray, group=None) -> Optional[np.ndarray]:
     """Concatenate every rank's 1-D float64 array on rank 0 (None elsewhere).
 
     CS7/CS11: the reference ``collect``s the batch's real/predicted values to
-    the driver for the Lightning plot; here each rank's shard is gathered
-    once per batch, off the training path."""
+    the driver for the Lightning plot; here each rank's sample is gathered
+    once per batch by the plot shipper thread (``report/plot_shipper.py``) on
+    a gloo ``group`` of its own, off the training path."""
     info = dist_info()
     a = np.ascontiguousarray(arr, dtype=np.float64).reshape(-1)
     if info.world <= 1:
         return a
     import torch
     import torch.distributed as dist
-    dev = "cuda" if info.backend == "nccl" else "cpu"
+    dev = "cuda" if (info.backend == "nccl" and group is None) else "cpu"
     n = torch.tensor([a.shape[0]], dtype=torch.int64, device=dev)
     sizes = [torch.zeros_like(n) for _ in range(info.world)]
-    dist.all_gather(sizes, n)
+    dist.all_gather(sizes, n, group=group)
     sizes = [int(s.item()) for s in sizes]
     m = max(sizes) if sizes else 0
     buf = torch.zeros(max(m, 1), dtype=torch.float64, device=dev)
     buf[:a.shape[0]] = torch.from_numpy(a).to(dev)
     parts = [torch.zeros_like(buf) for _ in range(info.world)]
-    dist.all_gather(parts, buf)   # all_gather: supported by gloo and RCCL alike
+    dist.all_gather(parts, buf, group=group)   # all_gather: supported by gloo and RCCL alike
     if info.rank != 0:
         return None
     return np.concatenate([p[:s].cpu().numpy() for p, s in zip(parts, sizes)])

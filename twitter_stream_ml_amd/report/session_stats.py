@@ -15,7 +15,8 @@ drops errors with ``Try``); when the queue is full the oldest update is
 dropped.  A Lightning server that is down at ``open()`` is logged instead of
 aborting the job unless ``strict=True`` (the reference's behaviour).
 ``plot_points`` caps the points appended per batch (0 = all, as the
-reference; useful at millions of tweets per batch).
+reference; the default of ``plotPoints`` is 10000, since a micro-batch here
+holds millions of tweets).
 """
 from __future__ import annotations
 
@@ -85,11 +86,14 @@ class SessionStats:
     def update(self, count: int, batch: int, mse: float, realStdev: float, predStdev: float,
                real: Sequence[float], pred: Sequence[float]) -> None:
         stats = (int(count), int(batch), int(mse), int(realStdev), int(predStdev))
-        series = self._series(int(batch), float(realStdev), float(predStdev), real, pred)
+        real = np.array(real, dtype=np.float64)   # a copy: the caller may reuse its buffers
+        pred = np.array(pred, dtype=np.float64)
 
         def push() -> None:
             self._try(lambda: self.web.stats(*stats))
             if self.viz is not None:
+                # the JSON series are built here, on the worker, not on the caller's thread
+                series = self._series(stats[1], float(realStdev), float(predStdev), real, pred)
                 self._try(lambda: self.lgn.line_streaming(series=series, viz=self.viz))
 
         if not self._async:
