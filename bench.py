@@ -49,6 +49,7 @@ import time
 
 import numpy as np
 
+T_START = time.time()
 BASELINE_TWEETS_PER_SEC = None  # the reference publishes no number
 
 
@@ -331,8 +332,10 @@ def main(argv=None) -> int:
     else:
         eng = DeviceLinearRegression(lr_config(args, B, max_units, ingest), device=device, comm=comm)
     u8s = []
+    pinned = 0   # bytes of page-locked host memory this rank holds (staging views + registered pool)
     if args.e2e:
         views = [HostBatchView(B, max_units) for _ in range(eng.raw_slots)]
+        pinned += sum(int(v._hb.bytes) for v in views)
         if is_km:
             for v in views:
                 v._hb.scalar_cols = 2   # k-means reads retweetCount and followersCount only
@@ -343,6 +346,7 @@ def main(argv=None) -> int:
             u8s = [encode_utf8(r) for r in pool_raw]
             for u in u8s:
                 register_host(u.data)
+                pinned += int(u.data.nbytes)
             # the UTF-16 copy is not staged in this mode: drop it (the batch
             # carries the receiver's UTF-8 buffer instead)
             pool_raw = [RawBatch(np.zeros(0, np.uint16), r.offsets, r.is_retweet, r.scalars, r.batch_time_ms,
@@ -350,6 +354,7 @@ def main(argv=None) -> int:
         elif ingest == "utf16":
             for r in pool_raw:   # the receiver's buffers: DMA source of the text
                 register_host(r.text)
+                pinned += int(r.text.nbytes)
     else:
         pool = []
         for r in pool_raw:
@@ -385,6 +390,9 @@ def main(argv=None) -> int:
     mine = float(sum(runner.kept)) / max(t1 - t0, 1e-12)   # this rank's own tweets/s over its window
     per_rank = D.gather_to_main(np.array([mine]))
     prestaged = int(D.allreduce_max_scalar(float(runner.prestaged_at_t0)))
+    import resource
+    rss_mb = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024.0
+    host = D.gather_to_main(np.array([rss_mb, pinned / 2**20, t_gen]))   # per rank, to rank 0
     stage = runner.stage
     par = f"dp{info.world}" + ("-gloo" if args.comm == "gloo" else "") + ("-forced" if args.force_dp else "")
     data = ("synthetic tweet-shaped records (seeded C++ generator, "
@@ -450,6 +458,11 @@ def main(argv=None) -> int:
         out["grad_allreduce_per_step"] = round(n_ar / len(runner.comm), 2)
         if args.force_dp:
             out["grad_allreduce_us_per_iter"] = round(1e3 * sum(c[1] for c in runner.comm) / n_ar, 2)
+    if host is not None:   # the host budget of every rank (8-rank rehearsal, README)
+        h = np.asarray(host).reshape(-1, 3)
+        out["per_rank_host"] = [{"peak_rss_mb": round(float(a), 1), "pinned_mb": round(float(b), 1),
+                                 "pool_gen_s": round(float(c), 2)} for a, b, c in h]
+    out["wall_s"] = round(time.time() - T_START, 1)
     out["pool_gen_s"] = round(t_gen, 2)
     out["pool_batches"] = n_pool
     out["numa_bound_cpus"] = len(numa_cpus) if numa_cpus else None

@@ -188,6 +188,7 @@ PYBIND11_MODULE(_twtml_hip, m) {
       .def(py::init<int64_t, int64_t>(), py::arg("max_rows"), py::arg("max_bytes"))
       .def_readonly("max_rows", &HostBatch::max_rows)
       .def_readonly("max_bytes", &HostBatch::max_bytes)
+      .def_readonly("bytes", &HostBatch::bytes)   // page-locked bytes of the staging buffer
       .def_property_readonly("text", [](py::object self) {
         auto& h = self.cast<HostBatch&>();
         return view<uint8_t>(h.text, {py::ssize_t(h.max_bytes)}, self);

@@ -396,3 +396,40 @@ def test_utf8_truncated_sequences_stay_in_their_row(hip_module):
         s, e = Xt.indptr[k], Xt.indptr[k + 1]
         want = np.repeat(Xt.indices[s:e], Xt.data[s:e].astype(np.int64))
         np.testing.assert_array_equal(rows[k], np.sort(want), err_msg=f"row {k}")
+
+
+def test_long_run_parity_wide(hip_module):
+    """the fixed-point GD departs from MLlib's fp64 update
+    (weights quantised relative to max |w|, residuals to a bound); over a
+    long stream the drift must stay bounded.  60 warm-started batches of the
+    realistic multi-script vocabulary, the fp64 oracle continuing from its own
+    weights (never re-seeded): early-stop iteration counts agree (a one-step
+    difference only where the oracle's own convergence margin is tiny), the
+    prequential MSE per batch agrees, and the weight drift stays small."""
+    F = 1 << 20
+    cfg = SynthConfig.profile("wide", seed=21)
+    eng = _engine(F, step_size=0.005, num_iterations=50)
+    w = np.zeros(F + 4)
+    same = 0
+    worst_mse = worst_w = 0.0
+    T = 60
+    for t in range(T):
+        raw = generate_batch(cfg, t * 2000, 2000, batch_time_ms=NOW + t * 5000)
+        fb = featurize_batch(raw, F, 100, 1000)
+        pred_o = round_half_up_array(fb.X @ w)
+        res = eng.train_batch(raw, want_pred=False)
+        assert res["n_kept"] == fb.n
+        n, sy, sy2, sp, sp2, se2 = res["stats"]
+        mse_o = float(np.mean((fb.y - pred_o) ** 2))
+        worst_mse = max(worst_mse, abs(se2 / n - mse_o) / max(mse_o, 1e-30))
+        r = run_minibatch_sgd(fb.X, fb.y, w, 0.005, 50)
+        w = r.weights
+        assert abs(res["iterations"] - r.iterations) <= 1, (t, res["iterations"], r.iterations)
+        same += res["iterations"] == r.iterations
+        wg = eng.get_weights()
+        worst_w = max(worst_w, np.linalg.norm(wg - w) / max(np.linalg.norm(w), 1e-30))
+    print(f"long run: iterations equal in {same}/{T} batches, worst mse rel {worst_mse:.2e}, "
+          f"worst |dw|/|w| {worst_w:.2e}")
+    assert same >= 0.9 * T
+    assert worst_mse < 1e-3
+    assert worst_w < 1e-3
