@@ -280,6 +280,7 @@ struct DevSgd {
   const uint32_t* fcsc_pos;
   const uint32_t* fcsc_slot;
   const int64_t* far_n;      // device: far entries (CSC length)
+  const uint64_t* fcsc_off;  // [n_far + 1] CSC offset of every far slot (slot-sorted)
   int64_t F;
   int64_t ns;           // 4 + n_unique + pads (rounded)
   int64_t n_unique;
@@ -296,7 +297,7 @@ constexpr int kNormParts = 1024;   // grid cap of the norm / gather / scatter ke
 // i, written by its gradient kernel), [10] |r| bound B, [11] scales invalid
 // (diverged); [kRecHead + 3w] ||dw||^2, ||w||^2 and max |w_text| partials of
 // update workgroup w.
-constexpr int kMaxUpdGrid = 256;
+constexpr int kMaxUpdGrid = 1024;   // update workgroups: near column tiles + far slot ranges
 constexpr int kRecHead = 16;
 constexpr int kRecStride = kRecHead + 3 * kMaxUpdGrid;
 constexpr int kRecK = 3, kRecS = 4, kRecL = 5, kRecN = 6, kRecB = 10, kRecBad = 11;

@@ -1011,7 +1011,8 @@ int sgd_partials(int64_t ns, bool u16, int grid) {
 //                 iteration i's fixed-point scales; workgroup 0 records them
 //                 and publishes state[0..1] and the host flag.  Then one int64
 //                 partial row per workgroup.
-//   k_far_grad    (tiered) far slots' int64 sums into gacc[far_off ..].
+//   k_far_grad    (tiered, DP only) far slots' int64 sums into gacc[far_off ..]
+//                 (one GPU: the update kernel's far blocks sum them in LDS).
 //   [DP: k_sgd_reduce sums the partial rows into gacc[0, nl + 2), adds rank
 //    0's verdict on update i-1 and this rank's ready word to the tail, and
 //    ONE int64 all-reduce covers the whole packed buffer (near columns, loss,
@@ -1024,7 +1025,8 @@ int sgd_partials(int64_t ns, bool u16, int grid) {
 //    disagree on the iteration count (a mismatch would pair unequal
 //    collectives).]
 //   k_sgd_update  (iteration i)  multi-workgroup: sums the partial rows of
-//                 64 columns (world 1) or reads the all-reduced gacc,
+//                 64 columns (world 1) or reads the all-reduced gacc, and
+//                 (tiered) updates the far slots in fixed slot ranges,
 //                 SimpleUpdater on them, per-workgroup ||dw||^2, ||w||^2,
 //                 max |w_text| into record i.
 //   k_sgd_finish  after the loop: convergence of the last update.
@@ -1090,7 +1092,55 @@ __device__ __forceinline__ double flag_word(bool stop, bool all_ready, int64_t m
   return double(stop ? 1 : 0) + 2.0 * double(all_ready ? 1 : 0) + 4.0 * double(max_u);
 }
 
-__global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int nparts) {
+// One Hillis-Steele step of a segmented 64-bit sum: lanes without a DPP
+// source (or outside ROWS) see slot ~0 and add nothing.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t old, uint32_t v) {
+  return uint32_t(__builtin_amdgcn_update_dpp(int(old), int(v), CTRL, ROWS, 0xf, false));
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void seg_scan_step(long long& q, uint32_t sl) {
+  const uint32_t lo = dpp_u32<CTRL, ROWS>(0u, uint32_t(uint64_t(q)));
+  const uint32_t hi = dpp_u32<CTRL, ROWS>(0u, uint32_t(uint64_t(q) >> 32));
+  const uint32_t su = dpp_u32<CTRL, ROWS>(0xFFFFFFFFu, sl);
+  if (su == sl) q += (long long)((uint64_t(hi) << 32) | lo);
+}
+
+// Segmented inclusive sum over the wave of far CSC entries e (slot-sorted):
+// q = rint(residual of the entry's row * 2^S); the last lane of each run of
+// equal slots returns true with the run's sum in q.  DPP row shifts, then the
+// row broadcasts across the four 16-lane rows: the CSC is slot-sorted, so a
+// lane k places back is in this lane's run iff it holds the same slot.
+__device__ __forceinline__ bool far_seg_sum(const DevSgd& d, int64_t e, int64_t n, float qscale, uint32_t& sl,
+                                            long long& q) {
+  const int lane = lane_id();
+  const bool valid = e < n;
+  sl = valid ? d.fcsc_slot[e] : 0xFFFFFFFFu;
+  q = valid ? (long long)__float2int_rn(d.rbuf[d.fcsc_pos[e]] * qscale) : 0;
+  seg_scan_step<0x111, 0xf>(q, sl);   // row_shr:1
+  seg_scan_step<0x112, 0xf>(q, sl);   // row_shr:2
+  seg_scan_step<0x114, 0xf>(q, sl);   // row_shr:4
+  seg_scan_step<0x118, 0xf>(q, sl);   // row_shr:8
+  seg_scan_step<0x142, 0xa>(q, sl);   // row_bcast:15 -> rows 1, 3
+  seg_scan_step<0x143, 0xc>(q, sl);   // row_bcast:31 -> rows 2, 3
+  const uint32_t sn = uint32_t(__shfl_down(int(sl), 1, kWave));
+  return valid && (lane == kWave - 1 || e + 1 >= n || sn != sl);
+}
+
+// Update workgroups.  Blocks [0, nt) own 64-column tiles of the near (LDS)
+// slots, grid-stride over nt; blocks [nt, nt + nf) own far slot range k =
+// [n_far k / nf, n_far (k + 1) / nf) of the tiered layout.  On one GPU a far
+// block first sums its range's far gradients itself -- the CSC is
+// slot-sorted, so the range's entries are contiguous, [fcsc_off[lo],
+// fcsc_off[hi]) -- with wave segmented sums into an LDS int64 row (exact
+// integer sums), then applies the updates: the far backward needs no kernel
+// and no global atomics of its own, and it overlaps the near tiles'
+// partial-row sums.  DP: the far sums come from the all-reduced packed
+// buffer (k_far_grad before the all-reduce).  The grouping does not depend on
+// the rank's entries, so the fp64 norm partials -- and the convergence
+// verdicts -- are the same bits on one GPU and in DP.
+__global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int nparts, int nt, int nf) {
+  extern __shared__ long long lacc[];   // far blocks, one GPU: the range's far sums
   __shared__ double wsc[kUpdWaves][3];
   __shared__ int64_t red[kUpdWaves][kWave];
   __shared__ double m_sh;
@@ -1149,36 +1199,59 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
   const double alpha = sp.step_size / sqrt(double(it));
   const double gsc = ldexp(1.0, -sS);
   double ds = 0.0, ws = 0.0, mx = 0.0;
-  for (int64_t col0 = int64_t(blockIdx.x) * kWave; col0 < ncols; col0 += int64_t(gridDim.x) * kWave) {
-    const int64_t gp = nparts > 0 ? part_block_sum(d, col0, ncols, ns + 2, nparts, red) : 0;
-    const int64_t col = col0 + lane;
-    if (w == 0 && col < ncols) {
-      const int64_t gi = (nparts > 0 ? gp : (col <= ns + 1 ? d.gacc[col] : 0));
-      if (col < hi) {
-        double wn = d.wc64[col];
-        if (m > 0.0) {
-          const double g = double(gi) * (col < kNumNumeric ? ldexp(1.0, -int(rec_it[kRecN + col])) : gsc);
-          const double step = alpha * (g / m);
-          wn -= step;
-          d.wc64[col] = wn;
-          d.wc32[col] = float(wn);
-          ds += step * step;
-          ws += wn * wn;
+  if (int(blockIdx.x) < nt) {
+    for (int64_t col0 = int64_t(blockIdx.x) * kWave; col0 < ncols; col0 += int64_t(nt) * kWave) {
+      const int64_t gp = nparts > 0 ? part_block_sum(d, col0, ncols, ns + 2, nparts, red) : 0;
+      const int64_t col = col0 + lane;
+      if (w == 0 && col < ncols) {
+        const int64_t gi = (nparts > 0 ? gp : (col <= ns + 1 ? d.gacc[col] : 0));
+        if (col < hi) {
+          double wn = d.wc64[col];
+          if (m > 0.0) {
+            const double g = double(gi) * (col < kNumNumeric ? ldexp(1.0, -int(rec_it[kRecN + col])) : gsc);
+            const double step = alpha * (g / m);
+            wn -= step;
+            d.wc64[col] = wn;
+            d.wc32[col] = float(wn);
+            ds += step * step;
+            ws += wn * wn;
+          }
+          if (col >= kNumNumeric) mx = fmax(mx, fabs(double(float(wn))));   // the next iteration's weight scale
+        } else if (col == ns) {
+          if (m > 0.0) d.loss_hist[it] = 0.5 * double(gi) * ldexp(1.0, -sL) / m;
+        } else if (col >= ns + 2 && nparts > 0) {
+          d.stats[col - ns - 2] += __builtin_bit_cast(double, gp);   // batch stats (iteration 1, single GPU)
         }
-        if (col >= kNumNumeric) mx = fmax(mx, fabs(double(float(wn))));   // the next iteration's weight scale
-      } else if (col == ns) {
-        if (m > 0.0) d.loss_hist[it] = 0.5 * double(gi) * ldexp(1.0, -sL) / m;
-      } else if (col >= ns + 2 && nparts > 0) {
-        d.stats[col - ns - 2] += __builtin_bit_cast(double, gp);   // batch stats (iteration 1, single GPU)
       }
     }
-  }
-  // tiered: far slots [far_base, 4 + n_unique), one thread per slot, from
-  // the fixed-point far gradient (k_far_grad / all-reduced), re-zeroed here
-  if (n_far > 0) {
-    for (int64_t j = int64_t(blockIdx.x) * 1024 + tid; j < n_far; j += int64_t(gridDim.x) * 1024) {
-      const double g = double(gfar[j]) * gsc;
-      gfar[j] = 0;
+  } else if (n_far > 0) {
+    // tiered: far slots [far_base + jlo, far_base + jhi)
+    const int64_t k = int64_t(blockIdx.x) - nt;
+    const int64_t jlo = n_far * k / nf, jhi = n_far * (k + 1) / nf;
+    if (!sp.dp) {
+      for (int64_t i = tid; i < jhi - jlo; i += 1024) lacc[i] = 0;
+      __syncthreads();
+      const int64_t E0 = int64_t(d.fcsc_off[jlo]);
+      const int64_t E1 = jhi >= n_far ? *d.far_n : int64_t(d.fcsc_off[jhi]);   // the scan leaves no end entry
+      const float qscale = ldexpf(1.f, sS);
+      const uint32_t base = uint32_t(d.far_base + jlo);
+      for (int64_t e0 = E0 + int64_t(w) * kWave; e0 < E1; e0 += 1024) {
+        uint32_t sl;
+        long long q;
+        if (far_seg_sum(d, e0 + lane, E1, qscale, sl, q) && q != 0)
+          atomicAdd(reinterpret_cast<unsigned long long*>(&lacc[sl - base]), (unsigned long long)q);   // ds_add_u64
+      }
+      __syncthreads();
+    }
+    for (int64_t j = jlo + tid; j < jhi; j += 1024) {
+      int64_t gi;
+      if (sp.dp) {
+        gi = gfar[j];
+        gfar[j] = 0;
+      } else {
+        gi = lacc[j - jlo];
+      }
+      const double g = double(gi) * gsc;
       const int64_t col = d.far_base + j;
       double wn = d.wc64[col];
       if (m > 0.0) {
@@ -1219,11 +1292,22 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
   }
 }
 
-void launch_sgd_update(const DevSgd& d, const SgdParams& sp, int nparts, hipStream_t s) {
+// Near tiles and far ranges of the update grid: a function of the layout
+// only, the same on every DP rank.
+static void update_split(const DevSgd& d, int& nt, int& nf) {
   const int64_t tiles = (d.nl + kPartVals - kNumNumeric + kWave - 1) / kWave;
-  const int64_t far_tiles = (kNumNumeric + d.n_unique - d.far_base + 1023) / 1024;
-  const int grid = int(std::max<int64_t>(1, std::min<int64_t>(std::max(tiles, far_tiles), kMaxUpdGrid)));
-  hipLaunchKernelGGL(k_sgd_update, dim3(grid), dim3(1024), 0, s, d, sp, nparts);
+  const int64_t n_far = kNumNumeric + d.n_unique - d.far_base;
+  nt = int(std::max<int64_t>(1, std::min<int64_t>(tiles, kMaxUpdGrid / 2)));
+  nf = n_far > 0 ? int(std::max<int64_t>(1, std::min<int64_t>((n_far + 767) / 768, kMaxUpdGrid - nt))) : 0;
+}
+
+void launch_sgd_update(const DevSgd& d, const SgdParams& sp, int nparts, hipStream_t s) {
+  int nt = 0, nf = 0;
+  update_split(d, nt, nf);
+  const int64_t n_far = kNumNumeric + d.n_unique - d.far_base;
+  const size_t lds = (nf > 0 && !sp.dp) ? sizeof(long long) * size_t((n_far + nf - 1) / nf) : 0;
+  if (lds > 96 * 1024) throw std::runtime_error("update: too many far slots per workgroup");
+  hipLaunchKernelGGL(k_sgd_update, dim3(nt + nf), dim3(1024), lds, s, d, sp, nparts, nt, nf);
 }
 
 // DP: cross-workgroup reduction of the partial rows into the packed buffer
@@ -1291,20 +1375,6 @@ void launch_sgd_finish(const DevSgd& d, const SgdParams& sp, hipStream_t s) {
 // so the result does not depend on the order of entries inside a slot or on
 // which wave adds first: deterministic across runs and DP ranks.
 // ---------------------------------------------------------------------------
-template <int CTRL, int ROWS>
-__device__ __forceinline__ uint32_t dpp_u32(uint32_t old, uint32_t v) {
-  return uint32_t(__builtin_amdgcn_update_dpp(int(old), int(v), CTRL, ROWS, 0xf, false));
-}
-// One Hillis-Steele step of a segmented 64-bit sum: lanes without a DPP
-// source (or outside ROWS) see slot ~0 and add nothing.
-template <int CTRL, int ROWS>
-__device__ __forceinline__ void seg_scan_step(long long& q, uint32_t sl) {
-  const uint32_t lo = dpp_u32<CTRL, ROWS>(0u, uint32_t(uint64_t(q)));
-  const uint32_t hi = dpp_u32<CTRL, ROWS>(0u, uint32_t(uint64_t(q) >> 32));
-  const uint32_t su = dpp_u32<CTRL, ROWS>(0xFFFFFFFFu, sl);
-  if (su == sl) q += (long long)((uint64_t(hi) << 32) | lo);
-}
-
 __global__ __launch_bounds__(256) void k_far_grad(DevSgd d, SgdParams sp) {
   if (d.state[0] != 0.0 || d.state[8] == double(sp.iteration)) return;   // done / DP pass skipped
   const int64_t n = *d.far_n;
@@ -1313,23 +1383,9 @@ __global__ __launch_bounds__(256) void k_far_grad(DevSgd d, SgdParams sp) {
   unsigned long long* gfar = reinterpret_cast<unsigned long long*>(d.gacc + d.far_off);
   const int64_t stride = int64_t(gridDim.x) * 256;
   for (int64_t e0 = int64_t(blockIdx.x) * 256 + (threadIdx.x & ~(kWave - 1)); e0 < n; e0 += stride) {
-    const int64_t e = e0 + lane;
-    const bool valid = e < n;
-    uint32_t sl = valid ? d.fcsc_slot[e] : 0xFFFFFFFFu;
-    long long q = valid ? (long long)__float2int_rn(d.rbuf[d.fcsc_pos[e]] * qscale) : 0;
-    // segmented inclusive scan on the VALU (DPP row shifts, then the row
-    // broadcasts across the four 16-lane rows) instead of 18 LDS permutes:
-    // the CSC is slot-sorted, so a lane k places back is in this lane's
-    // segment iff it holds the same slot
-    seg_scan_step<0x111, 0xf>(q, sl);   // row_shr:1
-    seg_scan_step<0x112, 0xf>(q, sl);   // row_shr:2
-    seg_scan_step<0x114, 0xf>(q, sl);   // row_shr:4
-    seg_scan_step<0x118, 0xf>(q, sl);   // row_shr:8
-    seg_scan_step<0x142, 0xa>(q, sl);   // row_bcast:15 -> rows 1, 3
-    seg_scan_step<0x143, 0xc>(q, sl);   // row_bcast:31 -> rows 2, 3
-    const uint32_t sn = uint32_t(__shfl_down(int(sl), 1, kWave));
-    const bool tail = valid && (lane == kWave - 1 || e + 1 >= n || sn != sl);
-    if (tail && q != 0) atomicAdd(&gfar[sl - d.far_base], (unsigned long long)q);
+    uint32_t sl;
+    long long q;
+    if (far_seg_sum(d, e0 + lane, n, qscale, sl, q) && q != 0) atomicAdd(&gfar[sl - d.far_base], (unsigned long long)q);
   }
 }
 
