@@ -847,9 +847,19 @@ __device__ __forceinline__ void hyb_lds_init(const DevPrepared& p, const float* 
                                              float wscale, int32_t* wl, unsigned long long* gl,
                                              uint32_t* whl, unsigned long long* hsum, uint32_t* wctr) {
   if (threadIdx.x == 0) *wctr = 0u;
-  for (int64_t s = threadIdx.x; s < ns; s += kIterBlock)
-    wl[s] = (s >= kNumNumeric && s < hi) ? w_to_fix(wsrc[s], wscale) : 0;
-  for (int64_t s = threadIdx.x; s < ns * REP; s += kIterBlock) gl[s] = 0ull;
+  // 16-byte LDS stores (ns is a multiple of 64; wl and gl are 16-B aligned):
+  // 4 weights and 2 gradient words per store instead of one
+  for (int64_t s4 = threadIdx.x; s4 < ns / 4; s4 += kIterBlock) {
+    const int64_t s = 4 * s4;
+    const float4 wv = *reinterpret_cast<const float4*>(wsrc + s);
+    const float wf[4] = {wv.x, wv.y, wv.z, wv.w};
+    int32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = (s + k >= kNumNumeric && s + k < hi) ? w_to_fix(wf[k], wscale) : 0;
+    reinterpret_cast<int4*>(wl)[s4] = make_int4(o[0], o[1], o[2], o[3]);
+  }
+  for (int64_t s2 = threadIdx.x; s2 < ns * REP / 2; s2 += kIterBlock)
+    reinterpret_cast<uint4*>(gl)[s2] = make_uint4(0u, 0u, 0u, 0u);
   for (int s = threadIdx.x; s < kHot + 8; s += kIterBlock) hsum[s] = 0ull;
   __syncthreads();
   if (threadIdx.x < kWave) hot_digits(p, wl, whl);
