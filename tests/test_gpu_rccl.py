@@ -79,7 +79,7 @@ def test_forced_dp_rccl_equals_plain_engine(hip_module, ci, ahead):
     plain = DeviceLinearRegression(LRDeviceConfig(**base), device=0)
     rd = _train(dp, batches, ahead)
     rp = _train(plain, batches, ahead)
-    total_iters = 0
+    total_iters = comm_iters = 0
     for a, b in zip(rd, rp):
         assert bool(b["tiered"]) == tiered
         assert (a["iterations"], a["n_kept"], a["n_kept_global"], a["n_unique"], bool(a["tiered"])) == \
@@ -87,15 +87,19 @@ def test_forced_dp_rccl_equals_plain_engine(hip_module, ci, ahead):
         assert list(a["stats"]) == list(b["stats"])
         assert list(a["loss_history"]) == list(b["loss_history"])
         np.testing.assert_array_equal(np.asarray(a["pred"]), np.asarray(b["pred"]))
-        # one packed int64 gradient all-reduce per GD iteration, timed on the stream
-        assert a["comm_iters"] == a["iterations"] and b["comm_iters"] == 0
+        # one packed int64 gradient all-reduce per enqueued GD iteration (the
+        # host runs up to early_exit_depth iterations ahead of the verdict;
+        # those early-exit on the device but keep the collectives paired),
+        # timed on the stream
+        assert a["iterations"] <= a["comm_iters"] <= a["iterations"] + 4 and b["comm_iters"] == 0
         assert a["comm_ms"] > 0.0
         total_iters += a["iterations"]
+        comm_iters += a["comm_iters"]
     np.testing.assert_array_equal(dp.get_weights(), plain.get_weights())
     c = comm.counters()
     # gradient all-reduces + one stats all-reduce per batch (+ the in-line
     # active-set size all-reduce of a batch not gathered ahead)
-    assert total_iters + nb <= c["allreduce_calls"] <= total_iters + 2 * nb
+    assert comm_iters + nb <= c["allreduce_calls"] <= comm_iters + 2 * nb
     assert c["allgather_calls"] == nb          # one prep-packet all-gather per batch
     assert c["allreduce_bytes"] > 8 * total_iters
 
