@@ -1121,12 +1121,9 @@ __device__ __forceinline__ void seg_scan_step(long long& q, uint32_t sl) {
 // equal slots returns true with the run's sum in q.  DPP row shifts, then the
 // row broadcasts across the four 16-lane rows: the CSC is slot-sorted, so a
 // lane k places back is in this lane's run iff it holds the same slot.
-__device__ __forceinline__ bool far_seg_sum(const DevSgd& d, int64_t e, int64_t n, float qscale, uint32_t& sl,
-                                            long long& q) {
+__device__ __forceinline__ bool far_seg_scan(int64_t e, int64_t n, uint32_t sl, long long& q) {
   const int lane = lane_id();
   const bool valid = e < n;
-  sl = valid ? d.fcsc_slot[e] : 0xFFFFFFFFu;
-  q = valid ? (long long)__float2int_rn(d.rbuf[d.fcsc_pos[e]] * qscale) : 0;
   seg_scan_step<0x111, 0xf>(q, sl);   // row_shr:1
   seg_scan_step<0x112, 0xf>(q, sl);   // row_shr:2
   seg_scan_step<0x114, 0xf>(q, sl);   // row_shr:4
@@ -1135,6 +1132,14 @@ __device__ __forceinline__ bool far_seg_sum(const DevSgd& d, int64_t e, int64_t 
   seg_scan_step<0x143, 0xc>(q, sl);   // row_bcast:31 -> rows 2, 3
   const uint32_t sn = uint32_t(__shfl_down(int(sl), 1, kWave));
   return valid && (lane == kWave - 1 || e + 1 >= n || sn != sl);
+}
+
+__device__ __forceinline__ bool far_seg_sum(const DevSgd& d, int64_t e, int64_t n, float qscale, uint32_t& sl,
+                                            long long& q) {
+  const bool valid = e < n;
+  sl = valid ? d.fcsc_slot[e] : 0xFFFFFFFFu;
+  q = valid ? (long long)__float2int_rn(d.rbuf[d.fcsc_pos[e]] * qscale) : 0;
+  return far_seg_scan(e, n, sl, q);
 }
 
 // Update workgroups.  Blocks [0, nt) own 64-column tiles of the near (LDS)
@@ -1245,11 +1250,27 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
       const int64_t E1 = jhi >= n_far ? *d.far_n : int64_t(d.fcsc_off[jhi]);   // the scan leaves no end entry
       const float qscale = ldexpf(1.f, sS);
       const uint32_t base = uint32_t(d.far_base + jlo);
-      for (int64_t e0 = E0 + int64_t(w) * kWave; e0 < E1; e0 += 1024) {
-        uint32_t sl;
-        long long q;
-        if (far_seg_sum(d, e0 + lane, E1, qscale, sl, q) && q != 0)
-          atomicAdd(reinterpret_cast<unsigned long long*>(&lacc[sl - base]), (unsigned long long)q);   // ds_add_u64
+      // two 64-entry tiles per wave step: both tiles' (slot, row) loads, then
+      // both residual gathers, are in flight before the scans
+      constexpr int kU = 2;
+      for (int64_t e0 = E0 + int64_t(w) * (kU * kWave); e0 < E1; e0 += kU * 1024) {
+        uint32_t sl[kU], ps[kU];
+        float rv[kU];
+        long long q[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          const int64_t e = e0 + u * kWave + lane;
+          sl[u] = e < E1 ? d.fcsc_slot[e] : 0xFFFFFFFFu;
+          ps[u] = e < E1 ? d.fcsc_pos[e] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) rv[u] = e0 + u * kWave + lane < E1 ? d.rbuf[ps[u]] : 0.f;
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          q[u] = (long long)__float2int_rn(rv[u] * qscale);
+          if (far_seg_scan(e0 + u * kWave + lane, E1, sl[u], q[u]) && q[u] != 0)
+            atomicAdd(reinterpret_cast<unsigned long long*>(&lacc[sl[u] - base]), (unsigned long long)q[u]);   // ds_add_u64
+        }
       }
       __syncthreads();
     }
