@@ -33,6 +33,20 @@ def test_bench_json_line(hip_module, mode):
     assert d["steps"] == 3 and d["warmup"] == 1
     assert d["config"]["global_batch"] == 100000
     assert ("e2e" in d["ingest"]) == (not mode)
+    # the timed window starts with an empty pipeline
+    assert d["prestaged_at_t0"] == 0
+    assert d["comm_world"] == 1 and len(d["per_rank_value"]) == 1
+    assert d["per_rank_host"][0]["pinned_mb"] > 0
+
+
+def test_bench_force_dp_reports_the_collective(hip_module):
+    """--force-dp: the engine's DP path through a world-1 RCCL communicator;
+    the JSON shows the gradient all-reduces per step and their time."""
+    d = _bench("--batch", "100000", "--steps", "3", "--warmup", "1", "--pool", "2", "--force-dp")
+    assert d["config"]["parallelism"] == "dp1-forced" and d["comm_kind"] == "rccl"
+    assert d["comm_world"] == 1 and d["grad_allreduce_per_step"] >= 1
+    assert d["grad_allreduce_us_per_iter"] > 0
+    assert d["comm_counters"]["allgather_calls"] >= 3 + 1
 
 
 def test_bench_hbm_batch_sizing(hip_module):
