@@ -801,7 +801,6 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred, int64_t plot_points) {
     sgd_.fcsc_pos = prep.fcsc_pos;
     sgd_.fcsc_slot = prep.fcsc_slot;
     sgd_.far_n = prep.tparam + 2;
-    sgd_.fcsc_off = prep.fhist;
   }
   launch_batch_init(sgd_, double(n_glob), cfg_.num_iterations + 2, s);  // state[5] = m (global kept rows)
   if (norm_age_ < 0 || norm_age_ >= kNormRefresh) {
@@ -881,10 +880,7 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred, int64_t plot_points) {
       // every rank launches the gradient kernel (an empty shard writes zero
       // partials) so every rank runs the convergence prologue
       launch_sgd_iter(sgd_, prep, sp, pb.host_counters[2], u16, grid, s);
-      // one GPU: the far backward runs inside the update kernel (its far
-      // workgroups sum their slot range's CSC segments); DP: before the
-      // all-reduce, into the packed buffer
-      if (tiered && dp_) launch_far_grad(sgd_, sp, num_cu_, s);
+      if (tiered) launch_far_grad(sgd_, sp, num_cu_, s);
       if (dp_) {
         // ONE collective per iteration: the packed int64 buffer (near
         // columns, loss, sampled m, verdict, ready words, far slots); integer

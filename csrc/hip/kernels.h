@@ -280,7 +280,6 @@ struct DevSgd {
   const uint32_t* fcsc_pos;
   const uint32_t* fcsc_slot;
   const int64_t* far_n;      // device: far entries (CSC length)
-  const uint64_t* fcsc_off;  // [n_far + 1] CSC offset of every far slot (slot-sorted)
   int64_t F;
   int64_t ns;           // 4 + n_unique + pads (rounded)
   int64_t n_unique;

@@ -1021,8 +1021,7 @@ int sgd_partials(int64_t ns, bool u16, int grid) {
 //                 iteration i's fixed-point scales; workgroup 0 records them
 //                 and publishes state[0..1] and the host flag.  Then one int64
 //                 partial row per workgroup.
-//   k_far_grad    (tiered, DP only) far slots' int64 sums into gacc[far_off ..]
-//                 (one GPU: the update kernel's far blocks sum them in LDS).
+//   k_far_grad    (tiered) far slots' int64 sums into gacc[far_off ..].
 //   [DP: k_sgd_reduce sums the partial rows into gacc[0, nl + 2), adds rank
 //    0's verdict on update i-1 and this rank's ready word to the tail, and
 //    ONE int64 all-reduce covers the whole packed buffer (near columns, loss,
@@ -1144,18 +1143,16 @@ __device__ __forceinline__ bool far_seg_sum(const DevSgd& d, int64_t e, int64_t 
 
 // Update workgroups.  Blocks [0, nt) own 64-column tiles of the near (LDS)
 // slots, grid-stride over nt; blocks [nt, nt + nf) own far slot range k =
-// [n_far k / nf, n_far (k + 1) / nf) of the tiered layout.  On one GPU a far
-// block first sums its range's far gradients itself -- the CSC is
-// slot-sorted, so the range's entries are contiguous, [fcsc_off[lo],
-// fcsc_off[hi]) -- with wave segmented sums into an LDS int64 row (exact
-// integer sums), then applies the updates: the far backward needs no kernel
-// and no global atomics of its own, and it overlaps the near tiles'
-// partial-row sums.  DP: the far sums come from the all-reduced packed
-// buffer (k_far_grad before the all-reduce).  The grouping does not depend on
-// the rank's entries, so the fp64 norm partials -- and the convergence
-// verdicts -- are the same bits on one GPU and in DP.
+// [n_far k / nf, n_far (k + 1) / nf) of the tiered layout, read from the far
+// gradient sums (k_far_grad; DP: the all-reduced packed buffer).  The near
+// tiles and the far ranges run side by side instead of every block doing a
+// tile and then a grid-stride share of the far slots (r3: 26 us -> 17 us
+// on the wide profile).  Measured and reverted: far blocks summing their
+// range's CSC segments themselves (no k_far_grad) -- the far entries are
+// skewed over slot ranges, and the slowest block made the update ~100 us.
+// The grouping is a function of the layout only, so the fp64 norm partials
+// (and the convergence verdicts) are the same bits on one GPU and in DP.
 __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int nparts, int nt, int nf) {
-  extern __shared__ long long lacc[];   // far blocks, one GPU: the range's far sums
   __shared__ double wsc[kUpdWaves][3];
   __shared__ int64_t red[kUpdWaves][kWave];
   __shared__ double m_sh;
@@ -1240,49 +1237,13 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
       }
     }
   } else if (n_far > 0) {
-    // tiered: far slots [far_base + jlo, far_base + jhi)
+    // tiered: far slots [far_base + jlo, far_base + jhi) from the far
+    // gradient sums (k_far_grad; DP: all-reduced), re-zeroed here
     const int64_t k = int64_t(blockIdx.x) - nt;
     const int64_t jlo = n_far * k / nf, jhi = n_far * (k + 1) / nf;
-    if (!sp.dp) {
-      for (int64_t i = tid; i < jhi - jlo; i += 1024) lacc[i] = 0;
-      __syncthreads();
-      const int64_t E0 = int64_t(d.fcsc_off[jlo]);
-      const int64_t E1 = jhi >= n_far ? *d.far_n : int64_t(d.fcsc_off[jhi]);   // the scan leaves no end entry
-      const float qscale = ldexpf(1.f, sS);
-      const uint32_t base = uint32_t(d.far_base + jlo);
-      // two 64-entry tiles per wave step: both tiles' (slot, row) loads, then
-      // both residual gathers, are in flight before the scans
-      constexpr int kU = 2;
-      for (int64_t e0 = E0 + int64_t(w) * (kU * kWave); e0 < E1; e0 += kU * 1024) {
-        uint32_t sl[kU], ps[kU];
-        float rv[kU];
-        long long q[kU];
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-          const int64_t e = e0 + u * kWave + lane;
-          sl[u] = e < E1 ? d.fcsc_slot[e] : 0xFFFFFFFFu;
-          ps[u] = e < E1 ? d.fcsc_pos[e] : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < kU; ++u) rv[u] = e0 + u * kWave + lane < E1 ? d.rbuf[ps[u]] : 0.f;
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-          q[u] = (long long)__float2int_rn(rv[u] * qscale);
-          if (far_seg_scan(e0 + u * kWave + lane, E1, sl[u], q[u]) && q[u] != 0)
-            atomicAdd(reinterpret_cast<unsigned long long*>(&lacc[sl[u] - base]), (unsigned long long)q[u]);   // ds_add_u64
-        }
-      }
-      __syncthreads();
-    }
     for (int64_t j = jlo + tid; j < jhi; j += 1024) {
-      int64_t gi;
-      if (sp.dp) {
-        gi = gfar[j];
-        gfar[j] = 0;
-      } else {
-        gi = lacc[j - jlo];
-      }
-      const double g = double(gi) * gsc;
+      const double g = double(gfar[j]) * gsc;
+      gfar[j] = 0;
       const int64_t col = d.far_base + j;
       double wn = d.wc64[col];
       if (m > 0.0) {
@@ -1335,10 +1296,7 @@ static void update_split(const DevSgd& d, int& nt, int& nf) {
 void launch_sgd_update(const DevSgd& d, const SgdParams& sp, int nparts, hipStream_t s) {
   int nt = 0, nf = 0;
   update_split(d, nt, nf);
-  const int64_t n_far = kNumNumeric + d.n_unique - d.far_base;
-  const size_t lds = (nf > 0 && !sp.dp) ? sizeof(long long) * size_t((n_far + nf - 1) / nf) : 0;
-  if (lds > 96 * 1024) throw std::runtime_error("update: too many far slots per workgroup");
-  hipLaunchKernelGGL(k_sgd_update, dim3(nt + nf), dim3(1024), lds, s, d, sp, nparts, nt, nf);
+  hipLaunchKernelGGL(k_sgd_update, dim3(nt + nf), dim3(1024), 0, s, d, sp, nparts, nt, nf);
 }
 
 // DP: cross-workgroup reduction of the partial rows into the packed buffer
