@@ -25,6 +25,12 @@ def is_rccl(name: str) -> bool:
     return bool(re.search(r"nccl|rccl", name, re.I))
 
 
+def is_copy(name: str) -> bool:
+    # a world-1 communicator: RCCL's all-gather is a device copy, its in-place
+    # all-reduce does nothing on the device
+    return name.startswith("__amd_rocclr_copyBuffer")
+
+
 def main(path: str) -> None:
     rows = list(csv.DictReader(open(path)))
     for r in rows:
@@ -67,6 +73,23 @@ def main(path: str) -> None:
         gaps = sorted((seq[i + 1]["t0"] - seq[i - 1]["t1"]) / 1e3 for i, _ in inloop)
         print(f"  k_sgd_reduce end -> k_sgd_update start: median {gaps[len(gaps) // 2]:.2f} us")
     print(f"other RCCL kernels on the compute stream: {len(other)}")
+    # what the gradient collective costs the stream: k_sgd_reduce end -> k_sgd_update start
+    gaps = sorted((seq[i + 1]["t0"] - r["t1"]) / 1e3 for i, r in enumerate(seq[:-1])
+                  if r["k"] == "k_sgd_reduce" and seq[i + 1]["k"].startswith("k_sgd_update") or
+                  (r["k"] == "k_sgd_reduce" and i + 2 < len(seq) and seq[i + 2]["k"].startswith("k_sgd_update")))
+    if gaps:
+        print(f"k_sgd_reduce end -> next kernel (all-reduce on the stream) over {len(gaps)} iterations: "
+              f"median {gaps[len(gaps) // 2]:.2f} us, p90 {gaps[int(0.9 * (len(gaps) - 1))]:.2f} us")
+    # copies inside the GD loop (between an update and the next iteration
+    # kernel): the world-1 packet all-gather issued mid-loop
+    mid = [(i, r) for i, r in enumerate(seq) if is_copy(r["k"]) and 0 < i < len(seq) - 1
+           and seq[i - 1]["k"].startswith("k_sgd_update") and seq[i + 1]["k"].startswith("k_sgd_iter")]
+    print(f"device copies between a GD update and the next iteration (mid-loop all-gather at world 1): {len(mid)}")
+    for i, r in mid[:8]:
+        ov = collections.Counter(o["k"] for s2, v in streams.items() if s2 != comp for o in v
+                                 if o["t0"] < r["t1"] and o["t1"] > r["t0"])
+        print(f"  {(r['t1'] - r['t0']) / 1e3:8.2f} us; overlapping other-stream kernels: "
+              + (", ".join(f"{k} x{v}" for k, v in ov.most_common(4)) or "none"))
     others = [r for s, v in streams.items() if s != comp for r in v]
     for i, r in other:
         ov = collections.Counter(o["k"] for o in others if o["t0"] < r["t1"] and o["t1"] > r["t0"])
