@@ -1133,13 +1133,6 @@ __device__ __forceinline__ bool far_seg_scan(int64_t e, int64_t n, uint32_t sl, 
   return valid && (lane == kWave - 1 || e + 1 >= n || sn != sl);
 }
 
-__device__ __forceinline__ bool far_seg_sum(const DevSgd& d, int64_t e, int64_t n, float qscale, uint32_t& sl,
-                                            long long& q) {
-  const bool valid = e < n;
-  sl = valid ? d.fcsc_slot[e] : 0xFFFFFFFFu;
-  q = valid ? (long long)__float2int_rn(d.rbuf[d.fcsc_pos[e]] * qscale) : 0;
-  return far_seg_scan(e, n, sl, q);
-}
 
 // Update workgroups.  Blocks [0, nt) own 64-column tiles of the near (LDS)
 // slots, grid-stride over nt; blocks [nt, nt + nf) own far slot range k =
@@ -1370,11 +1363,28 @@ __global__ __launch_bounds__(256) void k_far_grad(DevSgd d, SgdParams sp) {
   const int lane = lane_id();
   const float qscale = ldexpf(1.f, int(sgd_rec(d, sp.iteration)[kRecS]));
   unsigned long long* gfar = reinterpret_cast<unsigned long long*>(d.gacc + d.far_off);
-  const int64_t stride = int64_t(gridDim.x) * 256;
-  for (int64_t e0 = int64_t(blockIdx.x) * 256 + (threadIdx.x & ~(kWave - 1)); e0 < n; e0 += stride) {
-    uint32_t sl;
-    long long q;
-    if (far_seg_sum(d, e0 + lane, n, qscale, sl, q) && q != 0) atomicAdd(&gfar[sl - d.far_base], (unsigned long long)q);
+  // two 64-entry tiles per wave step: both tiles' (slot, row) loads, then
+  // both residual gathers, are in flight before the scans (half the
+  // dependent round trips of one tile per step)
+  constexpr int kU = 2;
+  const int64_t stride = int64_t(gridDim.x) * 256 * kU;
+  for (int64_t e0 = (int64_t(blockIdx.x) * 256 + (threadIdx.x & ~(kWave - 1))) * kU; e0 < n; e0 += stride) {
+    uint32_t sl[kU], ps[kU];
+    float rv[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t e = e0 + u * kWave + lane;
+      sl[u] = e < n ? d.fcsc_slot[e] : 0xFFFFFFFFu;
+      ps[u] = e < n ? d.fcsc_pos[e] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) rv[u] = e0 + u * kWave + lane < n ? d.rbuf[ps[u]] : 0.f;
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      long long q = (long long)__float2int_rn(rv[u] * qscale);
+      if (far_seg_scan(e0 + u * kWave + lane, n, sl[u], q) && q != 0)
+        atomicAdd(&gfar[sl[u] - d.far_base], (unsigned long long)q);
+    }
   }
 }
 
