@@ -3,7 +3,10 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <charconv>
+#include <cmath>
 #include <stdexcept>
+#include <string>
 #include <vector>
 
 #include "featurize_cpu.h"
@@ -131,6 +134,32 @@ PYBIND11_MODULE(_twtml_host, m) {
 
   m.def("wire_bound", &wire_bound, py::arg("units"), py::arg("rows"));
   m.def("utf8_bound", &utf8_bound, py::arg("units"));
+  // JSON array text of a float64 vector (shortest round-trip digits, like
+  // Python's repr; non-finite values as null), built with the GIL released:
+  // the Lightning plot's series are tens of thousands of numbers per append,
+  // and json.dumps holds the GIL for milliseconds (report/lightning.py).
+  m.def("json_floats", [](Arr<double> v) {
+    std::string out;
+    {
+      py::gil_scoped_release nogil;
+      const double* x = v.data();
+      const size_t n = size_t(v.size());
+      out.reserve(n * 12 + 2);
+      out.push_back('[');
+      char buf[32];
+      for (size_t i = 0; i < n; ++i) {
+        if (i) out.push_back(',');
+        if (!std::isfinite(x[i])) {
+          out += "null";
+          continue;
+        }
+        const auto r = std::to_chars(buf, buf + sizeof(buf), x[i]);
+        out.append(buf, r.ptr);
+      }
+      out.push_back(']');
+    }
+    return py::bytes(out);
+  }, py::arg("values"));
   m.def("utf8_encode",
         [](Arr<uint16_t> text, Arr<int64_t> offsets, int threads) {
           const int64_t n = int64_t(offsets.size()) - 1;

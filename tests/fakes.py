@@ -2,11 +2,18 @@
 
 The reference has no Lightning fake ("no mock HTTP server"); this
 one implements the three endpoints the client uses and remembers payloads.
+``FakeLightningProcess`` serves the same endpoints from a child process (so
+its JSON parsing does not share the test's GIL) and reports a summary of the
+appends over ``GET /_summary``.
 """
 from __future__ import annotations
 
 import asyncio
 import itertools
+import json
+import os
+import subprocess
+import sys
 import threading
 from typing import Any, Dict, List, Tuple
 
@@ -37,6 +44,13 @@ class FakeLightning:
                 return web.json_response({"id": f"v{next(self._ids)}"})
             return web.json_response({})
 
+        async def summary(request: web.Request) -> web.Response:
+            apps = self.appends()
+            return web.json_response({
+                "calls": len(self.calls), "appends": len(apps),
+                "last_series_lens": [len(s) for s in apps[-1]["data"]["series"]] if apps else []})
+
+        app.router.add_route("GET", "/_summary", summary)
         app.router.add_route("POST", "/{tail:.*}", handler)
         return app
 
@@ -69,3 +83,42 @@ class FakeLightning:
 
     def appends(self) -> List[Dict[str, Any]]:
         return [b for (m, p, b) in self.calls if p.endswith("/data/")]
+
+
+class FakeLightningProcess:
+    """``FakeLightning`` in a child process; ``summary()`` -> ``{"calls",
+    "appends", "last_series_lens"}``."""
+
+    def __init__(self):
+        self.proc = None
+        self.port = 0
+
+    def start(self) -> "FakeLightningProcess":
+        env = dict(os.environ, PYTHONPATH=os.path.dirname(os.path.abspath(__file__)))
+        self.proc = subprocess.Popen([sys.executable, "-c", "import fakes; fakes._serve()"],
+                                     stdout=subprocess.PIPE, env=env, text=True)
+        self.port = int(self.proc.stdout.readline())
+        return self
+
+    @property
+    def url(self) -> str:
+        return f"http://127.0.0.1:{self.port}"
+
+    def summary(self) -> Dict[str, Any]:
+        import requests
+        return requests.get(self.url + "/_summary", timeout=10).json()
+
+    def stop(self) -> None:
+        if self.proc is not None:
+            self.proc.terminate()
+            try:
+                self.proc.wait(10)
+            except subprocess.TimeoutExpired:
+                self.proc.kill()
+            self.proc = None
+
+
+def _serve() -> None:
+    srv = FakeLightning().start()
+    print(srv.port, flush=True)
+    srv._thread.join()

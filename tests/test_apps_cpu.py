@@ -111,3 +111,27 @@ def test_featurize_rows_rejects_offsets_beyond_text():
     with pytest.raises(ValueError, match="exceed"):
         host().featurize_rows(np.zeros(0, np.uint16), np.array([0, 5, 9], np.int64),
                               np.array([0, 1], np.int64), 1000, "java", 0)
+
+
+def test_lightning_numpy_append_matches_list_payload():
+    """The pre-encoded append (``_twtml_host.json_floats``, GIL released) posts
+    the same JSON as the list path: shortest round-trip floats, NaN -> null,
+    the optional keys after the series."""
+    from twitter_stream_ml_amd.report.lightning import Lightning, _json_floats
+    x = np.array([0.0, -0.0, 0.1, 1 / 3, 1e-310, 1.7976931348623157e308, 123456789012345.0, np.nan, np.inf])
+    assert json.loads(_json_floats(x)) == [v if np.isfinite(v) else None for v in x.tolist()]
+    r = np.random.default_rng(0).standard_normal(5000) * 1e3
+    assert json.loads(_json_floats(r)) == r.tolist()
+    lgn = FakeLightning().start()
+    try:
+        cli = Lightning(lgn.url)
+        viz = cli.line_streaming(series=[[0.0]] * 2)
+        series = [r[:100], np.full(100, 2.5)]
+        cli.line_streaming(series=series, viz=viz)                             # numpy: pre-encoded
+        cli.line_streaming(series=[s.tolist() for s in series], viz=viz)      # lists: json=
+        cli.line_streaming(series=series, size=[1.0, 2.0], xaxis="t", viz=viz)
+        a = lgn.appends()
+    finally:
+        lgn.stop()
+    assert a[0] == a[1] and a[0]["data"]["series"][0] == r[:100].tolist()
+    assert a[2]["data"]["size"] == [1.0, 2.0] and a[2]["data"]["xaxis"] == "t"

@@ -13,12 +13,19 @@ constant pool):
 * embed URL ``{host}/visualizations/{id}/pym``
 
 Optional HTTP basic auth as in the jar.  Default host ``http://localhost:3000``.
+
+Series given as numpy arrays are encoded by the host extension
+(``_twtml_host.json_floats``, GIL released) and posted as a pre-built body:
+an append carries tens of thousands of numbers, and ``json.dumps`` of them
+holds the GIL long enough to stall the training thread's host work.
 """
 from __future__ import annotations
 
+import json
 from dataclasses import dataclass
-from typing import Any, Dict, List, Optional, Sequence
+from typing import Any, Dict, List, Optional, Sequence, Union
 
+import numpy as np
 import requests
 
 __all__ = ["Lightning", "Visualization", "LightningError"]
@@ -34,9 +41,9 @@ class Visualization:
     id: str
     type: str = "line-streaming"
 
-    def append(self, data: Dict[str, Any]) -> Dict[str, Any]:
-        return self.lgn._post(f"/sessions/{self.lgn.session}/visualizations/{self.id}/data/",
-                              {"data": data})
+    def append(self, data: Union[Dict[str, Any], bytes]) -> Dict[str, Any]:
+        body = b'{"data":' + data + b"}" if isinstance(data, bytes) else {"data": data}
+        return self.lgn._post(f"/sessions/{self.lgn.session}/visualizations/{self.id}/data/", body)
 
     def get_pym_link(self) -> str:
         return f"{self.lgn.host}/visualizations/{self.id}/pym"
@@ -54,9 +61,13 @@ class Lightning:
         self._http = requests.Session()
 
     # ------------------------------------------------------------------
-    def _post(self, path: str, payload: Dict[str, Any]) -> Dict[str, Any]:
+    def _post(self, path: str, payload: Union[Dict[str, Any], bytes]) -> Dict[str, Any]:
         try:
-            r = self._http.post(self.host + path, json=payload, auth=self.auth, timeout=self.timeout)
+            if isinstance(payload, bytes):   # pre-encoded JSON
+                r = self._http.post(self.host + path, data=payload, auth=self.auth, timeout=self.timeout,
+                                    headers={"Content-Type": "application/json"})
+            else:
+                r = self._http.post(self.host + path, json=payload, auth=self.auth, timeout=self.timeout)
         except requests.RequestException as e:
             raise LightningError(f"lightning unreachable at {self.host}: {e}") from e
         if r.status_code >= 400:
@@ -92,6 +103,21 @@ class Lightning:
                        color: Sequence[Sequence[float]] = (), alpha: Sequence[float] = (),
                        label: Sequence[int] = (), xaxis: str = "", yaxis: str = "",
                        viz: Optional[Visualization] = None):
+        if viz is not None and series and all(isinstance(x, np.ndarray) for x in series):
+            # the append fast path: native encoding of the numbers, GIL released
+            rest: Dict[str, Any] = {}
+            if xaxis:
+                rest["xaxis"] = xaxis
+            if yaxis:
+                rest["yaxis"] = yaxis
+            body = b'{"series":[' + b",".join(_json_floats(x) for x in series) + b"]"
+            for key, val in (("size", size), ("color", color), ("alpha", alpha), ("label", label)):
+                if len(val):
+                    body += b',"' + key.encode() + b'":' + json.dumps(np.asarray(val).tolist()).encode()
+            for key, val in rest.items():
+                body += b',"' + key.encode() + b'":' + json.dumps(val).encode()
+            viz.append(body + b"}")
+            return viz
         data: Dict[str, Any] = {"series": [list(map(float, s)) for s in series]}
         if size:
             data["size"] = list(size)
@@ -111,3 +137,13 @@ class Lightning:
         return viz
 
     lineStreaming = line_streaming
+
+
+def _json_floats(x: np.ndarray) -> bytes:
+    """JSON array of ``x`` as float64 (non-finite -> null)."""
+    x = np.ascontiguousarray(x, dtype=np.float64).ravel()
+    try:
+        from ..ops._native import NativeUnavailable, host
+        return host().json_floats(x)
+    except (ImportError, NativeUnavailable):
+        return json.dumps([v if np.isfinite(v) else None for v in x.tolist()]).encode()

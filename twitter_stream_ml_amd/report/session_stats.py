@@ -120,14 +120,15 @@ class SessionStats:
         else:
             job()
 
-    def _series(self, batch: int, real_sd: float, pred_sd: float, real, pred) -> List[List[float]]:
+    def _series(self, batch: int, real_sd: float, pred_sd: float, real, pred) -> List[np.ndarray]:
         real = np.asarray(real, dtype=np.float64)
         pred = np.asarray(pred, dtype=np.float64)
         if self.plot_points and real.shape[0] > self.plot_points:
             idx = np.linspace(0, real.shape[0] - 1, self.plot_points).astype(np.int64)
             real, pred = real[idx], pred[idx]
         n = real.shape[0]
-        return [real.tolist(), pred.tolist(), [real_sd] * n, [pred_sd] * n]
+        # numpy series: the Lightning client encodes them natively (GIL released)
+        return [real, pred, np.full(n, real_sd), np.full(n, pred_sd)]
 
     def _try(self, fn: Callable[[], object]) -> None:
         try:
