@@ -1,4 +1,5 @@
 // pybind11 bindings of the MI355X engine (_twtml_hip).
+#include <ctime>
 #include <hip/hip_runtime.h>
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
@@ -292,11 +293,19 @@ PYBIND11_MODULE(_twtml_hip, m) {
       .def("process",
            [](LREngine& e, int slot, int64_t now_ms, bool want_pred, int64_t plot_points) {
              BatchResult r;
+             int64_t done_ns = 0;
              {
                py::gil_scoped_release nogil;
                r = e.process(slot, now_ms, want_pred, plot_points);
+               timespec ts;
+               clock_gettime(CLOCK_MONOTONIC, &ts);
+               done_ns = int64_t(ts.tv_sec) * 1000000000 + ts.tv_nsec;
              }
-             return result_dict(r);
+             // done_ns (time.monotonic_ns clock): the engine's return, before
+             // this thread took the GIL back -- the GIL wait is the difference
+             auto d = result_dict(r);
+             d["done_ns"] = done_ns;
+             return d;
            },
            py::arg("slot"), py::arg("now_ms"), py::arg("want_pred") = false, py::arg("plot_points") = 0)
       .def_property_readonly("lazy_bytes", &LREngine::lazy_bytes,

@@ -293,6 +293,8 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
   TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_out_),
                                 (32 + size_t(std::max(1, cfg_.num_iterations))) * sizeof(double),
                                 hipHostMallocDefault));
+  TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&plot_host_), 2 * sizeof(float) * size_t(cfg_.max_rows),
+                                hipHostMallocDefault));
   TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_flags_),
                                 (2 + size_t(std::max(1, cfg_.num_iterations))) * sizeof(double),
                                 hipHostMallocMapped | hipHostMallocCoherent));
@@ -508,6 +510,7 @@ LREngine::~LREngine() {
                   lower_page_, lower_blocks_};
   for (void* b : bufs) if (b) (void)hipFree(b);
   if (host_out_) (void)hipHostFree(host_out_);
+  if (plot_host_) (void)hipHostFree(plot_host_);
   if (host_flags_) (void)hipHostFree(host_flags_);
   if (ready_host_) (void)hipHostFree(ready_host_);
   if (hnu_) (void)hipHostFree(hnu_);
@@ -912,22 +915,22 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred, int64_t plot_points) {
                                  hipMemcpyDeviceToHost, s));
   // the plot's (pred, real) pairs of this rank's kept rows: all of them, or
   // plot_points evenly spaced ones sampled on the device
-  std::vector<float> pairs;
+  // (pinned target: a pageable D2H is staged through the runtime's bounce
+  // buffers on the calling thread)
+  size_t P = 0;
   if (want_pred && res.n_kept > 0) {
-    const int64_t P = plot_points > 0 ? std::min<int64_t>(plot_points, res.n_kept) : res.n_kept;
-    launch_plot_sample(sgd_.pred_out, sgd_.real_out, res.n_kept, P, plot_buf_, s);
-    pairs.resize(2 * size_t(P));
-    TWTML_HIP_CHECK(hipMemcpyAsync(pairs.data(), plot_buf_, sizeof(float) * pairs.size(), hipMemcpyDeviceToHost, s));
+    P = size_t(plot_points > 0 ? std::min<int64_t>(plot_points, res.n_kept) : res.n_kept);
+    launch_plot_sample(sgd_.pred_out, sgd_.real_out, res.n_kept, int64_t(P), plot_buf_, s);
+    TWTML_HIP_CHECK(hipMemcpyAsync(plot_host_, plot_buf_, 2 * sizeof(float) * P, hipMemcpyDeviceToHost, s));
   }
   TWTML_HIP_CHECK(hipStreamSynchronize(s));
   if (comm_) comm_->check_async();
-  if (!pairs.empty()) {
-    const size_t P = pairs.size() / 2;
+  if (P > 0) {
     res.pred.resize(P);
     res.real.resize(P);
     for (size_t i = 0; i < P; ++i) {
-      res.pred[i] = pairs[2 * i];
-      res.real[i] = pairs[2 * i + 1];
+      res.pred[i] = plot_host_[2 * i];
+      res.real[i] = plot_host_[2 * i + 1];
     }
   }
   for (int k = 0; k < 6; ++k) res.stats[k] = host_out_[k];

@@ -312,6 +312,7 @@ class LREngine {
   uint8_t* lower_page_ = nullptr;
   uint16_t* lower_blocks_ = nullptr;
   double* host_out_ = nullptr;        // pinned [16 + iters]
+  float* plot_host_ = nullptr;        // pinned [2 max_rows]: the plot sample's D2H target
   double* host_flags_ = nullptr;      // pinned [iters + 1] convergence flag per iteration
   std::vector<hipEvent_t> iter_events_;
   hipEvent_t ev_[4] = {nullptr, nullptr, nullptr, nullptr};

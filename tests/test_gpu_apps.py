@@ -121,9 +121,12 @@ def test_lr_driver_plot_does_not_stall_training(hip_module, tmp_path, monkeypatc
     def p99(path, lightning):
         monkeypatch.setenv("TWTML_METRICS", str(path))
         assert app.main(base + ["--lightning", lightning]) == 0
-        steps = [r["step_ms"] for r in (json.loads(l) for l in open(path)) if "step_ms" in r]
-        assert len(steps) == 40
-        return float(np.percentile(steps[8:], 99))   # after warm-up
+        recs = [r for r in (json.loads(l) for l in open(path)) if "step_ms" in r]
+        assert len(recs) == 40
+        for k in ("step_ms", "call_ms", "gil_wait_ms"):
+            v = [r[k] for r in recs[8:]]
+            print(f"{lightning} {k}: p50 {np.percentile(v, 50):.3f} p99 {np.percentile(v, 99):.3f} max {max(v):.3f}")
+        return float(np.percentile([r["step_ms"] for r in recs[8:]], 99))   # after warm-up
 
     off = p99(tmp_path / "off.jsonl", "http://127.0.0.1:9")   # unreachable: plotting disabled
     lgn = FakeLightningProcess().start()   # its JSON parsing off this process's GIL

@@ -33,6 +33,7 @@ from ..parallel.dist import barrier, check_replicas
 from ..runtime.streaming import StreamingContext
 from ..sources import make_source
 from ..utils.faults import maybe_inject
+from ..utils.gil import short_gil_slices
 from ..utils.logging import setup_logging
 from ._common import (ResumeState, StreamCheckpointer, exit_on_sigterm, load_resume_state,
                       make_watchdog)
@@ -217,7 +218,8 @@ def main(argv: Optional[List[str]] = None) -> int:
     ssc.start()
     failed = False
     try:
-        ssc.awaitTermination()
+        with short_gil_slices():   # background report threads never hold the training thread up long
+            ssc.awaitTermination()
     except KeyboardInterrupt:
         pass
     except BaseException:

@@ -45,6 +45,7 @@ from ..checkpoint.saveable import SparseWeights
 from ._common import (ResumeState, StreamCheckpointer, exit_on_sigterm, load_resume_state,
                       make_watchdog)
 from ..oracle.mllib import round_half_up
+from ..utils.gil import short_gil_slices
 from ..report.session_stats import SessionStats
 from ..runtime.streaming import StreamingContext
 from ..sources import make_source
@@ -150,6 +151,10 @@ class LinearRegressionJob:
         t0 = self._t0 = time.perf_counter()
         res = self.engine.train_batch(raw, want_pred=self.plot, plot_points=self.plot_points)  # op #1, op #2
         t1 = time.perf_counter()
+        # the engine call on this thread, and the part of it spent waiting to
+        # take the GIL back after the device work (other Python threads)
+        self._call_ms = (t1 - t0) * 1e3
+        self._gil_ms = (time.monotonic_ns() - res["done_ns"]) / 1e6 if "done_ns" in res else None
         if self.t_first is None:
             self.t_first = t0
         self.t_last = t1
@@ -219,7 +224,9 @@ class LinearRegressionJob:
                          iterations=res["iterations"], converged=bool(res["converged"]),
                          diverged=bool(res.get("diverged", False)),
                          prep_ms=res.get("prep_ms", 0.0), train_ms=res.get("train_ms", 0.0),
-                         step_ms=round((time.perf_counter() - self._t0) * 1e3, 3))
+                         step_ms=round((time.perf_counter() - self._t0) * 1e3, 3),
+                         call_ms=round(self._call_ms, 3),
+                         **({} if self._gil_ms is None else {"gil_wait_ms": round(self._gil_ms, 3)}))
 
     def summary(self) -> dict:
         """Throughput of the run: trained tweets (all ranks) over the wall
@@ -329,7 +336,8 @@ def main(argv: Optional[List[str]] = None) -> int:
     log.info("Initialization complete.")
     failed = False
     try:
-        ssc.awaitTermination()
+        with short_gil_slices():   # background report threads never hold the training thread up long
+            ssc.awaitTermination()
     except KeyboardInterrupt:
         pass
     except BaseException:
