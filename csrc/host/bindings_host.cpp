@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "featurize_cpu.h"
+#include "http_post.h"
 #include "synth.h"
 #include "unicode_lower.h"
 #include "wire.h"
@@ -138,6 +139,19 @@ PYBIND11_MODULE(_twtml_host, m) {
   // Python's repr; non-finite values as null), built with the GIL released:
   // the Lightning plot's series are tens of thousands of numbers per append,
   // and json.dumps holds the GIL for milliseconds (report/lightning.py).
+  // report/http.py: a whole POST with the GIL released (http_post.cpp)
+  py::register_exception<HttpError>(m, "HttpError", PyExc_ConnectionError);
+  m.def("http_post", [](const std::string& host, int port, const std::string& path, const py::bytes& body,
+                        const std::string& headers, double timeout_s) {
+    std::string b = body;
+    HttpResponse r;
+    {
+      py::gil_scoped_release nogil;
+      r = http_post(host, port, path, b, headers, timeout_s);
+    }
+    return py::make_tuple(r.status, py::bytes(r.body));
+  }, py::arg("host"), py::arg("port"), py::arg("path"), py::arg("body"), py::arg("headers") = "",
+     py::arg("timeout") = 5.0);
   m.def("json_floats", [](Arr<double> v) {
     std::string out;
     {

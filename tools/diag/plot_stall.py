@@ -10,7 +10,9 @@ training thread), ``call_ms`` (the engine call) and ``gil_wait_ms`` (the part
 of the call after the engine returned, spent taking the GIL back).
 """
 import argparse
+import functools
 import json
+import time
 import os
 import sys
 import tempfile
@@ -32,9 +34,32 @@ def main() -> None:
             "--seconds", "0", "--batchSize", "1000000", "--sourceRate", "0", "--numBatches", str(a.batches),
             "-f", "1000000"]
     default_si = sys.getswitchinterval()
+    # timelines: the training thread's batches, the report threads' calls
+    from twitter_stream_ml_amd.report import http as rhttp, lightning as lgm, session_stats as ssm
+    ev = []
+
+    def wrap(obj, name, tag=None):
+        fn = getattr(obj, name)
+
+        @functools.wraps(fn)
+        def w(*x, **k):
+            t0 = time.perf_counter()
+            try:
+                return fn(*x, **k)
+            finally:
+                ev.append((tag or name, t0, time.perf_counter()))
+        setattr(obj, name, w)
+    wrap(app.LinearRegressionJob, "on_batch", "BATCH")
+    wrap(lgm, "_json_floats")
+    wrap(ssm.SessionStats, "_series")
+    wrap(rhttp, "post", "http_post")
+    lgm.http_post = rhttp.post
+    from twitter_stream_ml_amd.report import webclient as wcm
+    wcm.http_post = rhttp.post
 
     def run(tag, lightning, si_us):
         sys.setswitchinterval(si_us / 1e6 if si_us > 0 else default_si)
+        ev.clear()
         path = os.path.join(tempfile.mkdtemp(), "m.jsonl")
         os.environ["TWTML_METRICS"] = path
         assert app.main(base + ["--lightning", lightning]) == 0
@@ -46,6 +71,14 @@ def main() -> None:
             out[k] = {"p50": round(float(np.nanpercentile(v, 50)), 3), "p90": round(float(np.nanpercentile(v, 90)), 3),
                       "p99": round(float(np.nanpercentile(v, 99)), 3), "max": round(float(np.nanmax(v)), 3)}
         print(json.dumps(out), flush=True)
+        # the slow batches after warm-up, with the report calls overlapping them
+        bt = [e for e in ev if e[0] == "BATCH"][8:]
+        med = float(np.median([b - a for _, a, b in bt]))
+        for _, a, b in bt:
+            if b - a > 1.5 * med:
+                ov = [(n, round((x - a) * 1e3, 2), round((y - x) * 1e3, 2)) for n, x, y in ev
+                      if n != "BATCH" and x < b and y > a]
+                print(f"  slow batch {(b - a) * 1e3:.2f} ms (median {med * 1e3:.2f}): {ov}", flush=True)
 
     sis = [int(x) for x in a.switch_us.split(",")]
     run("off", "http://127.0.0.1:9", sis[0])

@@ -28,6 +28,8 @@ from typing import Any, Dict, List, Optional, Sequence, Union
 import numpy as np
 import requests
 
+from .http import post as http_post
+
 __all__ = ["Lightning", "Visualization", "LightningError"]
 
 
@@ -62,18 +64,16 @@ class Lightning:
 
     # ------------------------------------------------------------------
     def _post(self, path: str, payload: Union[Dict[str, Any], bytes]) -> Dict[str, Any]:
+        body = payload if isinstance(payload, bytes) else json.dumps(payload).encode()   # bytes: pre-encoded
         try:
-            if isinstance(payload, bytes):   # pre-encoded JSON
-                r = self._http.post(self.host + path, data=payload, auth=self.auth, timeout=self.timeout,
-                                    headers={"Content-Type": "application/json"})
-            else:
-                r = self._http.post(self.host + path, json=payload, auth=self.auth, timeout=self.timeout)
+            status, content = http_post(self.host + path, body, auth=self.auth, timeout=self.timeout,
+                                        session=self._http)
         except requests.RequestException as e:
             raise LightningError(f"lightning unreachable at {self.host}: {e}") from e
-        if r.status_code >= 400:
-            raise LightningError(f"lightning {path}: HTTP {r.status_code} {r.text[:200]}")
+        if status >= 400:
+            raise LightningError(f"lightning {path}: HTTP {status} {content[:200].decode('utf-8', 'replace')}")
         try:
-            return r.json()
+            return json.loads(content) if content else {}
         except ValueError:
             return {}
 

@@ -13,6 +13,7 @@ from typing import List, Optional
 
 import requests
 
+from .http import post as http_post
 from .api_types import Config, Stats, TypeData, parse_type_data
 
 __all__ = ["WebClient"]
@@ -35,15 +36,16 @@ class WebClient:
         return self.server + "/api" + kind
 
     def post(self, data: TypeData) -> str:
-        r = self._session.post(self._url(), data=data.to_json().encode("utf-8"), headers=_HEADERS,
-                               timeout=self.timeout)
-        r.raise_for_status()
-        return r.text
+        status, content = http_post(self._url(), data.to_json().encode("utf-8"), timeout=self.timeout,
+                                    session=self._session)
+        if status >= 400:
+            raise requests.HTTPError(f"{status} posting to {self._url()}")
+        return content.decode("utf-8", "replace")
 
     def get(self, kind: str) -> TypeData:
         r = self._session.get(self._url(kind), headers=_HEADERS, timeout=self.timeout)
         r.raise_for_status()
-        return parse_type_data(r.text)
+        return parse_type_data(_text(r))
 
     # -- the reference's four calls (WebClient.scala:31-46) ----------------
     def config(self, id: Optional[str] = None, host: Optional[str] = None,
@@ -60,3 +62,11 @@ class WebClient:
 
     def close(self) -> None:
         self._session.close()
+
+
+def _text(r: "requests.Response") -> str:
+    # UTF-8 JSON: decoded directly; ``Response.text`` guesses an encoding
+    # when the server names none, and its first use imports a charset
+    # detector on the reporting thread while the training thread waits on
+    # the GIL
+    return r.content.decode("utf-8", "replace")
