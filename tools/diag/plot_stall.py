@@ -27,6 +27,7 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--batches", type=int, default=40)
     ap.add_argument("--switch-us", default="0")
+    ap.add_argument("--fresh-server", action="store_true", help="a new fake Lightning process per plot-on run")
     a = ap.parse_args()
     from fakes import FakeLightningProcess
     from twitter_stream_ml_amd.apps import linear_regression as app
@@ -50,6 +51,15 @@ def main() -> None:
                 ev.append((tag or name, t0, time.perf_counter()))
         setattr(obj, name, w)
     wrap(app.LinearRegressionJob, "on_batch", "BATCH")
+    import gc
+    gc_t0 = {}
+
+    def gc_cb(phase, info):
+        if phase == "start":
+            gc_t0[info["generation"]] = time.perf_counter()
+        elif info["generation"] in gc_t0:
+            ev.append((f"gc{info['generation']}", gc_t0.pop(info["generation"]), time.perf_counter()))
+    gc.callbacks.append(gc_cb)
     wrap(lgm, "_json_floats")
     wrap(ssm.SessionStats, "_series")
     wrap(rhttp, "post", "http_post")
@@ -64,18 +74,25 @@ def main() -> None:
         os.environ["TWTML_METRICS"] = path
         assert app.main(base + ["--lightning", lightning]) == 0
         recs = [json.loads(l) for l in open(path)]
-        recs = [r for r in recs if "step_ms" in r][8:]
+        recs = [r for r in recs if "step_ms" in r]
+        allrecs = recs
+        recs = recs[8:]
         out = {"run": tag, "switch_us": si_us or default_si * 1e6}
         for k in ("step_ms", "call_ms", "gil_wait_ms", "train_ms"):
             v = np.array([r.get(k, np.nan) for r in recs], float)
             out[k] = {"p50": round(float(np.nanpercentile(v, 50)), 3), "p90": round(float(np.nanpercentile(v, 90)), 3),
                       "p99": round(float(np.nanpercentile(v, 99)), 3), "max": round(float(np.nanmax(v)), 3)}
+        gcs = [(n, (y - x) * 1e3) for n, x, y in ev if n.startswith("gc")]
+        out["gc"] = {g: [sum(1 for n, _ in gcs if n == g), round(max([d for n, d in gcs if n == g] or [0]), 3)]
+                     for g in ("gc0", "gc1", "gc2")}
         print(json.dumps(out), flush=True)
         # the slow batches after warm-up, with the report calls overlapping them
-        bt = [e for e in ev if e[0] == "BATCH"][8:]
-        med = float(np.median([b - a for _, a, b in bt]))
-        for _, a, b in bt:
-            if b - a > 1.5 * med:
+        bt = [e for e in ev if e[0] == "BATCH"]
+        med = float(np.median([b - a for _, a, b in bt[8:]]))
+        for i, (_, a, b) in enumerate(bt):
+            if i >= 8 and b - a > 1.5 * med:
+                n_app = sum(1 for n, x, y in ev if n == "http_post" and y < a)
+                print(f"  batch {i}: {n_app} posts done before it; metrics {allrecs[i] if i < len(allrecs) else None}")
                 ov = [(n, round((x - a) * 1e3, 2), round((y - x) * 1e3, 2)) for n, x, y in ev
                       if n != "BATCH" and x < b and y > a]
                 print(f"  slow batch {(b - a) * 1e3:.2f} ms (median {med * 1e3:.2f}): {ov}", flush=True)
@@ -85,6 +102,9 @@ def main() -> None:
     lgn = FakeLightningProcess().start()
     try:
         for si in sis:
+            if a.fresh_server:
+                lgn.stop()
+                lgn = FakeLightningProcess().start()
             run("on", lgn.url, si)
         print(json.dumps({"lightning": lgn.summary()}), flush=True)
     finally:

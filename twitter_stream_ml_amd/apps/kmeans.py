@@ -33,7 +33,7 @@ from ..parallel.dist import barrier, check_replicas
 from ..runtime.streaming import StreamingContext
 from ..sources import make_source
 from ..utils.faults import maybe_inject
-from ..utils.gil import short_gil_slices
+from ..utils.gil import streaming_latency
 from ..utils.logging import setup_logging
 from ._common import (ResumeState, StreamCheckpointer, exit_on_sigterm, load_resume_state,
                       make_watchdog)
@@ -218,7 +218,7 @@ def main(argv: Optional[List[str]] = None) -> int:
     ssc.start()
     failed = False
     try:
-        with short_gil_slices():   # background report threads never hold the training thread up long
+        with streaming_latency():   # background threads never hold the training thread up long (GIL, GC)
             ssc.awaitTermination()
     except KeyboardInterrupt:
         pass

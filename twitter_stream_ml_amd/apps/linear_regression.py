@@ -45,7 +45,7 @@ from ..checkpoint.saveable import SparseWeights
 from ._common import (ResumeState, StreamCheckpointer, exit_on_sigterm, load_resume_state,
                       make_watchdog)
 from ..oracle.mllib import round_half_up
-from ..utils.gil import short_gil_slices
+from ..utils.gil import streaming_latency
 from ..report.session_stats import SessionStats
 from ..runtime.streaming import StreamingContext
 from ..sources import make_source
@@ -336,7 +336,7 @@ def main(argv: Optional[List[str]] = None) -> int:
     log.info("Initialization complete.")
     failed = False
     try:
-        with short_gil_slices():   # background report threads never hold the training thread up long
+        with streaming_latency():   # background threads never hold the training thread up long (GIL, GC)
             ssc.awaitTermination()
     except KeyboardInterrupt:
         pass
