@@ -215,11 +215,14 @@ def main(argv: Optional[List[str]] = None) -> int:
     if hasattr(engine, "prefetch"):   # device engine: H2D of queued batches overlaps training
         ssc.add_prefetch(engine.prefetch)
     log.info("Initialization complete.")
+    # from here background threads never hold the training thread up long
+    # (GIL slices, a frozen GC heap): entered before the first batch
+    latency = streaming_latency()
+    latency.__enter__()
     ssc.start()
     failed = False
     try:
-        with streaming_latency():   # background threads never hold the training thread up long (GIL, GC)
-            ssc.awaitTermination()
+        ssc.awaitTermination()
     except KeyboardInterrupt:
         pass
     except BaseException:
@@ -227,6 +230,7 @@ def main(argv: Optional[List[str]] = None) -> int:
         raise
     finally:
         ssc.stop()
+        latency.__exit__(None, None, None)
         if not failed:
             job.final_checkpoint()
         job.close()

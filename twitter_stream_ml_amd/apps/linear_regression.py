@@ -332,12 +332,15 @@ def main(argv: Optional[List[str]] = None) -> int:
     stream.foreachRDD(job.on_batch)   # op #1 (stats) + op #2 (trainOn), prequential order
     if hasattr(engine, "prefetch"):   # device engine: H2D of queued batches overlaps training
         ssc.add_prefetch(engine.prefetch)
+    # from here background threads never hold the training thread up long
+    # (GIL slices, a frozen GC heap): entered before the first batch
+    latency = streaming_latency()
+    latency.__enter__()
     ssc.start()
     log.info("Initialization complete.")
     failed = False
     try:
-        with streaming_latency():   # background threads never hold the training thread up long (GIL, GC)
-            ssc.awaitTermination()
+        ssc.awaitTermination()
     except KeyboardInterrupt:
         pass
     except BaseException:
@@ -345,6 +348,7 @@ def main(argv: Optional[List[str]] = None) -> int:
         raise
     finally:
         ssc.stop()
+        latency.__exit__(None, None, None)
         if not failed:
             job.final_checkpoint()
             if rank == 0:
