@@ -59,9 +59,11 @@ def test_real_process_affinity_untouched_without_gpu():
     assert os.sched_getaffinity(0) == before
 
 
-def test_share_host_threads_divides_the_node(monkeypatch):
+def test_share_host_threads_divides_the_node(monkeypatch, tmp_path):
     """8 ranks on 2 NUMA nodes (4 GPUs each): a rank gets its node's CPUs / 4."""
-    from twitter_stream_ml_amd.parallel.affinity import share_host_threads
+    from functools import partial
+    from twitter_stream_ml_amd.parallel import affinity
+    share_host_threads = partial(affinity.share_host_threads, cgroup=str(tmp_path))   # no quota
     monkeypatch.delenv("TWTML_HOST_THREADS", raising=False)
     nodes = {d: 0 if d < 4 else 1 for d in range(8)}
     monkeypatch.setattr("twitter_stream_ml_amd.parallel.affinity.gpu_numa_node",
@@ -86,3 +88,24 @@ def test_native_generator_uses_host_threads(monkeypatch):
     monkeypatch.setenv("TWTML_HOST_THREADS", "5")
     b = generate_batch(SynthConfig.profile("bench", seed=3), 0, 20000, batch_time_ms=0)
     np.testing.assert_array_equal(a.text, b.text)   # thread count never changes the data
+
+
+def test_cgroup_quota_caps_host_threads(monkeypatch, tmp_path):
+    """A 256-CPU affinity mask in a 16-CPU cgroup (the MI355X boxes): 16
+    threads for one rank, 2 each for 8 ranks; v1 files too; no limit -> 0."""
+    from twitter_stream_ml_amd.parallel.affinity import cgroup_cpu_limit, share_host_threads
+    (tmp_path / "cpu.max").write_text("1600000 100000\n")
+    assert cgroup_cpu_limit(str(tmp_path)) == 16
+    wide = lambda pid: set(range(256))   # noqa: E731
+    monkeypatch.delenv("TWTML_HOST_THREADS", raising=False)
+    assert share_host_threads(0, 0, 1, 1, pci_bus_id=str, getaffinity=wide, cgroup=str(tmp_path)) == 16
+    monkeypatch.delenv("TWTML_HOST_THREADS")
+    assert share_host_threads(0, 3, 8, 1, pci_bus_id=str, getaffinity=wide, cgroup=str(tmp_path)) == 2
+    (tmp_path / "cpu.max").write_text("max 100000\n")
+    assert cgroup_cpu_limit(str(tmp_path)) == 0
+    v1 = tmp_path / "v1"
+    (v1 / "cpu").mkdir(parents=True)
+    (v1 / "cpu" / "cpu.cfs_quota_us").write_text("250000\n")
+    (v1 / "cpu" / "cpu.cfs_period_us").write_text("100000\n")
+    assert cgroup_cpu_limit(str(v1)) == 3
+    assert cgroup_cpu_limit(str(tmp_path / "none")) == 0

@@ -35,6 +35,12 @@ def main() -> None:
             "--seconds", "0", "--batchSize", "1000000", "--sourceRate", "0", "--numBatches", str(a.batches),
             "-f", "1000000"]
     default_si = sys.getswitchinterval()
+
+    def cpu_stat():
+        try:
+            return {k: int(v) for k, v in (l.split() for l in open("/sys/fs/cgroup/cpu.stat"))}
+        except OSError:
+            return {}
     # timelines: the training thread's batches, the report threads' calls
     from twitter_stream_ml_amd.report import http as rhttp, lightning as lgm, session_stats as ssm
     ev = []
@@ -51,6 +57,18 @@ def main() -> None:
                 ev.append((tag or name, t0, time.perf_counter()))
         setattr(obj, name, w)
     wrap(app.LinearRegressionJob, "on_batch", "BATCH")
+    win = []   # cgroup cpu.stat at the start of batch 8 and after the last batch
+    ob = app.LinearRegressionJob.on_batch
+
+    def on_batch(self, *x, **k):
+        if self.batches == 8:
+            win.append(cpu_stat())
+        try:
+            return ob(self, *x, **k)
+        finally:
+            if self.batches == a.batches:
+                win.append(cpu_stat())
+    app.LinearRegressionJob.on_batch = on_batch
     import gc
     gc_t0 = {}
 
@@ -63,6 +81,22 @@ def main() -> None:
     wrap(lgm, "_json_floats")
     wrap(ssm.SessionStats, "_series")
     wrap(rhttp, "post", "http_post")
+    # the training thread's own phases, and the receiver's seals
+    from twitter_stream_ml_amd.ops import ingest, lr_engine
+    from twitter_stream_ml_amd.runtime import streaming
+    take0 = ingest.SlotPipeline.take
+
+    def take(self, raw):
+        hit = id(raw) in self._inflight
+        t0 = time.perf_counter()
+        try:
+            return take0(self, raw)
+        finally:
+            ev.append(("take_hit" if hit else "take_MISS", t0, time.perf_counter()))
+    ingest.SlotPipeline.take = take
+    wrap(ingest.SlotPipeline, "prefetch")
+    wrap(lr_engine.DeviceLinearRegression, "process")
+    wrap(streaming.StreamingContext, "_seal")
     lgm.http_post = rhttp.post
     from twitter_stream_ml_amd.report import webclient as wcm
     wcm.http_post = rhttp.post
@@ -70,14 +104,24 @@ def main() -> None:
     def run(tag, lightning, si_us):
         sys.setswitchinterval(si_us / 1e6 if si_us > 0 else default_si)
         ev.clear()
+        win.clear()
+        import resource
+        st0, ru0, w0 = cpu_stat(), resource.getrusage(resource.RUSAGE_SELF), time.perf_counter()
         path = os.path.join(tempfile.mkdtemp(), "m.jsonl")
         os.environ["TWTML_METRICS"] = path
         assert app.main(base + ["--lightning", lightning]) == 0
+        st1, ru1, w1 = cpu_stat(), resource.getrusage(resource.RUSAGE_SELF), time.perf_counter()
+        cpu = {k: st1[k] - st0.get(k, 0) for k in st1 if k in ("nr_periods", "nr_throttled", "throttled_usec", "usage_usec")}
+        cpu["proc_cpu_s"] = round(ru1.ru_utime + ru1.ru_stime - ru0.ru_utime - ru0.ru_stime, 3)
+        cpu["wall_s"] = round(w1 - w0, 3)
+        if len(win) == 2:   # the streaming window (batches 8..end)
+            cpu["window"] = {k: win[1][k] - win[0].get(k, 0) for k in win[1]
+                             if k in ("nr_periods", "nr_throttled", "throttled_usec", "usage_usec")}
         recs = [json.loads(l) for l in open(path)]
         recs = [r for r in recs if "step_ms" in r]
         allrecs = recs
         recs = recs[8:]
-        out = {"run": tag, "switch_us": si_us or default_si * 1e6}
+        out = {"run": tag, "switch_us": si_us or default_si * 1e6, "cgroup_cpu": cpu}
         for k in ("step_ms", "call_ms", "gil_wait_ms", "train_ms"):
             v = np.array([r.get(k, np.nan) for r in recs], float)
             out[k] = {"p50": round(float(np.nanpercentile(v, 50)), 3), "p90": round(float(np.nanpercentile(v, 90)), 3),

@@ -18,9 +18,10 @@ from __future__ import annotations
 import os
 from typing import Callable, Optional, Set
 
-__all__ = ["parse_cpulist", "gpu_numa_node", "bind_local_numa", "share_host_threads"]
+__all__ = ["parse_cpulist", "gpu_numa_node", "bind_local_numa", "share_host_threads", "cgroup_cpu_limit"]
 
 SYSFS = "/sys"
+CGROUP = "/sys/fs/cgroup"
 
 
 def parse_cpulist(text: str) -> Set[int]:
@@ -44,6 +45,28 @@ def _read(path: str) -> Optional[str]:
             return f.read()
     except OSError:
         return None
+
+
+def cgroup_cpu_limit(root: str = CGROUP) -> int:
+    """CPUs the cgroup's CFS quota allows (v2 ``cpu.max``, else v1
+    ``cpu.cfs_quota_us`` / ``cpu.cfs_period_us``), rounded up; 0 = no limit.
+    Mirrors ``csrc/common/host_threads.h``: a container may see 256 CPUs in
+    its affinity mask and be allowed 16, and threads past the quota get the
+    whole cgroup throttled for the rest of a 100 ms period."""
+    quota = period = 0
+    txt = _read(os.path.join(root, "cpu.max"))
+    if txt is not None:
+        parts = txt.split()
+        if len(parts) == 2 and parts[0] != "max":
+            quota, period = int(parts[0]), int(parts[1])
+    else:
+        q = _read(os.path.join(root, "cpu", "cpu.cfs_quota_us"))
+        p = _read(os.path.join(root, "cpu", "cpu.cfs_period_us"))
+        if q is not None and p is not None:
+            quota, period = int(q.strip()), int(p.strip())
+    if quota <= 0 or period <= 0:
+        return 0
+    return max(1, -(-quota // period))
 
 
 def gpu_numa_node(pci_bus_id: str, sysfs: str = SYSFS) -> Optional[int]:
@@ -88,9 +111,11 @@ def bind_local_numa(device: int, pci_bus_id: Optional[Callable[[int], str]] = No
 
 def share_host_threads(device: int, local_rank: int, local_world: int, n_devices: int,
                        pci_bus_id: Optional[Callable[[int], str]] = None, sysfs: str = SYSFS,
-                       getaffinity: Callable[[int], Set[int]] = os.sched_getaffinity) -> int:
+                       getaffinity: Callable[[int], Set[int]] = os.sched_getaffinity,
+                       cgroup: str = CGROUP) -> int:
     """Host worker threads for this rank: the CPUs it may run on divided by
-    the local ranks that share them, exported as ``TWTML_HOST_THREADS`` for
+    the local ranks that share them, and at most its share of the cgroup CPU
+    quota (all local ranks share one), exported as ``TWTML_HOST_THREADS`` for
     the native runtime (``csrc/common/host_threads.h``: the synthetic
     generator, the CPU featurizer, the wire packer and the staging pool).
     Local rank r drives device ``r % n_devices``; ranks whose devices sit on
@@ -119,5 +144,8 @@ def share_host_threads(device: int, local_rank: int, local_world: int, n_devices
             if all(x is not None for x in nodes):
                 sharing = max(1, sum(1 for x in nodes if x == mine))
     n = max(1, cpus // sharing)
+    quota = cgroup_cpu_limit(cgroup)
+    if quota > 0:
+        n = max(1, min(n, quota // max(1, int(local_world))))
     os.environ["TWTML_HOST_THREADS"] = str(n)
     return n
