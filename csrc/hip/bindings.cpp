@@ -60,6 +60,9 @@ static py::dict result_dict(BatchResult& r) {
   d["train_ms"] = r.train_ms;
   d["comm_iters"] = r.comm_iters;
   d["comm_ms"] = r.comm_ms;
+  d["wait_ms"] = r.wait_ms;
+  d["train_wall_ms"] = r.train_wall_ms;
+  d["prepared_ahead"] = r.prepared_ahead;
   if (!r.real.empty()) {
     auto* v = new std::vector<float>(std::move(r.real));
     py::capsule own(v, [](void* p) { delete static_cast<std::vector<float>*>(p); });

@@ -289,7 +289,13 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
   sgd_.world = world_;
   sgd_.rank = comm_ ? comm_->rank() : 0;
   sgd_.tail_len = sgd_tail_len(world_);
-  ensure_compact(4096);
+  // Compact weights / packed gradients sized for the largest active set the
+  // configuration allows (ids the hash can produce, at most one per unit of
+  // a full batch; capped at 16M slots = 448 MB): growing them later means a
+  // stream sync + hipFree on the training thread -- a ~10 ms stall of the
+  // batch that first exceeds the capacity, measured mid-stream
+  // (tools/diag/plot_stall.py).  Larger active sets still grow on demand.
+  ensure_compact((kNumNumeric + active_set_hint() + kPadSlots + 63) / 64 * 64);
   TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_out_),
                                 (32 + size_t(std::max(1, cfg_.num_iterations))) * sizeof(double),
                                 hipHostMallocDefault));
@@ -429,10 +435,13 @@ void LREngine::ensure_tier(PrepBuf& b, int64_t n_unique, hipStream_t s) {
     p.tparam = dmalloc<int64_t>(4);
   }
   if (n_unique <= p.cap_tier) return;
+  // first sized for the configuration's largest active set (see the
+  // constructor): a regrowth syncs and frees on the prep thread, and hipFree
+  // waits for the whole device -- the batch training meanwhile stalls
   TWTML_HIP_CHECK(hipStreamSynchronize(s));
   void* old[] = {p.newslot, p.slot_fid, p.tscan, p.tscan_blk, p.fhist, p.fcur};
   for (void* x : old) if (x) (void)hipFree(x);
-  const int64_t cap = std::max<int64_t>(n_unique, p.cap_tier * 2);
+  const int64_t cap = std::max({n_unique, p.cap_tier * 2, p.cap_tier == 0 ? active_set_hint() : int64_t(0)});
   p.cap_tier = cap;
   p.newslot = dmalloc<int32_t>(size_t(cap));
   p.slot_fid = dmalloc<int32_t>(size_t(cap) + kNumNumeric + 2 * kPadSlots);
@@ -449,6 +458,15 @@ void LREngine::ensure_tier(PrepBuf& b, int64_t n_unique, hipStream_t s) {
     // histogram pass that follows on `s`
     TWTML_HIP_CHECK(hipMemsetAsync(p.slot_hist, 0, sizeof(uint32_t) * size_t(b.slot_hist_cap), s));
   }
+}
+
+// Upper bound of a batch's active set (text slots) under the configuration:
+// the ids the hash can produce (Java-hash bigrams < 2^21), at most one per
+// text unit of a full batch, capped at 16M.
+int64_t LREngine::active_set_hint() const {
+  const int64_t F = cfg_.num_text_features;
+  const int64_t ids = cfg_.hash_kind == 0 ? std::min<int64_t>(F, int64_t(1) << 21) : F;
+  return std::max<int64_t>(1, std::min({ids, cfg_.max_units + 64, int64_t(1) << 24}));
 }
 
 void LREngine::ensure_part(int64_t n) {
@@ -1048,11 +1066,14 @@ void LREngine::schedule_ahead_locked() {
 BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred, int64_t plot_points) {
   TraceRange tr_batch("twtml.lr.batch");
   TWTML_HIP_CHECK(hipSetDevice(device_));
+  const auto t_in = std::chrono::steady_clock::now();
   int k = -1;
+  bool ahead = false;
   {
     std::unique_lock<std::mutex> lk(mu_);
     for (int i = 0; i < 2; ++i)
       if (pb_[i].state != 0 && pb_[i].slot == slot) k = i;
+    ahead = k >= 0;
     if (k >= 0 && dp_) {
       // DP: the packets were all-gathered during the previous batch, or are
       // now, in line -- the same choice on every rank (it follows the
@@ -1158,8 +1179,12 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred, int64_t 
     schedule_ahead_locked();   // batch t+1's prep overlaps batch t's training
   }
   BatchResult res;
+  const auto t_train = std::chrono::steady_clock::now();
   try {
     res = train(pb_[k], want_pred, plot_points);
+    res.prepared_ahead = ahead;
+    res.wait_ms = std::chrono::duration<float, std::milli>(t_train - t_in).count();
+    res.train_wall_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t_train).count();
   } catch (...) {
     std::lock_guard<std::mutex> lk(mu_);
     pb_[k].state = 0;

@@ -140,6 +140,10 @@ struct BatchResult {
   float prep_ms = 0.f, train_ms = 0.f;
   int32_t comm_iters = 0;   // DP: gradient all-reduces issued (one per GD iteration)
   float comm_ms = 0.f;      // DP + comm_timing: their summed time on the compute stream
+  // host side of process(): waiting for / doing this batch's preparation, and
+  // train() end to end (enqueue, early-exit polling, the result copies)
+  float wait_ms = 0.f, train_wall_ms = 0.f;
+  bool prepared_ahead = false;   // the batch was prepared on the prep thread ahead of process()
 };
 
 // One prepared micro-batch: filtered, featurized, compacted and laid out for
@@ -209,12 +213,15 @@ class LREngine {
   void get_weights(double* w, int64_t n) const;
   int64_t num_weights() const { return cfg_.num_text_features + kNumNumeric; }
   // Device bytes allocated on demand: by the first tiered batch (per prepared
-  // buffer: the entry-sized far lists and CSC; the trainer's residual row
+  // buffer: the entry-sized far lists and CSC, the slot-sized tier arrays; the trainer's residual row
   // buffer) and by the first checkpoint snapshot ((index, value) pairs for
   // every weight): ops/sizing.py adds them to the construction footprint.
   int64_t lazy_bytes() const {
     const int nbuf = overlap_ ? 2 : 1;
+    // + the slot-sized tier arrays (newslot, slot_fid, tscan, fhist, fcur,
+    // slot_hist: 36 B per slot of active_set_hint())
     return int64_t(nbuf) * 3 * int64_t(sizeof(uint32_t)) * pb_[0].dp.cap_entries +
+           (pb_[0].dp.cap_tier ? 0 : int64_t(nbuf) * 36 * active_set_hint()) +
            int64_t(sizeof(float)) * pb_[0].dp.cap_rows16 +
            (snap_idx_ ? 0 : num_weights() * int64_t(sizeof(int32_t) + sizeof(double)));
   }
@@ -249,6 +256,7 @@ class LREngine {
   void free_prepared(PrepBuf& b);
   void ensure_compact(int64_t ns);
   void ensure_part(int64_t n);
+  int64_t active_set_hint() const;
   void ensure_tier(PrepBuf& b, int64_t n_unique, hipStream_t s);
   void prepare_local(PrepBuf& b, int slot, int64_t now_ms, hipStream_t s);
   void prepare_global(PrepBuf& b, hipStream_t s);

@@ -226,6 +226,9 @@ class LinearRegressionJob:
                          prep_ms=res.get("prep_ms", 0.0), train_ms=res.get("train_ms", 0.0),
                          step_ms=round((time.perf_counter() - self._t0) * 1e3, 3),
                          call_ms=round(self._call_ms, 3),
+                         wait_ms=round(float(res.get("wait_ms", 0.0)), 3),
+                         train_wall_ms=round(float(res.get("train_wall_ms", 0.0)), 3),
+                         ahead=bool(res.get("prepared_ahead", False)),
                          **({} if self._gil_ms is None else {"gil_wait_ms": round(self._gil_ms, 3)}))
 
     def summary(self) -> dict:
