@@ -802,6 +802,9 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred, int64_t plot_points) {
   const int world = world_;
   DevPrepared& prep = pb.dp;
   BatchResult res = pb.res;
+  using Clk = std::chrono::steady_clock;
+  Clk::time_point th[5];
+  th[0] = Clk::now();
   TWTML_HIP_CHECK(hipStreamWaitEvent(s, pb.ev_done, 0));
   TWTML_HIP_CHECK(hipEventRecord(ev_[0], s));
   const int64_t nU = res.n_unique;
@@ -833,6 +836,7 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred, int64_t plot_points) {
   ++norm_age_;
   launch_gather_w(sgd_, prep, s);
   TWTML_HIP_CHECK(hipEventRecord(ev_[1], s));
+  th[1] = Clk::now();
   TraceRange tr_train("twtml.lr.train");   // GD iterations (host enqueue + early-stop polling)
 
   const int64_t nl = sgd_.nl;
@@ -925,6 +929,7 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred, int64_t plot_points) {
   }
   if (n_glob <= 0 || diverged_) launch_norm_next(sgd_, false, s);   // weights unchanged: carry |w|^2 as is
   TWTML_HIP_CHECK(hipEventRecord(ev_[2], s));
+  th[2] = Clk::now();
   if (dp_) comm_->allreduce(sgd_.stats, 6, ncclFloat64, ncclSum, s);
   TWTML_HIP_CHECK(hipMemcpyAsync(host_out_, sgd_.stats, 8 * sizeof(double), hipMemcpyDeviceToHost, s));
   TWTML_HIP_CHECK(hipMemcpyAsync(host_out_ + 8, sgd_.state, 8 * sizeof(double), hipMemcpyDeviceToHost, s));
@@ -941,7 +946,9 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred, int64_t plot_points) {
     launch_plot_sample(sgd_.pred_out, sgd_.real_out, res.n_kept, int64_t(P), plot_buf_, s);
     TWTML_HIP_CHECK(hipMemcpyAsync(plot_host_, plot_buf_, 2 * sizeof(float) * P, hipMemcpyDeviceToHost, s));
   }
+  TWTML_HIP_CHECK(hipEventRecord(ev_[3], s));
   TWTML_HIP_CHECK(hipStreamSynchronize(s));
+  th[3] = Clk::now();
   if (comm_) comm_->check_async();
   if (P > 0) {
     res.pred.resize(P);
@@ -962,6 +969,10 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred, int64_t plot_points) {
   // batch's training when prepared ahead); train_ms: compute stream
   TWTML_HIP_CHECK(hipEventElapsedTime(&res.prep_ms, pb.ev_start, pb.ev_done));
   TWTML_HIP_CHECK(hipEventElapsedTime(&res.train_ms, ev_[1], ev_[2]));
+  th[4] = Clk::now();
+  for (int q = 0; q < 4; ++q) res.phases[q] = std::chrono::duration<float, std::milli>(th[q + 1] - th[q]).count();
+  TWTML_HIP_CHECK(hipEventElapsedTime(&res.phases[4], ev_[0], ev_[1]));
+  TWTML_HIP_CHECK(hipEventElapsedTime(&res.phases[5], ev_[2], ev_[3]));
   res.comm_iters = comm_iters;
   if (comm_timing_) {   // the per-iteration gradient all-reduces on the compute stream
     for (int q = 0; q < comm_iters; ++q) {

@@ -144,6 +144,11 @@ struct BatchResult {
   // train() end to end (enqueue, early-exit polling, the result copies)
   float wait_ms = 0.f, train_wall_ms = 0.f;
   bool prepared_ahead = false;   // the batch was prepared on the prep thread ahead of process()
+  // train() on the host: up to the first GD kernel's enqueue, the GD loop
+  // (enqueue + verdict polling), the final stream sync, the result copies;
+  // on the device: batch init .. weight gather, and the tail after the GD
+  // loop (stats / plot sample copies)
+  float phases[6] = {0, 0, 0, 0, 0, 0};
 };
 
 // One prepared micro-batch: filtered, featurized, compacted and laid out for

@@ -229,6 +229,7 @@ class LinearRegressionJob:
                          wait_ms=round(float(res.get("wait_ms", 0.0)), 3),
                          train_wall_ms=round(float(res.get("train_wall_ms", 0.0)), 3),
                          ahead=bool(res.get("prepared_ahead", False)),
+                         phases=[round(float(x), 3) for x in res.get("phases", ())],
                          **({} if self._gil_ms is None else {"gil_wait_ms": round(self._gil_ms, 3)}))
 
     def summary(self) -> dict:
