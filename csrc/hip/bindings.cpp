@@ -63,7 +63,7 @@ static py::dict result_dict(BatchResult& r) {
   d["wait_ms"] = r.wait_ms;
   d["train_wall_ms"] = r.train_wall_ms;
   d["prepared_ahead"] = r.prepared_ahead;
-  d["phases"] = std::vector<float>(r.phases, r.phases + 6);
+  d["phases"] = std::vector<float>(r.phases, r.phases + 7);
   if (!r.real.empty()) {
     auto* v = new std::vector<float>(std::move(r.real));
     py::capsule own(v, [](void* p) { delete static_cast<std::vector<float>*>(p); });

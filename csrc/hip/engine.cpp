@@ -936,6 +936,7 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred, int64_t plot_points) {
   TWTML_HIP_CHECK(hipMemcpyAsync(host_out_ + 16, sgd_.loss_hist,
                                  sizeof(double) * size_t(cfg_.num_iterations + 1),
                                  hipMemcpyDeviceToHost, s));
+  TWTML_HIP_CHECK(hipEventRecord(ev_[4], s));
   // the plot's (pred, real) pairs of this rank's kept rows: all of them, or
   // plot_points evenly spaced ones sampled on the device
   // (pinned target: a pageable D2H is staged through the runtime's bounce
@@ -973,6 +974,7 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred, int64_t plot_points) {
   for (int q = 0; q < 4; ++q) res.phases[q] = std::chrono::duration<float, std::milli>(th[q + 1] - th[q]).count();
   TWTML_HIP_CHECK(hipEventElapsedTime(&res.phases[4], ev_[0], ev_[1]));
   TWTML_HIP_CHECK(hipEventElapsedTime(&res.phases[5], ev_[2], ev_[3]));
+  TWTML_HIP_CHECK(hipEventElapsedTime(&res.phases[6], ev_[2], ev_[4]));
   res.comm_iters = comm_iters;
   if (comm_timing_) {   // the per-iteration gradient all-reduces on the compute stream
     for (int q = 0; q < comm_iters; ++q) {

@@ -148,7 +148,7 @@ struct BatchResult {
   // (enqueue + verdict polling), the final stream sync, the result copies;
   // on the device: batch init .. weight gather, and the tail after the GD
   // loop (stats / plot sample copies)
-  float phases[6] = {0, 0, 0, 0, 0, 0};
+  float phases[7] = {0, 0, 0, 0, 0, 0, 0};   // [6]: the tail's result copies alone
 };
 
 // One prepared micro-batch: filtered, featurized, compacted and laid out for
@@ -328,7 +328,7 @@ class LREngine {
   float* plot_host_ = nullptr;        // pinned [2 max_rows]: the plot sample's D2H target
   double* host_flags_ = nullptr;      // pinned [iters + 1] convergence flag per iteration
   std::vector<hipEvent_t> iter_events_;
-  hipEvent_t ev_[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev_[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
   int num_cu_ = 256;
   // weight snapshot (snapshot.hip); allocated on the first snapshot_begin
   std::mutex snap_mu_;
