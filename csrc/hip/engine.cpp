@@ -283,7 +283,6 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
   sgd_.itrec = dmalloc<double>((size_t(std::max(1, cfg_.num_iterations)) + 2) * kRecStride);
   sgd_.pred_out = dmalloc<float>(size_t(cfg_.max_rows));
   sgd_.real_out = dmalloc<float>(size_t(cfg_.max_rows));
-  plot_buf_ = dmalloc<float>(2 * size_t(cfg_.max_rows));
   sgd_.nrm = dmalloc<double>(2 * kNormParts);
   sgd_.wnorm_next = dmalloc<double>(1);
   sgd_.world = world_;
@@ -299,8 +298,12 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
   TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_out_),
                                 (32 + size_t(std::max(1, cfg_.num_iterations))) * sizeof(double),
                                 hipHostMallocDefault));
+  // the plot sample: written by k_plot_sample straight into mapped host
+  // memory (no copy engine: an 80 KB D2H on the compute stream was measured
+  // waiting 25 ms behind other transfers once per process)
   TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&plot_host_), 2 * sizeof(float) * size_t(cfg_.max_rows),
-                                hipHostMallocDefault));
+                                hipHostMallocMapped | hipHostMallocCoherent));
+  TWTML_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&plot_dev_), plot_host_, 0));
   TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_flags_),
                                 (2 + size_t(std::max(1, cfg_.num_iterations))) * sizeof(double),
                                 hipHostMallocMapped | hipHostMallocCoherent));
@@ -524,7 +527,7 @@ LREngine::~LREngine() {
   if (snap_total_) (void)hipHostFree(snap_total_);
   if (snap_stage_) (void)hipHostFree(snap_stage_);
   void* bufs[] = {sgd_.gacc, sgd_.rbuf, sgd_.w64, sgd_.wc64, sgd_.wc32, sgd_.stats, sgd_.state,
-                  sgd_.loss_hist, sgd_.pred_out, sgd_.real_out, plot_buf_, sgd_.nrm, sgd_.wnorm_next, sgd_.part, sgd_.itrec, iter_tdbg_,
+                  sgd_.loss_hist, sgd_.pred_out, sgd_.real_out, sgd_.nrm, sgd_.wnorm_next, sgd_.part, sgd_.itrec, iter_tdbg_,
                   lower_page_, lower_blocks_};
   for (void* b : bufs) if (b) (void)hipFree(b);
   if (host_out_) (void)hipHostFree(host_out_);
@@ -938,14 +941,12 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred, int64_t plot_points) {
                                  hipMemcpyDeviceToHost, s));
   TWTML_HIP_CHECK(hipEventRecord(ev_[4], s));
   // the plot's (pred, real) pairs of this rank's kept rows: all of them, or
-  // plot_points evenly spaced ones sampled on the device
-  // (pinned target: a pageable D2H is staged through the runtime's bounce
-  // buffers on the calling thread)
+  // plot_points evenly spaced ones sampled on the device, written by the
+  // kernel into mapped host memory
   size_t P = 0;
   if (want_pred && res.n_kept > 0) {
     P = size_t(plot_points > 0 ? std::min<int64_t>(plot_points, res.n_kept) : res.n_kept);
-    launch_plot_sample(sgd_.pred_out, sgd_.real_out, res.n_kept, int64_t(P), plot_buf_, s);
-    TWTML_HIP_CHECK(hipMemcpyAsync(plot_host_, plot_buf_, 2 * sizeof(float) * P, hipMemcpyDeviceToHost, s));
+    launch_plot_sample(sgd_.pred_out, sgd_.real_out, res.n_kept, int64_t(P), plot_dev_, s);
   }
   TWTML_HIP_CHECK(hipEventRecord(ev_[3], s));
   TWTML_HIP_CHECK(hipStreamSynchronize(s));

@@ -285,7 +285,6 @@ class LREngine {
   LRConfig cfg_;
   std::shared_ptr<Comm> comm_;
   int world_ = 1;
-  float* plot_buf_ = nullptr;       // [2 max_rows] sampled (pred, real) pairs
   bool dp_ = false;                 // DP path: world > 1, or forced with a world-1 communicator
   bool comm_timing_ = false;
   std::vector<hipEvent_t> comm_ev_; // comm_timing: [2 iters] around each gradient all-reduce
@@ -325,7 +324,8 @@ class LREngine {
   uint8_t* lower_page_ = nullptr;
   uint16_t* lower_blocks_ = nullptr;
   double* host_out_ = nullptr;        // pinned [16 + iters]
-  float* plot_host_ = nullptr;        // pinned [2 max_rows]: the plot sample's D2H target
+  float* plot_host_ = nullptr;        // mapped pinned [2 max_rows]: sampled (pred, real) pairs
+  float* plot_dev_ = nullptr;         // ... its device address (k_plot_sample writes it)
   double* host_flags_ = nullptr;      // pinned [iters + 1] convergence flag per iteration
   std::vector<hipEvent_t> iter_events_;
   hipEvent_t ev_[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
