@@ -359,6 +359,7 @@ def main(argv=None) -> int:
         pool = []
         for r in pool_raw:
             v = HostBatchView(B, max_units)
+            pinned += int(v._hb.bytes)
             if is_km:
                 v._hb.scalar_cols = 2
             pool.append(v.load(r))
