@@ -59,20 +59,26 @@ def _parity(profile, F, hash, n, batches, seed, expect_tiered, eng=None):
     return out
 
 
-def _check(out, werr_same=1e-6, werr_diff=3e-3):
+def _check(out, werr_same=2e-7, werr_diff=3e-3):
     """Bounds for the exact fixed-point GD (``csrc/hip/sgd.hip``: int32 row
     dots of weights quantised to 2^K with K from max |w| and the longest row,
     residuals to 2^S with |q| <= 2^22, int64 sums) against the fp64 oracle,
-    3 warm-started batches of 50 iterations at most -- re-measured on MI355X
-    in round 4 (the per-batch values are printed; see the test log)."""
+    3 warm-started batches of 50 iterations at most.  Re-derived from the
+    round-4 MI355X run of all five cases below (15 batches, values printed
+    per batch): worst relative weight error 3.6e-8 (bound 2e-7), worst
+    relative max-weight error 6.2e-8, rounded-prediction mismatches 1.6e-4
+    of the rows (bound 5e-4; each off by exactly 1: a fixed-point
+    prediction on the other side of a .5 rounding edge), MSE 8.0e-8 relative
+    (bound 1e-6); the iteration counts agreed on every batch."""
     for o in out:
         assert abs(o["it_gpu"] - o["it_orc"]) <= 1, o
         # an iteration count differing by one moves the weights by one step
         # below the convergence tolerance (1e-3 |w|)
         assert o["werr"] < (werr_same if o["it_gpu"] == o["it_orc"] else werr_diff), o
-        assert o["pred_mis"] < 1e-3, o
+        assert o["wmax"] < (werr_same * 2 if o["it_gpu"] == o["it_orc"] else werr_diff), o
+        assert o["pred_mis"] < 5e-4, o
         assert o["pred_maxdiff"] <= 1.0 + 1e-9, o
-        assert o["mse_rel"] < 1e-5, o
+        assert o["mse_rel"] < 1e-6, o
 
 
 def test_tiered_small_matches_oracle(hip_module):
