@@ -57,7 +57,8 @@ def test_kill_rank_then_resume_equals_uninterrupted(tmp_path, ck_async):
     """Synchronous checkpoints leave batch 3 (the last batch every rank
     finished) on disk.  Asynchronous ones skip a checkpoint that comes due
     while the previous write is in flight, so the model on disk is from some
-    batch 1..3 -- resume must continue exactly from whichever it is."""
+    batch 1..3, or there is none yet -- resume must continue exactly from
+    whichever it is."""
     world = 2
     ref = tmp_path / "ref"
     _run(world, _argv(ref), ck_async=ck_async)
@@ -71,9 +72,12 @@ def test_kill_rank_then_resume_equals_uninterrupted(tmp_path, ck_async):
     if ck_async == "0":
         assert prog["batches"] == 3                 # last batch every rank finished
     else:
-        assert 1 <= prog["batches"] <= 3
-    w3, _ = load_linear_regression(str(ck))
-    assert not np.array_equal(w3, w_ref)
+        # the first write may still be in flight when the job dies: then no
+        # checkpoint is durable yet and --resume auto starts from scratch
+        assert prog is None or 1 <= prog["batches"] <= 3
+    if prog is not None:
+        w3, _ = load_linear_regression(str(ck))
+        assert not np.array_equal(w3, w_ref)
 
     _run(world, _argv(ck) + ["--resume", "auto"], ck_async=ck_async)   # restart: continue
     w, _ = load_linear_regression(str(ck))
