@@ -280,10 +280,7 @@ struct RowAcc {
   int32_t qn = 0;     // sum rint(r n_t 2^N_t)
   int32_t ql = 0;     // sum rint((r 2^(L/2))^2) (t == 0)
   int32_t msum = 0;   // rows in the sampled gradient (t == 0, SAMPLE)
-  // STATS: this wave's 6 batch-stat sums, in LDS (the wave's wsc[w][6..11]
-  // slots, added to by lane 0 once per chunk) -- 12 fewer live VGPRs in the
-  // iteration-1 kernel, which spilled at the 128-VGPR cap
-  double* wst = nullptr;
+  double st[6] = {0, 0, 0, 0, 0, 0};
 };
 
 struct RowIn {
@@ -319,28 +316,17 @@ __device__ __forceinline__ float row_residual(int32_t dot_fix, const RowIn& ri, 
   if (SAMPLE && valid)
     in = sample_uniform(uint64_t(42 + sp.iteration), uint64_t(sp.row_offset + p.perm[pos])) < sp.fraction;
   const float r = in ? dot - ri.y : 0.f;
-  if (STATS) {
-    // the chunk's 6 stat sums over its rows (integer valued: exact in any
-    // order), added to the wave's LDS sums by lane 0
-    double v[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-    if (t == 0 && valid) {
+  if (t == 0) {
+    if (STATS && valid) {
       const double pr = round_half_away(double(dot));
       if (sp.want_pred) {
         d.pred_out[p.perm[pos]] = float(pr);
         d.real_out[p.perm[pos]] = ri.y;
       }
       const double yd = double(ri.y), e = yd - pr;
-      v[0] = 1.0; v[1] = yd; v[2] = yd * yd;
-      v[3] = pr; v[4] = pr * pr; v[5] = e * e;
+      acc.st[0] += 1.0; acc.st[1] += yd; acc.st[2] += yd * yd;
+      acc.st[3] += pr; acc.st[4] += pr * pr; acc.st[5] += e * e;
     }
-#pragma unroll
-    for (int k = 0; k < 6; ++k) v[k] = wave_sum(v[k]);
-    if (lane_id() == 0) {
-#pragma unroll
-      for (int k = 0; k < 6; ++k) acc.wst[k] += v[k];
-    }
-  }
-  if (t == 0) {
     if (SAMPLE && in) ++acc.msum;
     const float u = r * sc.lhalf;
     acc.ql += __float2int_rn(u * u);
@@ -368,14 +354,15 @@ __device__ __forceinline__ void part_scalars(const DevSgd& d, int64_t qn, int64_
   qn += shfl_xor_i64(qn, 32);
   ql = wave_sum_i64(ql);
   const int ms = wave_sum(acc.msum);
+  double st[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) st[k] = STATS ? wave_sum(acc.st[k]) : 0.0;
   if (lane < kNumNumeric) wsc[w][lane] = qn;
   if (lane == 0) {
     wsc[w][4] = ql;
     wsc[w][5] = ms;
-    if (!STATS) {   // STATS: wsc[w][6..11] already hold the wave's stat sums (acc.wst)
 #pragma unroll
-      for (int k = 0; k < 6; ++k) wsc[w][6 + k] = 0;
-    }
+    for (int k = 0; k < 6; ++k) wsc[w][6 + k] = __builtin_bit_cast(int64_t, st[k]);
   }
   __syncthreads();
   const int tid = threadIdx.x;
@@ -440,9 +427,6 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_lds(DevSgd d, DevPrepar
   const int64_t nwaves = int64_t(gridDim.x) * (kIterBlock / kWave);
   const uint16_t* slot = static_cast<const uint16_t*>(p.slot);
   RowAcc acc;
-  acc.wst = reinterpret_cast<double*>(&wsc[threadIdx.x / kWave][6]);
-  if (STATS && lane == 0)
-    for (int k = 0; k < 6; ++k) acc.wst[k] = 0.0;
   int64_t qn64 = 0, ql64 = 0;   // acc.qn / acc.ql folded every chunk
 
   // chunk metadata for 64 chunks at a time in lanes
@@ -680,9 +664,6 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
 #pragma unroll
   for (int i = 0; i < kHotPerLane; ++i) gh[i] = 0;
   RowAcc acc;
-  acc.wst = reinterpret_cast<double*>(&wsc[w][6]);
-  if (STATS && lane == 0)
-    for (int k = 0; k < 6; ++k) acc.wst[k] = 0.0;
 
   // Dynamic chunk assignment inside the workgroup: workgroup b owns chunks
   // b, b + G, b + 2G, ... and its waves take the next one from an LDS
