@@ -584,7 +584,7 @@ void LREngine::prepare_local(PrepBuf& pb, int slot, int64_t now_ms, hipStream_t 
 
   FeaturizeParams fp{cfg_.num_text_features, cfg_.hash_kind, cfg_.require_retweet,
                      cfg_.range_filter, cfg_.begin, cfg_.end, now_ms};
-  launch_prep_init(prep, pb.n_global, 2 * world + 2, s);
+  launch_prep_init(prep, pb.n_global, 2 * world + 2, s, pb.bounds, kBoundsLen);
   launch_filter_sort(b, prep, fp, s);
   launch_chunk_layout(b, prep, s);
   // lazy ids: only the histogram's sample chunks keep their hashed ids; the
@@ -592,7 +592,7 @@ void LREngine::prepare_local(PrepBuf& pb, int slot, int64_t now_ms, hipStream_t 
   const bool lazy = cfg_.lazy_idx && cfg_.hybrid && !cfg_.dedup;
   fp.idx_mode = lazy ? 1 : 0;
   launch_featurize(b, prep, fp, lower_page_, lower_blocks_, s);
-  launch_batch_bounds(prep, pb.bounds, s);   // fixed-point scale bounds of this rank's rows
+  launch_batch_bounds(prep, pb.bounds, s, true);   // fixed-point scale bounds of this rank's rows
   if (!lazy) raw_.release_slot(slot, s);  // raw slot may be overwritten now
   launch_compact_active(prep, s);        // this rank's active ids (clears the flags)
   TWTML_HIP_CHECK(hipMemcpyAsync(pb.host_counters, prep.counters, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, s));

@@ -39,18 +39,38 @@ namespace twtml {
 constexpr int kScanPer = 8;
 constexpr int kScanTile = 1024 * kScanPer;
 
-// Block b scans [b * span, min(n, (b + 1) * span)) starting from carry_in[b]
-// (0 without carry_in); single block: span = n.
+// Sum of ts[0, b) over the 1024 threads of a block (every thread gets it).
+// The multi-block scans take their tile's carry from the UNSCANNED tile sums
+// this way (a few hundred values at most) instead of a separate
+// single-block scan launch between the two passes: on the prep stream every
+// launch waits for a gap between the GD loop's kernels.
+__device__ __forceinline__ int64_t block_prefix_of_sums(const int64_t* ts, int64_t b, int64_t* wsum16) {
+  int64_t c = 0;
+  for (int64_t j = threadIdx.x; j < b; j += 1024) c += ts[j];
+  c = wave_sum(c);
+  if ((threadIdx.x & 63) == 0) wsum16[threadIdx.x >> 6] = c;
+  __syncthreads();
+  int64_t t = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) t += wsum16[k];
+  __syncthreads();
+  return t;
+}
+
+// Block b scans [b * span, min(n, (b + 1) * span)) starting from the sum of
+// tile_sums[0, b) (0 without tile_sums); single block: span = n.  out2, if
+// given, receives the same values.  total: the grand total (written by the
+// last block).
 __global__ __launch_bounds__(1024) void k_scan_excl(const int64_t* in, int64_t* out, int64_t n,
-                                                    int64_t* total, const int64_t* carry_in = nullptr,
-                                                    int64_t span = 0) {
+                                                    int64_t* total, const int64_t* tile_sums = nullptr,
+                                                    int64_t span = 0, int64_t* out2 = nullptr) {
   __shared__ int64_t tile_v[kScanTile + kScanTile / 32];   // +1 word per 32: fewer bank conflicts
   __shared__ int64_t wsum[16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   auto at = [](int i) { return i + (i >> 5); };
-  int64_t carry = carry_in ? carry_in[blockIdx.x] : 0;
-  const int64_t b0 = carry_in ? int64_t(blockIdx.x) * span : 0;
-  const int64_t b1 = carry_in ? (b0 + span < n ? b0 + span : n) : n;
+  int64_t carry = tile_sums ? block_prefix_of_sums(tile_sums, blockIdx.x, wsum) : 0;
+  const int64_t b0 = tile_sums ? int64_t(blockIdx.x) * span : 0;
+  const int64_t b1 = tile_sums ? (b0 + span < n ? b0 + span : n) : n;
   for (int64_t base = b0; base < b1; base += kScanTile) {
 #pragma unroll
     for (int k = 0; k < kScanPer; ++k) {
@@ -90,12 +110,16 @@ __global__ __launch_bounds__(1024) void k_scan_excl(const int64_t* in, int64_t* 
 #pragma unroll
     for (int k = 0; k < kScanPer; ++k) {
       const int64_t i = base + k * 1024 + tid;
-      if (i < b1) out[i] = tile_v[at(k * 1024 + tid)];
+      if (i < b1) {
+        const int64_t v = tile_v[at(k * 1024 + tid)];
+        out[i] = v;
+        if (out2) out2[i] = v;
+      }
     }
     carry += tot;
     __syncthreads();
   }
-  if (tid == 0 && total && !carry_in) *total = carry;
+  if (tid == 0 && total && blockIdx.x == gridDim.x - 1) *total = carry;
 }
 
 // Tile sums for the multi-block scan: block b sums in[b * kScanTile, ...).
@@ -118,27 +142,29 @@ __global__ __launch_bounds__(1024) void k_tile_sum(const int64_t* in, int64_t n,
   }
 }
 
-static void scan_excl(const int64_t* in, int64_t* out, int64_t n, int64_t* total, hipStream_t s) {
-  hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, s, in, out, n, total, nullptr, int64_t(0));
+static void scan_excl(const int64_t* in, int64_t* out, int64_t n, int64_t* total, hipStream_t s,
+                      int64_t* out2 = nullptr) {
+  hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, s, in, out, n, total, nullptr, int64_t(0), out2);
 }
 
-// Multi-block exclusive scan (in place safe): tile sums, a single-block scan
-// of them, then every tile scanned from its offset.  tsum: ceil(n / 8192) + 1.
+// Multi-block exclusive scan (in place safe): tile sums, then every tile
+// scanned from the sum of the tile sums before it -- two launches.
+// tsum: ceil(n / 8192) + 1.
 static void scan_excl_big(const int64_t* in, int64_t* out, int64_t n, int64_t* total, int64_t* tsum,
-                          hipStream_t s) {
+                          hipStream_t s, int64_t* out2 = nullptr) {
   if (n <= kScanTile) {
-    scan_excl(in, out, n, total, s);
+    scan_excl(in, out, n, total, s, out2);
     return;
   }
   const int tiles = int((n + kScanTile - 1) / kScanTile);
   hipLaunchKernelGGL(k_tile_sum, dim3(tiles), dim3(1024), 0, s, in, n, tsum);
-  scan_excl(tsum, tsum, tiles, total, s);
-  hipLaunchKernelGGL(k_scan_excl, dim3(tiles), dim3(1024), 0, s, in, out, n, nullptr,
-                     static_cast<const int64_t*>(tsum), int64_t(kScanTile));
+  hipLaunchKernelGGL(k_scan_excl, dim3(tiles), dim3(1024), 0, s, in, out, n, total,
+                     static_cast<const int64_t*>(tsum), int64_t(kScanTile), out2);
 }
 
-void launch_scan_excl(const int64_t* in, int64_t* out, int64_t n, int64_t* total, int64_t* tsum, hipStream_t s) {
-  scan_excl_big(in, out, n, total, tsum, s);
+void launch_scan_excl(const int64_t* in, int64_t* out, int64_t n, int64_t* total, int64_t* tsum, hipStream_t s,
+                      int64_t* out2) {
+  scan_excl_big(in, out, n, total, tsum, s, out2);
 }
 
 void scan_excl_launch(const int64_t* in, int64_t* out, int64_t n, int64_t* total, hipStream_t s) {
@@ -212,7 +238,9 @@ __global__ __launch_bounds__(1024) void k_rows_scan(const uint16_t* rp, int64_t 
   int64_t s = 0;
 #pragma unroll
   for (int k = 0; k < 8; ++k) s += w[k] & ((1u << kRowLenBits) - 1u);
-  int64_t o = tsum[blockIdx.x] + block_excl_scan_1024(s, wsum, &total);
+  const int64_t carry = block_prefix_of_sums(tsum, blockIdx.x, wsum);
+  int64_t o = carry + block_excl_scan_1024(s, wsum, &total);
+  if (threadIdx.x == 0 && blockIdx.x == gridDim.x - 1) offsets[n] = carry + total;   // total bytes
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     if (i0 + k < n) {
@@ -231,7 +259,6 @@ void launch_unpack_rows(const uint16_t* rowpack, int64_t n, int64_t* offsets, ui
   }
   const int tiles = int((n + kRowTile - 1) / kRowTile);
   hipLaunchKernelGGL(k_rows_tilesum, dim3(tiles), dim3(1024), 0, s, rowpack, n, tsum);
-  scan_excl(tsum, tsum, tiles, offsets + n, s);   // offsets[n] = total bytes
   hipLaunchKernelGGL(k_rows_scan, dim3(tiles), dim3(1024), 0, s, rowpack, n, tsum, offsets, flags);
 }
 
@@ -693,18 +720,21 @@ __global__ __launch_bounds__(kSegThreads) void k_sort_scatter(const int32_t* nnz
 
 // Per-batch zeroing of the small prep buffers in one launch (instead of a
 // hipMemsetAsync per buffer): counters, length histogram, DP kept counts,
-// hybrid slot histogram.
-__global__ __launch_bounds__(1024) void k_prep_init(DevPrepared p, int64_t* n_global, int ng) {
+// hybrid slot histogram, the batch's fixed-point scale bounds (max-reduced
+// by k_batch_bounds later in the same prep).
+__global__ __launch_bounds__(1024) void k_prep_init(DevPrepared p, int64_t* n_global, int ng, double* bounds,
+                                                    int nb) {
   const int64_t i = int64_t(blockIdx.x) * 1024 + threadIdx.x;
   if (i < 8) p.counters[i] = 0;
   if (i < kLenBuckets + 1) p.hist[i] = 0;
   if (i < ng) n_global[i] = 0;
   if (i < kMaxHybridSlots) p.slot_hist[i] = 0u;
+  if (bounds && i < nb) bounds[i] = 0.0;
 }
 
-void launch_prep_init(const DevPrepared& p, int64_t* n_global, int ng, hipStream_t s) {
+void launch_prep_init(const DevPrepared& p, int64_t* n_global, int ng, hipStream_t s, double* bounds, int nb) {
   const int64_t n = std::max<int64_t>(kLenBuckets + 1, kMaxHybridSlots);
-  hipLaunchKernelGGL(k_prep_init, dim3(ceil_div(n, 1024)), dim3(1024), 0, s, p, n_global, ng);
+  hipLaunchKernelGGL(k_prep_init, dim3(ceil_div(n, 1024)), dim3(1024), 0, s, p, n_global, ng, bounds, nb);
 }
 
 void launch_filter_sort(const DevRawBatch& b, const DevPrepared& p, const FeaturizeParams& fp,

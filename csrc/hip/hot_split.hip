@@ -668,6 +668,14 @@ int64_t tier_near_cap() {
   return 0;
 }
 
+__global__ __launch_bounds__(1024) void k_tier_zero(uint32_t* buckets, uint32_t* hist_near, uint64_t* fhist,
+                                                    int64_t n_fhist) {
+  const int64_t i0 = int64_t(blockIdx.x) * 1024 + threadIdx.x, st = int64_t(gridDim.x) * 1024;
+  for (int64_t i = i0; i < kCountBuckets; i += st) buckets[i] = 0u;
+  for (int64_t i = i0; i < kMaxHybridSlots; i += st) hist_near[i] = 0u;
+  for (int64_t i = i0; i < n_fhist; i += st) fhist[i] = 0ull;
+}
+
 void launch_tier_layout(const DevPrepared& p, int64_t entries, int64_t n_unique, int64_t n_near, int64_t ns,
                         int64_t nl, int num_cu, const DevRawBatch& b, const FeaturizeParams& fp, bool from_text,
                         hipStream_t s) {
@@ -677,30 +685,32 @@ void launch_tier_layout(const DevPrepared& p, int64_t entries, int64_t n_unique,
   const int g = int(std::max<int64_t>(1, std::min<int64_t>((n_unique + 1023) / 1024, int64_t(num_cu) * 4)));
   // count buckets: 4096 u32 after the cap_tier + 1 scan elements of tscan
   uint32_t* buckets = reinterpret_cast<uint32_t*>(p.tscan + p.cap_tier + 1);
-  TWTML_HIP_CHECK(hipMemsetAsync(buckets, 0, sizeof(uint32_t) * kCountBuckets, s));
+  const int64_t n_far = kNumNumeric + n_unique - p.near_end;
+  // the count buckets, the near-slot histogram and the far counts zeroed in
+  // one launch (three fills before; each prep-stream launch waits for a gap
+  // between the GD loop's kernels)
+  hipLaunchKernelGGL(k_tier_zero, dim3(int(std::min<int64_t>(256, (n_far + 1 + 1023) / 1024 + 1))), dim3(1024), 0, s,
+                     buckets, p.hist_near, p.fhist, n_far + 1);
   hipLaunchKernelGGL(k_tier_buckets, dim3(g), dim3(1024), 0, s, hist, n_unique, buckets);
   hipLaunchKernelGGL(k_tier_threshold, dim3(1), dim3(1024), 0, s, buckets, n_near, p.tparam);
   hipLaunchKernelGGL(k_tier_eqflag, dim3(g), dim3(1024), 0, s, hist, n_unique, p.tparam, p.tscan);
   launch_scan_excl(p.tscan, p.tscan, n_unique, p.tparam + 3, p.tscan_blk, s);
   hipLaunchKernelGGL(k_tier_nearflag, dim3(g), dim3(1024), 0, s, hist, n_unique, p.tparam, p.tscan, p.newslot);
   launch_scan_excl(p.tscan, p.tscan, n_unique, p.tparam + 3, p.tscan_blk, s);
-  TWTML_HIP_CHECK(hipMemsetAsync(p.hist_near, 0, sizeof(uint32_t) * kMaxHybridSlots, s));
   hipLaunchKernelGGL(k_tier_number, dim3(g), dim3(1024), 0, s, p, hist, n_unique, p.tscan);
   // hot ids among the near slots (new numbering)
   hipLaunchKernelGGL(k_hot_select, dim3(1), dim3(1024), 0, s, p.hist_near, nl, p.near_end, p.hot_of,
                      p.hot_slot);
   hipLaunchKernelGGL(k_code_table_tiered, dim3(kCodeIds / 1024), dim3(1024), 0, s, p, p.code);
   hipLaunchKernelGGL(k_code_tag_tiered, dim3(int((n_unique + 1023) / 1024)), dim3(1024), 0, s, p, n_unique);
-  const int64_t n_far = kNumNumeric + n_unique - p.near_end;
-  TWTML_HIP_CHECK(hipMemsetAsync(p.fhist, 0, sizeof(uint64_t) * size_t(n_far + 1), s));
   if (entries > 0) {
     const int64_t cmax = (p.cap_rows + kRowsPerChunk - 1) / kRowsPerChunk;
     launch_remap_slices<true>(p, ns, p.near_end, cmax, num_cu, b, fp, from_text, s);
   }
   // CSC offsets (exclusive scan of the far counts, in place), cursors, scatter
+  // CSC offsets, and the scatter cursors as a second copy of them
   launch_scan_excl(reinterpret_cast<const int64_t*>(p.fhist), reinterpret_cast<int64_t*>(p.fhist), n_far,
-                   p.tparam + 2, p.tscan_blk, s);
-  TWTML_HIP_CHECK(hipMemcpyAsync(p.fcur, p.fhist, sizeof(uint64_t) * size_t(n_far), hipMemcpyDeviceToDevice, s));
+                   p.tparam + 2, p.tscan_blk, s, reinterpret_cast<int64_t*>(p.fcur));
   if (entries > 0) {
     const int64_t cmax = (p.cap_rows + kRowsPerChunk - 1) / kRowsPerChunk;
     const int nsl = prep_slices();

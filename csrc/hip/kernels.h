@@ -188,7 +188,8 @@ void upload_lower_tables(hipStream_t s, uint8_t** d_page, uint16_t** d_blocks);
 
 // zero counters, length histogram, n_global[0..ng) and the hybrid slot
 // histogram (before launch_filter_sort)
-void launch_prep_init(const DevPrepared& p, int64_t* n_global, int ng, hipStream_t s);
+void launch_prep_init(const DevPrepared& p, int64_t* n_global, int ng, hipStream_t s, double* bounds = nullptr,
+                      int nb = 0);
 void launch_filter_sort(const DevRawBatch& b, const DevPrepared& p, const FeaturizeParams& fp,
                         hipStream_t s);
 void launch_chunk_layout(const DevRawBatch& b, const DevPrepared& p, hipStream_t s);
@@ -219,7 +220,8 @@ void launch_remap_hybrid(const DevPrepared& p, int64_t entries, int64_t ns, int6
                          const DevRawBatch& b, const FeaturizeParams& fp, bool from_text, hipStream_t s);
 
 // Exclusive int64 scan (in place safe); tsum: ceil(n / 8192) + 2 scratch.
-void launch_scan_excl(const int64_t* in, int64_t* out, int64_t n, int64_t* total, int64_t* tsum, hipStream_t s);
+void launch_scan_excl(const int64_t* in, int64_t* out, int64_t n, int64_t* total, int64_t* tsum, hipStream_t s,
+                      int64_t* out2 = nullptr);
 
 // ---------------------------------------------------------------------------
 // Tiered layout (tiered.hip), in place of launch_remap_hybrid when the active
@@ -355,7 +357,7 @@ void launch_norm_next(const DevSgd& d, bool trained, hipStream_t s);
 void launch_norm_carry(const DevSgd& d, hipStream_t s);
 // batch bounds of the scale choice (max row bigram count, max |y|, max |n_k|)
 // of this rank's kept rows -> out[kBoundsLen] (zeroed here)
-void launch_batch_bounds(const DevPrepared& p, double* out, hipStream_t s);
+void launch_batch_bounds(const DevPrepared& p, double* out, hipStream_t s, bool zeroed = false);
 int sgd_lds_rep(int64_t ns);
 // the hybrid iteration kernel's LDS (gradient replicas + hot partials) fits
 bool sgd_hybrid_fits(int64_t ns);

@@ -1574,8 +1574,9 @@ __global__ __launch_bounds__(kBlock) void k_batch_bounds(DevPrepared p, double* 
   }
 }
 
-void launch_batch_bounds(const DevPrepared& p, double* out, hipStream_t s) {
-  TWTML_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(double) * kBoundsLen, s));
+void launch_batch_bounds(const DevPrepared& p, double* out, hipStream_t s, bool zeroed) {
+  // zeroed: k_prep_init cleared them earlier in this prep
+  if (!zeroed) TWTML_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(double) * kBoundsLen, s));
   const int grid = int(std::max<int64_t>(1, std::min<int64_t>((p.cap_rows + kBlock - 1) / kBlock, 256)));
   hipLaunchKernelGGL(k_batch_bounds, dim3(grid), dim3(kBlock), 0, s, p, out);
 }
