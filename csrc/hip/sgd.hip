@@ -1147,13 +1147,13 @@ __device__ __forceinline__ bool far_seg_scan(int64_t e, int64_t n, uint32_t sl, 
 // skewed over slot ranges, and the slowest block made the update ~100 us.
 // The grouping is a function of the layout only, so the fp64 norm partials
 // (and the convergence verdicts) are the same bits on one GPU and in DP.
-// The update of block `bid` of the whole update grid [0, nblk) (1024 threads).
-__device__ __forceinline__ void sgd_update_block(DevSgd& d, const SgdParams& sp, int nparts, int nt, int nf, int bid,
-                                                 int nblk) {
+__global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int nparts, int nt, int nf, int blk0,
+                                                     int nblk) {
   __shared__ double wsc[kUpdWaves][3];
   __shared__ int64_t red[kUpdWaves][kWave];
   __shared__ double m_sh;
   const int tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
+  const int bid = blk0 + int(blockIdx.x);   // block of the whole update grid [0, nblk)
   const int it = sp.iteration;
   const int64_t ns = d.nl, hi = d.far_base;   // partial-row columns; near text slots end at far_base
   int64_t* tail = d.gacc + ns;
@@ -1281,11 +1281,6 @@ __device__ __forceinline__ void sgd_update_block(DevSgd& d, const SgdParams& sp,
   }
 }
 
-__global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int nparts, int nt, int nf, int blk0,
-                                                     int nblk) {
-  sgd_update_block(d, sp, nparts, nt, nf, blk0 + int(blockIdx.x), nblk);
-}
-
 // Near tiles and far ranges of the update grid: a function of the layout
 // only, the same on every DP rank.
 static void update_split(const DevSgd& d, int& nt, int& nf) {
@@ -1377,8 +1372,7 @@ void launch_sgd_finish(const DevSgd& d, const SgdParams& sp, hipStream_t s) {
 // so the result does not depend on the order of entries inside a slot or on
 // which wave adds first: deterministic across runs and DP ranks.
 // ---------------------------------------------------------------------------
-// Block vb of nvb blocks of `threads` threads each.
-__device__ __forceinline__ void far_grad_block(const DevSgd& d, const SgdParams& sp, int vb, int nvb, int threads) {
+__global__ __launch_bounds__(256) void k_far_grad(DevSgd d, SgdParams sp) {
   if (d.state[0] != 0.0 || d.state[8] == double(sp.iteration)) return;   // done / DP pass skipped
   const int64_t n = *d.far_n;
   const int lane = lane_id();
@@ -1388,8 +1382,8 @@ __device__ __forceinline__ void far_grad_block(const DevSgd& d, const SgdParams&
   // both residual gathers, are in flight before the scans (half the
   // dependent round trips of one tile per step)
   constexpr int kU = 2;
-  const int64_t stride = int64_t(nvb) * threads * kU;
-  for (int64_t e0 = (int64_t(vb) * threads + (threadIdx.x & ~(kWave - 1))) * kU; e0 < n; e0 += stride) {
+  const int64_t stride = int64_t(gridDim.x) * 256 * kU;
+  for (int64_t e0 = (int64_t(blockIdx.x) * 256 + (threadIdx.x & ~(kWave - 1))) * kU; e0 < n; e0 += stride) {
     uint32_t sl[kU], ps[kU];
     float rv[kU];
 #pragma unroll
@@ -1409,32 +1403,8 @@ __device__ __forceinline__ void far_grad_block(const DevSgd& d, const SgdParams&
   }
 }
 
-__global__ __launch_bounds__(256) void k_far_grad(DevSgd d, SgdParams sp) {
-  far_grad_block(d, sp, int(blockIdx.x), int(gridDim.x), 256);
-}
-
 void launch_far_grad(const DevSgd& d, const SgdParams& sp, int num_cu, hipStream_t s) {
   hipLaunchKernelGGL(k_far_grad, dim3(std::max(1, num_cu * 4)), dim3(256), 0, s, d, sp);
-}
-
-// One GPU, tiered: the far backward and the update's near tiles in ONE
-// launch (blocks [0, nfg) sum the far gradients, blocks [nfg, nfg + nt) update
-// the near tiles -- they touch disjoint data), then the far ranges of the
-// update in a second launch once the far sums are complete.  Before: far
-// backward, then the whole update, one after the other.
-__global__ __launch_bounds__(1024) void k_far_near(DevSgd d, SgdParams sp, int nparts, int nt, int nf, int nfg) {
-  if (int(blockIdx.x) < nfg) {
-    far_grad_block(d, sp, int(blockIdx.x), nfg, 1024);
-  } else {
-    sgd_update_block(d, sp, nparts, nt, nf, int(blockIdx.x) - nfg, nt + nf);
-  }
-}
-
-void launch_far_near(const DevSgd& d, const SgdParams& sp, int nparts, int num_cu, hipStream_t s) {
-  int nt = 0, nf = 0;
-  update_split(d, nt, nf);
-  const int nfg = std::max(1, num_cu);
-  hipLaunchKernelGGL(k_far_near, dim3(nfg + nt), dim3(1024), 0, s, d, sp, nparts, nt, nf, nfg);
 }
 
 // ---------------------------------------------------------------------------
