@@ -266,11 +266,6 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
   }
   if (!pstream_) TWTML_HIP_CHECK(hipStreamCreateWithPriority(&pstream_, hipStreamNonBlocking, lo));
   TWTML_HIP_CHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
-  if (const char* v = std::getenv("TWTML_SPLIT_FAR")) split_far_ = v[0] != '0';
-  if (split_far_) {
-    TWTML_HIP_CHECK(hipStreamCreateWithPriority(&aux_, hipStreamNonBlocking, hi));
-    for (auto& e : ev_far_) TWTML_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  }
   raw_.init(cfg_.max_rows, text_bytes_for_units(cfg_.max_units));
   for (auto& e : ev_) TWTML_HIP_CHECK(hipEventCreate(&e));
   upload_lower_tables(compute_, &lower_page_, &lower_blocks_);
@@ -546,8 +541,6 @@ LREngine::~LREngine() {
   (void)hipStreamDestroy(compute_);
   (void)hipStreamDestroy(pstream_);
   (void)hipStreamDestroy(copy_);
-  for (auto e : ev_far_) if (e) (void)hipEventDestroy(e);
-  if (aux_) (void)hipStreamDestroy(aux_);
 }
 
 void LREngine::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, const uint8_t* ext_text,
@@ -881,7 +874,6 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred, int64_t plot_points) {
     std::fill(host_flags_, host_flags_ + iters + 2, -1.0);   // -1: verdict not published yet
     // single GPU with partial rows: the update kernel reduces them itself
     const bool fused = !dp_ && sgd_.nparts > 0;
-    const bool split_far = split_far_ && aux_ && update_far_blocks(sgd_) > 0;
     const bool itime = std::getenv("TWTML_ITER_TIMING") != nullptr;
     if (itime && !iter_tdbg_) iter_tdbg_ = dmalloc<uint64_t>(4096 + size_t(iters + 2) * 32);
     sgd_.tdbg = itime ? iter_tdbg_ : nullptr;
@@ -916,18 +908,6 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred, int64_t plot_points) {
       // every rank launches the gradient kernel (an empty shard writes zero
       // partials) so every rank runs the convergence prologue
       launch_sgd_iter(sgd_, prep, sp, pb.host_counters[2], u16, grid, s);
-      if (tiered && split_far && !dp_) {
-        // the far sums on aux_ while the update's near tiles run on s; the
-        // far ranges of the update wait for them
-        TWTML_HIP_CHECK(hipEventRecord(ev_far_[0], s));
-        TWTML_HIP_CHECK(hipStreamWaitEvent(aux_, ev_far_[0], 0));
-        launch_far_grad(sgd_, sp, num_cu_, aux_);
-        TWTML_HIP_CHECK(hipEventRecord(ev_far_[1], aux_));
-        launch_sgd_update(sgd_, sp, fused ? sgd_.nparts : 0, s, 1);
-        TWTML_HIP_CHECK(hipStreamWaitEvent(s, ev_far_[1], 0));
-        launch_sgd_update(sgd_, sp, fused ? sgd_.nparts : 0, s, 2);
-        continue;
-      }
       if (tiered) launch_far_grad(sgd_, sp, num_cu_, s);
       if (dp_) {
         // ONE collective per iteration: the packed int64 buffer (near

@@ -289,12 +289,6 @@ class LREngine {
   bool comm_timing_ = false;
   std::vector<hipEvent_t> comm_ev_; // comm_timing: [2 iters] around each gradient all-reduce
   hipStream_t compute_ = nullptr, pstream_ = nullptr, copy_ = nullptr;
-  // one GPU, tiered: k_far_grad on aux_ beside the update's near tiles on
-  // compute_ (TWTML_SPLIT_FAR=0 turns it off); ev_far_[0] iteration done,
-  // ev_far_[1] far sums done
-  hipStream_t aux_ = nullptr;
-  hipEvent_t ev_far_[2] = {nullptr, nullptr};
-  bool split_far_ = true;
   RawSlots raw_;
   PrepBuf pb_[2];
   int last_buf_ = -1;               // buffer of the last trained batch (debug_*)

@@ -343,8 +343,7 @@ int sgd_partials(int64_t ns, bool u16, int grid);
 // DP: gacc[0, nl + 2) = sums of the d.nparts partial rows (+ stats), verdict and ready words
 void launch_sgd_reduce(const DevSgd& d, const SgdParams& sp, hipStream_t s);
 // nparts > 0: sums the partial rows itself (single GPU, no separate reduce)
-void launch_sgd_update(const DevSgd& d, const SgdParams& sp, int nparts, hipStream_t s, int part = 0);
-int update_far_blocks(const DevSgd& d);   // far-range blocks of the update grid (0: none)
+void launch_sgd_update(const DevSgd& d, const SgdParams& sp, int nparts, hipStream_t s);
 // Far backward of one iteration: gacc[far_off + slot - far_base] += sum of the
 // fixed-point residuals of the slot's entries (CSC segmented sums).
 void launch_far_grad(const DevSgd& d, const SgdParams& sp, int num_cu, hipStream_t s);

@@ -1139,21 +1139,17 @@ __device__ __forceinline__ bool far_seg_scan(int64_t e, int64_t n, uint32_t sl, 
 // [n_far k / nf, n_far (k + 1) / nf) of the tiered layout, read from the far
 // gradient sums (k_far_grad; DP: the all-reduced packed buffer).  The near
 // tiles and the far ranges run side by side instead of every block doing a
-// tile and then a grid-stride share of the far slots.  On one GPU the two
-// groups can also be launched apart (blk0 / nblk: this launch's first block
-// and the whole grid's size), the near tiles beside k_far_grad on a second
-// stream and the far ranges after it.  Measured and reverted: far blocks summing their
+// tile and then a grid-stride share of the far slots (r3: 26 us -> 17 us
+// on the wide profile).  Measured and reverted: far blocks summing their
 // range's CSC segments themselves (no k_far_grad) -- the far entries are
 // skewed over slot ranges, and the slowest block made the update ~100 us.
 // The grouping is a function of the layout only, so the fp64 norm partials
 // (and the convergence verdicts) are the same bits on one GPU and in DP.
-__global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int nparts, int nt, int nf, int blk0,
-                                                     int nblk) {
+__global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int nparts, int nt, int nf) {
   __shared__ double wsc[kUpdWaves][3];
   __shared__ int64_t red[kUpdWaves][kWave];
   __shared__ double m_sh;
   const int tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
-  const int bid = blk0 + int(blockIdx.x);   // block of the whole update grid [0, nblk)
   const int it = sp.iteration;
   const int64_t ns = d.nl, hi = d.far_base;   // partial-row columns; near text slots end at far_base
   int64_t* tail = d.gacc + ns;
@@ -1163,7 +1159,7 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
     // the agreed verdict on update it - 1 (checked before state[0]: block 0
     // sets it below while other blocks may still start), and the ready words
     const bool stop = it > 1 && tail[kTailVerdict] != 0;
-    if (bid == 0 && tid == 0 && d.host_flags) {
+    if (blockIdx.x == 0 && tid == 0 && d.host_flags) {
       bool all = true;
       int64_t mx = 0;
       for (int r = 0; r < d.world; ++r) {
@@ -1175,9 +1171,9 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
                          __HIP_MEMORY_SCOPE_SYSTEM);
     }
     if (stop) {
-      for (int64_t j = int64_t(bid) * 1024 + tid; j < n_far; j += int64_t(nblk) * 1024)
+      for (int64_t j = int64_t(blockIdx.x) * 1024 + tid; j < n_far; j += int64_t(gridDim.x) * 1024)
         gfar[j] = 0;   // this pass's far sums are dropped
-      if (bid == 0 && tid == 0) {
+      if (blockIdx.x == 0 && tid == 0) {
         d.state[0] = 1.0;
         if (d.state[7] == 0.0) d.state[1] = 1.0;
       }
@@ -1208,8 +1204,8 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
   const double alpha = sp.step_size / sqrt(double(it));
   const double gsc = ldexp(1.0, -sS);
   double ds = 0.0, ws = 0.0, mx = 0.0;
-  if (bid < nt) {
-    for (int64_t col0 = int64_t(bid) * kWave; col0 < ncols; col0 += int64_t(nt) * kWave) {
+  if (int(blockIdx.x) < nt) {
+    for (int64_t col0 = int64_t(blockIdx.x) * kWave; col0 < ncols; col0 += int64_t(nt) * kWave) {
       const int64_t gp = nparts > 0 ? part_block_sum(d, col0, ncols, ns + 2, nparts, red) : 0;
       const int64_t col = col0 + lane;
       if (w == 0 && col < ncols) {
@@ -1236,7 +1232,7 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
   } else if (n_far > 0) {
     // tiered: far slots [far_base + jlo, far_base + jhi) from the far
     // gradient sums (k_far_grad; DP: all-reduced), re-zeroed here
-    const int64_t k = int64_t(bid) - nt;
+    const int64_t k = int64_t(blockIdx.x) - nt;
     const int64_t jlo = n_far * k / nf, jhi = n_far * (k + 1) / nf;
     for (int64_t j = jlo + tid; j < jhi; j += 1024) {
       const double g = double(gfar[j]) * gsc;
@@ -1269,13 +1265,13 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
   if (tid < 3) {
     double t = 0.0;
     for (int k = 0; k < kUpdWaves; ++k) t = tid < 2 ? t + wsc[k][tid] : fmax(t, wsc[k][tid]);
-    rec[kRecHead + 3 * bid + tid] = t;
+    rec[kRecHead + 3 * blockIdx.x + tid] = t;
   }
-  if (bid == 0 && tid == 0) {
+  if (blockIdx.x == 0 && tid == 0) {
     const double nupd = (it > 1 ? sgd_rec(d, it - 1)[0] : 0.0) + (m > 0.0 ? 1.0 : 0.0);
     rec[0] = nupd;
     rec[1] = m;
-    rec[2] = double(nblk);
+    rec[2] = double(gridDim.x);
     d.state[2] = nupd;
     d.state[3] = double(it);
   }
@@ -1290,21 +1286,10 @@ static void update_split(const DevSgd& d, int& nt, int& nf) {
   nf = n_far > 0 ? int(std::max<int64_t>(1, std::min<int64_t>((n_far + 767) / 768, kMaxUpdGrid - nt))) : 0;
 }
 
-// part: 0 = the whole grid, 1 = the near tiles only, 2 = the far ranges only
-// (one GPU: the near tiles beside k_far_grad, the far ranges after it)
-void launch_sgd_update(const DevSgd& d, const SgdParams& sp, int nparts, hipStream_t s, int part) {
+void launch_sgd_update(const DevSgd& d, const SgdParams& sp, int nparts, hipStream_t s) {
   int nt = 0, nf = 0;
   update_split(d, nt, nf);
-  const int blk0 = part == 2 ? nt : 0;
-  const int grid = part == 0 ? nt + nf : part == 1 ? nt : nf;
-  if (grid <= 0) return;
-  hipLaunchKernelGGL(k_sgd_update, dim3(grid), dim3(1024), 0, s, d, sp, nparts, nt, nf, blk0, nt + nf);
-}
-
-int update_far_blocks(const DevSgd& d) {
-  int nt = 0, nf = 0;
-  update_split(d, nt, nf);
-  return nf;
+  hipLaunchKernelGGL(k_sgd_update, dim3(nt + nf), dim3(1024), 0, s, d, sp, nparts, nt, nf);
 }
 
 // DP: cross-workgroup reduction of the partial rows into the packed buffer
