@@ -174,6 +174,24 @@ def run_device_pipeline(r: Runner, pool, warmup: int, steps: int, sync):
     return t0, t1
 
 
+def _h2d_gbps(device: int, mb: int = 256, reps: int = 4) -> float:
+    """Pinned host-to-device copy bandwidth of this GPU's link (GB/s)."""
+    import torch
+    n = mb << 20
+    h = torch.empty(n, dtype=torch.uint8).pin_memory()
+    d = torch.empty(n, dtype=torch.uint8, device=f"cuda:{device}")
+    s = torch.cuda.Stream(device=device)
+    with torch.cuda.stream(s):
+        d.copy_(h, non_blocking=True)
+    torch.cuda.synchronize(device)
+    t = time.perf_counter()
+    with torch.cuda.stream(s):
+        for _ in range(reps):
+            d.copy_(h, non_blocking=True)
+    torch.cuda.synchronize(device)
+    return n * reps / (time.perf_counter() - t) / 1e9
+
+
 def run_e2e(r: Runner, raws, u8s, views, ingest: str, warmup: int, steps: int, sync):
     """Host staging inside the loop: a staging thread loads raw batch i into
     the staging buffer of a free raw slot (wire pack or UTF-16 row words +
@@ -367,15 +385,19 @@ def main(argv=None) -> int:
     t_gen = time.time() - t_gen
     runner = Runner(eng, is_km, now_ms)
 
+    h2d = {}
+
     def sync(fn):
         eng.synchronize()
         D.barrier()
         torch.cuda.synchronize()
+        h2d["b0"] = eng.h2d_bytes
         t0 = time.perf_counter()
         fn()
         eng.synchronize()
         torch.cuda.synchronize()
         t1 = time.perf_counter()
+        h2d["b1"] = eng.h2d_bytes
         D.barrier()
         return t0, t1
 
@@ -391,6 +413,10 @@ def main(argv=None) -> int:
     mine = float(sum(runner.kept)) / max(t1 - t0, 1e-12)   # this rank's own tweets/s over its window
     per_rank = D.gather_to_main(np.array([mine]))
     prestaged = int(D.allreduce_max_scalar(float(runner.prestaged_at_t0)))
+    # host-link floor: the timed window's H2D bytes (engine counter) over this
+    # box's pinned host-to-device bandwidth (measured here, after the window)
+    moved = float(h2d.get("b1", 0) - h2d.get("b0", 0))
+    gbps = D.allreduce_min_scalar(_h2d_gbps(device))
     import resource
     rss_mb = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024.0
     host = D.gather_to_main(np.array([rss_mb, pinned / 2**20, t_gen]))   # per rank, to rank 0
@@ -454,6 +480,10 @@ def main(argv=None) -> int:
     if per_rank is not None:
         out["per_rank_value"] = [round(float(v), 1) for v in per_rank]
     out["prestaged_at_t0"] = prestaged
+    if moved > 0:
+        out["h2d_bytes_per_tweet"] = round(moved / (args.steps * B), 1)
+        out["h2d_gbps"] = round(gbps, 1)
+        out["h2d_floor_ms_per_step"] = round(moved / args.steps / (gbps * 1e9) * 1e3, 3) if gbps > 0 else None
     if runner.comm and sum(c[0] for c in runner.comm) > 0:
         n_ar = sum(c[0] for c in runner.comm)
         out["grad_allreduce_per_step"] = round(n_ar / len(runner.comm), 2)

@@ -312,6 +312,7 @@ PYBIND11_MODULE(_twtml_hip, m) {
              return d;
            },
            py::arg("slot"), py::arg("now_ms"), py::arg("want_pred") = false, py::arg("plot_points") = 0)
+      .def_property_readonly("h2d_bytes", &LREngine::h2d_bytes, "host-to-device bytes submitted so far")
       .def_property_readonly("lazy_bytes", &LREngine::lazy_bytes,
                              "device bytes the engine allocates on its first tiered batch (sizing)")
       .def("get_weights", [](const LREngine& e) {

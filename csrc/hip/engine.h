@@ -221,6 +221,7 @@ class LREngine {
   // buffer: the entry-sized far lists and CSC, the slot-sized tier arrays; the trainer's residual row
   // buffer) and by the first checkpoint snapshot ((index, value) pairs for
   // every weight): ops/sizing.py adds them to the construction footprint.
+  int64_t h2d_bytes() const { return raw_.h2d_bytes(); }   // host-to-device bytes submitted so far
   int64_t lazy_bytes() const {
     const int nbuf = overlap_ ? 2 : 1;
     // + the slot-sized tier arrays (newslot, slot_fid, tscan, fhist, fcur,

@@ -282,6 +282,7 @@ void bind_kmeans(py::module_& m) {
         py::gil_scoped_release nogil;
         e.submit(hb, n, bytes, slot, reinterpret_cast<const uint8_t*>(ext_text));
       }, py::arg("host_batch"), py::arg("n"), py::arg("bytes"), py::arg("slot"), py::arg("ext_text") = 0)
+      .def_property_readonly("h2d_bytes", &KMEngine::h2d_bytes, "host-to-device bytes submitted so far")
       .def("process", [](KMEngine& e, int slot, bool want_labels) {
         KMResult r;
         {

@@ -50,6 +50,7 @@ class KMEngine {
   int k() const { return cfg_.k; }
   int d() const { return d_; }
   int dp() const { return dp_; }
+  int64_t h2d_bytes() const { return raw_.h2d_bytes(); }
   void synchronize();
 
  private:

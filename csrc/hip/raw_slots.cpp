@@ -105,6 +105,10 @@ void RawSlots::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, h
                                    hipMemcpyHostToDevice, copy));
   }
   TWTML_HIP_CHECK(hipEventRecord(s.h2d_done, copy));
+  int64_t moved = int64_t(pre) + bytes;
+  if (!packed) moved += int64_t(sizeof(int64_t)) * (n + 1) + (n > 0 ? n : 0);
+  if (n > 0) moved += hb.soff[scalar_cols];
+  h2d_bytes_.fetch_add(moved, std::memory_order_relaxed);
   for (int c = 0; c < kScalarCols; ++c) {
     s.soff[c] = hb.soff[c];
     s.sbase[c] = hb.sbase[c];

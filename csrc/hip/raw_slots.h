@@ -11,6 +11,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 
 #include "kernels.h"
@@ -50,6 +51,8 @@ class RawSlots {
   // expanded to UTF-16 / narrowed UTF-16 rows (<= 2 bytes per wire byte),
   // then for lowered special rows (<= 2 bytes per wire byte, rows.hip)
   int64_t max_bytes() const { return max_bytes_; }
+  // bytes enqueued host-to-device by submit() so far (every copy of a batch)
+  int64_t h2d_bytes() const { return h2d_bytes_.load(std::memory_order_relaxed); }
 
  private:
   static int check(int slot);
@@ -74,6 +77,7 @@ class RawSlots {
     bool used = false;
   } slots_[kRawSlots];
   int64_t max_rows_ = 0, max_bytes_ = 0;
+  std::atomic<int64_t> h2d_bytes_{0};
   DevCaseTables case_{};
 };
 

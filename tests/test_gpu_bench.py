@@ -37,6 +37,10 @@ def test_bench_json_line(hip_module, mode):
     assert d["prestaged_at_t0"] == 0
     assert d["comm_world"] == 1 and len(d["per_rank_value"]) == 1
     assert d["per_rank_host"][0]["pinned_mb"] > 0
+    # the window's H2D bytes (engine counter, ~150-200 B per wide tweet) and
+    # the host-link floor they imply at this box's measured pinned bandwidth
+    assert 100 < d["h2d_bytes_per_tweet"] < 400, d["h2d_bytes_per_tweet"]
+    assert 20 < d["h2d_gbps"] < 200 and 0 < d["h2d_floor_ms_per_step"] <= d["ms_per_step"] * 1.05
 
 
 def test_bench_force_dp_reports_the_collective(hip_module):

@@ -150,5 +150,10 @@ class DeviceKMeans:
         """One micro-batch: uses its prefetched slot, else stages + H2D now."""
         return self.process(self._pipe.take(raw), want_pred)
 
+    @property
+    def h2d_bytes(self) -> int:
+        """Host-to-device bytes submitted so far (every copy of every batch)."""
+        return int(self._eng.h2d_bytes)
+
     def synchronize(self) -> None:
         self._eng.synchronize()

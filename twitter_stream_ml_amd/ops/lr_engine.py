@@ -309,6 +309,11 @@ class DeviceLinearRegression:
         """Train on one micro-batch: uses its prefetched slot, else stages + H2D now."""
         return self.process(self._pipe.take(raw), raw.batch_time_ms, want_pred, plot_points)
 
+    @property
+    def h2d_bytes(self) -> int:
+        """Host-to-device bytes submitted so far (every copy of every batch)."""
+        return int(self._eng.h2d_bytes)
+
     def synchronize(self) -> None:
         self._eng.synchronize()
 

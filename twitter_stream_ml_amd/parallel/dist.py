@@ -27,7 +27,7 @@ import numpy as np
 
 __all__ = ["DistInfo", "init_distributed", "dist_info", "make_rccl_comm", "make_comm", "broadcast_flag",
            "allreduce_fn",
-           "barrier", "allreduce_max_scalar", "allreduce_sum_scalar", "shutdown",
+           "barrier", "allreduce_max_scalar", "allreduce_sum_scalar", "allreduce_min_scalar", "shutdown",
            "check_replicas", "replica_digest", "ReplicaDivergence", "gather_to_main"]
 
 
@@ -186,7 +186,8 @@ def _reduce_scalar(x: float, op: str) -> float:
     t = torch.tensor([float(x)], dtype=torch.float64)
     if info.backend == "nccl":
         t = t.cuda()
-    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+    red = {"max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}.get(op, dist.ReduceOp.SUM)
+    dist.all_reduce(t, op=red)
     return float(t.item())
 
 
@@ -196,6 +197,10 @@ def allreduce_max_scalar(x: float) -> float:
 
 def allreduce_sum_scalar(x: float) -> float:
     return _reduce_scalar(x, "sum")
+
+
+def allreduce_min_scalar(x: float) -> float:
+    return _reduce_scalar(x, "min")
 
 
 class ReplicaDivergence(RuntimeError):
