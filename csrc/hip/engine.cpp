@@ -245,7 +245,6 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
   // ranks' packets between two of t's GD iterations) the rest.
   overlap_ = cfg_.overlap != 0;
   if (const char* v = std::getenv("TWTML_OVERLAP")) overlap_ = overlap_ && v[0] != '0';
-  if (const char* v = std::getenv("TWTML_HEAD_AHEAD")) head_ahead_ = v[0] != '0';
   TWTML_HIP_CHECK(hipSetDevice(device_));
   hipDeviceProp_t prop;
   TWTML_HIP_CHECK(hipGetDeviceProperties(&prop, device_));
@@ -377,8 +376,6 @@ void LREngine::alloc_prepared(PrepBuf& b) {
   TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&b.host_norm), 2 * sizeof(int64_t), hipHostMallocDefault));
   TWTML_HIP_CHECK(hipEventCreate(&b.ev_start));
   TWTML_HIP_CHECK(hipEventCreate(&b.ev_done));
-  TWTML_HIP_CHECK(hipEventCreate(&b.ev_h0));
-  TWTML_HIP_CHECK(hipEventCreate(&b.ev_h1));
   if (dp_) {
     TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&b.host_hdr),
                                   sizeof(int64_t) * size_t(world_) * (kC1HeaderWords / 2), hipHostMallocDefault));
@@ -403,8 +400,6 @@ void LREngine::free_prepared(PrepBuf& b) {
   if (b.ev_c1) (void)hipEventDestroy(b.ev_c1);
   if (b.ev_start) (void)hipEventDestroy(b.ev_start);
   if (b.ev_done) (void)hipEventDestroy(b.ev_done);
-  if (b.ev_h0) (void)hipEventDestroy(b.ev_h0);
-  if (b.ev_h1) (void)hipEventDestroy(b.ev_h1);
   b = PrepBuf{};
 }
 
@@ -804,15 +799,21 @@ void LREngine::finish_layout(PrepBuf& pb, hipStream_t s, bool dp_hist) {
 // ---------------------------------------------------------------------------
 // train: GD on a prepared batch, on the compute stream (after its prep).
 // ---------------------------------------------------------------------------
-void LREngine::issue_head(PrepBuf& pb) {
+BatchResult LREngine::train(PrepBuf& pb, bool want_pred, int64_t plot_points) {
+  TWTML_HIP_CHECK(hipSetDevice(device_));
   hipStream_t s = compute_;
+  const int world = world_;
   DevPrepared& prep = pb.dp;
-  const BatchResult& res = pb.res;
+  BatchResult res = pb.res;
+  using Clk = std::chrono::steady_clock;
+  Clk::time_point th[5];
+  th[0] = Clk::now();
   TWTML_HIP_CHECK(hipStreamWaitEvent(s, pb.ev_done, 0));
-  TWTML_HIP_CHECK(hipEventRecord(pb.ev_h0, s));
+  TWTML_HIP_CHECK(hipEventRecord(ev_[0], s));
   const int64_t nU = res.n_unique;
   const int64_t n_glob = res.n_kept_global;
   const bool tiered = res.tiered;
+  const bool u16 = pb.u16;
   ensure_compact(pb.ns);
   sgd_.ns = pb.ns;
   sgd_.n_unique = nU;
@@ -837,25 +838,7 @@ void LREngine::issue_head(PrepBuf& pb) {
   }
   ++norm_age_;
   launch_gather_w(sgd_, prep, s);
-  TWTML_HIP_CHECK(hipEventRecord(pb.ev_h1, s));
-}
-
-BatchResult LREngine::train(PrepBuf& pb, bool want_pred, int64_t plot_points) {
-  TWTML_HIP_CHECK(hipSetDevice(device_));
-  hipStream_t s = compute_;
-  const int world = world_;
-  DevPrepared& prep = pb.dp;
-  BatchResult res = pb.res;
-  using Clk = std::chrono::steady_clock;
-  Clk::time_point th[5];
-  th[0] = Clk::now();
-  const int64_t nU = res.n_unique;
-  const int64_t n_glob = res.n_kept_global;
-  const bool tiered = res.tiered;
-  const bool u16 = pb.u16;
-  // the head was enqueued at the end of the previous batch (issue_head), or now
-  if (head_buf_ != &pb) issue_head(pb);
-  head_buf_ = nullptr;
+  TWTML_HIP_CHECK(hipEventRecord(ev_[1], s));
   th[1] = Clk::now();
   TraceRange tr_train("twtml.lr.train");   // GD iterations (host enqueue + early-stop polling)
 
@@ -966,22 +949,6 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred, int64_t plot_points) {
     launch_plot_sample(sgd_.pred_out, sgd_.real_out, res.n_kept, int64_t(P), plot_dev_, s);
   }
   TWTML_HIP_CHECK(hipEventRecord(ev_[3], s));
-  if (head_ahead_) {
-    // the next prepared batch's head behind this batch's result copies: the
-    // compute stream keeps working while this thread returns the results
-    // and the caller turns around (it only reads this batch's copies, which
-    // precede it on the stream)
-    PrepBuf* nb = nullptr;
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      for (auto& b : pb_)
-        if (&b != &pb && b.state == 2 && !b.error) nb = &b;
-    }
-    if (nb) {
-      issue_head(*nb);
-      head_buf_ = nb;
-    }
-  }
   TWTML_HIP_CHECK(hipStreamSynchronize(s));
   th[3] = Clk::now();
   if (comm_) comm_->check_async();
@@ -1003,10 +970,10 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred, int64_t plot_points) {
   // prep_ms: the batch's prep on its own stream (overlapped with the previous
   // batch's training when prepared ahead); train_ms: compute stream
   TWTML_HIP_CHECK(hipEventElapsedTime(&res.prep_ms, pb.ev_start, pb.ev_done));
-  TWTML_HIP_CHECK(hipEventElapsedTime(&res.train_ms, pb.ev_h1, ev_[2]));
+  TWTML_HIP_CHECK(hipEventElapsedTime(&res.train_ms, ev_[1], ev_[2]));
   th[4] = Clk::now();
   for (int q = 0; q < 4; ++q) res.phases[q] = std::chrono::duration<float, std::milli>(th[q + 1] - th[q]).count();
-  TWTML_HIP_CHECK(hipEventElapsedTime(&res.phases[4], pb.ev_h0, pb.ev_h1));
+  TWTML_HIP_CHECK(hipEventElapsedTime(&res.phases[4], ev_[0], ev_[1]));
   TWTML_HIP_CHECK(hipEventElapsedTime(&res.phases[5], ev_[2], ev_[3]));
   TWTML_HIP_CHECK(hipEventElapsedTime(&res.phases[6], ev_[2], ev_[4]));
   res.comm_iters = comm_iters;
@@ -1160,7 +1127,6 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred, int64_t 
           std::rethrow_exception(err);
         }
         pb_[k].state = 1;
-        if (head_buf_ == &pb_[k]) head_buf_ = nullptr;   // re-prepared: its head is stale
         lk.unlock();
         prepare_local(pb_[k], slot, now_ms, pstream_);
         prepare_global(pb_[k], pstream_);
@@ -1188,7 +1154,6 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred, int64_t 
         for (int i = 0; i < 2 && k < 0; ++i)
           if (pb_[i].state == 2) {
             submitted_.push_front({pb_[i].slot, pb_[i].now_ms});
-            if (head_buf_ == &pb_[i]) head_buf_ = nullptr;
             pb_[i].state = 0;
             pb_[i].error = nullptr;
             k = i;
@@ -1253,7 +1218,6 @@ void LREngine::set_weights(const double* w, int64_t n) {
   if (n != num_weights()) throw std::invalid_argument("weights size mismatch");
   TWTML_HIP_CHECK(hipSetDevice(device_));
   TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
-  head_buf_ = nullptr;   // a head enqueued ahead gathered the old weights
   if (snap_guard_) {
     TWTML_HIP_CHECK(hipEventSynchronize(snap_ev_));
     snap_guard_ = false;

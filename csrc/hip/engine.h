@@ -177,10 +177,6 @@ struct PrepBuf {
   double* bounds = nullptr;           // device [kBoundsLen] batch bounds of the fixed-point scales
                                       // (DP: the max over ranks)
   hipEvent_t ev_start = nullptr, ev_done = nullptr;
-  // compute stream: the batch's head (batch init .. weight gather) began /
-  // ended -- per buffer, since the next batch's head may be enqueued before
-  // this batch's results are read (LREngine::issue_head)
-  hipEvent_t ev_h0 = nullptr, ev_h1 = nullptr;
   // guarded by LREngine::mu_
   int state = 0;                      // 0 free, 1 being prepared, 2 prepared
   int slot = -1;
@@ -266,9 +262,6 @@ class LREngine {
   void free_prepared(PrepBuf& b);
   void ensure_compact(int64_t ns);
   void ensure_part(int64_t n);
-  // The head of a prepared batch on the compute stream: wait for its prep,
-  // per-batch state, |w|^2, gather of its compact weights.
-  void issue_head(PrepBuf& pb);
   int64_t active_set_hint() const;
   void ensure_tier(PrepBuf& b, int64_t n_unique, hipStream_t s);
   void prepare_local(PrepBuf& b, int slot, int64_t now_ms, hipStream_t s);
@@ -301,12 +294,6 @@ class LREngine {
   PrepBuf pb_[2];
   int last_buf_ = -1;               // buffer of the last trained batch (debug_*)
   bool overlap_ = true;
-  // The next prepared batch's head enqueued at the end of train(), before its
-  // stream sync, so the compute stream does not idle through the host's turn
-  // between two batches (TWTML_HEAD_AHEAD=0: off).  head_buf_: the buffer
-  // whose head is on the stream; cleared when anything could make it stale.
-  bool head_ahead_ = true;
-  PrepBuf* head_buf_ = nullptr;
   int64_t* ready_host_ = nullptr;   // DP: pinned mapped ready word (next packet's pairs + 1; 0: none)
   int64_t* dnu_ = nullptr;          // DP: device [world] active-set sizes (in-line all-gather sizing)
   int64_t* hnu_ = nullptr;          // pinned [world]
