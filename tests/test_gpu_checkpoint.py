@@ -64,13 +64,15 @@ def _run(tmp_path, interval, pool, n_batches, F=100_000_000):
     eng.set_weights(np.zeros(eng.num_weights))
     job = LinearRegressionJob(conf, eng, None, 0, plot=False)
     lat = []
-    for t in range(n_batches):
-        raw = pool[t % len(pool)].with_time(NOW + t * 5000)
-        nxt = pool[(t + 1) % len(pool)].with_time(NOW + (t + 1) * 5000)
-        t0 = time.perf_counter()
-        job.on_batch(SimpleNamespace(raw=raw), raw.batch_time_ms)
-        lat.append(time.perf_counter() - t0)
-        eng.prefetch(nxt)                       # the receiver's next batch, as the app's scheduler does
+    from twitter_stream_ml_amd.utils.gil import streaming_latency
+    with streaming_latency():   # as the driver streams (apps/linear_regression.py main)
+        for t in range(n_batches):
+            raw = pool[t % len(pool)].with_time(NOW + t * 5000)
+            nxt = pool[(t + 1) % len(pool)].with_time(NOW + (t + 1) * 5000)
+            t0 = time.perf_counter()
+            job.on_batch(SimpleNamespace(raw=raw), raw.batch_time_ms)
+            lat.append(time.perf_counter() - t0)
+            eng.prefetch(nxt)                       # the receiver's next batch, as the app's scheduler does
     job.final_checkpoint()
     ckp = job.checkpointer
     w = eng.get_weights()
