@@ -245,7 +245,6 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
   // ranks' packets between two of t's GD iterations) the rest.
   overlap_ = cfg_.overlap != 0;
   if (const char* v = std::getenv("TWTML_OVERLAP")) overlap_ = overlap_ && v[0] != '0';
-  if (const char* v = std::getenv("TWTML_PREP_GATE")) prep_gate_ = v[0] != '0';
   TWTML_HIP_CHECK(hipSetDevice(device_));
   hipDeviceProp_t prop;
   TWTML_HIP_CHECK(hipGetDeviceProperties(&prop, device_));
@@ -269,7 +268,6 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
   TWTML_HIP_CHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
   raw_.init(cfg_.max_rows, text_bytes_for_units(cfg_.max_units));
   for (auto& e : ev_) TWTML_HIP_CHECK(hipEventCreate(&e));
-  TWTML_HIP_CHECK(hipEventCreateWithFlags(&gate_ev_, hipEventDisableTiming));
   upload_lower_tables(compute_, &lower_page_, &lower_blocks_);
   near_cap_ = tier_near_cap();
   if (const char* v = std::getenv("TWTML_NEAR_CAP"))   // tests / tuning: a smaller LDS tier
@@ -516,7 +514,6 @@ LREngine::~LREngine() {
   (void)hipDeviceSynchronize();
   raw_.release();
   for (auto& e : ev_) (void)hipEventDestroy(e);
-  if (gate_ev_) (void)hipEventDestroy(gate_ev_);
   for (auto& b : pb_) free_prepared(b);
   if (snap_stream_) {
     (void)hipStreamSynchronize(snap_stream_);
@@ -574,9 +571,6 @@ void LREngine::prepare_local(PrepBuf& pb, int slot, int64_t now_ms, hipStream_t 
   DevPrepared& prep = pb.dp;
   BatchResult& res = pb.res;
   res = BatchResult{};
-  // ahead of its batch: not before the batch training now passed its first
-  // GD iteration (a no-op for an in-line prep: that gate has completed)
-  if (prep_gate_) TWTML_HIP_CHECK(hipStreamWaitEvent(s, gate_ev_, 0));
   const DevRawBatch b = raw_.acquire(slot, s);
   res.n_raw = b.n;
   TWTML_HIP_CHECK(hipEventRecord(pb.ev_start, s));
@@ -926,7 +920,6 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred, int64_t plot_points) {
         ++comm_iters;
       }
       launch_sgd_update(sgd_, sp, fused ? sgd_.nparts : 0, s);
-      if (i == 1) open_prep_gate();
     }
     launch_sgd_finish(sgd_, sp, s);
     if (snap_guard_) {   // a checkpoint snapshot still reading the master weights
@@ -938,7 +931,6 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred, int64_t plot_points) {
     if (itime) print_iter_timing(iters);
   }
   if (n_glob <= 0 || diverged_) launch_norm_next(sgd_, false, s);   // weights unchanged: carry |w|^2 as is
-  open_prep_gate();   // (no-op if the first iteration opened it)
   TWTML_HIP_CHECK(hipEventRecord(ev_[2], s));
   th[2] = Clk::now();
   if (dp_) comm_->allreduce(sgd_.stats, 6, ncclFloat64, ncclSum, s);
@@ -1067,16 +1059,6 @@ void LREngine::prep_worker() {
 
 // Caller holds mu_: start preparing the next submitted slot if a buffer and
 // the prep thread are free.
-// The next batch's prep may start: gate_ev_ behind the first GD iteration on
-// the compute stream, then the prep thread is scheduled.
-void LREngine::open_prep_gate() {
-  if (gate_open_) return;
-  gate_open_ = true;
-  TWTML_HIP_CHECK(hipEventRecord(gate_ev_, compute_));
-  std::lock_guard<std::mutex> lk(mu_);
-  schedule_ahead_locked();
-}
-
 void LREngine::schedule_ahead_locked() {
   if (!overlap_ || job_ >= 0 || submitted_.empty()) return;
   int free_buf = -1;
@@ -1208,8 +1190,7 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred, int64_t 
       pb_[k].state = 2;
     }
     last_buf_ = k;
-    gate_open_ = !prep_gate_;
-    if (gate_open_) schedule_ahead_locked();   // batch t+1's prep overlaps batch t's training
+    schedule_ahead_locked();   // batch t+1's prep overlaps batch t's training
   }
   BatchResult res;
   const auto t_train = std::chrono::steady_clock::now();
@@ -1228,9 +1209,7 @@ BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred, int64_t 
     std::lock_guard<std::mutex> lk(mu_);
     pb_[k].state = 0;
     pb_[k].c1 = 0;
-    // gated: the next prep is scheduled by the next batch's first GD
-    // iteration (open_prep_gate), not here at the start of its training
-    if (!prep_gate_) schedule_ahead_locked();
+    schedule_ahead_locked();
   }
   return res;
 }

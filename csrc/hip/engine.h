@@ -294,14 +294,6 @@ class LREngine {
   PrepBuf pb_[2];
   int last_buf_ = -1;               // buffer of the last trained batch (debug_*)
   bool overlap_ = true;
-  // The next batch's prep starts on the device after this batch's first
-  // (stats) GD iteration: the prep thread is scheduled only once gate_ev_ is
-  // recorded behind it, and prepare_local's first op on the prep stream
-  // waits for it (TWTML_PREP_GATE=0: prep starts with the batch)
-  bool prep_gate_ = true;
-  hipEvent_t gate_ev_ = nullptr;
-  bool gate_open_ = true;   // this batch has scheduled the next one's prep
-  void open_prep_gate();
   int64_t* ready_host_ = nullptr;   // DP: pinned mapped ready word (next packet's pairs + 1; 0: none)
   int64_t* dnu_ = nullptr;          // DP: device [world] active-set sizes (in-line all-gather sizing)
   int64_t* hnu_ = nullptr;          // pinned [world]
