@@ -27,7 +27,9 @@ def server(tmp_path_factory):
     srv.stop()
 
 
-# ---- WebTestSuite (order-dependent, as in the reference) ------------------
+# ---- WebTestSuite (order-dependent in the reference: a get reads what the
+# previous test posted; each get here posts first, so the pair also holds
+# when pytest-xdist runs the tests on different workers) ------------------
 config_test = Config("100", "http://localhost:8888", ["101", "102"])
 stats_test = Stats(1000, 10, 2000, 15, 25)
 
@@ -37,6 +39,7 @@ def test_client_posts_config(server):
 
 
 def test_client_gets_correct_config(server):
+    test_client_posts_config(server)
     assert WebClient(server.url).config() == config_test
 
 
@@ -46,6 +49,7 @@ def test_client_posts_stats(server):
 
 
 def test_client_gets_correct_stats(server):
+    test_client_posts_stats(server)
     assert WebClient(server.url).stats() == stats_test
 
 
