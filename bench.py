@@ -61,7 +61,7 @@ def parse_args(argv=None):
     ap.add_argument("--k", type=int, default=1024, help="kmeans clusters")
     ap.add_argument("--text-dims", type=int, default=62, help="kmeans hashed bigram dims (+2 numeric)")
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", default="1000000",
                     help="raw tweets per GPU per step, or 'hbm': the largest micro-batch whose engine "
                          "fits --hbm-fraction of the GPU's free memory (config 5 sizing), capped by --batch-cap")
