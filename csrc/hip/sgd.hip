@@ -1139,8 +1139,9 @@ __device__ __forceinline__ bool far_seg_scan(int64_t e, int64_t n, uint32_t sl, 
 // [n_far k / nf, n_far (k + 1) / nf) of the tiered layout, read from the far
 // gradient sums (k_far_grad; DP: the all-reduced packed buffer).  The near
 // tiles and the far ranges run side by side instead of every block doing a
-// tile and then a grid-stride share of the far slots (r3: 26 us -> 17 us
-// on the wide profile).  Measured and reverted: far blocks summing their
+// tile and then a grid-stride share of the far slots (under prep overlap
+// the kernel tables show no measurable change: r3 27-32 us, r4 30-35 us;
+// 21 us alone, profiles/r4/pmc_summary.md).  Measured and reverted: far blocks summing their
 // range's CSC segments themselves (no k_far_grad) -- the far entries are
 // skewed over slot ranges, and the slowest block made the update ~100 us.
 // The grouping is a function of the layout only, so the fp64 norm partials
