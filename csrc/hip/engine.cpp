@@ -291,9 +291,8 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
   // Compact weights / packed gradients sized for the largest active set the
   // configuration allows (ids the hash can produce, at most one per unit of
   // a full batch; capped at 16M slots = 448 MB): growing them later means a
-  // stream sync + hipFree on the training thread -- a ~10 ms stall of the
-  // batch that first exceeds the capacity, measured mid-stream
-  // (tools/diag/plot_stall.py).  Larger active sets still grow on demand.
+  // stream sync + hipFree (a device-wide wait) on the training thread in the
+  // middle of the stream.  Larger active sets still grow on demand.
   ensure_compact((kNumNumeric + active_set_hint() + kPadSlots + 63) / 64 * 64);
   TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_out_),
                                 (32 + size_t(std::max(1, cfg_.num_iterations))) * sizeof(double),
