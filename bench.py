@@ -98,6 +98,9 @@ def parse_args(argv=None):
                     help="take the engine's DP path at world 1 through a world-1 RCCL communicator (every "
                          "collective issued on the compute stream) and report the per-iteration all-reduce "
                          "time")
+    ap.add_argument("--timeout", type=float, default=480.0,
+                    help="whole-run watchdog (s, 0 = off): on expiry every rank dumps its Python stacks and "
+                         "communicator counters, aborts the communicator and exits non-zero")
     ap.add_argument("--json-out", default="")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args(argv)
@@ -111,8 +114,14 @@ class Runner:
         self.lat, self.kept, self.iters, self.stage, self.extra = [], [], [], [], []
         self.comm = []            # (gradient all-reduces, their ms) per timed batch
         self.prestaged_at_t0 = 0  # batches of the timed window staged / submitted before t0
+        self.steps_done = 0
+        self.hang_at = 0          # TWTML_BENCH_HANG=<rank>:<step>: that rank hangs before that step
 
     def process(self, slot: int):
+        self.steps_done += 1
+        if self.hang_at and self.steps_done == self.hang_at:   # TWTML_BENCH_HANG (tests): never returns
+            while True:
+                time.sleep(3600)
         if self.is_km:
             return self.eng.process(slot, want_pred=False)
         return self.eng.process(slot, self.now_ms)
@@ -127,7 +136,7 @@ class Runner:
             self.iters.append(res["iterations"])
             self.stage.append((res["prep_ms"], res["train_ms"]))
             self.extra.append((res.get("tiered", False), res.get("n_unique", 0), res.get("n_near", 0)))
-            self.comm.append((res.get("comm_iters", 0), res.get("comm_ms", 0.0)))
+            self.comm.append((res.get("comm_iters", 0), res.get("comm_ms", 0.0), res.get("comm_bytes", 0)))
 
 
 def run_device_pipeline(r: Runner, pool, warmup: int, steps: int, sync):
@@ -261,7 +270,7 @@ def run_e2e(r: Runner, raws, u8s, views, ingest: str, warmup: int, steps: int, s
     return t0, t1
 
 
-def lr_config(args, rows: int, max_units: int, ingest: str):
+def lr_config(args, rows: int, max_units: int, ingest: str, dp: bool = False):
     from twitter_stream_ml_amd.ops.lr_engine import LRDeviceConfig
     return LRDeviceConfig(num_text_features=args.features, hash=args.hash,
                           step_size=args.step_size, num_iterations=args.iters, fraction=1.0,
@@ -269,7 +278,9 @@ def lr_config(args, rows: int, max_units: int, ingest: str):
                           sgd_grid=args.sgd_grid, ablate=args.ablate, tol=args.tol, dedup=bool(args.dedup),
                           hybrid=bool(args.hybrid), ingest=ingest if args.e2e else "wire",
                           force_dp=bool(getattr(args, "force_dp", False)),
-                          comm_timing=bool(getattr(args, "force_dp", False)))
+                          # the per-iteration gradient all-reduce is timed whenever the
+                          # engine is in DP (events around it on the compute stream)
+                          comm_timing=dp or bool(getattr(args, "force_dp", False)))
 
 
 def hbm_batch(args, synth, device: int, ingest: str):
@@ -292,6 +303,53 @@ def hbm_batch(args, synth, device: int, ingest: str):
     B = min(rows, args.batch_cap)
     return B, {"rule": f"hbm: {args.hbm_fraction:.2f} x {free / 2**30:.0f} GiB free of {total / 2**30:.0f} GiB",
                "hbm_max_rows": rows, "batch_cap": args.batch_cap}
+
+
+def final_model(eng, is_km: bool) -> np.ndarray:
+    """The replicated model state every DP rank must hold bit for bit."""
+    if is_km:
+        c, w = eng.get_state()
+        return np.concatenate([np.asarray(c, np.float64).ravel(), np.asarray(w, np.float64).ravel()])
+    return np.asarray(eng.get_weights())
+
+
+def rccl_version() -> str:
+    try:
+        from twitter_stream_ml_amd.ops._native import hip
+        return str(hip().rccl_version())
+    except Exception as e:   # noqa: BLE001 -- informational
+        return f"unknown ({e})"
+
+
+def start_watchdog(timeout_s: float, comm, rank: int):
+    """Whole-run watchdog (--timeout): a rank whose run does not finish in
+    time (a peer died inside a collective, a hung device) dumps every
+    thread's Python stack and its communicator counters to stderr, aborts
+    the communicator (RCCL: ncclCommAbort, so peers blocked in a collective
+    error out too) and exits with EXIT_HUNG -- the driver sees a non-zero
+    exit long before its own timeout.  No re-exec."""
+    if not timeout_s or timeout_s <= 0:
+        return None
+    import faulthandler
+    from twitter_stream_ml_amd.utils.faults import EXIT_HUNG, Watchdog
+
+    def on_timeout() -> None:
+        try:
+            sys.stderr.write(f"[bench rank {rank}] watchdog: run not finished after {timeout_s:.0f} s; "
+                             "Python stacks:\n")
+            faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+            if comm is not None:
+                sys.stderr.write(f"[bench rank {rank}] comm {comm.kind} world {comm.world} counters "
+                                 f"{dict(comm.counters())}\n")
+            sys.stderr.flush()
+            if comm is not None:
+                comm.abort()
+        finally:
+            os._exit(EXIT_HUNG)
+
+    wd = Watchdog(timeout_s, on_timeout, name="bench run")
+    wd.arm()
+    return wd
 
 
 def main(argv=None) -> int:
@@ -325,6 +383,7 @@ def main(argv=None) -> int:
         print("--force-dp is a world-1 RCCL mode", file=sys.stderr)
         return 2
     comm = D.make_comm(device, args.comm, force=args.force_dp)
+    watchdog = start_watchdog(args.timeout, comm, info.rank)
     ingest = args.ingest or "utf8"
 
     synth = SynthConfig.profile(args.profile, seed=args.seed + 7919 * info.rank)
@@ -348,7 +407,8 @@ def main(argv=None) -> int:
                               max_units=max_units, seed=args.seed, force_dp=args.force_dp)
         eng = DeviceKMeans(kcfg, device=device, comm=comm)
     else:
-        eng = DeviceLinearRegression(lr_config(args, B, max_units, ingest), device=device, comm=comm)
+        eng = DeviceLinearRegression(lr_config(args, B, max_units, ingest, dp=comm is not None), device=device,
+                                     comm=comm)
     u8s = []
     pinned = 0   # bytes of page-locked host memory this rank holds (staging views + registered pool)
     if args.e2e:
@@ -384,6 +444,9 @@ def main(argv=None) -> int:
         del pool_raw
     t_gen = time.time() - t_gen
     runner = Runner(eng, is_km, now_ms)
+    hang = os.environ.get("TWTML_BENCH_HANG", "")
+    if hang and int(hang.split(":")[0]) == info.rank:
+        runner.hang_at = int(hang.split(":")[1])
 
     h2d = {}
 
@@ -405,6 +468,8 @@ def main(argv=None) -> int:
         t0, t1 = run_e2e(runner, pool_raw, u8s, views, ingest, args.warmup, args.steps, sync)
     else:
         t0, t1 = run_device_pipeline(runner, pool, args.warmup, args.steps, sync)
+    # DP replicas must be bit-identical after the run (SURVEY §5 race detection)
+    replicas = D.replicas_identical(final_model(eng, is_km))
     elapsed = D.allreduce_max_scalar(t1 - t0)
     tweets = D.allreduce_sum_scalar(float(sum(runner.kept)))
     p50 = D.allreduce_max_scalar(float(np.median(runner.lat)))
@@ -487,8 +552,15 @@ def main(argv=None) -> int:
     if runner.comm and sum(c[0] for c in runner.comm) > 0:
         n_ar = sum(c[0] for c in runner.comm)
         out["grad_allreduce_per_step"] = round(n_ar / len(runner.comm), 2)
-        if args.force_dp:
-            out["grad_allreduce_us_per_iter"] = round(1e3 * sum(c[1] for c in runner.comm) / n_ar, 2)
+        # events around every gradient all-reduce (timed whenever the engine is in DP); the max over ranks
+        out["grad_allreduce_us_per_iter"] = round(D.allreduce_max_scalar(
+            1e3 * sum(c[1] for c in runner.comm) / n_ar), 2)
+        out["allreduce_bytes_per_iter"] = int(round(sum(c[2] for c in runner.comm) / n_ar))
+    out["replicas_identical"] = bool(replicas)
+    if comm is not None:
+        out["rccl_version"] = rccl_version()
+        out["comm_env"] = {k: v for k, v in sorted(os.environ.items())
+                           if k.startswith(("NCCL_", "RCCL_", "HSA_ENABLE_IPC"))}
     if host is not None:   # the host budget of every rank (8-rank rehearsal, README)
         h = np.asarray(host).reshape(-1, 3)
         out["per_rank_host"] = [{"peak_rss_mb": round(float(a), 1), "pinned_mb": round(float(b), 1),
@@ -504,6 +576,8 @@ def main(argv=None) -> int:
         if args.json_out:
             with open(args.json_out, "w") as fh:
                 fh.write(line + "\n")
+    if watchdog is not None:
+        watchdog.close()
     D.shutdown()
     return 0
 

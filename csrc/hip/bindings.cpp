@@ -60,6 +60,8 @@ static py::dict result_dict(BatchResult& r) {
   d["train_ms"] = r.train_ms;
   d["comm_iters"] = r.comm_iters;
   d["comm_ms"] = r.comm_ms;
+  d["comm_bytes"] = r.comm_bytes;
+  d["stats_spill"] = r.stats_spill;
   d["wait_ms"] = r.wait_ms;
   d["train_wall_ms"] = r.train_wall_ms;
   d["prepared_ahead"] = r.prepared_ahead;

@@ -1,9 +1,12 @@
 #include "comm.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <stdexcept>
+#include <string>
+#include <vector>
 
 #include "common.h"
 #include "trace.h"
@@ -233,12 +236,26 @@ static int op_code(ncclRedOp_t op) {
 // Floating-point sums over > 2 ranks depend on the summation order, and
 // gloo's order differs between ranks: the parts are all-gathered and every
 // rank adds them in rank order, so all replicas get the same bits.
+// TWTML_HOSTCOMM_ORDER=rotate (tests): rank r adds them starting at part r
+// instead, i.e. every rank in a different order -- the engines' collectives
+// are int64 sums (or fp64 sums of exact zeros), so their results must not
+// change (tests/test_gpu_dp_procs.py).
 template <typename T>
-static void sum_parts_in_order(T* parts, size_t count, int world) {
-  for (int r = 1; r < world; ++r) {
-    const T* p = parts + size_t(r) * count;
-    for (size_t i = 0; i < count; ++i) parts[i] += p[i];
+static void sum_parts_in_order(T* parts, size_t count, int world, int first) {
+  std::vector<T> acc(parts + size_t(first) * count, parts + size_t(first + 1) * count);
+  for (int k = 1; k < world; ++k) {
+    const T* p = parts + size_t((first + k) % world) * count;
+    for (size_t i = 0; i < count; ++i) acc[i] += p[i];
   }
+  std::copy(acc.begin(), acc.end(), parts);
+}
+
+static bool rotate_order() {
+  static const bool v = [] {
+    const char* e = std::getenv("TWTML_HOSTCOMM_ORDER");
+    return e && std::string(e) == "rotate";
+  }();
+  return v;
 }
 
 void HostComm::allreduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t s) {
@@ -251,8 +268,9 @@ void HostComm::allreduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t
     TWTML_HIP_CHECK(hipMemcpyAsync(h + bytes * size_t(rank_), buf, bytes, hipMemcpyDeviceToHost, s));
     TWTML_HIP_CHECK(hipStreamSynchronize(s));
     fn_(h, count, dt, -2, 0);
-    if (dt == ncclFloat64) sum_parts_in_order(reinterpret_cast<double*>(h), count, world_);
-    else sum_parts_in_order(reinterpret_cast<float*>(h), count, world_);
+    const int first = rotate_order() ? rank_ : 0;
+    if (dt == ncclFloat64) sum_parts_in_order(reinterpret_cast<double*>(h), count, world_, first);
+    else sum_parts_in_order(reinterpret_cast<float*>(h), count, world_, first);
     TWTML_HIP_CHECK(hipMemcpyAsync(buf, h, bytes, hipMemcpyHostToDevice, s));
     TWTML_HIP_CHECK(hipStreamSynchronize(s));
     return;

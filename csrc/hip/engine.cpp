@@ -278,6 +278,8 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
   sgd_.w64 = dmalloc<double>(size_t(nw));
   TWTML_HIP_CHECK(hipMemset(sgd_.w64, 0, sizeof(double) * size_t(nw)));  // Vectors.zeros
   sgd_.stats = dmalloc<double>(8);
+  sgd_.stat_i = dmalloc<int64_t>(16);
+  sgd_.stat_part = dmalloc<int64_t>(size_t(kStatBlocks) * 16);
   sgd_.state = dmalloc<double>(kStateLen);
   sgd_.loss_hist = dmalloc<double>(size_t(std::max(1, cfg_.num_iterations)) + 2);
   sgd_.itrec = dmalloc<double>((size_t(std::max(1, cfg_.num_iterations)) + 2) * kRecStride);
@@ -294,6 +296,7 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
   // stream sync + hipFree (a device-wide wait) on the training thread in the
   // middle of the stream.  Larger active sets still grow on demand.
   ensure_compact((kNumNumeric + active_set_hint() + kPadSlots + 63) / 64 * 64);
+  TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_stat_), 16 * sizeof(int64_t), hipHostMallocDefault));
   TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_out_),
                                 (32 + size_t(std::max(1, cfg_.num_iterations))) * sizeof(double),
                                 hipHostMallocDefault));
@@ -525,11 +528,13 @@ LREngine::~LREngine() {
     if (b) (void)hipFree(b);
   if (snap_total_) (void)hipHostFree(snap_total_);
   if (snap_stage_) (void)hipHostFree(snap_stage_);
-  void* bufs[] = {sgd_.gacc, sgd_.rbuf, sgd_.w64, sgd_.wc64, sgd_.wc32, sgd_.stats, sgd_.state,
+  void* bufs[] = {sgd_.gacc, sgd_.rbuf, sgd_.pbuf, sgd_.stat_i, sgd_.stat_part, sgd_.w64, sgd_.wc64, sgd_.wc32,
+                  sgd_.stats, sgd_.state,
                   sgd_.loss_hist, sgd_.pred_out, sgd_.real_out, sgd_.nrm, sgd_.wnorm_next, sgd_.part, sgd_.itrec, iter_tdbg_,
                   lower_page_, lower_blocks_};
   for (void* b : bufs) if (b) (void)hipFree(b);
   if (host_out_) (void)hipHostFree(host_out_);
+  if (host_stat_) (void)hipHostFree(host_stat_);
   if (plot_host_) (void)hipHostFree(plot_host_);
   if (host_flags_) (void)hipHostFree(host_flags_);
   if (ready_host_) (void)hipHostFree(ready_host_);
@@ -709,6 +714,17 @@ bool LREngine::issue_c1_inline(PrepBuf* pb) {
 void LREngine::prepare_global_dp(PrepBuf& pb, hipStream_t s) {
   TraceRange tr_prep("twtml.lr.prep_global");
   TWTML_HIP_CHECK(hipSetDevice(device_));
+  // A failure here (after the packet all-gather) raises on this rank only:
+  // its peers go on into the batch's first gradient all-reduce and wait
+  // there, and the batch watchdog (--batchTimeout; bench.py --timeout) or
+  // the launcher tearing the group down after this rank's exit ends them.
+  // TWTML_INJECT_GLOBAL_PREP_FAIL=<rank>:<n> (tests) fails this rank's n-th
+  // global prep.
+  if (const char* f = std::getenv("TWTML_INJECT_GLOBAL_PREP_FAIL")) {
+    int fr = -1, fn = 1;
+    if (std::sscanf(f, "%d:%d", &fr, &fn) >= 1 && fr == comm_->rank() && ++gprep_calls_ == fn)
+      throw std::runtime_error("injected global prep failure");
+  }
   const int world = world_, rank = comm_->rank();
   DevPrepared& prep = pb.dp;
   BatchResult& res = pb.res;
@@ -828,6 +844,7 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred, int64_t plot_points) {
     sgd_.fcsc_slot = prep.fcsc_slot;
     sgd_.far_n = prep.tparam + 2;
   }
+  if (!sgd_.pbuf) sgd_.pbuf = dmalloc<float>(size_t(prep.cap_rows16));
   launch_batch_init(sgd_, double(n_glob), cfg_.num_iterations + 2, s);  // state[5] = m (global kept rows)
   if (norm_age_ < 0 || norm_age_ >= kNormRefresh) {
     launch_norm2(sgd_.w64, num_weights(), &sgd_.state[4], sgd_, s);
@@ -907,6 +924,7 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred, int64_t plot_points) {
       // every rank launches the gradient kernel (an empty shard writes zero
       // partials) so every rank runs the convergence prologue
       launch_sgd_iter(sgd_, prep, sp, pb.host_counters[2], u16, grid, s);
+      if (i == 1) launch_batch_stats(sgd_, prep, s);   // exact moments of the prequential pass
       if (tiered) launch_far_grad(sgd_, sp, num_cu_, s);
       if (dp_) {
         // ONE collective per iteration: the packed int64 buffer (near
@@ -915,6 +933,7 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred, int64_t plot_points) {
         launch_sgd_reduce(sgd_, sp, s);
         if (comm_timing_) TWTML_HIP_CHECK(hipEventRecord(comm_ev_[size_t(2 * (i - 1))], s));
         comm_->allreduce(sgd_.gacc, size_t(sgd_.far_off + n_far), ncclInt64, ncclSum, s);
+        res.comm_bytes += int64_t(sizeof(int64_t)) * (sgd_.far_off + n_far);
         if (comm_timing_) TWTML_HIP_CHECK(hipEventRecord(comm_ev_[size_t(2 * (i - 1) + 1)], s));
         ++comm_iters;
       }
@@ -932,8 +951,14 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred, int64_t plot_points) {
   if (n_glob <= 0 || diverged_) launch_norm_next(sgd_, false, s);   // weights unchanged: carry |w|^2 as is
   TWTML_HIP_CHECK(hipEventRecord(ev_[2], s));
   th[2] = Clk::now();
-  if (dp_) comm_->allreduce(sgd_.stats, 6, ncclFloat64, ncclSum, s);
+  if (dp_) {
+    // the exact int64 moments (any summation order gives the same bits), then
+    // the fp64 sums of spill rows (zero unless a prediction left +-2^31)
+    comm_->allreduce(sgd_.stat_i, size_t(kStatI), ncclInt64, ncclSum, s);
+    comm_->allreduce(sgd_.stats, 6, ncclFloat64, ncclSum, s);
+  }
   TWTML_HIP_CHECK(hipMemcpyAsync(host_out_, sgd_.stats, 8 * sizeof(double), hipMemcpyDeviceToHost, s));
+  TWTML_HIP_CHECK(hipMemcpyAsync(host_stat_, sgd_.stat_i, size_t(kStatI) * sizeof(int64_t), hipMemcpyDeviceToHost, s));
   TWTML_HIP_CHECK(hipMemcpyAsync(host_out_ + 8, sgd_.state, 8 * sizeof(double), hipMemcpyDeviceToHost, s));
   TWTML_HIP_CHECK(hipMemcpyAsync(host_out_ + 16, sgd_.loss_hist,
                                  sizeof(double) * size_t(cfg_.num_iterations + 1),
@@ -959,7 +984,16 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred, int64_t plot_points) {
       res.real[i] = plot_host_[2 * i + 1];
     }
   }
-  for (int k = 0; k < 6; ++k) res.stats[k] = host_out_[k];
+  {
+    // exact moments (int64; squares from two 32-bit limbs, as 128-bit) plus
+    // the fp64 spill sums (0.0 unless a prediction left +-2^31: then exact)
+    const int64_t* si = host_stat_;
+    auto limbs = [](int64_t hi, int64_t lo) { return double((__int128)hi * 4294967296LL + lo); };
+    const double ex[6] = {double(si[0]), double(si[1]), limbs(si[3], si[4]), double(si[2]), limbs(si[5], si[6]),
+                          limbs(si[7], si[8])};
+    for (int k = 0; k < 6; ++k) res.stats[k] = ex[k] + host_out_[k];
+    res.stats_spill = si[9];
+  }
   const double* st = host_out_ + 8;
   res.converged = st[1] != 0.0;
   res.diverged = diverged_ || st[7] == 1.0;

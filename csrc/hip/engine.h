@@ -134,12 +134,14 @@ struct BatchResult {
   bool tiered = false;    // active set beyond LDS: tiered layout (near slots in LDS, far via CSC)
   int64_t n_near = 0;     // text slots in the LDS tier
   double stats[6] = {0, 0, 0, 0, 0, 0};  // n, sum y, sum y^2, sum p, sum p^2, sum (y-p)^2
+  int64_t stats_spill = 0;   // kept rows whose |y| or |prediction| >= 2^31 (fp64 moments, not order-exact)
   std::vector<double> loss_history;
   std::vector<float> pred;   // want_pred: rounded predictions of this rank's kept rows (or a sample)
   std::vector<float> real;   // ... and their labels
   float prep_ms = 0.f, train_ms = 0.f;
   int32_t comm_iters = 0;   // DP: gradient all-reduces issued (one per GD iteration)
   float comm_ms = 0.f;      // DP + comm_timing: their summed time on the compute stream
+  int64_t comm_bytes = 0;   // DP: bytes of those gradient all-reduces (packed int64 buffer)
   // host side of process(): waiting for / doing this batch's preparation, and
   // train() end to end (enqueue, early-exit polling, the result copies)
   float wait_ms = 0.f, train_wall_ms = 0.f;
@@ -321,10 +323,12 @@ class LREngine {
   int64_t near_cap_ = 0;          // tiered layout: LDS-resident text slots (tier_near_cap)
   bool force_tiered_ = false;     // TWTML_FORCE_TIERED=1: tiered layout for any active set (tests)
   int prep_calls_ = 0;            // local preps so far (TWTML_INJECT_PREP_FAIL, tests)
+  int gprep_calls_ = 0;           // DP global preps so far (TWTML_INJECT_GLOBAL_PREP_FAIL, tests)
   uint64_t* iter_tdbg_ = nullptr;
   uint8_t* lower_page_ = nullptr;
   uint16_t* lower_blocks_ = nullptr;
   double* host_out_ = nullptr;        // pinned [16 + iters]
+  int64_t* host_stat_ = nullptr;      // pinned [16]: exact batch moments (stat_i)
   float* plot_host_ = nullptr;        // mapped pinned [2 max_rows]: sampled (pred, real) pairs
   float* plot_dev_ = nullptr;         // ... its device address (k_plot_sample writes it)
   double* host_flags_ = nullptr;      // pinned [iters + 1] convergence flag per iteration

@@ -260,7 +260,10 @@ struct DevSgd {
   int64_t* gacc;
   int64_t far_off;      // = nl + tail_len
   int32_t tail_len;
-  double* stats;        // [8] n, sum_y, sum_y2, sum_p, sum_p2, sum_e2, -, -
+  double* stats;        // [8] fp64 moments of the spill rows (k_batch_stats): n, sum_y, sum_y2, sum_p, sum_p2, sum_e2
+  int64_t* stat_i;      // [kStatI] exact int64 batch moments (k_batch_stats)
+  int64_t* stat_part;   // [kStatBlocks][16] block partials of k_batch_stats
+  float* pbuf;          // [R16] rounded prediction per sorted position (iteration 1)
   double* state;        // [kStateLen] see below
   double* loss_hist;    // [max_iters+1]
   float* pred_out;      // [R] rounded predictions in kept order (optional)
@@ -307,6 +310,14 @@ constexpr int kRecK = 3, kRecS = 4, kRecL = 5, kRecN = 6, kRecB = 10, kRecBad = 
 // one ready word per rank (next batch's local prep done: its active-set size + 1).
 constexpr int kTailLoss = 0, kTailM = 1, kTailVerdict = 2, kTailReady = 3;
 inline int32_t sgd_tail_len(int world) { return (kTailReady + world + 7) / 8 * 8; }
+
+// Exact int64 batch moments (stat_i): n, sum y, sum p, sum y^2 hi/lo,
+// sum p^2 hi/lo, sum (y-p)^2 hi/lo (32-bit limbs), spill rows.
+constexpr int kStatI = 10;
+constexpr int kStatBlocks = 256;   // k_batch_stats grid: stat_part holds kStatBlocks x 16 words
+// After iteration 1: the batch moments from pbuf and the labels (exact
+// int64; DP: all-reduced as ncclInt64 after the GD loop).
+void launch_batch_stats(const DevSgd& d, const DevPrepared& p, hipStream_t s);
 
 // Partial-row stride for a compact space of ns slots (multiple of 64).
 constexpr int64_t sgd_part_stride(int64_t ns) { return ns + 64; }

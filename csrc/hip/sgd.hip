@@ -280,7 +280,6 @@ struct RowAcc {
   int32_t qn = 0;     // sum rint(r n_t 2^N_t)
   int32_t ql = 0;     // sum rint((r 2^(L/2))^2) (t == 0)
   int32_t msum = 0;   // rows in the sampled gradient (t == 0, SAMPLE)
-  double st[6] = {0, 0, 0, 0, 0, 0};
 };
 
 struct RowIn {
@@ -299,9 +298,10 @@ __device__ __forceinline__ int32_t row_total(int32_t v) {
 }
 
 // Residual of the row at sorted position pos from its fixed-point text dot
-// (already summed over the row's 4 lanes); accumulates stats (iteration 1),
-// numeric-feature gradients, loss and the sampled count.  Returns r (0 for
-// rows outside the batch / the sample).
+// (already summed over the row's 4 lanes); STATS (iteration 1): the row's
+// rounded prediction to pbuf (k_batch_stats sums the moments exactly) and
+// the plot's pred / real; accumulates numeric-feature gradients, loss and
+// the sampled count.  Returns r (0 for rows outside the batch / the sample).
 template <bool STATS, bool SAMPLE>
 __device__ __forceinline__ float row_residual(int32_t dot_fix, const RowIn& ri, int64_t pos, int t,
                                               const DevSgd& d, const DevPrepared& p, const SgdParams& sp,
@@ -318,14 +318,14 @@ __device__ __forceinline__ float row_residual(int32_t dot_fix, const RowIn& ri, 
   const float r = in ? dot - ri.y : 0.f;
   if (t == 0) {
     if (STATS && valid) {
-      const double pr = round_half_away(double(dot));
+      // round half away of an fp32 value is an fp32 value (|dot| >= 2^23 is
+      // already an integer), so the float holds the prediction exactly
+      const float pr = float(round_half_away(double(dot)));
+      d.pbuf[pos] = pr;
       if (sp.want_pred) {
-        d.pred_out[p.perm[pos]] = float(pr);
+        d.pred_out[p.perm[pos]] = pr;
         d.real_out[p.perm[pos]] = ri.y;
       }
-      const double yd = double(ri.y), e = yd - pr;
-      acc.st[0] += 1.0; acc.st[1] += yd; acc.st[2] += yd * yd;
-      acc.st[3] += pr; acc.st[4] += pr * pr; acc.st[5] += e * e;
     }
     if (SAMPLE && in) ++acc.msum;
     const float u = r * sc.lhalf;
@@ -338,10 +338,8 @@ __device__ __forceinline__ float row_residual(int32_t dot_fix, const RowIn& ri, 
 // Workgroup epilogue: every workgroup writes one int64 partial row (plain
 // stores) that k_sgd_update / k_sgd_reduce sum (exact in any order):
 //   cols 0..3 numeric gradients (2^N_k), 4..far_base-1 text slots (2^S),
-//   far_base..nl-1 zero, nl loss (2^L), nl+1 sampled row count, nl+2..nl+7
-//   batch stats (fp64 bits, STATS: integer-valued, so their fp64 sums are
-//   exact too).
-constexpr int kPartVals = 12;
+//   far_base..nl-1 zero, nl loss (2^L), nl+1 sampled row count.
+constexpr int kPartVals = 6;
 
 template <bool STATS>
 __device__ __forceinline__ void part_scalars(const DevSgd& d, int64_t qn, int64_t ql, const RowAcc& acc,
@@ -354,29 +352,17 @@ __device__ __forceinline__ void part_scalars(const DevSgd& d, int64_t qn, int64_
   qn += shfl_xor_i64(qn, 32);
   ql = wave_sum_i64(ql);
   const int ms = wave_sum(acc.msum);
-  double st[6];
-#pragma unroll
-  for (int k = 0; k < 6; ++k) st[k] = STATS ? wave_sum(acc.st[k]) : 0.0;
   if (lane < kNumNumeric) wsc[w][lane] = qn;
   if (lane == 0) {
     wsc[w][4] = ql;
     wsc[w][5] = ms;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) wsc[w][6 + k] = __builtin_bit_cast(int64_t, st[k]);
   }
   __syncthreads();
   const int tid = threadIdx.x;
   if (tid < kPartVals) {
     const int nw = int(blockDim.x) / kWave;
-    int64_t v;
-    if (tid < 6) {
-      v = (wg_tot && tid < 5) ? (long long)wg_tot[tid] : 0;
-      for (int k = 0; k < nw; ++k) v += wsc[k][tid];
-    } else {
-      double t = 0.0;
-      for (int k = 0; k < nw; ++k) t += __builtin_bit_cast(double, wsc[k][tid]);
-      v = __builtin_bit_cast(int64_t, t);
-    }
+    int64_t v = (wg_tot && tid < 5) ? (long long)wg_tot[tid] : 0;
+    for (int k = 0; k < nw; ++k) v += wsc[k][tid];
     const int64_t col = tid < kNumNumeric ? int64_t(tid) : d.nl + (tid - kNumNumeric);
     prow[col] = v;
   }
@@ -1181,10 +1167,20 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
       return;
     }
   }
+  const int64_t ncols = ns + kPartVals - kNumNumeric;
+  // Single GPU: the first column tile's partial-row loads and its master
+  // weights are issued before the batch-state / record loads are waited on
+  // (they do not depend on them), so the kernel's dependent chain is one
+  // memory round trip shorter; a block that then finds the batch finished
+  // drops them.
+  const int64_t col_first = int64_t(blockIdx.x) * kWave;
+  const bool pre = nparts > 0 && int(blockIdx.x) < nt;
+  double wn_first = 0.0;
+  if (pre && w == 0 && col_first + lane < hi) wn_first = d.wc64[col_first + lane];
+  const int64_t gp_first = pre ? part_block_sum(d, col_first, ncols, ncols, nparts, red) : 0;
   if (d.state[0] != 0.0) return;
   const double* rec_it = sgd_rec(d, it);
   const int sS = int(rec_it[kRecS]), sL = int(rec_it[kRecL]);
-  const int64_t ncols = ns + kPartVals - kNumNumeric;
   // m: global kept rows, or the sampled row count of this iteration
   if (tid < kWave) {
     double m = d.state[5];
@@ -1206,13 +1202,14 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
   const double gsc = ldexp(1.0, -sS);
   double ds = 0.0, ws = 0.0, mx = 0.0;
   if (int(blockIdx.x) < nt) {
-    for (int64_t col0 = int64_t(blockIdx.x) * kWave; col0 < ncols; col0 += int64_t(nt) * kWave) {
-      const int64_t gp = nparts > 0 ? part_block_sum(d, col0, ncols, ns + 2, nparts, red) : 0;
+    for (int64_t col0 = col_first; col0 < ncols; col0 += int64_t(nt) * kWave) {
+      const bool first = pre && col0 == col_first;
+      const int64_t gp = first ? gp_first : (nparts > 0 ? part_block_sum(d, col0, ncols, ncols, nparts, red) : 0);
       const int64_t col = col0 + lane;
       if (w == 0 && col < ncols) {
         const int64_t gi = (nparts > 0 ? gp : (col <= ns + 1 ? d.gacc[col] : 0));
         if (col < hi) {
-          double wn = d.wc64[col];
+          double wn = first ? wn_first : d.wc64[col];
           if (m > 0.0) {
             const double g = double(gi) * (col < kNumNumeric ? ldexp(1.0, -int(rec_it[kRecN + col])) : gsc);
             const double step = alpha * (g / m);
@@ -1225,8 +1222,6 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
           if (col >= kNumNumeric) mx = fmax(mx, fabs(double(float(wn))));   // the next iteration's weight scale
         } else if (col == ns) {
           if (m > 0.0) d.loss_hist[it] = 0.5 * double(gi) * ldexp(1.0, -sL) / m;
-        } else if (col >= ns + 2 && nparts > 0) {
-          d.stats[col - ns - 2] += __builtin_bit_cast(double, gp);   // batch stats (iteration 1, single GPU)
         }
       }
     }
@@ -1294,9 +1289,9 @@ void launch_sgd_update(const DevSgd& d, const SgdParams& sp, int nparts, hipStre
 }
 
 // DP: cross-workgroup reduction of the partial rows into the packed buffer
-// gacc[0, nl + 2) (slots, loss, sampled count; the batch stats add into
-// d.stats), rank 0's verdict on update i-1 and this rank's ready word into
-// the tail -- all of it int64, ahead of the one all-reduce per iteration.
+// gacc[0, nl + 2) (slots, loss, sampled count), rank 0's verdict on update
+// i-1 and this rank's ready word into the tail -- all of it int64, ahead of
+// the one all-reduce per iteration.
 __global__ __launch_bounds__(1024) void k_sgd_reduce(DevSgd d, SgdParams sp) {
   __shared__ int64_t red[kUpdWaves][kWave];
   if (d.state[0] != 0.0) return;
@@ -1306,12 +1301,9 @@ __global__ __launch_bounds__(1024) void k_sgd_reduce(DevSgd d, SgdParams sp) {
   if (d.nparts > 0) {
     const int64_t ncols = nl + kPartVals - kNumNumeric;
     const int64_t col0 = int64_t(blockIdx.x) * kWave;
-    const int64_t v = skipped ? 0 : part_block_sum(d, col0, ncols, nl + 2, d.nparts, red);
+    const int64_t v = skipped ? 0 : part_block_sum(d, col0, ncols, ncols, d.nparts, red);
     const int64_t col = col0 + lane_id();
-    if (threadIdx.x < kWave && col < ncols) {
-      if (col <= nl + 1) d.gacc[col] = v;                                  // slots, loss, sampled count
-      else if (!skipped) d.stats[col - nl - 2] += __builtin_bit_cast(double, v);   // batch stats (iteration 1)
-    }
+    if (threadIdx.x < kWave && col < ncols) d.gacc[col] = v;   // slots, loss, sampled count
   }
   if (blockIdx.x == 0 && threadIdx.x < kWave) {
     // rank 0's verdict on update i-1 (converged, or this iteration's scales invalid)
@@ -1358,16 +1350,16 @@ void launch_sgd_finish(const DevSgd& d, const SgdParams& sp, hipStream_t s) {
 // so the result does not depend on the order of entries inside a slot or on
 // which wave adds first: deterministic across runs and DP ranks.
 // ---------------------------------------------------------------------------
+template <int kU>
 __global__ __launch_bounds__(256) void k_far_grad(DevSgd d, SgdParams sp) {
   if (d.state[0] != 0.0 || d.state[8] == double(sp.iteration)) return;   // done / DP pass skipped
   const int64_t n = *d.far_n;
   const int lane = lane_id();
   const float qscale = ldexpf(1.f, int(sgd_rec(d, sp.iteration)[kRecS]));
   unsigned long long* gfar = reinterpret_cast<unsigned long long*>(d.gacc + d.far_off);
-  // two 64-entry tiles per wave step: both tiles' (slot, row) loads, then
-  // both residual gathers, are in flight before the scans (half the
+  // kU 64-entry tiles per wave step: every tile's (slot, row) loads, then
+  // every residual gather, are in flight before the scans (1 / kU of the
   // dependent round trips of one tile per step)
-  constexpr int kU = 2;
   const int64_t stride = int64_t(gridDim.x) * 256 * kU;
   for (int64_t e0 = (int64_t(blockIdx.x) * 256 + (threadIdx.x & ~(kWave - 1))) * kU; e0 < n; e0 += stride) {
     uint32_t sl[kU], ps[kU];
@@ -1390,7 +1382,15 @@ __global__ __launch_bounds__(256) void k_far_grad(DevSgd d, SgdParams sp) {
 }
 
 void launch_far_grad(const DevSgd& d, const SgdParams& sp, int num_cu, hipStream_t s) {
-  hipLaunchKernelGGL(k_far_grad, dim3(std::max(1, num_cu * 4)), dim3(256), 0, s, d, sp);
+  static const int ku = [] {
+    const char* e = std::getenv("TWTML_FAR_U");   // tiles per wave step (A/B): 2, 4 or 8
+    const int v = e ? std::atoi(e) : 2;
+    return v == 4 || v == 8 ? v : 2;
+  }();
+  const dim3 g(std::max(1, num_cu * 4));
+  if (ku == 8) hipLaunchKernelGGL(k_far_grad<8>, g, dim3(256), 0, s, d, sp);
+  else if (ku == 4) hipLaunchKernelGGL(k_far_grad<4>, g, dim3(256), 0, s, d, sp);
+  else hipLaunchKernelGGL(k_far_grad<2>, g, dim3(256), 0, s, d, sp);
 }
 
 // ---------------------------------------------------------------------------
@@ -1520,6 +1520,7 @@ __global__ void k_batch_init(DevSgd d, double m_global, int n_loss) {
   const int i = threadIdx.x;
   if (i < kStateLen) d.state[i] = i == 5 ? m_global : 0.0;
   if (i < 8) d.stats[i] = 0.0;
+  if (i < kStatI) d.stat_i[i] = 0;
   for (int k = i; k < n_loss; k += blockDim.x) d.loss_hist[k] = 0.0;
 }
 
@@ -1580,6 +1581,99 @@ void launch_batch_bounds(const DevPrepared& p, double* out, hipStream_t s, bool 
   if (!zeroed) TWTML_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(double) * kBoundsLen, s));
   const int grid = int(std::max<int64_t>(1, std::min<int64_t>((p.cap_rows + kBlock - 1) / kBlock, 256)));
   hipLaunchKernelGGL(k_batch_bounds, dim3(grid), dim3(kBlock), 0, s, p, out);
+}
+
+// ---------------------------------------------------------------------------
+// Exact batch statistics (K7; LinearRegression.scala:59-65: count, stdev of
+// the labels and of the rounded predictions, MSE).  Every kept row's label y
+// (a retweet count) and rounded prediction p (pbuf, written by iteration 1)
+// are integers, so with |y|, |p| < 2^31 the six moments are int64 sums --
+// n, sum y, sum p exactly, y^2 / p^2 / (y - p)^2 (< 2^64) in two 32-bit limbs
+// each -- which no summation order changes: one GPU, any DP sharding and any
+// all-reduce order (ncclInt64) give the same bits.  Rows outside that range
+// (predictions beyond 2^31 retweets: a model close to divergence) are
+// counted and summed in fp64 ("spill"; DP order then matters for them only).
+// Block partials -> stat_part, one wave adds them in block order
+// (k_batch_stats_fin): deterministic, no atomics.
+//   stat_i: [0] n  [1] sum y  [2] sum p  [3,4] sum y^2 hi/lo  [5,6] sum p^2
+//           hi/lo  [7,8] sum (y-p)^2 hi/lo  [9] spill rows
+//   stats (fp64, spill rows): [0] n [1] sum y [2] sum y^2 [3] sum p [4] sum p^2 [5] sum (y-p)^2
+// ---------------------------------------------------------------------------
+constexpr int kStatThreads = 256;
+
+__global__ __launch_bounds__(kStatThreads) void k_batch_stats(DevSgd d, const float* y, const int64_t* counters) {
+  __shared__ int64_t wi[kStatThreads / kWave][kStatI];
+  __shared__ double wf[kStatThreads / kWave][6];
+  // no prequential pass on this batch (diverged at iteration 1; DP: skipped)
+  const bool none = d.state[0] != 0.0 || d.state[8] == 1.0;
+  const int64_t n_kept = none ? 0 : counters[0];
+  int64_t a[kStatI];
+  double f[6];
+#pragma unroll
+  for (int k = 0; k < kStatI; ++k) a[k] = 0;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) f[k] = 0.0;
+  constexpr float kLim = 2147483648.0f;   // 2^31
+  for (int64_t pos = int64_t(blockIdx.x) * kStatThreads + threadIdx.x; pos < n_kept;
+       pos += int64_t(gridDim.x) * kStatThreads) {
+    const float yv = y[pos], pv = d.pbuf[pos];
+    if (fabsf(yv) < kLim && fabsf(pv) < kLim) {   // NaN fails the test: spill
+      const int64_t Y = int64_t(yv), P = int64_t(pv);
+      const uint64_t ay = uint64_t(Y < 0 ? -Y : Y), ap = uint64_t(P < 0 ? -P : P);
+      const int64_t E = Y - P;
+      const uint64_t ae = uint64_t(E < 0 ? -E : E);   // < 2^32
+      const uint64_t y2 = ay * ay, p2 = ap * ap, e2 = ae * ae;
+      a[0] += 1; a[1] += Y; a[2] += P;
+      a[3] += int64_t(y2 >> 32); a[4] += int64_t(y2 & 0xFFFFFFFFull);
+      a[5] += int64_t(p2 >> 32); a[6] += int64_t(p2 & 0xFFFFFFFFull);
+      a[7] += int64_t(e2 >> 32); a[8] += int64_t(e2 & 0xFFFFFFFFull);
+    } else {
+      const double yd = double(yv), pd = double(pv), e = yd - pd;
+      a[9] += 1;
+      f[0] += 1.0; f[1] += yd; f[2] += yd * yd; f[3] += pd; f[4] += pd * pd; f[5] += e * e;
+    }
+  }
+  const int w = threadIdx.x / kWave;
+#pragma unroll
+  for (int k = 0; k < kStatI; ++k) {
+    const int64_t v = wave_sum_i64(a[k]);
+    if (lane_id() == 0) wi[w][k] = v;
+  }
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const double v = wave_sum(f[k]);
+    if (lane_id() == 0) wf[w][k] = v;
+  }
+  __syncthreads();
+  int64_t* out = d.stat_part + int64_t(blockIdx.x) * 16;
+  if (threadIdx.x < kStatI) {
+    int64_t v = 0;
+    for (int k = 0; k < kStatThreads / kWave; ++k) v += wi[k][threadIdx.x];
+    out[threadIdx.x] = v;
+  } else if (threadIdx.x < kStatI + 6) {
+    double v = 0.0;
+    for (int k = 0; k < kStatThreads / kWave; ++k) v += wf[k][threadIdx.x - kStatI];
+    out[threadIdx.x] = __builtin_bit_cast(int64_t, v);
+  }
+}
+
+__global__ void k_batch_stats_fin(DevSgd d, int nblocks) {
+  const int k = lane_id();
+  if (k >= kStatI + 6) return;
+  int64_t v = 0;
+  double vf = 0.0;
+  for (int b = 0; b < nblocks; ++b) {   // block order: deterministic
+    const int64_t x = d.stat_part[int64_t(b) * 16 + k];
+    if (k < kStatI) v += x;
+    else vf += __builtin_bit_cast(double, x);
+  }
+  if (k < kStatI) d.stat_i[k] = v;
+  else d.stats[k - kStatI] = vf;
+}
+
+void launch_batch_stats(const DevSgd& d, const DevPrepared& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_batch_stats, dim3(kStatBlocks), dim3(kStatThreads), 0, s, d, p.y, p.counters);
+  hipLaunchKernelGGL(k_batch_stats_fin, dim3(1), dim3(kWave), 0, s, d, kStatBlocks);
 }
 
 // ---------------------------------------------------------------------------

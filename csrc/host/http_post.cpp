@@ -11,6 +11,10 @@
 // read-to-close bodies.
 #include "http_post.h"
 
+#include <charconv>
+#include <climits>
+#include <cstdint>
+
 #include <netdb.h>
 #include <poll.h>
 #include <sys/socket.h>
@@ -131,16 +135,31 @@ std::string lower(std::string s) {
   return s;
 }
 
+// A header number (decimal Content-Length, hex chunk size, optional chunk
+// extensions after ';'): malformed or out-of-range text is an HttpError
+// (-> requests.ConnectionError in report/http.py), never std::invalid_argument.
+uint64_t parse_number(const std::string& text, int base, const char* what) {
+  size_t b = text.find_first_not_of(" \t");
+  size_t e = text.find_first_of(base == 16 ? "; \t" : " \t", b == std::string::npos ? 0 : b);
+  if (b == std::string::npos) b = e = text.size();
+  if (e == std::string::npos) e = text.size();
+  uint64_t v = 0;
+  const auto r = std::from_chars(text.data() + b, text.data() + e, v, base);
+  if (b == e || r.ec != std::errc() || r.ptr != text.data() + e) fail(std::string("malformed ") + what + ": '" +
+                                                                          text.substr(0, 40) + "'");
+  return v;
+}
+
 std::string dechunk(const std::string& in) {
   std::string out;
   size_t i = 0;
   for (;;) {
     const size_t eol = in.find("\r\n", i);
     if (eol == std::string::npos) fail("truncated chunked body");
-    const size_t n = std::stoul(in.substr(i, eol - i), nullptr, 16);
+    const uint64_t n = parse_number(in.substr(i, eol - i), 16, "chunk size");
     i = eol + 2;
     if (n == 0) return out;
-    if (i + n > in.size()) fail("truncated chunked body");
+    if (n > in.size() || i + n > in.size()) fail("truncated chunked body");
     out.append(in, i, n);
     i += n + 2;
   }
@@ -155,7 +174,9 @@ HttpResponse http_post(const std::string& host, int port, const std::string& pat
   sock.fd = connect_to(host, port, deadline);
   std::string req;
   req.reserve(256 + body.size());
-  req += "POST " + path + " HTTP/1.1\r\nHost: " + host + ":" + std::to_string(port) +
+  // an IPv6 literal goes in brackets in the Host header (RFC 7230 5.4)
+  const bool v6 = host.find(':') != std::string::npos && host.front() != '[';
+  req += "POST " + path + " HTTP/1.1\r\nHost: " + (v6 ? "[" + host + "]" : host) + ":" + std::to_string(port) +
          "\r\nContent-Type: application/json\r\nAccept: application/json\r\nConnection: close\r\n"
          "Content-Length: " + std::to_string(body.size()) + "\r\n" + extra_headers + "\r\n";
   req += body;
@@ -181,7 +202,11 @@ HttpResponse http_post(const std::string& host, int port, const std::string& pat
       const std::string k = lower(line.substr(0, c));
       std::string v = line.substr(c + 1);
       v.erase(0, v.find_first_not_of(" \t"));
-      if (k == "content-length") content_length = std::stoll(v);
+      if (k == "content-length") {
+        const uint64_t n = parse_number(v, 10, "Content-Length");
+        if (n > uint64_t(INT64_MAX)) fail("Content-Length out of range");
+        content_length = int64_t(n);
+      }
       if (k == "transfer-encoding" && lower(v).find("chunked") != std::string::npos) chunked = true;
     }
     i = e < head.size() ? e : std::string::npos;

@@ -155,3 +155,15 @@ def test_positions_survive_a_slow_writer(tmp_path):
     ck.after_batch(61, 610, 610, force=True)
     other.record(61, 427)
     assert len(StreamPositions(path, 0).history()) <= 16 + 1
+
+
+def test_positions_history_is_bounded_without_a_model(tmp_path):
+    """with no model readable on this rank's filesystem (every
+    write failing, or a rank that cannot see rank 0's directory) the floor
+    is 0; the history must still stay bounded (keep * 64 entries)."""
+    from twitter_stream_ml_amd.checkpoint.stream_state import StreamPositions
+    sp = StreamPositions(str(tmp_path / "ckpt"), rank=1, keep=4)
+    for b in range(1, 1001):
+        sp.record(b, 10 * b)
+    h = sp.history()
+    assert len(h) == 4 * 64 and max(h) == 1000 and h[1000] == 10000

@@ -177,3 +177,11 @@ def test_extension_flags():
                                   "--hash", "murmur3", "--numBatches", "3"])
     assert (conf.source, conf.batchSize, conf.hash, conf.numBatches) == ("replay:x.jsonl", 64,
                                                                         "murmur3", 3)
+
+
+def test_plot_points_default_plots_every_row():
+    """the reference appends every kept row's (real, pred) pair
+    (LinearRegression.scala:76-77), so the default plotPoints is 0 (= all);
+    a cap is opt-in."""
+    assert ConfArguments().parse([]).plotPoints == 0
+    assert ConfArguments().parse(["--plotPoints", "10000"]).plotPoints == 10000

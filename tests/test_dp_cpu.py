@@ -138,3 +138,72 @@ def test_dp_driver_plot_samples_reach_rank0(tmp_path):
         assert all(100 <= v <= 1000 for v in series[0])                      # real: kept retweet counts
     recs = [json.loads(l) for l in open(tmp_path / "m0.jsonl") if '"summary"' not in l]
     assert len(recs) == 3 and all("step_ms" in r for r in recs)
+
+
+class _RecSession:
+    """append_plot recorder standing in for rank 0's SessionStats."""
+
+    def __init__(self):
+        self.plots = []
+
+    def append_plot(self, batch, real_sd, pred_sd, real, pred):
+        self.plots.append((int(batch), np.array(real), np.array(pred)))
+
+
+def _stall_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import json
+    import time
+    from twitter_stream_ml_amd.parallel import dist as D
+    from twitter_stream_ml_amd.report import plot_shipper as P
+    D.init_distributed(backend="gloo")
+    real_gather = D.gather_parts
+    calls = [0]
+
+    def slow_gather(arr, group=None):   # the last rank's gathers stall for the first batches
+        calls[0] += 1
+        if rank == world - 1 and calls[0] <= 6:
+            time.sleep(0.25)
+        return real_gather(arr, group)
+
+    D.gather_parts = slow_gather
+    sess = _RecSession() if rank == 0 else None
+    sh = P.PlotShipper(sess, rank, world, maxsize=4)
+    n = 60
+    worst = 0.0
+    for b in range(n):   # the "training thread": one submit per batch, never held up
+        real = np.full(3, 1000.0 * rank + b)   # encodes (rank, batch)
+        t = time.perf_counter()
+        sh.submit((b, b + 1, 0, 0, 0), real, -real)
+        worst = max(worst, time.perf_counter() - t)
+        time.sleep(0.002)
+    sh.close(timeout=60)
+    out = {"worst_submit_s": worst, "dropped": sh.dropped, "shipped": sh.shipped, "stopped": sh.stopped}
+    if rank == 0:
+        out.update(skipped=sh.skipped, plots=[(b, r.tolist()) for b, r, _ in sess.plots])
+    with open(os.path.join(out_dir, f"s{rank}.json"), "w") as fh:
+        json.dump(out, fh)
+    D.barrier()
+    D.shutdown()
+
+
+def test_plot_shipper_backpressure_never_blocks_training(tmp_path):
+    """A stalled gather on one rank: submit() returns at
+    once on every rank, samples beyond the backlog are dropped, every rank
+    still gathers every batch in order (paired), and rank 0 plots only
+    batches for which it holds every rank's sample of that same batch."""
+    import json
+    world = 2
+    mp.start_processes(_stall_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    outs = [json.load(open(tmp_path / f"s{r}.json")) for r in range(world)]
+    for o in outs:
+        assert o["worst_submit_s"] < 0.05, o
+        assert not o["stopped"] and o["shipped"] == 60
+    assert outs[world - 1]["dropped"] > 0 or outs[0]["dropped"] > 0   # the stall did fill a backlog
+    plots, skipped = outs[0]["plots"], outs[0]["skipped"]
+    assert len(plots) + skipped == 60 and skipped > 0
+    for batch, real in plots:
+        b = batch - 1
+        assert real == [float(b)] * 3 + [1000.0 + b] * 3   # rank 0's then rank 1's sample of batch b

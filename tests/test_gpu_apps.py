@@ -116,7 +116,7 @@ def test_lr_driver_plot_does_not_stall_training(hip_module, tmp_path, monkeypatc
     from twitter_stream_ml_amd.apps import linear_regression as app
     base = ["--master", "rocm[1]", "--twtweb", "http://127.0.0.1:9", "--source", "replay:synthetic:wide:4",
             "--seconds", "0", "--batchSize", "1000000", "--sourceRate", "0", "--numBatches", "40",
-            "-f", "1000000"]
+            "-f", "1000000", "--plotPoints", "10000"]
 
     def p99(path, lightning):
         monkeypatch.setenv("TWTML_METRICS", str(path))

@@ -58,8 +58,11 @@ def _batches(profile, rows, n, seed):
 
 
 def _worker(rank, world, port, out_dir):
+    # every rank adds the parts of a floating-point all-reduce in a different
+    # order (csrc/hip/comm.cpp): the engines' collectives are int64 sums, so
+    # DP must still equal one engine bit for bit
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), TWTML_HOSTCOMM_ORDER="rotate")
     import torch  # noqa: F401  (binds the HIP runtime before the engine loads)
     from twitter_stream_ml_amd.ops.kmeans_engine import DeviceKMeans
     from twitter_stream_ml_amd.ops.lr_engine import DeviceLinearRegression
@@ -75,6 +78,7 @@ def _worker(rank, world, port, out_dir):
             eng.prefetch(sh)
         for sh in shards:
             r = eng.train_batch(sh, want_pred=False)
+            assert r["stats_spill"] == 0   # every moment went through the exact int64 path
             meta.append([r["iterations"], r["n_kept_global"], r["n_unique"], int(r["tiered"])]
                         + list(r["stats"]))
         out[f"lr{ci}_w"] = eng.get_weights()
@@ -117,8 +121,9 @@ def test_lr_dp_processes_equal_single_engine(dp_runs, ci):
             stats = d[f"lr{ci}_meta"][t][4:]
             assert (int(it), int(kept), int(nu), bool(tr)) == (r1["iterations"], r1["n_kept"],
                                                                 r1["n_unique"], tiered)
-            # exact GD arithmetic (int32 / int64 fixed point, csrc/hip/sgd.hip): the
-            # prequential stats and the weights of DP over any sharding are the
+            # exact GD arithmetic (int32 / int64 fixed point, csrc/hip/sgd.hip) and
+            # int64 batch moments (k_batch_stats): the prequential stats and the
+            # weights of DP over any sharding and any summation order are the
             # single engine's, bit for bit
             np.testing.assert_array_equal(stats, np.asarray(r1["stats"]))
     w1 = single.get_weights()
@@ -142,17 +147,66 @@ def test_kmeans_dp_processes(dp_runs):
             np.testing.assert_array_equal(d[f"km{t}_w"], w1)
 
 
-def test_torchrun_bench_two_ranks_gloo(hip_module):
-    """The driver's launcher on one GPU: 2 ranks, engine DP through gloo."""
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+def _torchrun_bench(nproc, extra, env_extra=None, timeout=300):
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4", **(env_extra or {}))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--comm", "gloo", "--batch", "100000", "--steps", "3", "--warmup", "1",
-           "--pool", "2"]
-    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+           "--gpus", str(nproc), "--comm", "gloo"] + extra
+    return subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.parametrize("nproc", [2, 4])
+def test_torchrun_bench_gloo(hip_module, nproc):
+    """The driver's launcher on one GPU: N ranks, engine DP through gloo.
+    The JSON carries what a first real multi-GPU run needs to be diagnosed
+    (VERDICT r4 #2): per-iteration all-reduce time and bytes, the RCCL
+    version and NCCL_/RCCL_ environment, and the end-of-run replica check."""
+    p = _torchrun_bench(nproc, ["--batch", "100000", "--steps", "3", "--warmup", "1", "--pool", "2"])
     assert p.returncode == 0, p.stderr[-4000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2-gloo"
-    assert d["config"]["global_batch"] == 200000 and d["value"] > 0
+    assert d["n_gpus"] == nproc and d["config"]["parallelism"] == f"dp{nproc}-gloo"
+    assert d["config"]["global_batch"] == 100000 * nproc and d["value"] > 0
+    assert d["replicas_identical"] is True
+    assert d["grad_allreduce_per_step"] > 1 and d["grad_allreduce_us_per_iter"] > 0
+    # one packed int64 buffer per GD iteration (near columns + tail + far
+    # slots), averaged over the window's batches
+    assert d["allreduce_bytes_per_iter"] > 8 * 64
+    assert isinstance(d["rccl_version"], str) and d["rccl_version"]
+    assert isinstance(d["comm_env"], dict) and d["comm_env"].get("HSA_ENABLE_IPC_MODE_LEGACY") == "0"
+    print(f"dp{nproc}: {d['grad_allreduce_us_per_iter']} us / {d['allreduce_bytes_per_iter']} B per all-reduce")
+
+
+def test_torchrun_bench_hang_exits_nonzero(hip_module):
+    """A rank that hangs (TWTML_BENCH_HANG=1:2: rank 1 never processes its
+    second step) leaves rank 0 blocked in a collective; the bench watchdog
+    dumps the stacks, aborts the communicator and exits non-zero on every
+    rank well inside the driver's timeout."""
+    import time
+    t = time.monotonic()
+    p = _torchrun_bench(2, ["--batch", "50000", "--steps", "3", "--warmup", "1", "--pool", "2",
+                            "--timeout", "40"], env_extra={"TWTML_BENCH_HANG": "1:2"}, timeout=240)
+    took = time.monotonic() - t
+    assert p.returncode != 0, p.stdout[-2000:]
+    assert "watchdog: run not finished" in p.stderr, p.stderr[-4000:]
+    assert "Python stacks" in p.stderr and "counters" in p.stderr
+    print(f"hung run exited {p.returncode} after {took:.1f} s")
+    assert took < 200
+
+
+def test_torchrun_bench_global_prep_failure_ends_the_group(hip_module):
+    """a failure in the DP global prep (after the packet
+    all-gather) raises on that rank only; its peers wait in the batch's
+    first gradient all-reduce.  The group still ends promptly and non-zero:
+    the failing rank exits, the launcher tears the others down, and the
+    bench watchdog bounds whatever is left."""
+    import time
+    t = time.monotonic()
+    p = _torchrun_bench(2, ["--batch", "50000", "--steps", "3", "--warmup", "1", "--pool", "2",
+                            "--timeout", "60"], env_extra={"TWTML_INJECT_GLOBAL_PREP_FAIL": "1:2"}, timeout=240)
+    took = time.monotonic() - t
+    assert p.returncode != 0, p.stdout[-2000:]
+    assert "injected global prep failure" in p.stderr, p.stderr[-4000:]
+    print(f"global prep failure: group exited {p.returncode} after {took:.1f} s")
+    assert took < 200

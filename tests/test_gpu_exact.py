@@ -113,3 +113,35 @@ def test_divergence_stops_training(hip_module):
     eng.set_weights(np.zeros_like(w))       # a new model trains again
     r = eng.train_batch(generate_batch(synth, 99 * 8000, 8000, batch_time_ms=NOW))
     assert r["diverged"] and r["stats"][0] > 0
+
+
+def test_batch_stats_exact_int64_and_spill(hip_module):
+    """the prequential moments are exact integers (k_batch_stats,
+    int64 with 32-bit limbs for the squares): n, sum y, sum y^2, sum p, sum p^2
+    and sum (y - p)^2 equal Python's exact integer sums of the engine's own
+    (label, rounded prediction) pairs, correctly rounded once.  Predictions
+    beyond 2^31 go through the counted fp64 spill path."""
+    from twitter_stream_ml_amd.ops.lr_engine import DeviceLinearRegression, LRDeviceConfig
+    F = 1 << 20
+    eng = DeviceLinearRegression(LRDeviceConfig(num_text_features=F, max_rows=8192, max_units=8192 * 300,
+                                                num_iterations=3), device=0)
+    synth = SynthConfig.profile("twitter", seed=21)
+
+    def exact(res):
+        y = [int(v) for v in np.asarray(res["real"], np.float64)]
+        p = [int(v) for v in np.asarray(res["pred"], np.float64)]
+        return [float(len(y)), float(sum(y)), float(sum(a * a for a in y)), float(sum(p)),
+                float(sum(b * b for b in p)), float(sum((a - b) ** 2 for a, b in zip(y, p)))]
+
+    w = np.random.default_rng(3).normal(0.0, 2e5, F + 4)
+    w[F:] = 0.0
+    # |predictions| ~1e6-1e7 (< 2^31): sum (y - p)^2 ~1e17, beyond fp64's exact
+    # integers -- only the int64 limbs give order-free bits
+    eng.set_weights(w)
+    res = eng.train_batch(generate_batch(synth, 0, 4000, batch_time_ms=NOW), want_pred=True)
+    assert res["stats_spill"] == 0
+    assert list(res["stats"]) == exact(res)
+    eng.set_weights(np.where(np.arange(F + 4) < F, 3e7, 0.0))   # every |prediction| >= 2^31
+    res = eng.train_batch(generate_batch(synth, 4000, 4000, batch_time_ms=NOW), want_pred=True)
+    assert res["stats_spill"] == res["n_kept"] > 0
+    np.testing.assert_allclose(res["stats"], exact(res), rtol=1e-12)

@@ -132,3 +132,44 @@ def test_post_releases_the_gil(srv):
     th.join()
     gaps = [b - a for a, b in zip(ticks, ticks[1:])]
     assert len(ticks) > 100 and max(gaps) < 0.1
+
+
+def _raw_server(response: bytes):
+    """One-shot TCP server that answers any request with `response` bytes."""
+    ls = socket.socket()
+    ls.bind(("127.0.0.1", 0))
+    ls.listen(1)
+
+    def run():
+        c, _ = ls.accept()
+        c.settimeout(5)
+        try:
+            c.recv(65536)
+            c.sendall(response)
+        finally:
+            c.close()
+            ls.close()
+
+    threading.Thread(target=run, daemon=True).start()
+    return ls.getsockname()[1]
+
+
+@pytest.mark.parametrize("response", [
+    b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\nConnection: close\r\n\r\nZZ\r\nabc\r\n0\r\n\r\n",
+    b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\nConnection: close\r\n\r\nffffffffffffffffff\r\nabc\r\n",
+    b"HTTP/1.1 200 OK\r\nContent-Length: 12abc\r\nConnection: close\r\n\r\nhello",
+    b"HTTP/1.1 200 OK\r\nContent-Length: 99999999999999999999999\r\nConnection: close\r\n\r\nhello",
+], ids=["bad-chunk", "huge-chunk", "bad-length", "huge-length"])
+def test_post_malformed_response_is_a_connection_error(response):
+    """a malformed chunk size or Content-Length is an HttpError
+    (-> requests.ConnectionError, what the Lightning / twtml-web clients
+    catch), not a ValueError / IndexError leaking from std::stoul."""
+    port = _raw_server(response)
+    with pytest.raises(requests.ConnectionError, match="malformed|range|truncated"):
+        post(f"http://127.0.0.1:{port}/x", b"{}", timeout=5.0)
+
+
+def test_chunk_extension_is_accepted():
+    port = _raw_server(b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\nConnection: close\r\n\r\n"
+                       b"3;ext=1\r\nabc\r\n0\r\n\r\n")
+    assert post(f"http://127.0.0.1:{port}/x", b"{}", timeout=5.0) == (200, b"abc")

@@ -215,6 +215,8 @@ class LinearRegressionJob:
                       [(float(a), float(b)) for a, b in zip(real[:10], pred[:10])])
         stats = (self.count, batch, mse, real_sd, pred_sd)
         if self.shipper is not None:   # every rank: its sample goes to rank 0 off this thread
+            if self.session is not None and self.rank == 0:
+                self.session.push_stats(*stats)   # not held back by the plot gather
             self.shipper.submit(stats, real, pred)
         elif self.session is not None and self.rank == 0:
             self.session.update(*stats, real, pred)

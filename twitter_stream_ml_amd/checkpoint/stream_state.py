@@ -89,6 +89,14 @@ class StreamPositions:
         for k in sorted(h)[:-self.keep]:
             if k < lo:
                 del h[k]
+        # hard cap: with no model readable on this rank's
+        # filesystem the floor stays 0 and nothing above prunes; keep the
+        # newest keep * 64 positions even then, so the file (rewritten on the
+        # training thread) cannot grow for the whole run
+        cap = self.keep * 64
+        if len(h) > cap:
+            for k in sorted(h)[:-cap]:
+                del h[k]
         os.makedirs(self.dir, exist_ok=True)
         fd, tmp = tempfile.mkstemp(prefix=".pos-", dir=self.dir)
         with os.fdopen(fd, "w") as fh:

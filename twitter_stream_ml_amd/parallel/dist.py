@@ -28,7 +28,8 @@ import numpy as np
 __all__ = ["DistInfo", "init_distributed", "dist_info", "make_rccl_comm", "make_comm", "broadcast_flag",
            "allreduce_fn",
            "barrier", "allreduce_max_scalar", "allreduce_sum_scalar", "allreduce_min_scalar", "shutdown",
-           "check_replicas", "replica_digest", "ReplicaDivergence", "gather_to_main"]
+           "check_replicas", "replica_digest", "replicas_identical", "ReplicaDivergence", "gather_to_main",
+           "gather_parts"]
 
 
 @dataclass(frozen=True)
@@ -234,6 +235,16 @@ def check_replicas(arr: np.ndarray, what: str = "model") -> None:
                                 f"{info.rank}: {d:#x})")
 
 
+def replicas_identical(arr: np.ndarray) -> bool:
+    """:func:`check_replicas` as a verdict instead of an exception: True when
+    every rank's replica has the same digest (True at world 1)."""
+    try:
+        check_replicas(arr)
+    except ReplicaDivergence:
+        return False
+    return True
+
+
 def broadcast_flag(flag: bool) -> bool:
     """Rank 0's boolean on every rank (True/False as the max of 0/1 with the
     other ranks contributing 0)."""
@@ -250,10 +261,17 @@ def gather_to_main(arr: np.ndarray, group=None) -> Optional[np.ndarray]:
     the driver for the Lightning plot; here each rank's sample is gathered
     once per batch by the plot shipper thread (``report/plot_shipper.py``) on
     a gloo ``group`` of its own, off the training path."""
+    parts = gather_parts(arr, group)
+    return None if parts is None else np.concatenate(parts)
+
+
+def gather_parts(arr: np.ndarray, group=None) -> Optional[list]:
+    """Every rank's 1-D float64 array on rank 0, one entry per rank in rank
+    order (None elsewhere)."""
     info = dist_info()
     a = np.ascontiguousarray(arr, dtype=np.float64).reshape(-1)
     if info.world <= 1:
-        return a
+        return [a]
     import torch
     import torch.distributed as dist
     dev = "cuda" if (info.backend == "nccl" and group is None) else "cpu"
@@ -268,7 +286,7 @@ def gather_to_main(arr: np.ndarray, group=None) -> Optional[np.ndarray]:
     dist.all_gather(parts, buf, group=group)   # all_gather: supported by gloo and RCCL alike
     if info.rank != 0:
         return None
-    return np.concatenate([p[:s].cpu().numpy() for p, s in zip(parts, sizes)])
+    return [p[:s].cpu().numpy() for p, s in zip(parts, sizes)]
 
 
 def shutdown() -> None:

@@ -7,19 +7,28 @@ effort.  Here the device samples ``plotPoints`` (pred, real) pairs per batch
 (``sgd.hip`` ``k_plot_sample``), and a shipper thread on every rank takes
 them from there: with several ranks it gathers the samples to rank 0 over a
 gloo process group of its own (so its collectives never interleave with the
-training thread's), and rank 0 hands stats + series to the
-:class:`SessionStats` worker, which does the HTTP.  The training thread only
-enqueues.
+training thread's), and rank 0 hands the series to the :class:`SessionStats`
+worker, which does the HTTP.  The batch's twtml-web ``Stats`` do not wait for
+the gather: rank 0's training thread posts them itself (async, drop-oldest).
 
-Every rank must submit the same sequence of batches (each submit is one
-gather); the queue is bounded and a full queue blocks the producer instead
-of dropping, so the gathers stay paired across ranks.  Rank 0's own HTTP
-pushes are drop-oldest in :class:`SessionStats`.
+Back-pressure never reaches training (``SessionStats.scala:29-33``: best
+effort).  :meth:`submit` never blocks: it appends a (sequence number,
+sample) entry; when more than ``maxsize`` samples wait, the oldest waiting
+sample is dropped but its sequence number stays queued.  The shipper gathers
+every sequence number in order on every rank -- a dropped sample travels as
+an empty "dropped" record -- so the gathers stay paired across ranks
+whatever each rank dropped, and a stalled gather only makes the backlog of
+tiny markers grow.  Every gather carries its sequence number and rank 0
+checks them: a batch whose sample some rank dropped is not plotted (the same
+batch is then missing on every rank's side of the plot, not half of it), and
+a sequence mismatch or a gather error stops the shipping for good (pairs
+could no longer be trusted) instead of plotting mismatched pairs.
 """
 from __future__ import annotations
 
+import collections
+import datetime
 import logging
-import queue
 import threading
 from typing import Optional
 
@@ -31,45 +40,108 @@ log = logging.getLogger("twtml.report.plot")
 
 
 class PlotShipper:
-    def __init__(self, session, rank: int = 0, world: int = 1, maxsize: int = 64):
+    def __init__(self, session, rank: int = 0, world: int = 1, maxsize: int = 64,
+                 gather_timeout_s: float = 60.0):
         self.session = session
         self.rank, self.world = int(rank), int(world)
+        self.maxsize = max(1, int(maxsize))
         self.group = None
         if self.world > 1:
             import torch.distributed as dist
-            self.group = dist.new_group(backend="gloo")   # collective: every rank creates it
-        self._q: "queue.Queue" = queue.Queue(maxsize=maxsize)
+            # collective: every rank creates it; the timeout bounds a gather
+            # stuck on a dead peer
+            self.group = dist.new_group(backend="gloo",
+                                        timeout=datetime.timedelta(seconds=gather_timeout_s))
+        self._cv = threading.Condition()
+        self._items: "collections.deque" = collections.deque()   # [seq, stats, real, pred] / None
+        self._waiting = 0          # entries that still hold their sample
+        self._seq = 0
         self._err: Optional[BaseException] = None
-        self.shipped = 0
+        self.shipped = 0           # batches plotted (rank 0) / gathered (other ranks)
+        self.dropped = 0           # this rank's samples dropped on a full backlog
+        self.skipped = 0           # rank 0: batches not plotted because some rank dropped its sample
+        self.stopped = False       # a gather failed or paired different batches: shipping ended
         self._th = threading.Thread(target=self._run, name="plot-shipper", daemon=True)
         self._th.start()
 
     def submit(self, stats, real, pred) -> None:
         """stats: (count, batch, mse, realStdev, predStdev); real / pred: this
-        rank's sampled series (copied: the caller may reuse its arrays)."""
-        self._q.put((tuple(stats), np.array(real, np.float64), np.array(pred, np.float64)))
+        rank's sampled series (copied: the caller may reuse its arrays).
+        Never blocks."""
+        with self._cv:
+            if self.stopped:
+                return
+            self._items.append([self._seq, tuple(stats), np.array(real, np.float64),
+                                np.array(pred, np.float64)])
+            self._seq += 1
+            self._waiting += 1
+            if self._waiting > self.maxsize:   # drop the oldest waiting sample, keep its marker
+                for it in self._items:
+                    if it is not None and it[2] is not None:
+                        it[2] = it[3] = None
+                        self._waiting -= 1
+                        self.dropped += 1
+                        break
+            self._cv.notify()
+
+    def backlog(self) -> int:
+        with self._cv:
+            return len(self._items)
+
+    def _next(self):
+        with self._cv:
+            while not self._items:
+                self._cv.wait()
+            it = self._items.popleft()
+            if it is not None and it[2] is not None:
+                self._waiting -= 1
+            return it
+
+    def _stop(self, why: str) -> None:
+        with self._cv:
+            self.stopped = True
+            self._items.clear()
+            self._waiting = 0
+        log.warning("plot shipping stopped: %s", why)
 
     def _run(self) -> None:
-        from ..parallel.dist import gather_to_main
+        from ..parallel.dist import gather_parts
         while True:
-            item = self._q.get()
-            if item is None:
+            it = self._next()
+            if it is None:
                 return
-            stats, real, pred = item
+            seq, stats, real, pred = it
+            ok = real is not None
             try:
                 if self.world > 1:
-                    both = gather_to_main(np.stack([real, pred]).T.reshape(-1), group=self.group)
-                    if both is not None:
-                        both = both.reshape(-1, 2)
-                        real, pred = both[:, 0], both[:, 1]
+                    head = np.array([float(seq), 1.0 if ok else 0.0])
+                    body = np.stack([real, pred]).T.reshape(-1) if ok else np.zeros(0)
+                    parts = gather_parts(np.concatenate([head, body]), group=self.group)
+                    if parts is not None:   # rank 0
+                        seqs = [int(p[0]) for p in parts]
+                        if any(s != seq for s in seqs):
+                            self._stop(f"gather paired batches {seqs} (expected {seq})")
+                            return
+                        ok = all(p[1] == 1.0 for p in parts)
+                        if ok:
+                            both = np.concatenate([p[2:] for p in parts]).reshape(-1, 2)
+                            real, pred = both[:, 0], both[:, 1]
                 if self.rank == 0 and self.session is not None:
-                    self.session.update(*stats, real, pred)
+                    if ok:
+                        _, batch, _, real_sd, pred_sd = stats
+                        self.session.append_plot(batch, real_sd, pred_sd, real, pred)
+                    else:
+                        self.skipped += 1
                 self.shipped += 1
             except BaseException as e:   # noqa: BLE001 -- best effort, like the reference's Try
                 self._err = e
-                log.warning("plot shipping failed: %s", e)
+                self._stop(f"gather failed: {e}")
+                return
 
     def close(self, timeout: float = 60.0) -> None:
         if self._th.is_alive():
-            self._q.put(None)
-            self._th.join(timeout)
+            with self._cv:
+                self._items.append(None)
+                self._cv.notify()
+            # a shipper that already failed has exited; a healthy one drains
+            self._th.join(0.0 if self.stopped else timeout)

@@ -14,9 +14,8 @@ stalls training (the reference blocks the output op on each HTTP call, then
 drops errors with ``Try``); when the queue is full the oldest update is
 dropped.  A Lightning server that is down at ``open()`` is logged instead of
 aborting the job unless ``strict=True`` (the reference's behaviour).
-``plot_points`` caps the points appended per batch (0 = all, as the
-reference; the default of ``plotPoints`` is 10000, since a micro-batch here
-holds millions of tweets).
+``plot_points`` caps the points appended per batch (0 = all, the default,
+as the reference; at millions of tweets per batch pass ``--plotPoints 10000``).
 """
 from __future__ import annotations
 
@@ -96,6 +95,29 @@ class SessionStats:
                 series = self._series(stats[1], float(realStdev), float(predStdev), real, pred)
                 self._try(lambda: self.lgn.line_streaming(series=series, viz=self.viz))
 
+        self._enqueue(push)
+
+    def push_stats(self, count: int, batch: int, mse: float, realStdev: float, predStdev: float) -> None:
+        """The twtml-web half of :meth:`update` (``SessionStats.scala:29``):
+        posted whether or not the batch's plot sample reaches rank 0."""
+        stats = (int(count), int(batch), int(mse), int(realStdev), int(predStdev))
+        self._enqueue(lambda: self._try(lambda: self.web.stats(*stats)))
+
+    def append_plot(self, batch: int, realStdev: float, predStdev: float,
+                    real: Sequence[float], pred: Sequence[float]) -> None:
+        """The Lightning half of :meth:`update` (``SessionStats.scala:31-33``)."""
+        if self.viz is None:
+            return
+        real = np.array(real, dtype=np.float64)
+        pred = np.array(pred, dtype=np.float64)
+
+        def push() -> None:
+            series = self._series(int(batch), float(realStdev), float(predStdev), real, pred)
+            self._try(lambda: self.lgn.line_streaming(series=series, viz=self.viz))
+
+        self._enqueue(push)
+
+    def _enqueue(self, push: Callable[[], None]) -> None:
         if not self._async:
             push()
             return
