@@ -144,7 +144,7 @@ def run_device_pipeline(r: Runner, pool, warmup: int, steps: int, sync):
     is trained, so the copy engine always has the next batch queued.  Every
     timed step trains one batch and submits one."""
     eng = r.eng
-    depth = max(1, min(int(os.environ.get("TWTML_BENCH_DEPTH", "2")), eng.raw_slots - 1))
+    depth = max(1, min(int(os.environ.get("TWTML_BENCH_DEPTH", eng.raw_slots - 1)), eng.raw_slots - 1))
     state = {"next": 0, "cur": 0}
     sealed_at = {}
 
@@ -412,7 +412,9 @@ def main(argv=None) -> int:
     u8s = []
     pinned = 0   # bytes of page-locked host memory this rank holds (staging views + registered pool)
     if args.e2e:
-        views = [HostBatchView(B, max_units) for _ in range(eng.raw_slots)]
+        # utf8 / utf16 ingest DMAs the text from the receiver's registered
+        # buffers: the staging views hold row words and scalars only
+        views = [HostBatchView(B, max_units, text=ingest == "wire") for _ in range(eng.raw_slots)]
         pinned += sum(int(v._hb.bytes) for v in views)
         if is_km:
             for v in views:

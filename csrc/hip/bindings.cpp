@@ -35,7 +35,7 @@ static LRConfig lr_config(const py::dict& d) {
   GET(end, int64_t) GET(require_retweet, int32_t) GET(range_filter, int32_t)
   GET(max_rows, int64_t) GET(max_units, int64_t) GET(sgd_grid, int32_t)
   GET(early_exit_depth, int32_t) GET(ablate, int32_t) GET(dedup, int32_t) GET(hybrid, int32_t) GET(lazy_idx, int32_t)
-  GET(overlap, int32_t) GET(force_dp, int32_t) GET(comm_timing, int32_t)
+  GET(overlap, int32_t) GET(force_dp, int32_t) GET(comm_timing, int32_t) GET(raw_slots, int32_t)
 #undef GET
   return c;
 }
@@ -85,7 +85,7 @@ static py::dict result_dict(BatchResult& r) {
 
 PYBIND11_MODULE(_twtml_hip, m) {
   m.doc() = "twtml MI355X engine: HIP/CDNA4 kernels, micro-batch engines, RCCL";
-  m.attr("RAW_SLOTS") = kRawSlots;   // device raw-batch slots per engine (submit/process)
+  m.attr("RAW_SLOTS") = kDefaultRawSlots;   // default device raw-batch slots per engine (submit/process)
 
   m.def("pci_bus_id", [](int device) {
     char buf[64] = {0};
@@ -315,6 +315,7 @@ PYBIND11_MODULE(_twtml_hip, m) {
            },
            py::arg("slot"), py::arg("now_ms"), py::arg("want_pred") = false, py::arg("plot_points") = 0)
       .def_property_readonly("h2d_bytes", &LREngine::h2d_bytes, "host-to-device bytes submitted so far")
+      .def_property_readonly("raw_slots", &LREngine::raw_slots, "device raw-batch slots")
       .def_property_readonly("lazy_bytes", &LREngine::lazy_bytes,
                              "device bytes the engine allocates on its first tiered batch (sizing)")
       .def("get_weights", [](const LREngine& e) {

@@ -266,7 +266,7 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
   }
   if (!pstream_) TWTML_HIP_CHECK(hipStreamCreateWithPriority(&pstream_, hipStreamNonBlocking, lo));
   TWTML_HIP_CHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
-  raw_.init(cfg_.max_rows, text_bytes_for_units(cfg_.max_units));
+  raw_.init(cfg_.raw_slots, cfg_.max_rows, text_bytes_for_units(cfg_.max_units));
   for (auto& e : ev_) TWTML_HIP_CHECK(hipEventCreate(&e));
   upload_lower_tables(compute_, &lower_page_, &lower_blocks_);
   near_cap_ = tier_near_cap();
@@ -530,7 +530,7 @@ LREngine::~LREngine() {
   if (snap_stage_) (void)hipHostFree(snap_stage_);
   void* bufs[] = {sgd_.gacc, sgd_.rbuf, sgd_.pbuf, sgd_.stat_i, sgd_.stat_part, sgd_.w64, sgd_.wc64, sgd_.wc32,
                   sgd_.stats, sgd_.state,
-                  sgd_.loss_hist, sgd_.pred_out, sgd_.real_out, sgd_.nrm, sgd_.wnorm_next, sgd_.part, sgd_.itrec, iter_tdbg_,
+                  sgd_.loss_hist, sgd_.pred_out, sgd_.real_out, sgd_.nrm, sgd_.wnorm_next, sgd_.part, sgd_.itrec, iter_tdbg_, iter_kdbg_,
                   lower_page_, lower_blocks_};
   for (void* b : bufs) if (b) (void)hipFree(b);
   if (host_out_) (void)hipHostFree(host_out_);
@@ -892,8 +892,12 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred, int64_t plot_points) {
     const bool fused = !dp_ && sgd_.nparts > 0;
     const bool itime = std::getenv("TWTML_ITER_TIMING") != nullptr;
     if (itime && !iter_tdbg_) iter_tdbg_ = dmalloc<uint64_t>(4096 + size_t(iters + 2) * 32);
+    const size_t kd_words = size_t(iters + 2) * 3 * kKdbgWgs * 2;
+    if (itime && !iter_kdbg_) iter_kdbg_ = dmalloc<uint64_t>(kd_words);
     sgd_.tdbg = itime ? iter_tdbg_ : nullptr;
+    sgd_.kdbg = itime ? iter_kdbg_ : nullptr;
     if (itime) TWTML_HIP_CHECK(hipMemsetAsync(iter_tdbg_, 0, sizeof(uint64_t) * (4096 + size_t(iters + 2) * 32), s));
+    if (itime) TWTML_HIP_CHECK(hipMemsetAsync(iter_kdbg_, 0, sizeof(uint64_t) * kd_words, s));
     if (comm_timing_ && comm_ev_.size() < size_t(2 * iters)) {
       for (size_t q = comm_ev_.size(); q < size_t(2 * iters); ++q) {
         hipEvent_t e;
@@ -1044,6 +1048,45 @@ void LREngine::print_iter_timing(int iters) {
   std::fprintf(stderr, "wave ends (us after kernel start) / chunks, WG 0 it %d:", i);
   for (int w = 0; w < 16; ++w) std::fprintf(stderr, " %.1f/%d", double(we[2 * w] - t0[0]) * 0.01, int(we[2 * w + 1]));
   std::fprintf(stderr, "\n");
+  // per-kernel workgroup stamps: dispatch ramp (last start - first start),
+  // span (last end - first start), median / max workgroup time, and the gap
+  // from the previous kernel's last end to this one's first start
+  const size_t kd_words = size_t(iters + 2) * 3 * kKdbgWgs * 2;
+  std::vector<uint64_t> kd(kd_words);
+  TWTML_HIP_CHECK(hipMemcpyAsync(kd.data(), iter_kdbg_, kd_words * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  TWTML_HIP_CHECK(hipStreamSynchronize(s));
+  const char* names[3] = {"iteration", "far backward", "update"};
+  double acc[3][5] = {};
+  int cnt[3] = {0, 0, 0};
+  for (int it = 2; it <= iters; ++it) {
+    uint64_t prev_end = 0;
+    for (int k = 0; k < 3; ++k) {
+      const uint64_t* b = kd.data() + (size_t(it) * 3 + size_t(k)) * kKdbgWgs * 2;
+      uint64_t s0 = UINT64_MAX, s1 = 0, e1 = 0;
+      std::vector<double> dur;
+      for (int g = 0; g < kKdbgWgs; ++g) {
+        if (b[2 * g] == 0 || b[2 * g + 1] == 0) continue;
+        s0 = std::min(s0, b[2 * g]);
+        s1 = std::max(s1, b[2 * g]);
+        e1 = std::max(e1, b[2 * g + 1]);
+        dur.push_back(double(b[2 * g + 1] - b[2 * g]) * 0.01);
+      }
+      if (dur.empty()) continue;
+      std::sort(dur.begin(), dur.end());
+      acc[k][0] += double(s1 - s0) * 0.01;
+      acc[k][1] += double(e1 - s0) * 0.01;
+      acc[k][2] += dur[dur.size() / 2];
+      acc[k][3] += dur.back();
+      acc[k][4] += prev_end ? double(int64_t(s0) - int64_t(prev_end)) * 0.01 : 0.0;
+      prev_end = e1;
+      ++cnt[k];
+    }
+  }
+  for (int k = 0; k < 3; ++k)
+    if (cnt[k])
+      std::fprintf(stderr, "kernel %-12s (us, %d iters): ramp %.2f span %.2f wg p50 %.2f wg max %.2f gap before %.2f\n",
+                   names[k], cnt[k], acc[k][0] / cnt[k], acc[k][1] / cnt[k], acc[k][2] / cnt[k], acc[k][3] / cnt[k],
+                   acc[k][4] / cnt[k]);
 }
 
 // ---------------------------------------------------------------------------

@@ -56,6 +56,7 @@ struct LRConfig {
   int32_t force_dp = 0;          // take the DP path (packet all-gather, packed all-reduce, stats
                                  // all-reduce) even with a world-1 communicator (also TWTML_FORCE_DP=1)
   int32_t comm_timing = 0;       // DP: time the per-iteration gradient all-reduce (events)
+  int32_t raw_slots = kDefaultRawSlots;   // device raw-batch slots (H2D run-ahead depth + 1)
 };
 
 // Pinned staging buffer of one raw batch in the wire format
@@ -224,6 +225,7 @@ class LREngine {
   // buffer) and by the first checkpoint snapshot ((index, value) pairs for
   // every weight): ops/sizing.py adds them to the construction footprint.
   int64_t h2d_bytes() const { return raw_.h2d_bytes(); }   // host-to-device bytes submitted so far
+  int raw_slots() const { return raw_.count(); }
   int64_t lazy_bytes() const {
     const int nbuf = overlap_ ? 2 : 1;
     // + the slot-sized tier arrays (newslot, slot_fid, tscan, fhist, fcur,
@@ -329,6 +331,7 @@ class LREngine {
   uint16_t* lower_blocks_ = nullptr;
   double* host_out_ = nullptr;        // pinned [16 + iters]
   int64_t* host_stat_ = nullptr;      // pinned [16]: exact batch moments (stat_i)
+  uint64_t* iter_kdbg_ = nullptr;     // TWTML_ITER_TIMING: per-workgroup GD kernel stamps
   float* plot_host_ = nullptr;        // mapped pinned [2 max_rows]: sampled (pred, real) pairs
   float* plot_dev_ = nullptr;         // ... its device address (k_plot_sample writes it)
   double* host_flags_ = nullptr;      // pinned [iters + 1] convergence flag per iteration

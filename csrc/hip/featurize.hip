@@ -433,16 +433,47 @@ __device__ __forceinline__ void decode_rows2(const LdsBytes& src, uint8_t* text,
   }
 }
 
-// One lane's row class from the staged bytes [lo, le) (as row_class).
-__device__ __forceinline__ int lane_row_class(const uint8_t* lbuf, int lo, int le) {
-  uint32_t acc = 0, big = 0;
+// Bytes of x equal to b (per byte: bit 7 set), exact (no borrow between bytes).
+__device__ __forceinline__ uint32_t bytes_eq(uint32_t x, uint32_t b) {
+  const uint32_t t = x ^ (b * 0x01010101u);
+  return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
+}
+
+// UTF-8 byte pairs that start a unit whose lower-casing is not one UTF-16
+// unit per unit (rows.hip's special rows): C4 B0 (U+0130), CE A3 (U+03A3,
+// Final_Sigma), F0 90 / F0 91 / F0 96 / F0 9E (the planes of the astral
+// cased letters: Deseret, Osage, Old Hungarian, Warang Citi, Medefaidrin,
+// Adlam; emoji, F0 9F, are not).  A superset of the special rows: the
+// normaliser checks every flagged row exactly.  v: four bytes, n: the
+// byte after each of them.
+__device__ __forceinline__ uint32_t special_pairs(uint32_t v, uint32_t n) {
+  const uint32_t c4 = bytes_eq(v, 0xC4u), ce = bytes_eq(v, 0xCEu), f0 = bytes_eq(v, 0xF0u);
+  if (!(c4 | ce | f0)) return 0u;   // most multi-byte text (CJK, Cyrillic, Arabic, ...) has none of the leads
+  uint32_t m = (c4 & bytes_eq(n, 0xB0u)) | (ce & bytes_eq(n, 0xA3u));
+  if (f0)
+    m |= f0 & (bytes_eq(n, 0x90u) | bytes_eq(n, 0x91u) | bytes_eq(n, 0x96u) | bytes_eq(n, 0x9Eu));
+  return m;
+}
+
+// One lane's row class from the staged bytes [lo, le) (as row_class), and
+// (sp) whether the row holds a special-unit candidate (class 2 rows only:
+// every special pair has a byte >= 0xC4).
+__device__ __forceinline__ int lane_row_class(const uint8_t* lbuf, int lo, int le, bool& sp) {
+  uint32_t acc = 0, big = 0, spec = 0, prev = 0;
   for (int w = lo & ~3; w < le; w += 4) {
     uint32_t v = *reinterpret_cast<const uint32_t*>(lbuf + w);
     if (w < lo) v &= 0xFFFFFFFFu << (8 * (lo - w));
     if (w + 4 > le) v &= 0xFFFFFFFFu >> (8 * (w + 4 - le));
     acc |= v;
     big |= v & ((v & 0x7F7F7F7Fu) + 0x3C3C3C3Cu);   // a byte >= 0xC4 sets its bit 7
+    // the previous dword's byte pairs, its last byte paired with this
+    // dword's first (no extra LDS read: a dependent load per dword made the
+    // loop latency-bound)
+    if (prev & 0x80808080u) spec |= special_pairs(prev, (prev >> 8) | (v << 24));
+    prev = v;
   }
+  if (prev & 0x80808080u) spec |= special_pairs(prev, prev >> 8);
+  sp = spec != 0u;
   if (big & 0x80808080u) return 2;
   return (acc & 0x80808080u) ? 1 : 0;
 }
@@ -510,9 +541,10 @@ __global__ __launch_bounds__(kDecWaves * kWave) void k_cesu_decode(uint8_t* text
       // staged: every lane classifies its own row from LDS (aligned dwords),
       // so ASCII rows -- most tweets -- leave the wave's per-row walk entirely
       int my_cls = -1;
+      bool my_sp = true;   // rows walked from global memory: a candidate (checked exactly later)
       if (staged) {
         const bool in_win = (m >> lane) & 1u;
-        if (in_win) my_cls = lane_row_class(lbuf, int(s0 - a0), int(s1 - a0));
+        if (in_win) my_cls = lane_row_class(lbuf, int(s0 - a0), int(s1 - a0), my_sp);
         if (my_cls == 0) fl = uint8_t(fl & ~kRowCesu);
         m = __ballot(my_cls > 0);
       }
@@ -535,12 +567,12 @@ __global__ __launch_bounds__(kDecWaves * kWave) void k_cesu_decode(uint8_t* text
           if (lane == lA) {
             s0 = d0A;
             s1 = d0A + (narA ? kA : 2 * kA);
-            fl = narA ? uint8_t(fl & ~kRowCesu) : uint8_t((fl & ~kRowCesu) | kRowWide);
+            fl = narA ? uint8_t(fl & ~kRowCesu) : uint8_t((fl & ~kRowCesu) | kRowWide | (my_sp ? kRowSpecial : 0));
           }
           if (two && lane == lB) {
             s0 = d0B;
             s1 = d0B + (narB ? kB : 2 * kB);
-            fl = narB ? uint8_t(fl & ~kRowCesu) : uint8_t((fl & ~kRowCesu) | kRowWide);
+            fl = narB ? uint8_t(fl & ~kRowCesu) : uint8_t((fl & ~kRowCesu) | kRowWide | (my_sp ? kRowSpecial : 0));
           }
           n_nar += (narA ? 1 : 0) + (narB ? 1 : 0);
         }
@@ -564,7 +596,7 @@ __global__ __launch_bounds__(kDecWaves * kWave) void k_cesu_decode(uint8_t* text
         if (lane == l) {
           s0 = d0;
           s1 = d0 + (nar ? k : 2 * k);
-          fl = nar ? uint8_t(fl & ~kRowCesu) : uint8_t((fl & ~kRowCesu) | kRowWide);
+          fl = nar ? uint8_t(fl & ~kRowCesu) : uint8_t((fl & ~kRowCesu) | kRowWide | (my_sp ? kRowSpecial : 0));
         }
         n_nar += nar ? 1 : 0;
       }

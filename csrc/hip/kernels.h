@@ -56,6 +56,9 @@ __device__ __forceinline__ int64_t raw_scalar(const DevRawBatch& b, int c, int64
 constexpr uint8_t kRowRetweet = 1;
 constexpr uint8_t kRowWide = 2;
 constexpr uint8_t kRowCesu = 4;   // wire only (csrc/host/wire.h); expanded by launch_cesu_expand
+// device only: a row launch_cesu_expand decoded holds a unit whose lower-casing
+// is not one unit per unit (candidate for k_row_normalize's full case mapping)
+constexpr uint8_t kRowSpecial = 8;
 // Packed row words on the wire (HostBatch::pack_rows): byte length in the
 // low kRowLenBits bits, the three flag bits above.
 constexpr int kRowLenBits = 13;
@@ -83,10 +86,13 @@ void free_case_tables(DevCaseTables* ct);
 // batches when `narrow`), see rows.hip.  Reads rows at [cur_s, cur_e),
 // writes every row's extents to out_s / out_e (may alias cur_*) and clears
 // the wide flag of narrowed rows.  text needs lower_base + 2 * wire bytes.
+// flagged_only (UTF-8 batches: every wide row came out of the decoder, which
+// flags kRowSpecial candidates and narrows Latin-1 rows itself): only flagged
+// rows are scanned.
 void launch_row_normalize(uint8_t* text, const int64_t* wire_off, const int64_t* cur_s, const int64_t* cur_e,
                           uint8_t* flags, int64_t* out_s, int64_t* out_e, int64_t n, int64_t tail,
                           int64_t lower_base, bool narrow, const DevCaseTables& ct, int64_t* stats,
-                          hipStream_t s);
+                          hipStream_t s, bool flagged_only = false);
 
 // Row r: byte offset, wide flag and length in UTF-16 units.
 struct RowText {
@@ -272,6 +278,8 @@ struct DevSgd {
   int64_t* part;        // [nparts][pstride] per-workgroup int64 partial rows
   double* itrec;        // [max_iters+2][kRecStride] per-iteration scale / update records
   uint64_t* tdbg;       // optional phase stamps (TWTML_ITER_TIMING): [iter][wg 0 / last][8]
+  uint64_t* kdbg;       // optional per-workgroup start / end stamps (TWTML_ITER_TIMING):
+                        // [iter][iteration, far backward, update][kKdbgWgs][2]
   const double* bounds; // [8] batch bounds: max row bigram count, max |y|, max |n_k| (k = 0..3)
   const volatile int64_t* ready_word;   // DP: host-mapped, this rank's next-batch ready word
   int32_t rank, world;
@@ -295,6 +303,8 @@ struct DevSgd {
 };
 
 constexpr int kNormParts = 1024;   // grid cap of the norm / gather / scatter kernels
+constexpr int kKdbgWgs = 1024;     // workgroups stamped per kernel (TWTML_ITER_TIMING)
+
 
 // Iteration record i: [0] updates so far, [1] m, [2] update workgroups,
 // [3] K, [4] S, [5] L, [6..9] N_0..N_3 (fixed-point exponents of iteration

@@ -44,7 +44,7 @@ KMEngine::KMEngine(int device, const KMConfig& cfg, std::shared_ptr<Comm> comm)
   TWTML_HIP_CHECK(hipSetDevice(device_));
   TWTML_HIP_CHECK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
   TWTML_HIP_CHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
-  raw_.init(cfg_.max_rows, text_bytes_for_units(cfg_.max_units));
+  raw_.init(cfg_.raw_slots, cfg_.max_rows, text_bytes_for_units(cfg_.max_units));
   const int64_t R = cfg_.max_rows;
   prep_.cap_rows = R;
   prep_.kept = km_alloc<int64_t>(size_t(R));
@@ -272,7 +272,7 @@ void bind_kmeans(py::module_& m) {
 #define GET(name, type) if (d.contains(#name)) c.name = d[#name].cast<type>();
              GET(k, int32_t) GET(text_dims, int32_t) GET(decay, double) GET(points_unit, int32_t)
              GET(scale, int32_t) GET(mfma, int32_t) GET(max_rows, int64_t) GET(max_units, int64_t)
-             GET(force_dp, int32_t)
+             GET(force_dp, int32_t) GET(raw_slots, int32_t)
 #undef GET
              py::gil_scoped_release nogil;
              return std::make_shared<KMEngine>(device, c, comm);
@@ -283,6 +283,7 @@ void bind_kmeans(py::module_& m) {
         e.submit(hb, n, bytes, slot, reinterpret_cast<const uint8_t*>(ext_text));
       }, py::arg("host_batch"), py::arg("n"), py::arg("bytes"), py::arg("slot"), py::arg("ext_text") = 0)
       .def_property_readonly("h2d_bytes", &KMEngine::h2d_bytes, "host-to-device bytes submitted so far")
+      .def_property_readonly("raw_slots", &KMEngine::raw_slots, "device raw-batch slots")
       .def("process", [](KMEngine& e, int slot, bool want_labels) {
         KMResult r;
         {

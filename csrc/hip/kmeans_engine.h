@@ -25,6 +25,7 @@ struct KMConfig {
   int64_t max_rows = 1 << 16;
   int64_t max_units = (1 << 16) * 281;
   int32_t force_dp = 0;        // DP collectives even with a world-1 communicator (also TWTML_FORCE_DP=1)
+  int32_t raw_slots = kDefaultRawSlots;   // device raw-batch slots (H2D run-ahead depth + 1)
 };
 
 struct KMResult {
@@ -51,6 +52,7 @@ class KMEngine {
   int d() const { return d_; }
   int dp() const { return dp_; }
   int64_t h2d_bytes() const { return raw_.h2d_bytes(); }
+  int raw_slots() const { return raw_.count(); }
   void synchronize();
 
  private:

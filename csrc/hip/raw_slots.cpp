@@ -2,6 +2,7 @@
 #include "alloc.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 
 #include "engine.h"
@@ -13,14 +14,16 @@ static T* slot_alloc(size_t n) {
   return static_cast<T*>(dev_alloc(n * sizeof(T)));
 }
 
-int RawSlots::check(int slot) {
-  if (slot < 0 || slot >= kRawSlots) throw std::invalid_argument("slot must be in [0, kRawSlots)");
+int RawSlots::check(int slot) const {
+  if (slot < 0 || slot >= int(slots_.size())) throw std::invalid_argument("slot must be in [0, raw slots)");
   return slot;
 }
 
-void RawSlots::init(int64_t max_rows, int64_t max_bytes) {
+void RawSlots::init(int n_slots, int64_t max_rows, int64_t max_bytes) {
   if (max_rows < 0 || max_bytes < 0) throw std::invalid_argument("RawSlots: negative capacity");
+  if (n_slots < 2 || n_slots > kMaxRawSlots) throw std::invalid_argument("RawSlots: 2 .. 32 slots");
   release();
+  slots_.assign(size_t(n_slots), Slot{});
   max_rows_ = max_rows;
   max_bytes_ = max_bytes;
   for (auto& s : slots_) {
@@ -56,6 +59,7 @@ void RawSlots::release() {
     if (s.consumed) (void)hipEventDestroy(s.consumed);
     s = Slot{};
   }
+  slots_.clear();
   free_case_tables(&case_);
 }
 
@@ -144,9 +148,15 @@ DevRawBatch RawSlots::acquire(int slot, hipStream_t compute) {
   if (s.utf16 || s.cesu_rows > 0 || s.wide_rows > 0) {
     // special rows -> fully lower-cased UTF-16; UTF-16 / UTF-8 batches: Latin-1
     // rows narrowed (a decoded UTF-8 row in place: byte i <- unit i, forward)
+    // UTF-8 batches: the decoder flagged the candidate special rows (and
+    // narrowed the Latin-1 ones itself), so only those are scanned
+    static const bool scan_all = [] {   // TWTML_NORMALIZE_ALL=1: scan every wide row (A/B)
+      const char* e = std::getenv("TWTML_NORMALIZE_ALL");
+      return e && e[0] == '1';
+    }();
     launch_row_normalize(s.text, s.offsets, b.offsets, b.oend, s.flags, s.rstart, s.rend, s.n, tail,
                          tail + 2 * ((s.bytes + 15) / 16 * 16), s.utf16 || s.utf8, case_, s.nstats,
-                         compute);
+                         compute, s.utf8 && !s.utf16 && s.cesu_rows > 0 && !scan_all);
     b.offsets = s.rstart;
     b.oend = s.rend;
   }

@@ -1,18 +1,22 @@
-// Triple-buffered device copies of raw wire-format batches (csrc/host/wire.h).
+// Multi-buffered device copies of raw wire-format batches (csrc/host/wire.h).
 //
 // submit() enqueues the H2D of a pinned HostBatch on the copy stream into one
-// of kRawSlots slots; the compute stream waits on that slot's h2d event and
+// of the engine's raw slots; the compute stream waits on that slot's h2d event and
 // records `consumed` once its kernels no longer read the raw bytes, so the
 // next H2D into the slot overlaps the rest of the batch's compute.  With three
 // slots the host can keep two batches queued ahead of the one being trained,
 // so the PCIe copy engine never idles while the host waits for a batch's
 // results (double buffering only starts batch t+1's copy once batch t-1 has
-// returned to the host).
+// returned to the host).  More slots let the copy engine run further ahead
+// while young-model batches (many GD iterations) keep the GPU busier than
+// the link: the slack is spent when the model converges and batches run at
+// GPU speed (kDefaultRawSlots; LRConfig / KMConfig raw_slots).
 #pragma once
 #include <hip/hip_runtime.h>
 
 #include <atomic>
 #include <cstdint>
+#include <vector>
 
 #include "kernels.h"
 
@@ -20,7 +24,8 @@ namespace twtml {
 
 struct HostBatch;
 
-constexpr int kRawSlots = 4;
+constexpr int kDefaultRawSlots = 8;
+constexpr int kMaxRawSlots = 32;
 
 class RawSlots {
  public:
@@ -29,7 +34,8 @@ class RawSlots {
   RawSlots& operator=(const RawSlots&) = delete;
   ~RawSlots() { release(); }
 
-  void init(int64_t max_rows, int64_t max_bytes);
+  void init(int n_slots, int64_t max_rows, int64_t max_bytes);
+  int count() const { return int(slots_.size()); }
   void release();
   // H2D of rows [0, n) / `bytes` text bytes of hb into `slot` on `copy`.
   // scalar_cols: leading scalar columns to copy (the rest stay stale); the
@@ -55,7 +61,7 @@ class RawSlots {
   int64_t h2d_bytes() const { return h2d_bytes_.load(std::memory_order_relaxed); }
 
  private:
-  static int check(int slot);
+  int check(int slot) const;
   struct Slot {
     uint8_t* text_base = nullptr;     // [row words prefix | text] (one H2D copy)
     uint8_t* text = nullptr;
@@ -75,7 +81,8 @@ class RawSlots {
     int64_t n = 0, bytes = 0;
     hipEvent_t h2d_done = nullptr, consumed = nullptr;
     bool used = false;
-  } slots_[kRawSlots];
+  };
+  std::vector<Slot> slots_;
   int64_t max_rows_ = 0, max_bytes_ = 0;
   std::atomic<int64_t> h2d_bytes_{0};
   DevCaseTables case_{};

@@ -58,6 +58,7 @@ struct RowNorm {
   int64_t n;
   int64_t tail, lower_base;
   int32_t narrow;
+  int32_t flagged_only;      // scan only rows the decoder flagged kRowSpecial
   DevCaseTables ct;
   int64_t* stats;            // [0] lowered rows, [1] narrowed rows (nullable)
 };
@@ -140,7 +141,8 @@ __global__ __launch_bounds__(256) void k_row_normalize(RowNorm a) {
     uint8_t fl = in ? a.flags[r] : 0;
     int64_t s0 = in ? a.cur_s[r] : 0, s1 = in ? a.cur_e[r] : 0;
     const int64_t wo = in ? a.wire_off[r] : 0;
-    uint64_t m = __ballot(in && (fl & kRowWide));
+    uint64_t m = __ballot(in && (fl & kRowWide) && (!a.flagged_only || (fl & kRowSpecial)));
+    fl = uint8_t(fl & ~kRowSpecial);
     int n_low = 0, n_nar = 0;
     while (m) {
       // pass 1 over up to kScanRows wide rows at once (their unit loads all
@@ -278,9 +280,10 @@ void free_case_tables(DevCaseTables* ct) {
 void launch_row_normalize(uint8_t* text, const int64_t* wire_off, const int64_t* cur_s, const int64_t* cur_e,
                           uint8_t* flags, int64_t* out_s, int64_t* out_e, int64_t n, int64_t tail,
                           int64_t lower_base, bool narrow, const DevCaseTables& ct, int64_t* stats,
-                          hipStream_t s) {
+                          hipStream_t s, bool flagged_only) {
   if (n <= 0) return;
-  RowNorm a{text, wire_off, cur_s, cur_e, flags, out_s, out_e, n, tail, lower_base, narrow ? 1 : 0, ct, stats};
+  RowNorm a{text, wire_off, cur_s, cur_e, flags, out_s, out_e, n, tail, lower_base, narrow ? 1 : 0,
+            flagged_only ? 1 : 0, ct, stats};
   const int grid = int(std::min<int64_t>((n + 255) / 256, 4096));
   hipLaunchKernelGGL(k_row_normalize, dim3(grid), dim3(256), 0, s, a);
 }

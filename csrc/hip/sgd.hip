@@ -51,6 +51,12 @@
 
 namespace twtml {
 
+// Per-workgroup start / end stamps of the GD kernels (TWTML_ITER_TIMING only).
+__device__ __forceinline__ void kdbg_stamp(uint64_t* base, int it, int kind, int end) {
+  if (!base || threadIdx.x != 0 || blockIdx.x >= unsigned(kKdbgWgs)) return;
+  base[((int64_t(it) * 3 + kind) * kKdbgWgs + blockIdx.x) * 2 + end] = __builtin_amdgcn_s_memrealtime();
+}
+
 // Iteration record i and its per-update-workgroup partials.
 __device__ __forceinline__ double* sgd_rec(const DevSgd& d, int it) { return d.itrec + int64_t(it) * kRecStride; }
 
@@ -866,6 +872,7 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_hyb(DevSgd d, DevPrepar
   if (d.tdbg && threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1))
     tst = d.tdbg + (int64_t(sp.iteration) * 2 + (blockIdx.x == 0 ? 0 : 1)) * 8;
   if (tst) tst[0] = __builtin_amdgcn_s_memrealtime();
+  kdbg_stamp(d.kdbg, sp.iteration, 0, 0);
   if (sgd_prologue(d, sp, &stop_flag, &scs)) return;
   const LaneScale sc = lane_scale(scs, d, lane_id() % kLanesPerRow);
   if (tst) tst[1] = __builtin_amdgcn_s_memrealtime();
@@ -876,6 +883,10 @@ __global__ __launch_bounds__(kIterBlock) void k_sgd_iter_hyb(DevSgd d, DevPrepar
   hyb_pass<STATS, SAMPLE, REP, TIERED>(d, p, sp, sc, wl, gl, whl, hsum, wsc,
                                        d.part + int64_t(blockIdx.x) * d.pstride, &wctr, fdot, tst);
   if (tst) tst[6] = __builtin_amdgcn_s_memrealtime();
+  if (d.kdbg) {
+    __syncthreads();
+    kdbg_stamp(d.kdbg, sp.iteration, 0, 1);
+  }
 }
 
 // LDS bytes of the fast path for a given replication factor.
@@ -1041,7 +1052,13 @@ int sgd_partials(int64_t ns, bool u16, int grid) {
 // nparts > 0: the column sums come from the partial rows (single GPU);
 // nparts == 0: gacc holds them (all-reduced).
 // ---------------------------------------------------------------------------
-constexpr int kUpdWaves = 1024 / kWave;   // waves per workgroup (partial-row split)
+// 256-thread update / reduce workgroups: they run beside the prep stream's
+// kernels, and a 1024-thread workgroup needs 16 free wave slots on one CU --
+// with prep workgroups resident, the r5 per-workgroup stamps showed the
+// 433 update workgroups dispatched over ~52 us for ~5 us of work each.
+constexpr int kUpdThreads = 256;
+constexpr int kUpdWaves = kUpdThreads / kWave;   // waves per workgroup (partial-row split)
+constexpr int kUpdFarSlots = kUpdThreads;        // far slots per far update workgroup (one per thread)
 
 // Sum of partial rows for columns [col0, col0 + 64): returns lane's column
 // sum in wave 0 (other waves: 0); columns >= dcol0 are fp64 (bits returned).
@@ -1057,7 +1074,7 @@ __device__ __forceinline__ int64_t part_block_sum(const DevSgd& d, int64_t col0,
     const int64_t* src = d.part + col;
     const int64_t ps = d.pstride;
     if (!dbl) {
-#pragma unroll 8
+#pragma unroll 16
       for (int g = w; g < nparts; g += kUpdWaves) acc += src[int64_t(g) * ps];
     } else {
       for (int g = w; g < nparts; g += kUpdWaves) accd += __builtin_bit_cast(double, src[int64_t(g) * ps]);
@@ -1132,12 +1149,13 @@ __device__ __forceinline__ bool far_seg_scan(int64_t e, int64_t n, uint32_t sl, 
 // skewed over slot ranges, and the slowest block made the update ~100 us.
 // The grouping is a function of the layout only, so the fp64 norm partials
 // (and the convergence verdicts) are the same bits on one GPU and in DP.
-__global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int nparts, int nt, int nf) {
+__global__ __launch_bounds__(kUpdThreads) void k_sgd_update(DevSgd d, SgdParams sp, int nparts, int nt, int nf) {
   __shared__ double wsc[kUpdWaves][3];
   __shared__ int64_t red[kUpdWaves][kWave];
   __shared__ double m_sh;
   const int tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
   const int it = sp.iteration;
+  kdbg_stamp(d.kdbg, it, 2, 0);
   const int64_t ns = d.nl, hi = d.far_base;   // partial-row columns; near text slots end at far_base
   int64_t* tail = d.gacc + ns;
   const int64_t n_far = kNumNumeric + d.n_unique - d.far_base;
@@ -1158,7 +1176,7 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
                          __HIP_MEMORY_SCOPE_SYSTEM);
     }
     if (stop) {
-      for (int64_t j = int64_t(blockIdx.x) * 1024 + tid; j < n_far; j += int64_t(gridDim.x) * 1024)
+      for (int64_t j = int64_t(blockIdx.x) * kUpdThreads + tid; j < n_far; j += int64_t(gridDim.x) * kUpdThreads)
         gfar[j] = 0;   // this pass's far sums are dropped
       if (blockIdx.x == 0 && tid == 0) {
         d.state[0] = 1.0;
@@ -1174,6 +1192,7 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
   // memory round trip shorter; a block that then finds the batch finished
   // drops them.
   const int64_t col_first = int64_t(blockIdx.x) * kWave;
+  if (sp.ablate == 10) nparts = 0;   // timing only: the update without its partial-row reads
   const bool pre = nparts > 0 && int(blockIdx.x) < nt;
   double wn_first = 0.0;
   if (pre && w == 0 && col_first + lane < hi) wn_first = d.wc64[col_first + lane];
@@ -1230,7 +1249,7 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
     // gradient sums (k_far_grad; DP: all-reduced), re-zeroed here
     const int64_t k = int64_t(blockIdx.x) - nt;
     const int64_t jlo = n_far * k / nf, jhi = n_far * (k + 1) / nf;
-    for (int64_t j = jlo + tid; j < jhi; j += 1024) {
+    for (int64_t j = jlo + tid; j < jhi; j += kUpdThreads) {
       const double g = double(gfar[j]) * gsc;
       gfar[j] = 0;
       const int64_t col = d.far_base + j;
@@ -1271,6 +1290,10 @@ __global__ __launch_bounds__(1024) void k_sgd_update(DevSgd d, SgdParams sp, int
     d.state[2] = nupd;
     d.state[3] = double(it);
   }
+  if (d.kdbg) {
+    __syncthreads();
+    kdbg_stamp(d.kdbg, it, 2, 1);
+  }
 }
 
 // Near tiles and far ranges of the update grid: a function of the layout
@@ -1279,20 +1302,21 @@ static void update_split(const DevSgd& d, int& nt, int& nf) {
   const int64_t tiles = (d.nl + kPartVals - kNumNumeric + kWave - 1) / kWave;
   const int64_t n_far = kNumNumeric + d.n_unique - d.far_base;
   nt = int(std::max<int64_t>(1, std::min<int64_t>(tiles, kMaxUpdGrid / 2)));
-  nf = n_far > 0 ? int(std::max<int64_t>(1, std::min<int64_t>((n_far + 767) / 768, kMaxUpdGrid - nt))) : 0;
+  nf = n_far > 0 ? int(std::max<int64_t>(1, std::min<int64_t>((n_far + kUpdFarSlots - 1) / kUpdFarSlots,
+                                                                 kMaxUpdGrid - nt))) : 0;
 }
 
 void launch_sgd_update(const DevSgd& d, const SgdParams& sp, int nparts, hipStream_t s) {
   int nt = 0, nf = 0;
   update_split(d, nt, nf);
-  hipLaunchKernelGGL(k_sgd_update, dim3(nt + nf), dim3(1024), 0, s, d, sp, nparts, nt, nf);
+  hipLaunchKernelGGL(k_sgd_update, dim3(nt + nf), dim3(kUpdThreads), 0, s, d, sp, nparts, nt, nf);
 }
 
 // DP: cross-workgroup reduction of the partial rows into the packed buffer
 // gacc[0, nl + 2) (slots, loss, sampled count), rank 0's verdict on update
 // i-1 and this rank's ready word into the tail -- all of it int64, ahead of
 // the one all-reduce per iteration.
-__global__ __launch_bounds__(1024) void k_sgd_reduce(DevSgd d, SgdParams sp) {
+__global__ __launch_bounds__(kUpdThreads) void k_sgd_reduce(DevSgd d, SgdParams sp) {
   __shared__ int64_t red[kUpdWaves][kWave];
   if (d.state[0] != 0.0) return;
   // pass skipped on this rank's verdict: its partial rows are stale, it contributes zeros
@@ -1321,7 +1345,7 @@ __global__ __launch_bounds__(1024) void k_sgd_reduce(DevSgd d, SgdParams sp) {
 
 void launch_sgd_reduce(const DevSgd& d, const SgdParams& sp, hipStream_t s) {
   const int grid = d.nparts > 0 ? int((d.nl + kPartVals - kNumNumeric + kWave - 1) / kWave) : 1;
-  hipLaunchKernelGGL(k_sgd_reduce, dim3(grid), dim3(1024), 0, s, d, sp);
+  hipLaunchKernelGGL(k_sgd_reduce, dim3(grid), dim3(kUpdThreads), 0, s, d, sp);
 }
 
 // Convergence of the last update (the loop ended without a prologue seeing it).
@@ -1352,6 +1376,7 @@ void launch_sgd_finish(const DevSgd& d, const SgdParams& sp, hipStream_t s) {
 // ---------------------------------------------------------------------------
 template <int kU>
 __global__ __launch_bounds__(256) void k_far_grad(DevSgd d, SgdParams sp) {
+  kdbg_stamp(d.kdbg, sp.iteration, 1, 0);
   if (d.state[0] != 0.0 || d.state[8] == double(sp.iteration)) return;   // done / DP pass skipped
   const int64_t n = *d.far_n;
   const int lane = lane_id();
@@ -1375,17 +1400,23 @@ __global__ __launch_bounds__(256) void k_far_grad(DevSgd d, SgdParams sp) {
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       long long q = (long long)__float2int_rn(rv[u] * qscale);
-      if (far_seg_scan(e0 + u * kWave + lane, n, sl[u], q) && q != 0)
+      if (far_seg_scan(e0 + u * kWave + lane, n, sl[u], q) && q != 0 && sp.ablate != 9)   // 9: no atomics (timing)
         atomicAdd(&gfar[sl[u] - d.far_base], (unsigned long long)q);
     }
+  }
+  if (d.kdbg) {
+    __syncthreads();
+    kdbg_stamp(d.kdbg, sp.iteration, 1, 1);
   }
 }
 
 void launch_far_grad(const DevSgd& d, const SgdParams& sp, int num_cu, hipStream_t s) {
   static const int ku = [] {
-    const char* e = std::getenv("TWTML_FAR_U");   // tiles per wave step (A/B): 2, 4 or 8
-    const int v = e ? std::atoi(e) : 2;
-    return v == 4 || v == 8 ? v : 2;
+    // tiles per wave step: 4 (r5 A/B on the wide bench: 2 -> 231.9, 4 ->
+    // 233.1, 8 -> 233.2 M tweets/s; 8 costs VGPRs for no further gain)
+    const char* e = std::getenv("TWTML_FAR_U");
+    const int v = e ? std::atoi(e) : 4;
+    return v == 2 || v == 8 ? v : 4;
   }();
   const dim3 g(std::max(1, num_cu * 4));
   if (ku == 8) hipLaunchKernelGGL(k_far_grad<8>, g, dim3(256), 0, s, d, sp);

@@ -29,7 +29,7 @@ from ..oracle.mllib import KMeansState, decay_factor_from_half_life
 from ..records.batch import RawBatch
 from ._native import hip
 from .ingest import SlotPipeline
-from .lr_engine import HostBatchView, Utf8Text
+from .lr_engine import HostBatchView, Utf8Text, raw_slots_entry
 
 
 def no_text(raw: RawBatch) -> Utf8Text:
@@ -63,6 +63,7 @@ class KMDeviceConfig:
     # take the DP path (scaler / cluster-sum all-reduces) even with a
     # world-1 communicator: RCCL carries the collectives on one GPU
     force_dp: bool = False
+    raw_slots: int = 0   # device raw-batch slots (0: TWTML_RAW_SLOTS or the engine default; lr_engine)
 
     def as_dict(self) -> Dict[str, object]:
         if self.time_unit not in ("batches", "points"):
@@ -77,6 +78,7 @@ class KMDeviceConfig:
             "max_rows": int(self.max_rows),
             "max_units": int(self.max_units),
             "force_dp": int(bool(self.force_dp)),
+            **raw_slots_entry(self.raw_slots),
         }
 
 
@@ -92,7 +94,7 @@ class DeviceKMeans:
         st = KMeansState.random(cfg.k, self.dim, cfg.init_weight, cfg.seed)
         self.set_state(st.centers, st.weights)
         self._staging: List[HostBatchView] = []
-        self.raw_slots = int(hip().RAW_SLOTS)
+        self.raw_slots = int(self._eng.raw_slots)
         me = weakref.proxy(self)   # no reference cycle (see DeviceLinearRegression)
         self._pipe = SlotPipeline(self.raw_slots, lambda s, raw: me._stage(s, raw),
                                   lambda hb, slot: me.submit(hb, slot), lambda: me.synchronize())

@@ -20,6 +20,7 @@ from __future__ import annotations
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
+import os
 import weakref
 
 import numpy as np
@@ -93,6 +94,12 @@ class LRDeviceConfig:
     # DP: time each gradient all-reduce on the compute stream (result
     # "comm_ms"; events around the collective)
     comm_timing: bool = False
+    # device raw-batch slots: the copy engine runs up to raw_slots - 1
+    # batches ahead of the one training (0: TWTML_RAW_SLOTS or the engine
+    # default, 8).  Deeper buffering lets the H2D of later batches proceed
+    # while young-model batches (many GD iterations) keep the GPU busy, at
+    # the cost of queueing latency.
+    raw_slots: int = 0
 
     def as_dict(self) -> Dict[str, object]:
         return {
@@ -116,7 +123,15 @@ class LRDeviceConfig:
             "overlap": int(bool(self.overlap)),
             "force_dp": int(bool(self.force_dp)),
             "comm_timing": int(bool(self.comm_timing)),
+            **raw_slots_entry(self.raw_slots),
         }
+
+
+def raw_slots_entry(n: int) -> Dict[str, int]:
+    """The engine config's raw_slots (explicit, TWTML_RAW_SLOTS, else the
+    engine's default)."""
+    n = int(n) or int(os.environ.get("TWTML_RAW_SLOTS", "0") or 0)
+    return {"raw_slots": n} if n > 0 else {}
 
 
 class HostBatchView:
@@ -133,9 +148,16 @@ class HostBatchView:
     No lower-casing happens on the host in either mode.
     """
 
-    def __init__(self, max_rows: int, max_units: int):
+    def __init__(self, max_rows: int, max_units: int, text: bool = True):
+        """text=False: no text buffer (row words and scalars only), for batches
+        whose text is DMA'd from the receiver's registered buffer
+        (``load_utf8(copy_text=False)``): the pinned footprint of a staging
+        slot drops from ~3 bytes per unit to ~60 bytes per row."""
         self.max_units = int(max_units)
+        self.has_text = bool(text)
         cap = max(int(host().wire_bound(self.max_units, int(max_rows))), int(host().utf8_bound(self.max_units)))
+        if not self.has_text:
+            cap = 256
         self._hb = hip().HostBatch(int(max_rows), cap)
         self.text = self._hb.text
         self.offsets = self._hb.offsets
@@ -163,6 +185,8 @@ class HostBatchView:
                              f"({self.max_rows}, {self.max_units})")
 
     def load(self, raw: RawBatch, ingest: str = "wire") -> "HostBatchView":
+        if not self.has_text and not (ingest == "utf8" and raw.utf8 is not None and raw.utf8.pinned):
+            raise ValueError("this staging view has no text buffer (HostBatchView(text=False))")
         if ingest == "utf8" and raw.utf8 is not None:
             # the receiver's own UTF-8 bytes: DMA'd from its page-locked
             # buffer (no host copy), or copied into the staging buffer
@@ -190,6 +214,8 @@ class HostBatchView:
         plus the text copy, which copy_text=False skips: ``submit`` then DMAs
         the text from ``raw.text`` -- register it with :func:`register_host`)."""
         self._check(raw)
+        if copy_text and not self.has_text:
+            raise ValueError("this staging view has no text buffer (HostBatchView(text=False))")
         text = np.ascontiguousarray(raw.text, dtype=np.uint16)
         sc = np.ascontiguousarray(raw.scalars, dtype=np.int64)
         self.bytes = int(self._hb.load_utf16(text, np.ascontiguousarray(raw.offsets, dtype=np.int64),
@@ -207,6 +233,8 @@ class HostBatchView:
         ``u8.data`` -- register it with :func:`register_host`.  ``raw``
         supplies the scalar columns, retweet flags and unit count."""
         self._check(raw)
+        if copy_text and not self.has_text:
+            raise ValueError("this staging view has no text buffer (HostBatchView(text=False))")
         if u8.offsets.shape[0] != raw.n + 1:
             raise ValueError("UTF-8 offsets do not match the batch")
         sc = np.ascontiguousarray(raw.scalars, dtype=np.int64)
@@ -252,7 +280,7 @@ class DeviceLinearRegression:
         self.comm = comm
         self._eng = hip().LREngine(self.device, cfg.as_dict(), comm)
         self._staging: List[HostBatchView] = []
-        self.raw_slots = int(hip().RAW_SLOTS)
+        self.raw_slots = int(self._eng.raw_slots)
         # callbacks through a weak proxy: no reference cycle, so dropping the
         # last reference frees the engine's device memory at once
         me = weakref.proxy(self)
