@@ -270,7 +270,7 @@ def run_e2e(r: Runner, raws, u8s, views, ingest: str, warmup: int, steps: int, s
     return t0, t1
 
 
-def lr_config(args, rows: int, max_units: int, ingest: str, dp: bool = False):
+def lr_config(args, rows: int, max_units: int, ingest: str, dp: bool = False, raw_slots: int = 0):
     from twitter_stream_ml_amd.ops.lr_engine import LRDeviceConfig
     return LRDeviceConfig(num_text_features=args.features, hash=args.hash,
                           step_size=args.step_size, num_iterations=args.iters, fraction=1.0,
@@ -280,7 +280,8 @@ def lr_config(args, rows: int, max_units: int, ingest: str, dp: bool = False):
                           force_dp=bool(getattr(args, "force_dp", False)),
                           # the per-iteration gradient all-reduce is timed whenever the
                           # engine is in DP (events around it on the compute stream)
-                          comm_timing=dp or bool(getattr(args, "force_dp", False)))
+                          comm_timing=dp or bool(getattr(args, "force_dp", False)),
+                          raw_slots=raw_slots or (4 if str(args.batch).lower() == "hbm" else 0))
 
 
 def hbm_batch(args, synth, device: int, ingest: str):
@@ -547,6 +548,9 @@ def main(argv=None) -> int:
     if per_rank is not None:
         out["per_rank_value"] = [round(float(v), 1) for v in per_rank]
     out["prestaged_at_t0"] = prestaged
+    # device raw-batch slots: the H2D runs up to raw_slots - 1 batches ahead of
+    # the batch training (throughput vs queueing latency: TWTML_RAW_SLOTS)
+    out["raw_slots"] = int(eng.raw_slots)
     if moved > 0:
         out["h2d_bytes_per_tweet"] = round(moved / (args.steps * B), 1)
         out["h2d_gbps"] = round(gbps, 1)

@@ -725,7 +725,7 @@ struct KmKeys4 {           // sorted b[0] <= b[1] <= b[2] <= b[3]
     const float n3 = __builtin_amdgcn_fmed3f(b[2], b[3], key);
     const float n2 = __builtin_amdgcn_fmed3f(b[1], b[2], key);
     const float n1 = __builtin_amdgcn_fmed3f(b[0], b[1], key);
-    b[0] = fminf(b[0], key);
+    b[0] = __builtin_amdgcn_fmed3f(b[0], key, -FLT_MAX);   // a min without fminf's canonicalize
     b[1] = n1;
     b[2] = n2;
     b[3] = n3;
@@ -979,6 +979,173 @@ __global__ __launch_bounds__(kBlock) void k_km_assign_bf16x3_lds(const float* X,
   }
 }
 
+// bf16x3 assignment with the epilogue software-pipelined behind the next
+// tile's MFMAs (TWTML_KM_ASSIGN=pipe; one 32-point block per wave).  In
+// k_km_assign_bf16x3_lds a wave runs its 12 dependent MFMAs, then its 16
+// distance insertions, then the barrier: the matrix pipe idles during the
+// wave's VALU and the VALU during its MFMAs unless the SIMD's other waves
+// happen to be out of phase.  Here the MFMAs of tile t and the insertions of
+// tile t-1 (accumulator and centre norms held in registers across the
+// barrier) sit in one basic block, interleaved by sched_group_barrier: ~10
+// VALU per MFMA fill its dependency shadow.  Two accumulators and two norm
+// sets (32 VGPRs) are the price.
+template <int DP>
+__global__ __launch_bounds__(kBlock) void k_km_assign_bf16x3_pipe(const float* X, const float* fac,
+                                                                  const int64_t* counters,
+                                                                  const uint16_t* frag,
+                                                                  const float* cnp, int ntiles,
+                                                                  int lbits, int32_t* labels,
+                                                                  int32_t* refine,
+                                                                  unsigned long long* refine_cnt,
+                                                                  int64_t R) {
+  static_assert(DP % 16 == 0, "bf16x3 path needs DP % 16 == 0");
+  constexpr int KB = DP / 16;
+  constexpr int TILE_V = KB * 2 * kWave;
+  constexpr int PER_T = (TILE_V + kBlock - 1) / kBlock;
+  __shared__ bf16x8 fs[2][TILE_V];
+  __shared__ float cs[2][32];
+  const int lane = lane_id(), h = lane >> 5;
+  const int64_t n = counters[0];
+  const int64_t pb = int64_t(blockIdx.x) * (kBlock / kWave) * 32;
+  if (pb >= n) return;                                   // block-uniform
+  const int64_t p = pb + int64_t(threadIdx.x / kWave) * 32 + (lane & 31);
+  const bf16x8* F = reinterpret_cast<const bf16x8*>(frag);
+  bf16x8 pre[PER_T];
+  float pc = 0.f;
+  auto fetch = [&](int tile) {
+#pragma unroll
+    for (int j = 0; j < PER_T; ++j) {
+      const int v = threadIdx.x + j * kBlock;
+      if (TILE_V % kBlock == 0 || v < TILE_V) pre[j] = F[int64_t(tile) * TILE_V + v];
+    }
+    pc = cnp[tile * 32 + (threadIdx.x & 31)];   // branch-free: keeps the loop body one block
+  };
+  auto park = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < PER_T; ++j) {
+      const int v = threadIdx.x + j * kBlock;
+      if (TILE_V % kBlock == 0 || v < TILE_V) fs[buf][v] = pre[j];
+    }
+    cs[buf][threadIdx.x & 31] = pc;   // 8 lanes store each (identical) norm
+  };
+  fetch(0);
+  bf16x8 xh[KB], xl[KB];
+  float xn = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) {
+    const int col = 16 * kb + 8 * h;
+    float v[8];
+    if (p < n) {
+      const float4 a = *reinterpret_cast<const float4*>(X + p * DP + col);
+      const float4 c = *reinterpret_cast<const float4*>(X + p * DP + col + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = c.x; v[5] = c.y; v[6] = c.z; v[7] = c.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float x = v[j] * fac[col + j];
+      xn += x * x;
+      const uint16_t hi = km_f2bf(x);
+      xh[kb][j] = short(hi);
+      xl[kb][j] = short(km_f2bf(x - km_bf2f(hi)));
+    }
+  }
+  xn += __shfl_xor(xn, 32, kWave);
+  const uint32_t imask = (1u << lbits) - 1u;
+  KmKeys4 t;
+  auto mfma_tile = [&](int tile, f32x16& acc, float (&cn)[16]) {
+    const int buf = tile & 1;
+    acc = f32x16{};
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+      const bf16x8 ah = fs[buf][(kb * 2) * kWave + lane];
+      const bf16x8 al = fs[buf][(kb * 2 + 1) * kWave + lane];
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, xh[kb], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, xl[kb], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, xh[kb], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 c = *reinterpret_cast<const float4*>(&cs[buf][8 * q + 4 * h]);
+      cn[4 * q] = c.x; cn[4 * q + 1] = c.y; cn[4 * q + 2] = c.z; cn[4 * q + 3] = c.w;
+    }
+  };
+  auto epi = [&](int tile, const f32x16& acc, const float (&cn)[16]) {
+    const uint32_t base = uint32_t(tile * 32 + 4 * h);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float dist = fmaf(-2.f, acc[r], cn[r]);
+      t.add(__uint_as_float((__float_as_uint(dist) & ~imask) | (base + uint32_t((r & 3) + 8 * (r >> 2)))));
+    }
+  };
+  // 12 MFMAs (d = 64) with the previous tile's ~130 VALU spread between them.
+  // The empty asm pins the insertions ahead of the barrier (pure arithmetic
+  // is otherwise sunk past it, next to the following tile's epilogue).
+  auto interleave = [&] {
+    asm volatile("" : "+v"(t.b[0]), "+v"(t.b[1]), "+v"(t.b[2]), "+v"(t.b[3]));
+#pragma unroll
+    for (int i = 0; i < 3 * KB; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);    // one MFMA
+      __builtin_amdgcn_sched_group_barrier(0x002, 10, 0);   // then up to 10 VALU
+    }
+  };
+  f32x16 acc0, acc1;
+  float cn0[16], cn1[16];
+  park(0);
+  if (ntiles > 1) fetch(1);
+  __syncthreads();
+  mfma_tile(0, acc0, cn0);
+  if (ntiles > 1) park(1);
+  __syncthreads();
+  int tile = 1;
+  for (; tile + 1 < ntiles; tile += 2) {
+    fetch(tile + 1);
+    mfma_tile(tile, acc1, cn1);
+    epi(tile - 1, acc0, cn0);
+    interleave();
+    park(0);   // tile + 1 (even); tile - 1's readers passed the last barrier
+    __syncthreads();
+    const bool more = tile + 2 < ntiles;
+    if (more) fetch(tile + 2);
+    mfma_tile(tile + 1, acc0, cn0);
+    epi(tile, acc1, cn1);
+    interleave();
+    if (more) park(1);
+    __syncthreads();
+  }
+  if (tile < ntiles) {
+    mfma_tile(tile, acc1, cn1);
+    epi(tile - 1, acc0, cn0);
+    interleave();
+    epi(tile, acc1, cn1);
+  } else {
+    epi(tile - 1, acc0, cn0);
+  }
+  const float q = ldexpf(1.f, lbits - 21);   // 4 key quanta, relative
+  float o[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = __shfl_xor(t.b[j], 32, kWave);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) t.add(o[j]);
+  if (h != 0 || p >= n) return;
+  const float* k4 = t.b;
+  const int i1 = int(__float_as_uint(k4[0]) & imask);
+  labels[p] = i1;
+  const float m = 1e-4f * (3.f * xn + fabsf(k4[0]) + cnp[i1]) + q * fabsf(k4[0]) + 1e-30f;
+  if (k4[1] - k4[0] > m) return;
+  if (k4[3] - k4[0] <= m) {
+    refine[atomicAdd(&refine_cnt[0], 1ull)] = int32_t(p);
+  } else {
+    const int64_t qn = int64_t(atomicAdd(&refine_cnt[1], 1ull));
+    refine[R + qn] = int32_t(p);
+    reinterpret_cast<int4*>(refine + 2 * R)[qn] =
+        make_int4(i1, int(__float_as_uint(k4[1]) & imask),
+                  k4[2] - k4[0] <= m ? int(__float_as_uint(k4[2]) & imask) : -1, -1);
+  }
+}
+
 // Generic fallback (any width): one thread per point, scalar fp32.
 __global__ __launch_bounds__(kBlock) void k_km_assign_scalar(const float* X, const float* fac,
                                                              const int64_t* counters,
@@ -1104,9 +1271,21 @@ void launch_km_assign(const float* X, const float* f32, const double* f64, const
       const char* e = std::getenv("TWTML_KM_ASSIGN");
       if (e && std::strcmp(e, "reg") == 0) return 0;
       if (e && std::strcmp(e, "lds2") == 0) return 2;
+      if (e && std::strcmp(e, "pipe") == 0) return 3;
       return 1;
     }();
-    if (variant == 0) {
+#define KM_BF16P(DPV)                                                                              \
+  case DPV: {                                                                                      \
+    const int64_t waves = (max_rows + 31) / 32;                                                    \
+    hipLaunchKernelGGL((k_km_assign_bf16x3_pipe<DPV>), dim3(int((waves + 3) / 4)), dim3(kBlock),   \
+                       0, s, X, f32, counters, frag, cnp, ntiles, lbits, labels, refine, refine_cnt, \
+                       R);                                                                         \
+    done = true;                                                                                   \
+    break;                                                                                         \
+  }
+    if (variant == 3) {
+      switch (dp) { KM_BF16P(16) KM_BF16P(32) KM_BF16P(64) KM_BF16P(128) default: break; }
+    } else if (variant == 0) {
       switch (dp) { KM_BF16(16, 2) KM_BF16(32, 2) KM_BF16(64, 2) KM_BF16(128, 1) default: break; }
     } else if (variant == 2) {
       switch (dp) { KM_BF16L(16, 2) KM_BF16L(32, 2) KM_BF16L(64, 2) KM_BF16L(128, 1) default: break; }
@@ -1115,6 +1294,7 @@ void launch_km_assign(const float* X, const float* f32, const double* f64, const
     }
 #undef KM_BF16
 #undef KM_BF16L
+#undef KM_BF16P
   }
   if (mfma && !done) {
 #define KM_MFMA(DPV)                                                                                \

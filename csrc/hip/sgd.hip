@@ -1688,23 +1688,43 @@ __global__ __launch_bounds__(kStatThreads) void k_batch_stats(DevSgd d, const fl
   }
 }
 
-__global__ void k_batch_stats_fin(DevSgd d, int nblocks) {
-  const int k = lane_id();
-  if (k >= kStatI + 6) return;
-  int64_t v = 0;
-  double vf = 0.0;
-  for (int b = 0; b < nblocks; ++b) {   // block order: deterministic
-    const int64_t x = d.stat_part[int64_t(b) * 16 + k];
-    if (k < kStatI) v += x;
-    else vf += __builtin_bit_cast(double, x);
+// Block partials -> totals: lane l of wave w holds block w * 64 + l's
+// partials (all loads in flight at once; a single lane walking the blocks
+// was 256 dependent loads, ~70 us on the compute stream), a fixed butterfly
+// per wave, then the 4 wave sums in order: deterministic for the fp64
+// spill columns, exact for the int64 ones.
+__global__ __launch_bounds__(kStatBlocks) void k_batch_stats_fin(DevSgd d, int nblocks) {
+  __shared__ int64_t ws[kStatBlocks / kWave][kStatI + 6];
+  const int b = threadIdx.x, lane = lane_id(), w = threadIdx.x / kWave;
+  int64_t v[kStatI + 6];
+#pragma unroll
+  for (int k = 0; k < kStatI + 6; ++k) v[k] = b < nblocks ? d.stat_part[int64_t(b) * 16 + k] : 0;
+#pragma unroll
+  for (int k = 0; k < kStatI; ++k) {
+    const int64_t t = wave_sum_i64(v[k]);
+    if (lane == 0) ws[w][k] = t;
   }
-  if (k < kStatI) d.stat_i[k] = v;
-  else d.stats[k - kStatI] = vf;
+#pragma unroll
+  for (int k = kStatI; k < kStatI + 6; ++k) {
+    const double t = wave_sum(b < nblocks ? __builtin_bit_cast(double, v[k]) : 0.0);
+    if (lane == 0) ws[w][k] = __builtin_bit_cast(int64_t, t);
+  }
+  __syncthreads();
+  const int k = threadIdx.x;
+  if (k < kStatI) {
+    int64_t t = 0;
+    for (int j = 0; j < kStatBlocks / kWave; ++j) t += ws[j][k];
+    d.stat_i[k] = t;
+  } else if (k < kStatI + 6) {
+    double t = 0.0;
+    for (int j = 0; j < kStatBlocks / kWave; ++j) t += __builtin_bit_cast(double, ws[j][k]);
+    d.stats[k - kStatI] = t;
+  }
 }
 
 void launch_batch_stats(const DevSgd& d, const DevPrepared& p, hipStream_t s) {
   hipLaunchKernelGGL(k_batch_stats, dim3(kStatBlocks), dim3(kStatThreads), 0, s, d, p.y, p.counters);
-  hipLaunchKernelGGL(k_batch_stats_fin, dim3(1), dim3(kWave), 0, s, d, kStatBlocks);
+  hipLaunchKernelGGL(k_batch_stats_fin, dim3(1), dim3(kStatBlocks), 0, s, d, kStatBlocks);
 }
 
 // ---------------------------------------------------------------------------

@@ -284,3 +284,44 @@ def test_kmeans_features_exact(hip_module, text_dims):
         assert got.shape[0] == want.shape[0]
         np.testing.assert_array_equal(got[:, :2 + text_dims], want.astype(np.float32))
         assert not got[:, 2 + text_dims:].any()
+
+
+_VARIANT_SCRIPT = r"""
+import hashlib, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+from twitter_stream_ml_amd.ops.kmeans_engine import DeviceKMeans, KMDeviceConfig
+from twitter_stream_ml_amd.sources.synthetic import SynthConfig, generate_batch
+h = hashlib.sha256()
+for k, td in ((1024, 62), (200, 14), (64, 30), (96, 126)):
+    dev = DeviceKMeans(KMDeviceConfig(k=k, text_dims=td, max_rows=8192, max_units=8192 * 300,
+                                      precision="bf16x3", seed=3), device=0)
+    synth = SynthConfig.profile("twitter", seed=17, unicode_fraction=0.2)
+    for t in range(3):
+        r = dev.update_raw(generate_batch(synth, t * 6000, 6000, batch_time_ms=1_700_000_000_000 + t))
+        h.update(np.asarray(r["pred"]).tobytes())
+    c, w = dev.get_state()
+    h.update(c.tobytes()); h.update(w.tobytes())
+print("DIGEST", h.hexdigest())
+"""
+
+
+def test_kmeans_assign_variants_bitwise(hip_module, tmp_path):
+    """The bf16x3 assignment variants (``TWTML_KM_ASSIGN``: lds default, pipe
+    = epilogue software-pipelined behind the next tile's MFMAs, lds2, reg)
+    issue the same MFMAs in the same order, so labels, refine routing and
+    the updated model are identical bit for bit (d = 16, 32, 64, 128)."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "km_variant.py"
+    script.write_text(_VARIANT_SCRIPT)
+    digests = {}
+    for v in ("lds", "pipe", "lds2", "reg"):
+        env = dict(os.environ, TWTML_KM_ASSIGN=v)
+        out = subprocess.run([sys.executable, str(script), repo], env=env, capture_output=True,
+                             text=True, timeout=240)
+        assert out.returncode == 0, out.stderr[-2000:]
+        digests[v] = [ln for ln in out.stdout.splitlines() if ln.startswith("DIGEST")][-1]
+    assert len(set(digests.values())) == 1, digests

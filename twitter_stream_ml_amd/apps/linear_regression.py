@@ -73,17 +73,21 @@ def build_engine(conf: ConfArguments, rank: int, world: int, device: Optional[in
         import torch
         share_host_threads(dev, rank, int(os.environ.get("LOCAL_WORLD_SIZE", world)),
                            max(1, torch.cuda.device_count()))
+        cap = os.environ.get("TWTML_BATCH_ROWS", "")
+
         def lr_cfg(rows: int) -> LRDeviceConfig:
             # ingest "utf8": the receiver's UTF-8 bytes cross PCIe as they are
             # (DMA'd from its page-locked buffer when the source pins them) and
-            # the device decodes / lower-cases / narrows -- the path bench.py times
+            # the device decodes / lower-cases / narrows -- the path bench.py times.
+            # HBM-sized batches keep 4 raw slots: each slot holds a whole batch
+            # of text, and the rows are worth more than run-ahead depth there
             return LRDeviceConfig(num_text_features=F, hash=conf.hash, step_size=conf.stepSize,
                                   num_iterations=conf.numIterations, fraction=conf.miniBatchFraction,
                                   begin=conf.numRetweetBegin, end=conf.numRetweetEnd,
-                                  max_rows=rows, max_units=rows * 290, ingest="utf8")
+                                  max_rows=rows, max_units=rows * 290, ingest="utf8",
+                                  raw_slots=4 if cap.lower() == "hbm" else 0)
 
         rows = max_rows or max(65536, int(conf.batchSize or 0))
-        cap = os.environ.get("TWTML_BATCH_ROWS", "")
         if cap.lower() == "hbm":   # the largest micro-batch 80 % of this GPU's free HBM holds
             import torch
             from ..ops.sizing import hbm_max_rows
