@@ -562,6 +562,8 @@ def main(argv=None) -> int:
         out["grad_allreduce_us_per_iter"] = round(D.allreduce_max_scalar(
             1e3 * sum(c[1] for c in runner.comm) / n_ar), 2)
         out["allreduce_bytes_per_iter"] = int(round(sum(c[2] for c in runner.comm) / n_ar))
+        # gradient all-reduce time per timed step (max over ranks): the DP cost model's check
+        out["comm_ms_per_step"] = round(D.allreduce_max_scalar(sum(c[1] for c in runner.comm) / len(runner.comm)), 3)
     out["replicas_identical"] = bool(replicas)
     if comm is not None:
         out["rccl_version"] = rccl_version()

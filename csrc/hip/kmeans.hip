@@ -169,7 +169,7 @@ constexpr int kKmStageDw = 1216;   // staged dwords per wave (4.75 KB; wide chun
 __host__ __device__ constexpr int km_hist_words(int td) { return (td + 1) / 2; }
 
 __host__ __device__ constexpr int km_bal_wave_dwords(int td) {
-  return kKmStageDw + kRowsPerChunk * km_hist_words(td) + kRowsPerChunk * 4 + kRowsPerChunk * 2;
+  return kKmStageDw + kRowsPerChunk * km_hist_words(td) + kRowsPerChunk * 4 + kRowsPerChunk * 2 + kRowsPerChunk;
 }
 
 __global__ __launch_bounds__(kBlock) void k_km_features_bal(DevRawBatch b, const int64_t* kept,
@@ -189,6 +189,7 @@ __global__ __launch_bounds__(kBlock) void k_km_features_bal(DevRawBatch b, const
   uint32_t* hist = st + kKmStageDw;                          // [16][hw]: bin b in the half b & 1 of word b >> 1
   int32_t* meta = reinterpret_cast<int32_t*>(hist + kRowsPerChunk * hw);   // [16][4]
   int64_t* mo = reinterpret_cast<int64_t*>(meta + kRowsPerChunk * 4);       // [16] row byte offsets
+  int32_t* dwe = reinterpret_cast<int32_t*>(mo + kRowsPerChunk);            // [16] staged dword ends
   const uint8_t* stb = reinterpret_cast<const uint8_t*>(st);
   const int64_t n_kept = counters[0];
   const int64_t nch = (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;
@@ -233,6 +234,7 @@ __global__ __launch_bounds__(kBlock) void k_km_features_bal(DevRawBatch b, const
       meta[4 * lane + 2] = staged ? 4 * dw0 + ob : -1;       // staged byte offset
       meta[4 * lane + 3] = wide | (len == 1 ? 2 : 0);
       mo[lane] = o;
+      dwe[lane] = staged ? sdw : dw0;                        // unstaged: an empty dword range
     }
     const int T = __shfl(snz, kRowsPerChunk - 1, kWave);
     for (int i = lane; i < kRowsPerChunk * hw; i += kWave) hist[i] = 0u;
@@ -320,69 +322,53 @@ __global__ __launch_bounds__(kBlock) void k_km_features_bal(DevRawBatch b, const
         }
       }
     };
-    // Staged chunks: the lane's range is walked by kCur independent cursors in
-    // lock step, so kCur LDS unit reads and kCur histogram adds are in flight
-    // per step (the single walk was one dependent read -> hash -> ds_add
-    // chain per bigram, at ~2.5 waves per SIMD).
-    auto walk_multi = [&]() {
-      constexpr int kCur = 4;
-      int cg[kCur], ce[kCur], cq[kCur], cj[kCur], cn[kCur], cb[kCur], ck[kCur];
-      uint32_t cu[kCur];
+    // Staged chunks: every lane takes an equal share of the chunk's staged
+    // dwords and hashes the bigrams that START in each of its dwords -- 4
+    // narrow or 2 wide slots per dword, the slot's two units cut out of the
+    // dword pair (d, d + 1) by one v_alignbyte -- so the walk has no
+    // per-bigram cursor state and each lane has 4 independent hash -> add
+    // chains per dword.  (Round 3-4: four bigram cursors per lane, ~110
+    // lane-ops per bigram in the PMC counts.)  Staged bytes outside a row's
+    // units (alignment head, tail) fail the slot's range check.
+    auto walk_dw = [&]() {
+      const int dtot = __shfl(sdw, kRowsPerChunk - 1, kWave);
+      const int d0 = int((int64_t(lane) * dtot) >> 6), d1 = int((int64_t(lane + 1) * dtot) >> 6);
+      if (d0 >= d1) return;
+      int q = 0;
 #pragma unroll
-      for (int i = 0; i < kCur; ++i) {
-        cg[i] = g0 + int((int64_t(g1 - g0) * i) / kCur);
-        ce[i] = g0 + int((int64_t(g1 - g0) * (i + 1)) / kCur);
-        int qq = 0;
+      for (int k = 0; k < kRowsPerChunk; ++k) q += (d0 >= __builtin_amdgcn_readlane(sdw, k)) ? 1 : 0;
+      int rend = 0, b0 = 0, lim = 0, us = 1, one1 = 0, rq = 0;
+      auto row = [&]() {
+        rend = dwe[q];
+        b0 = meta[4 * q + 2];
+        const int rk = meta[4 * q + 3];
+        us = 1 + (rk & 1);
+        one1 = rk & 2;
+        lim = meta[4 * q + 1] * us;   // byte span of the row's bigram starts
+        rq = q * hw;
+      };
+      row();
+      for (int d = d0; d < d1; ++d) {
+        while (d >= rend) { ++q; row(); }   // (empty and unstaged rows have empty ranges)
+        const uint32_t v = st[d], v2 = st[d + 1];   // (d + 1 may read the histograms: masked)
+        const int pb = 4 * d - b0;                   // slot 0's byte within the row's units
+        const uint32_t ub = 8u * uint32_t(us);
+        const uint32_t umask = us == 1 ? 0xFFu : 0xFFFFu;
 #pragma unroll
-        for (int k = 0; k < kRowsPerChunk; ++k) qq += (cg[i] >= __builtin_amdgcn_readlane(snz, k)) ? 1 : 0;
-        qq = qq < kRowsPerChunk ? qq : kRowsPerChunk - 1;
-        cq[i] = qq;
-        cn[i] = meta[4 * qq + 1];
-        cb[i] = max(meta[4 * qq + 2], 0);   // (-1: an invalid row, only under an empty cursor)
-        ck[i] = meta[4 * qq + 3];
-        cj[i] = cg[i] - meta[4 * qq + 0];
-        const int wd = ck[i] & 1;
-        const int jj = cg[i] < ce[i] ? cj[i] : 0;
-        cu[i] = wd ? uint32_t(*reinterpret_cast<const uint16_t*>(stb + cb[i] + 2 * jj)) : uint32_t(stb[cb[i] + jj]);
-      }
-      while (true) {
-        bool live = false;
-#pragma unroll
-        for (int i = 0; i < kCur; ++i) live |= cg[i] < ce[i];
-        if (!live) break;
-        uint32_t u1[kCur];
-#pragma unroll
-        for (int i = 0; i < kCur; ++i) {   // unconditional reads (clamped): all in flight together
-          const int wd = ck[i] & 1;
-          const int jj = (cg[i] < ce[i] && !(ck[i] & 2)) ? cj[i] + 1 : 0;
-          u1[i] = wd ? uint32_t(*reinterpret_cast<const uint16_t*>(stb + cb[i] + 2 * jj)) : uint32_t(stb[cb[i] + jj]);
-        }
-#pragma unroll
-        for (int i = 0; i < kCur; ++i) {
-          if (cg[i] >= ce[i]) continue;
-          const uint32_t v1 = (ck[i] & 2) ? 0u : u1[i];
-          const uint32_t h = (ck[i] & 2) ? cu[i] : 31u * cu[i] + v1;
-          const uint32_t bin = one ? 0u : h - __umulhi(h, mg) * tdu;
-          __hip_atomic_fetch_add(hist + cq[i] * hw + int(bin >> 1), 1u << ((bin & 1u) * 16), __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-          if (++cg[i] >= ce[i]) continue;
-          if (++cj[i] < cn[i]) {
-            cu[i] = v1;
-          } else {                                 // next row with bigrams
-            do {
-              ++cq[i];
-              cn[i] = meta[4 * cq[i] + 1];
-            } while (cn[i] == 0);
-            cb[i] = meta[4 * cq[i] + 2];
-            ck[i] = meta[4 * cq[i] + 3];
-            cj[i] = 0;
-            const int wd = ck[i] & 1;
-            cu[i] = wd ? uint32_t(*reinterpret_cast<const uint16_t*>(stb + cb[i])) : uint32_t(stb[cb[i]]);
+        for (int y = 0; y < 4; ++y) {
+          const int sh = y * us;
+          if (sh < 4 && unsigned(pb + sh) < unsigned(lim)) {
+            const uint32_t wv = __builtin_amdgcn_alignbyte(v2, v, uint32_t(sh));
+            const uint32_t u0 = wv & umask;
+            const uint32_t h = one1 ? u0 : 31u * u0 + __builtin_amdgcn_ubfe(wv, ub, ub);
+            const uint32_t bin = one ? 0u : h - __umulhi(h, mg) * tdu;
+            __hip_atomic_fetch_add(hist + rq + int(bin >> 1), 1u << ((bin & 1u) * 16), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
           }
         }
       }
     };
-    if (all_staged) walk_multi();
+    if (all_staged) walk_dw();
     else walk(std::false_type{});
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
