@@ -51,6 +51,20 @@
 
 namespace twtml {
 
+// Workgroup epilogue: every workgroup writes one int64 partial row (plain
+// stores) that k_sgd_update / k_sgd_reduce sum (exact in any order):
+//   cols 0..3 numeric gradients (2^N_k), 4..far_base-1 text slots (2^S),
+//   far_base..nl-1 zero, nl loss (2^L), nl+1 sampled row count.
+constexpr int kPartVals = 6;
+
+// 256-thread update / reduce workgroups: they run beside the prep stream's
+// kernels, and a 1024-thread workgroup needs 16 free wave slots on one CU --
+// with prep workgroups resident, the r5 per-workgroup stamps showed the
+// 433 update workgroups dispatched over ~52 us for ~5 us of work each.
+constexpr int kUpdThreads = 256;
+constexpr int kUpdWaves = kUpdThreads / kWave;   // waves per workgroup (partial-row split)
+constexpr int kUpdFarSlots = kUpdThreads;        // far slots per far update workgroup (one per thread)
+
 // Per-workgroup start / end stamps of the GD kernels (TWTML_ITER_TIMING only).
 __device__ __forceinline__ void kdbg_stamp(uint64_t* base, int it, int kind, int end) {
   if (!base || threadIdx.x != 0 || blockIdx.x >= unsigned(kKdbgWgs)) return;
@@ -124,9 +138,8 @@ struct IterScale {
 
 // Deterministic in (max |w_text|, numeric weights, batch bounds, m): every
 // workgroup, every iteration kernel and every DP rank derives the same.
-__device__ IterScale sgd_scales(const DevSgd& d, double maxw, const float* wn) {
+__device__ IterScale sgd_scales(const double* bd, double maxw, const float* wn) {
   IterScale s{};
-  const double* bd = d.bounds;
   double B = bd[0] * maxw + bd[1];
 #pragma unroll
   for (int k = 0; k < kNumNumeric; ++k) B += bd[2 + k] * fabs(double(wn[k]));
@@ -205,9 +218,20 @@ __device__ __forceinline__ LaneScale lane_scale(const IterScale& sc, const DevSg
 // fixed-order DPP reduction): identical in every caller.  Also returns the
 // max |w_text| after that update (the next iteration's weight scale).
 // ---------------------------------------------------------------------------
+// Workgroups of every update launch of the batch (host: update_split): the
+// number of partials in each record, known without reading the record.
+__device__ __forceinline__ int upd_grid(const DevSgd& d) {
+  const int64_t tiles = (d.nl + kPartVals - kNumNumeric + kWave - 1) / kWave;
+  const int64_t n_far = kNumNumeric + d.n_unique - d.far_base;
+  const int nt = int(max(int64_t(1), min(tiles, int64_t(kMaxUpdGrid / 2))));
+  const int nf = n_far > 0 ? int(max(int64_t(1), min((n_far + kUpdFarSlots - 1) / kUpdFarSlots, int64_t(kMaxUpdGrid - nt))))
+                           : 0;
+  return nt + nf;
+}
+
 __device__ bool sgd_converged_wave(const DevSgd& d, int it, double tol, double* maxw_out = nullptr) {
   const double* rec = sgd_rec(d, it);
-  const int nw = int(rec[2]);
+  const int nw = upd_grid(d);   // (rec[2] holds the same; reading it first cost a dependent round trip)
   double ds = 0.0, ws = 0.0, mx = 0.0;
   for (int k = lane_id(); k < nw; k += kWave) {
     ds += rec[kRecHead + 3 * k];
@@ -238,13 +262,20 @@ __device__ bool sgd_converged_wave(const DevSgd& d, int it, double tol, double* 
 __device__ bool sgd_prologue(const DevSgd& d, const SgdParams& sp, int* flag, IterScale* sc) {
   if (threadIdx.x < kWave) {
     const int it = sp.iteration;
-    const bool done = d.state[0] != 0.0;
+    // every load up front and independent of the others (one memory round
+    // trip instead of four dependent ones: ~3.8 us of each iteration's
+    // prologue in the per-workgroup timeline, r5)
+    const double st0 = d.state[0];
+    double maxw = d.state[9];
+    const float wn[kNumNumeric] = {d.wc32[0], d.wc32[1], d.wc32[2], d.wc32[3]};
+    double bd[kBoundsLen];
+#pragma unroll
+    for (int k = 0; k < kBoundsLen; ++k) bd[k] = d.bounds[k];
+    const bool conv = it > 1 && sgd_converged_wave(d, it - 1, sp.tol, &maxw);
+    const bool done = st0 != 0.0;
     bool stop = done;
     if (!done) {
-      double maxw = d.state[9];
-      const bool conv = it > 1 && sgd_converged_wave(d, it - 1, sp.tol, &maxw);
-      const float wn[kNumNumeric] = {d.wc32[0], d.wc32[1], d.wc32[2], d.wc32[3]};
-      const IterScale s = sgd_scales(d, maxw, wn);
+      const IterScale s = sgd_scales(bd, maxw, wn);
       stop = conv || s.bad;
       if (blockIdx.x == 0 && threadIdx.x == 0) {
         double* rec = sgd_rec(d, it);
@@ -341,11 +372,6 @@ __device__ __forceinline__ float row_residual(int32_t dot_fix, const RowIn& ri, 
   return r;
 }
 
-// Workgroup epilogue: every workgroup writes one int64 partial row (plain
-// stores) that k_sgd_update / k_sgd_reduce sum (exact in any order):
-//   cols 0..3 numeric gradients (2^N_k), 4..far_base-1 text slots (2^S),
-//   far_base..nl-1 zero, nl loss (2^L), nl+1 sampled row count.
-constexpr int kPartVals = 6;
 
 template <bool STATS>
 __device__ __forceinline__ void part_scalars(const DevSgd& d, int64_t qn, int64_t ql, const RowAcc& acc,
@@ -1052,13 +1078,6 @@ int sgd_partials(int64_t ns, bool u16, int grid) {
 // nparts > 0: the column sums come from the partial rows (single GPU);
 // nparts == 0: gacc holds them (all-reduced).
 // ---------------------------------------------------------------------------
-// 256-thread update / reduce workgroups: they run beside the prep stream's
-// kernels, and a 1024-thread workgroup needs 16 free wave slots on one CU --
-// with prep workgroups resident, the r5 per-workgroup stamps showed the
-// 433 update workgroups dispatched over ~52 us for ~5 us of work each.
-constexpr int kUpdThreads = 256;
-constexpr int kUpdWaves = kUpdThreads / kWave;   // waves per workgroup (partial-row split)
-constexpr int kUpdFarSlots = kUpdThreads;        // far slots per far update workgroup (one per thread)
 
 // Sum of partial rows for columns [col0, col0 + 64): returns lane's column
 // sum in wave 0 (other waves: 0); columns >= dcol0 are fp64 (bits returned).

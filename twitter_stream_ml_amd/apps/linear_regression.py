@@ -85,7 +85,12 @@ def build_engine(conf: ConfArguments, rank: int, world: int, device: Optional[in
                                   num_iterations=conf.numIterations, fraction=conf.miniBatchFraction,
                                   begin=conf.numRetweetBegin, end=conf.numRetweetEnd,
                                   max_rows=rows, max_units=rows * 290, ingest="utf8",
-                                  raw_slots=4 if cap.lower() == "hbm" else 0)
+                                  # 4 device raw slots (TWTML_RAW_SLOTS overrides): the driver
+                                  # prefetches only the batches its scheduler has sealed, and
+                                  # latency matters more here than the bench's 8-slot run-ahead
+                                  # (tests/test_gpu_checkpoint.py p99 failed at 8); the HBM
+                                  # sizing counts 4 slots' bytes
+                                  raw_slots=int(os.environ.get("TWTML_RAW_SLOTS", "0") or 0) or 4)
 
         rows = max_rows or max(65536, int(conf.batchSize or 0))
         if cap.lower() == "hbm":   # the largest micro-batch 80 % of this GPU's free HBM holds
