@@ -325,6 +325,28 @@ __device__ __forceinline__ uint32_t byte_bits(uint32_t x) {
   return (x * 0x10204080u) >> 28;   // the four products land on bits 28..31, no carries
 }
 
+// Bytes of x equal to b (per byte: bit 7 set), exact (no borrow between bytes).
+__device__ __forceinline__ uint32_t bytes_eq(uint32_t x, uint32_t b) {
+  const uint32_t t = x ^ (b * 0x01010101u);
+  return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
+}
+
+// UTF-8 byte pairs that start a unit whose lower-casing is not one UTF-16
+// unit per unit (rows.hip's special rows): C4 B0 (U+0130), CE A3 (U+03A3,
+// Final_Sigma), F0 90 / F0 91 / F0 96 / F0 9E (the planes of the astral
+// cased letters: Deseret, Osage, Old Hungarian, Warang Citi, Medefaidrin,
+// Adlam; emoji, F0 9F, are not).  A superset of the special rows: the
+// normaliser checks every flagged row exactly.  v: four bytes, n: the
+// byte after each of them.
+__device__ __forceinline__ uint32_t special_pairs(uint32_t v, uint32_t n) {
+  const uint32_t c4 = bytes_eq(v, 0xC4u), ce = bytes_eq(v, 0xCEu), f0 = bytes_eq(v, 0xF0u);
+  if (!(c4 | ce | f0)) return 0u;   // most multi-byte text (CJK, Cyrillic, Arabic, ...) has none of the leads
+  uint32_t m = (c4 & bytes_eq(n, 0xB0u)) | (ce & bytes_eq(n, 0xA3u));
+  if (f0)
+    m |= f0 & (bytes_eq(n, 0x90u) | bytes_eq(n, 0x91u) | bytes_eq(n, 0x96u) | bytes_eq(n, 0x9Eu));
+  return m;
+}
+
 // One decode step of row [o, e) (class 1 or 2, output at text + d0): the
 // lane's aligned dword v of the row at w0 + 4 lane (and the next one, v2,
 // for the continuation bytes of its leads); k = the row's units so far.
@@ -333,8 +355,11 @@ __device__ __forceinline__ uint32_t byte_bits(uint32_t x) {
 // non-continuation byte (two at a 4-byte lead: the surrogate pair); a lane's
 // units (0..8) are ranked across the wave from four ballots of their bit
 // planes.
+// UTF-16 (class 2) rows also OR their special-pair candidates into `spec`
+// (the lane's dword, bytes inside the row, each paired with the byte after
+// it): one check per dword here, where all 64 lanes walk the row together.
 __device__ __forceinline__ void decode_step(uint8_t* text, int64_t o, int32_t ie, int64_t d0, bool nar,
-                                            int64_t w0, uint32_t v, uint32_t v2, int32_t& k) {
+                                            int64_t w0, uint32_t v, uint32_t v2, int32_t& k, uint32_t& spec) {
   uint16_t* dst = reinterpret_cast<uint16_t*>(text + d0);
   uint8_t* dst8 = text + d0;
   const int lane = lane_id();
@@ -344,6 +369,11 @@ __device__ __forceinline__ void decode_step(uint8_t* text, int64_t o, int32_t ie
   const int32_t lo = iw < 0 ? -iw : 0;
   const int32_t hi = ie - iw >= 4 ? 4 : (ie - iw < 0 ? 0 : ie - iw);
   const uint32_t rng = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+  if (!nar) {
+    const uint32_t bm = (hi >= 4 ? 0xFFFFFFFFu : ((1u << (8 * hi)) - 1u)) & ~((1u << (8 * lo)) - 1u);
+    const uint32_t vm = v & bm;
+    if (vm & 0x80808080u) spec |= special_pairs(vm, (v >> 8) | (v2 << 24));
+  }
   // a 4-byte lead also needs iw + j + 3 < ie
   const int32_t h3 = ie - iw - 3;
   const uint32_t rng3 = h3 >= 4 ? 0xFu : (h3 <= 0 ? 0u : (1u << h3) - 1u);
@@ -385,9 +415,10 @@ __device__ __forceinline__ void decode_step(uint8_t* text, int64_t o, int32_t ie
 // Decode row [o, e) (class 1 or 2) to dst (tail + 2 o); returns its units.
 template <typename Src>
 __device__ __forceinline__ int64_t decode_row(const Src& src, uint8_t* text, int64_t o, int64_t e, int64_t d0,
-                                              bool nar) {
+                                              bool nar, bool& sp) {
   const int32_t ie = int32_t(e - o);   // row bytes (< 2^13)
   int32_t k = 0;
+  uint32_t spec = 0;
   for (int64_t w0 = o & ~int64_t(3); w0 < e; w0 += 4 * kWave) {
     const int32_t iw = int32_t(w0 - o) + 4 * lane_id();
     uint32_t v = 0, v2 = 0;
@@ -395,8 +426,9 @@ __device__ __forceinline__ int64_t decode_row(const Src& src, uint8_t* text, int
       v = src.dword(w0 + 4 * lane_id());
       v2 = src.dword(w0 + 4 * lane_id() + 4);
     }
-    decode_step(text, o, ie, d0, nar, w0, v, v2, k);
+    decode_step(text, o, ie, d0, nar, w0, v, v2, k, spec);
   }
+  sp = __any(spec != 0u);
   return k;
 }
 
@@ -406,11 +438,12 @@ __device__ __forceinline__ int64_t decode_row(const Src& src, uint8_t* text, int
 // latency-bound at ~0.1 instructions per cycle per SIMD.)
 __device__ __forceinline__ void decode_rows2(const LdsBytes& src, uint8_t* text, int64_t oA, int64_t eA,
                                              int64_t d0A, bool narA, int32_t& kA, int64_t oB, int64_t eB,
-                                             int64_t d0B, bool narB, int32_t& kB) {
+                                             int64_t d0B, bool narB, int32_t& kB, bool& spA, bool& spB) {
   const int32_t ieA = int32_t(eA - oA), ieB = int32_t(eB - oB);
   const int lane = lane_id();
   kA = 0;
   kB = 0;
+  uint32_t sA = 0, sB = 0;
   int64_t wA = oA & ~int64_t(3), wB = oB & ~int64_t(3);
   while (wA < eA || wB < eB) {
     const bool actA = wA < eA, actB = wB < eB;   // wave-uniform
@@ -423,57 +456,28 @@ __device__ __forceinline__ void decode_rows2(const LdsBytes& src, uint8_t* text,
     if (!okA) vA = v2A = 0u;
     if (!okB) vB = v2B = 0u;
     if (actA) {
-      decode_step(text, oA, ieA, d0A, narA, wA, vA, v2A, kA);
+      decode_step(text, oA, ieA, d0A, narA, wA, vA, v2A, kA, sA);
       wA += 4 * kWave;
     }
     if (actB) {
-      decode_step(text, oB, ieB, d0B, narB, wB, vB, v2B, kB);
+      decode_step(text, oB, ieB, d0B, narB, wB, vB, v2B, kB, sB);
       wB += 4 * kWave;
     }
   }
+  spA = __any(sA != 0u);
+  spB = __any(sB != 0u);
 }
 
-// Bytes of x equal to b (per byte: bit 7 set), exact (no borrow between bytes).
-__device__ __forceinline__ uint32_t bytes_eq(uint32_t x, uint32_t b) {
-  const uint32_t t = x ^ (b * 0x01010101u);
-  return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
-}
-
-// UTF-8 byte pairs that start a unit whose lower-casing is not one UTF-16
-// unit per unit (rows.hip's special rows): C4 B0 (U+0130), CE A3 (U+03A3,
-// Final_Sigma), F0 90 / F0 91 / F0 96 / F0 9E (the planes of the astral
-// cased letters: Deseret, Osage, Old Hungarian, Warang Citi, Medefaidrin,
-// Adlam; emoji, F0 9F, are not).  A superset of the special rows: the
-// normaliser checks every flagged row exactly.  v: four bytes, n: the
-// byte after each of them.
-__device__ __forceinline__ uint32_t special_pairs(uint32_t v, uint32_t n) {
-  const uint32_t c4 = bytes_eq(v, 0xC4u), ce = bytes_eq(v, 0xCEu), f0 = bytes_eq(v, 0xF0u);
-  if (!(c4 | ce | f0)) return 0u;   // most multi-byte text (CJK, Cyrillic, Arabic, ...) has none of the leads
-  uint32_t m = (c4 & bytes_eq(n, 0xB0u)) | (ce & bytes_eq(n, 0xA3u));
-  if (f0)
-    m |= f0 & (bytes_eq(n, 0x90u) | bytes_eq(n, 0x91u) | bytes_eq(n, 0x96u) | bytes_eq(n, 0x9Eu));
-  return m;
-}
-
-// One lane's row class from the staged bytes [lo, le) (as row_class), and
-// (sp) whether the row holds a special-unit candidate (class 2 rows only:
-// every special pair has a byte >= 0xC4).
-__device__ __forceinline__ int lane_row_class(const uint8_t* lbuf, int lo, int le, bool& sp) {
-  uint32_t acc = 0, big = 0, spec = 0, prev = 0;
+// One lane's row class from the staged bytes [lo, le) (as row_class).
+__device__ __forceinline__ int lane_row_class(const uint8_t* lbuf, int lo, int le) {
+  uint32_t acc = 0, big = 0;
   for (int w = lo & ~3; w < le; w += 4) {
     uint32_t v = *reinterpret_cast<const uint32_t*>(lbuf + w);
     if (w < lo) v &= 0xFFFFFFFFu << (8 * (lo - w));
     if (w + 4 > le) v &= 0xFFFFFFFFu >> (8 * (w + 4 - le));
     acc |= v;
     big |= v & ((v & 0x7F7F7F7Fu) + 0x3C3C3C3Cu);   // a byte >= 0xC4 sets its bit 7
-    // the previous dword's byte pairs, its last byte paired with this
-    // dword's first (no extra LDS read: a dependent load per dword made the
-    // loop latency-bound)
-    if (prev & 0x80808080u) spec |= special_pairs(prev, (prev >> 8) | (v << 24));
-    prev = v;
   }
-  if (prev & 0x80808080u) spec |= special_pairs(prev, prev >> 8);
-  sp = spec != 0u;
   if (big & 0x80808080u) return 2;
   return (acc & 0x80808080u) ? 1 : 0;
 }
@@ -541,10 +545,9 @@ __global__ __launch_bounds__(kDecWaves * kWave) void k_cesu_decode(uint8_t* text
       // staged: every lane classifies its own row from LDS (aligned dwords),
       // so ASCII rows -- most tweets -- leave the wave's per-row walk entirely
       int my_cls = -1;
-      bool my_sp = true;   // rows walked from global memory: a candidate (checked exactly later)
       if (staged) {
         const bool in_win = (m >> lane) & 1u;
-        if (in_win) my_cls = lane_row_class(lbuf, int(s0 - a0), int(s1 - a0), my_sp);
+        if (in_win) my_cls = lane_row_class(lbuf, int(s0 - a0), int(s1 - a0));
         if (my_cls == 0) fl = uint8_t(fl & ~kRowCesu);
         m = __ballot(my_cls > 0);
       }
@@ -563,16 +566,17 @@ __global__ __launch_bounds__(kDecWaves * kWave) void k_cesu_decode(uint8_t* text
           const bool narB = two && __builtin_amdgcn_readlane(my_cls, lB) == 1;
           const int64_t d0A = tail + 2 * oA, d0B = tail + 2 * oB;
           int32_t kA = 0, kB = 0;
-          decode_rows2(lsrc, text, oA, eA, d0A, narA, kA, oB, eB, d0B, narB, kB);
+          bool spA = false, spB = false;
+          decode_rows2(lsrc, text, oA, eA, d0A, narA, kA, oB, eB, d0B, narB, kB, spA, spB);
           if (lane == lA) {
             s0 = d0A;
             s1 = d0A + (narA ? kA : 2 * kA);
-            fl = narA ? uint8_t(fl & ~kRowCesu) : uint8_t((fl & ~kRowCesu) | kRowWide | (my_sp ? kRowSpecial : 0));
+            fl = narA ? uint8_t(fl & ~kRowCesu) : uint8_t((fl & ~kRowCesu) | kRowWide | (spA ? kRowSpecial : 0));
           }
           if (two && lane == lB) {
             s0 = d0B;
             s1 = d0B + (narB ? kB : 2 * kB);
-            fl = narB ? uint8_t(fl & ~kRowCesu) : uint8_t((fl & ~kRowCesu) | kRowWide | (my_sp ? kRowSpecial : 0));
+            fl = narB ? uint8_t(fl & ~kRowCesu) : uint8_t((fl & ~kRowCesu) | kRowWide | (spB ? kRowSpecial : 0));
           }
           n_nar += (narA ? 1 : 0) + (narB ? 1 : 0);
         }
@@ -592,11 +596,12 @@ __global__ __launch_bounds__(kDecWaves * kWave) void k_cesu_decode(uint8_t* text
         // narrowing pass in k_row_normalize); others to UTF-16
         const bool nar = cls == 1;
         const int64_t d0 = tail + 2 * o;
-        const int64_t k = staged ? decode_row(lsrc, text, o, e, d0, nar) : decode_row(gsrc, text, o, e, d0, nar);
+        bool sp = false;
+        const int64_t k = staged ? decode_row(lsrc, text, o, e, d0, nar, sp) : decode_row(gsrc, text, o, e, d0, nar, sp);
         if (lane == l) {
           s0 = d0;
           s1 = d0 + (nar ? k : 2 * k);
-          fl = nar ? uint8_t(fl & ~kRowCesu) : uint8_t((fl & ~kRowCesu) | kRowWide | (my_sp ? kRowSpecial : 0));
+          fl = nar ? uint8_t(fl & ~kRowCesu) : uint8_t((fl & ~kRowCesu) | kRowWide | (sp ? kRowSpecial : 0));
         }
         n_nar += nar ? 1 : 0;
       }
