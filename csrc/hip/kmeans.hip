@@ -824,7 +824,7 @@ __global__ __launch_bounds__(kBlock) void k_km_assign_bf16x3(const float* X, con
 }
 
 // The same bf16x3 assignment with the centre fragments shared through LDS
-// (the default for 16 <= dp <= 128).  k_km_assign_bf16x3 has every wave
+// (TWTML_KM_ASSIGN=lds; the pipelined variant below is the default).  k_km_assign_bf16x3 has every wave
 // fetch every tile's fragments from L2 (8 KB per tile per wave at d = 64:
 // ~4 GB of L2 reads per 1M points x 1024 centres) and wait on them right
 // before its MFMAs -- 545 us at 1.8 waves/SIMD.  Here the
@@ -966,7 +966,8 @@ __global__ __launch_bounds__(kBlock) void k_km_assign_bf16x3_lds(const float* X,
 }
 
 // bf16x3 assignment with the epilogue software-pipelined behind the next
-// tile's MFMAs (TWTML_KM_ASSIGN=pipe; one 32-point block per wave).  In
+// tile's MFMAs (the default; TWTML_KM_ASSIGN=lds selects the kernel above;
+// one 32-point block per wave).  In
 // k_km_assign_bf16x3_lds a wave runs its 12 dependent MFMAs, then its 16
 // distance insertions, then the barrier: the matrix pipe idles during the
 // wave's VALU and the VALU during its MFMAs unless the SIMD's other waves
@@ -1249,16 +1250,20 @@ void launch_km_assign(const float* X, const float* f32, const double* f64, const
     done = true;                                                                                   \
     break;                                                                                         \
   }
-    // TWTML_KM_ASSIGN: lds (default: one 32-point block per wave, 4 waves per
-    // SIMD at d = 64), lds2 (two blocks per wave, 2 waves per SIMD), reg
-    // (per-wave L2 fragment loads, the round-2 kernel) -- for A/B runs.
-    // Measured at k = 1024, d = 64, 1M points: reg 572 us, lds2 538, lds 462.
+    // TWTML_KM_ASSIGN: pipe (default: the lds kernel with its epilogue
+    // software-pipelined behind the next tile's MFMAs), lds (one 32-point
+    // block per wave, 4 waves per SIMD at d = 64), lds2 (two blocks per wave,
+    // 2 waves per SIMD), reg (per-wave L2 fragment loads, the round-2 kernel)
+    // -- for A/B runs; all four are bitwise identical
+    // (tests/test_gpu_kmeans.py).  Measured at k = 1024, d = 64, 1M points:
+    // round 3 reg 572 us, lds2 538, lds 462; round 5 (overlapped with the
+    // next batch's decode, profiles/r5/kernels_kmeans_*.txt) lds 440, pipe 424.
     static const int variant = [] {
       const char* e = std::getenv("TWTML_KM_ASSIGN");
       if (e && std::strcmp(e, "reg") == 0) return 0;
       if (e && std::strcmp(e, "lds2") == 0) return 2;
-      if (e && std::strcmp(e, "pipe") == 0) return 3;
-      return 1;
+      if (e && std::strcmp(e, "lds") == 0) return 1;
+      return 3;
     }();
 #define KM_BF16P(DPV)                                                                              \
   case DPV: {                                                                                      \

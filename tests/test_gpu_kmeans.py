@@ -307,8 +307,8 @@ print("DIGEST", h.hexdigest())
 
 
 def test_kmeans_assign_variants_bitwise(hip_module, tmp_path):
-    """The bf16x3 assignment variants (``TWTML_KM_ASSIGN``: lds default, pipe
-    = epilogue software-pipelined behind the next tile's MFMAs, lds2, reg)
+    """The bf16x3 assignment variants (``TWTML_KM_ASSIGN``: pipe, the default
+    = epilogue software-pipelined behind the next tile's MFMAs; lds, lds2, reg)
     issue the same MFMAs in the same order, so labels, refine routing and
     the updated model are identical bit for bit (d = 16, 32, 64, 128)."""
     import os

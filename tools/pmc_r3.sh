@@ -3,7 +3,7 @@
 # sys/runtime trace); rounds 3-4.  Passes respect the per-block limits (SQ <= 8,
 # TCC <= 4, GRBM <= 2).  Output: gpurun_out/pmc_r3/<case>_p<k>/ + summary.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out/pmc_r3; export TMPDIR=/tmp
-LR_RE='k_sgd_iter_hyb|k_remap_hybrid|k_featurize|k_far_grad|k_sgd_update|k_sgd_reduce|k_cesu_decode|k_row_normalize|k_tier|k_prep_init|k_scan_excl|k_tile_sum|k_rows_scan'
+LR_RE='k_sgd_iter_hyb|k_remap_hybrid|k_featurize|k_far_grad|k_sgd_update|k_sgd_reduce|k_cesu_decode|k_row_normalize|k_tier|k_prep_init|k_scan_excl|k_tile_sum|k_rows_scan|k_batch_stats|k_batch_bounds|k_far_csc'
 KM_RE='k_km_'
 PASSES=("SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU"
         "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_INSTS_MFMA GRBM_GUI_ACTIVE GRBM_COUNT"
