@@ -392,7 +392,7 @@ void LREngine::free_prepared(PrepBuf& b) {
   void* bufs[] = {p.kept, p.nnz, p.sorted, p.blk, p.hist, p.clen8, p.cfast, p.clen8d, p.cnt, p.cslot,
                   p.hot_dense, p.clen8c, p.hot_slot, p.hot_of, p.slot_hist, p.code, p.cbase, p.idx, p.slot,
                   p.y, p.num, p.perm, p.rtext, p.scan_tmp, p.flags, p.uniq, p.slot_of, p.ublk, p.counters,
-                  p.fslot, p.fcount, p.fhist, p.fcur, p.fcsc_pos, p.fcsc_slot, p.newslot, p.slot_fid, p.tscan,
+                  p.fslot, p.fcount, p.fhist, p.fcur, p.fcsc, p.newslot, p.slot_fid, p.tscan,
                   p.tscan_blk, p.hist_near, p.tparam, b.n_global, b.ugather, b.bounds, b.packet, b.gathered};
   for (void* x : bufs) if (x) (void)hipFree(x);
   if (b.host_counters) (void)hipHostFree(b.host_counters);
@@ -433,8 +433,7 @@ void LREngine::ensure_tier(PrepBuf& b, int64_t n_unique, hipStream_t s) {
   if (!p.fslot) {
     const size_t E = size_t(p.cap_entries);
     p.fslot = dmalloc<uint32_t>(E);
-    p.fcsc_pos = dmalloc<uint32_t>(E);
-    p.fcsc_slot = dmalloc<uint32_t>(E);
+    p.fcsc = dmalloc<uint2>(E);
     p.fcount = dmalloc<int32_t>(size_t(p.cap_chunks) + 1);
     p.hist_near = dmalloc<uint32_t>(kMaxHybridSlots);
     p.tparam = dmalloc<int64_t>(4);
@@ -840,8 +839,7 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred, int64_t plot_points) {
   sgd_.far_off = pb.nl + sgd_.tail_len;
   if (tiered) {
     if (!sgd_.rbuf) sgd_.rbuf = dmalloc<float>(size_t(prep.cap_rows16));
-    sgd_.fcsc_pos = prep.fcsc_pos;
-    sgd_.fcsc_slot = prep.fcsc_slot;
+    sgd_.fcsc = prep.fcsc;
     sgd_.far_n = prep.tparam + 2;
   }
   if (!sgd_.pbuf) sgd_.pbuf = dmalloc<float>(size_t(prep.cap_rows16));

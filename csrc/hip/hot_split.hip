@@ -594,8 +594,7 @@ __global__ __launch_bounds__(256) void k_far_csc(DevPrepared p, int64_t c_lo, in
       const uint32_t e = fl[k];
       const uint32_t sl = e & kTagSlot;
       const uint64_t at = atomicAdd(reinterpret_cast<unsigned long long*>(&p.fcur[sl - near_end]), 1ull);
-      p.fcsc_pos[at] = uint32_t(c * kRowsPerChunk + (e >> 28));
-      p.fcsc_slot[at] = sl;
+      p.fcsc[at] = make_uint2(uint32_t(c * kRowsPerChunk + (e >> 28)), sl);
     }
   }
 }

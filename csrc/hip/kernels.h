@@ -163,8 +163,7 @@ struct DevPrepared {
   int32_t* fcount;          // [C] far entries per chunk
   uint64_t* fhist;          // [cap_tier + 1] entries per far slot, scanned in place into CSC offsets
   uint64_t* fcur;           // [cap_tier] CSC scatter cursors
-  uint32_t* fcsc_pos;       // [E] CSC: sorted position of the entry's row
-  uint32_t* fcsc_slot;      // [E] CSC: far slot of the entry
+  uint2* fcsc;              // [E] CSC: (sorted position of the entry's row, far slot) -- one 8-B scattered store
   int32_t* newslot;         // [cap_tier] compact index u -> slot
   int32_t* slot_fid;        // [cap_tier + 64] slot -> feature id
   int64_t* tscan;           // [cap_tier + 1] scan scratch
@@ -290,8 +289,7 @@ struct DevSgd {
   int64_t far_base;
   float* rbuf;          // [R16] residual per sorted position (tiered backward)
   const int32_t* slot_fid;   // slot -> feature id (tiered); null: uniq[slot - 4]
-  const uint32_t* fcsc_pos;
-  const uint32_t* fcsc_slot;
+  const uint2* fcsc;
   const int64_t* far_n;      // device: far entries (CSC length)
   int64_t F;
   int64_t ns;           // 4 + n_unique + pads (rounded)

@@ -1411,8 +1411,9 @@ __global__ __launch_bounds__(256) void k_far_grad(DevSgd d, SgdParams sp) {
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const int64_t e = e0 + u * kWave + lane;
-      sl[u] = e < n ? d.fcsc_slot[e] : 0xFFFFFFFFu;
-      ps[u] = e < n ? d.fcsc_pos[e] : 0u;
+      const uint2 v = e < n ? d.fcsc[e] : make_uint2(0u, 0xFFFFFFFFu);
+      ps[u] = v.x;
+      sl[u] = v.y;
     }
 #pragma unroll
     for (int u = 0; u < kU; ++u) rv[u] = e0 + u * kWave + lane < n ? d.rbuf[ps[u]] : 0.f;
