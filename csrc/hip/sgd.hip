@@ -1596,9 +1596,11 @@ __device__ __forceinline__ uint32_t abs_bits(uint32_t x) {
 // atomic per value per workgroup: a wave-level atomicMax from every wave
 // (12K same-address L2 atomics on a 1M-row batch) serialised this kernel at
 // 146 us for 24 MB of input.
-__global__ __launch_bounds__(kBlock) void k_batch_bounds(DevPrepared p, double* out) {
+constexpr int kBoundsThreads = 1024;   // 16 waves per workgroup, 256 workgroups: 4 waves per SIMD in flight
+
+__global__ __launch_bounds__(kBoundsThreads) void k_batch_bounds(DevPrepared p, double* out) {
   constexpr int kB = 2 + kNumNumeric;
-  __shared__ uint32_t red[kBlock / kWave][kB];
+  __shared__ uint32_t red[kBoundsThreads / kWave][kB];
   const int64_t n_kept = p.counters[0];
   const int64_t cap = p.cap_rows16;
   uint32_t b[kB] = {0, 0, 0, 0, 0, 0};
@@ -1606,7 +1608,7 @@ __global__ __launch_bounds__(kBlock) void k_batch_bounds(DevPrepared p, double* 
   const uint32_t* nb = reinterpret_cast<const uint32_t*>(p.num);
   // 4 rows per thread per step: six 16-B loads in flight (a row per step left
   // one wave per SIMD waiting on 6 dependent-latency loads: 64 us for 24 MB)
-  const int64_t gid = int64_t(blockIdx.x) * kBlock + threadIdx.x, gstride = int64_t(gridDim.x) * kBlock;
+  const int64_t gid = int64_t(blockIdx.x) * kBoundsThreads + threadIdx.x, gstride = int64_t(gridDim.x) * kBoundsThreads;
   const int64_t n4 = n_kept >> 2;
   for (int64_t i4 = gid; i4 < n4; i4 += gstride) {
     const int4 z = reinterpret_cast<const int4*>(p.nnz)[i4];
@@ -1637,7 +1639,7 @@ __global__ __launch_bounds__(kBlock) void k_batch_bounds(DevPrepared p, double* 
   if (threadIdx.x < kB) {
     const int k = threadIdx.x;
     uint32_t v = 0;
-    for (int j = 0; j < kBlock / kWave; ++j) v = max(v, red[j][k]);
+    for (int j = 0; j < kBoundsThreads / kWave; ++j) v = max(v, red[j][k]);
     const double dv = k == 0 ? double(v) : double(__builtin_bit_cast(float, v));
     if (dv > 0.0)
       atomicMax(reinterpret_cast<unsigned long long*>(&out[k]), __builtin_bit_cast(unsigned long long, dv));
@@ -1647,8 +1649,8 @@ __global__ __launch_bounds__(kBlock) void k_batch_bounds(DevPrepared p, double* 
 void launch_batch_bounds(const DevPrepared& p, double* out, hipStream_t s, bool zeroed) {
   // zeroed: k_prep_init cleared them earlier in this prep
   if (!zeroed) TWTML_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(double) * kBoundsLen, s));
-  const int grid = int(std::max<int64_t>(1, std::min<int64_t>((p.cap_rows + kBlock - 1) / kBlock, 256)));
-  hipLaunchKernelGGL(k_batch_bounds, dim3(grid), dim3(kBlock), 0, s, p, out);
+  const int grid = int(std::max<int64_t>(1, std::min<int64_t>((p.cap_rows + kBoundsThreads - 1) / kBoundsThreads, 256)));
+  hipLaunchKernelGGL(k_batch_bounds, dim3(grid), dim3(kBoundsThreads), 0, s, p, out);
 }
 
 // ---------------------------------------------------------------------------
