@@ -173,6 +173,10 @@ def test_torchrun_bench_gloo(hip_module, nproc):
     # one packed int64 buffer per GD iteration (near columns + tail + far
     # slots), averaged over the window's batches
     assert d["allreduce_bytes_per_iter"] > 8 * 64
+    # the DP cost model's check: all-reduce time per step ~ per-iteration time x all-reduces per step
+    assert d["comm_ms_per_step"] > 0
+    assert abs(d["comm_ms_per_step"] * 1e3 - d["grad_allreduce_us_per_iter"] * d["grad_allreduce_per_step"]) \
+        <= 0.5 * d["comm_ms_per_step"] * 1e3 + 1.0
     assert isinstance(d["rccl_version"], str) and d["rccl_version"]
     assert isinstance(d["comm_env"], dict) and d["comm_env"].get("HSA_ENABLE_IPC_MODE_LEGACY") == "0"
     print(f"dp{nproc}: {d['grad_allreduce_us_per_iter']} us / {d['allreduce_bytes_per_iter']} B per all-reduce")
