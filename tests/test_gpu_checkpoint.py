@@ -83,7 +83,7 @@ def _run(tmp_path, interval, pool, n_batches, F=100_000_000):
     return np.asarray(lat), w, ck, ckp
 
 
-def test_async_checkpoint_p99_wide_1e8(hip_module, tmp_path):
+def test_async_checkpoint_p99_wide_1e8(hip_module, tmp_path, timing_margin):
     from twitter_stream_ml_amd.checkpoint import load_linear_regression, load_progress
     from twitter_stream_ml_amd.sources.synthetic import SyntheticReplaySource
     rows, n = 500_000, 60
@@ -106,6 +106,7 @@ def test_async_checkpoint_p99_wide_1e8(hip_module, tmp_path):
             json.dump(res, fh)
     print(res)
     assert cp1.written >= 3, res
+    timing_margin("checkpoint-every-batch p99 (1.10 x no-checkpoint)", p99_1 * 1e3, 1.10 * p99_0 * 1e3)
     assert p99_1 <= 1.10 * p99_0, res
     # the final (synchronous) checkpoint is the trained model, bit for bit
     w_disk, _ = load_linear_regression(ck1)
