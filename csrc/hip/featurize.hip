@@ -485,7 +485,10 @@ __device__ __forceinline__ int lane_row_class(const uint8_t* lbuf, int lo, int l
 // LDS staging per wave: the 64 rows of a group are consecutive on the wire,
 // so their bytes are one range, loaded with 16-B loads (8 per lane in
 // flight) -- one memory round trip per group instead of several per row.
-constexpr int kDecStage = 12288;   // bytes per wave (groups beyond: global reads)
+// bytes per wave (groups beyond: two windows, or global reads): 6 KB leaves
+// room for 6 workgroups (24 waves) per CU; r5 same-box A/B, decode under
+// overlap 12 KB 466 us, 8 KB 436, 6 KB 414, 4 KB 455 (profiles/r5/ab_decode_stage.txt)
+constexpr int kDecStage = 6144;
 constexpr int kDecWaves = 4;
 
 __global__ __launch_bounds__(kDecWaves * kWave) void k_cesu_decode(uint8_t* text, const int64_t* offsets,

@@ -330,9 +330,15 @@ __global__ __launch_bounds__(kSplitWaves * kWave) void k_remap_hybrid(DevPrepare
         const int4* s4 = reinterpret_cast<const int4*>(src + int64_t(g) * kChunkStride);
         const int4 a = s4[0], b = s4[1];
         const int32_t v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        // the group's 8 codes first (their slot_of gathers in flight together:
+        // a far entry's list store may alias slot_of, which kept the compiler
+        // from hoisting the next entry's gather above it), then the counts
+        uint32_t cd[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) cd[e] = v[e] >= 0 ? id_code<TIERED>(lcode, p, v[e]) : 0u;
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          if (v[e] >= 0) count(id_code<TIERED>(lcode, p, v[e]));
+          if (v[e] >= 0) count(cd[e]);
       }
     }
     wave_lds_sync();

@@ -1,11 +1,11 @@
 #!/bin/bash
-# Kernel-trace stats of two builds (ab/A.so, ab/B.so) on one box:
+# Kernel-trace stats of builds (ab/A.so, ab/B.so, ...; AB_VARIANTS="A C" picks some) on one box:
 # tools/kprof_ab.sh <kernel regex> [bench args]
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 SO=twitter_stream_ml_amd/_twtml_hip.cpython-310-x86_64-linux-gnu.so
 re=$1; shift
 cp $SO ab/orig.so
-for v in A B; do
+for v in ${AB_VARIANTS:-A B}; do
   cp ab/$v.so $SO
   rm -rf gpurun_out/kpab_$v
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kpab_$v -o run -- \
