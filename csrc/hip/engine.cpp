@@ -296,10 +296,14 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
   // stream sync + hipFree (a device-wide wait) on the training thread in the
   // middle of the stream.  Larger active sets still grow on demand.
   ensure_compact((kNumNumeric + active_set_hint() + kPadSlots + 63) / 64 * 64);
-  TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_stat_), 16 * sizeof(int64_t), hipHostMallocDefault));
+  // the batch's results: written by k_batch_out into mapped host memory
+  TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_stat_), 16 * sizeof(int64_t),
+                                hipHostMallocMapped | hipHostMallocCoherent));
+  TWTML_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&host_stat_dev_), host_stat_, 0));
   TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_out_),
                                 (32 + size_t(std::max(1, cfg_.num_iterations))) * sizeof(double),
-                                hipHostMallocDefault));
+                                hipHostMallocMapped | hipHostMallocCoherent));
+  TWTML_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&host_out_dev_), host_out_, 0));
   // the plot sample: written by k_plot_sample straight into mapped host
   // memory (no copy engine: an 80 KB D2H on the compute stream was measured
   // waiting 25 ms behind other transfers once per process)
@@ -959,12 +963,7 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred, int64_t plot_points) {
     comm_->allreduce(sgd_.stat_i, size_t(kStatI), ncclInt64, ncclSum, s);
     comm_->allreduce(sgd_.stats, 6, ncclFloat64, ncclSum, s);
   }
-  TWTML_HIP_CHECK(hipMemcpyAsync(host_out_, sgd_.stats, 8 * sizeof(double), hipMemcpyDeviceToHost, s));
-  TWTML_HIP_CHECK(hipMemcpyAsync(host_stat_, sgd_.stat_i, size_t(kStatI) * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  TWTML_HIP_CHECK(hipMemcpyAsync(host_out_ + 8, sgd_.state, 8 * sizeof(double), hipMemcpyDeviceToHost, s));
-  TWTML_HIP_CHECK(hipMemcpyAsync(host_out_ + 16, sgd_.loss_hist,
-                                 sizeof(double) * size_t(cfg_.num_iterations + 1),
-                                 hipMemcpyDeviceToHost, s));
+  launch_batch_out(sgd_, host_out_dev_, host_stat_dev_, cfg_.num_iterations + 1, s);
   TWTML_HIP_CHECK(hipEventRecord(ev_[4], s));
   // the plot's (pred, real) pairs of this rank's kept rows: all of them, or
   // plot_points evenly spaced ones sampled on the device, written by the

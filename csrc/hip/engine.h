@@ -329,8 +329,10 @@ class LREngine {
   uint64_t* iter_tdbg_ = nullptr;
   uint8_t* lower_page_ = nullptr;
   uint16_t* lower_blocks_ = nullptr;
-  double* host_out_ = nullptr;        // pinned [16 + iters]
-  int64_t* host_stat_ = nullptr;      // pinned [16]: exact batch moments (stat_i)
+  double* host_out_ = nullptr;        // mapped pinned [16 + iters]: stats, state, loss history
+  int64_t* host_stat_ = nullptr;      // mapped pinned [16]: exact batch moments (stat_i)
+  double* host_out_dev_ = nullptr;    // device view of host_out_ (k_batch_out)
+  int64_t* host_stat_dev_ = nullptr;  // device view of host_stat_
   uint64_t* iter_kdbg_ = nullptr;     // TWTML_ITER_TIMING: per-workgroup GD kernel stamps
   float* plot_host_ = nullptr;        // mapped pinned [2 max_rows]: sampled (pred, real) pairs
   float* plot_dev_ = nullptr;         // ... its device address (k_plot_sample writes it)

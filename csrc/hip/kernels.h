@@ -325,6 +325,7 @@ constexpr int kStatI = 10;
 constexpr int kStatBlocks = 256;   // k_batch_stats grid: stat_part holds kStatBlocks x 16 words
 // After iteration 1: the batch moments from pbuf and the labels (exact
 // int64; DP: all-reduced as ncclInt64 after the GD loop).
+void launch_batch_out(const DevSgd& d, double* out, int64_t* stat, int n_loss, hipStream_t s);
 void launch_batch_stats(const DevSgd& d, const DevPrepared& p, hipStream_t s);
 
 // Partial-row stride for a compact space of ns slots (multiple of 64).

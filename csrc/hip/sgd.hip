@@ -1669,7 +1669,7 @@ void launch_batch_bounds(const DevPrepared& p, double* out, hipStream_t s, bool 
 //           hi/lo  [7,8] sum (y-p)^2 hi/lo  [9] spill rows
 //   stats (fp64, spill rows): [0] n [1] sum y [2] sum y^2 [3] sum p [4] sum p^2 [5] sum (y-p)^2
 // ---------------------------------------------------------------------------
-constexpr int kStatThreads = 256;
+constexpr int kStatThreads = 256;   // (1024 threads: 14 -> 25 us under prep overlap, waiting for 16 free wave slots per CU)
 
 __global__ __launch_bounds__(kStatThreads) void k_batch_stats(DevSgd d, const float* y, const int64_t* counters) {
   __shared__ int64_t wi[kStatThreads / kWave][kStatI];
@@ -1759,6 +1759,22 @@ __global__ __launch_bounds__(kStatBlocks) void k_batch_stats_fin(DevSgd d, int n
     for (int j = 0; j < kStatBlocks / kWave; ++j) t += __builtin_bit_cast(double, ws[j][k]);
     d.stats[k - kStatI] = t;
   }
+}
+
+// The batch's results for the host -- model statistics (fp64 spill sums and
+// the exact int64 moments), batch state, loss history -- written straight
+// into mapped host memory by one launch (four small D2H copies were four
+// blit kernels on the compute stream, ~14 us each under prep overlap).
+__global__ __launch_bounds__(256) void k_batch_out(DevSgd d, double* out, int64_t* stat, int n_loss) {
+  const int t = threadIdx.x;
+  if (t < 8) out[t] = d.stats[t];
+  else if (t < 16) out[t] = d.state[t - 8];
+  else if (t < 16 + kStatI) stat[t - 16] = d.stat_i[t - 16];
+  for (int i = t; i < n_loss; i += 256) out[16 + i] = d.loss_hist[i];
+}
+
+void launch_batch_out(const DevSgd& d, double* out, int64_t* stat, int n_loss, hipStream_t s) {
+  hipLaunchKernelGGL(k_batch_out, dim3(1), dim3(256), 0, s, d, out, stat, n_loss);
 }
 
 void launch_batch_stats(const DevSgd& d, const DevPrepared& p, hipStream_t s) {
