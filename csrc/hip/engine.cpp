@@ -363,7 +363,7 @@ void LREngine::alloc_prepared(PrepBuf& b) {
   p.num = dmalloc<float>(4 * size_t(R16));
   p.perm = dmalloc<int32_t>(size_t(R16));
   p.rtext = dmalloc<int64_t>(size_t(R16));
-  p.scan_tmp = dmalloc<int64_t>(size_t(C) / 8192 + 2);
+  p.scan_tmp = dmalloc<int64_t>(size_t(C) / 2048 + 2);   // multi-block scan tiles of 2048
   // active-feature flags: Java-hash bigrams are < 2^21 whatever F is
   const int64_t F = cfg_.num_text_features;
   int64_t fl = cfg_.hash_kind == 0 ? std::min<int64_t>(F, int64_t(1) << 21) : F;
@@ -454,7 +454,7 @@ void LREngine::ensure_tier(PrepBuf& b, int64_t n_unique, hipStream_t s) {
   p.newslot = dmalloc<int32_t>(size_t(cap));
   p.slot_fid = dmalloc<int32_t>(size_t(cap) + kNumNumeric + 2 * kPadSlots);
   p.tscan = dmalloc<int64_t>(size_t(cap) + 1 + 2048);   // + 4096 u32 count buckets
-  p.tscan_blk = dmalloc<int64_t>(size_t(cap) / 8192 + 4);
+  p.tscan_blk = dmalloc<int64_t>(size_t(cap) / 2048 + 4);   // multi-block scan tiles of 2048
   p.fhist = dmalloc<uint64_t>(size_t(cap) + 1);
   p.fcur = dmalloc<uint64_t>(size_t(cap) + 1);
   if (cap + kNumNumeric + 64 > b.slot_hist_cap) {

@@ -37,22 +37,29 @@ namespace twtml {
 // makes every load instruction touch 64 cache lines: 16 us per tile.)
 // ---------------------------------------------------------------------------
 constexpr int kScanPer = 8;
-constexpr int kScanTile = 1024 * kScanPer;
+constexpr int kScanTile = 1024 * kScanPer;   // single-block scans: 1024 threads
+// Multi-block scans run 256-thread blocks over 2048-element tiles: on the
+// prep stream every block waits for free wave slots on a CU the GD loop
+// shares, and a 1024-thread block needs 16 of them (k_tile_sum 33 us under
+// overlap for ~1 us of work, round 5).
+constexpr int kScanBT = 256;
+constexpr int kScanTileBig = kScanBT * kScanPer;
 
-// Sum of ts[0, b) over the 1024 threads of a block (every thread gets it).
+// Sum of ts[0, b) over the BT threads of a block (every thread gets it).
 // The multi-block scans take their tile's carry from the UNSCANNED tile sums
 // this way (a few hundred values at most) instead of a separate
 // single-block scan launch between the two passes: on the prep stream every
 // launch waits for a gap between the GD loop's kernels.
-__device__ __forceinline__ int64_t block_prefix_of_sums(const int64_t* ts, int64_t b, int64_t* wsum16) {
+template <int BT>
+__device__ __forceinline__ int64_t block_prefix_of_sums(const int64_t* ts, int64_t b, int64_t* wsum) {
   int64_t c = 0;
-  for (int64_t j = threadIdx.x; j < b; j += 1024) c += ts[j];
+  for (int64_t j = threadIdx.x; j < b; j += BT) c += ts[j];
   c = wave_sum(c);
-  if ((threadIdx.x & 63) == 0) wsum16[threadIdx.x >> 6] = c;
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
   __syncthreads();
   int64_t t = 0;
 #pragma unroll
-  for (int k = 0; k < 16; ++k) t += wsum16[k];
+  for (int k = 0; k < BT / 64; ++k) t += wsum[k];
   __syncthreads();
   return t;
 }
@@ -61,21 +68,24 @@ __device__ __forceinline__ int64_t block_prefix_of_sums(const int64_t* ts, int64
 // tile_sums[0, b) (0 without tile_sums); single block: span = n.  out2, if
 // given, receives the same values.  total: the grand total (written by the
 // last block).
-__global__ __launch_bounds__(1024) void k_scan_excl(const int64_t* in, int64_t* out, int64_t n,
-                                                    int64_t* total, const int64_t* tile_sums = nullptr,
-                                                    int64_t span = 0, int64_t* out2 = nullptr) {
-  __shared__ int64_t tile_v[kScanTile + kScanTile / 32];   // +1 word per 32: fewer bank conflicts
-  __shared__ int64_t wsum[16];
+template <int BT>
+__global__ __launch_bounds__(BT) void k_scan_excl(const int64_t* in, int64_t* out, int64_t n,
+                                                  int64_t* total, const int64_t* tile_sums = nullptr,
+                                                  int64_t span = 0, int64_t* out2 = nullptr) {
+  constexpr int kTile = BT * kScanPer;
+  constexpr int kW = BT / 64;
+  __shared__ int64_t tile_v[kTile + kTile / 32];   // +1 word per 32: fewer bank conflicts
+  __shared__ int64_t wsum[kW];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   auto at = [](int i) { return i + (i >> 5); };
-  int64_t carry = tile_sums ? block_prefix_of_sums(tile_sums, blockIdx.x, wsum) : 0;
+  int64_t carry = tile_sums ? block_prefix_of_sums<BT>(tile_sums, blockIdx.x, wsum) : 0;
   const int64_t b0 = tile_sums ? int64_t(blockIdx.x) * span : 0;
   const int64_t b1 = tile_sums ? (b0 + span < n ? b0 + span : n) : n;
-  for (int64_t base = b0; base < b1; base += kScanTile) {
+  for (int64_t base = b0; base < b1; base += kTile) {
 #pragma unroll
     for (int k = 0; k < kScanPer; ++k) {
-      const int64_t i = base + k * 1024 + tid;
-      tile_v[at(k * 1024 + tid)] = i < b1 ? in[i] : 0;
+      const int64_t i = base + k * BT + tid;
+      tile_v[at(k * BT + tid)] = i < b1 ? in[i] : 0;
     }
     __syncthreads();
     int64_t v[kScanPer];
@@ -95,7 +105,7 @@ __global__ __launch_bounds__(1024) void k_scan_excl(const int64_t* in, int64_t* 
     __syncthreads();
     int64_t woff = 0, tot = 0;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
+    for (int k = 0; k < kW; ++k) {
       const int64_t ws = wsum[k];
       woff += k < w ? ws : 0;
       tot += ws;
@@ -109,9 +119,9 @@ __global__ __launch_bounds__(1024) void k_scan_excl(const int64_t* in, int64_t* 
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < kScanPer; ++k) {
-      const int64_t i = base + k * 1024 + tid;
+      const int64_t i = base + k * BT + tid;
       if (i < b1) {
-        const int64_t v = tile_v[at(k * 1024 + tid)];
+        const int64_t v = tile_v[at(k * BT + tid)];
         out[i] = v;
         if (out2) out2[i] = v;
       }
@@ -122,14 +132,15 @@ __global__ __launch_bounds__(1024) void k_scan_excl(const int64_t* in, int64_t* 
   if (tid == 0 && total && blockIdx.x == gridDim.x - 1) *total = carry;
 }
 
-// Tile sums for the multi-block scan: block b sums in[b * kScanTile, ...).
-__global__ __launch_bounds__(1024) void k_tile_sum(const int64_t* in, int64_t n, int64_t* tsum) {
-  __shared__ int64_t wsum[16];
+// Tile sums for the multi-block scan: block b sums in[b * tile, ...).
+template <int BT>
+__global__ __launch_bounds__(BT) void k_tile_sum(const int64_t* in, int64_t n, int64_t* tsum) {
+  __shared__ int64_t wsum[BT / 64];
   int64_t v = 0;
-  const int64_t b0 = int64_t(blockIdx.x) * kScanTile;
+  const int64_t b0 = int64_t(blockIdx.x) * (BT * kScanPer);
 #pragma unroll
   for (int k = 0; k < kScanPer; ++k) {
-    const int64_t i = b0 + k * 1024 + threadIdx.x;
+    const int64_t i = b0 + k * BT + threadIdx.x;
     v += i < n ? in[i] : 0;
   }
   v = wave_sum(v);
@@ -137,29 +148,29 @@ __global__ __launch_bounds__(1024) void k_tile_sum(const int64_t* in, int64_t n,
   __syncthreads();
   if (threadIdx.x == 0) {
     int64_t t = 0;
-    for (int k = 0; k < 16; ++k) t += wsum[k];
+    for (int k = 0; k < BT / 64; ++k) t += wsum[k];
     tsum[blockIdx.x] = t;
   }
 }
 
 static void scan_excl(const int64_t* in, int64_t* out, int64_t n, int64_t* total, hipStream_t s,
                       int64_t* out2 = nullptr) {
-  hipLaunchKernelGGL(k_scan_excl, dim3(1), dim3(1024), 0, s, in, out, n, total, nullptr, int64_t(0), out2);
+  hipLaunchKernelGGL(k_scan_excl<1024>, dim3(1), dim3(1024), 0, s, in, out, n, total, nullptr, int64_t(0), out2);
 }
 
 // Multi-block exclusive scan (in place safe): tile sums, then every tile
 // scanned from the sum of the tile sums before it -- two launches.
-// tsum: ceil(n / 8192) + 1.
+// tsum: ceil(n / kScanTileBig) + 1.
 static void scan_excl_big(const int64_t* in, int64_t* out, int64_t n, int64_t* total, int64_t* tsum,
                           hipStream_t s, int64_t* out2 = nullptr) {
   if (n <= kScanTile) {
     scan_excl(in, out, n, total, s, out2);
     return;
   }
-  const int tiles = int((n + kScanTile - 1) / kScanTile);
-  hipLaunchKernelGGL(k_tile_sum, dim3(tiles), dim3(1024), 0, s, in, n, tsum);
-  hipLaunchKernelGGL(k_scan_excl, dim3(tiles), dim3(1024), 0, s, in, out, n, total,
-                     static_cast<const int64_t*>(tsum), int64_t(kScanTile), out2);
+  const int tiles = int((n + kScanTileBig - 1) / kScanTileBig);
+  hipLaunchKernelGGL(k_tile_sum<kScanBT>, dim3(tiles), dim3(kScanBT), 0, s, in, n, tsum);
+  hipLaunchKernelGGL(k_scan_excl<kScanBT>, dim3(tiles), dim3(kScanBT), 0, s, in, out, n, total,
+                     static_cast<const int64_t*>(tsum), int64_t(kScanTileBig), out2);
 }
 
 void launch_scan_excl(const int64_t* in, int64_t* out, int64_t n, int64_t* total, int64_t* tsum, hipStream_t s,
@@ -238,7 +249,7 @@ __global__ __launch_bounds__(1024) void k_rows_scan(const uint16_t* rp, int64_t 
   int64_t s = 0;
 #pragma unroll
   for (int k = 0; k < 8; ++k) s += w[k] & ((1u << kRowLenBits) - 1u);
-  const int64_t carry = block_prefix_of_sums(tsum, blockIdx.x, wsum);
+  const int64_t carry = block_prefix_of_sums<1024>(tsum, blockIdx.x, wsum);
   int64_t o = carry + block_excl_scan_1024(s, wsum, &total);
   if (threadIdx.x == 0 && blockIdx.x == gridDim.x - 1) offsets[n] = carry + total;   // total bytes
 #pragma unroll

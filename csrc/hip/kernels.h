@@ -131,7 +131,7 @@ struct DevPrepared {
   float* num;               // [4][R16] numeric features (SoA by sorted position)
   int32_t* perm;            // [R16] kept index at sorted position p, -1 if none
   int64_t* rtext;           // [R16] fast chunks: text byte offset * 512 + length of the row at p
-  int64_t* scan_tmp;        // [C/8192+2] tile sums of the multi-block chunk-base scan
+  int64_t* scan_tmp;        // [C/2048+2] tile sums of the multi-block chunk-base scan
   // active set
   uint8_t* flags;           // [Fh]
   int32_t* uniq;            // [Fh]  sorted touched feature ids
@@ -167,7 +167,7 @@ struct DevPrepared {
   int32_t* newslot;         // [cap_tier] compact index u -> slot
   int32_t* slot_fid;        // [cap_tier + 64] slot -> feature id
   int64_t* tscan;           // [cap_tier + 1] scan scratch
-  int64_t* tscan_blk;       // [cap_tier / 8192 + 2]
+  int64_t* tscan_blk;       // [cap_tier / 2048 + 4]
   uint32_t* hist_near;      // [kMaxHybridSlots] sampled counts of the near slots (new numbering)
   int64_t* tparam;          // [4] near threshold T, ties to take, far entries, -
   int64_t cap_tier;
@@ -224,7 +224,7 @@ constexpr int kMaxHybridSlots = 16384;
 void launch_remap_hybrid(const DevPrepared& p, int64_t entries, int64_t ns, int64_t pad_base, int num_cu,
                          const DevRawBatch& b, const FeaturizeParams& fp, bool from_text, hipStream_t s);
 
-// Exclusive int64 scan (in place safe); tsum: ceil(n / 8192) + 2 scratch.
+// Exclusive int64 scan (in place safe); tsum: ceil(n / 2048) + 2 scratch.
 void launch_scan_excl(const int64_t* in, int64_t* out, int64_t n, int64_t* total, int64_t* tsum, hipStream_t s,
                       int64_t* out2 = nullptr);
 
