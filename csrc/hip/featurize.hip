@@ -900,15 +900,21 @@ __device__ __forceinline__ void row_scalars(const DevRawBatch& b, const DevPrepa
 // distinct ids, almost every lookup hits.
 constexpr int kFlagCache = 4096;
 
+// k_featurize (wide rows, murmur3 over F > 2^24): the cache takes the LDS
+// of the id bitmap (ids < 2^16 are 0.07 % of a uniform hash over 1e8), so
+// the workgroups stay at three per CU
+constexpr int kFlagCacheWide = 2048;
+
 __device__ __forceinline__ void flag_id(uint32_t* fbits, const DevPrepared& p, int64_t idx,
-                                        int64_t lds_lim, uint32_t* fcache = nullptr) {
+                                        int64_t lds_lim, uint32_t* fcache = nullptr,
+                                        uint32_t cmask = kFlagCache - 1) {
   if (idx < lds_lim) {
     // hot ids are flagged early: a (broadcast) read skips the atomic
     const uint32_t bit = 1u << (idx & 31);
     if (!(fbits[idx >> 5] & bit)) atomicOr(&fbits[idx >> 5], bit);
   } else if (idx < p.flag_len) {
     if (fcache) {
-      uint32_t& e = fcache[uint32_t(idx) & (kFlagCache - 1)];
+      uint32_t& e = fcache[uint32_t(idx) & cmask];
       if (e != uint32_t(idx)) {
         p.flags[idx] = 1;
         e = uint32_t(idx);   // racing lanes may both store: harmless
@@ -937,14 +943,20 @@ __device__ __forceinline__ void flush_flag_bits(const uint32_t* fbits, const Dev
 // output stores, which serialised the old per-entry loop).  The 4 lanes of a
 // row then take entries j = t, t+4, ... from LDS and write 8 entries per
 // lane with two 16-byte stores.  Rows too long to stage read global memory.
+template <bool CACHE>
 __global__ __launch_bounds__(kBlock) void k_featurize(DevRawBatch b, DevPrepared p, FeaturizeParams fp,
                                                       const uint8_t* lpage, const uint16_t* lblocks,
                                                       int64_t cmax) {
-  __shared__ uint32_t fbits[kFlagWords];
+  __shared__ uint32_t fbits[CACHE ? 1 : kFlagWords];
+  __shared__ uint32_t fcache_s[CACHE ? kFlagCacheWide : 1];
+  uint32_t* fcache = CACHE ? fcache_s : nullptr;
+  if (CACHE)
+    for (int i = threadIdx.x; i < kFlagCacheWide; i += kBlock) fcache_s[i] = 0xFFFFFFFFu;
+  else
+    for (int i = threadIdx.x; i < kFlagWords; i += kBlock) fbits[i] = 0u;
   __shared__ uint32_t stage[kFeatWaves][kRowsPerChunk * kStageStride];
   __shared__ __attribute__((aligned(16))) uint8_t lpage_s[256];
   __shared__ __attribute__((aligned(16))) uint16_t lblk_s[kLowerLdsBlocks * 256];
-  for (int i = threadIdx.x; i < kFlagWords; i += kBlock) fbits[i] = 0u;
   stage_lower_tables(lpage_s, lblk_s, lpage, lblocks, threadIdx.x, kBlock);
   __syncthreads();
   const LowerLds lt{lpage_s, lblk_s, lblocks};
@@ -957,7 +969,7 @@ __global__ __launch_bounds__(kBlock) void k_featurize(DevRawBatch b, DevPrepared
   const int64_t F = fp.num_text_features;
   const bool f32 = F <= 0xffffffffLL;
   const FastMod32 fm(f32 ? uint32_t(F) : 1u);
-  const int64_t lds_lim = p.flag_len < kFlagLds ? p.flag_len : kFlagLds;
+  const int64_t lds_lim = CACHE ? 0 : (p.flag_len < kFlagLds ? p.flag_len : kFlagLds);
   const int64_t cap_groups = p.cap_entries / kChunkStride;
   const int64_t nch = (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;
   for (int64_t c = fp.c_lo + wave; c < nch && c < cmax && c < fp.c_hi; c += nwaves) {
@@ -1021,7 +1033,7 @@ __global__ __launch_bounds__(kBlock) void k_featurize(DevRawBatch b, DevPrepared
           }
           const int64_t idx = term_mod(h, F, fm, f32);
           v[k] = int32_t(idx);
-          flag_id(fbits, p, idx, lds_lim);
+          flag_id(fbits, p, idx, lds_lim, fcache, kFlagCacheWide - 1);
         }
       }
       int4* dst = reinterpret_cast<int4*>(out + (jj0 >> 3) * kChunkStride);
@@ -1031,8 +1043,10 @@ __global__ __launch_bounds__(kBlock) void k_featurize(DevRawBatch b, DevPrepared
     __builtin_amdgcn_wave_barrier();   // LDS reads of this chunk precede the next staging
     if (t == 0) row_scalars(b, p, fp, pos, valid, row, kidx);
   }
-  __syncthreads();
-  flush_flag_bits(fbits, p);
+  if (!CACHE) {
+    __syncthreads();
+    flush_flag_bits(fbits, p);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1132,7 +1146,16 @@ void launch_featurize(const DevRawBatch& b, const DevPrepared& p, const Featuriz
       hipLaunchKernelGGL(k_featurize_narrow<true>, dim3(grid), dim3(kBlock), 0, s, b, p, f, cmax);
     else
       hipLaunchKernelGGL(k_featurize_narrow<false>, dim3(grid), dim3(kBlock), 0, s, b, p, f, cmax);
-    hipLaunchKernelGGL(k_featurize, dim3(grid), dim3(kBlock), 0, s, b, p, f, lpage, lblocks, cmax);
+    // wide-row ids of murmur3 over F > 2^24 land in a flag array far beyond
+    // L2 / MALL: the LDS cache drops the repeats' byte stores
+    static const int wcache = [] {   // TWTML_FEAT_WCACHE=0/1 forces (A/B)
+      const char* e = std::getenv("TWTML_FEAT_WCACHE");
+      return e ? std::atoi(e) : -1;
+    }();
+    if (wcache == 1 || (wcache < 0 && f.hash_kind == 1 && p.flag_len > (int64_t(1) << 24)))
+      hipLaunchKernelGGL(k_featurize<true>, dim3(grid), dim3(kBlock), 0, s, b, p, f, lpage, lblocks, cmax);
+    else
+      hipLaunchKernelGGL(k_featurize<false>, dim3(grid), dim3(kBlock), 0, s, b, p, f, lpage, lblocks, cmax);
   }
 }
 
