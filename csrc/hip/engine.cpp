@@ -596,7 +596,11 @@ void LREngine::prepare_local(PrepBuf& pb, int slot, int64_t now_ms, hipStream_t 
   launch_chunk_layout(b, prep, s);
   // lazy ids: only the histogram's sample chunks keep their hashed ids; the
   // hybrid remap re-reads the (still resident) raw text for the rest
-  const bool lazy = cfg_.lazy_idx && cfg_.hybrid && !cfg_.dedup;
+  static const int lazy_env = [] {   // TWTML_LAZY_IDX=0/1 forces (A/B)
+    const char* e = std::getenv("TWTML_LAZY_IDX");
+    return e ? std::atoi(e) : -1;
+  }();
+  const bool lazy = (lazy_env >= 0 ? lazy_env != 0 : cfg_.lazy_idx != 0) && cfg_.hybrid && !cfg_.dedup;
   fp.idx_mode = lazy ? 1 : 0;
   launch_featurize(b, prep, fp, lower_page_, lower_blocks_, s);
   launch_batch_bounds(prep, pb.bounds, s, true);   // fixed-point scale bounds of this rank's rows
