@@ -24,7 +24,7 @@ one() {   # case regex args...
   done
   return 0
 }
-[ -z "$CASES" ] && CASES="lr_wide km"
-for c in $CASES; do case $c in lr_wide) one lr_wide "$LR_RE" --prepacked --profile wide --pool 3 --steps 2 --warmup 1 || exit 1;; lr_forced) one lr_forced "$LR_RE" --force-dp --prepacked --profile wide --pool 3 --steps 2 --warmup 1 || exit 1;; lr_bench) one lr_bench "$LR_RE" --prepacked --profile bench --pool 4 --steps 3 --warmup 1 || exit 1;; km) one km "$KM_RE" --model kmeans --prepacked --pool 4 --steps 3 --warmup 1 || exit 1;; esac; done
+[ -z "$CASES" ] && CASES="lr_wide km"   # also: lr_forced, lr_bench, lr_1e8 (config 5)
+for c in $CASES; do case $c in lr_wide) one lr_wide "$LR_RE" --prepacked --profile wide --pool 3 --steps 2 --warmup 1 || exit 1;; lr_forced) one lr_forced "$LR_RE" --force-dp --prepacked --profile wide --pool 3 --steps 2 --warmup 1 || exit 1;; lr_bench) one lr_bench "$LR_RE" --prepacked --profile bench --pool 4 --steps 3 --warmup 1 || exit 1;; km) one km "$KM_RE" --model kmeans --prepacked --pool 4 --steps 3 --warmup 1 || exit 1;; lr_1e8) one lr_1e8 "$LR_RE" --prepacked --profile wide --features 100000000 --hash murmur3 --pool 3 --steps 2 --warmup 1 || exit 1;; esac; done
 python tools/pmc_report.py gpurun_out/pmc_r3 > gpurun_out/pmc_r3/summary.md
 head -60 gpurun_out/pmc_r3/summary.md
