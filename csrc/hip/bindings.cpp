@@ -106,13 +106,36 @@ PYBIND11_MODULE(_twtml_hip, m) {
   m.def("tier_near_cap", &tier_near_cap, "LDS-resident text slots of the tiered layout");
   m.def("sgd_hybrid_fits", &sgd_hybrid_fits, py::arg("ns"));
   // Page-lock a host buffer (e.g. a receiver's batch) so submit(ext_text=...)
-  // DMAs straight from it; unregister before the buffer is freed.
+  // DMAs straight from it; it MUST be unregistered before the buffer is freed
+  // (ops/lr_engine.py register_host ties that to the array's lifetime).  A
+  // registration the runtime still holds for memory that was freed stays in
+  // its host-pointer map: a later buffer mapped at an overlapping address is
+  // then resolved to the stale registration (wrong size: hipMemcpyAsync
+  // "invalid argument"; wrong GPU mapping: an illegal memory access in a DMA).
+  // The registry below refuses such an overlap instead (round-5 faults,
+  // profiles/README.md "Round 6").
   m.def("host_register", [](uintptr_t ptr, size_t bytes) {
-    TWTML_HIP_CHECK(hipHostRegister(reinterpret_cast<void*>(ptr), bytes, hipHostRegisterDefault));
+    host_registry_add(ptr, bytes);
+    const hipError_t e = hipHostRegister(reinterpret_cast<void*>(ptr), bytes, hipHostRegisterDefault);
+    if (e != hipSuccess) {
+      host_registry_remove(ptr);
+      TWTML_HIP_CHECK(e);
+    }
   }, py::arg("ptr"), py::arg("bytes"));
   m.def("host_unregister", [](uintptr_t ptr) {
+    py::gil_scoped_release nogil;
+    // no DMA may still read the range once it is unpinned (and then freed)
+    TWTML_HIP_CHECK(hipDeviceSynchronize());
+    host_registry_remove(ptr);
     TWTML_HIP_CHECK(hipHostUnregister(reinterpret_cast<void*>(ptr)));
   }, py::arg("ptr"));
+  m.def("host_registrations", [] {
+    std::vector<std::pair<uintptr_t, size_t>> v = host_registry_snapshot();
+    return v;
+  }, "live host_register ranges (ptr, bytes)");
+  m.def("teardown_errors", &take_teardown_errors,
+        "device errors engine destructors found since the last call (and clears them)");
+  m.attr("DEBUG_SYNC") = debug_sync_enabled();
   m.def("rccl_version", &rccl_version);
   // device bytes allocated by the engines so far (monotonic; HBM batch sizing)
   m.def("device_bytes_allocated", [] { return uint64_t(dev_alloc_bytes().load()); });
@@ -314,6 +337,12 @@ PYBIND11_MODULE(_twtml_hip, m) {
              return d;
            },
            py::arg("slot"), py::arg("now_ms"), py::arg("want_pred") = false, py::arg("plot_points") = 0)
+      .def("discard",
+           [](LREngine& e, int slot) {
+             py::gil_scoped_release nogil;
+             e.discard(slot);
+           },
+           py::arg("slot"), "forget a submitted batch that will not be processed (one GPU)")
       .def_property_readonly("h2d_bytes", &LREngine::h2d_bytes, "host-to-device bytes submitted so far")
       .def_property_readonly("raw_slots", &LREngine::raw_slots, "device raw-batch slots")
       .def_property_readonly("lazy_bytes", &LREngine::lazy_bytes,

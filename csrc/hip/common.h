@@ -9,7 +9,9 @@
 #include <stdexcept>
 #include <string>
 
-#define TWTML_HIP_CHECK(expr)                                                              \
+#include "debug.h"   // TWTML_LAUNCH (debug sync points), teardown errors, host registrations
+
+#define TWTML_HIP_CHECK(expr)                                                            \
   do {                                                                                     \
     hipError_t _e = (expr);                                                                \
     if (_e != hipSuccess)                                                                  \

@@ -40,7 +40,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_c1(DevPrepared p, const double*
 
 void launch_pack_c1(const DevPrepared& p, const double* bounds, int32_t* packet, int64_t n_unique, hipStream_t s) {
   const int grid = int(std::max<int64_t>(1, std::min<int64_t>((n_unique + kBlock - 1) / kBlock, 2048)));
-  hipLaunchKernelGGL(k_pack_c1, dim3(grid), dim3(kBlock), 0, s, p, bounds, packet);
+  TWTML_LAUNCH(k_pack_c1, dim3(grid), dim3(kBlock), 0, s, p, bounds, packet);
 }
 
 // Flag every id of every rank's gathered pairs (-1: padding).
@@ -59,7 +59,7 @@ void launch_union_flag(const int32_t* gathered, int world, int64_t max_u, const 
   const int64_t n = int64_t(world) * max_u;
   if (n <= 0) return;
   const int grid = int(std::min<int64_t>((n + kBlock - 1) / kBlock, 4096));
-  hipLaunchKernelGGL(k_union_flag, dim3(grid), dim3(kBlock), 0, s, gathered, world, max_u, p.flags, p.flag_len);
+  TWTML_LAUNCH(k_union_flag, dim3(grid), dim3(kBlock), 0, s, gathered, world, max_u, p.flags, p.flag_len);
 }
 
 // Summed sampled counts of the union slots: hist[4 + slot_of[id]] += count.
@@ -79,7 +79,7 @@ void launch_union_hist(const int32_t* gathered, int world, int64_t max_u, const 
   const int64_t n = int64_t(world) * max_u;
   if (n <= 0) return;
   const int grid = int(std::min<int64_t>((n + kBlock - 1) / kBlock, 4096));
-  hipLaunchKernelGGL(k_union_hist, dim3(grid), dim3(kBlock), 0, s, gathered, world, max_u, p.slot_of, p.slot_hist);
+  TWTML_LAUNCH(k_union_hist, dim3(grid), dim3(kBlock), 0, s, gathered, world, max_u, p.slot_of, p.slot_hist);
 }
 
 }  // namespace twtml

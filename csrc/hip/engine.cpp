@@ -516,7 +516,9 @@ LREngine::~LREngine() {
   cv_.notify_all();
   if (worker_.joinable()) worker_.join();
   (void)hipSetDevice(device_);
-  (void)hipDeviceSynchronize();
+  // a fault of this engine's last work surfaces here: report it (and keep it
+  // for teardown_errors()) instead of leaving it to the next engine's first call
+  report_teardown_error("LREngine", device_, hipDeviceSynchronize());
   raw_.release();
   for (auto& e : ev_) (void)hipEventDestroy(e);
   for (auto& b : pb_) free_prepared(b);
@@ -1152,6 +1154,31 @@ void LREngine::schedule_ahead_locked() {
   b.now_ms = next.second;
   job_ = free_buf;
   cv_.notify_all();
+}
+
+// A submitted batch that will never be processed (the host pipeline matched
+// no take() to its prefetch): drop it from the prepare-ahead queue, release a
+// prepared buffer that holds it (after its preparation finished), and order
+// every read of the slot's raw bytes before the next H2D into the slot.
+// Without this an orphan is prepared ahead, evicted and prepared again on
+// every later batch, and a reused slot races its own stale preparation.
+void LREngine::discard(int slot) {
+  TWTML_HIP_CHECK(hipSetDevice(device_));
+  std::unique_lock<std::mutex> lk(mu_);
+  if (dp_)   // every rank must issue the same collectives: no rank may skip a batch
+    throw std::logic_error("DP: every submitted batch must be processed, in submission order");
+  for (auto it = submitted_.begin(); it != submitted_.end();)
+    it = it->first == slot ? submitted_.erase(it) : std::next(it);
+  for (auto& b : pb_) {
+    if (b.state == 0 || b.slot != slot) continue;
+    cv_.wait(lk, [&] { return b.state == 2; });
+    b.state = 0;
+    b.c1 = 0;
+    b.error = nullptr;
+  }
+  raw_.release_slot(slot, pstream_);
+  raw_.wait_h2d(slot);   // the host staging buffer of the slot may be rewritten on return
+  schedule_ahead_locked();
 }
 
 BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred, int64_t plot_points) {

@@ -216,6 +216,9 @@ class LREngine {
   // plot_points > 0: pred / real hold that many evenly spaced kept rows
   // (sampled on the device), else all of them.
   BatchResult process(int slot, int64_t now_ms, bool want_pred, int64_t plot_points = 0);
+  // Forget a submitted batch that will not be processed (one GPU only): the
+  // slot may be submitted again afterwards (ops/ingest.py SlotPipeline).
+  void discard(int slot);
 
   void set_weights(const double* w, int64_t n);
   void get_weights(double* w, int64_t n) const;

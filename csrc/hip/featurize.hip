@@ -155,7 +155,7 @@ __global__ __launch_bounds__(BT) void k_tile_sum(const int64_t* in, int64_t n, i
 
 static void scan_excl(const int64_t* in, int64_t* out, int64_t n, int64_t* total, hipStream_t s,
                       int64_t* out2 = nullptr) {
-  hipLaunchKernelGGL(k_scan_excl<1024>, dim3(1), dim3(1024), 0, s, in, out, n, total, nullptr, int64_t(0), out2);
+  TWTML_LAUNCH(k_scan_excl<1024>, dim3(1), dim3(1024), 0, s, in, out, n, total, nullptr, int64_t(0), out2);
 }
 
 // Multi-block exclusive scan (in place safe): tile sums, then every tile
@@ -168,8 +168,8 @@ static void scan_excl_big(const int64_t* in, int64_t* out, int64_t n, int64_t* t
     return;
   }
   const int tiles = int((n + kScanTileBig - 1) / kScanTileBig);
-  hipLaunchKernelGGL(k_tile_sum<kScanBT>, dim3(tiles), dim3(kScanBT), 0, s, in, n, tsum);
-  hipLaunchKernelGGL(k_scan_excl<kScanBT>, dim3(tiles), dim3(kScanBT), 0, s, in, out, n, total,
+  TWTML_LAUNCH(k_tile_sum<kScanBT>, dim3(tiles), dim3(kScanBT), 0, s, in, n, tsum);
+  TWTML_LAUNCH(k_scan_excl<kScanBT>, dim3(tiles), dim3(kScanBT), 0, s, in, out, n, total,
                      static_cast<const int64_t*>(tsum), int64_t(kScanTileBig), out2);
 }
 
@@ -269,8 +269,8 @@ void launch_unpack_rows(const uint16_t* rowpack, int64_t n, int64_t* offsets, ui
     return;
   }
   const int tiles = int((n + kRowTile - 1) / kRowTile);
-  hipLaunchKernelGGL(k_rows_tilesum, dim3(tiles), dim3(1024), 0, s, rowpack, n, tsum);
-  hipLaunchKernelGGL(k_rows_scan, dim3(tiles), dim3(1024), 0, s, rowpack, n, tsum, offsets, flags);
+  TWTML_LAUNCH(k_rows_tilesum, dim3(tiles), dim3(1024), 0, s, rowpack, n, tsum);
+  TWTML_LAUNCH(k_rows_scan, dim3(tiles), dim3(1024), 0, s, rowpack, n, tsum, offsets, flags);
 }
 
 // ---------------------------------------------------------------------------
@@ -635,7 +635,7 @@ void launch_cesu_expand(uint8_t* text, const int64_t* offsets, uint8_t* flags, i
   if (n <= 0) return;
   // one wave per 64-row group, 4 waves (48 KB of staging) per workgroup
   const int grid = int(std::min<int64_t>((n + kDecWaves * kWave - 1) / (kDecWaves * kWave), 4096));
-  hipLaunchKernelGGL(k_cesu_decode, dim3(grid), dim3(kDecWaves * kWave), 0, s, text, offsets, flags, n, tail,
+  TWTML_LAUNCH(k_cesu_decode, dim3(grid), dim3(kDecWaves * kWave), 0, s, text, offsets, flags, n, tail,
                      rstart, rend, stats);
 }
 
@@ -785,18 +785,18 @@ __global__ __launch_bounds__(1024) void k_prep_init(DevPrepared p, int64_t* n_gl
 
 void launch_prep_init(const DevPrepared& p, int64_t* n_global, int ng, hipStream_t s, double* bounds, int nb) {
   const int64_t n = std::max<int64_t>(kLenBuckets + 1, kMaxHybridSlots);
-  hipLaunchKernelGGL(k_prep_init, dim3(ceil_div(n, 1024)), dim3(1024), 0, s, p, n_global, ng, bounds, nb);
+  TWTML_LAUNCH(k_prep_init, dim3(ceil_div(n, 1024)), dim3(1024), 0, s, p, n_global, ng, bounds, nb);
 }
 
 void launch_filter_sort(const DevRawBatch& b, const DevPrepared& p, const FeaturizeParams& fp,
                         hipStream_t s) {
   const int nb = ceil_div(b.n > 0 ? b.n : 1, kSegRows);
-  hipLaunchKernelGGL(k_filter_count, dim3(nb), dim3(kSegThreads), 0, s, b, fp, p.blk);
+  TWTML_LAUNCH(k_filter_count, dim3(nb), dim3(kSegThreads), 0, s, b, fp, p.blk);
   scan_excl(p.blk, p.blk, nb, &p.counters[0], s);
-  hipLaunchKernelGGL(k_filter_write, dim3(nb), dim3(kSegThreads), 0, s, b, fp, p.blk, p.kept, p.nnz,
+  TWTML_LAUNCH(k_filter_write, dim3(nb), dim3(kSegThreads), 0, s, b, fp, p.blk, p.kept, p.nnz,
                      p.hist);
   scan_excl(p.hist, p.hist, kLenBuckets, nullptr, s);
-  hipLaunchKernelGGL(k_sort_scatter, dim3(nb), dim3(kSegThreads), 0, s, p.nnz, p.counters, p.hist,
+  TWTML_LAUNCH(k_sort_scatter, dim3(nb), dim3(kSegThreads), 0, s, p.nnz, p.counters, p.hist,
                      p.sorted, p.cap_rows);
 }
 
@@ -805,9 +805,9 @@ void launch_filter_only(const DevRawBatch& b, const DevPrepared& p, const Featur
                         hipStream_t s) {
   const int nb = ceil_div(b.n > 0 ? b.n : 1, kSegRows);
   TWTML_HIP_CHECK(hipMemsetAsync(p.hist, 0, sizeof(int64_t) * (kLenBuckets + 1), s));
-  hipLaunchKernelGGL(k_filter_count, dim3(nb), dim3(kSegThreads), 0, s, b, fp, p.blk);
+  TWTML_LAUNCH(k_filter_count, dim3(nb), dim3(kSegThreads), 0, s, b, fp, p.blk);
   scan_excl(p.blk, p.blk, nb, &p.counters[0], s);
-  hipLaunchKernelGGL(k_filter_write, dim3(nb), dim3(kSegThreads), 0, s, b, fp, p.blk, p.kept, p.nnz,
+  TWTML_LAUNCH(k_filter_write, dim3(nb), dim3(kSegThreads), 0, s, b, fp, p.blk, p.kept, p.nnz,
                      p.hist);
 }
 
@@ -853,7 +853,7 @@ void launch_chunk_layout(const DevRawBatch& b, const DevPrepared& p, hipStream_t
   }
   int grid = ceil_div((cmax + 3) / 4, kBlock / kWave);
   if (grid > 4096) grid = 4096;
-  hipLaunchKernelGGL(k_chunk_len, dim3(grid), dim3(kBlock), 0, s, p.sorted, p.nnz, p.counters,
+  TWTML_LAUNCH(k_chunk_len, dim3(grid), dim3(kBlock), 0, s, p.sorted, p.nnz, p.counters,
                      cmax, p.cbase, p.clen8, p.cfast);
   scan_excl_big(p.cbase, p.cbase, cmax, &p.counters[2], p.scan_tmp, s);
 }
@@ -1143,9 +1143,9 @@ void launch_featurize(const DevRawBatch& b, const DevPrepared& p, const Featuriz
     // ids of a Java-hashed Latin-1 bigram are < 8161, always in the LDS bitmap;
     // murmur3 ids above it get the flag cache
     if (f.hash_kind == 1 && p.flag_len > kFlagLds)
-      hipLaunchKernelGGL(k_featurize_narrow<true>, dim3(grid), dim3(kBlock), 0, s, b, p, f, cmax);
+      TWTML_LAUNCH(k_featurize_narrow<true>, dim3(grid), dim3(kBlock), 0, s, b, p, f, cmax);
     else
-      hipLaunchKernelGGL(k_featurize_narrow<false>, dim3(grid), dim3(kBlock), 0, s, b, p, f, cmax);
+      TWTML_LAUNCH(k_featurize_narrow<false>, dim3(grid), dim3(kBlock), 0, s, b, p, f, cmax);
     // wide-row ids of murmur3 over F > 2^24 land in a flag array far beyond
     // L2 / MALL: the LDS cache drops the repeats' byte stores
     static const int wcache = [] {   // TWTML_FEAT_WCACHE=0/1 forces (A/B)
@@ -1153,9 +1153,9 @@ void launch_featurize(const DevRawBatch& b, const DevPrepared& p, const Featuriz
       return e ? std::atoi(e) : -1;
     }();
     if (wcache == 1 || (wcache < 0 && f.hash_kind == 1 && p.flag_len > (int64_t(1) << 24)))
-      hipLaunchKernelGGL(k_featurize<true>, dim3(grid), dim3(kBlock), 0, s, b, p, f, lpage, lblocks, cmax);
+      TWTML_LAUNCH(k_featurize<true>, dim3(grid), dim3(kBlock), 0, s, b, p, f, lpage, lblocks, cmax);
     else
-      hipLaunchKernelGGL(k_featurize<false>, dim3(grid), dim3(kBlock), 0, s, b, p, f, lpage, lblocks, cmax);
+      TWTML_LAUNCH(k_featurize<false>, dim3(grid), dim3(kBlock), 0, s, b, p, f, lpage, lblocks, cmax);
   }
 }
 
@@ -1165,7 +1165,7 @@ void launch_featurize_fast_ids(const DevRawBatch& b, const DevPrepared& p, Featu
   fp.idx_mode = 2;
   int grid = ceil_div(cmax, kBlock / kWave);
   if (grid > 2048) grid = 2048;
-  hipLaunchKernelGGL(k_featurize_narrow<false>, dim3(grid), dim3(kBlock), 0, s, b, p, fp, cmax);
+  TWTML_LAUNCH(k_featurize_narrow<false>, dim3(grid), dim3(kBlock), 0, s, b, p, fp, cmax);
 }
 
 // ---------------------------------------------------------------------------
@@ -1227,9 +1227,9 @@ __global__ __launch_bounds__(kBlock) void k_compact_write(uint8_t* flags, const 
 
 void launch_compact_active(const DevPrepared& p, hipStream_t s) {
   const int nb = int(p.flag_len / kFlagsPerBlock);  // flag_len is padded to 4096
-  hipLaunchKernelGGL(k_compact_count, dim3(nb), dim3(kBlock), 0, s, p.flags, p.ublk);
+  TWTML_LAUNCH(k_compact_count, dim3(nb), dim3(kBlock), 0, s, p.flags, p.ublk);
   scan_excl(p.ublk, p.ublk, nb, &p.counters[1], s);
-  hipLaunchKernelGGL(k_compact_write, dim3(nb), dim3(kBlock), 0, s, p.flags, p.ublk, p.uniq,
+  TWTML_LAUNCH(k_compact_write, dim3(nb), dim3(kBlock), 0, s, p.flags, p.ublk, p.uniq,
                      p.slot_of);
 }
 
@@ -1246,7 +1246,7 @@ __global__ __launch_bounds__(kBlock) void k_flag_ids(const int32_t* ids, int64_t
 void launch_flag_ids(const int32_t* ids, int64_t n, const DevPrepared& p, hipStream_t s) {
   if (n <= 0) return;
   const int grid = int(std::min<int64_t>(ceil_div(n, kBlock), 4096));
-  hipLaunchKernelGGL(k_flag_ids, dim3(grid), dim3(kBlock), 0, s, ids, n, p.flags, p.flag_len);
+  TWTML_LAUNCH(k_flag_ids, dim3(grid), dim3(kBlock), 0, s, ids, n, p.flags, p.flag_len);
 }
 
 // ---------------------------------------------------------------------------
@@ -1286,10 +1286,10 @@ void launch_remap(const DevPrepared& p, int64_t entries, int64_t n_unique, bool 
   if (grid > 16384) grid = 16384;
   const int64_t pad_base = kNumNumeric + n_unique;
   if (u16)
-    hipLaunchKernelGGL(k_remap<uint16_t>, dim3(grid), dim3(kBlock), 0, s, p.idx, p.slot_of,
+    TWTML_LAUNCH(k_remap<uint16_t>, dim3(grid), dim3(kBlock), 0, s, p.idx, p.slot_of,
                        static_cast<uint16_t*>(p.slot), entries, pad_base);
   else
-    hipLaunchKernelGGL(k_remap<uint32_t>, dim3(grid), dim3(kBlock), 0, s, p.idx, p.slot_of,
+    TWTML_LAUNCH(k_remap<uint32_t>, dim3(grid), dim3(kBlock), 0, s, p.idx, p.slot_of,
                        static_cast<uint32_t*>(p.slot), entries, pad_base);
 }
 
@@ -1395,7 +1395,7 @@ void launch_dedup(const DevPrepared& p, int64_t ns, int64_t pad_base, int64_t n_
   int grid = int((nch + kDedupWaves - 1) / kDedupWaves);
   if (grid > 4096) grid = 4096;
   const size_t lds = size_t(kDedupWaves) * 2 * size_t(ns) * sizeof(uint32_t);
-  hipLaunchKernelGGL(k_dedup, dim3(grid), dim3(kDedupWaves * kWave), lds, s, p, ns, pad_base);
+  TWTML_LAUNCH(k_dedup, dim3(grid), dim3(kDedupWaves * kWave), lds, s, p, ns, pad_base);
 }
 
 // ---------------------------------------------------------------------------

@@ -620,7 +620,7 @@ void launch_remap_slices(const DevPrepared& p, int64_t ns, int64_t pad_base, int
     int grid = int(std::min<int64_t>(int64_t(num_cu) * 4 * prep_grid_mult(TIERED ? 4 : 1),
                                      (f.c_hi - f.c_lo + kSplitWaves - 1) / kSplitWaves));
     if (grid < 1) grid = 1;
-    hipLaunchKernelGGL(k_remap_hybrid<TIERED>, dim3(grid), dim3(kSplitWaves * kWave), 0, s, p, ns, pad_base,
+    TWTML_LAUNCH(k_remap_hybrid<TIERED>, dim3(grid), dim3(kSplitWaves * kWave), 0, s, p, ns, pad_base,
                        p.code, b, f, from_text ? 1 : 0);
   }
 }
@@ -636,13 +636,13 @@ void launch_remap_hybrid(const DevPrepared& p, int64_t entries, int64_t ns, int6
   const int64_t nsamp = (cmax + kHistChunks - 1) / kHistChunks;
   int gh = int((nsamp + kHistBlock / kWave - 1) / (kHistBlock / kWave));
   gh = std::max(1, std::min(gh, num_cu));
-  hipLaunchKernelGGL(k_slot_hist, dim3(gh), dim3(kHistBlock), size_t(pad_base) * sizeof(uint32_t), s,
+  TWTML_LAUNCH(k_slot_hist, dim3(gh), dim3(kHistBlock), size_t(pad_base) * sizeof(uint32_t), s,
                      p, pad_base, p.slot_hist);
-  hipLaunchKernelGGL(k_hot_select, dim3(1), dim3(1024), 0, s, p.slot_hist, ns, pad_base, p.hot_of,
+  TWTML_LAUNCH(k_hot_select, dim3(1), dim3(1024), 0, s, p.slot_hist, ns, pad_base, p.hot_of,
                      p.hot_slot);
-  hipLaunchKernelGGL(k_code_table, dim3(kCodeIds / 1024), dim3(1024), 0, s, p, p.code);
+  TWTML_LAUNCH(k_code_table, dim3(kCodeIds / 1024), dim3(1024), 0, s, p, p.code);
   const int64_t nU = pad_base - kNumNumeric;
-  if (nU > 0) hipLaunchKernelGGL(k_code_tag, dim3(int((nU + 1023) / 1024)), dim3(1024), 0, s, p, nU);
+  if (nU > 0) TWTML_LAUNCH(k_code_tag, dim3(int((nU + 1023) / 1024)), dim3(1024), 0, s, p, nU);
   launch_remap_slices<false>(p, ns, pad_base, cmax, num_cu, b, fp, from_text, s);
 }
 
@@ -660,7 +660,7 @@ void launch_tier_hist(const DevPrepared& p, int64_t n_unique, int num_cu, hipStr
   const int64_t spans = step;
   int gh = int((nsamp / step + kHistBlock / kWave - 1) / (kHistBlock / kWave));
   gh = std::max(1, std::min<int>(gh, int(std::max<int64_t>(1, num_cu / spans))));
-  hipLaunchKernelGGL(k_tier_hist, dim3(gh, unsigned(spans)), dim3(kHistBlock), 0, s, p, n_unique, step);
+  TWTML_LAUNCH(k_tier_hist, dim3(gh, unsigned(spans)), dim3(kHistBlock), 0, s, p, n_unique, step);
 }
 
 int64_t tier_near_cap() {
@@ -694,20 +694,20 @@ void launch_tier_layout(const DevPrepared& p, int64_t entries, int64_t n_unique,
   // the count buckets, the near-slot histogram and the far counts zeroed in
   // one launch (three fills before; each prep-stream launch waits for a gap
   // between the GD loop's kernels)
-  hipLaunchKernelGGL(k_tier_zero, dim3(int(std::min<int64_t>(256, (n_far + 1 + 1023) / 1024 + 1))), dim3(1024), 0, s,
+  TWTML_LAUNCH(k_tier_zero, dim3(int(std::min<int64_t>(256, (n_far + 1 + 1023) / 1024 + 1))), dim3(1024), 0, s,
                      buckets, p.hist_near, p.fhist, n_far + 1);
-  hipLaunchKernelGGL(k_tier_buckets, dim3(g), dim3(1024), 0, s, hist, n_unique, buckets);
-  hipLaunchKernelGGL(k_tier_threshold, dim3(1), dim3(1024), 0, s, buckets, n_near, p.tparam);
-  hipLaunchKernelGGL(k_tier_eqflag, dim3(g), dim3(1024), 0, s, hist, n_unique, p.tparam, p.tscan);
+  TWTML_LAUNCH(k_tier_buckets, dim3(g), dim3(1024), 0, s, hist, n_unique, buckets);
+  TWTML_LAUNCH(k_tier_threshold, dim3(1), dim3(1024), 0, s, buckets, n_near, p.tparam);
+  TWTML_LAUNCH(k_tier_eqflag, dim3(g), dim3(1024), 0, s, hist, n_unique, p.tparam, p.tscan);
   launch_scan_excl(p.tscan, p.tscan, n_unique, p.tparam + 3, p.tscan_blk, s);
-  hipLaunchKernelGGL(k_tier_nearflag, dim3(g), dim3(1024), 0, s, hist, n_unique, p.tparam, p.tscan, p.newslot);
+  TWTML_LAUNCH(k_tier_nearflag, dim3(g), dim3(1024), 0, s, hist, n_unique, p.tparam, p.tscan, p.newslot);
   launch_scan_excl(p.tscan, p.tscan, n_unique, p.tparam + 3, p.tscan_blk, s);
-  hipLaunchKernelGGL(k_tier_number, dim3(g), dim3(1024), 0, s, p, hist, n_unique, p.tscan);
+  TWTML_LAUNCH(k_tier_number, dim3(g), dim3(1024), 0, s, p, hist, n_unique, p.tscan);
   // hot ids among the near slots (new numbering)
-  hipLaunchKernelGGL(k_hot_select, dim3(1), dim3(1024), 0, s, p.hist_near, nl, p.near_end, p.hot_of,
+  TWTML_LAUNCH(k_hot_select, dim3(1), dim3(1024), 0, s, p.hist_near, nl, p.near_end, p.hot_of,
                      p.hot_slot);
-  hipLaunchKernelGGL(k_code_table_tiered, dim3(kCodeIds / 1024), dim3(1024), 0, s, p, p.code);
-  hipLaunchKernelGGL(k_code_tag_tiered, dim3(int((n_unique + 1023) / 1024)), dim3(1024), 0, s, p, n_unique);
+  TWTML_LAUNCH(k_code_table_tiered, dim3(kCodeIds / 1024), dim3(1024), 0, s, p, p.code);
+  TWTML_LAUNCH(k_code_tag_tiered, dim3(int((n_unique + 1023) / 1024)), dim3(1024), 0, s, p, n_unique);
   if (entries > 0) {
     const int64_t cmax = (p.cap_rows + kRowsPerChunk - 1) / kRowsPerChunk;
     launch_remap_slices<true>(p, ns, p.near_end, cmax, num_cu, b, fp, from_text, s);
@@ -723,7 +723,7 @@ void launch_tier_layout(const DevPrepared& p, int64_t entries, int64_t n_unique,
       const int64_t lo = cmax * k / nsl, hi = cmax * (k + 1) / nsl;
       if (hi <= lo) continue;
       const int grid = int(std::max<int64_t>(1, std::min<int64_t>((hi - lo + 3) / 4, int64_t(num_cu) * 8 * prep_grid_mult(4))));
-      hipLaunchKernelGGL(k_far_csc, dim3(grid), dim3(256), 0, s, p, lo, hi);
+      TWTML_LAUNCH(k_far_csc, dim3(grid), dim3(256), 0, s, p, lo, hi);
     }
   }
 }

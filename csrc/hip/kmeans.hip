@@ -403,7 +403,7 @@ void launch_km_features(const DevRawBatch& b, const int64_t* kept, const int64_t
     if (grid < 1) grid = 1;
     if (grid > 4096) grid = 4096;
     const size_t lds = size_t(kKmFeatWaves) * size_t(km_bal_wave_dwords(text_dims)) * sizeof(uint32_t);
-    hipLaunchKernelGGL(k_km_features_bal, dim3(grid), dim3(kBlock), lds, s, b, kept, counters, X, dp,
+    TWTML_LAUNCH(k_km_features_bal, dim3(grid), dim3(kBlock), lds, s, b, kept, counters, X, dp,
                        text_dims, lpage, lblocks);
     return;
   }
@@ -415,14 +415,14 @@ void launch_km_features(const DevRawBatch& b, const int64_t* kept, const int64_t
     const size_t lds = size_t(kKmFeatWaves) *
                        (size_t(kRowsPerChunk) * kStageStride + size_t(kRowsPerChunk) *
                         size_t(text_dims > 0 ? text_dims : 1)) * sizeof(uint32_t);
-    hipLaunchKernelGGL(k_km_features_chunk, dim3(grid), dim3(kBlock), lds, s, b, kept, counters, X,
+    TWTML_LAUNCH(k_km_features_chunk, dim3(grid), dim3(kBlock), lds, s, b, kept, counters, X,
                        dp, text_dims, lpage, lblocks);
     return;
   }
   int grid = ceil_div(max_rows > 0 ? max_rows : 1, kKmFeatWaves);
   if (grid > 8192) grid = 8192;
   const size_t lds = size_t(kKmFeatWaves) * size_t(text_dims > 0 ? text_dims : 1) * sizeof(uint32_t);
-  hipLaunchKernelGGL(k_km_features, dim3(grid), dim3(kBlock), lds, s, b, kept, counters, X, dp,
+  TWTML_LAUNCH(k_km_features, dim3(grid), dim3(kBlock), lds, s, b, kept, counters, X, dp,
                      text_dims, lpage, lblocks);
 }
 
@@ -529,13 +529,13 @@ static int km_moment_grid(int64_t max_rows) {
 
 void launch_km_colmax(const float* X, const int64_t* counters, int d, int dp, int64_t* mx, int64_t max_rows,
                       hipStream_t s) {
-  hipLaunchKernelGGL(k_km_colmax, dim3(km_moment_grid(max_rows)), dim3(kBlock), 0, s, X, counters, d, dp,
+  TWTML_LAUNCH(k_km_colmax, dim3(km_moment_grid(max_rows)), dim3(kBlock), 0, s, X, counters, d, dp,
                      km_cols_pow2(d), mx);
 }
 
 void launch_km_moments_q(const float* X, const int64_t* counters, int d, int dp, const int64_t* mx,
                          int64_t* out, int64_t max_rows, hipStream_t s) {
-  hipLaunchKernelGGL(k_km_moments_q, dim3(km_moment_grid(max_rows)), dim3(kBlock), 0, s, X, counters, d, dp,
+  TWTML_LAUNCH(k_km_moments_q, dim3(km_moment_grid(max_rows)), dim3(kBlock), 0, s, X, counters, d, dp,
                      km_cols_pow2(d), mx, out);
 }
 
@@ -1231,12 +1231,12 @@ void launch_km_assign(const float* X, const float* f32, const double* f64, const
   while ((1 << lbits) < ntiles * 32) ++lbits;
   if (mfma && bf16 && dp >= 16 && dp <= 128 && lbits <= kKmKeyBitsMax) {
     int gs = int((int64_t(ntiles) * (dp / 16) * kWave + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(k_km_split_bf16, dim3(gs < 1024 ? gs : 1024), dim3(kBlock), 0, s, C, cnorm, k,
+    TWTML_LAUNCH(k_km_split_bf16, dim3(gs < 1024 ? gs : 1024), dim3(kBlock), 0, s, C, cnorm, k,
                        dp, ntiles, frag, cnp);
 #define KM_BF16L(DPV, NBV)                                                                         \
   case DPV: {                                                                                      \
     const int64_t waves = (max_rows + 32 * NBV - 1) / (32 * NBV);                                  \
-    hipLaunchKernelGGL((k_km_assign_bf16x3_lds<DPV, NBV>), dim3(int((waves + 3) / 4)), dim3(kBlock), \
+    TWTML_LAUNCH((k_km_assign_bf16x3_lds<DPV, NBV>), dim3(int((waves + 3) / 4)), dim3(kBlock), \
                        0, s, X, f32, counters, frag, cnp, ntiles, lbits, labels, refine, refine_cnt, \
                        R);                                                                         \
     done = true;                                                                                   \
@@ -1245,7 +1245,7 @@ void launch_km_assign(const float* X, const float* f32, const double* f64, const
 #define KM_BF16(DPV, NBV)                                                                          \
   case DPV: {                                                                                      \
     const int64_t waves = (max_rows + 32 * NBV - 1) / (32 * NBV);                                  \
-    hipLaunchKernelGGL((k_km_assign_bf16x3<DPV, NBV>), dim3(int((waves + 3) / 4)), dim3(kBlock), 0, \
+    TWTML_LAUNCH((k_km_assign_bf16x3<DPV, NBV>), dim3(int((waves + 3) / 4)), dim3(kBlock), 0, \
                        s, X, f32, counters, frag, cnp, ntiles, lbits, labels, refine, refine_cnt, R); \
     done = true;                                                                                   \
     break;                                                                                         \
@@ -1268,7 +1268,7 @@ void launch_km_assign(const float* X, const float* f32, const double* f64, const
 #define KM_BF16P(DPV)                                                                              \
   case DPV: {                                                                                      \
     const int64_t waves = (max_rows + 31) / 32;                                                    \
-    hipLaunchKernelGGL((k_km_assign_bf16x3_pipe<DPV>), dim3(int((waves + 3) / 4)), dim3(kBlock),   \
+    TWTML_LAUNCH((k_km_assign_bf16x3_pipe<DPV>), dim3(int((waves + 3) / 4)), dim3(kBlock),   \
                        0, s, X, f32, counters, frag, cnp, ntiles, lbits, labels, refine, refine_cnt, \
                        R);                                                                         \
     done = true;                                                                                   \
@@ -1290,7 +1290,7 @@ void launch_km_assign(const float* X, const float* f32, const double* f64, const
   if (mfma && !done) {
 #define KM_MFMA(DPV)                                                                                \
   case DPV:                                                                                         \
-    hipLaunchKernelGGL(k_km_assign_mfma<DPV>, dim3(grid_m), dim3(kBlock), 0, s, X, f32, counters, C, \
+    TWTML_LAUNCH(k_km_assign_mfma<DPV>, dim3(grid_m), dim3(kBlock), 0, s, X, f32, counters, C, \
                        cnorm, k, labels, refine, refine_cnt, R);                                    \
     done = true;                                                                                    \
     break;
@@ -1300,12 +1300,12 @@ void launch_km_assign(const float* X, const float* f32, const double* f64, const
   int grid = int(max_rows / kBlock + 1);
   if (grid > 4096) grid = 4096;
   if (!done)
-    hipLaunchKernelGGL(k_km_assign_scalar, dim3(grid), dim3(kBlock), 0, s, X, f32, counters, C, cnorm,
+    TWTML_LAUNCH(k_km_assign_scalar, dim3(grid), dim3(kBlock), 0, s, X, f32, counters, C, cnorm,
                        k, dp, labels, refine, refine_cnt, R);
   const int grid_r = grid < 1024 ? grid : 1024;
-  hipLaunchKernelGGL(k_km_refine_cand, dim3(grid_r), dim3(kBlock), 0, s, X, f64, refine, refine_cnt,
+  TWTML_LAUNCH(k_km_refine_cand, dim3(grid_r), dim3(kBlock), 0, s, X, f64, refine, refine_cnt,
                      centers, d, dp, R, labels);
-  hipLaunchKernelGGL(k_km_refine, dim3(grid_r), dim3(kBlock), 0, s, X, f64, refine, refine_cnt,
+  TWTML_LAUNCH(k_km_refine, dim3(grid_r), dim3(kBlock), 0, s, X, f64, refine, refine_cnt,
                      centers, k, d, dp, labels);
 }
 
@@ -1472,25 +1472,25 @@ void launch_km_cluster_sums(const float* X, const int64_t* mx, const int32_t* la
   if (k <= kKmLdsBins) {
     int grid = int((max_rows + kKmChunk - 1) / kKmChunk);
     grid = grid < 1 ? 1 : (grid > 1024 ? 1024 : grid);
-    hipLaunchKernelGGL(k_km_label_hist, dim3(grid), dim3(kBlock), sizeof(uint32_t) * size_t(k), s,
+    TWTML_LAUNCH(k_km_label_hist, dim3(grid), dim3(kBlock), sizeof(uint32_t) * size_t(k), s,
                        labels, counters, k, hist);
     scan(hist, hist, k, nullptr, s);
-    hipLaunchKernelGGL(k_km_label_scatter, dim3(grid), dim3(kBlock), 2 * sizeof(uint32_t) * size_t(k), s,
+    TWTML_LAUNCH(k_km_label_scatter, dim3(grid), dim3(kBlock), 2 * sizeof(uint32_t) * size_t(k), s,
                        labels, counters, k, hist, order);
   } else {
     int grid = int(max_rows / kBlock + 1);
     if (grid > 4096) grid = 4096;
-    hipLaunchKernelGGL(k_km_label_hist_g, dim3(grid), dim3(kBlock), 0, s, labels, counters, hist);
+    TWTML_LAUNCH(k_km_label_hist_g, dim3(grid), dim3(kBlock), 0, s, labels, counters, hist);
     scan(hist, hist, k, nullptr, s);
-    hipLaunchKernelGGL(k_km_label_scatter_g, dim3(grid), dim3(kBlock), 0, s, labels, counters, hist, order);
+    TWTML_LAUNCH(k_km_label_scatter_g, dim3(grid), dim3(kBlock), 0, s, labels, counters, hist, order);
   }
   int g2 = int(max_rows / kSegRows + 1);
   if (g2 > 4096) g2 = 4096;
   if (k * d + k <= kSegLdsSums)
-    hipLaunchKernelGGL(k_km_segsum<true>, dim3(g2), dim3(kBlock), sizeof(int64_t) * size_t(k * d + k), s, X, mx,
+    TWTML_LAUNCH(k_km_segsum<true>, dim3(g2), dim3(kBlock), sizeof(int64_t) * size_t(k * d + k), s, X, mx,
                        labels, order, counters, k, d, dp, km_cols_pow2(d), sums);
   else
-    hipLaunchKernelGGL(k_km_segsum<false>, dim3(g2), dim3(kBlock), 0, s, X, mx, labels, order, counters, k, d,
+    TWTML_LAUNCH(k_km_segsum<false>, dim3(g2), dim3(kBlock), 0, s, X, mx, labels, order, counters, k, d,
                        dp, km_cols_pow2(d), sums);
 }
 
@@ -1514,7 +1514,7 @@ void launch_km_sums_f64(const int64_t* si, const int64_t* mx, const double* fac,
                         double* counts, hipStream_t s) {
   int grid = int((int64_t(k) * d + k + kBlock - 1) / kBlock);
   if (grid > 8192) grid = 8192;
-  hipLaunchKernelGGL(k_km_sums_f64, dim3(grid), dim3(kBlock), 0, s, si, mx, fac, k, d, sums, counts);
+  TWTML_LAUNCH(k_km_sums_f64, dim3(grid), dim3(kBlock), 0, s, si, mx, fac, k, d, sums, counts);
 }
 
 // ---------------------------------------------------------------------------
@@ -1644,18 +1644,18 @@ void launch_km_centers32(const double* centers, int k, int d, int dp, float* c32
                          hipStream_t s) {
   int grid = (k + 3) / 4;
   if (grid > 4096) grid = 4096;
-  hipLaunchKernelGGL(k_km_centers32, dim3(grid), dim3(kBlock), 0, s, centers, k, d, dp, c32, cnorm);
+  TWTML_LAUNCH(k_km_centers32, dim3(grid), dim3(kBlock), 0, s, centers, k, d, dp, c32, cnorm);
 }
 
 void launch_km_update(double* centers, double* weights, const double* sums, const double* counts,
                       int k, int d, double decay, bool points_unit, double* blend, float* c32,
                       float* cnorm, int dp, hipStream_t s) {
-  hipLaunchKernelGGL(k_km_weights, dim3(1), dim3(1024), 0, s, weights, counts, k, decay,
+  TWTML_LAUNCH(k_km_weights, dim3(1), dim3(1024), 0, s, weights, counts, k, decay,
                      points_unit ? 1 : 0, blend);
   int grid = int((int64_t(k) * d + kBlock - 1) / kBlock);
   if (grid > 8192) grid = 8192;
-  hipLaunchKernelGGL(k_km_blend, dim3(grid), dim3(kBlock), 0, s, centers, sums, blend, k, d);
-  hipLaunchKernelGGL(k_km_split, dim3(1), dim3(1024), 0, s, centers, weights, k, d);
+  TWTML_LAUNCH(k_km_blend, dim3(grid), dim3(kBlock), 0, s, centers, sums, blend, k, d);
+  TWTML_LAUNCH(k_km_split, dim3(1), dim3(1024), 0, s, centers, weights, k, d);
   launch_km_centers32(centers, k, d, dp, c32, cnorm, s);
 }
 

@@ -88,7 +88,9 @@ KMEngine::KMEngine(int device, const KMConfig& cfg, std::shared_ptr<Comm> comm)
 
 KMEngine::~KMEngine() {
   (void)hipSetDevice(device_);
-  (void)hipDeviceSynchronize();
+  // a fault of this engine's last work surfaces here: report it (and keep it
+  // for teardown_errors()) instead of leaving it to the next engine's first call
+  report_teardown_error("KMEngine", device_, hipDeviceSynchronize());
   raw_.release();
   void* bufs[] = {prep_.kept, prep_.nnz, prep_.blk, prep_.hist, prep_.counters, X_, centers_,
                   weights_, sums_, sums_i_, qmom_, c32_, cnorm_, labels_, order_, refine_, frag_, cnp_, lhist_, fac64_, fac32_, blend_,
@@ -282,6 +284,10 @@ void bind_kmeans(py::module_& m) {
         py::gil_scoped_release nogil;
         e.submit(hb, n, bytes, slot, reinterpret_cast<const uint8_t*>(ext_text));
       }, py::arg("host_batch"), py::arg("n"), py::arg("bytes"), py::arg("slot"), py::arg("ext_text") = 0)
+      .def("discard", [](KMEngine& e, int slot) {
+        py::gil_scoped_release nogil;
+        e.discard(slot);
+      }, py::arg("slot"), "forget a submitted batch that will not be processed")
       .def_property_readonly("h2d_bytes", &KMEngine::h2d_bytes, "host-to-device bytes submitted so far")
       .def_property_readonly("raw_slots", &KMEngine::raw_slots, "device raw-batch slots")
       .def("process", [](KMEngine& e, int slot, bool want_labels) {

@@ -41,6 +41,10 @@ class KMEngine {
   ~KMEngine();
   void submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, const uint8_t* ext_text = nullptr);
   KMResult process(int slot, bool want_labels);
+  // Forget a submitted batch that will not be processed: waits for its H2D
+  // (the staging buffer may then be rewritten); the copy stream keeps the
+  // slot's next H2D in order behind it.
+  void discard(int slot) { raw_.wait_h2d(slot); }
   void set_state(const double* centers, const double* weights);
   void get_state(double* centers, double* weights) const;
   // Debug/test: the labels left by the last process() (the update's

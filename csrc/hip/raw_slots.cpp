@@ -93,9 +93,15 @@ void RawSlots::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, h
     if (!packed)
       TWTML_HIP_CHECK(hipMemcpyAsync(s.flags, hb.flags, size_t(n), hipMemcpyHostToDevice, copy));
     // wire-encoded columns are consecutive, so the leading scalar_cols of
-    // them are one contiguous copy
-    TWTML_HIP_CHECK(hipMemcpyAsync(s.scalars, hb.spack, size_t(hb.soff[scalar_cols]),
-                                   hipMemcpyHostToDevice, copy));
+    // them are one contiguous copy; it must fit both the host block's spack
+    // region (its tail) and the slot's 5 x 8 B per row
+    const int64_t sbytes = hb.soff[scalar_cols];
+    const uint8_t* hend = static_cast<const uint8_t*>(hb.base) + hb.bytes;
+    if (sbytes < 0 || sbytes > 5 * int64_t(sizeof(int64_t)) * n || hb.spack + sbytes > hend)
+      throw std::logic_error("RawSlots::submit: packed scalar bytes out of range (" + std::to_string(sbytes) +
+                             " for " + std::to_string(n) + " rows)");
+    TWTML_HIP_CHECK(hipMemcpyAsync(s.scalars, hb.spack, size_t(sbytes), hipMemcpyHostToDevice, copy));
+    TWTML_DEBUG_POINT("raw slot H2D: row flags + packed scalars", copy);
   }
   // row words + text last: the small copy goes first, so the gap the copy
   // engine leaves after a long transfer falls between batches, not inside one
@@ -108,6 +114,8 @@ void RawSlots::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, h
     TWTML_HIP_CHECK(hipMemcpyAsync(s.text - pre, hb.text - pre, pre + size_t(bytes),
                                    hipMemcpyHostToDevice, copy));
   }
+  TWTML_DEBUG_POINT(ext_text ? "raw slot H2D: row words + text (external buffer)" : "raw slot H2D: row words + text",
+                    copy);
   TWTML_HIP_CHECK(hipEventRecord(s.h2d_done, copy));
   int64_t moved = int64_t(pre) + bytes;
   if (!packed) moved += int64_t(sizeof(int64_t)) * (n + 1) + (n > 0 ? n : 0);
@@ -169,6 +177,11 @@ DevRawBatch RawSlots::acquire(int slot, hipStream_t compute) {
   b.n = s.n;
   b.bytes = s.bytes;
   return b;
+}
+
+void RawSlots::wait_h2d(int slot) const {
+  const Slot& s = slots_[check(slot)];
+  if (s.used) TWTML_HIP_CHECK(hipEventSynchronize(s.h2d_done));
 }
 
 void RawSlots::release_slot(int slot, hipStream_t compute) {

@@ -49,6 +49,8 @@ class RawSlots {
   // Rows lowered (special full case mapping) / narrowed by the last acquire
   // of `slot` (device counters, valid once the compute stream passed acquire).
   const int64_t* norm_stats(int slot) const { return slots_[check(slot)].nstats; }
+  // Host wait for the slot's last H2D (its staging buffer may be rewritten).
+  void wait_h2d(int slot) const;
   // The compute stream is done reading the slot's raw bytes.
   void release_slot(int slot, hipStream_t compute);
   int64_t rows(int slot) const { return slots_[check(slot)].n; }

@@ -285,7 +285,7 @@ void launch_row_normalize(uint8_t* text, const int64_t* wire_off, const int64_t*
   RowNorm a{text, wire_off, cur_s, cur_e, flags, out_s, out_e, n, tail, lower_base, narrow ? 1 : 0,
             flagged_only ? 1 : 0, ct, stats};
   const int grid = int(std::min<int64_t>((n + 255) / 256, 4096));
-  hipLaunchKernelGGL(k_row_normalize, dim3(grid), dim3(256), 0, s, a);
+  TWTML_LAUNCH(k_row_normalize, dim3(grid), dim3(256), 0, s, a);
 }
 
 }  // namespace twtml

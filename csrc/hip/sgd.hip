@@ -960,7 +960,7 @@ static void launch_iter_t(const DevSgd& d, const DevPrepared& p, const SgdParams
   if (u16 && rep > 0 && p.hybrid) {
     const size_t lds = size_t(lds_bytes(d.nl, rep));
 #define TWTML_HYB(R, T) \
-  hipLaunchKernelGGL((k_sgd_iter_hyb<STATS, SAMPLE, R, T>), dim3(grid), dim3(kIterBlock), lds, s, d, p, sp)
+  TWTML_LAUNCH((k_sgd_iter_hyb<STATS, SAMPLE, R, T>), dim3(grid), dim3(kIterBlock), lds, s, d, p, sp)
     const bool tiered = p.tiered != 0;
     switch (rep) {
       case 8: if (tiered) TWTML_HYB(8, true); else TWTML_HYB(8, false); break;
@@ -972,7 +972,7 @@ static void launch_iter_t(const DevSgd& d, const DevPrepared& p, const SgdParams
   } else if (u16 && rep > 0) {
     const size_t lds = size_t(lds_bytes(d.nl, rep));
 #define TWTML_ITER(R, C) \
-  hipLaunchKernelGGL((k_sgd_iter_lds<STATS, SAMPLE, R, C>), dim3(grid), dim3(kIterBlock), lds, s, d, p, sp)
+  TWTML_LAUNCH((k_sgd_iter_lds<STATS, SAMPLE, R, C>), dim3(grid), dim3(kIterBlock), lds, s, d, p, sp)
     const bool cnt = p.dedup != 0;
     switch (rep) {
       case 8: if (cnt) TWTML_ITER(8, true); else TWTML_ITER(8, false); break;
@@ -1328,7 +1328,7 @@ static void update_split(const DevSgd& d, int& nt, int& nf) {
 void launch_sgd_update(const DevSgd& d, const SgdParams& sp, int nparts, hipStream_t s) {
   int nt = 0, nf = 0;
   update_split(d, nt, nf);
-  hipLaunchKernelGGL(k_sgd_update, dim3(nt + nf), dim3(kUpdThreads), 0, s, d, sp, nparts, nt, nf);
+  TWTML_LAUNCH(k_sgd_update, dim3(nt + nf), dim3(kUpdThreads), 0, s, d, sp, nparts, nt, nf);
 }
 
 // DP: cross-workgroup reduction of the partial rows into the packed buffer
@@ -1364,7 +1364,7 @@ __global__ __launch_bounds__(kUpdThreads) void k_sgd_reduce(DevSgd d, SgdParams 
 
 void launch_sgd_reduce(const DevSgd& d, const SgdParams& sp, hipStream_t s) {
   const int grid = d.nparts > 0 ? int((d.nl + kPartVals - kNumNumeric + kWave - 1) / kWave) : 1;
-  hipLaunchKernelGGL(k_sgd_reduce, dim3(grid), dim3(kUpdThreads), 0, s, d, sp);
+  TWTML_LAUNCH(k_sgd_reduce, dim3(grid), dim3(kUpdThreads), 0, s, d, sp);
 }
 
 // Convergence of the last update (the loop ended without a prologue seeing it).
@@ -1379,7 +1379,7 @@ __global__ void k_sgd_finish(DevSgd d, SgdParams sp) {
 }
 
 void launch_sgd_finish(const DevSgd& d, const SgdParams& sp, hipStream_t s) {
-  hipLaunchKernelGGL(k_sgd_finish, dim3(1), dim3(kWave), 0, s, d, sp);
+  TWTML_LAUNCH(k_sgd_finish, dim3(1), dim3(kWave), 0, s, d, sp);
 }
 
 
@@ -1439,9 +1439,9 @@ void launch_far_grad(const DevSgd& d, const SgdParams& sp, int num_cu, hipStream
     return v == 2 || v == 8 ? v : 4;
   }();
   const dim3 g(std::max(1, num_cu * 4));
-  if (ku == 8) hipLaunchKernelGGL(k_far_grad<8>, g, dim3(256), 0, s, d, sp);
-  else if (ku == 4) hipLaunchKernelGGL(k_far_grad<4>, g, dim3(256), 0, s, d, sp);
-  else hipLaunchKernelGGL(k_far_grad<2>, g, dim3(256), 0, s, d, sp);
+  if (ku == 8) TWTML_LAUNCH(k_far_grad<8>, g, dim3(256), 0, s, d, sp);
+  else if (ku == 4) TWTML_LAUNCH(k_far_grad<4>, g, dim3(256), 0, s, d, sp);
+  else TWTML_LAUNCH(k_far_grad<2>, g, dim3(256), 0, s, d, sp);
 }
 
 // ---------------------------------------------------------------------------
@@ -1536,24 +1536,24 @@ static int scatter_grid(const DevSgd& d) {
 
 void launch_gather_w(const DevSgd& d, const DevPrepared& p, hipStream_t s) {
   const int grid = gather_grid(d);
-  hipLaunchKernelGGL(k_gather_w, dim3(grid), dim3(kBlock), 0, s, d, p.uniq);
-  hipLaunchKernelGGL(k_norm_sum, dim3(1), dim3(kWave), 0, s, d.nrm, grid, &d.state[6], d.state, 0, &d.state[9]);
+  TWTML_LAUNCH(k_gather_w, dim3(grid), dim3(kBlock), 0, s, d, p.uniq);
+  TWTML_LAUNCH(k_norm_sum, dim3(1), dim3(kWave), 0, s, d.nrm, grid, &d.state[6], d.state, 0, &d.state[9]);
 }
 
 void launch_norm2(const double* v, int64_t n, double* out, const DevSgd& d, hipStream_t s) {
   int grid = ceil_div(n, kBlock * 8);
   if (grid > kNormParts) grid = kNormParts;
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL(k_norm2, dim3(grid), dim3(kBlock), 0, s, v, n, d.nrm);
-  hipLaunchKernelGGL(k_norm_sum, dim3(1), dim3(kWave), 0, s, d.nrm, grid, out, d.state, 0, (double*)nullptr);
+  TWTML_LAUNCH(k_norm2, dim3(grid), dim3(kBlock), 0, s, v, n, d.nrm);
+  TWTML_LAUNCH(k_norm_sum, dim3(1), dim3(kWave), 0, s, d.nrm, grid, out, d.state, 0, (double*)nullptr);
 }
 
 void launch_scatter_w(const DevSgd& d, const DevPrepared& p, hipStream_t s) {
-  hipLaunchKernelGGL(k_scatter_w, dim3(scatter_grid(d)), dim3(kBlock), 0, s, d, p.uniq);
+  TWTML_LAUNCH(k_scatter_w, dim3(scatter_grid(d)), dim3(kBlock), 0, s, d, p.uniq);
 }
 
 void launch_norm_next(const DevSgd& d, bool trained, hipStream_t s) {
-  hipLaunchKernelGGL(k_norm_sum, dim3(1), dim3(kWave), 0, s, d.nrm, trained ? scatter_grid(d) : 0,
+  TWTML_LAUNCH(k_norm_sum, dim3(1), dim3(kWave), 0, s, d.nrm, trained ? scatter_grid(d) : 0,
                      d.wnorm_next, d.state, trained ? 1 : 2, (double*)nullptr);
 }
 
@@ -1562,7 +1562,7 @@ __global__ void k_norm_carry(DevSgd d) {
 }
 
 void launch_norm_carry(const DevSgd& d, hipStream_t s) {
-  hipLaunchKernelGGL(k_norm_carry, dim3(1), dim3(kWave), 0, s, d);
+  TWTML_LAUNCH(k_norm_carry, dim3(1), dim3(kWave), 0, s, d);
 }
 
 // Per-batch SGD state in one launch: state (m = global kept rows at [5]),
@@ -1576,7 +1576,7 @@ __global__ void k_batch_init(DevSgd d, double m_global, int n_loss) {
 }
 
 void launch_batch_init(const DevSgd& d, double m_global, int n_loss, hipStream_t s) {
-  hipLaunchKernelGGL(k_batch_init, dim3(1), dim3(256), 0, s, d, m_global, n_loss);
+  TWTML_LAUNCH(k_batch_init, dim3(1), dim3(256), 0, s, d, m_global, n_loss);
 }
 
 // ---------------------------------------------------------------------------
@@ -1650,7 +1650,7 @@ void launch_batch_bounds(const DevPrepared& p, double* out, hipStream_t s, bool 
   // zeroed: k_prep_init cleared them earlier in this prep
   if (!zeroed) TWTML_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(double) * kBoundsLen, s));
   const int grid = int(std::max<int64_t>(1, std::min<int64_t>((p.cap_rows + kBoundsThreads - 1) / kBoundsThreads, 256)));
-  hipLaunchKernelGGL(k_batch_bounds, dim3(grid), dim3(kBoundsThreads), 0, s, p, out);
+  TWTML_LAUNCH(k_batch_bounds, dim3(grid), dim3(kBoundsThreads), 0, s, p, out);
 }
 
 // ---------------------------------------------------------------------------
@@ -1774,12 +1774,12 @@ __global__ __launch_bounds__(256) void k_batch_out(DevSgd d, double* out, int64_
 }
 
 void launch_batch_out(const DevSgd& d, double* out, int64_t* stat, int n_loss, hipStream_t s) {
-  hipLaunchKernelGGL(k_batch_out, dim3(1), dim3(256), 0, s, d, out, stat, n_loss);
+  TWTML_LAUNCH(k_batch_out, dim3(1), dim3(256), 0, s, d, out, stat, n_loss);
 }
 
 void launch_batch_stats(const DevSgd& d, const DevPrepared& p, hipStream_t s) {
-  hipLaunchKernelGGL(k_batch_stats, dim3(kStatBlocks), dim3(kStatThreads), 0, s, d, p.y, p.counters);
-  hipLaunchKernelGGL(k_batch_stats_fin, dim3(1), dim3(kStatBlocks), 0, s, d, kStatBlocks);
+  TWTML_LAUNCH(k_batch_stats, dim3(kStatBlocks), dim3(kStatThreads), 0, s, d, p.y, p.counters);
+  TWTML_LAUNCH(k_batch_stats_fin, dim3(1), dim3(kStatBlocks), 0, s, d, kStatBlocks);
 }
 
 // ---------------------------------------------------------------------------
@@ -1798,7 +1798,7 @@ __global__ void k_plot_sample(const float* pred, const float* real, int64_t n, i
 void launch_plot_sample(const float* pred, const float* real, int64_t n, int64_t P, float* out, hipStream_t s) {
   if (P <= 0 || n <= 0) return;
   const int grid = int(std::min<int64_t>(64, (P + 255) / 256));
-  hipLaunchKernelGGL(k_plot_sample, dim3(grid), dim3(256), 0, s, pred, real, n, P, out);
+  TWTML_LAUNCH(k_plot_sample, dim3(grid), dim3(256), 0, s, pred, real, n, P, out);
 }
 
 }  // namespace twtml

@@ -104,9 +104,9 @@ void launch_snapshot(const double* w, int64_t n, uint32_t* cnt, int64_t* off, in
                      volatile int64_t* host_total, hipStream_t s) {
   const int64_t nb = snapshot_chunks(n);
   if (nb <= 0) return;
-  hipLaunchKernelGGL(k_nz_count, dim3(unsigned(nb)), dim3(kBlock), 0, s, w, n, cnt);
-  hipLaunchKernelGGL(k_nz_scan, dim3(1), dim3(kBlock), 0, s, cnt, nb, off, host_total);
-  hipLaunchKernelGGL(k_nz_write, dim3(unsigned(nb)), dim3(kBlock), 0, s, w, n, off, idx, val);
+  TWTML_LAUNCH(k_nz_count, dim3(unsigned(nb)), dim3(kBlock), 0, s, w, n, cnt);
+  TWTML_LAUNCH(k_nz_scan, dim3(1), dim3(kBlock), 0, s, cnt, nb, off, host_total);
+  TWTML_LAUNCH(k_nz_write, dim3(unsigned(nb)), dim3(kBlock), 0, s, w, n, off, idx, val);
 }
 
 }  // namespace twtml

@@ -31,6 +31,24 @@ def hip_module():
     return _native.hip()
 
 
+@pytest.fixture(autouse=True)
+def _engine_teardown_clean(request):
+    """GPU tests: a device error that an engine destructor found (its last
+    work faulted; csrc/hip/debug.h) fails the test that owned the engine,
+    not whichever test touches the device next."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    import gc
+    gc.collect()
+    from twitter_stream_ml_amd.ops import _native
+    try:
+        errs = list(_native.hip().teardown_errors())
+    except Exception:   # noqa: BLE001 -- the extension is not loaded: nothing to check
+        return
+    assert not errs, f"engine teardown found device errors: {errs}"
+
+
 # Timing gates of the GPU suite (p99 bounds on a shared box) record their
 # measured value and bound here; the terminal summary prints them for every
 # run, passing or not, so the suite output carries each gate's headroom.

@@ -6,6 +6,12 @@ apps/_common.py StreamCheckpointer).
   keeps the per-batch p99 latency within 10 % of a run without checkpoints
   (VERDICT r2 item 6), and the model on disk loads back bit-exactly.
 
+What the p99 gate covers is a *coalescing* asynchronous writer: one write in
+flight at most, a checkpoint that comes due during a write is skipped and the
+next due batch snapshots the newest model.  At F = 1e8 a write (~30 MB of
+non-zero pairs to parquet) spans several 5 ms batches, so only a fraction of
+the due checkpoints is written; the test prints and bounds that fraction.
+
 SURVEY §5 checkpoint row; the reference keeps no checkpoint at all.
 """
 import json
@@ -65,9 +71,10 @@ def _run(tmp_path, interval, pool, n_batches, F=100_000_000):
     job = LinearRegressionJob(conf, eng, None, 0, plot=False)
     lat = []
     from twitter_stream_ml_amd.utils.gil import streaming_latency
+    nxt = pool[0].with_time(NOW)
     with streaming_latency():   # as the driver streams (apps/linear_regression.py main)
         for t in range(n_batches):
-            raw = pool[t % len(pool)].with_time(NOW + t * 5000)
+            raw = nxt                               # the object that was prefetched (round-5 verdict)
             nxt = pool[(t + 1) % len(pool)].with_time(NOW + (t + 1) * 5000)
             t0 = time.perf_counter()
             job.on_batch(SimpleNamespace(raw=raw), raw.batch_time_ms)
@@ -75,6 +82,11 @@ def _run(tmp_path, interval, pool, n_batches, F=100_000_000):
             eng.prefetch(nxt)                       # the receiver's next batch, as the app's scheduler does
     job.final_checkpoint()
     ckp = job.checkpointer
+    pipe = eng._pipe
+    # every prefetch was trained from its slot; nothing orphaned or left in flight
+    assert (pipe.prefetched, pipe.hits, pipe.orphaned) == (n_batches, n_batches - 1, 0), \
+        (pipe.prefetched, pipe.hits, pipe.orphaned)
+    assert pipe.in_flight == 1   # the prefetch after the last batch
     w = eng.get_weights()
     job.close()
     del job, eng
@@ -111,8 +123,11 @@ def test_async_checkpoint_p99_wide_1e8(hip_module, tmp_path, timing_margin):
             os.makedirs(out, exist_ok=True)
             with open(os.path.join(out, "ckpt_p99.json"), "w") as fh:
                 json.dump(res, fh)
+        res["written_fraction"] = (cp1.written - 1) / n   # the final checkpoint is forced
         print(res)
-        assert cp1.written >= 3, res
+        # every due checkpoint is either written or coalesced into a later one
+        assert cp1.written + cp1.skipped == n + 1, res
+        assert res["written_fraction"] >= 0.05, res
         timing_margin(f"checkpoint-every-batch p99, attempt {attempt} (1.10 x no-checkpoint)", p99_1 * 1e3,
                       1.10 * p99_0 * 1e3)
         if p99_1 <= 1.10 * p99_0:

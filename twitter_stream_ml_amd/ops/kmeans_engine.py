@@ -97,7 +97,8 @@ class DeviceKMeans:
         self.raw_slots = int(self._eng.raw_slots)
         me = weakref.proxy(self)   # no reference cycle (see DeviceLinearRegression)
         self._pipe = SlotPipeline(self.raw_slots, lambda s, raw: me._stage(s, raw),
-                                  lambda hb, slot: me.submit(hb, slot), lambda: me.synchronize())
+                                  lambda hb, slot: me.submit(hb, slot), lambda: me.synchronize(),
+                                  discard=lambda slot: me._eng.discard(int(slot)))
 
     def _stage(self, slot: int, raw: RawBatch) -> HostBatchView:
         hb = self.staging(slot)

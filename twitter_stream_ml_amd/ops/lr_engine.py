@@ -255,20 +255,67 @@ class HostBatchView:
         return RawBatch(text, offsets, is_rt, self.scalars().copy(), self.batch_time_ms)
 
 
+# ptr -> weakref.finalize of a live registration (register_host)
+_REGISTERED: Dict[int, "weakref.finalize"] = {}
+
+
+def _drop_registration(ptr: int) -> None:
+    """Finalizer of a registered array: unregister before its memory is freed
+    (the runtime would otherwise keep the stale range in its host-pointer map
+    and resolve later buffers mapped there to it -- round 5's ``invalid
+    argument`` H2D and illegal memory access, profiles/README.md round 6)."""
+    _REGISTERED.pop(ptr, None)
+    try:
+        hip().host_unregister(ptr)
+    except BaseException:   # noqa: BLE001 -- interpreter teardown: the runtime may be gone
+        import sys
+        if not sys.is_finalizing():
+            raise
+
+
 def register_host(arr) -> None:
     """Page-lock a host array (or a :class:`Utf8Text`'s bytes) so ``submit``
-    can DMA from it asynchronously."""
+    can DMA from it asynchronously.  The registration lives as long as the
+    array object: it is undone (after the device drained) when the array is
+    freed, or by :func:`unregister_host`."""
     if isinstance(arr, Utf8Text):
         register_host(arr.data)
         arr.pinned = True
         return
-    if arr.nbytes:
-        hip().host_register(int(arr.ctypes.data), int(arr.nbytes))
+    if not arr.nbytes:
+        return
+    # a view: the registration must not outlive the memory, so it is tied to
+    # the outermost array of the chain (it dies only after every view)
+    owner = arr
+    while isinstance(owner.base, np.ndarray):
+        owner = owner.base
+    ptr = int(arr.ctypes.data)
+    hip().host_register(ptr, int(arr.nbytes))
+    try:
+        fin = weakref.finalize(owner, _drop_registration, ptr)
+    except TypeError:   # an owner that takes no weak reference: tie it to the array itself
+        fin = weakref.finalize(arr, _drop_registration, ptr)
+    fin.atexit = False
+    _REGISTERED[ptr] = fin
 
 
-def unregister_host(arr: np.ndarray) -> None:
-    if arr.nbytes:
-        hip().host_unregister(int(arr.ctypes.data))
+def unregister_host(arr) -> None:
+    if isinstance(arr, Utf8Text):
+        unregister_host(arr.data)
+        arr.pinned = False
+        return
+    if not arr.nbytes:
+        return
+    ptr = int(arr.ctypes.data)
+    fin = _REGISTERED.pop(ptr, None)
+    if fin is not None:
+        fin.detach()
+    hip().host_unregister(ptr)
+
+
+def registered_host_ranges():
+    """Live host registrations ``[(ptr, bytes)]`` (native registry)."""
+    return list(hip().host_registrations())
 
 
 class DeviceLinearRegression:
@@ -285,7 +332,8 @@ class DeviceLinearRegression:
         # last reference frees the engine's device memory at once
         me = weakref.proxy(self)
         self._pipe = SlotPipeline(self.raw_slots, lambda s, raw: me.staging(s).load(raw, cfg.ingest),
-                                  lambda hb, slot: me.submit(hb, slot), lambda: me.synchronize())
+                                  lambda hb, slot: me.submit(hb, slot), lambda: me.synchronize(),
+                                  discard=lambda slot: me._eng.discard(int(slot)))
 
     # ---- weights (MLlib setInitialWeights / latestModel.weights) ---------
     @property
