@@ -101,6 +101,10 @@ def parse_args(argv=None):
     ap.add_argument("--timeout", type=float, default=480.0,
                     help="whole-run watchdog (s, 0 = off): on expiry every rank dumps its Python stacks and "
                          "communicator counters, aborts the communicator and exits non-zero")
+    ap.add_argument("--master", default="",
+                    help="local[N]: BASELINE config 1 -- the fp64 CPU engine (oracle/mllib.py semantics, "
+                         "what the reference's --master local[2] runs) on the same synthetic data, N host "
+                         "threads (one stands for the receiver, as in Spark local mode); no GPU is used")
     ap.add_argument("--json-out", default="")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args(argv)
@@ -353,8 +357,92 @@ def start_watchdog(timeout_s: float, comm, rank: int):
     return wd
 
 
+def run_cpu_local(args) -> int:
+    """BASELINE config 1: ``--master local[N]`` -- the reference's own mode
+    (``ConfArguments.scala:54-56``, README ``local[2]``): the fp64 CPU engine
+    (``models/linear_regression.py CpuLinearRegression``, MLlib 1.6.1
+    semantics of ``LinearRegression.scala:36-91``) trains the same synthetic
+    tweets as the GPU line.  N host threads, one of which stands for Spark's
+    receiver (as in local mode), so the featurizer and the GD loop get N - 1.
+    A step = one micro-batch: featurize (filter, lower-case, bigram hashing),
+    prequential predict + stats, GD to convergence; the latency of a batch is
+    its step (the CPU engine has no queue).  The batch is smaller than the
+    GPU line's (``--batch``, default 50000 here) and the JSON says so."""
+    import re
+    m = re.fullmatch(r"local\[(\d+|\*)\]", args.master)
+    if not m:
+        print(f"--master {args.master}: expected local[N]", file=sys.stderr)
+        return 2
+    n_thr = os.cpu_count() or 1 if m.group(1) == "*" else int(m.group(1))
+    workers = max(1, n_thr - 1)
+    os.environ["TWTML_HOST_THREADS"] = str(workers)
+    from twitter_stream_ml_amd.models.linear_regression import CpuLinearRegression, CpuLRConfig
+    from twitter_stream_ml_amd.sources.synthetic import SynthConfig, generate_batch
+    B = 50_000 if str(args.batch) == "1000000" else int(args.batch)
+    synth = SynthConfig.profile(args.profile, seed=args.seed)
+    n_pool = args.warmup + args.steps
+    t_gen = time.time()
+    pool = [generate_batch(synth, i * B, B, batch_time_ms=synth.now_ms) for i in range(n_pool)]
+    t_gen = time.time() - t_gen
+    eng = CpuLinearRegression(CpuLRConfig(num_text_features=args.features, hash=args.hash,
+                                          step_size=args.step_size, num_iterations=args.iters, fraction=1.0,
+                                          tol=args.tol, begin=100, end=1000))
+    lat, kept, iters = [], [], []
+    for i, raw in enumerate(pool):
+        if i == args.warmup:
+            t0 = time.perf_counter()
+        s = time.perf_counter()
+        res = eng.train_batch(raw, want_pred=False)
+        if i >= args.warmup:
+            lat.append((time.perf_counter() - s) * 1e3)
+            kept.append(res["n_kept"])
+            iters.append(res["iterations"])
+    t1 = time.perf_counter()
+    value = float(sum(kept)) / (t1 - t0)
+    out = {
+        "metric": "tweets/sec trained (whole node)",
+        "value": round(value, 1),
+        "unit": "tweets/s",
+        "n_gpus": 0,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round((t1 - t0) / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": 1.0,
+        "dtype": "fp64",
+        "data": (f"synthetic tweet-shaped records (seeded C++ generator, "
+                 f"{'realistic 50K-word multi-script' if args.profile == 'wide' else 'toy ~300-word'} vocabulary, "
+                 f"{n_pool} distinct batches), zero-init weights"),
+        "config": {
+            "model": f"StreamingLinearRegressionWithSGD, {args.features}-dim hashed bigrams + 4 numeric",
+            "global_batch": B, "seq_len": 280, "parallelism": f"cpu {args.master}",
+            "numIterations": args.iters, "stepSize": args.step_size, "miniBatchFraction": 1.0,
+            "hash": args.hash, "profile": args.profile,
+            "batch_note": f"{B} tweets per micro-batch (the GPU line trains 1M per GPU per step)",
+        },
+        "baseline_config": "BASELINE.json config 1: --master local[2] CPU, synthetic tweet source",
+        "engine": "fp64 CPU engine (MLlib 1.6.1 semantics, oracle/mllib.py run_minibatch_sgd over scipy CSR; "
+                  "native C++ featurizer)",
+        "host_threads": workers,
+        "gd_iterations_mean": float(np.mean(iters)) if iters else 0.0,
+        "p50_microbatch_latency_ms": round(float(np.median(lat)), 3),
+        "trained_tweets_per_step": round(float(np.mean(kept)), 1),
+        "pool_gen_s": round(t_gen, 2),
+        "wall_s": round(time.time() - T_START, 1),
+    }
+    line = json.dumps(out)
+    print(line, flush=True)
+    if args.json_out:
+        with open(args.json_out, "w") as fh:
+            fh.write(line + "\n")
+    return 0
+
+
 def main(argv=None) -> int:
     args = parse_args(argv)
+    if args.master.startswith("local"):
+        return run_cpu_local(args)
     args.e2e = not args.prepacked
     import torch  # noqa: F401  (binds the HIP runtime before the engine loads)
     from twitter_stream_ml_amd.parallel import dist as D

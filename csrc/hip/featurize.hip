@@ -346,13 +346,16 @@ __device__ __forceinline__ uint32_t bytes_eq(uint32_t x, uint32_t b) {
 // unit per unit (rows.hip's special rows): C4 B0 (U+0130), CE A3 (U+03A3,
 // Final_Sigma), F0 90 / F0 91 / F0 96 / F0 9E (the planes of the astral
 // cased letters: Deseret, Osage, Old Hungarian, Warang Citi, Medefaidrin,
-// Adlam; emoji, F0 9F, are not).  A superset of the special rows: the
-// normaliser checks every flagged row exactly.  v: four bytes, n: the
-// byte after each of them.
+// Adlam; emoji, F0 9F, are not), and ED A0: a high surrogate D800..D83F
+// written as its own 3-byte sequence (CESU-8 / Java's modified UTF-8: the
+// same astral letters as a surrogate pair of 3-byte sequences).
+// A superset of the special rows: the normaliser checks every flagged row
+// exactly.  v: four bytes, n: the byte after each of them.
 __device__ __forceinline__ uint32_t special_pairs(uint32_t v, uint32_t n) {
   const uint32_t c4 = bytes_eq(v, 0xC4u), ce = bytes_eq(v, 0xCEu), f0 = bytes_eq(v, 0xF0u);
-  if (!(c4 | ce | f0)) return 0u;   // most multi-byte text (CJK, Cyrillic, Arabic, ...) has none of the leads
-  uint32_t m = (c4 & bytes_eq(n, 0xB0u)) | (ce & bytes_eq(n, 0xA3u));
+  const uint32_t ed = bytes_eq(v, 0xEDu);
+  if (!(c4 | ce | f0 | ed)) return 0u;   // most multi-byte text (CJK, Cyrillic, Arabic, ...) has none of the leads
+  uint32_t m = (c4 & bytes_eq(n, 0xB0u)) | (ce & bytes_eq(n, 0xA3u)) | (ed & bytes_eq(n, 0xA0u));
   if (f0)
     m |= f0 & (bytes_eq(n, 0x90u) | bytes_eq(n, 0x91u) | bytes_eq(n, 0x96u) | bytes_eq(n, 0x9Eu));
   return m;

@@ -218,15 +218,29 @@ __device__ __forceinline__ LaneScale lane_scale(const IterScale& sc, const DevSg
 // fixed-order DPP reduction): identical in every caller.  Also returns the
 // max |w_text| after that update (the next iteration's weight scale).
 // ---------------------------------------------------------------------------
-// Workgroups of every update launch of the batch (host: update_split): the
-// number of partials in each record, known without reading the record.
-__device__ __forceinline__ int upd_grid(const DevSgd& d) {
+// Near column tiles and far slot ranges of every update launch of the batch:
+// a function of the layout only (the same on every DP rank).  ONE helper for
+// the host launch (launch_sgd_update) and the device convergence check, which
+// reads that many partials per record without reading the record's own count
+// (rec[2]) first (the two must not drift).
+struct UpdSplit {
+  int nt, nf;
+};
+__host__ __device__ __forceinline__ UpdSplit upd_split(const DevSgd& d) {
   const int64_t tiles = (d.nl + kPartVals - kNumNumeric + kWave - 1) / kWave;
   const int64_t n_far = kNumNumeric + d.n_unique - d.far_base;
-  const int nt = int(max(int64_t(1), min(tiles, int64_t(kMaxUpdGrid / 2))));
-  const int nf = n_far > 0 ? int(max(int64_t(1), min((n_far + kUpdFarSlots - 1) / kUpdFarSlots, int64_t(kMaxUpdGrid - nt))))
-                           : 0;
-  return nt + nf;
+  const int64_t nt = tiles < 1 ? 1 : (tiles < kMaxUpdGrid / 2 ? tiles : kMaxUpdGrid / 2);
+  int64_t nf = 0;
+  if (n_far > 0) {
+    nf = (n_far + kUpdFarSlots - 1) / kUpdFarSlots;
+    if (nf > kMaxUpdGrid - nt) nf = kMaxUpdGrid - nt;
+    if (nf < 1) nf = 1;
+  }
+  return UpdSplit{int(nt), int(nf)};
+}
+__device__ __forceinline__ int upd_grid(const DevSgd& d) {
+  const UpdSplit u = upd_split(d);
+  return u.nt + u.nf;
 }
 
 __device__ bool sgd_converged_wave(const DevSgd& d, int it, double tol, double* maxw_out = nullptr) {
@@ -1315,20 +1329,9 @@ __global__ __launch_bounds__(kUpdThreads) void k_sgd_update(DevSgd d, SgdParams 
   }
 }
 
-// Near tiles and far ranges of the update grid: a function of the layout
-// only, the same on every DP rank.
-static void update_split(const DevSgd& d, int& nt, int& nf) {
-  const int64_t tiles = (d.nl + kPartVals - kNumNumeric + kWave - 1) / kWave;
-  const int64_t n_far = kNumNumeric + d.n_unique - d.far_base;
-  nt = int(std::max<int64_t>(1, std::min<int64_t>(tiles, kMaxUpdGrid / 2)));
-  nf = n_far > 0 ? int(std::max<int64_t>(1, std::min<int64_t>((n_far + kUpdFarSlots - 1) / kUpdFarSlots,
-                                                                 kMaxUpdGrid - nt))) : 0;
-}
-
 void launch_sgd_update(const DevSgd& d, const SgdParams& sp, int nparts, hipStream_t s) {
-  int nt = 0, nf = 0;
-  update_split(d, nt, nf);
-  TWTML_LAUNCH(k_sgd_update, dim3(nt + nf), dim3(kUpdThreads), 0, s, d, sp, nparts, nt, nf);
+  const UpdSplit u = upd_split(d);
+  TWTML_LAUNCH(k_sgd_update, dim3(u.nt + u.nf), dim3(kUpdThreads), 0, s, d, sp, nparts, u.nt, u.nf);
 }
 
 // DP: cross-workgroup reduction of the partial rows into the packed buffer

@@ -179,9 +179,9 @@ def test_extension_flags():
                                                                         "murmur3", 3)
 
 
-def test_plot_points_default_plots_every_row():
-    """the reference appends every kept row's (real, pred) pair
-    (LinearRegression.scala:76-77), so the default plotPoints is 0 (= all);
-    a cap is opt-in."""
-    assert ConfArguments().parse([]).plotPoints == 0
-    assert ConfArguments().parse(["--plotPoints", "10000"]).plotPoints == 10000
+def test_plot_points_default_is_bounded():
+    """a bounded default (10000 pairs per batch, sampled on the
+    device) -- at the reference's batch sizes that is every kept row
+    (LinearRegression.scala:76-77); 0 (= all rows) is opt-in."""
+    assert ConfArguments().parse([]).plotPoints == 10000
+    assert ConfArguments().parse(["--plotPoints", "0"]).plotPoints == 0

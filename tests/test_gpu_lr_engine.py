@@ -158,6 +158,54 @@ def test_device_special_lowering(hip_module, ingest):
         np.testing.assert_array_equal(rows[k], np.sort(want), err_msg=f"row {k}: {texts[k]!r}")
 
 
+def test_utf8_cesu_surrogate_pairs_are_lowered(hip_module):
+    """a receiver that writes astral letters as a surrogate pair of
+    3-byte sequences (CESU-8, Java's modified UTF-8: ED A0 81 ED B0 80 for
+    U+10400) must get them lower-cased like 4-byte UTF-8 does.  The decoder
+    flags such rows as special candidates (ED A0), so the flagged-rows-only
+    normaliser (the default) lowers them: device == oracle."""
+    from twitter_stream_ml_amd.records.batch import RawBatch, Utf8Text, utf16_units
+    base = generate_batch(SynthConfig.profile("twitter", seed=5), 0, 300, batch_time_ms=NOW)
+    texts = [base.text_of(i) for i in range(base.n)]
+    for j, s in enumerate(["\U00010400bc", "x \U00010401\U00010402 y", "\U0001E900 adlam", "ok \U00010427",
+                           "\U0001F600 emoji only", "\U00010C80 hungarian"]):
+        texts[11 * j + 1] = s
+
+    def cesu(s):
+        out = bytearray()
+        for ch in s:
+            c = ord(ch)
+            if c > 0xFFFF:
+                c -= 0x10000
+                out += chr(0xD800 + (c >> 10)).encode("utf-8", "surrogatepass")
+                out += chr(0xDC00 + (c & 0x3FF)).encode("utf-8", "surrogatepass")
+            else:
+                out += ch.encode("utf-8", "surrogatepass")
+        return bytes(out)
+
+    units = [utf16_units(s) for s in texts]
+    off = np.zeros(len(texts) + 1, np.int64)
+    off[1:] = np.cumsum([u.shape[0] for u in units])
+    enc = [cesu(s) for s in texts]
+    boff = np.zeros(len(texts) + 1, np.int64)
+    boff[1:] = np.cumsum([len(b) for b in enc])
+    u8 = Utf8Text(np.frombuffer(b"".join(enc), np.uint8).copy(), boff)
+    sc = base.scalars.copy()
+    sc[0, :] = 500
+    raw = RawBatch(np.concatenate(units), off, np.ones(len(texts), np.uint8), sc, NOW, utf8=u8)
+    eng = _engine(1 << 20, "murmur3", lazy_idx=False, ingest="utf8")
+    res = eng.train_batch(raw, want_pred=True)
+    assert res["rows_lowered"] >= 1, res["rows_lowered"]
+    dbg = eng._eng.debug_prepared()
+    fb = featurize_batch(raw, 1 << 20, 100, 1000, now_ms=NOW, hash="murmur3")
+    rows = _rows_from_debug(dbg)
+    Xt = fb.X[:, :1 << 20].tocsr()
+    for k in range(fb.n):
+        s, e = Xt.indptr[k], Xt.indptr[k + 1]
+        want = np.repeat(Xt.indices[s:e], Xt.data[s:e].astype(np.int64))
+        np.testing.assert_array_equal(rows[k], np.sort(want), err_msg=f"row {k}: {texts[k]!r}")
+
+
 @pytest.mark.parametrize("profile,F,hash", [("twitter", 1 << 20, "java"), ("wide", 1 << 20, "java"),
                                             ("wide", 100_000_000, "murmur3")])
 def test_utf8_ingest_trains_like_wire(hip_module, profile, F, hash):

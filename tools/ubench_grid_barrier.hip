@@ -1,5 +1,5 @@
 // Grid-wide barrier cost on MI355X, with the barrier the persistent GD loop
-// uses (csrc/hip/grid_sync.h: XCD-hierarchical arrival, relaxed polling with
+// uses (tools/grid_sync.h: XCD-hierarchical arrival, relaxed polling with
 // s_sleep, ONE agent-scope acquire after the exit).  Round 4's version put
 // all 256 arrivals on one counter and polled with an acquire load per spin
 // (an L1 invalidate per poll): 13.7 us per barrier.
@@ -20,7 +20,7 @@
 #include <cstdio>
 #include <cstdlib>
 
-#include "hip/grid_sync.h"
+#include "grid_sync.h"
 
 #define CHECK(x)                                                                       \
   do {                                                                                 \

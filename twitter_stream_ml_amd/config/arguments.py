@@ -186,7 +186,11 @@ class ConfArguments:
         self.checkpointInterval = (c.getInt("checkpointInterval")
                                    if c.hasPath("checkpointInterval") else 10)
         self.resume = ""
-        self.plotPoints = c.getInt("plotPoints") if c.hasPath("plotPoints") else 0
+        # bounded by default: at the reference's batch sizes (~11
+        # tweets per 5 s batch) 10000 is every row, as
+        # LinearRegression.scala:76-77 appends them; at 1M-tweet batches the
+        # device samples 10000 evenly spaced pairs.  0 = every row.
+        self.plotPoints = c.getInt("plotPoints") if c.hasPath("plotPoints") else 10000
         self.seed = 42
         self.batchTimeout = 0.0
         self.checkReplicas = 0
@@ -226,7 +230,7 @@ Usage: twtml-spark [options]
                                                   continuing its stream position)
   --batchTimeout <seconds>                        abort the process if a batch hangs (0 = off)
   --checkReplicas <n>                             verify DP replicas agree every n batches
-  --plotPoints <n>                                points per Lightning append (default 0 = all)
+  --plotPoints <n>                                points per Lightning append (default 10000; 0 = all)
   --legacyNumTextFeatures                         reproduce the reference bug: ignore -f
   """
 

@@ -41,10 +41,14 @@ log = logging.getLogger("twtml.report.plot")
 
 class PlotShipper:
     def __init__(self, session, rank: int = 0, world: int = 1, maxsize: int = 64,
-                 gather_timeout_s: float = 60.0):
+                 gather_timeout_s: float = 60.0, max_bytes: int = 64 << 20):
         self.session = session
         self.rank, self.world = int(rank), int(world)
         self.maxsize = max(1, int(maxsize))
+        # the backlog is also bounded in bytes: with --plotPoints 0 a waiting
+        # sample holds every kept row (16 B per row as two fp64 series)
+        self.max_bytes = max(1, int(max_bytes))
+        self._bytes = 0
         self.group = None
         if self.world > 1:
             import torch.distributed as dist
@@ -71,13 +75,17 @@ class PlotShipper:
         with self._cv:
             if self.stopped:
                 return
-            self._items.append([self._seq, tuple(stats), np.array(real, np.float64),
-                                np.array(pred, np.float64)])
+            r, p = np.array(real, np.float64), np.array(pred, np.float64)
+            self._items.append([self._seq, tuple(stats), r, p])
             self._seq += 1
             self._waiting += 1
-            if self._waiting > self.maxsize:   # drop the oldest waiting sample, keep its marker
+            self._bytes += r.nbytes + p.nbytes
+            # drop the oldest waiting samples (keep their markers) beyond either bound;
+            # the newest sample always stays
+            while self._waiting > 1 and (self._waiting > self.maxsize or self._bytes > self.max_bytes):
                 for it in self._items:
                     if it is not None and it[2] is not None:
+                        self._bytes -= it[2].nbytes + it[3].nbytes
                         it[2] = it[3] = None
                         self._waiting -= 1
                         self.dropped += 1
@@ -95,6 +103,7 @@ class PlotShipper:
             it = self._items.popleft()
             if it is not None and it[2] is not None:
                 self._waiting -= 1
+                self._bytes -= it[2].nbytes + it[3].nbytes
             return it
 
     def _stop(self, why: str) -> None:
@@ -102,6 +111,7 @@ class PlotShipper:
             self.stopped = True
             self._items.clear()
             self._waiting = 0
+            self._bytes = 0
         log.warning("plot shipping stopped: %s", why)
 
     def _run(self) -> None:
