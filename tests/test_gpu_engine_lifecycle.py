@@ -109,7 +109,7 @@ def test_back_to_back_engines_deep_prefetch_async_checkpoint(hip_module, tmp_pat
         assert pipe.in_flight == 0
         eng.synchronize()
         job.close()
-        del job, eng, src, batches, stray
+        del job, eng, src, batches, stray, u   # u: the prefetch loop's last batch
         gc.collect()
         assert list(hip_module.teardown_errors()) == []
         assert _live(hip_module) == base_regs           # the pool's registrations ended with it
