@@ -29,6 +29,35 @@ def _live(hip_module):
     return {p: n for p, n in hip_module.host_registrations()}
 
 
+def _who_holds(ptrs, depth=5):
+    """Referrer chains of the objects still holding registered arrays
+    (diagnostics; ndarrays are not tracked by gc, their holders are)."""
+    import types
+    names = ("Utf8Text", "RawBatch", "HostBatchView", "DeviceLinearRegression", "SlotPipeline")
+    live = [o for o in gc.get_objects() if type(o).__name__ in names]
+    roots = [o for o in live if type(o).__name__ != "Utf8Text" or int(o.data.ctypes.data) in ptrs]
+    out = [f"live: " + ", ".join(f"{n}={sum(type(o).__name__ == n for o in live)}" for n in names)]
+    for a in roots[:2]:
+        out.append(f"-- {type(a).__name__}")
+        frontier, seen = [a], {id(a), id(roots), id(live)}
+        for d in range(depth):
+            nxt = []
+            for o in frontier:
+                for r in gc.get_referrers(o):
+                    if id(r) in seen or isinstance(r, types.FrameType) or r is frontier or r is nxt:
+                        continue
+                    seen.add(id(r))
+                    desc = type(r).__name__
+                    if isinstance(r, dict):
+                        desc += "{" + ",".join(str(k) for k in list(r)[:8]) + "}"
+                    elif isinstance(r, types.FunctionType):
+                        desc += f" {r.__qualname__}"
+                    out.append(f"{'  ' * (d + 1)}{desc}")
+                    nxt.append(r)
+            frontier = nxt[:12]
+    return "\n".join(out[:120])
+
+
 def test_registration_follows_array_lifetime(hip_module):
     import torch
     from twitter_stream_ml_amd.ops.lr_engine import register_host, unregister_host
@@ -112,6 +141,7 @@ def test_back_to_back_engines_deep_prefetch_async_checkpoint(hip_module, tmp_pat
         del job, eng, src, batches, stray, u   # u: the prefetch loop's last batch
         gc.collect()
         assert list(hip_module.teardown_errors()) == []
-        assert _live(hip_module) == base_regs           # the pool's registrations ended with it
+        left = set(_live(hip_module)) - set(base_regs)
+        assert not left, _who_holds(left)               # the pool's registrations ended with it
     # three different streams: three different models
     assert not np.array_equal(weights[0], weights[1])

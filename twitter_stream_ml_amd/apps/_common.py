@@ -44,6 +44,25 @@ def load_resume_state(resume: str, checkpoint: str, rank: int) -> ResumeState:
     return st
 
 
+def background_writer_thread(threads: int = 2) -> None:
+    """The calling thread is a background writer (checkpoints): lowest CPU
+    priority for it, and at most ``threads`` pyarrow encode threads.  On a
+    CPU quota (a GPU box's cgroup: 16 CPUs) a writer that fans out over
+    pyarrow's default pool (one thread per machine CPU) throttles the whole
+    process, the training thread included."""
+    try:
+        os.setpriority(os.PRIO_PROCESS, threading.get_native_id(), 19)   # this thread only (Linux)
+    except (OSError, AttributeError):
+        pass
+    try:
+        import pyarrow as pa
+        if pa.cpu_count() > threads:
+            pa.set_cpu_count(threads)
+        pa.set_io_thread_count(min(threads, pa.io_thread_count()))
+    except Exception:   # noqa: BLE001 -- pyarrow absent: the writer is not ours to tune
+        pass
+
+
 class StreamCheckpointer:
     """Every ``interval`` batches: each rank records its stream position, a
     barrier, then rank 0 takes a snapshot of the model and replaces the model
@@ -115,6 +134,7 @@ class StreamCheckpointer:
         self._wait_writer()
 
     def _write(self, save, progress: dict, batches: int) -> None:
+        background_writer_thread()
         try:
             save(self.path, progress)
             self.written += 1
