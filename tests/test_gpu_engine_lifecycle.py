@@ -138,7 +138,9 @@ def test_back_to_back_engines_deep_prefetch_async_checkpoint(hip_module, tmp_pat
         assert pipe.in_flight == 0
         eng.synchronize()
         job.close()
-        del job, eng, src, batches, stray, u   # u: the prefetch loop's last batch
+        # every local that reaches the engine (cp -> job -> engine -> staging views,
+        # which hold the DMA'd pool arrays) or a batch (u: the prefetch loop's last)
+        del job, eng, src, batches, stray, u, cp, pipe
         gc.collect()
         assert list(hip_module.teardown_errors()) == []
         left = set(_live(hip_module)) - set(base_regs)
