@@ -240,6 +240,7 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
   const char* fdp = std::getenv("TWTML_FORCE_DP");
   dp_ = world_ > 1 || (comm_ && (cfg_.force_dp != 0 || (fdp && fdp[0] == '1')));
   comm_timing_ = dp_ && cfg_.comm_timing != 0;
+  if (const char* e = std::getenv("TWTML_RCCL_STANDIN"); e && dp_) standin_wgs_ = std::max(0, std::atoi(e));
   // Prepare-ahead of batch t+1 while t trains: all of it on one GPU; on DP
   // ranks the local part, then (after the training thread all-gathered the
   // ranks' packets between two of t's GD iterations) the rest.
@@ -545,6 +546,7 @@ LREngine::~LREngine() {
   if (ready_host_) (void)hipHostFree(ready_host_);
   if (hnu_) (void)hipHostFree(hnu_);
   if (dnu_) (void)hipFree(dnu_);
+  if (standin_buf_) (void)hipFree(standin_buf_);
   for (auto e : iter_events_) (void)hipEventDestroy(e);
   for (auto e : comm_ev_) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(compute_);
@@ -900,7 +902,7 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred, int64_t plot_points) {
     const bool fused = !dp_ && sgd_.nparts > 0;
     const bool itime = std::getenv("TWTML_ITER_TIMING") != nullptr;
     if (itime && !iter_tdbg_) iter_tdbg_ = dmalloc<uint64_t>(4096 + size_t(iters + 2) * 32);
-    const size_t kd_words = size_t(iters + 2) * 3 * kKdbgWgs * 2;
+    const size_t kd_words = size_t(iters + 2) * kKdbgKinds * kKdbgWgs * 2;
     if (itime && !iter_kdbg_) iter_kdbg_ = dmalloc<uint64_t>(kd_words);
     sgd_.tdbg = itime ? iter_tdbg_ : nullptr;
     sgd_.kdbg = itime ? iter_kdbg_ : nullptr;
@@ -946,6 +948,18 @@ BatchResult LREngine::train(PrepBuf& pb, bool want_pred, int64_t plot_points) {
         if (comm_timing_) TWTML_HIP_CHECK(hipEventRecord(comm_ev_[size_t(2 * (i - 1))], s));
         comm_->allreduce(sgd_.gacc, size_t(sgd_.far_off + n_far), ncclInt64, ncclSum, s);
         res.comm_bytes += int64_t(sizeof(int64_t)) * (sgd_.far_off + n_far);
+        if (standin_wgs_ > 0) {   // DP cost model: the CU footprint of a multi-rank all-reduce
+          const int64_t nw = sgd_.far_off + n_far;
+          if (nw > standin_cap_) {
+            if (standin_buf_) {
+              TWTML_HIP_CHECK(hipStreamSynchronize(s));
+              (void)hipFree(standin_buf_);
+            }
+            standin_cap_ = nw + nw / 4;
+            standin_buf_ = dmalloc<int64_t>(size_t(standin_cap_));
+          }
+          launch_rccl_standin(sgd_.gacc, standin_buf_, nw, standin_wgs_, sgd_.kdbg, i, s);
+        }
         if (comm_timing_) TWTML_HIP_CHECK(hipEventRecord(comm_ev_[size_t(2 * (i - 1) + 1)], s));
         ++comm_iters;
       }
@@ -1054,17 +1068,20 @@ void LREngine::print_iter_timing(int iters) {
   // per-kernel workgroup stamps: dispatch ramp (last start - first start),
   // span (last end - first start), median / max workgroup time, and the gap
   // from the previous kernel's last end to this one's first start
-  const size_t kd_words = size_t(iters + 2) * 3 * kKdbgWgs * 2;
+  const size_t kd_words = size_t(iters + 2) * kKdbgKinds * kKdbgWgs * 2;
   std::vector<uint64_t> kd(kd_words);
   TWTML_HIP_CHECK(hipMemcpyAsync(kd.data(), iter_kdbg_, kd_words * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
   TWTML_HIP_CHECK(hipStreamSynchronize(s));
-  const char* names[3] = {"iteration", "far backward", "update"};
-  double acc[3][5] = {};
-  int cnt[3] = {0, 0, 0};
+  const char* names[kKdbgKinds] = {"iteration", "far backward", "update", "rccl stand-in"};
+  double acc[kKdbgKinds][5] = {};
+  int cnt[kKdbgKinds] = {0, 0, 0, 0};
+  // launch order within an iteration: iteration, far backward, [stand-in], update
+  const int order[kKdbgKinds] = {0, 1, 3, 2};
   for (int it = 2; it <= iters; ++it) {
     uint64_t prev_end = 0;
-    for (int k = 0; k < 3; ++k) {
-      const uint64_t* b = kd.data() + (size_t(it) * 3 + size_t(k)) * kKdbgWgs * 2;
+    for (int ko = 0; ko < kKdbgKinds; ++ko) {
+      const int k = order[ko];
+      const uint64_t* b = kd.data() + (size_t(it) * kKdbgKinds + size_t(k)) * kKdbgWgs * 2;
       uint64_t s0 = UINT64_MAX, s1 = 0, e1 = 0;
       std::vector<double> dur;
       for (int g = 0; g < kKdbgWgs; ++g) {
@@ -1085,9 +1102,9 @@ void LREngine::print_iter_timing(int iters) {
       ++cnt[k];
     }
   }
-  for (int k = 0; k < 3; ++k)
+  for (int k = 0; k < kKdbgKinds; ++k)
     if (cnt[k])
-      std::fprintf(stderr, "kernel %-12s (us, %d iters): ramp %.2f span %.2f wg p50 %.2f wg max %.2f gap before %.2f\n",
+      std::fprintf(stderr, "kernel %-13s (us, %d iters): ramp %.2f span %.2f wg p50 %.2f wg max %.2f gap before %.2f\n",
                    names[k], cnt[k], acc[k][0] / cnt[k], acc[k][1] / cnt[k], acc[k][2] / cnt[k], acc[k][3] / cnt[k],
                    acc[k][4] / cnt[k]);
 }

@@ -337,6 +337,9 @@ class LREngine {
   double* host_out_dev_ = nullptr;    // device view of host_out_ (k_batch_out)
   int64_t* host_stat_dev_ = nullptr;  // device view of host_stat_
   uint64_t* iter_kdbg_ = nullptr;     // TWTML_ITER_TIMING: per-workgroup GD kernel stamps
+  int standin_wgs_ = 0;               // DP: TWTML_RCCL_STANDIN workgroups after each gradient all-reduce
+  int64_t* standin_buf_ = nullptr;    // ... their destination buffer
+  int64_t standin_cap_ = 0;
   float* plot_host_ = nullptr;        // mapped pinned [2 max_rows]: sampled (pred, real) pairs
   float* plot_dev_ = nullptr;         // ... its device address (k_plot_sample writes it)
   double* host_flags_ = nullptr;      // pinned [iters + 1] convergence flag per iteration

@@ -278,7 +278,7 @@ struct DevSgd {
   double* itrec;        // [max_iters+2][kRecStride] per-iteration scale / update records
   uint64_t* tdbg;       // optional phase stamps (TWTML_ITER_TIMING): [iter][wg 0 / last][8]
   uint64_t* kdbg;       // optional per-workgroup start / end stamps (TWTML_ITER_TIMING):
-                        // [iter][iteration, far backward, update][kKdbgWgs][2]
+                        // [iter][iteration, far backward, update, rccl stand-in][kKdbgWgs][2]
   const double* bounds; // [8] batch bounds: max row bigram count, max |y|, max |n_k| (k = 0..3)
   const volatile int64_t* ready_word;   // DP: host-mapped, this rank's next-batch ready word
   int32_t rank, world;
@@ -302,6 +302,9 @@ struct DevSgd {
 
 constexpr int kNormParts = 1024;   // grid cap of the norm / gather / scatter kernels
 constexpr int kKdbgWgs = 1024;     // workgroups stamped per kernel (TWTML_ITER_TIMING)
+// kernels stamped per GD iteration: iteration, far backward, update, and the
+// DP RCCL-footprint stand-in (TWTML_RCCL_STANDIN)
+constexpr int kKdbgKinds = 4;
 
 
 // Iteration record i: [0] updates so far, [1] m, [2] update workgroups,
@@ -369,6 +372,11 @@ void launch_sgd_update(const DevSgd& d, const SgdParams& sp, int nparts, hipStre
 void launch_far_grad(const DevSgd& d, const SgdParams& sp, int num_cu, hipStream_t s);
 // after the GD loop: convergence of the last update -> state
 void launch_sgd_finish(const DevSgd& d, const SgdParams& sp, hipStream_t s);
+// DP cost model: a kernel with the CU footprint of an RCCL all-reduce of n
+// int64 (wgs workgroups of 256 threads reading n and writing n words), with
+// TWTML_ITER_TIMING stamps as kind 3 of iteration `it`
+void launch_rccl_standin(const int64_t* src, int64_t* dst, int64_t n, int wgs, uint64_t* kdbg, int it,
+                         hipStream_t s);
 void launch_scatter_w(const DevSgd& d, const DevPrepared& p, hipStream_t s);
 // |w|^2 for the next batch: |w_rest|^2 + |w_active after training|^2, from
 // the scatter's block partials (trained) or state[4] unchanged (no rows)

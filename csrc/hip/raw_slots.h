@@ -24,7 +24,11 @@ namespace twtml {
 
 struct HostBatch;
 
-constexpr int kDefaultRawSlots = 8;
+// 6: the knee of the headline bench's depth sweep (profiles/r6/raw_slots_sweep.txt:
+// 4 -> 237 M tweets/s at p50 10.0 ms, 5 -> 248 M / 12.7 ms, 6 -> 260 M / 14.9 ms,
+// 8 -> 261 M / 21.1 ms); the streaming drivers size their own (apps/, scheduler
+// prefetch depth + 2)
+constexpr int kDefaultRawSlots = 6;
 constexpr int kMaxRawSlots = 32;
 
 class RawSlots {

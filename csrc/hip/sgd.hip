@@ -68,7 +68,7 @@ constexpr int kUpdFarSlots = kUpdThreads;        // far slots per far update wor
 // Per-workgroup start / end stamps of the GD kernels (TWTML_ITER_TIMING only).
 __device__ __forceinline__ void kdbg_stamp(uint64_t* base, int it, int kind, int end) {
   if (!base || threadIdx.x != 0 || blockIdx.x >= unsigned(kKdbgWgs)) return;
-  base[((int64_t(it) * 3 + kind) * kKdbgWgs + blockIdx.x) * 2 + end] = __builtin_amdgcn_s_memrealtime();
+  base[((int64_t(it) * kKdbgKinds + kind) * kKdbgWgs + blockIdx.x) * 2 + end] = __builtin_amdgcn_s_memrealtime();
 }
 
 // Iteration record i and its per-update-workgroup partials.
@@ -1379,6 +1379,25 @@ __global__ void k_sgd_finish(DevSgd d, SgdParams sp) {
     d.state[0] = 1.0;
     if (conv) d.state[1] = 1.0;
   }
+}
+
+// RCCL-footprint stand-in (DP cost model, README): at the all-reduce point of
+// every GD iteration, wgs workgroups move the packed gradient buffer's bytes
+// (read n, write n int64) -- the CU share a ring all-reduce kernel holds on
+// each rank beside the next batch's prep.  Its workgroup stamps give the
+// dispatch ramp it meets there (TWTML_ITER_TIMING).
+__global__ __launch_bounds__(256) void k_rccl_standin(const int64_t* src, int64_t* dst, int64_t n,
+                                                      uint64_t* kdbg, int it) {
+  kdbg_stamp(kdbg, it, 3, 0);
+  for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) dst[i] = src[i];
+  __syncthreads();
+  kdbg_stamp(kdbg, it, 3, 1);
+}
+
+void launch_rccl_standin(const int64_t* src, int64_t* dst, int64_t n, int wgs, uint64_t* kdbg, int it,
+                         hipStream_t s) {
+  if (n <= 0 || wgs <= 0) return;
+  TWTML_LAUNCH(k_rccl_standin, dim3(wgs), dim3(256), 0, s, src, dst, n, kdbg, it);
 }
 
 void launch_sgd_finish(const DevSgd& d, const SgdParams& sp, hipStream_t s) {

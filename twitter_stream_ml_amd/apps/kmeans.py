@@ -78,8 +78,10 @@ def build_kmeans_engine(args, dim: int, rank: int, world: int):
         share_host_threads(dev, rank, int(os.environ.get("LOCAL_WORLD_SIZE", world)),
                            max(1, torch.cuda.device_count()))
         rows = max(65536, args.batchSize)
+        from .linear_regression import DRIVER_RAW_SLOTS   # sized from the scheduler's prefetch depth
         cfg = KMDeviceConfig(k=args.k, text_dims=args.textDims, half_life=args.halfLife,
-                             max_rows=rows, max_units=rows * 290, seed=args.seed)
+                             max_rows=rows, max_units=rows * 290, seed=args.seed,
+                             raw_slots=int(os.environ.get("TWTML_RAW_SLOTS", "0") or 0) or DRIVER_RAW_SLOTS)
         return DeviceKMeans(cfg, device=dev, comm=make_rccl_comm(dev) if world > 1 else None)
     from ..parallel.dist import allreduce_fn
     return CpuKMeans(args.k, dim, half_life=args.halfLife, init_weight=0.0, seed=args.seed,

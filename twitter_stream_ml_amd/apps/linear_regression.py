@@ -58,6 +58,13 @@ log = logging.getLogger("com.giorgioinf.twtml.spark.LinearRegression")
 APP_NAME = "twitter-stream-ml-linear-regression"
 
 
+# The streaming scheduler offers at most this many sealed batches to the
+# engine's prefetch (runtime/streaming.py prefetch_depth): one slot trains, one
+# is the free slot a batch without a prefetch takes, the rest hold prefetches.
+DRIVER_PREFETCH_DEPTH = 2
+DRIVER_RAW_SLOTS = DRIVER_PREFETCH_DEPTH + 2
+
+
 def build_engine(conf: ConfArguments, rank: int, world: int, device: Optional[int] = None,
                  max_rows: int = 0):
     """CPU (local[N]) or MI355X (rocm...) engine for this process."""
@@ -85,12 +92,11 @@ def build_engine(conf: ConfArguments, rank: int, world: int, device: Optional[in
                                   num_iterations=conf.numIterations, fraction=conf.miniBatchFraction,
                                   begin=conf.numRetweetBegin, end=conf.numRetweetEnd,
                                   max_rows=rows, max_units=rows * 290, ingest="utf8",
-                                  # 4 device raw slots (TWTML_RAW_SLOTS overrides): the driver
-                                  # prefetches only the batches its scheduler has sealed, and
-                                  # latency matters more here than the bench's 8-slot run-ahead
-                                  # (tests/test_gpu_checkpoint.py p99 failed at 8); the HBM
-                                  # sizing counts 4 slots' bytes
-                                  raw_slots=int(os.environ.get("TWTML_RAW_SLOTS", "0") or 0) or 4)
+                                  # device raw slots (TWTML_RAW_SLOTS overrides): the driver
+                                  # prefetches only the batches its scheduler has sealed (at most
+                                  # DRIVER_PREFETCH_DEPTH), so it never uses more than that + 2;
+                                  # the HBM sizing counts these slots' bytes
+                                  raw_slots=int(os.environ.get("TWTML_RAW_SLOTS", "0") or 0) or DRIVER_RAW_SLOTS)
 
         rows = max_rows or max(65536, int(conf.batchSize or 0))
         if cap.lower() == "hbm":   # the largest micro-batch 80 % of this GPU's free HBM holds

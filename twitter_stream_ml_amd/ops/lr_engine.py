@@ -96,9 +96,10 @@ class LRDeviceConfig:
     comm_timing: bool = False
     # device raw-batch slots: the copy engine runs up to raw_slots - 1
     # batches ahead of the one training (0: TWTML_RAW_SLOTS or the engine
-    # default, 8).  Deeper buffering lets the H2D of later batches proceed
+    # default, 6).  Deeper buffering lets the H2D of later batches proceed
     # while young-model batches (many GD iterations) keep the GPU busy, at
-    # the cost of queueing latency.
+    # the cost of queueing latency (profiles/r6/raw_slots_sweep.txt: 6 is
+    # the knee of tweets/s vs p50 on the headline bench).
     raw_slots: int = 0
 
     def as_dict(self) -> Dict[str, object]:
