@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 
 #include "common.h"
@@ -207,17 +208,19 @@ __global__ __launch_bounds__(1024) void k_code_tag(DevPrepared p, int64_t n_uniq
 //           (narrow_text.h) instead of reading idx
 //   far     (TIERED) entries of far slots go to the chunk's far list
 //           (row << 28 | slot, at cbase * 512 ..) and count into fhist
-template <bool TIERED>
-__global__ __launch_bounds__(kSplitWaves * kWave) void k_remap_hybrid(DevPrepared p, int64_t ns,
+// NW waves per workgroup (the code table is loaded once per workgroup): 4,
+// or 8 with a 6-waves-per-SIMD register budget (TWTML_REMAP_WAVES=8, A/B)
+template <bool TIERED, int NW>
+__global__ __launch_bounds__(NW * kWave) __attribute__((amdgpu_waves_per_eu(NW == 8 ? 6 : 1))) void k_remap_hybrid(DevPrepared p, int64_t ns,
                                                                       int64_t pad_base,
                                                                       const uint16_t* code,
                                                                       DevRawBatch rb, FeaturizeParams fp,
                                                                       int from_text) {
   __shared__ uint16_t lcode[kCodeIds];
-  __shared__ uint32_t cnt[kSplitWaves][kRowsPerChunk * kCntStride];
-  __shared__ uint32_t ccnt[kSplitWaves][kRowsPerChunk];
-  __shared__ uint32_t fcnt[kSplitWaves];
-  for (int i = threadIdx.x; i < kCodeIds / 8; i += kSplitWaves * kWave)
+  __shared__ uint32_t cnt[NW][kRowsPerChunk * kCntStride];
+  __shared__ uint32_t ccnt[NW][kRowsPerChunk];
+  __shared__ uint32_t fcnt[NW];
+  for (int i = threadIdx.x; i < kCodeIds / 8; i += NW * kWave)
     reinterpret_cast<uint4*>(lcode)[i] = reinterpret_cast<const uint4*>(code)[i];
   __syncthreads();
   const int lane = lane_id();
@@ -225,8 +228,8 @@ __global__ __launch_bounds__(kSplitWaves * kWave) void k_remap_hybrid(DevPrepare
   const int r = lane / kLanesPerRow, t = lane % kLanesPerRow;
   const int64_t n_kept = p.counters[0];
   const int64_t nch = (n_kept + kRowsPerChunk - 1) / kRowsPerChunk;
-  const int64_t wave = int64_t(blockIdx.x) * kSplitWaves + w;
-  const int64_t nwaves = int64_t(gridDim.x) * kSplitWaves;
+  const int64_t wave = int64_t(blockIdx.x) * NW + w;
+  const int64_t nwaves = int64_t(gridDim.x) * NW;
   uint32_t* cw = cnt[w];
   uint32_t* crow = cw + r * kCntStride;
   const uint32_t pad = uint32_t(pad_base + lane);
@@ -617,11 +620,19 @@ void launch_remap_slices(const DevPrepared& p, int64_t ns, int64_t pad_base, int
     f.c_lo = cmax * k / nsl;
     f.c_hi = cmax * (k + 1) / nsl;
     if (f.c_hi <= f.c_lo) continue;
-    int grid = int(std::min<int64_t>(int64_t(num_cu) * 4 * prep_grid_mult(TIERED ? 4 : 1),
-                                     (f.c_hi - f.c_lo + kSplitWaves - 1) / kSplitWaves));
+    static const int nw = [] {
+      const char* e = std::getenv("TWTML_REMAP_WAVES");
+      return e && std::atoi(e) == 8 ? 8 : kSplitWaves;
+    }();
+    int grid = int(std::min<int64_t>(int64_t(num_cu) * 4 * prep_grid_mult(TIERED ? 4 : 1) * kSplitWaves / nw,
+                                     (f.c_hi - f.c_lo + nw - 1) / nw));
     if (grid < 1) grid = 1;
-    TWTML_LAUNCH(k_remap_hybrid<TIERED>, dim3(grid), dim3(kSplitWaves * kWave), 0, s, p, ns, pad_base,
-                       p.code, b, f, from_text ? 1 : 0);
+    if (nw == 8)
+      TWTML_LAUNCH((k_remap_hybrid<TIERED, 8>), dim3(grid), dim3(8 * kWave), 0, s, p, ns, pad_base, p.code, b, f,
+                   from_text ? 1 : 0);
+    else
+      TWTML_LAUNCH((k_remap_hybrid<TIERED, kSplitWaves>), dim3(grid), dim3(kSplitWaves * kWave), 0, s, p, ns,
+                   pad_base, p.code, b, f, from_text ? 1 : 0);
   }
 }
 
