@@ -50,7 +50,12 @@ import time
 import numpy as np
 
 T_START = time.time()
-BASELINE_TWEETS_PER_SEC = None  # the reference publishes no number
+# The reference publishes no number, so vs_baseline is against
+# BASELINE.json config 1 measured here: the reference's own mode, --master
+# local[2] (fp64 CPU engine, MLlib semantics) on the same wide synthetic data,
+# on a GPU box's host CPU -- profiles/r6/config1_local2.json
+# (python bench.py --master 'local[2]' --steps 20 --warmup 5).
+BASELINE_TWEETS_PER_SEC = 119353.4
 
 
 def parse_args(argv=None):
@@ -409,7 +414,7 @@ def run_cpu_local(args) -> int:
         "ms_per_step": round((t1 - t0) / args.steps * 1e3, 3),
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": 1.0,
+        "vs_baseline": round(value / BASELINE_TWEETS_PER_SEC, 3),
         "dtype": "fp64",
         "data": (f"synthetic tweet-shaped records (seeded C++ generator, "
                  f"{'realistic 50K-word multi-script' if args.profile == 'wide' else 'toy ~300-word'} vocabulary, "
@@ -441,7 +446,7 @@ def run_cpu_local(args) -> int:
 
 def main(argv=None) -> int:
     args = parse_args(argv)
-    if args.master.startswith("local"):
+    if args.master:   # config 1: the CPU engine (local[N] only)
         return run_cpu_local(args)
     args.e2e = not args.prepacked
     import torch  # noqa: F401  (binds the HIP runtime before the engine loads)
@@ -592,7 +597,9 @@ def main(argv=None) -> int:
         "ms_per_step": round(ms, 3),
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": (value / BASELINE_TWEETS_PER_SEC) if BASELINE_TWEETS_PER_SEC else None,
+        # against config 1 (the LR model on the CPU, local[2]); k-means has no CPU line
+        "vs_baseline": (round(value / BASELINE_TWEETS_PER_SEC, 1)
+                        if BASELINE_TWEETS_PER_SEC and not is_km else None),
         "dtype": "fp32",
     }
     if is_km:
@@ -622,6 +629,10 @@ def main(argv=None) -> int:
             out["active_features"] = int(np.mean([e[1] for e in runner.extra]))
             out["lds_tier_features"] = int(runner.extra[-1][2])
     out["p50_microbatch_latency_ms"] = round(p50, 3)
+    if out["vs_baseline"] is not None:
+        out["baseline"] = {"config": "BASELINE.json config 1: --master local[2] CPU (fp64 MLlib-semantics engine), "
+                                     "same synthetic data, 50K-tweet batches",
+                           "tweets_per_sec": BASELINE_TWEETS_PER_SEC, "source": "profiles/r6/config1_local2.json"}
     out["trained_tweets_per_step"] = round(tweets / args.steps, 1)
     out["ingest"] = (f"e2e-{ingest}: host staging of every batch in the timed region"
                      if args.e2e else "device pipeline: pre-packed wire pool, H2D in the timed region")
