@@ -310,8 +310,8 @@ constexpr int kKdbgKinds = 4;
 // Iteration record i: [0] updates so far, [1] m, [2] update workgroups,
 // [3] K, [4] S, [5] L, [6..9] N_0..N_3 (fixed-point exponents of iteration
 // i, written by its gradient kernel), [10] |r| bound B, [11] scales invalid
-// (diverged); [kRecHead + 3w] ||dw||^2, ||w||^2 and max |w_text| partials of
-// update workgroup w.
+// (diverged); [kRecHead + c kMaxUpdGrid + w] the ||dw||^2 (c = 0), ||w||^2
+// (c = 1) and max |w_text| (c = 2) partials of update workgroup w.
 constexpr int kMaxUpdGrid = 1024;   // update workgroups: near column tiles + far slot ranges
 constexpr int kRecHead = 16;
 constexpr int kRecStride = kRecHead + 3 * kMaxUpdGrid;

@@ -243,21 +243,48 @@ __device__ __forceinline__ int upd_grid(const DevSgd& d) {
   return u.nt + u.nf;
 }
 
+// The update writes its per-workgroup partials (sum step^2, sum w^2, max |w|)
+// as three arrays of kMaxUpdGrid (rec_part): one wave reads them 512 B per
+// load instruction.
+__device__ __forceinline__ int rec_part(int c, int k) { return kRecHead + c * kMaxUpdGrid + k; }
+
+// Every load is issued before the first add: kConvU partials per lane and
+// array in flight, the record head and the norm state too (a loop that
+// waited on each step's loads made the iteration prologue ~14 dependent L2
+// round trips, 5.9 us per iteration kernel: profiles/r6/ablate_iter.txt).
+// The per-lane sums add the partials in increasing k, as before.
+constexpr int kConvU = 8;
+
 __device__ bool sgd_converged_wave(const DevSgd& d, int it, double tol, double* maxw_out = nullptr) {
   const double* rec = sgd_rec(d, it);
   const int nw = upd_grid(d);   // (rec[2] holds the same; reading it first cost a dependent round trip)
+  const double r0 = rec[0], r1 = rec[1], st4 = d.state[4], st6 = d.state[6];
   double ds = 0.0, ws = 0.0, mx = 0.0;
-  for (int k = lane_id(); k < nw; k += kWave) {
-    ds += rec[kRecHead + 3 * k];
-    ws += rec[kRecHead + 3 * k + 1];
-    mx = fmax(mx, rec[kRecHead + 3 * k + 2]);
+  for (int k0 = lane_id(); k0 < nw; k0 += kWave * kConvU) {
+    double a[kConvU], b[kConvU], c[kConvU];
+#pragma unroll
+    for (int u = 0; u < kConvU; ++u) {
+      const int k = k0 + u * kWave;
+      const bool ok = k < nw;
+      a[u] = ok ? rec[rec_part(0, k)] : 0.0;
+      b[u] = ok ? rec[rec_part(1, k)] : 0.0;
+      c[u] = ok ? rec[rec_part(2, k)] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kConvU; ++u) {
+      if (k0 + u * kWave < nw) {
+        ds += a[u];
+        ws += b[u];
+        mx = fmax(mx, c[u]);
+      }
+    }
   }
   ds = wave_sum(ds);
   ws = wave_sum(ws);
   mx = wave_max(mx);
   if (maxw_out) *maxw_out = mx;
-  if (!(rec[1] > 0.0) || rec[0] < 2.0) return false;   // no update this iteration / first update
-  double rest = d.state[4] - d.state[6];
+  if (!(r1 > 0.0) || r0 < 2.0) return false;   // no update this iteration / first update
+  double rest = st4 - st6;
   if (rest < 0.0) rest = 0.0;
   const double wnorm = sqrt(ws + rest);
   return sqrt(ds) < tol * (wnorm > 1.0 ? wnorm : 1.0);
@@ -860,14 +887,27 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
   part_scalars<STATS>(d, 0, 0, acc, hsum + kHot, wsc, prow);   // includes the block barrier
   if (tst) tst[5] = __builtin_amdgcn_s_memrealtime();
   const int64_t hi = d.far_base;            // pads (and far slots) are never flushed
-  for (int64_t s = kNumNumeric + threadIdx.x; s < ns; s += kIterBlock) {
-    int64_t v = 0;
-    if (s < hi) {
-      v = part_slot<REP>(gl, s);
-      const uint32_t h = p.hot_of[s];
-      if (h != 0xFFu) v += (long long)hsum[h];
+  // kFlushU slots per thread per step: their hot_of loads are all in flight
+  // before the first LDS read (one L2 round trip per step, not per slot)
+  constexpr int kFlushU = 4;
+  for (int64_t s0 = kNumNumeric + threadIdx.x; s0 < ns; s0 += int64_t(kIterBlock) * kFlushU) {
+    uint32_t h[kFlushU];
+#pragma unroll
+    for (int u = 0; u < kFlushU; ++u) {
+      const int64_t s = s0 + int64_t(u) * kIterBlock;
+      h[u] = s < hi ? uint32_t(p.hot_of[s]) : 0xFFu;
     }
-    prow[s] = v;
+#pragma unroll
+    for (int u = 0; u < kFlushU; ++u) {
+      const int64_t s = s0 + int64_t(u) * kIterBlock;
+      if (s >= ns) break;
+      int64_t v = 0;
+      if (s < hi) {
+        v = part_slot<REP>(gl, s);
+        if (h[u] != 0xFFu) v += (long long)hsum[h[u]];
+      }
+      prow[s] = v;
+    }
   }
 }
 
@@ -880,15 +920,28 @@ __device__ __forceinline__ void hyb_lds_init(const DevPrepared& p, const float* 
                                              uint32_t* whl, unsigned long long* hsum, uint32_t* wctr) {
   if (threadIdx.x == 0) *wctr = 0u;
   // 16-byte LDS stores (ns is a multiple of 64; wl and gl are 16-B aligned):
-  // 4 weights and 2 gradient words per store instead of one
-  for (int64_t s4 = threadIdx.x; s4 < ns / 4; s4 += kIterBlock) {
-    const int64_t s = 4 * s4;
-    const float4 wv = *reinterpret_cast<const float4*>(wsrc + s);
-    const float wf[4] = {wv.x, wv.y, wv.z, wv.w};
-    int32_t o[4];
+  // 4 weights and 2 gradient words per store instead of one; kInitU float4
+  // loads per thread in flight before the first store (the tiered near tier
+  // is ~3.3 float4 per thread: one L2 round trip instead of four)
+  constexpr int kInitU = 4;
+  for (int64_t q0 = threadIdx.x; q0 < ns / 4; q0 += int64_t(kIterBlock) * kInitU) {
+    float4 wv[kInitU];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) o[k] = (s + k >= kNumNumeric && s + k < hi) ? w_to_fix(wf[k], wscale) : 0;
-    reinterpret_cast<int4*>(wl)[s4] = make_int4(o[0], o[1], o[2], o[3]);
+    for (int u = 0; u < kInitU; ++u) {
+      const int64_t s4 = q0 + int64_t(u) * kIterBlock;
+      wv[u] = s4 < ns / 4 ? *reinterpret_cast<const float4*>(wsrc + 4 * s4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < kInitU; ++u) {
+      const int64_t s4 = q0 + int64_t(u) * kIterBlock;
+      if (s4 >= ns / 4) break;
+      const int64_t s = 4 * s4;
+      const float wf[4] = {wv[u].x, wv[u].y, wv[u].z, wv[u].w};
+      int32_t o[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = (s + k >= kNumNumeric && s + k < hi) ? w_to_fix(wf[k], wscale) : 0;
+      reinterpret_cast<int4*>(wl)[s4] = make_int4(o[0], o[1], o[2], o[3]);
+    }
   }
   for (int64_t s2 = threadIdx.x; s2 < ns * REP / 2; s2 += kIterBlock)
     reinterpret_cast<uint4*>(gl)[s2] = make_uint4(0u, 0u, 0u, 0u);
@@ -1313,7 +1366,7 @@ __global__ __launch_bounds__(kUpdThreads) void k_sgd_update(DevSgd d, SgdParams 
   if (tid < 3) {
     double t = 0.0;
     for (int k = 0; k < kUpdWaves; ++k) t = tid < 2 ? t + wsc[k][tid] : fmax(t, wsc[k][tid]);
-    rec[kRecHead + 3 * blockIdx.x + tid] = t;
+    rec[rec_part(tid, int(blockIdx.x))] = t;
   }
   if (blockIdx.x == 0 && tid == 0) {
     const double nupd = (it > 1 ? sgd_rec(d, it - 1)[0] : 0.0) + (m > 0.0 ? 1.0 : 0.0);
