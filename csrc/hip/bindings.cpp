@@ -235,6 +235,11 @@ PYBIND11_MODULE(_twtml_hip, m) {
         auto& h = self.cast<HostBatch&>();
         return view<int64_t>(h.scalars, {py::ssize_t(5 * h.max_rows)}, self);
       })
+      .def_property_readonly("spack_bytes", [](py::object self) {   // the packed scalar columns (tests)
+        auto& h = self.cast<HostBatch&>();
+        const size_t cap = static_cast<const uint8_t*>(h.base) + h.bytes - h.spack;
+        return view<uint8_t>(h.spack, {py::ssize_t(cap)}, self);
+      })
       .def("pack_rows", [](HostBatch& h, int64_t n) {
         py::gil_scoped_release nogil;
         return h.pack_rows(n);
@@ -247,38 +252,56 @@ PYBIND11_MODULE(_twtml_hip, m) {
       .def("load_utf16",
            [](HostBatch& h, py::array_t<uint16_t, py::array::c_style> text,
               py::array_t<int64_t, py::array::c_style> offsets, py::array_t<uint8_t, py::array::c_style> is_rt,
-              py::array_t<int64_t, py::array::c_style> scalars, bool copy_text, int threads) {
+              py::array_t<int64_t, py::array::c_style> scalars, bool copy_text, int threads,
+              py::object range) {
              const int64_t n = int64_t(offsets.size()) - 1;
              if (n < 0 || is_rt.size() < n || scalars.size() < 5 * n)
                throw std::invalid_argument("load_utf16: offsets / is_rt / scalars mismatch");
              if (n > 0 && offsets.data()[n] > text.size()) throw std::invalid_argument("offsets exceed text");
+             std::vector<int64_t> rng;   // optional [lo 0..4 | hi 0..4] from the receiver
+             if (!range.is_none()) {
+               auto r = range.cast<py::array_t<int64_t, py::array::c_style | py::array::forcecast>>();
+               if (r.size() != 2 * kScalarCols) throw std::invalid_argument("range: 10 int64 (lo[5], hi[5])");
+               rng.assign(r.data(), r.data() + 2 * kScalarCols);
+             }
              py::gil_scoped_release nogil;
-             h.load_utf16(text.data(), offsets.data(), is_rt.data(), scalars.data(), n, copy_text, threads);
+             h.load_utf16(text.data(), offsets.data(), is_rt.data(), scalars.data(), n, copy_text, threads,
+                         rng.empty() ? nullptr : rng.data());
              return n > 0 ? 2 * offsets.data()[n] : int64_t(0);
            },
            py::arg("text"), py::arg("offsets"), py::arg("is_rt"), py::arg("scalars"),
-           py::arg("copy_text") = true, py::arg("threads") = 0,
+           py::arg("copy_text") = true, py::arg("threads") = 0, py::arg("range") = py::none(),
            "Stage a raw UTF-16 batch (row words, offsets, packed scalars; text copied only if "
            "copy_text); returns the text bytes.")
       .def("load_utf8",
            [](HostBatch& h, py::array_t<uint8_t, py::array::c_style> text,
               py::array_t<int64_t, py::array::c_style> offsets, py::array_t<uint8_t, py::array::c_style> is_rt,
-              py::array_t<int64_t, py::array::c_style> scalars, bool copy_text, int threads) {
+              py::array_t<int64_t, py::array::c_style> scalars, bool copy_text, int threads,
+              py::object range) {
              const int64_t n = int64_t(offsets.size()) - 1;
              if (n < 0 || is_rt.size() < n || scalars.size() < 5 * n)
                throw std::invalid_argument("load_utf8: offsets / is_rt / scalars mismatch");
              if (n > 0 && offsets.data()[n] > text.size()) throw std::invalid_argument("offsets exceed text");
+             std::vector<int64_t> rng;   // optional [lo 0..4 | hi 0..4] from the receiver
+             if (!range.is_none()) {
+               auto r = range.cast<py::array_t<int64_t, py::array::c_style | py::array::forcecast>>();
+               if (r.size() != 2 * kScalarCols) throw std::invalid_argument("range: 10 int64 (lo[5], hi[5])");
+               rng.assign(r.data(), r.data() + 2 * kScalarCols);
+             }
              py::gil_scoped_release nogil;
-             h.load_utf8(text.data(), offsets.data(), is_rt.data(), scalars.data(), n, copy_text, threads);
+             h.load_utf8(text.data(), offsets.data(), is_rt.data(), scalars.data(), n, copy_text, threads,
+                         rng.empty() ? nullptr : rng.data());
              return n > 0 ? offsets.data()[n] : int64_t(0);
            },
            py::arg("text"), py::arg("offsets"), py::arg("is_rt"), py::arg("scalars"),
-           py::arg("copy_text") = true, py::arg("threads") = 0,
+           py::arg("copy_text") = true, py::arg("threads") = 0, py::arg("range") = py::none(),
            "Stage a raw UTF-8 batch (row words, offsets, packed scalars; text copied only if "
            "copy_text); returns the text bytes.")
       .def_readonly("utf16", &HostBatch::utf16)
       .def_readonly("utf8", &HostBatch::utf8)
       .def_readonly("rowpacked_n", &HostBatch::rowpacked_n)
+      .def_readonly("range_hits", &HostBatch::range_hits)
+      .def_readonly("range_misses", &HostBatch::range_misses)
       .def_readonly("wide_rows", &HostBatch::wide_rows)
       .def_property_readonly("scalar_wire", [](const HostBatch& h) {
         py::dict d;   // wire encoding of the last pack_scalars (tests / diagnostics)

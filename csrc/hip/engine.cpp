@@ -41,7 +41,7 @@ HostBatch::HostBatch(int64_t rows, int64_t text_bytes) : max_rows(rows), max_byt
   offsets[0] = 0;
 }
 
-void HostBatch::pack_scalars(int64_t n, const int64_t* src) {
+void HostBatch::pack_scalars(int64_t n, const int64_t* src, const int64_t* range) {
   if (n < 0 || n > max_rows) throw std::invalid_argument("pack_scalars: bad row count");
   if (!src) src = scalars;
   int64_t lo[kScalarCols], hi[kScalarCols];
@@ -53,7 +53,16 @@ void HostBatch::pack_scalars(int64_t n, const int64_t* src) {
   const int64_t part = std::max<int64_t>(32, (n / per_col + 31) / 32 * 32);
   const int nparts = int(std::max<int64_t>(1, (n + part - 1) / part));
   std::vector<int64_t> plo(size_t(ncols) * nparts), phi(size_t(ncols) * nparts);
-  pool.run(ncols * nparts, [&](int task) {
+  if (range && n > 0) {   // the receiver's bounds: one pass (checked while packing)
+    for (int c = 0; c < ncols; ++c) {
+      plo[size_t(c) * nparts] = range[c];
+      phi[size_t(c) * nparts] = range[kScalarCols + c];
+      for (int k = 1; k < nparts; ++k) {
+        plo[size_t(c) * nparts + k] = range[c];
+        phi[size_t(c) * nparts + k] = range[kScalarCols + c];
+      }
+    }
+  } else pool.run(ncols * nparts, [&](int task) {
     const int c = task / nparts;
     const int64_t i0 = int64_t(task % nparts) * part, i1 = std::min(n, i0 + part);
     const int64_t* v = src + int64_t(c) * n;
@@ -86,22 +95,25 @@ void HostBatch::pack_scalars(int64_t n, const int64_t* src) {
     soff[c + 1] = soff[c] + ((cb + 7) & ~int64_t(7));   // columns 8-B aligned
   }
   // rows [i0, i1) of column c; chunk boundaries are multiples of 32 rows, so
-  // chunks own whole 32-bit words of the stream
-  auto put = [&](int c, int64_t i0, int64_t i1) {
+  // chunks own whole 32-bit words of the stream.  Returns false if a value
+  // lies outside the column's encoding (a range hint that does not hold).
+  auto put = [&](int c, int64_t i0, int64_t i1) -> bool {
     const int64_t* v = src + int64_t(c) * n;
     uint8_t* o = spack + soff[c];
     const int bits = sw[c];
     if (bits == 64) {
       std::memcpy(o + 8 * i0, v + i0, sizeof(int64_t) * size_t(i1 - i0));
-      return;
+      return true;
     }
     // word-at-a-time writer: the chunk starts on a word boundary
     uint32_t* out = reinterpret_cast<uint32_t*>(o) + ((i0 * bits) >> 5);
     const uint64_t b = uint64_t(sbase[c]);
-    uint64_t acc = 0;
+    uint64_t acc = 0, over = 0;
     int nb = 0;
     for (int64_t i = i0; i < i1; ++i) {
-      acc |= (uint64_t(v[i]) - b) << nb;
+      const uint64_t x = uint64_t(v[i]) - b;
+      over |= x >> bits;   // bits < 64 here
+      acc |= x << nb;
       nb += bits;
       if (nb >= 32) {
         *out++ = uint32_t(acc);
@@ -112,12 +124,24 @@ void HostBatch::pack_scalars(int64_t n, const int64_t* src) {
     if (nb > 0) *out++ = uint32_t(acc);
     if (i1 == n)   // the column's slack words
       for (uint32_t* end = reinterpret_cast<uint32_t*>(o + (soff[c + 1] - soff[c])); out < end;) *out++ = 0u;
+    return over == 0;
   };
+  std::vector<uint8_t> fits(size_t(ncols) * nparts, 1);
   pool.run(ncols * nparts, [&](int task) {
     const int c = task / nparts;
     const int64_t i0 = int64_t(task % nparts) * part;
-    put(c, i0, std::min(n, i0 + part));
+    fits[size_t(task)] = put(c, i0, std::min(n, i0 + part)) ? 1 : 0;
   });
+  if (range && n > 0) {
+    bool ok = true;
+    for (auto f : fits) ok = ok && f;
+    if (!ok) {   // the hint did not hold: the exact two-pass encoding
+      ++range_misses;
+      pack_scalars(n, src, nullptr);
+      return;
+    }
+    ++range_hits;
+  }
   spacked_n = n;
   spacked_cols = ncols;
 }
@@ -149,7 +173,8 @@ bool HostBatch::pack_rows(int64_t n) {
 // `scale` is the bytes per offset unit (2: UTF-16 units, 1: UTF-8 bytes),
 // `row_flags` the wire flags every row carries besides the retweet bit.
 void HostBatch::load_raw(const uint8_t* t, const int64_t* uoff, int64_t scale, uint8_t row_flags,
-                         const uint8_t* is_rt, const int64_t* sc, int64_t n, bool copy_text, int threads) {
+                         const uint8_t* is_rt, const int64_t* sc, int64_t n, bool copy_text, int threads,
+                         const int64_t* range) {
   if (n < 0 || n > max_rows) throw std::invalid_argument("load: bad row count");
   const int64_t bytes = n > 0 ? scale * (uoff[n] - uoff[0]) : 0;
   if (copy_text && bytes > max_bytes) throw std::invalid_argument("load: text exceeds staging capacity");
@@ -191,14 +216,14 @@ void HostBatch::load_raw(const uint8_t* t, const int64_t* uoff, int64_t scale, u
   if (!copy_text && !all) pool.run(T, [&](int c) { host_rows(n * c / T, n * (c + 1) / T); });
   offsets[0] = 0;
   offsets[n] = scale * uoff[n];
-  pack_scalars(n, sc);
+  pack_scalars(n, sc, range);
   rows_scanned_n = n;
   if (all) rowpacked_n = n;
 }
 
 void HostBatch::load_utf16(const uint16_t* t, const int64_t* uoff, const uint8_t* is_rt, const int64_t* sc,
-                           int64_t n, bool copy_text, int threads) {
-  load_raw(reinterpret_cast<const uint8_t*>(t), uoff, 2, kRowWide, is_rt, sc, n, copy_text, threads);
+                           int64_t n, bool copy_text, int threads, const int64_t* range) {
+  load_raw(reinterpret_cast<const uint8_t*>(t), uoff, 2, kRowWide, is_rt, sc, n, copy_text, threads, range);
   cesu_rows = 0;
   wide_rows = n;
   utf16 = true;
@@ -209,8 +234,8 @@ void HostBatch::load_utf16(const uint16_t* t, const int64_t* uoff, const uint8_t
 // device decoder handles UTF-8, incl. 4-byte sequences); the device keeps
 // ASCII rows as they are and narrows decoded Latin-1 rows.
 void HostBatch::load_utf8(const uint8_t* t, const int64_t* boff, const uint8_t* is_rt, const int64_t* sc,
-                          int64_t n, bool copy_text, int threads) {
-  load_raw(t, boff, 1, kRowCesu, is_rt, sc, n, copy_text, threads);
+                          int64_t n, bool copy_text, int threads, const int64_t* range) {
+  load_raw(t, boff, 1, kRowCesu, is_rt, sc, n, copy_text, threads, range);
   cesu_rows = n;
   wide_rows = 0;
   utf16 = false;

@@ -92,23 +92,29 @@ struct HostBatch {
   bool utf8 = false;                   // text is UTF-8 (load_utf8): the device decodes non-ASCII
                                        // rows and narrows the Latin-1 ones
   int64_t rows_scanned_n = -1;         // rows of the last pack_rows call (fit or not)
+  int64_t range_hits = 0, range_misses = 0;   // pack_scalars with a range hint: one pass / fell back
   int64_t max_rows = 0, max_bytes = 0;
   HostBatch(int64_t rows, int64_t text_bytes);
   ~HostBatch();
   // Encode scalars[:, :n] (or src [5][n]) into spack (one thread per column).
-  void pack_scalars(int64_t n, const int64_t* src = nullptr);
+  // range: optional [lo 0..4 | hi 0..4] column bounds the receiver recorded
+  // while sealing the batch: the encoding is chosen from them and the packing
+  // pass checks every value against them (one pass over the scalars instead
+  // of a min/max pass plus a packing pass); a value outside falls back to
+  // the two-pass encoding, so a wrong hint costs time, never correctness.
+  void pack_scalars(int64_t n, const int64_t* src = nullptr, const int64_t* range = nullptr);
   // Raw UTF-16 ingest: row words / offsets / flags for `n` rows of UTF-16
   // text with unit offsets uoff [n+1], scalars from sc [5][n]; the text is
   // copied into `text` only if copy_text (else it is DMA'd from the caller's
   // registered buffer by submit).  No per-unit host work besides the copy:
   // the device narrows Latin-1 rows and lowers special rows (rows.hip).
   void load_utf16(const uint16_t* t, const int64_t* uoff, const uint8_t* is_rt, const int64_t* sc,
-                  int64_t n, bool copy_text, int threads);
+                  int64_t n, bool copy_text, int threads, const int64_t* range = nullptr);
   // Raw UTF-8 ingest (the bytes the network delivers): same contract with
   // byte offsets boff [n+1].  ~1.1 B per unit of tweet text on PCIe and no
   // per-byte host work: the device decodes (k_cesu_decode) and narrows.
   void load_utf8(const uint8_t* t, const int64_t* boff, const uint8_t* is_rt, const int64_t* sc,
-                 int64_t n, bool copy_text, int threads);
+                 int64_t n, bool copy_text, int threads, const int64_t* range = nullptr);
   // Offsets + flags of rows [0, n) as one u16 per row (the device rebuilds
   // both with a scan): 9 -> 2 bytes per row on PCIe.  False (and the batch
   // ships offsets + flags as before) if a row has >= 8192 wire bytes.
@@ -117,7 +123,7 @@ struct HostBatch {
 
  private:
   void load_raw(const uint8_t* t, const int64_t* off, int64_t scale, uint8_t row_flags, const uint8_t* is_rt,
-                const int64_t* sc, int64_t n, bool copy_text, int threads);
+                const int64_t* sc, int64_t n, bool copy_text, int threads, const int64_t* range);
 };
 
 // bytes of device text buffer for `units` UTF-16 units: all rows wide (2 B

@@ -221,7 +221,7 @@ class HostBatchView:
         sc = np.ascontiguousarray(raw.scalars, dtype=np.int64)
         self.bytes = int(self._hb.load_utf16(text, np.ascontiguousarray(raw.offsets, dtype=np.int64),
                                              np.ascontiguousarray(raw.is_retweet, dtype=np.uint8), sc,
-                                             bool(copy_text)))
+                                             bool(copy_text), range=raw.scalar_range))
         self.n, self.units, self.batch_time_ms = raw.n, raw.total_units, raw.batch_time_ms
         self.rows_packed = int(self._hb.rowpacked_n) == raw.n
         self.ext_text = 0 if copy_text else int(text.ctypes.data)
@@ -241,7 +241,7 @@ class HostBatchView:
         sc = np.ascontiguousarray(raw.scalars, dtype=np.int64)
         self.bytes = int(self._hb.load_utf8(u8.data, np.ascontiguousarray(u8.offsets, dtype=np.int64),
                                             np.ascontiguousarray(raw.is_retweet, dtype=np.uint8), sc,
-                                            bool(copy_text)))
+                                            bool(copy_text), range=raw.scalar_range))
         self.n, self.units, self.batch_time_ms = raw.n, raw.total_units, raw.batch_time_ms
         self.rows_packed = int(self._hb.rowpacked_n) == raw.n
         self.ext_text = 0 if copy_text else int(u8.data.ctypes.data)

@@ -78,6 +78,11 @@ class RawBatch:
     scalars: np.ndarray       # int64  [5, n]
     batch_time_ms: int = 0    # seal time ("now" for featurizeNumbers)
     utf8: Optional[Utf8Text] = None   # the receiver's UTF-8 bytes of the same text
+    # int64 [2, 5]: per-column min / max of ``scalars``, recorded by the
+    # receiver while it sealed the batch (:meth:`with_scalar_range`); the host
+    # staging encodes the wire columns from it in one pass and checks every
+    # value against it (a wrong range costs a second pass, never correctness)
+    scalar_range: Optional[np.ndarray] = None
 
     def __post_init__(self) -> None:
         self.text = np.ascontiguousarray(self.text, dtype=np.uint16)
@@ -116,6 +121,13 @@ class RawBatch:
     def with_time(self, batch_time_ms: int) -> "RawBatch":
         """Shallow copy (arrays shared) with another seal time."""
         return replace(self, batch_time_ms=int(batch_time_ms))
+
+    def with_scalar_range(self) -> "RawBatch":
+        """Record the per-column scalar bounds (what a receiver tracks while it
+        parses the records it seals into this batch)."""
+        if self.n:
+            self.scalar_range = np.stack([self.scalars.min(axis=1), self.scalars.max(axis=1)]).astype(np.int64)
+        return self
 
     @property
     def nbytes(self) -> int:
