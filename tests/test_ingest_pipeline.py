@@ -88,6 +88,62 @@ def test_drop_syncs_before_forgetting():
     assert e.pipe.hits == 0
 
 
+class DiscardEngine(FakeEngine):
+    """FakeEngine with the engine's discard hook (LREngine::discard)."""
+
+    def __init__(self, n_slots=4):
+        super().__init__(n_slots)
+        self.discarded = []
+        self.pipe = SlotPipeline(n_slots, self.stage, self.submit, self.sync, discard=self.discard)
+
+    def discard(self, slot):
+        assert slot in self.inflight, "discard of a slot that holds no batch"
+        self.inflight.discard(slot)
+        self.discarded.append(slot)
+
+
+def _batch(t, n=8):
+    import numpy as np
+    from twitter_stream_ml_amd.records.batch import RawBatch
+    return RawBatch(np.zeros(n * 3, np.uint16), np.arange(n + 1, dtype=np.int64) * 3, np.ones(n, np.uint8),
+                    np.zeros((5, n), np.int64), t)
+
+
+def test_prefetch_matches_copies_that_share_the_arrays():
+    """Round-5 verdict: a driver that prefetches pool[i].with_time(t) and
+    trains another with_time(t) copy of it must hit (the key is the batch's
+    content -- seal time, buffers -- not the Python object)."""
+    e = DiscardEngine(4)
+    pool = [_batch(0), _batch(0)]
+    nxt = pool[1].with_time(5000)
+    assert e.pipe.prefetch(nxt)
+    e.process(e.pipe.take(pool[1].with_time(5000)), nxt)
+    assert (e.pipe.hits, e.pipe.orphaned, e.pipe.in_flight) == (1, 0, 0)
+    # another seal time or other buffers are other batches
+    assert e.pipe.prefetch(pool[1].with_time(6000))
+    slot = e.pipe.take(pool[0].with_time(6000))
+    assert e.pipe.hits == 1 and e.pipe.in_flight == 1 and slot not in [s for _, s in e.pipe._inflight.values()]
+
+
+def test_skipped_prefetches_are_discarded_not_stranded():
+    """Entries prefetched before the batch a take matches can never be
+    trained in order: they go back to the engine (discard) and their slots
+    are reused; with the old id() keys they stayed pinned for the run."""
+    e = DiscardEngine(4)
+    b = [_batch(t * 1000) for t in range(12)]
+    assert e.pipe.prefetch(b[1]) and e.pipe.prefetch(b[2]) and e.pipe.prefetch(b[3])
+    e.train(b[0])                                   # not prefetched: the free slot
+    e.train(b[3])                                   # skips b[1], b[2]: orphans
+    assert e.pipe.orphaned == 2 and len(e.discarded) == 2
+    assert e.pipe.in_flight == 0
+    # every slot is usable again: three more prefetches fit
+    for u in b[4:7]:
+        assert e.pipe.prefetch(u)
+    for u in b[4:7]:
+        e.train(u)
+    assert e.pipe.prefetched == e.pipe.hits + e.pipe.orphaned + e.pipe.in_flight == 6
+
+
 def test_single_slot_pipeline_never_prefetches():
     e = FakeEngine(1)
     b = [object() for _ in range(3)]
