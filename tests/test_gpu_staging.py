@@ -34,9 +34,11 @@ def test_range_hint_gives_the_same_wire_columns(hip_module):
     pa, wa = _spack(a)
     pb, wb = _spack(b)
     assert wa == wb and np.array_equal(pa, pb)
-    # a hint that does not hold: the max of column 1 is understated
+    # a hint that does not hold: the min of column 1 is overstated (the true
+    # min lies below the encoding's base; an understated max that still fits
+    # the same bit width is a valid encoding and packs in one pass)
     bad = raw.scalar_range.copy()
-    bad[1, 1] = raw.scalars[1].max() - 1
+    bad[0, 1] = raw.scalars[1].min() + 1
     raw.scalar_range = bad
     b.load_utf8(raw, u8, copy_text=False)
     assert (b._hb.range_hits, b._hb.range_misses) == (1, 1)
