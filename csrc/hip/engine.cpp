@@ -1219,8 +1219,9 @@ void LREngine::discard(int slot) {
     b.error = nullptr;
   }
   raw_.release_slot(slot, pstream_);
-  raw_.wait_h2d(slot);   // the host staging buffer of the slot may be rewritten on return
   schedule_ahead_locked();
+  lk.unlock();           // (the copy stream does not depend on the prep thread)
+  raw_.wait_h2d(slot);   // the host staging buffer of the slot may be rewritten on return
 }
 
 BatchResult LREngine::process(int slot, int64_t now_ms, bool want_pred, int64_t plot_points) {
