@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <stdexcept>
 
 #include "../common/unicode_tables.h"
 #include "common.h"
@@ -508,7 +509,7 @@ constexpr int kDecWaves = 4;
 __global__ __launch_bounds__(kDecWaves * kWave) void k_cesu_decode(uint8_t* text, const int64_t* offsets,
                                                                    uint8_t* flags, int64_t n, int64_t tail,
                                                                    int64_t* rstart, int64_t* rend,
-                                                                   int64_t* stats) {
+                                                                   int64_t* stats, int32_t* special) {
   __shared__ __attribute__((aligned(16))) uint8_t stage[kDecWaves][kDecStage + 16];
   const int lane = lane_id();
   const int wv = threadIdx.x / kWave;
@@ -629,17 +630,28 @@ __global__ __launch_bounds__(kDecWaves * kWave) void k_cesu_decode(uint8_t* text
       rend[r] = s1;
       if (mine) flags[r] = fl;
     }
+    if (special) {   // the group's special rows onto the list (~0.3 % of rows: one atomic per wave that has any)
+      const bool sp = mine && (fl & kRowSpecial);
+      const uint64_t bm = __ballot(sp);
+      if (bm) {
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(reinterpret_cast<unsigned long long*>(&stats[2]), (unsigned long long)__popcll(bm));
+        base = (unsigned long long)bcast_lane64(int64_t(base), 0);
+        if (sp) special[int64_t(base) + __popcll(bm & lanes_below())] = int32_t(r);
+      }
+    }
   }
   if (stats && lane == 0 && n_nar) atomicAdd(reinterpret_cast<unsigned long long*>(&stats[1]), (unsigned long long)n_nar);
 }
 
 void launch_cesu_expand(uint8_t* text, const int64_t* offsets, uint8_t* flags, int64_t n, int64_t tail,
-                        int64_t* rstart, int64_t* rend, int64_t* stats, hipStream_t s) {
+                        int64_t* rstart, int64_t* rend, int64_t* stats, hipStream_t s, int32_t* special) {
+  if (special && !stats) throw std::invalid_argument("cesu_expand: the special-row list needs stats[2]");
   if (n <= 0) return;
   // one wave per 64-row group, 4 waves (48 KB of staging) per workgroup
   const int grid = int(std::min<int64_t>((n + kDecWaves * kWave - 1) / (kDecWaves * kWave), 4096));
   TWTML_LAUNCH(k_cesu_decode, dim3(grid), dim3(kDecWaves * kWave), 0, s, text, offsets, flags, n, tail,
-                     rstart, rend, stats);
+                     rstart, rend, stats, special);
 }
 
 // nnz[k] carries the row's bigram count in bits 0..29 and the wide (UTF-16

@@ -67,8 +67,11 @@ constexpr int kRowLenBits = 13;
 // for Latin-1 rows; ASCII rows stay in place.  Writes every row's start /
 // end offset; stats[1] (nullable) counts the rows decoded to narrow bytes.
 // text needs tail + 2 * bytes + 64.
+// special (nullable): the rows flagged kRowSpecial are appended to it, their
+// count in stats[2] (the list k_row_special walks, one wave per row).
 void launch_cesu_expand(uint8_t* text, const int64_t* offsets, uint8_t* flags, int64_t n, int64_t tail,
-                        int64_t* rstart, int64_t* rend, int64_t* stats, hipStream_t s);
+                        int64_t* rstart, int64_t* rend, int64_t* stats, hipStream_t s,
+                        int32_t* special = nullptr);
 // Rebuild offsets [n+1] (exclusive scan of the lengths) and flags [n] from
 // packed row words on `s`; tsum: scratch of ceil(n / 8192) int64.
 void launch_unpack_rows(const uint16_t* rowpack, int64_t n, int64_t* offsets, uint8_t* flags, int64_t* tsum,
@@ -78,6 +81,7 @@ void launch_unpack_rows(const uint16_t* rowpack, int64_t n, int64_t* offsets, ui
 struct DevCaseTables {
   const uint32_t* supp_lower = nullptr;    // [n_supp][2] astral code point -> lower case
   const uint32_t* case_ranges = nullptr;   // [n_ranges][3] lo, hi, class (1 ignorable, 2 cased)
+  const uint32_t* bmp_class = nullptr;     // [4096] the class of every BMP code point, 2 bits each
   int32_t n_supp = 0, n_ranges = 0;
 };
 void upload_case_tables(DevCaseTables* ct);
@@ -93,6 +97,12 @@ void launch_row_normalize(uint8_t* text, const int64_t* wire_off, const int64_t*
                           uint8_t* flags, int64_t* out_s, int64_t* out_e, int64_t n, int64_t tail,
                           int64_t lower_base, bool narrow, const DevCaseTables& ct, int64_t* stats,
                           hipStream_t s, bool flagged_only = false);
+// UTF-8 batches: the same for the decoder's list of kRowSpecial rows only
+// (stats[2] of them), one wave per row, every listed row at once.  The other
+// rows keep the extents and flags the decoder wrote (out_* alias cur_*).
+void launch_row_special(uint8_t* text, const int64_t* wire_off, int64_t* cur_s, int64_t* cur_e,
+                        uint8_t* flags, const int32_t* special, int64_t n, int64_t tail, int64_t lower_base,
+                        const DevCaseTables& ct, int64_t* stats, hipStream_t s);
 
 // Row r: byte offset, wide flag and length in UTF-16 units.
 struct RowText {

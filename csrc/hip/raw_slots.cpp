@@ -31,7 +31,8 @@ void RawSlots::init(int n_slots, int64_t max_rows, int64_t max_bytes) {
     // wire bytes of those rows); slack: featurize over-reads <= 80 B
     const size_t pre = (rowpack_prefix(max_rows) + 255) & ~size_t(255);
     s.text_base = slot_alloc<uint8_t>(pre + 5 * size_t(max_bytes) + 256);
-    s.nstats = slot_alloc<int64_t>(2);
+    s.nstats = slot_alloc<int64_t>(4);
+    s.special = slot_alloc<int32_t>(size_t(max_rows) + 1);
     s.text = s.text_base + pre;
     s.offsets = slot_alloc<int64_t>(size_t(max_rows) + 1);
     s.flags = slot_alloc<uint8_t>(size_t(max_rows));
@@ -55,6 +56,7 @@ void RawSlots::release() {
     if (s.rstart) (void)hipFree(s.rstart);
     if (s.rend) (void)hipFree(s.rend);
     if (s.nstats) (void)hipFree(s.nstats);
+    if (s.special) (void)hipFree(s.special);
     if (s.h2d_done) (void)hipEventDestroy(s.h2d_done);
     if (s.consumed) (void)hipEventDestroy(s.consumed);
     s = Slot{};
@@ -147,24 +149,37 @@ DevRawBatch RawSlots::acquire(int slot, hipStream_t compute) {
   b.oend = s.offsets + 1;
   b.flags = s.flags;
   const int64_t tail = (s.bytes + 15) / 16 * 16;
-  TWTML_HIP_CHECK(hipMemsetAsync(s.nstats, 0, 2 * sizeof(int64_t), compute));
+  TWTML_HIP_CHECK(hipMemsetAsync(s.nstats, 0, 4 * sizeof(int64_t), compute));
+  // UTF-8 batches: the decoder flags the candidate special rows (and narrows
+  // the Latin-1 ones itself) and lists them; only those are walked, one wave
+  // per row (launch_row_special).  TWTML_NORMALIZE_ALL=1 scans every wide
+  // row instead (A/B); TWTML_NORMALIZE_LIST=0 walks the flagged rows by
+  // 64-row group (the round-5 pass, A/B).
+  static const bool scan_all = [] {
+    const char* e = std::getenv("TWTML_NORMALIZE_ALL");
+    return e && e[0] == '1';
+  }();
+  static const bool by_list = [] {
+    const char* e = std::getenv("TWTML_NORMALIZE_LIST");
+    return !(e && e[0] == '0');
+  }();
+  const bool flagged_only = s.utf8 && !s.utf16 && s.cesu_rows > 0 && !scan_all;
+  const bool listed = flagged_only && by_list;
   if (s.cesu_rows > 0) {   // expand cesu / UTF-8 rows behind the wire bytes (16-byte aligned)
-    launch_cesu_expand(s.text, s.offsets, s.flags, s.n, tail, s.rstart, s.rend, s.nstats, compute);
+    launch_cesu_expand(s.text, s.offsets, s.flags, s.n, tail, s.rstart, s.rend, s.nstats, compute,
+                       listed ? s.special : nullptr);
     b.offsets = s.rstart;
     b.oend = s.rend;
   }
-  if (s.utf16 || s.cesu_rows > 0 || s.wide_rows > 0) {
+  const int64_t lower_base = tail + 2 * ((s.bytes + 15) / 16 * 16);
+  if (listed) {
+    launch_row_special(s.text, s.offsets, s.rstart, s.rend, s.flags, s.special, s.n, tail, lower_base, case_,
+                       s.nstats, compute);
+  } else if (s.utf16 || s.cesu_rows > 0 || s.wide_rows > 0) {
     // special rows -> fully lower-cased UTF-16; UTF-16 / UTF-8 batches: Latin-1
     // rows narrowed (a decoded UTF-8 row in place: byte i <- unit i, forward)
-    // UTF-8 batches: the decoder flagged the candidate special rows (and
-    // narrowed the Latin-1 ones itself), so only those are scanned
-    static const bool scan_all = [] {   // TWTML_NORMALIZE_ALL=1: scan every wide row (A/B)
-      const char* e = std::getenv("TWTML_NORMALIZE_ALL");
-      return e && e[0] == '1';
-    }();
     launch_row_normalize(s.text, s.offsets, b.offsets, b.oend, s.flags, s.rstart, s.rend, s.n, tail,
-                         tail + 2 * ((s.bytes + 15) / 16 * 16), s.utf16 || s.utf8, case_, s.nstats,
-                         compute, s.utf8 && !s.utf16 && s.cesu_rows > 0 && !scan_all);
+                         lower_base, s.utf16 || s.utf8, case_, s.nstats, compute, flagged_only);
     b.offsets = s.rstart;
     b.oend = s.rend;
   }

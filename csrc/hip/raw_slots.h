@@ -79,7 +79,8 @@ class RawSlots {
     int64_t* rstart = nullptr;        // cesu batches: row start / end after expansion
     int64_t* rend = nullptr;
     int64_t cesu_rows = 0, wide_rows = 0;
-    int64_t* nstats = nullptr;        // [2] rows lowered / narrowed by row_normalize
+    int64_t* nstats = nullptr;        // [4] rows lowered / narrowed by row_normalize, special-list length
+    int32_t* special = nullptr;       // UTF-8 batches: the decoder's kRowSpecial rows
     bool packed = false, utf16 = false, utf8 = false;
     int64_t soff[kScalarCols] = {};
     int64_t sbase[kScalarCols] = {};
