@@ -804,8 +804,14 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
     }
     if (L8c >= 0) {
       const uint16_t* sl = csl;
-      int32_t d0 = hot_dot(hv, wq), d1 = far;   // partial sums of the row's int32 dot
-      if (reg) {
+      // timing-only ablations (results meaningless): 12 no hot dot, 13 no
+      // cold forward, 14 no hot gradient, 11 no cold backward atomics
+      int32_t d0 = abl == 12 ? int32_t(hv.x) : hot_dot(hv, wq), d1 = far;   // partial sums of the row's int32 dot
+      if (reg && abl == 13) {
+#pragma unroll
+        for (int g = 0; g < kMaxColdGroups; ++g)
+          if (g < L8c) d0 += int32_t(v[g].x ^ v[g].y);
+      } else if (reg) {
 #pragma unroll
         for (int g = 0; g < kMaxColdGroups; ++g)
           if (g < L8c) {
@@ -828,8 +834,8 @@ __device__ __forceinline__ void hyb_pass(const DevSgd& d, const DevPrepared& p, 
       const int32_t q = __float2int_rn(res * sc.qscale);
       // unconditional (q = 0 adds nothing): the accumulators then need no
       // second register set for a skipped update
-      hot_grad(hv, q, gh);
-      if (res != 0.f) {
+      if (abl != 14) hot_grad(hv, q, gh);
+      if (res != 0.f && abl != 11) {
         const unsigned long long qq = (unsigned long long)(long long)q;
         if (reg) {
 #pragma unroll
