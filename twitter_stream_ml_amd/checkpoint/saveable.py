@@ -133,13 +133,20 @@ def _udt_array(vecs, sparse_density: float = SPARSE_DENSITY) -> pa.StructArray:
         vo.append(vo[-1] + vv[-1].shape[0])
     i32 = pa.list_(pa.field("element", pa.int32(), nullable=False))
     f64 = pa.list_(pa.field("element", pa.float64(), nullable=False))
-    ind = pa.ListArray.from_arrays(pa.array(np.asarray(io, np.int32)),
-                                   pa.array(np.concatenate(iv) if iv else np.zeros(0, np.int32)),
+
+    def cat(parts, dtype):
+        # one vector (a model): its buffer as it is -- pa.array of a numpy
+        # array is zero-copy, np.concatenate would copy ~MBs holding the GIL
+        # on the checkpoint writer thread while the training thread streams
+        if not parts:
+            return np.zeros(0, dtype)
+        return np.ascontiguousarray(parts[0], dtype) if len(parts) == 1 else np.concatenate(parts).astype(dtype, copy=False)
+
+    ind = pa.ListArray.from_arrays(pa.array(np.asarray(io, np.int32)), pa.array(cat(iv, np.int32)),
                                    type=i32, mask=pa.array(np.asarray(inull, bool)))
     if vo[-1] >= 2 ** 31:
         raise ValueError("VectorUDT column: more than 2^31 values")
-    val = pa.ListArray.from_arrays(pa.array(np.asarray(vo, np.int32)),
-                                   pa.array(np.concatenate(vv) if vv else np.zeros(0)), type=f64)
+    val = pa.ListArray.from_arrays(pa.array(np.asarray(vo, np.int32)), pa.array(cat(vv, np.float64)), type=f64)
     siz = pa.array(np.asarray(sizes, np.int32), mask=np.asarray(size_null, bool))
     return pa.StructArray.from_arrays([pa.array(np.asarray(types, np.int8)), siz, ind, val],
                                       fields=list(vector_udt_type()))
