@@ -303,6 +303,8 @@ LREngine::LREngine(int device, const LRConfig& cfg, std::shared_ptr<Comm> comm)
   sgd_.F = cfg_.num_text_features;
   sgd_.w64 = dmalloc<double>(size_t(nw));
   TWTML_HIP_CHECK(hipMemset(sgd_.w64, 0, sizeof(double) * size_t(nw)));  // Vectors.zeros
+  sgd_.touched = dmalloc<uint8_t>(size_t(nw));
+  TWTML_HIP_CHECK(hipMemset(sgd_.touched, 0, size_t(nw)));
   sgd_.stats = dmalloc<double>(8);
   sgd_.stat_i = dmalloc<int64_t>(16);
   sgd_.stat_part = dmalloc<int64_t>(size_t(kStatBlocks) * 16);
@@ -555,11 +557,12 @@ LREngine::~LREngine() {
   if (snap_ev_) (void)hipEventDestroy(snap_ev_);
   if (snap_src_ev_) (void)hipEventDestroy(snap_src_ev_);
   for (void* b : {static_cast<void*>(snap_cnt_), static_cast<void*>(snap_off_), static_cast<void*>(snap_idx_),
-                  static_cast<void*>(snap_val_)})
+                  static_cast<void*>(snap_val_), static_cast<void*>(snap_tidx_), static_cast<void*>(snap_tval_)})
     if (b) (void)hipFree(b);
   if (snap_total_) (void)hipHostFree(snap_total_);
   if (snap_stage_) (void)hipHostFree(snap_stage_);
-  void* bufs[] = {sgd_.gacc, sgd_.rbuf, sgd_.pbuf, sgd_.stat_i, sgd_.stat_part, sgd_.w64, sgd_.wc64, sgd_.wc32,
+  void* bufs[] = {sgd_.gacc, sgd_.rbuf, sgd_.pbuf, sgd_.stat_i, sgd_.stat_part, sgd_.w64, sgd_.touched, sgd_.wc64,
+                  sgd_.wc32,
                   sgd_.stats, sgd_.state,
                   sgd_.loss_hist, sgd_.pred_out, sgd_.real_out, sgd_.nrm, sgd_.wnorm_next, sgd_.part, sgd_.itrec, iter_tdbg_, iter_kdbg_,
                   lower_page_, lower_blocks_};
@@ -1372,6 +1375,7 @@ void LREngine::set_weights(const double* w, int64_t n) {
   // stream-ordered, complete on return (a pageable hipMemcpy may return
   // before its DMA lands, unordered against the non-blocking compute stream)
   TWTML_HIP_CHECK(hipMemcpyAsync(sgd_.w64, w, sizeof(double) * size_t(n), hipMemcpyHostToDevice, compute_));
+  launch_mark_nonzero(sgd_.w64, sgd_.touched, n, compute_);
   TWTML_HIP_CHECK(hipStreamSynchronize(compute_));
   norm_age_ = -1;   // the carried |w|^2 no longer holds
   diverged_ = false;
@@ -1396,6 +1400,8 @@ void LREngine::snapshot_begin() {
     snap_off_ = static_cast<int64_t*>(dev_alloc(sizeof(int64_t) * size_t(nb + 1)));
     snap_idx_ = static_cast<int32_t*>(dev_alloc(sizeof(int32_t) * size_t(n)));
     snap_val_ = static_cast<double*>(dev_alloc(sizeof(double) * size_t(n)));
+    snap_tidx_ = static_cast<int32_t*>(dev_alloc(sizeof(int32_t) * size_t(n)));
+    snap_tval_ = static_cast<double*>(dev_alloc(sizeof(double) * size_t(n)));
     TWTML_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&snap_total_), sizeof(int64_t), hipHostMallocMapped));
     TWTML_HIP_CHECK(hipHostMalloc(&snap_stage_, size_t(kSnapStage), hipHostMallocDefault));
     int lo = 0, hi = 0;
@@ -1413,7 +1419,8 @@ void LREngine::snapshot_begin() {
   // scatter waits for it (train: snap_guard_).
   TWTML_HIP_CHECK(hipEventRecord(snap_src_ev_, compute_));
   TWTML_HIP_CHECK(hipStreamWaitEvent(snap_stream_, snap_src_ev_, 0));
-  launch_snapshot(sgd_.w64, n, snap_cnt_, snap_off_, snap_idx_, snap_val_, dtot, snap_stream_);
+  launch_snapshot(sgd_.w64, sgd_.touched, n, snap_cnt_, snap_off_, snap_tidx_, snap_tval_, snap_idx_, snap_val_,
+                  dtot, snap_stream_);
   TWTML_HIP_CHECK(hipGetLastError());
   TWTML_HIP_CHECK(hipEventRecord(snap_ev_, snap_stream_));
   snap_guard_ = true;

@@ -242,7 +242,7 @@ class LREngine {
     return int64_t(nbuf) * 3 * int64_t(sizeof(uint32_t)) * pb_[0].dp.cap_entries +
            (pb_[0].dp.cap_tier ? 0 : int64_t(nbuf) * 36 * active_set_hint()) +
            int64_t(sizeof(float)) * pb_[0].dp.cap_rows16 +
-           (snap_idx_ ? 0 : num_weights() * int64_t(sizeof(int32_t) + sizeof(double)));
+           (snap_idx_ ? 0 : 2 * num_weights() * int64_t(sizeof(int32_t) + sizeof(double)));
   }
   // Non-blocking checkpoints: snapshot_begin() (training thread, between
   // batches) compacts the non-zero master weights on the device behind the
@@ -359,6 +359,8 @@ class LREngine {
   int64_t* snap_off_ = nullptr;
   int32_t* snap_idx_ = nullptr;
   double* snap_val_ = nullptr;
+  int32_t* snap_tidx_ = nullptr;      // scratch pairs of the one-pass compaction (snapshot.hip)
+  double* snap_tval_ = nullptr;
   int64_t* snap_total_ = nullptr;     // pinned mapped
   void* snap_stage_ = nullptr;        // pinned staging, kSnapStage bytes
   hipStream_t snap_stream_ = nullptr;

@@ -266,6 +266,7 @@ int64_t tier_near_cap();
 // any sharding is bit-identical to one GPU on the concatenated batch.
 struct DevSgd {
   double* w64;          // [F+4] master weights (fp64)
+  uint8_t* touched;     // [F+4] 1: the weight was ever written (k_scatter_w / set_weights), for the snapshot
   double* wc64;         // [NS]  compact master weights
   float* wc32;          // [NS]  compact fp32 copy read by the gradient kernel
   // Packed int64 gradient buffer (one all-reduce per GD iteration in DP):
@@ -418,8 +419,14 @@ void launch_union_hist(const int32_t* gathered, int world, int64_t max_u, const 
 // of the master weights, in index order, for non-blocking checkpoints --------
 constexpr int64_t kSnapChunk = 16384;   // weights per counting / writing workgroup
 int64_t snapshot_chunks(int64_t n);
-void launch_snapshot(const double* w, int64_t n, uint32_t* cnt, int64_t* off, int32_t* idx, double* val,
-                     volatile int64_t* host_total, hipStream_t s);
+// tidx / tval: scratch pairs of n entries (each chunk's pairs packed at its base);
+// touched (nullable): only weights marked there can be non-zero, the others
+// are not read
+void launch_snapshot(const double* w, const uint8_t* touched, int64_t n, uint32_t* cnt, int64_t* off,
+                     int32_t* tidx, double* tval, int32_t* idx, double* val, volatile int64_t* host_total,
+                     hipStream_t s);
+// touched[i] = w[i] != 0 for every weight (after set_weights)
+void launch_mark_nonzero(const double* w, uint8_t* touched, int64_t n, hipStream_t s);
 
 // (k-means launchers: kmeans_kernels.h)
 

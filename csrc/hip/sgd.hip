@@ -1600,8 +1600,9 @@ __global__ __launch_bounds__(kBlock) void k_scatter_w(DevSgd d, const int32_t* u
   for (int64_t s = int64_t(blockIdx.x) * kBlock + threadIdx.x; s < kNumNumeric + d.n_unique;
        s += int64_t(gridDim.x) * kBlock) {
     const double v = d.wc64[s];
-    if (s < kNumNumeric) d.w64[d.F + s] = v;
-    else d.w64[d.slot_fid ? d.slot_fid[s] : uniq[s - kNumNumeric]] = v;
+    const int64_t id = s < kNumNumeric ? d.F + s : int64_t(d.slot_fid ? d.slot_fid[s] : uniq[s - kNumNumeric]);
+    d.w64[id] = v;
+    d.touched[id] = 1;   // the snapshot reads only written weights
     acc += v * v;
   }
   acc = block_sum(acc, scratch);

@@ -7,10 +7,15 @@
 // to the host (800 MB at F = 1e8) and scanning them there on the training
 // thread, the engine compacts the non-zeros on the device, stream-ordered
 // right behind the batch the checkpoint is taken after:
-//   k_nz_count  one count per chunk of kSnapChunk weights (ballot popcounts)
+//   k_nz_pack   per chunk of kSnapChunk weights: its ordered (index, value)
+//               pairs packed at the chunk's own base in a scratch pair array,
+//               and its count
 //   k_nz_scan   one workgroup: exclusive chunk offsets + the total
-//   k_nz_write  ordered (index, value) pairs, one tile of kBlock at a time
-// Two streaming passes over the weights (HBM-bound: ~0.3 ms at F = 1e8); the
+//   k_nz_move   every chunk's pairs to their final offset
+// One streaming pass over the weights (800 MB at F = 1e8) plus the pairs
+// (12 B per non-zero) twice: the weights were read twice before (count, then
+// write), and every GD workgroup that meets a snapshot workgroup on its CU
+// waits for it -- the snapshot's device time is the batch's p99 cost.  The
 // writer thread then copies only the pairs to the host on its own stream
 // (engine.cpp snapshot_fetch) while training goes on.
 #include <hip/hip_runtime.h>
@@ -25,17 +30,6 @@ namespace twtml {
 __device__ __forceinline__ uint32_t nz_prefix(uint64_t mask) {
   // set bits of `mask` below this lane
   return uint32_t(__builtin_amdgcn_mbcnt_hi(uint32_t(mask >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(mask), 0u)));
-}
-
-__global__ __launch_bounds__(kBlock) void k_nz_count(const double* __restrict__ w, int64_t n,
-                                                     uint32_t* __restrict__ cnt) {
-  __shared__ uint32_t red[kBlock / kWave];
-  const int64_t b0 = int64_t(blockIdx.x) * kSnapChunk;
-  const int64_t b1 = std::min<int64_t>(n, b0 + kSnapChunk);
-  uint32_t c = 0;
-  for (int64_t i = b0 + threadIdx.x; i < b1; i += kBlock) c += (w[i] != 0.0) ? 1u : 0u;
-  c = block_sum(c, red);
-  if (threadIdx.x == 0) cnt[blockIdx.x] = c;
 }
 
 // Exclusive offsets of `nb` chunk counts (one workgroup); off[nb] = total,
@@ -67,17 +61,22 @@ __global__ __launch_bounds__(kBlock) void k_nz_scan(const uint32_t* __restrict__
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_nz_write(const double* __restrict__ w, int64_t n,
-                                                     const int64_t* __restrict__ off, int32_t* __restrict__ idx,
-                                                     double* __restrict__ val) {
+// touched (nullable): a weight never written is zero and is not read -- at
+// F = 1e8 the model's non-zeros are a few percent of the array, so most
+// lines of the 800 MB weight array are never fetched (100 MB of marks are)
+__global__ __launch_bounds__(kBlock) void k_nz_pack(const double* __restrict__ w,
+                                                    const uint8_t* __restrict__ touched, int64_t n,
+                                                    int32_t* __restrict__ tidx, double* __restrict__ tval,
+                                                    uint32_t* __restrict__ cnt) {
   __shared__ uint32_t wtot[kBlock / kWave];
   const int64_t b0 = int64_t(blockIdx.x) * kSnapChunk;
   const int64_t b1 = std::min<int64_t>(n, b0 + kSnapChunk);
   const int wv = threadIdx.x / kWave;
-  int64_t base = off[blockIdx.x];
+  int64_t base = b0;   // the chunk's pairs at its own base (<= kSnapChunk of them)
   for (int64_t t0 = b0; t0 < b1; t0 += kBlock) {
     const int64_t i = t0 + threadIdx.x;
-    const double x = i < b1 ? w[i] : 0.0;
+    const bool in = i < b1 && (touched == nullptr || touched[i] != 0);
+    const double x = in ? w[i] : 0.0;
     const bool nz = x != 0.0;
     const uint64_t m = __ballot(nz);
     if (lane_id() == 0) wtot[wv] = uint32_t(__popcll(m));
@@ -90,23 +89,50 @@ __global__ __launch_bounds__(kBlock) void k_nz_write(const double* __restrict__ 
     }
     if (nz) {
       const int64_t o = base + before + nz_prefix(m);
-      idx[o] = int32_t(i);
-      val[o] = x;
+      tidx[o] = int32_t(i);
+      tval[o] = x;
     }
     base += tile;
     __syncthreads();   // wtot is rewritten by the next tile
+  }
+  if (threadIdx.x == 0) cnt[blockIdx.x] = uint32_t(base - b0);
+}
+
+__global__ __launch_bounds__(kBlock) void k_nz_move(const int32_t* __restrict__ tidx,
+                                                    const double* __restrict__ tval,
+                                                    const uint32_t* __restrict__ cnt,
+                                                    const int64_t* __restrict__ off, int32_t* __restrict__ idx,
+                                                    double* __restrict__ val) {
+  const int64_t b0 = int64_t(blockIdx.x) * kSnapChunk, o = off[blockIdx.x];
+  const int64_t c = cnt[blockIdx.x];
+  for (int64_t j = threadIdx.x; j < c; j += kBlock) {
+    idx[o + j] = tidx[b0 + j];
+    val[o + j] = tval[b0 + j];
   }
 }
 
 int64_t snapshot_chunks(int64_t n) { return (n + kSnapChunk - 1) / kSnapChunk; }
 
-void launch_snapshot(const double* w, int64_t n, uint32_t* cnt, int64_t* off, int32_t* idx, double* val,
-                     volatile int64_t* host_total, hipStream_t s) {
+__global__ __launch_bounds__(kBlock) void k_mark_nonzero(const double* __restrict__ w, uint8_t* __restrict__ touched,
+                                                         int64_t n) {
+  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock)
+    touched[i] = w[i] != 0.0 ? 1 : 0;
+}
+
+void launch_mark_nonzero(const double* w, uint8_t* touched, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  TWTML_LAUNCH(k_mark_nonzero, dim3(unsigned(std::min<int64_t>((n + kBlock - 1) / kBlock, 8192))), dim3(kBlock), 0,
+               s, w, touched, n);
+}
+
+void launch_snapshot(const double* w, const uint8_t* touched, int64_t n, uint32_t* cnt, int64_t* off,
+                     int32_t* tidx, double* tval, int32_t* idx, double* val, volatile int64_t* host_total,
+                     hipStream_t s) {
   const int64_t nb = snapshot_chunks(n);
   if (nb <= 0) return;
-  TWTML_LAUNCH(k_nz_count, dim3(unsigned(nb)), dim3(kBlock), 0, s, w, n, cnt);
+  TWTML_LAUNCH(k_nz_pack, dim3(unsigned(nb)), dim3(kBlock), 0, s, w, touched, n, tidx, tval, cnt);
   TWTML_LAUNCH(k_nz_scan, dim3(1), dim3(kBlock), 0, s, cnt, nb, off, host_total);
-  TWTML_LAUNCH(k_nz_write, dim3(unsigned(nb)), dim3(kBlock), 0, s, w, n, off, idx, val);
+  TWTML_LAUNCH(k_nz_move, dim3(unsigned(nb)), dim3(kBlock), 0, s, tidx, tval, cnt, off, idx, val);
 }
 
 }  // namespace twtml
