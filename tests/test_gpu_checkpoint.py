@@ -59,6 +59,30 @@ def test_snapshot_is_the_nonzero_weights(hip_module):
     assert zi.shape[0] == 0 and zv.shape[0] == 0
 
 
+def test_snapshot_after_set_weights_and_training(hip_module):
+    """The snapshot reads only weights ever written (k_scatter_w and
+    set_weights mark them, csrc/hip/snapshot.hip): weights set from the host
+    and weights the batches then train are all in it, in index order."""
+    from twitter_stream_ml_amd.ops.lr_engine import DeviceLinearRegression, LRDeviceConfig
+    F = 20_000_000
+    eng = DeviceLinearRegression(LRDeviceConfig(num_text_features=F, hash="murmur3", max_rows=30_000,
+                                                max_units=30_000 * 300), device=0)
+    rng = np.random.default_rng(5)
+    w = np.zeros(F + 4)
+    w[rng.choice(F, 5000, replace=False)] = rng.standard_normal(5000) * 1e-3
+    w[F:] = [1e-3, -2e-3, 0.0, 4e-3]
+    eng.set_weights(w)
+    synth = SynthConfig.profile("wide", seed=9)
+    eng.train_batch(generate_batch(synth, 0, 30_000, batch_time_ms=NOW), want_pred=False)
+    eng.snapshot_begin()
+    size, idx, val = eng.snapshot_fetch()
+    w1 = eng.get_weights()
+    nz = np.flatnonzero(w1)
+    assert size == F + 4 and np.array_equal(idx, nz) and np.array_equal(val, w1[nz])
+    assert np.count_nonzero(w1[np.flatnonzero(w)]) > 0           # host-set weights survive in it
+    assert nz.shape[0] > 5000                                      # and the trained ones joined
+
+
 def _run(tmp_path, interval, pool, n_batches, F=100_000_000):
     from twitter_stream_ml_amd.apps.linear_regression import LinearRegressionJob, build_engine
     from twitter_stream_ml_amd.config.arguments import ConfArguments
