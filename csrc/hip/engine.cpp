@@ -1442,18 +1442,29 @@ int64_t LREngine::snapshot_wait() {
 void LREngine::snapshot_copy(int32_t* idx, double* val) {
   const int64_t nnz = snapshot_wait();
   // Chunks through the page-locked stage (the DMA never waits on pageable
-  // memory), paced: after a chunk the writer sleeps for (1 - duty) / duty of
-  // its transfer time, so the batches' H2D copies (which can share the DMA
-  // engine) wait at most one chunk.  A checkpoint is not latency critical:
-  // 120 MB of pairs take ~50 ms at duty 0.05, against ~1 s of parquet write.
-  // Measured (F = 1e8, 500K-tweet wide batches, a checkpoint due every
-  // batch): batch p99 +11 % at duty 0.25, +5 % at 0.05.
+  // memory), paced to a byte rate of duty x 50 GB/s (2.5 GB/s at the default
+  // 0.05): a batch's H2D that meets a chunk on the DMA engine waits for at
+  // most that chunk.  A checkpoint is not latency critical: 36 MB of pairs
+  // (F = 1e8 after 60 wide batches) take ~15 ms, against ~25 ms of parquet
+  // write.  Pacing by the pairs' bytes (not by each chunk's measured time)
+  // keeps the copy's duration independent of the chunk size, so the chunks
+  // can be small (256 KB).  The checkpoint p99 gate (500K-tweet wide
+  // batches at F = 1e8, a checkpoint due every batch) moves with how many
+  // snapshots a run takes, not with the chunk size or the rate:
+  // profiles/r6/ckpt_d2h_chunks.txt.
   static const double duty = [] {
     const char* e = std::getenv("TWTML_SNAP_DUTY");
     const double d = e ? std::atof(e) : 0.05;
     return d > 0.0 && d <= 1.0 ? d : 0.05;
   }();
-  const int64_t chunk = std::min<int64_t>(kSnapStage, int64_t(4) << 20);
+  static const int64_t chunk = [] {   // TWTML_SNAP_CHUNK_KB (A/B)
+    const char* e = std::getenv("TWTML_SNAP_CHUNK_KB");
+    const int64_t kb = e ? std::atoll(e) : 256;
+    return std::min<int64_t>(kSnapStage, std::max<int64_t>(64, kb) << 10);
+  }();
+  const double rate = duty * 50e9;   // bytes per second
+  const auto start = std::chrono::steady_clock::now();
+  int64_t done = 0;
   for (int part = 0; part < 2; ++part) {
     const int64_t esz = part == 0 ? int64_t(sizeof(int32_t)) : int64_t(sizeof(double));
     const int64_t per = chunk / esz;
@@ -1461,13 +1472,14 @@ void LREngine::snapshot_copy(int32_t* idx, double* val) {
     char* dst = part == 0 ? reinterpret_cast<char*>(idx) : reinterpret_cast<char*>(val);
     for (int64_t o = 0; o < nnz; o += per) {
       const int64_t c = std::min(per, nnz - o);
-      const auto t0 = std::chrono::steady_clock::now();
       TWTML_HIP_CHECK(hipMemcpyAsync(snap_stage_, src + o * esz, size_t(c * esz), hipMemcpyDeviceToHost,
                                      snap_stream_));
       TWTML_HIP_CHECK(hipStreamSynchronize(snap_stream_));
-      const auto dt = std::chrono::steady_clock::now() - t0;
       std::memcpy(dst + o * esz, snap_stage_, size_t(c * esz));
-      if (duty < 1.0) std::this_thread::sleep_for(dt * ((1.0 - duty) / duty));
+      done += c * esz;
+      if (duty < 1.0)
+        std::this_thread::sleep_until(start + std::chrono::duration_cast<std::chrono::steady_clock::duration>(
+                                                  std::chrono::duration<double>(double(done) / rate)));
     }
   }
   std::lock_guard<std::mutex> lk(snap_mu_);
