@@ -424,11 +424,24 @@ PYBIND11_MODULE(_twtml_hip, m) {
            },
            "compact the non-zero weights on the device behind the last batch (non-blocking)")
       .def("snapshot_fetch",
-           [](LREngine& e) {
+           [](py::object self, bool reuse) {
+             LREngine& e = self.cast<LREngine&>();
              int64_t nnz;
              {
                py::gil_scoped_release nogil;
                nnz = e.snapshot_wait();
+             }
+             if (reuse) {   // views of the engine's host buffers, valid until the next fetch
+               int32_t* pi = nullptr;
+               double* pv = nullptr;
+               {
+                 py::gil_scoped_release nogil;
+                 e.snapshot_host(nnz, &pi, &pv);
+                 e.snapshot_copy(pi, pv);
+               }
+               py::array_t<int32_t> idx({nnz}, {int64_t(sizeof(int32_t))}, pi, self);
+               py::array_t<double> val({nnz}, {int64_t(sizeof(double))}, pv, self);
+               return py::make_tuple(idx, val);
              }
              py::array_t<int32_t> idx(nnz);
              py::array_t<double> val(nnz);
@@ -440,7 +453,9 @@ PYBIND11_MODULE(_twtml_hip, m) {
              }
              return py::make_tuple(idx, val);
            },
-           "(indices int32, values fp64) of the begun snapshot's non-zero weights, in index order")
+           py::arg("reuse") = false,
+           "(indices int32, values fp64) of the begun snapshot's non-zero weights, in index order; "
+           "reuse=True: views of buffers the engine keeps (valid until the next fetch)")
       .def_property_readonly("device", &LREngine::device);
 
   bind_kmeans(m);

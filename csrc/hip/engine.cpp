@@ -1427,6 +1427,16 @@ void LREngine::snapshot_begin() {
   snap_pending_ = true;
 }
 
+void LREngine::snapshot_host(int64_t nnz, int32_t** idx, double** val) {
+  if (int64_t(snap_hidx_.size()) < nnz) {   // value-initialised: every page is touched now
+    const size_t cap = size_t(std::max<int64_t>(nnz + nnz / 4, int64_t(1) << 16));
+    snap_hidx_.assign(cap, 0);
+    snap_hval_.assign(cap, 0.0);
+  }
+  *idx = snap_hidx_.data();
+  *val = snap_hval_.data();
+}
+
 int64_t LREngine::snapshot_wait() {
   TWTML_HIP_CHECK(hipSetDevice(device_));
   {

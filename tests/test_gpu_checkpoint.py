@@ -119,45 +119,65 @@ def _run(tmp_path, interval, pool, n_batches, F=100_000_000):
     return np.asarray(lat), w, ck, ckp
 
 
-def test_async_checkpoint_p99_wide_1e8(hip_module, tmp_path, timing_margin):
+def _measure(base: str) -> dict:
+    """One attempt of the p99 gate: the run without checkpoints, then the
+    run with one due every batch (same pool, same engine configuration);
+    returns the two p99s, the writer's counts and the invariants' results."""
+    from pathlib import Path
     from twitter_stream_ml_amd.checkpoint import load_linear_regression, load_progress
     from twitter_stream_ml_amd.sources.synthetic import SyntheticReplaySource
-    rows, n = 500_000, 60
+    rows, n, warm = 500_000, 60, 8
     src = SyntheticReplaySource(SynthConfig.profile("wide", seed=22), batches=6, batch_rows=rows)
     pool = list(src.pool)
-    warm = 8
-    # a shared box's noise can move a 52-sample p99 by more than the bound
-    # (round 5: margins +1.1 % to +7.5 %, one first-attempt miss in six
-    # suite runs): a miss is measured again (both runs), up to three pairs,
-    # and the last pair decides; every pair's margin is printed
+    base = Path(base)
+    lat0, w0, _, _ = _run(base, 0, pool, n)
+    lat1, w1, ck1, cp1 = _run(base, 1, pool, n)
+    w_disk, _ = load_linear_regression(ck1)
+    return dict(p99_ms_no_ckpt=float(np.percentile(lat0[warm:], 99)) * 1e3,
+                p99_ms_ckpt1=float(np.percentile(lat1[warm:], 99)) * 1e3,
+                p50_ms_no_ckpt=float(np.median(lat0[warm:])) * 1e3,
+                p50_ms_ckpt1=float(np.median(lat1[warm:])) * 1e3,
+                written=cp1.written, skipped=cp1.skipped, batches=n, rows=rows,
+                same_model=bool(np.array_equal(w0, w1)),                 # checkpoints never change the model
+                disk_is_model=bool(np.array_equal(w_disk, w1)),          # the final checkpoint, bit for bit
+                disk_batches=int(load_progress(ck1)["batches"]))
+
+
+def test_async_checkpoint_p99_wide_1e8(hip_module, tmp_path, timing_margin):
+    """Each attempt runs in a fresh interpreter (tools-free: this module's
+    ``_measure``): in the suite's process the gate measured the state the
+    earlier modules left behind -- three app / bench modules before it took
+    the p50 of the checkpointing run from +5 % to +10-20 % (the same runs
+    alone: +4-7 %)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import json, sys; sys.path[:0] = [%r, %r]; import test_gpu_checkpoint as t; "
+            "print('RESULT ' + json.dumps(t._measure(sys.argv[1])))" % (root, os.path.join(root, "tests")))
+    # a shared box's noise can move a 52-sample p99 by more than the bound: a
+    # miss is measured again (both runs), up to three pairs, and the last
+    # pair decides; every pair's margin is printed
     for attempt in (1, 2, 3):
         base = tmp_path / f"a{attempt}"
         base.mkdir()
-        lat0, w0, _, _ = _run(base, 0, pool, n)
-        lat1, w1, ck1, cp1 = _run(base, 1, pool, n)
-        np.testing.assert_array_equal(w0, w1)            # checkpoints never change the model
-        p99_0 = float(np.percentile(lat0[warm:], 99))
-        p99_1 = float(np.percentile(lat1[warm:], 99))
-        res = dict(p99_ms_no_ckpt=p99_0 * 1e3, p99_ms_ckpt1=p99_1 * 1e3,
-                   p50_ms_no_ckpt=float(np.median(lat0[warm:])) * 1e3,
-                   p50_ms_ckpt1=float(np.median(lat1[warm:])) * 1e3,
-                   written=cp1.written, skipped=cp1.skipped, batches=n, rows=rows, attempt=attempt)
-        out = os.environ.get("TWTML_TEST_OUT")
-        if out:
-            os.makedirs(out, exist_ok=True)
-            with open(os.path.join(out, "ckpt_p99.json"), "w") as fh:
+        out = subprocess.run([sys.executable, "-c", code, str(base)], capture_output=True, text=True, timeout=240)
+        lines = [l for l in out.stdout.splitlines() if l.startswith("RESULT ")]
+        assert out.returncode == 0 and lines, (out.returncode, out.stdout[-2000:], out.stderr[-4000:])
+        res = json.loads(lines[-1][len("RESULT "):])
+        res["attempt"] = attempt
+        outdir = os.environ.get("TWTML_TEST_OUT")
+        if outdir:
+            os.makedirs(outdir, exist_ok=True)
+            with open(os.path.join(outdir, "ckpt_p99.json"), "w") as fh:
                 json.dump(res, fh)
-        res["written_fraction"] = (cp1.written - 1) / n   # the final checkpoint is forced
+        res["written_fraction"] = (res["written"] - 1) / res["batches"]   # the final checkpoint is forced
         print(res)
+        assert res["same_model"] and res["disk_is_model"] and res["disk_batches"] == res["batches"], res
         # every due checkpoint is either written or coalesced into a later one
-        assert cp1.written + cp1.skipped == n + 1, res
+        assert res["written"] + res["skipped"] == res["batches"] + 1, res
         assert res["written_fraction"] >= 0.05, res
-        timing_margin(f"checkpoint-every-batch p99, attempt {attempt} (1.10 x no-checkpoint)", p99_1 * 1e3,
-                      1.10 * p99_0 * 1e3)
+        p99_0, p99_1 = res["p99_ms_no_ckpt"], res["p99_ms_ckpt1"]
+        timing_margin(f"checkpoint-every-batch p99, attempt {attempt} (1.10 x no-checkpoint)", p99_1, 1.10 * p99_0)
         if p99_1 <= 1.10 * p99_0:
             break
     assert p99_1 <= 1.10 * p99_0, res
-    # the final (synchronous) checkpoint is the trained model, bit for bit
-    w_disk, _ = load_linear_regression(ck1)
-    np.testing.assert_array_equal(w_disk, w1)
-    assert load_progress(ck1)["batches"] == n

@@ -54,6 +54,9 @@ from ..utils.metrics import MetricsLogger
 
 __all__ = ["main", "build_engine", "LinearRegressionJob"]
 
+# TWTML_SNAP_REUSE=0 (A/B): a fresh host array per checkpoint
+_SNAP_REUSE = os.environ.get("TWTML_SNAP_REUSE", "1") != "0"
+
 log = logging.getLogger("com.giorgioinf.twtml.spark.LinearRegression")
 APP_NAME = "twitter-stream-ml-linear-regression"
 
@@ -279,7 +282,9 @@ class LinearRegressionJob:
             eng.snapshot_begin()
 
             def save(path, prog):
-                size, idx, val = eng.snapshot_fetch()
+                # views of the engine's own host buffers: one write in flight at
+                # a time, so nothing else fetches before this save is done
+                size, idx, val = eng.snapshot_fetch(reuse=_SNAP_REUSE)
                 LinearRegressionModel.save_sparse(path, SparseWeights(size, idx, val), 0.0, prog)
             return save
         w = np.array(eng.get_weights(), dtype=np.float64, copy=True)

@@ -350,11 +350,14 @@ class DeviceLinearRegression:
         (``csrc/hip/snapshot.hip``); nothing is copied yet."""
         self._eng.snapshot_begin()
 
-    def snapshot_fetch(self):
+    def snapshot_fetch(self, reuse: bool = False):
         """Part 2 (any thread, e.g. a checkpoint writer): ``(size, indices,
         values)`` of the begun snapshot -- only the non-zero weights cross
-        PCIe, on the engine's snapshot stream, while training goes on."""
-        idx, val = self._eng.snapshot_fetch()
+        PCIe, on the engine's snapshot stream, while training goes on.
+        ``reuse=True`` (the checkpoint writer): the arrays view host buffers
+        the engine keeps across snapshots (no fresh pages per checkpoint);
+        they are overwritten by the next fetch."""
+        idx, val = self._eng.snapshot_fetch(reuse)
         return self.num_weights, np.asarray(idx), np.asarray(val)
 
     def set_weights(self, w: np.ndarray) -> None:
