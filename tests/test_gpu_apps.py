@@ -113,14 +113,21 @@ def test_lr_driver_plot_does_not_stall_training(hip_module, tmp_path, monkeypatc
     stays within 5 % of the plot-off run on the same data."""
     import json
     from fakes import FakeLightningProcess
-    from twitter_stream_ml_amd.apps import linear_regression as app
     base = ["--master", "rocm[1]", "--twtweb", "http://127.0.0.1:9", "--source", "replay:synthetic:wide:4",
             "--seconds", "0", "--batchSize", "1000000", "--sourceRate", "0", "--numBatches", "40",
             "-f", "1000000", "--plotPoints", "10000"]
 
     def p99(path, lightning):
-        monkeypatch.setenv("TWTML_METRICS", str(path))
-        assert app.main(base + ["--lightning", lightning]) == 0
+        # each run in a fresh interpreter, as the driver runs: in one process
+        # the second and third of the four runs each met one ~3.5-ms stall,
+        # which set a 32-sample p99 whichever of off / on it landed in
+        import os
+        import subprocess
+        import sys
+        env = dict(os.environ, TWTML_METRICS=str(path))
+        out = subprocess.run([sys.executable, "-m", "twitter_stream_ml_amd", *base, "--lightning", lightning],
+                             env=env, capture_output=True, text=True, timeout=240)
+        assert out.returncode == 0, (out.returncode, out.stderr[-4000:])
         recs = [r for r in (json.loads(l) for l in open(path)) if "step_ms" in r]
         assert len(recs) == 40
         for k in ("step_ms", "call_ms", "gil_wait_ms"):
