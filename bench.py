@@ -659,6 +659,19 @@ def main(argv=None) -> int:
         out["h2d_bytes_per_tweet"] = round(moved / (args.steps * B), 1)
         out["h2d_gbps"] = round(gbps, 1)
         out["h2d_floor_ms_per_step"] = round(moved / args.steps / (gbps * 1e9) * 1e3, 3) if gbps > 0 else None
+    # TWTML_H2D_TIMING=1 (diagnostics): the copy stream's busy time and gaps
+    # over the timed batches (their submits are the last args.steps ones)
+    native = getattr(eng, "_eng", None)
+    if os.environ.get("TWTML_H2D_TIMING") == "1" and native is not None and hasattr(native, "h2d_timeline"):
+        tl = native.h2d_timeline()[-args.steps:]
+        if tl:
+            busy = sum(e - s for s, e, _ in tl)
+            gaps = [tl[i + 1][0] - tl[i][1] for i in range(len(tl) - 1)]
+            out["h2d_timeline"] = {
+                "batches": len(tl), "busy_ms": round(busy, 3), "span_ms": round(tl[-1][1] - tl[0][0], 3),
+                "gap_ms_total": round(sum(gaps), 3), "gap_ms_max": round(max(gaps), 3) if gaps else 0.0,
+                "gbps_while_busy": round(sum(b for _, _, b in tl) / (busy * 1e6), 2) if busy > 0 else None,
+                "per_batch_ms": [round(e - s, 3) for s, e, _ in tl]}
     if runner.comm and sum(c[0] for c in runner.comm) > 0:
         n_ar = sum(c[0] for c in runner.comm)
         out["grad_allreduce_per_step"] = round(n_ar / len(runner.comm), 2)

@@ -367,6 +367,11 @@ PYBIND11_MODULE(_twtml_hip, m) {
            },
            py::arg("slot"), "forget a submitted batch that will not be processed (one GPU)")
       .def_property_readonly("h2d_bytes", &LREngine::h2d_bytes, "host-to-device bytes submitted so far")
+      .def("h2d_timeline", [](LREngine& e) {
+             py::gil_scoped_release nogil;
+             return e.h2d_timeline();
+           },
+           "TWTML_H2D_TIMING=1: per submitted batch (start ms, end ms, bytes) of its copies")
       .def_property_readonly("raw_slots", &LREngine::raw_slots, "device raw-batch slots")
       .def_property_readonly("lazy_bytes", &LREngine::lazy_bytes,
                              "device bytes the engine allocates on its first tiered batch (sizing)")

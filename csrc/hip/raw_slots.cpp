@@ -46,7 +46,26 @@ void RawSlots::init(int n_slots, int64_t max_rows, int64_t max_bytes) {
   upload_case_tables(&case_);
 }
 
+std::vector<std::array<double, 3>> RawSlots::h2d_timeline() {
+  std::lock_guard<std::mutex> lk(tl_mu_);
+  std::vector<std::array<double, 3>> out;
+  if (tl_.empty()) return out;
+  TWTML_HIP_CHECK(hipEventSynchronize(tl_.back().b));
+  for (const H2DMark& m : tl_) {
+    float a = 0.f, b = 0.f;
+    TWTML_HIP_CHECK(hipEventElapsedTime(&a, tl_.front().a, m.a));
+    TWTML_HIP_CHECK(hipEventElapsedTime(&b, tl_.front().a, m.b));
+    out.push_back({double(a), double(b), double(m.bytes)});
+  }
+  return out;
+}
+
 void RawSlots::release() {
+  for (H2DMark& m : tl_) {
+    if (m.a) (void)hipEventDestroy(m.a);
+    if (m.b) (void)hipEventDestroy(m.b);
+  }
+  tl_.clear();
   for (auto& s : slots_) {
     if (s.text_base) (void)hipFree(s.text_base);
     if (s.offsets) (void)hipFree(s.offsets);
@@ -79,6 +98,16 @@ void RawSlots::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, h
   if (n > 0 && hb.rows_scanned_n != n) throw std::logic_error("HostBatch rows not packed (pack_rows) for this row count");
   // wait until the compute stream has finished reading this slot
   if (s.used) TWTML_HIP_CHECK(hipStreamWaitEvent(copy, s.consumed, 0));
+  if (tl_on_ < 0) {
+    const char* e = std::getenv("TWTML_H2D_TIMING");
+    tl_on_ = e && e[0] == '1' ? 1 : 0;
+  }
+  H2DMark mark;
+  if (tl_on_ == 1) {   // after the slot wait: the mark times the copies themselves
+    TWTML_HIP_CHECK(hipEventCreate(&mark.a));
+    TWTML_HIP_CHECK(hipEventCreate(&mark.b));
+    TWTML_HIP_CHECK(hipEventRecord(mark.a, copy));
+  }
   // offsets + flags: one u16 per row when the batch was packed (the compute
   // stream rebuilds both in acquire), else as they are.  Packed row words sit
   // right before the text on both sides and travel with it (below).
@@ -123,6 +152,12 @@ void RawSlots::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, h
   if (!packed) moved += int64_t(sizeof(int64_t)) * (n + 1) + (n > 0 ? n : 0);
   if (n > 0) moved += hb.soff[scalar_cols];
   h2d_bytes_.fetch_add(moved, std::memory_order_relaxed);
+  if (tl_on_ == 1) {
+    TWTML_HIP_CHECK(hipEventRecord(mark.b, copy));
+    mark.bytes = moved;
+    std::lock_guard<std::mutex> lk(tl_mu_);
+    tl_.push_back(mark);
+  }
   for (int c = 0; c < kScalarCols; ++c) {
     s.soff[c] = hb.soff[c];
     s.sbase[c] = hb.sbase[c];

@@ -14,7 +14,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <array>
 #include <atomic>
+#include <mutex>
 #include <cstdint>
 #include <vector>
 
@@ -65,6 +67,10 @@ class RawSlots {
   int64_t max_bytes() const { return max_bytes_; }
   // bytes enqueued host-to-device by submit() so far (every copy of a batch)
   int64_t h2d_bytes() const { return h2d_bytes_.load(std::memory_order_relaxed); }
+  // TWTML_H2D_TIMING=1 (diagnostics): timing events around every submit's
+  // copies; h2d_timeline() synchronises them and returns, per submit in
+  // order, (start, end, bytes) with times in ms from the first submit's start.
+  std::vector<std::array<double, 3>> h2d_timeline();
 
  private:
   int check(int slot) const;
@@ -92,6 +98,13 @@ class RawSlots {
   std::vector<Slot> slots_;
   int64_t max_rows_ = 0, max_bytes_ = 0;
   std::atomic<int64_t> h2d_bytes_{0};
+  struct H2DMark {
+    hipEvent_t a = nullptr, b = nullptr;
+    int64_t bytes = 0;
+  };
+  std::mutex tl_mu_;
+  std::vector<H2DMark> tl_;
+  int tl_on_ = -1;   // TWTML_H2D_TIMING, read once
   DevCaseTables case_{};
 };
 
