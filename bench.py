@@ -124,6 +124,7 @@ class Runner:
         self.comm = []            # (gradient all-reduces, their ms) per timed batch
         self.prestaged_at_t0 = 0  # batches of the timed window staged / submitted before t0
         self.steps_done = 0
+        self.marks = []           # (sealed, done) host clock per timed batch
         self.hang_at = 0          # TWTML_BENCH_HANG=<rank>:<step>: that rank hangs before that step
 
     def process(self, slot: int):
@@ -137,6 +138,7 @@ class Runner:
 
     def record(self, res, sealed: float, done: float) -> None:
         self.lat.append((done - sealed) * 1e3)
+        self.marks.append((sealed, done))
         if self.is_km:
             self.kept.append(res["n_local"])
             self.stage.append((res["ms"], 0.0))
@@ -549,17 +551,24 @@ def main(argv=None) -> int:
         runner.hang_at = int(hang.split(":")[1])
 
     h2d = {}
+    # TWTML_H2D_TIMING=1: events on the copy stream at the window's ends (diagnostics)
+    wmark = getattr(getattr(eng, "_eng", None), "h2d_window_mark", None) \
+        if os.environ.get("TWTML_H2D_TIMING") == "1" else None
 
     def sync(fn):
         eng.synchronize()
         D.barrier()
         torch.cuda.synchronize()
         h2d["b0"] = eng.h2d_bytes
+        if wmark:
+            wmark()
         t0 = time.perf_counter()
         fn()
         eng.synchronize()
         torch.cuda.synchronize()
         t1 = time.perf_counter()
+        if wmark:
+            wmark()
         h2d["b1"] = eng.h2d_bytes
         D.barrier()
         return t0, t1
@@ -664,14 +673,31 @@ def main(argv=None) -> int:
     native = getattr(eng, "_eng", None)
     if os.environ.get("TWTML_H2D_TIMING") == "1" and native is not None and hasattr(native, "h2d_timeline"):
         tl = native.h2d_timeline()[-args.steps:]
+        win = native.h2d_window()[-2:]
         if tl:
-            busy = sum(e - s for s, e, _ in tl)
-            gaps = [tl[i + 1][0] - tl[i][1] for i in range(len(tl) - 1)]
+            busy = sum(e - a for _, a, e, _ in tl)
+            gaps = [tl[i + 1][1] - tl[i][2] for i in range(len(tl) - 1)]
             out["h2d_timeline"] = {
-                "batches": len(tl), "busy_ms": round(busy, 3), "span_ms": round(tl[-1][1] - tl[0][0], 3),
+                "batches": len(tl), "busy_ms": round(busy, 3), "span_ms": round(tl[-1][2] - tl[0][1], 3),
                 "gap_ms_total": round(sum(gaps), 3), "gap_ms_max": round(max(gaps), 3) if gaps else 0.0,
-                "gbps_while_busy": round(sum(b for _, _, b in tl) / (busy * 1e6), 2) if busy > 0 else None,
-                "per_batch_ms": [round(e - s, 3) for s, e, _ in tl]}
+                "gbps_while_busy": round(sum(b for _, _, _, b in tl) / (busy * 1e6), 2) if busy > 0 else None,
+                "per_batch_ms": [round(e - a, 3) for _, a, e, _ in tl],
+                # per gap: the part the copy stream waited for the slot's previous batch
+                # (start - queued) and the part no copy was queued yet (host late)
+                "gaps_ms": [round(g, 3) for g in gaps],
+                "slot_wait_ms": [round(tl[i + 1][1] - max(tl[i + 1][0], tl[i][2]), 3) for i in range(len(tl) - 1)],
+                "host_late_ms": [round(max(0.0, tl[i + 1][0] - tl[i][2]), 3) for i in range(len(tl) - 1)]}
+            # host clock, ms from t0: a batch's staging start and its process() return
+            out["h2d_timeline"]["host_sealed_ms"] = [round((a - t0) * 1e3, 3) for a, _ in runner.marks]
+            out["h2d_timeline"]["host_done_ms"] = [round((b - t0) * 1e3, 3) for _, b in runner.marks]
+            out["h2d_timeline"]["iterations"] = [int(x) for x in runner.iters]
+            out["h2d_timeline"]["prep_ms"] = [round(float(a), 3) for a, _ in runner.stage]
+            out["h2d_timeline"]["train_ms"] = [round(float(b), 3) for _, b in runner.stage]
+            if len(win) == 2:   # the window's ends against the first copy's start / the last copy's end
+                out["h2d_timeline"].update(
+                    window_ms=round(win[1] - win[0], 3), first_copy_start_ms=round(tl[0][1] - win[0], 3),
+                    first_copy_queued_ms=round(tl[0][0] - win[0], 3),
+                    after_last_copy_ms=round(win[1] - tl[-1][2], 3))
     if runner.comm and sum(c[0] for c in runner.comm) > 0:
         n_ar = sum(c[0] for c in runner.comm)
         out["grad_allreduce_per_step"] = round(n_ar / len(runner.comm), 2)

@@ -371,7 +371,14 @@ PYBIND11_MODULE(_twtml_hip, m) {
              py::gil_scoped_release nogil;
              return e.h2d_timeline();
            },
-           "TWTML_H2D_TIMING=1: per submitted batch (start ms, end ms, bytes) of its copies")
+           "TWTML_H2D_TIMING=1: per submitted batch (queued ms, start ms, end ms, bytes) of its copies")
+      .def("h2d_window_mark", &LREngine::h2d_window_mark,
+           "TWTML_H2D_TIMING=1: a timing event on the copy stream (the bench's window ends)")
+      .def("h2d_window", [](LREngine& e) {
+             py::gil_scoped_release nogil;
+             return e.h2d_window();
+           },
+           "the h2d_window_mark events, ms in the h2d_timeline time base")
       .def_property_readonly("raw_slots", &LREngine::raw_slots, "device raw-batch slots")
       .def_property_readonly("lazy_bytes", &LREngine::lazy_bytes,
                              "device bytes the engine allocates on its first tiered batch (sizing)")

@@ -234,7 +234,9 @@ class LREngine {
   // buffer) and by the first checkpoint snapshot ((index, value) pairs for
   // every weight): ops/sizing.py adds them to the construction footprint.
   int64_t h2d_bytes() const { return raw_.h2d_bytes(); }   // host-to-device bytes submitted so far
-  std::vector<std::array<double, 3>> h2d_timeline() { return raw_.h2d_timeline(); }   // TWTML_H2D_TIMING
+  std::vector<std::array<double, 4>> h2d_timeline() { return raw_.h2d_timeline(); }   // TWTML_H2D_TIMING
+  void h2d_window_mark() { raw_.h2d_window_mark(copy_); }
+  std::vector<double> h2d_window() { return raw_.h2d_window(); }
   int raw_slots() const { return raw_.count(); }
   int64_t lazy_bytes() const {
     const int nbuf = overlap_ ? 2 : 1;

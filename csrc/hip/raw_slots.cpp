@@ -46,22 +46,48 @@ void RawSlots::init(int n_slots, int64_t max_rows, int64_t max_bytes) {
   upload_case_tables(&case_);
 }
 
-std::vector<std::array<double, 3>> RawSlots::h2d_timeline() {
+std::vector<std::array<double, 4>> RawSlots::h2d_timeline() {
   std::lock_guard<std::mutex> lk(tl_mu_);
-  std::vector<std::array<double, 3>> out;
+  std::vector<std::array<double, 4>> out;
   if (tl_.empty()) return out;
   TWTML_HIP_CHECK(hipEventSynchronize(tl_.back().b));
   for (const H2DMark& m : tl_) {
-    float a = 0.f, b = 0.f;
-    TWTML_HIP_CHECK(hipEventElapsedTime(&a, tl_.front().a, m.a));
-    TWTML_HIP_CHECK(hipEventElapsedTime(&b, tl_.front().a, m.b));
-    out.push_back({double(a), double(b), double(m.bytes)});
+    float q = 0.f, a = 0.f, b = 0.f;
+    TWTML_HIP_CHECK(hipEventElapsedTime(&q, tl_.front().q, m.q));
+    TWTML_HIP_CHECK(hipEventElapsedTime(&a, tl_.front().q, m.a));
+    TWTML_HIP_CHECK(hipEventElapsedTime(&b, tl_.front().q, m.b));
+    out.push_back({double(q), double(a), double(b), double(m.bytes)});
+  }
+  return out;
+}
+
+void RawSlots::h2d_window_mark(hipStream_t copy) {
+  if (tl_on_ != 1) return;
+  hipEvent_t e = nullptr;
+  TWTML_HIP_CHECK(hipEventCreate(&e));
+  TWTML_HIP_CHECK(hipEventRecord(e, copy));
+  std::lock_guard<std::mutex> lk(tl_mu_);
+  win_.push_back(e);
+}
+
+std::vector<double> RawSlots::h2d_window() {
+  std::lock_guard<std::mutex> lk(tl_mu_);
+  std::vector<double> out;
+  if (tl_.empty()) return out;
+  for (hipEvent_t e : win_) {
+    TWTML_HIP_CHECK(hipEventSynchronize(e));
+    float t = 0.f;
+    TWTML_HIP_CHECK(hipEventElapsedTime(&t, tl_.front().q, e));
+    out.push_back(double(t));
   }
   return out;
 }
 
 void RawSlots::release() {
+  for (hipEvent_t e : win_) (void)hipEventDestroy(e);
+  win_.clear();
   for (H2DMark& m : tl_) {
+    if (m.q) (void)hipEventDestroy(m.q);
     if (m.a) (void)hipEventDestroy(m.a);
     if (m.b) (void)hipEventDestroy(m.b);
   }
@@ -96,18 +122,21 @@ void RawSlots::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, h
   if (n > 0 && hb.spacked_cols < scalar_cols)
     throw std::logic_error("HostBatch packed fewer scalar columns than this engine reads");
   if (n > 0 && hb.rows_scanned_n != n) throw std::logic_error("HostBatch rows not packed (pack_rows) for this row count");
-  // wait until the compute stream has finished reading this slot
-  if (s.used) TWTML_HIP_CHECK(hipStreamWaitEvent(copy, s.consumed, 0));
   if (tl_on_ < 0) {
     const char* e = std::getenv("TWTML_H2D_TIMING");
     tl_on_ = e && e[0] == '1' ? 1 : 0;
   }
   H2DMark mark;
-  if (tl_on_ == 1) {   // after the slot wait: the mark times the copies themselves
+  if (tl_on_ == 1) {   // queued: before the slot wait
+    TWTML_HIP_CHECK(hipEventCreate(&mark.q));
     TWTML_HIP_CHECK(hipEventCreate(&mark.a));
     TWTML_HIP_CHECK(hipEventCreate(&mark.b));
-    TWTML_HIP_CHECK(hipEventRecord(mark.a, copy));
+    TWTML_HIP_CHECK(hipEventRecord(mark.q, copy));
   }
+  // wait until the compute stream has finished reading this slot
+  if (s.used) TWTML_HIP_CHECK(hipStreamWaitEvent(copy, s.consumed, 0));
+  // after the slot wait: a..b times the copies themselves
+  if (tl_on_ == 1) TWTML_HIP_CHECK(hipEventRecord(mark.a, copy));
   // offsets + flags: one u16 per row when the batch was packed (the compute
   // stream rebuilds both in acquire), else as they are.  Packed row words sit
   // right before the text on both sides and travel with it (below).

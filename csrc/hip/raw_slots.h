@@ -69,8 +69,15 @@ class RawSlots {
   int64_t h2d_bytes() const { return h2d_bytes_.load(std::memory_order_relaxed); }
   // TWTML_H2D_TIMING=1 (diagnostics): timing events around every submit's
   // copies; h2d_timeline() synchronises them and returns, per submit in
-  // order, (start, end, bytes) with times in ms from the first submit's start.
-  std::vector<std::array<double, 3>> h2d_timeline();
+  // order, (queued, start, end, bytes) with times in ms from the first
+  // submit's queued mark.  queued is recorded before the wait for the slot's
+  // previous batch (so start - queued is slot back-pressure, and a queued
+  // mark after the previous copy's end is the host submitting late).
+  std::vector<std::array<double, 4>> h2d_timeline();
+  // Timing event on `copy` (diagnostics: the bench marks its timed window's
+  // ends with it); h2d_window() returns them in the timeline's time base.
+  void h2d_window_mark(hipStream_t copy);
+  std::vector<double> h2d_window();
 
  private:
   int check(int slot) const;
@@ -99,11 +106,12 @@ class RawSlots {
   int64_t max_rows_ = 0, max_bytes_ = 0;
   std::atomic<int64_t> h2d_bytes_{0};
   struct H2DMark {
-    hipEvent_t a = nullptr, b = nullptr;
+    hipEvent_t q = nullptr, a = nullptr, b = nullptr;
     int64_t bytes = 0;
   };
   std::mutex tl_mu_;
   std::vector<H2DMark> tl_;
+  std::vector<hipEvent_t> win_;
   int tl_on_ = -1;   // TWTML_H2D_TIMING, read once
   DevCaseTables case_{};
 };
