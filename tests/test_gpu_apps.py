@@ -113,8 +113,11 @@ def test_lr_driver_plot_does_not_stall_training(hip_module, tmp_path, monkeypatc
     stays within 5 % of the plot-off run on the same data."""
     import json
     from fakes import FakeLightningProcess
+    # 100 batches (92 measured): a p99 over 32 samples is nearly their
+    # maximum, so one scheduler hiccup decided it (round 6 margins +0.9 %)
+    nb = 100
     base = ["--master", "rocm[1]", "--twtweb", "http://127.0.0.1:9", "--source", "replay:synthetic:wide:4",
-            "--seconds", "0", "--batchSize", "1000000", "--sourceRate", "0", "--numBatches", "40",
+            "--seconds", "0", "--batchSize", "1000000", "--sourceRate", "0", "--numBatches", str(nb),
             "-f", "1000000", "--plotPoints", "10000"]
 
     def p99(path, lightning):
@@ -129,13 +132,13 @@ def test_lr_driver_plot_does_not_stall_training(hip_module, tmp_path, monkeypatc
                              env=env, capture_output=True, text=True, timeout=240)
         assert out.returncode == 0, (out.returncode, out.stderr[-4000:])
         recs = [r for r in (json.loads(l) for l in open(path)) if "step_ms" in r]
-        assert len(recs) == 40
+        assert len(recs) == nb
         for k in ("step_ms", "call_ms", "gil_wait_ms"):
             v = [r[k] for r in recs[8:]]
             print(f"{lightning} {k}: p50 {np.percentile(v, 50):.3f} p99 {np.percentile(v, 99):.3f} max {max(v):.3f}")
         return float(np.percentile([r["step_ms"] for r in recs[8:]], 99))   # after warm-up
 
-    # A shared box's noise can move a 32-sample p99 by more than the 5 %
+    # A shared box's noise can move a p99 by more than the 5 %
     # bound (one suite run: both p50 and p99 of the plot-on run 13 % up);
     # a miss is measured once more, off and on, and the second pair decides.
     for attempt in (1, 2):
@@ -146,7 +149,7 @@ def test_lr_driver_plot_does_not_stall_training(hip_module, tmp_path, monkeypatc
             summ = lgn.summary()
         finally:
             lgn.stop()
-        assert summ["appends"] >= 30 and summ["last_series_lens"] == [10000] * 4, summ
+        assert summ["appends"] >= nb - 10 and summ["last_series_lens"] == [10000] * 4, summ
         print(f"step p99 (attempt {attempt}): plot off {off:.3f} ms, plot on {on:.3f} ms")
         timing_margin(f"plot-on step p99, attempt {attempt} (1.05 x plot-off + 0.05 ms)", on, 1.05 * off + 0.05)
         if on <= 1.05 * off + 0.05:
