@@ -61,8 +61,16 @@ std::vector<std::array<double, 4>> RawSlots::h2d_timeline() {
   return out;
 }
 
+bool RawSlots::timing_on() {
+  if (tl_on_ < 0) {
+    const char* e = std::getenv("TWTML_H2D_TIMING");
+    tl_on_ = e && e[0] == '1' ? 1 : 0;
+  }
+  return tl_on_ == 1;
+}
+
 void RawSlots::h2d_window_mark(hipStream_t copy) {
-  if (tl_on_ != 1) return;
+  if (!timing_on()) return;
   hipEvent_t e = nullptr;
   TWTML_HIP_CHECK(hipEventCreate(&e));
   TWTML_HIP_CHECK(hipEventRecord(e, copy));
@@ -122,12 +130,9 @@ void RawSlots::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, h
   if (n > 0 && hb.spacked_cols < scalar_cols)
     throw std::logic_error("HostBatch packed fewer scalar columns than this engine reads");
   if (n > 0 && hb.rows_scanned_n != n) throw std::logic_error("HostBatch rows not packed (pack_rows) for this row count");
-  if (tl_on_ < 0) {
-    const char* e = std::getenv("TWTML_H2D_TIMING");
-    tl_on_ = e && e[0] == '1' ? 1 : 0;
-  }
+  const bool timed = timing_on();
   H2DMark mark;
-  if (tl_on_ == 1) {   // queued: before the slot wait
+  if (timed) {   // queued: before the slot wait
     TWTML_HIP_CHECK(hipEventCreate(&mark.q));
     TWTML_HIP_CHECK(hipEventCreate(&mark.a));
     TWTML_HIP_CHECK(hipEventCreate(&mark.b));
@@ -136,7 +141,7 @@ void RawSlots::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, h
   // wait until the compute stream has finished reading this slot
   if (s.used) TWTML_HIP_CHECK(hipStreamWaitEvent(copy, s.consumed, 0));
   // after the slot wait: a..b times the copies themselves
-  if (tl_on_ == 1) TWTML_HIP_CHECK(hipEventRecord(mark.a, copy));
+  if (timed) TWTML_HIP_CHECK(hipEventRecord(mark.a, copy));
   // offsets + flags: one u16 per row when the batch was packed (the compute
   // stream rebuilds both in acquire), else as they are.  Packed row words sit
   // right before the text on both sides and travel with it (below).
@@ -181,7 +186,7 @@ void RawSlots::submit(const HostBatch& hb, int64_t n, int64_t bytes, int slot, h
   if (!packed) moved += int64_t(sizeof(int64_t)) * (n + 1) + (n > 0 ? n : 0);
   if (n > 0) moved += hb.soff[scalar_cols];
   h2d_bytes_.fetch_add(moved, std::memory_order_relaxed);
-  if (tl_on_ == 1) {
+  if (timed) {
     TWTML_HIP_CHECK(hipEventRecord(mark.b, copy));
     mark.bytes = moved;
     std::lock_guard<std::mutex> lk(tl_mu_);

@@ -81,6 +81,7 @@ class RawSlots {
 
  private:
   int check(int slot) const;
+  bool timing_on();   // TWTML_H2D_TIMING, read once
   struct Slot {
     uint8_t* text_base = nullptr;     // [row words prefix | text] (one H2D copy)
     uint8_t* text = nullptr;
