@@ -125,6 +125,7 @@ class Runner:
         self.prestaged_at_t0 = 0  # batches of the timed window staged / submitted before t0
         self.steps_done = 0
         self.marks = []           # (sealed, done) host clock per timed batch
+        self.phases = []          # the engine's per-batch host / device phase times (LR)
         self.hang_at = 0          # TWTML_BENCH_HANG=<rank>:<step>: that rank hangs before that step
 
     def process(self, slot: int):
@@ -147,6 +148,7 @@ class Runner:
             self.iters.append(res["iterations"])
             self.stage.append((res["prep_ms"], res["train_ms"]))
             self.extra.append((res.get("tiered", False), res.get("n_unique", 0), res.get("n_near", 0)))
+            self.phases.append(list(res.get("phases", [])))
             self.comm.append((res.get("comm_iters", 0), res.get("comm_ms", 0.0), res.get("comm_bytes", 0)))
 
 
@@ -693,6 +695,10 @@ def main(argv=None) -> int:
             out["h2d_timeline"]["iterations"] = [int(x) for x in runner.iters]
             out["h2d_timeline"]["prep_ms"] = [round(float(a), 3) for a, _ in runner.stage]
             out["h2d_timeline"]["train_ms"] = [round(float(b), 3) for _, b in runner.stage]
+            # engine phases (ms): host pre-GD enqueue, GD loop, post-GD enqueue + sync, result read;
+            # device pre-GD kernels, post-GD kernels
+            if runner.phases:
+                out["h2d_timeline"]["phases_ms"] = [[round(float(x), 3) for x in p[:6]] for p in runner.phases]
             if len(win) == 2:   # the window's ends against the first copy's start / the last copy's end
                 out["h2d_timeline"].update(
                     window_ms=round(win[1] - win[0], 3), first_copy_start_ms=round(tl[0][1] - win[0], 3),
